@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Headline benchmark: env-steps/s of the full PPO rollout (BASELINE.json configs[2]:
+4096 envs x 16 UAVs x 32 targets, transformer policy + env step on each MI355X).
+
+One timed "step" = one rollout iteration per rank: T (=64) x {fused policy forward (fp32 MFMA) ->
+on-device sample -> fused env step (fp64)} over E envs, a bootstrap value pass, GAE + advantage
+normalisation, and with N > 1 GPUs the RCCL all-gather of the trajectories.
+value = E * T * K * N / max-over-ranks wall time. Inputs (scenes, windows) are resident in HBM.
+
+Also reported (same JSON line):
+  roofline      dominant kernel = k_policy_forward, MFMA fp32 peak, algorithmic 2,446,208
+                FLOP/sample (last-token-pruned forward) x E per launch / its average
+                HIP-event duration over the timed region
+  env_roofline  k_env_step against HBM, algorithmic 24*M + 490 B per env-step
+  ppo_samples_per_s  one update() over the rank's E*T batch (5 epochs, minibatch --ppo-minibatch)
+  cpu_baseline  the CPU port (C oracle env.step + torch-CPU fp32 policy + numpy GAE) on host cores,
+                rank 0 at N = 1 only, bounded sample
+Launch for N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "target-allocation-ppo-transformer_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+POLICY_FLOP_PER_SAMPLE = 2_446_208  # SURVEY.md 8(d), derived in DESIGN.md
+MFMA_F32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: fp32 MFMA = vector peak
+HBM_PEAK_GBS = 8000.0
+
+
+def env_bytes_per_step(M):
+    return 24 * M + 490
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--uavs", type=int, default=16)
+    ap.add_argument("--targets", type=int, default=32)
+    ap.add_argument("--horizon", type=int, default=64)
+    ap.add_argument("--ppo-minibatch", type=int, default=4096)
+    ap.add_argument("--no-ppo", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(args, state_dict, seconds):
+    """The CPU port on the host cores: C oracle env.step + torch fp32 policy (oracle.policy_ref)."""
+    import random
+    import oracle
+    from oracle import gae as ogae
+    from oracle import policy_ref
+    from uavhip.config import Config, params_vector
+    from uavhip.scene import generate_scene
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(cores)
+    c = Config()
+    c.NUM_UAVS, c.NUM_TARGETS = args.uavs, args.targets
+    np.random.seed(0); random.seed(0)
+    E = 64
+    prm = params_vector(c)
+    envs = [oracle.OracleEnv(generate_scene(c), prm) for _ in range(E)]
+    obs = np.stack([e.reset() for e in envs])
+    sd = {k: v.detach().float().cpu() for k, v in state_dict.items()}
+    rng = np.random.default_rng(0)
+    steps = 0
+    rew_buf, done_buf, val_buf = [], [], []
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        with torch.no_grad():
+            logits, value = policy_ref.heads(sd, torch.from_numpy(obs))
+            p1 = torch.softmax(logits, -1)[:, 1].numpy()
+        acts = (rng.random(E) < p1).astype(np.int64)
+        rw = np.zeros(E); dn = np.zeros(E, np.uint8)
+        for i, e in enumerate(envs):
+            o, r, d, _ = e.step(int(acts[i]))
+            rw[i], dn[i] = r, d
+            obs[i] = e.reset() if d else o
+        rew_buf.append(rw); done_buf.append(dn); val_buf.append(value.numpy())
+        steps += E
+        if len(rew_buf) == 64:
+            ogae.gae_2d(np.stack(rew_buf), np.stack(done_buf), np.stack(val_buf))
+            rew_buf, done_buf, val_buf = [], [], []
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "sample": f"{E} envs x {steps // E} steps of {args.uavs}x{args.targets} ({dt:.1f} s): torch-CPU fp32 "
+                      f"policy forward ({cores} threads) + C oracle UAVEnv.step (1 thread) + numpy GAE"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.ppo import make_optimizer, ppo_epochs
+    from uavhip.rollout import RolloutEngine
+    from uavhip.vec_env import VecUAVEnv
+
+    E, T = args.envs, args.horizon
+    torch.manual_seed(0)  # identical initial policy on every rank
+    policy = TransformerActorCritic().to(dev)
+    env = VecUAVEnv(E, args.uavs, args.targets, 1, 1, seed=1 + rank, full_reset_period=200)
+    eng = RolloutEngine(env, policy, T, want_info=True, bootstrap=True, seed=1000 + rank)
+    eng.start()
+
+    # HIP events around every policy launch (same stream as the launch)
+    ev = []
+    orig = policy.fused_forward
+
+    def timed_forward(*a, **k):
+        s0 = torch.cuda.Event(enable_timing=True); s1 = torch.cuda.Event(enable_timing=True)
+        s0.record(); out = orig(*a, **k); s1.record()
+        if timing[0]:
+            ev.append((s0, s1))
+        return out
+
+    timing = [False]
+    policy.fused_forward = timed_forward
+    env_ev = []
+    orig_step = env.step
+
+    def timed_step(*a, **k):
+        s0 = torch.cuda.Event(enable_timing=True); s1 = torch.cuda.Event(enable_timing=True)
+        s0.record(); out = orig_step(*a, **k); s1.record()
+        if timing[0]:
+            env_ev.append((s0, s1))
+        return out
+
+    env.step = timed_step
+
+    def iteration():
+        eng.collect()
+        if dist is not None:
+            eng.gather()
+        eng.roll()
+
+    for _ in range(args.warmup):
+        iteration()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timing[0] = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        iteration()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    timing[0] = False
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    env_steps = E * T * args.steps * world
+    value = env_steps / elapsed
+
+    pol_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    env_ms = float(np.mean([a.elapsed_time(b) for a, b in env_ev]))
+    achieved_tf = POLICY_FLOP_PER_SAMPLE * E / (pol_ms * 1e-3) / 1e12
+    env_gbs = env_bytes_per_step(args.targets) * E / (env_ms * 1e-3) / 1e9
+
+    ppo = None
+    if not args.no_ppo:
+        tr = eng.traj
+        n = E * T
+        states = tr.obs[:T].reshape(n, 5, 14)
+        acts = tr.actions.reshape(n).long()
+        opt = make_optimizer(policy)
+        torch.cuda.synchronize()
+        p0 = time.perf_counter()
+        _, _, _, cnt = ppo_epochs(policy, opt, states, acts, tr.logp.reshape(n), tr.values.reshape(n),
+                                  tr.ret.reshape(n), tr.adv.reshape(n), batch_size=args.ppo_minibatch)
+        torch.cuda.synchronize()
+        pdt = time.perf_counter() - p0
+        ppo = {"value": n / pdt, "unit": "PPO samples/s (per GPU)", "epochs": 5, "minibatch": args.ppo_minibatch,
+               "optimizer_steps": cnt, "impl": "torch autograd on GPU (SURVEY 8f next row)"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, policy.state_dict(), args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "env-steps/sec (whole node), full PPO rollout, 4096 envs x 16 UAV x 32 tgt per GPU",
+            "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32 policy (MFMA) + f64 env", "data": "synthetic (on-device Philox scenes, "
+            "random-init policy, actions sampled from the policy)",
+            "config": {"workload": "BASELINE configs[2]: full rollout (policy fwd -> sample -> env.step) + GAE"
+                       + (" + RCCL trajectory all-gather" if world > 1 else ""),
+                       "envs_per_gpu": E, "uavs": args.uavs, "targets": args.targets, "horizon": T,
+                       "env_steps_per_step": E * T * world, "parallelism": f"env-sharded x{world}",
+                       "full_reset_period": 200},
+            "roofline": {"kernel": "k_policy_forward", "bound": "mfma", "achieved": achieved_tf,
+                         "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / MFMA_F32_PEAK_TFLOPS,
+                         "traffic": None, "avg_launch_ms": pol_ms, "flop_per_launch": POLICY_FLOP_PER_SAMPLE * E},
+            "env_roofline": {"kernel": "k_env_step", "bound": "hbm", "achieved": env_gbs, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS, "avg_launch_ms": env_ms,
+                             "bytes_per_env_step": env_bytes_per_step(args.targets)},
+            "ppo_samples_per_s": ppo,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

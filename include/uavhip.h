@@ -1,0 +1,229 @@
+/*
+ * uavhip.h -- C ABI of libuavhip.so, the MI355X (gfx950) implementation of the PPO rollout
+ * hot path of the UAV->target allocation reference (envs/uav_env.py, envs/mechanics.py,
+ * networks/transformer_net.py, agents/ppo.py).
+ *
+ * The reference has no FFI layer: its boundary is the Python object API that main_train.py
+ * calls (UAVEnv.reset/step, PPOAgent.select_action/store_transition/update). Each entry point
+ * below replaces one piece of that API; the Python mirror in
+ * target-allocation-ppo-transformer_amd/uavhip binds them with ctypes.
+ *
+ * Conventions
+ *  - every pointer is CALLER-OWNED DEVICE memory (torch tensors), except the `const
+ *    uavhip_env*` / `const uavhip_policy*` descriptors themselves, which live on the host and are
+ *    copied into the launch; the library never allocates or frees on the hot path;
+ *  - every call is asynchronous on `stream` (a hipStream_t; NULL = the legacy default stream)
+ *    and never synchronises the device;
+ *  - return 0 on success, a negative UAVHIP_E* code otherwise; uavhip_last_error() returns a
+ *    thread-local message. No C++ exception crosses this boundary;
+ *  - layouts are row-major, env index outermost ("[E][N][M]" = e*N*M + u*M + t).
+ */
+#ifndef UAVHIP_H
+#define UAVHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* uavhip_stream_t; /* hipStream_t */
+
+#define UAVHIP_SEQ_LEN 5    /* config.py:62 SEQ_LEN    */
+#define UAVHIP_STATE_DIM 14 /* config.py:61 STATE_DIM  */
+#define UAVHIP_OBS_FLOATS (UAVHIP_SEQ_LEN * UAVHIP_STATE_DIM)
+#define UAVHIP_MAX_N 64     /* UAVs per env (one wave lane each)          */
+#define UAVHIP_MAX_M 128    /* targets per env (<= 2 per wave lane)       */
+#define UAVHIP_MAX_OBSTACLES 8
+
+enum uavhip_status {
+    UAVHIP_OK = 0,
+    UAVHIP_EINVAL = -1, /* bad argument / shape */
+    UAVHIP_EHIP = -2,   /* HIP launch or runtime error */
+};
+
+/* Physics constants (config.py:7-12,53 / config0.py), passed by value. */
+enum uavhip_param {
+    UAVHIP_PRM_ZETA_D = 0, /* PARAM_ZETA_D, target distance scale (150)        */
+    UAVHIP_PRM_K,          /* PARAM_K, speed ratio weight (1.2; 5.0 in config0)  */
+    UAVHIP_PRM_C1,         /* PARAM_C1 */
+    UAVHIP_PRM_C2,         /* PARAM_C2 */
+    UAVHIP_PRM_C3,         /* PARAM_C3 */
+    UAVHIP_PRM_C4,         /* PARAM_C4 */
+    UAVHIP_PRM_OMEGA,      /* COST_WEIGHT_OMEGA */
+    UAVHIP_PRM_ZETA_OBS,   /* obstacle distance scale, 10 (mechanics.py:79)      */
+    UAVHIP_PRM_COUNT
+};
+
+/* On-device scene generator ranges (uav_env.py:65-173). */
+enum uavhip_gen {
+    UAVHIP_GEN_UAV_X0 = 0, UAVHIP_GEN_UAV_X1, /* UAV_GEN_X_RANGE            */
+    UAVHIP_GEN_TGT_X0, UAVHIP_GEN_TGT_X1,     /* TARGET_GEN_X_RANGE         */
+    UAVHIP_GEN_MAP_H,                         /* MAP_HEIGHT                 */
+    UAVHIP_GEN_WEATHER_SPEED,                 /* WEATHER_SPEED_FACTOR       */
+    UAVHIP_GEN_WEATHER_LOAD,                  /* WEATHER_LOAD_FACTOR        */
+    UAVHIP_GEN_NFZ_X0, UAVHIP_GEN_NFZ_X1,     /* 120, 140 (uav_env.py:150)  */
+    UAVHIP_GEN_ICP_X0, UAVHIP_GEN_ICP_X1,     /* 140, 160 (uav_env.py:160)  */
+    UAVHIP_GEN_ICP_S0, UAVHIP_GEN_ICP_S1,     /* 0.30, 0.32 (uav_env.py:164)*/
+    UAVHIP_GEN_COUNT = 16
+};
+
+/* Per-step diagnostics (uav_env.py:426-433 `info`), one row of doubles per env-step. */
+enum uavhip_info {
+    UAVHIP_INFO_J = 0,          /* J_val after the action (_calc_J_X)               */
+    UAVHIP_INFO_NUM_ASSIGNED,   /* num_assigned = N0, covered targets                */
+    UAVHIP_INFO_IS_VALID,       /* is_valid_action: 1/0, or -1 for None (action 0)   */
+    UAVHIP_INFO_AVG_P_DMG,      /* avg_p_dmg over locked pairs                       */
+    UAVHIP_INFO_AVG_P_FINAL,    /* avg_p_final over locked pairs                     */
+    UAVHIP_INFO_UAV_IDX,        /* pointer after the action (before any auto-reset)  */
+    UAVHIP_INFO_TARGET_IDX,
+    UAVHIP_INFO_EPISODE,        /* 1-based episode index the step belonged to        */
+    UAVHIP_INFO_COUNT
+};
+
+/* Integer per-env scalars, istate[E][UAVHIP_IST_COUNT]. */
+enum uavhip_ist {
+    UAVHIP_IST_UAV_IDX = 0, /* uav_env.py:33 self.uav_idx    */
+    UAVHIP_IST_TARGET_IDX,  /* uav_env.py:34 self.target_idx */
+    UAVHIP_IST_N_COVERED,   /* N0: targets with >= 1 lock    */
+    UAVHIP_IST_N_ASSIGNED,  /* locked (uav, target) pairs    */
+    UAVHIP_IST_EPISODE,     /* 1-based episode counter (main_train.py:77-79 cadence) */
+    UAVHIP_IST_ERROR,       /* set to 1 when a finished env is stepped without auto-reset */
+    UAVHIP_IST_PAD0, UAVHIP_IST_PAD1,
+    UAVHIP_IST_COUNT
+};
+
+/* Float64 per-env scalars, dstate[E][UAVHIP_DST_COUNT]. */
+enum uavhip_dst {
+    UAVHIP_DST_R = 0,      /* cached r(X) (_calculate_paper_reward of the current state) */
+    UAVHIP_DST_J,          /* cached J(X)                                                */
+    UAVHIP_DST_ASG_COST,   /* sum of costs of unavailable UAVs (chi_c numerator)         */
+    UAVHIP_DST_COV_VALUE,  /* sum of values of covered targets (chi_v numerator)         */
+    UAVHIP_DST_TOTAL_COST, /* total_swarm_cost (uav_env.py:118)                          */
+    UAVHIP_DST_TOTAL_VALUE,/* sum of target values                                       */
+    UAVHIP_DST_PAD0, UAVHIP_DST_PAD1,
+    UAVHIP_DST_COUNT
+};
+
+/*
+ * Vectorised env descriptor: E independent copies of UAVEnv (envs/uav_env.py:13) in SoA device
+ * tensors. Replaces the Python objects `self.uavs / self.targets / self.nfz_list /
+ * self.interceptors` (records of envs/entities.py:13-61) and the pointer/lock state.
+ */
+typedef struct uavhip_env {
+    int32_t E, N, M, Kn, Ki;
+    int32_t full_reset_period; /* auto-reset: regenerate the scene when episode % period == 0
+                                  (200 in main_train.py:79); 0 = state-only resets          */
+    uint64_t seed;             /* Philox key for on-device scene generation                 */
+    double prm[UAVHIP_PRM_COUNT];
+    double gen[UAVHIP_GEN_COUNT];
+    /* scene: entities.py records as SoA */
+    double* uav_pos;   /* [E][N][2]  UAV.pos                                  */
+    double* uav_vel;   /* [E][N][2]  UAV.velocity                             */
+    double* uav_load;  /* [E][N]     UAV.load (weather-scaled)                */
+    double* uav_cost;  /* [E][N]     UAV.cost (1.0 / 1.25)                    */
+    int32_t* uav_type; /* [E][N]     UAV.uav_type                             */
+    double* tgt_pos;   /* [E][M][2]  Target.pos, in LIST order (post-shuffle) */
+    double* tgt_vel;   /* [E][M][2]  Target.velocity                          */
+    double* tgt_value; /* [E][M]     Target.value                             */
+    int32_t* tgt_id;   /* [E][M]     Target.id (pre-shuffle index)            */
+    double* nfz_pos;   /* [E][Kn][2] NoFlyZone.pos                            */
+    double* icp_pos;   /* [E][Ki][2] Interceptor.pos                          */
+    double* icp_vel;   /* [E][Ki][2] Interceptor.velocity                     */
+    /* pair tables (uavhip_score_pairs output) */
+    double* p_dmg;     /* [E][N][M]  calc_damage_prob (mechanics.py:93)        */
+    double* p_pen;     /* [E][N]     calc_penetration_prob (mechanics.py:118) */
+    /* dynamic state */
+    double* nh_final;  /* [E][M] prod over lockers of (1 - p_final), lock order  */
+    double* nh_pure;   /* [E][M] prod over lockers of (1 - p_dmg)               */
+    double* t_cost;    /* [E][M] sum of locker costs, lock order                */
+    int32_t* n_lock;   /* [E][M] number of lockers                              */
+    int32_t* assigned; /* [E][N] target LIST index or -1 (id = tgt_id[..])       */
+    int32_t* istate;   /* [E][UAVHIP_IST_COUNT]                                */
+    double* dstate;    /* [E][UAVHIP_DST_COUNT]                                */
+    float* window;     /* [E][5][14] state_buffer deque (uav_env.py:37)        */
+} uavhip_env;
+
+/* ---------------------------------------------------------------- env (K1, K2, reset, gen) */
+
+/* K1. Dense pair tables p_dmg[E][N][M], p_pen[E][N] from the scene arrays, for the envs with
+ * mask[e] != 0 (mask NULL = all). Replaces calc_advantage's per-call recomputation
+ * (mechanics.py:93-181; called ~42x per env step by uav_env.py:184-435). */
+int uavhip_score_pairs(const uavhip_env* env, const uint8_t* mask, uavhip_stream_t stream);
+
+/* Philox4x32-10 scene generation on device (distribution of uav_env.py:65-173, not its
+ * MT19937 stream) for masked envs, followed by K1 for them. `episode` feeds the counter. */
+int uavhip_scene_generate(const uavhip_env* env, const uint8_t* mask, uavhip_stream_t stream);
+
+/* UAVEnv.reset(full_reset=False) (uav_env.py:42-63,175-182) for masked envs: clears the
+ * allocation, recomputes the scene totals, writes the first window to obs_out[E][5][14]
+ * (nullable). episode >= 0 sets istate[EPISODE]; < 0 leaves it. */
+int uavhip_env_reset(const uavhip_env* env, const uint8_t* mask, int32_t episode, float* obs_out,
+                     uavhip_stream_t stream);
+
+/* K2. UAVEnv.step (uav_env.py:295-435) for all E envs, T consecutive steps fused in one launch
+ * (T = 1 for the per-step rollout). actions: int8 [T][E] (0 skip, 1 assign). Outputs (each
+ * nullable): obs_out [T][E][5][14] f32, reward [T][E] f64, done [T][E] u8,
+ * info [T][E][UAVHIP_INFO_COUNT] f64.
+ * auto_reset != 0: a finished env is reset in-kernel (state-only, or a fresh on-device scene
+ * every full_reset_period episodes) and obs_out carries the NEW episode's first window;
+ * auto_reset == 0: obs_out is all zeros for a finished env (the reference returns zeros(14),
+ * uav_env.py:188-189) and stepping it again only sets istate[ERROR]. */
+int uavhip_env_step(const uavhip_env* env, const int8_t* actions, int32_t T, int32_t auto_reset,
+                    float* obs_out, double* reward, uint8_t* done, double* info, uavhip_stream_t stream);
+
+/* ---------------------------------------------------------------- PPO reductions (K3) */
+
+/* GAE over a time-major [T][E] buffer (agents/ppo.py:70-91, fp32 arithmetic in the reference's
+ * op order): next_v = v[t+1] (t < T-1) or last_value[e] (NULL -> 0, the reference's value at
+ * an episode end); done zeroes the bootstrap and the carry. Writes returns and raw advantages
+ * (returns - values), and per-block (sum, sum of squares) partials of the advantages to
+ * partials[2 * uavhip_gae_partials(T, E)] (nullable) for uavhip_adv_normalize. */
+int uavhip_gae(const double* reward, const uint8_t* done, const float* value, const float* last_value,
+               int32_t T, int32_t E, double gamma, double lam, float* ret, float* adv, double* partials,
+               uavhip_stream_t stream);
+int32_t uavhip_gae_partials(int32_t T, int32_t E);
+
+/* fp64 (sum, sum of squares) partials of adv[n] into partials[2 * n_partials] (one per block),
+ * for buffers that did not come out of uavhip_gae. */
+int uavhip_adv_partials(const float* adv, int64_t n, double* partials, int32_t n_partials, uavhip_stream_t stream);
+
+/* adv <- (adv - mean) / (std_unbiased + 1e-7) over n elements (ppo.py:94), mean/std folded in
+ * fp64 from partials[2 * n_partials] (uavhip_gae or uavhip_adv_partials) in a fixed order, then
+ * rounded to fp32 as the reference's fp32 tensors are. stats_out[2] = {mean, std} (nullable,
+ * device f64). */
+int uavhip_adv_normalize(float* adv, int64_t n, const double* partials, int32_t n_partials, double* stats_out,
+                         uavhip_stream_t stream);
+
+/* ---------------------------------------------------------------- policy forward (K4) */
+
+/* Packed fp32 weights of TransformerActorCritic (transformer_net.py:67-144), produced by
+ * uavhip/policy.py pack_weights() from the 50-key state_dict. */
+typedef struct uavhip_policy {
+    const float* weights; /* packed buffer, layout = uavhip_policy_layout() offsets */
+    int32_t n_floats;
+    int32_t d_model, n_heads, d_ff, d_head_hidden; /* 128, 8, 256, 64 */
+    int32_t actor_layers, critic_layers;           /* 1, 2 */
+} uavhip_policy;
+
+/* Offsets (in floats) of every parameter in the packed buffer, in state_dict key order
+ * (see policy.py). Returns the total number of floats; offsets may be NULL. */
+int32_t uavhip_policy_layout(int32_t* offsets, int32_t max_offsets);
+
+/* get_action / evaluate (transformer_net.py:96-144) for B windows states[B][5][14]:
+ * actions_in NULL -> sample a ~ Categorical(softmax(logits)) with Philox(seed, offset + b);
+ * else evaluate the given actions. Outputs (nullable except where noted): action_out [B] int8,
+ * logp [B], value [B], entropy [B], logits [B][2] (all f32). */
+int uavhip_policy_forward(const uavhip_policy* policy, const float* states, int32_t B, const int8_t* actions_in,
+                          uint64_t seed, uint64_t offset, int8_t* action_out, float* logp, float* value,
+                          float* entropy, float* logits, uavhip_stream_t stream);
+
+/* ---------------------------------------------------------------- misc */
+const char* uavhip_last_error(void);
+int32_t uavhip_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UAVHIP_H */

@@ -1,0 +1,138 @@
+// common.hpp -- shared device helpers for libuavhip.so (gfx950 / CDNA4, wave64).
+//
+// * fp64 mechanics (envs/mechanics.py) written as the reference evaluates them, one rounding
+//   per numpy scalar op; the env translation units are built with -ffp-contract=off so no
+//   product/sum is fused into an FMA (that would change the last bit of the rewards).
+// * Philox4x32-10 counter RNG for on-device scene generation and action sampling.
+// * wave-level helpers (readlane of doubles, ballots) for the one-wave-per-env kernels.
+// * thread-local last-error plumbing for the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/uavhip.h"
+
+#pragma clang fp contract(off)
+
+namespace uavhip {
+
+// ------------------------------------------------------------------ error plumbing (host)
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+// ------------------------------------------------------------------ wave helpers
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const unsigned long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffull), l);
+    const int hi = __builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint32_t readlane_u(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int ffs64(unsigned long long m) { return __ffsll((long long)m) - 1; }
+
+// ------------------------------------------------------------------ mechanics (fp64)
+__device__ __forceinline__ double clipd(double x, double lo, double hi) {
+    return x < lo ? lo : (x > hi ? hi : x);
+}
+__device__ __forceinline__ double norm2(double x, double y) { return sqrt(x * x + y * y); }
+
+// mechanics.py:11-57 calc_angle_score(uav_pos, uav_vel, target_pos)
+__device__ __forceinline__ double angle_score(double upx, double upy, double uvx, double uvy, double px,
+                                              double py) {
+    const double vx = px - upx, vy = py - upy;
+    const double dist = norm2(vx, vy);
+    if (dist < 1e-6) return 1.0;
+    const double nx = vx / dist, ny = vy / dist;
+    const double speed = norm2(uvx, uvy);
+    double hx = 1.0, hy = 0.0;
+    if (!(speed < 1e-6)) { hx = uvx / speed; hy = uvy / speed; }
+    const double c = nx * hx + ny * hy;
+    const double sigma = acos(clipd(c, -1.0, 1.0));
+    double b = 0.002 * dist;
+    if (b < 1e-6) b = 1e-6;
+    const double q = sigma / (b * M_PI);
+    return exp(-(q * q));
+}
+
+// mechanics.py:61-68
+__device__ __forceinline__ double speed_score(double us, double ts, double K) {
+    if (us < 1e-6) return 0.0;
+    return clipd(1.0 - (K * ts / us), 0.0, 1.0);
+}
+
+// mechanics.py:72-89 (D_mid = 0)
+__device__ __forceinline__ double dist_score(double d, double zeta) {
+    const double q = (d - 0.0) / zeta;
+    return exp(-(q * q));
+}
+
+// mechanics.py:93-114 calc_damage_prob
+__device__ __forceinline__ double damage_prob(double upx, double upy, double uvx, double uvy, double load,
+                                              double tpx, double tpy, double tvx, double tvy, const double* prm) {
+    const double dist = norm2(upx - tpx, upy - tpy);
+    const double us = norm2(uvx, uvy);
+    const double ts = norm2(tvx, tvy);
+    const double ea = angle_score(upx, upy, uvx, uvy, tpx, tpy);
+    const double ed = dist_score(dist, prm[UAVHIP_PRM_ZETA_D]);
+    const double es = speed_score(us, ts, prm[UAVHIP_PRM_K]);
+    const double term = prm[UAVHIP_PRM_C1] * ed + prm[UAVHIP_PRM_C2] * es;
+    const double p = ea * term * load;
+    return clipd(p, 0.0, 1.0);
+}
+
+// mechanics.py:118-163 calc_penetration_prob (independent of the target)
+__device__ __forceinline__ double penetration_prob(double upx, double upy, double uvx, double uvy,
+                                                   const double* nfz, int kn, const double* ip, const double* iv,
+                                                   int ki, const double* prm) {
+    double p = 1.0;
+    const double us = norm2(uvx, uvy);
+    for (int j = 0; j < kn; ++j) {
+        const double ox = nfz[2 * j], oy = nfz[2 * j + 1];
+        const double ea = angle_score(upx, upy, uvx, uvy, ox, oy);
+        const double ed = dist_score(norm2(upx - ox, upy - oy), prm[UAVHIP_PRM_ZETA_OBS]);
+        const double pn = (1.0 - ea) * (1.0 - ed);
+        p *= clipd(pn, 0.0, 1.0);
+    }
+    for (int j = 0; j < ki; ++j) {
+        const double ox = ip[2 * j], oy = ip[2 * j + 1];
+        const double ea = angle_score(upx, upy, uvx, uvy, ox, oy);
+        const double ed = dist_score(norm2(upx - ox, upy - oy), prm[UAVHIP_PRM_ZETA_OBS]);
+        const double es = speed_score(us, norm2(iv[2 * j], iv[2 * j + 1]), prm[UAVHIP_PRM_K]);
+        const double term = prm[UAVHIP_PRM_C3] * (1.0 - ed) + prm[UAVHIP_PRM_C4] * es;
+        const double pi = (1.0 - ea) * term;
+        p *= clipd(pi, 0.0, 1.0);
+    }
+    return p;
+}
+
+// ------------------------------------------------------------------ Philox4x32-10
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+// 53-bit uniform in [0, 1) from two words (numpy random_sample resolution)
+__device__ __forceinline__ double u01(uint32_t a, uint32_t b) {
+    const unsigned long long v = (((unsigned long long)a << 32) | b) >> 11;
+    return (double)v * 0x1.0p-53;
+}
+// 24-bit uniform in [0, 1) for fp32 sampling
+__device__ __forceinline__ float u01f(uint32_t a) { return (float)(a >> 8) * 0x1.0p-24f; }
+
+}  // namespace uavhip

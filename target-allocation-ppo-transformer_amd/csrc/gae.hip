@@ -1,0 +1,160 @@
+// gae.hip -- K3: GAE + advantage normalisation over a time-major [T][E] rollout buffer.
+// Reference: agents/ppo.py:70-94 (one Python iteration and a chain of 0-dim fp32 torch ops per
+// transition). Here: one lane per env walks t = T-1..0 with the loads of the next few steps in
+// flight (the recurrence is the only serial part); fp32 arithmetic in the reference's op order,
+// no FMA contraction, so returns are bitwise the reference's. The normalisation statistics are
+// fp64 block partials (fixed reduction order -> run-to-run deterministic, no atomics).
+#include "common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace uavhip {
+namespace {
+constexpr int kGaeBlock = 64;  // one wave per block: E = 4096 -> 64 blocks spread over the CUs
+constexpr int kRedBlock = 256;
+
+// Deterministic fp64 block reduction of (a, b); result valid in thread 0.
+template <int BLOCK>
+__device__ __forceinline__ void block_sum2(double& a, double& b) {
+    __shared__ double sa[BLOCK / kWave], sb[BLOCK / kWave];
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        a += __shfl_down(a, o);
+        b += __shfl_down(b, o);
+    }
+    const int w = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) { sa[w] = a; sb[w] = b; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a = 0.0; b = 0.0;
+        for (int i = 0; i < BLOCK / kWave; ++i) { a += sa[i]; b += sb[i]; }
+    }
+}
+}  // namespace
+
+__global__ __launch_bounds__(kGaeBlock) void k_gae(const double* __restrict__ reward, const uint8_t* __restrict__ done,
+                                                   const float* __restrict__ value,
+                                                   const float* __restrict__ last_value, int T, int E, float g,
+                                                   float gl, float* __restrict__ ret, float* __restrict__ adv,
+                                                   double* __restrict__ partials) {
+    const int e = blockIdx.x * kGaeBlock + threadIdx.x;
+    double s = 0.0, s2 = 0.0;
+    if (e < E) {
+        float nv = last_value ? last_value[e] : 0.0f;  // ppo.py:77 next_values[-1] = 0
+        float gae = 0.0f;
+#pragma unroll 8
+        for (int t = T - 1; t >= 0; --t) {
+            const long long i = (long long)t * E + e;
+            const float r = (float)reward[i];  // python float promoted into the fp32 tensor op
+            const float v = value[i];
+            float delta;
+            if (done[i]) {  // v_next = 0.0, carry cut (ppo.py:84-87)
+                delta = r - v;
+                gae = delta;
+            } else {
+                delta = (r + g * nv) - v;
+                gae = delta + gl * gae;
+            }
+            const float R = gae + v;
+            const float A = R - v;  // ppo.py:91 advantages = returns - values
+            ret[i] = R;
+            adv[i] = A;
+            s += (double)A;
+            s2 += (double)A * (double)A;
+            nv = v;
+        }
+    }
+    if (partials) {
+        block_sum2<kGaeBlock>(s, s2);
+        if (threadIdx.x == 0) {
+            partials[2 * blockIdx.x] = s;
+            partials[2 * blockIdx.x + 1] = s2;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kRedBlock) void k_adv_partials(const float* __restrict__ adv, long long n,
+                                                            double* __restrict__ partials) {
+    double s = 0.0, s2 = 0.0;
+    for (long long i = (long long)blockIdx.x * kRedBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kRedBlock) {
+        const double a = adv[i];
+        s += a;
+        s2 += a * a;
+    }
+    block_sum2<kRedBlock>(s, s2);
+    if (threadIdx.x == 0) {
+        partials[2 * blockIdx.x] = s;
+        partials[2 * blockIdx.x + 1] = s2;
+    }
+}
+
+// Every block folds the (few) partials in the same fixed order, then normalises its slice.
+__global__ __launch_bounds__(kRedBlock) void k_adv_normalize(float* __restrict__ adv, long long n,
+                                                             const double* __restrict__ partials, int np,
+                                                             double* __restrict__ stats) {
+    __shared__ float sm[2];
+    if (threadIdx.x == 0) {
+        double S = 0.0, S2 = 0.0;
+        for (int i = 0; i < np; ++i) { S += partials[2 * i]; S2 += partials[2 * i + 1]; }
+        const double mean = S / (double)n;
+        double var = n > 1 ? (S2 - S * mean) / (double)(n - 1) : __builtin_nan("");
+        if (var < 0.0) var = 0.0;
+        const double sd = sqrt(var);
+        sm[0] = (float)mean;
+        sm[1] = (float)sd;
+        if (stats && blockIdx.x == 0) { stats[0] = mean; stats[1] = sd; }
+    }
+    __syncthreads();
+    const float mean = sm[0];
+    const float den = sm[1] + 1e-7f;  // ppo.py:94 (std + 1e-7) in fp32
+    for (long long i = (long long)blockIdx.x * kRedBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kRedBlock)
+        adv[i] = (adv[i] - mean) / den;
+}
+
+}  // namespace uavhip
+
+using namespace uavhip;
+
+extern "C" int32_t uavhip_gae_partials(int32_t T, int32_t E) {
+    (void)T;
+    return (E + kGaeBlock - 1) / kGaeBlock;
+}
+
+extern "C" int uavhip_gae(const double* reward, const uint8_t* done, const float* value, const float* last_value,
+                          int32_t T, int32_t E, double gamma, double lam, float* ret, float* adv, double* partials,
+                          uavhip_stream_t stream) {
+    if (!reward || !done || !value || !ret || !adv || T <= 0 || E <= 0) {
+        set_error("uavhip_gae: NULL buffer or T=%d E=%d", T, E);
+        return UAVHIP_EINVAL;
+    }
+    const float g = (float)gamma;
+    const float gl = (float)(gamma * lam);  // cfg.GAMMA * cfg.GAE_LAMBDA is an f64 product (ppo.py:87)
+    hipLaunchKernelGGL(k_gae, dim3((E + kGaeBlock - 1) / kGaeBlock), dim3(kGaeBlock), 0, (hipStream_t)stream, reward,
+                       done, value, last_value, (int)T, (int)E, g, gl, ret, adv, partials);
+    return check_launch("k_gae");
+}
+
+extern "C" int uavhip_adv_partials(const float* adv, int64_t n, double* partials, int32_t n_partials,
+                                   uavhip_stream_t stream) {
+    if (!adv || !partials || n <= 0 || n_partials <= 0) {
+        set_error("uavhip_adv_partials: bad args n=%lld np=%d", (long long)n, n_partials);
+        return UAVHIP_EINVAL;
+    }
+    hipLaunchKernelGGL(k_adv_partials, dim3(n_partials), dim3(kRedBlock), 0, (hipStream_t)stream, adv, (long long)n,
+                       partials);
+    return check_launch("k_adv_partials");
+}
+
+extern "C" int uavhip_adv_normalize(float* adv, int64_t n, const double* partials, int32_t n_partials,
+                                    double* stats_out, uavhip_stream_t stream) {
+    if (!adv || !partials || n <= 0 || n_partials <= 0) {
+        set_error("uavhip_adv_normalize: bad args n=%lld np=%d", (long long)n, n_partials);
+        return UAVHIP_EINVAL;
+    }
+    long long blocks = (n + kRedBlock * 4 - 1) / (kRedBlock * 4);
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_adv_normalize, dim3((unsigned)blocks), dim3(kRedBlock), 0, (hipStream_t)stream, adv,
+                       (long long)n, partials, (int)n_partials, stats_out);
+    return check_launch("k_adv_normalize");
+}

@@ -1,0 +1,104 @@
+"""ctypes binding of libuavhip.so (C ABI declared in include/uavhip.h).
+
+The library is built in-tree (csrc/Makefile -> uavhip/libuavhip.so). There is deliberately no
+fallback: if the library is missing or cannot be loaded, importing this module raises, and every
+GPU entry point raises if its HIP call fails.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libuavhip.so")
+
+SEQ_LEN = 5
+STATE_DIM = 14
+OBS_FLOATS = SEQ_LEN * STATE_DIM
+MAX_N, MAX_M, MAX_OBSTACLES = 64, 128, 8
+
+PRM = dict(ZETA_D=0, K=1, C1=2, C2=3, C3=4, C4=5, OMEGA=6, ZETA_OBS=7)
+PRM_COUNT = 8
+GEN = dict(UAV_X0=0, UAV_X1=1, TGT_X0=2, TGT_X1=3, MAP_H=4, WEATHER_SPEED=5, WEATHER_LOAD=6, NFZ_X0=7, NFZ_X1=8,
+           ICP_X0=9, ICP_X1=10, ICP_S0=11, ICP_S1=12)
+GEN_COUNT = 16
+INFO = dict(J=0, NUM_ASSIGNED=1, IS_VALID=2, AVG_P_DMG=3, AVG_P_FINAL=4, UAV_IDX=5, TARGET_IDX=6, EPISODE=7)
+INFO_COUNT = 8
+IST = dict(UAV_IDX=0, TARGET_IDX=1, N_COVERED=2, N_ASSIGNED=3, EPISODE=4, ERROR=5)
+IST_COUNT = 8
+DST = dict(R=0, J=1, ASG_COST=2, COV_VALUE=3, TOTAL_COST=4, TOTAL_VALUE=5)
+DST_COUNT = 8
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+
+
+class EnvDesc(ctypes.Structure):
+    """Mirror of `struct uavhip_env` (include/uavhip.h)."""
+    _fields_ = [("E", _i32), ("N", _i32), ("M", _i32), ("Kn", _i32), ("Ki", _i32),
+                ("full_reset_period", _i32), ("seed", ctypes.c_uint64),
+                ("prm", ctypes.c_double * PRM_COUNT), ("gen", ctypes.c_double * GEN_COUNT)] + \
+              [(n, _vp) for n in ("uav_pos", "uav_vel", "uav_load", "uav_cost", "uav_type", "tgt_pos", "tgt_vel",
+                                  "tgt_value", "tgt_id", "nfz_pos", "icp_pos", "icp_vel", "p_dmg", "p_pen",
+                                  "nh_final", "nh_pure", "t_cost", "n_lock", "assigned", "istate", "dstate",
+                                  "window")]
+
+
+class PolicyDesc(ctypes.Structure):
+    """Mirror of `struct uavhip_policy`."""
+    _fields_ = [("weights", _vp), ("n_floats", _i32), ("d_model", _i32), ("n_heads", _i32), ("d_ff", _i32),
+                ("d_head_hidden", _i32), ("actor_layers", _i32), ("critic_layers", _i32)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "uavhip_score_pairs": (ctypes.c_int, [ctypes.POINTER(EnvDesc), _vp, _vp]),
+    "uavhip_scene_generate": (ctypes.c_int, [ctypes.POINTER(EnvDesc), _vp, _vp]),
+    "uavhip_env_reset": (ctypes.c_int, [ctypes.POINTER(EnvDesc), _vp, _i32, _vp, _vp]),
+    "uavhip_env_step": (ctypes.c_int, [ctypes.POINTER(EnvDesc), _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "uavhip_gae": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp,
+                                  _vp]),
+    "uavhip_gae_partials": (_i32, [_i32, _i32]),
+    "uavhip_adv_partials": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _i32, _vp]),
+    "uavhip_adv_normalize": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _i32, _vp, _vp]),
+    "uavhip_policy_layout": (_i32, [ctypes.POINTER(_i32), _i32]),
+    "uavhip_policy_forward": (ctypes.c_int, [ctypes.POINTER(PolicyDesc), _vp, _i32, _vp, ctypes.c_uint64,
+                                             ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "uavhip_last_error": (ctypes.c_char_p, []),
+    "uavhip_abi_version": (_i32, []),
+}
+EXPORTS = tuple(_SIGS)
+
+
+class UavHipError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libuavhip.so not built at {LIB_PATH}: run `make -C "
+                          f"target-allocation-ppo-transformer_amd/csrc` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+LIB = _load()
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = LIB.uavhip_last_error().decode(errors="replace")
+        raise UavHipError(f"{what} failed (rc={rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(stream=None):
+    import torch
+    s = torch.cuda.current_stream() if stream is None else stream
+    return ctypes.c_void_p(s.cuda_stream)

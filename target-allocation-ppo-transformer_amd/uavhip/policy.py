@@ -1,0 +1,162 @@
+"""TransformerActorCritic with the reference's parameter names, shapes and initialisation
+(networks/transformer_net.py:9-144), so its state_dict round-trips with the reference's
+checkpoints (main_train.py:211,232) and `torch.manual_seed(s); TransformerActorCritic()` yields the
+reference's initial weights.
+
+Two execution paths:
+  * `get_action` (rollout, no grad): the fused HIP forward of libuavhip.so (policy.hip, fp32 MFMA)
+    on packed weights; the action is drawn on device from Philox. GPU only: raises otherwise.
+  * `evaluate` (PPO update, autograd): the module's own torch forward, used by the update (SURVEY 8f
+    "next" row); also the torch fp32 reference the fused kernel is tested against.
+"""
+import ctypes
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.distributions import Categorical
+
+from . import _lib
+from ._lib import LIB, check, ptr, stream_handle
+from .config import cfg
+
+
+def _ortho(layer, std=float(np.sqrt(2)), bias=0.0):
+    """transformer_net.py:9-12: orthogonal weight (gain std), constant bias."""
+    nn.init.orthogonal_(layer.weight, std)
+    nn.init.constant_(layer.bias, bias)
+    return layer
+
+
+class _Trunk(nn.Module):
+    """Linear(14->128)+ReLU embedding, learned position embedding, post-LN encoder stack
+    (transformer_net.py:15-64). Attribute names fix the state_dict keys."""
+
+    def __init__(self, num_layers):
+        super().__init__()
+        self.embedding = nn.Sequential(_ortho(nn.Linear(cfg.STATE_DIM, cfg.EMBED_DIM)), nn.ReLU())
+        self.pos_embedding = nn.Parameter(torch.randn(1, cfg.SEQ_LEN, cfg.EMBED_DIM) * 0.02)
+        layer = nn.TransformerEncoderLayer(d_model=cfg.EMBED_DIM, nhead=cfg.NUM_HEADS, dim_feedforward=256,
+                                           dropout=0.0, batch_first=True)
+        # nn.TransformerEncoder deep-copies `layer`: every layer starts from identical weights,
+        # as in the reference.
+        self.transformer = nn.TransformerEncoder(layer, num_layers=num_layers, enable_nested_tensor=False)
+
+    def forward(self, x):
+        pad = x.abs().sum(dim=-1) == 0          # all-zero window rows are padding ...
+        pad[:, -1] = False                       # ... except the current step (transformer_net.py:52-54)
+        h = self.embedding(x) + self.pos_embedding[:, :x.size(1), :]
+        return self.transformer(h, src_key_padding_mask=pad)
+
+
+class TransformerActorCritic(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.hidden_dim = cfg.EMBED_DIM
+        self.actor_net = _Trunk(num_layers=1)
+        self.actor_head = nn.Sequential(_ortho(nn.Linear(self.hidden_dim, 64)), nn.ReLU(),
+                                        _ortho(nn.Linear(64, cfg.ACTION_DIM), std=0.01))
+        self.critic_net = _Trunk(num_layers=2)
+        self.critic_head = nn.Sequential(_ortho(nn.Linear(self.hidden_dim, 64)), nn.ReLU(),
+                                         _ortho(nn.Linear(64, 1), std=1.0))
+        self._packed = None
+        self._packed_key = None
+        self._desc = None
+        self.sample_seed = 0x1234ABCD
+        self._sample_offset = 0
+
+    def forward(self, state):
+        raise NotImplementedError("Please use get_action or evaluate.")
+
+    # ------------------------------------------------------------------ torch path
+    def heads(self, state):
+        """-> logits [B, 2], value [B, 1] via the torch modules (autograd-capable)."""
+        if state.dim() == 2:
+            state = state.unsqueeze(0)
+        logits = self.actor_head(self.actor_net(state)[:, -1, :])
+        value = self.critic_head(self.critic_net(state)[:, -1, :])
+        return logits, value
+
+    def evaluate(self, state, action):
+        """transformer_net.py:124-144 -> (log_prob(action), value [B, 1], entropy)."""
+        logits, value = self.heads(state)
+        dist = Categorical(torch.softmax(logits, dim=-1))
+        return dist.log_prob(action), value, dist.entropy()
+
+    # ------------------------------------------------------------------ fused HIP path
+    def packed_weights(self):
+        """Packed fp32 weight buffer in the layout of uavhip_policy_layout (repacked when any
+        parameter changed: optimizer steps and load_state_dict bump tensor versions)."""
+        params = list(self.state_dict(keep_vars=True).values())
+        dev = params[0].device
+        key = (dev, tuple(p._version for p in params), tuple(p.data_ptr() for p in params))
+        if self._packed is not None and self._packed_key == key:
+            return self._packed
+        self._packed = pack_weights(self.state_dict(), device=dev)
+        self._packed_key = key
+        d = _lib.PolicyDesc()
+        d.weights = self._packed.data_ptr()
+        d.n_floats = self._packed.numel()
+        d.d_model, d.n_heads, d.d_ff, d.d_head_hidden = cfg.EMBED_DIM, cfg.NUM_HEADS, 256, 64
+        d.actor_layers, d.critic_layers = 1, 2
+        self._desc = d
+        return self._packed
+
+    def fused_forward(self, states, actions=None, action_out=None, logp=None, value=None, entropy=None,
+                      logits=None, seed=None, offset=None):
+        """Raw fused forward on [B, 5, 14] fp32 device windows; returns the output tensors."""
+        if states.device.type != "cuda":
+            raise RuntimeError("the fused policy forward runs on the GPU (HIP) only")
+        states = states.contiguous()
+        if states.dtype != torch.float32:
+            states = states.float()
+        B = states.shape[0]
+        self.packed_weights()
+        dev = states.device
+        action_out = torch.empty(B, dtype=torch.int8, device=dev) if action_out is None else action_out
+        logp = torch.empty(B, dtype=torch.float32, device=dev) if logp is None else logp
+        value = torch.empty(B, dtype=torch.float32, device=dev) if value is None else value
+        if actions is not None:
+            actions = actions.to(device=dev, dtype=torch.int8).contiguous()
+        if offset is None:
+            offset = self._sample_offset
+            self._sample_offset += B
+        seed = self.sample_seed if seed is None else seed
+        check(LIB.uavhip_policy_forward(self._desc, ptr(states), B, ptr(actions), ctypes.c_uint64(seed),
+                                        ctypes.c_uint64(offset), ptr(action_out), ptr(logp), ptr(value),
+                                        ptr(entropy), ptr(logits), stream_handle()), "uavhip_policy_forward")
+        return action_out, logp, value, entropy, logits
+
+    @torch.no_grad()
+    def get_action(self, state):
+        """transformer_net.py:96-122 -> (action [B] int64, log_prob [B], value [B, 1], entropy [B])."""
+        if state.dim() == 2:
+            state = state.unsqueeze(0)
+        B = state.shape[0]
+        ent = torch.empty(B, dtype=torch.float32, device=state.device)
+        a, lp, v, ent, _ = self.fused_forward(state, entropy=ent)
+        return a.long(), lp, v.view(B, 1), ent
+
+
+def layout():
+    n = LIB.uavhip_policy_layout(None, 0)
+    offs = (ctypes.c_int32 * 64)()
+    LIB.uavhip_policy_layout(offs, 64)
+    return [offs[i] for i in range(50)], int(n)
+
+
+def pack_weights(state_dict, device=None):
+    """Flatten the 50-key state_dict into the kernel's packed buffer (state_dict key order)."""
+    offs, n = layout()
+    items = list(state_dict.items())
+    if len(items) != len(offs):
+        raise ValueError(f"expected {len(offs)} state_dict entries, got {len(items)}")
+    dev = device if device is not None else items[0][1].device
+    buf = torch.zeros(n, dtype=torch.float32, device=dev)
+    ends = offs[1:] + [n]
+    for (k, v), o, e in zip(items, offs, ends):
+        flat = v.detach().reshape(-1).to(device=dev, dtype=torch.float32)
+        if flat.numel() > e - o:
+            raise ValueError(f"{k}: {flat.numel()} floats do not fit the packed slot {e - o}")
+        buf[o:o + flat.numel()] = flat
+    return buf

@@ -1,0 +1,301 @@
+"""GPU parity of the env kernels (K1 score_pairs, reset, K2 step, on-device scene generation)
+against the reference's golden vectors and the CPU oracle. Marked gpu; run with -m gpu.
+
+Bars: allocation indices / pointer walk / done / num_assigned / is_valid bit-exact; pair
+probabilities to ulp level (ocml vs glibc acos/exp); rewards and info to 1e-9 relative; obs windows
+to 2e-6 (fp32 cast of fp64 features; almost all windows bit-identical)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import cases, has_gpu, sub
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs an MI355X")]
+
+RTOL_P, ATOL_P = 5e-12, 1e-15
+
+
+def _venv(E, N, M, Kn, Ki, params=None, period=0, seed=0):
+    from uavhip.vec_env import VecUAVEnv
+    v = VecUAVEnv(E, N, M, Kn, Ki, full_reset_period=period, seed=seed)
+    if params is not None:
+        v.set_params(params)
+    return v
+
+
+def test_score_pairs_vs_reference(scenes_npz):
+    groups = {}
+    for c in cases(scenes_npz):
+        s = sub(scenes_npz, c["key"])
+        key = (c["N"], c["M"], len(s["nfz_pos"]), len(s["icp_pos"]), tuple(s["params"]))
+        groups.setdefault(key, []).append(s)
+    for (N, M, Kn, Ki, prm), ss in groups.items():
+        v = _venv(len(ss), N, M, Kn, Ki, np.array(prm))
+        v.load_scenes(ss)
+        torch.cuda.synchronize()
+        p_dmg, p_pen = v.p_dmg.cpu().numpy(), v.p_pen.cpu().numpy()
+        for i, s in enumerate(ss):
+            np.testing.assert_allclose(p_dmg[i], s["p_dmg"], rtol=RTOL_P, atol=ATOL_P)
+            np.testing.assert_allclose(p_pen[i], s["p_pen"], rtol=RTOL_P, atol=ATOL_P)
+            np.testing.assert_allclose(p_dmg[i] * p_pen[i][:, None], s["p_final"], rtol=RTOL_P, atol=ATOL_P)
+
+
+def test_mechanics_records_vs_reference(mech_npz):
+    """envs/mechanics.py KATs incl. edge cases (zero velocity, coincident points, clip) via K1 with
+    one UAV and one target per env."""
+    d = mech_npz
+    P = len(d["rec_dmg"])
+    for kn in range(3):
+        for ki in range(3):
+            idx = [i for i in range(P) if d["rec_kn"][i] == kn and d["rec_ki"][i] == ki]
+            if not idx:
+                continue
+            v = _venv(len(idx), 1, 1, kn, ki, d["params"])
+            scenes = []
+            for i in idx:
+                scenes.append(dict(uav_pos=d["rec_u_pos"][i], uav_vel=d["rec_u_vel"][i], uav_load=[d["rec_u_load"][i]],
+                                   uav_cost=[1.0], tgt_pos=d["rec_t_pos"][i], tgt_vel=d["rec_t_vel"][i],
+                                   tgt_value=[4.0], tgt_id=[0], nfz_pos=d["rec_n_pos"][i][:kn],
+                                   icp_pos=d["rec_i_pos"][i][:ki], icp_vel=d["rec_i_vel"][i][:ki]))
+            v.load_scenes(scenes)
+            np.testing.assert_allclose(v.p_dmg.cpu().numpy().reshape(-1), d["rec_dmg"][idx], rtol=RTOL_P, atol=ATOL_P)
+            np.testing.assert_allclose(v.p_pen.cpu().numpy().reshape(-1), d["rec_pen"][idx], rtol=RTOL_P, atol=ATOL_P)
+
+
+def _check_traj(got, s, rtol_r=1e-9):
+    np.testing.assert_array_equal(got["done"], s["done"])
+    np.testing.assert_array_equal(got["uav_idx"], s["uav_idx"])
+    np.testing.assert_array_equal(got["target_idx"], s["target_idx"])
+    np.testing.assert_array_equal(got["assigned"], s["assigned"])
+    np.testing.assert_array_equal(got["num_assigned"], s["num_assigned"])
+    np.testing.assert_array_equal(got["is_valid"], s["is_valid"])
+    scale = np.maximum(np.abs(s["reward"]), 1e-3)
+    assert np.max(np.abs(got["reward"] - s["reward"]) / scale) < rtol_r
+    np.testing.assert_allclose(got["J_val"], s["J_val"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(got["avg_p_dmg"], s["avg_p_dmg"], rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(got["avg_p_final"], s["avg_p_final"], rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(got["obs"], s["obs"], rtol=2e-6, atol=1e-6)
+
+
+def _replay_batched(group, fused=False):
+    """Replay every case of `group` (same dims/params) in ONE VecUAVEnv, one env per case,
+    stepping all envs together; episodes restart with a state-only reset (host-driven)."""
+    from uavhip import _lib
+    s0 = group[0]
+    N, M = len(s0["uav_load"]), len(s0["tgt_value"])
+    v = _venv(len(group), N, M, len(s0["nfz_pos"]), len(s0["icp_pos"]), s0["params"])
+    v.load_scenes(group)
+    E = len(group)
+    res = [dict(obs=[], reward=[], done=[], uav_idx=[], target_idx=[], assigned=[], J_val=[], num_assigned=[],
+                is_valid=[], avg_p_dmg=[], avg_p_final=[], reset_obs=[]) for _ in range(E)]
+    # per env list of episodes of actions
+    eps = []
+    for s in group:
+        ep_actions = []
+        for ep in range(int(s["episode"].max()) + 1):
+            ep_actions.append(s["action"][s["episode"] == ep])
+        eps.append(ep_actions)
+    n_eps = max(len(x) for x in eps)
+    for ep in range(n_eps):
+        obs0 = v.reset(episode=ep + 1).cpu().numpy()
+        for e in range(E):
+            if ep < len(eps[e]):
+                res[e]["reset_obs"].append(obs0[e])
+        L = max(len(eps[e][ep]) if ep < len(eps[e]) else 0 for e in range(E))
+        acts = np.zeros((L, E), np.int8)
+        for e in range(E):
+            if ep < len(eps[e]):
+                acts[:len(eps[e][ep]), e] = eps[e][ep]
+        A = torch.as_tensor(acts, device="cuda")
+        if fused:
+            obs, rew, done, info = v.step(A, auto_reset=False)
+            outs = [(obs[t].cpu().numpy(), rew[t].cpu().numpy(), done[t].cpu().numpy(), info[t].cpu().numpy(),
+                     None) for t in range(L)]
+            asg_final = v.assigned_target_ids().cpu().numpy()
+        else:
+            outs = []
+            for t in range(L):
+                obs, rew, done, info = v.step(A[t], auto_reset=False)
+                outs.append((obs.cpu().numpy().copy(), rew.cpu().numpy().copy(), done.cpu().numpy().copy(),
+                             info.cpu().numpy().copy(), v.assigned_target_ids().cpu().numpy()))
+        for e in range(E):
+            if ep >= len(eps[e]):
+                continue
+            for t in range(len(eps[e][ep])):
+                o, r, d, inf, asg = outs[t]
+                R = res[e]
+                R["obs"].append(o[e]); R["reward"].append(r[e]); R["done"].append(int(d[e]))
+                R["uav_idx"].append(int(inf[e, _lib.INFO["UAV_IDX"]]))
+                R["target_idx"].append(int(inf[e, _lib.INFO["TARGET_IDX"]]))
+                R["J_val"].append(inf[e, _lib.INFO["J"]]); R["num_assigned"].append(int(inf[e, 1]))
+                R["is_valid"].append(int(inf[e, 2])); R["avg_p_dmg"].append(inf[e, 3])
+                R["avg_p_final"].append(inf[e, 4])
+                R["assigned"].append(asg[e] if asg is not None else None)
+        if fused:
+            for e in range(E):
+                if ep < len(eps[e]):
+                    res[e]["assigned"][-1] = asg_final[e]
+        assert int(v.errors().max()) <= 1
+    return [{k: np.asarray(x) if k != "assigned" else x for k, x in r.items()} for r in res]
+
+
+def _groups(traj_npz):
+    g = {}
+    for c in cases(traj_npz):
+        s = sub(traj_npz, c["key"])
+        key = (c["N"], c["M"], len(s["nfz_pos"]), len(s["icp_pos"]), tuple(s["params"]))
+        g.setdefault(key, []).append(s)
+    return g
+
+
+def test_trajectories_stepwise_vs_reference(traj_npz):
+    for key, group in _groups(traj_npz).items():
+        got = _replay_batched(group)
+        for r, s in zip(got, group):
+            r["assigned"] = np.stack(r["assigned"])
+            _check_traj(r, s)
+            np.testing.assert_allclose(np.stack(r["reset_obs"]), s["reset_obs"], rtol=2e-6, atol=1e-6)
+
+
+def test_trajectories_fused_vs_stepwise(traj_npz):
+    """The T-step fused launch gives the same per-step outputs as T single-step launches."""
+    for key, group in list(_groups(traj_npz).items())[:6]:
+        a = _replay_batched(group, fused=False)
+        b = _replay_batched(group, fused=True)
+        for ra, rb, s in zip(a, b, group):
+            for k in ("obs", "reward", "done", "uav_idx", "target_idx", "J_val", "num_assigned", "is_valid",
+                      "avg_p_dmg", "avg_p_final"):
+                np.testing.assert_array_equal(ra[k], rb[k], err_msg=k)
+            np.testing.assert_array_equal(ra["assigned"][-1], s["assigned"][-1])
+
+
+def test_against_oracle_bitwise_decisions(traj_npz):
+    """GPU vs CPU oracle on the same injected scene: identical decisions, rewards to 1e-12."""
+    import oracle
+    s = sub(traj_npz, "c15")  # 16x32
+    rng = np.random.default_rng(0)
+    v = _venv(1, len(s["uav_load"]), len(s["tgt_value"]), len(s["nfz_pos"]), len(s["icp_pos"]), s["params"])
+    v.load_scenes(s)
+    env = oracle.OracleEnv(s, s["params"])
+    for ep in range(3):
+        o_gpu = v.reset(episode=1).cpu().numpy()[0]
+        o_cpu = env.reset()
+        np.testing.assert_allclose(o_gpu, o_cpu, rtol=1e-6, atol=1e-7)
+        done = False
+        while not done:
+            a = int(rng.random() < 0.4)
+            obs_c, r_c, done, info_c = env.step(a)
+            obs_g, r_g, d_g, info_g = v.step(torch.tensor([a], dtype=torch.int8, device="cuda"), auto_reset=False)
+            assert bool(d_g.item()) == done
+            assert abs(r_g.item() - r_c) <= 1e-12 * max(1.0, abs(r_c))
+            np.testing.assert_array_equal(info_g.cpu().numpy()[0, [1, 2, 5, 6]], info_c[[1, 2, 5, 6]])
+            if not done:
+                np.testing.assert_allclose(obs_g.cpu().numpy()[0], obs_c, rtol=1e-6, atol=1e-7)
+        np.testing.assert_array_equal(v.assigned_target_ids().cpu().numpy()[0], env.assigned())
+
+
+def test_auto_reset_state_only(traj_npz):
+    """auto_reset: the obs returned with done is the next episode's first window, and the next
+    episode replays exactly like a host-driven reset."""
+    s = sub(traj_npz, "c1")
+    v = _venv(1, len(s["uav_load"]), len(s["tgt_value"]), len(s["nfz_pos"]), len(s["icp_pos"]), s["params"])
+    v.load_scenes(s)
+    v.reset(episode=1)
+    rewards = []
+    for i, a in enumerate(s["action"]):
+        obs, r, d, info = v.step(torch.tensor([a], dtype=torch.int8, device="cuda"), auto_reset=True)
+        rewards.append(r.item())
+        if s["done"][i]:
+            ep = s["episode"][i]
+            if ep + 1 <= s["episode"].max():
+                np.testing.assert_allclose(obs.cpu().numpy()[0], s["reset_obs"][ep + 1], rtol=2e-6, atol=1e-6)
+            assert int(v.episodes().item()) == ep + 2
+    scale = np.maximum(np.abs(s["reward"]), 1e-3)
+    assert np.max(np.abs(np.array(rewards) - s["reward"]) / scale) < 1e-9
+
+
+def test_step_after_done_flags_error(traj_npz):
+    s = sub(traj_npz, "c0")
+    v = _venv(1, 4, 4, 1, 1, s["params"])
+    v.load_scenes(s)
+    v.reset(episode=1)
+    one = torch.ones(1, dtype=torch.int8, device="cuda")
+    for _ in range(4):
+        v.step(one, auto_reset=False)
+    assert int(v.errors().item()) == 0
+    _, r, d, _ = v.step(one, auto_reset=False)
+    assert int(v.errors().item()) == 1 and int(d.item()) == 1 and r.item() == 0.0
+
+
+@pytest.mark.parametrize("N,M,Kn,Ki", [(16, 32, 1, 1), (4, 4, 2, 2), (64, 128, 1, 1), (30, 10, 1, 1)])
+def test_scene_generation_properties(N, M, Kn, Ki):
+    """On-device Philox scenes follow uav_env.py:65-173's distribution; the pair tables equal the
+    CPU oracle's on the generated scene."""
+    import oracle
+    from uavhip.config import cfg, params_vector
+    E = 64
+    v = _venv(E, N, M, Kn, Ki, seed=1234)
+    v.istate[:, 4] = torch.arange(E, dtype=torch.int32, device="cuda") + 1
+    v.generate_scenes()
+    torch.cuda.synchronize()
+    up = v.uav_pos.cpu().numpy(); uv = v.uav_vel.cpu().numpy(); ut = v.uav_type.cpu().numpy()
+    assert ((up[..., 0] >= 60) & (up[..., 0] <= 90)).all() and ((up[..., 1] >= 0) & (up[..., 1] <= 160)).all()
+    assert ((ut == 2).sum(1) == N // 4).all()
+    sp = np.linalg.norm(uv, axis=-1)
+    assert np.all(np.where(ut == 1, (sp >= 0.35 - 1e-12) & (sp <= 0.5 + 1e-12), (sp >= 0.75 - 1e-12) & (sp <= 0.9 + 1e-12)))
+    cost = v.uav_cost.cpu().numpy()
+    np.testing.assert_array_equal(cost, np.where(ut == 1, 1.0, 1.25))
+    tv = v.tgt_value.cpu().numpy(); tid = v.tgt_id.cpu().numpy()
+    for e in range(E):
+        assert sorted(tid[e].tolist()) == list(range(M))
+        assert (tv[e] == 4.0).sum() == M // 2 and (tv[e] == 16.0).sum() == 1
+    tp = v.tgt_pos.cpu().numpy()
+    assert ((tp[..., 0] >= 160) & (tp[..., 0] <= 180)).all()
+    assert np.abs(v.tgt_vel.cpu().numpy()).max() <= 0.015
+    assert len({tuple(np.round(up[e, 0], 9)) for e in range(E)}) == E  # distinct scenes per env
+    prm = params_vector(cfg)
+    for e in range(0, E, 16):
+        s = dict(uav_pos=up[e], uav_vel=uv[e], uav_load=v.uav_load[e].cpu().numpy(), tgt_pos=tp[e],
+                 tgt_vel=v.tgt_vel[e].cpu().numpy(), nfz_pos=v.nfz_pos[e, :Kn].cpu().numpy(),
+                 icp_pos=v.icp_pos[e, :Ki].cpu().numpy(), icp_vel=v.icp_vel[e, :Ki].cpu().numpy(), tgt_value=tv[e])
+        pd, pp = oracle.score_pairs(s, prm)
+        np.testing.assert_allclose(v.p_dmg[e].cpu().numpy(), pd, rtol=RTOL_P, atol=ATOL_P)
+        np.testing.assert_allclose(v.p_pen[e].cpu().numpy(), pp, rtol=RTOL_P, atol=ATOL_P)
+    # determinism: same seed and episode -> same scene
+    w = _venv(E, N, M, Kn, Ki, seed=1234)
+    w.istate[:, 4] = torch.arange(E, dtype=torch.int32, device="cuda") + 1
+    w.generate_scenes()
+    assert torch.equal(w.uav_pos, v.uav_pos) and torch.equal(w.p_dmg, v.p_dmg)
+
+
+def test_auto_full_reset_regenerates_scene():
+    """With full_reset_period P the scene changes exactly when the episode index hits a multiple of P."""
+    v = _venv(8, 4, 4, 1, 1, period=3, seed=7)
+    v.istate[:, 4] = 1
+    v.generate_scenes()
+    v.reset(episode=1)
+    one = torch.ones(8, dtype=torch.int8, device="cuda")
+    pos_prev = v.uav_pos.clone()
+    for ep in range(2, 8):
+        for _ in range(4):  # 4 UAVs x assign = 4 steps per episode
+            v.step(one, auto_reset=True)
+        torch.cuda.synchronize()
+        assert (v.episodes() == ep).all()
+        changed = not torch.equal(v.uav_pos, pos_prev)
+        assert changed == (ep % 3 == 0), ep
+        pos_prev = v.uav_pos.clone()
+
+
+def test_c5_stress_dims_run():
+    """BASELINE config 4 dims (64 UAVs x 128 targets, 2 targets per lane) step cleanly with auto-reset."""
+    v = _venv(256, 64, 128, 1, 1, period=200, seed=3)
+    v.istate[:, 4] = 1
+    v.generate_scenes()
+    v.reset(episode=1)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for _ in range(50):
+        a = (torch.rand(256, device="cuda", generator=g) < 0.3).to(torch.int8)
+        obs, r, d, info = v.step(a)
+    torch.cuda.synchronize()
+    assert torch.isfinite(obs).all() and torch.isfinite(r).all() and (r >= 0).all()
+    assert int(v.errors().max()) == 0

@@ -1,0 +1,206 @@
+"""GPU parity of the fused policy forward (policy.hip) and the GAE kernels (gae.hip), plus the
+drop-in UAVEnv / PPOAgent and the batched rollout engine. Marked gpu.
+
+Policy tolerance (fp32 vs fp32 in a different summation order, transformer depth 2): logits /
+logp / entropy 2e-5 absolute + 1e-4 relative, value 1e-4 relative. GAE returns bit-exact."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import cases, has_gpu, sub
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs an MI355X")]
+
+
+def _load_policy(policy_npz, tag):
+    from uavhip.policy import TransformerActorCritic
+    net = TransformerActorCritic()
+    sd = {k[len(f"{tag}/w/"):]: torch.from_numpy(policy_npz[k].copy()) for k in policy_npz.files
+          if k.startswith(f"{tag}/w/")}
+    net.load_state_dict(sd)
+    return net.cuda()
+
+
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_fused_policy_vs_reference(policy_npz, tag):
+    net = _load_policy(policy_npz, tag)
+    x = torch.from_numpy(policy_npz["states"]).cuda()
+    a = torch.from_numpy(policy_npz["actions"]).cuda()
+    B = x.shape[0]
+    ent = torch.empty(B, device="cuda")
+    lg = torch.empty(B, 2, device="cuda")
+    _, logp, value, ent, lg = net.fused_forward(x, actions=a, entropy=ent, logits=lg)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(lg.cpu().numpy(), policy_npz[f"{tag}/logits"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(logp.cpu().numpy(), policy_npz[f"{tag}/logp"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(ent.cpu().numpy(), policy_npz[f"{tag}/entropy"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(value.cpu().numpy(), policy_npz[f"{tag}/value"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("B", [1, 7, 16, 300, 4096])
+def test_fused_policy_vs_torch_module(policy_npz, B):
+    """Random windows with every padding pattern, batch tails (B % 16 != 0) and the C3 batch."""
+    net = _load_policy(policy_npz, "b")
+    g = torch.Generator().manual_seed(B)
+    x = torch.randn(B, 5, 14, generator=g) * 0.7
+    pad = torch.randint(0, 5, (B,), generator=g)
+    for i in range(B):
+        x[i, :pad[i]] = 0.0
+    x = x.cuda()
+    a = torch.randint(0, 2, (B,), generator=g).cuda()
+    with torch.no_grad():
+        logp_t, v_t, ent_t = net.evaluate(x, a)
+    ent = torch.empty(B, device="cuda")
+    _, logp, value, ent, _ = net.fused_forward(x, actions=a, entropy=ent)
+    np.testing.assert_allclose(logp.cpu().numpy(), logp_t.cpu().numpy(), rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(ent.cpu().numpy(), ent_t.cpu().numpy(), rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(value.cpu().numpy(), v_t[:, 0].cpu().numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_fused_sampling_distribution(policy_npz):
+    net = _load_policy(policy_npz, "a")
+    x = torch.from_numpy(np.repeat(policy_npz["states"][:1], 65536, axis=0)).cuda()
+    lg = torch.empty(65536, 2, device="cuda")
+    act, logp, _, _, lg = net.fused_forward(x, logits=lg, seed=99, offset=0)
+    p1 = torch.softmax(lg[0], -1)[1].item()
+    freq = act.float().mean().item()
+    assert abs(freq - p1) < 5 * np.sqrt(p1 * (1 - p1) / 65536) + 1e-4
+    lp_expected = torch.log_softmax(lg, -1).gather(1, act.long()[:, None])[:, 0]
+    torch.testing.assert_close(logp, lp_expected, rtol=1e-5, atol=1e-6)
+
+
+def test_gae_vs_reference(gae_npz):
+    from uavhip.ppo import gae
+    for c in cases(gae_npz):
+        s = sub(gae_npz, c["key"])
+        ret, adv, stats = gae(torch.from_numpy(s["rewards"]), torch.from_numpy(s["dones"]),
+                              torch.from_numpy(s["values"]).cuda())
+        np.testing.assert_array_equal(ret.cpu().numpy(), s["returns"])  # bit-exact fp32 recurrence
+        np.testing.assert_allclose(adv.cpu().numpy(), s["advantages"], rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("T,E,boot", [(64, 4096, True), (7, 33, False), (1, 5, True), (300, 64, True)])
+def test_gae_2d_vs_oracle(T, E, boot):
+    from oracle import gae as ogae
+    from uavhip.ppo import gae
+    rng = np.random.default_rng(T * 1000 + E)
+    r = np.where(rng.random((T, E)) < 0.5, 0.0, rng.uniform(0, 3, (T, E)))
+    d = (rng.random((T, E)) < 0.05).astype(np.uint8)
+    v = rng.normal(size=(T, E)).astype(np.float32) * 3
+    lv = rng.normal(size=E).astype(np.float32) if boot else None
+    ret, adv, stats = gae(torch.from_numpy(r), torch.from_numpy(d), torch.from_numpy(v).cuda(),
+                          None if lv is None else torch.from_numpy(lv).cuda(), normalize=False)
+    r_o, a_o = ogae.gae_2d(r, d, v, last_values=lv)
+    np.testing.assert_array_equal(ret.cpu().numpy(), r_o)
+    np.testing.assert_array_equal(adv.cpu().numpy(), a_o)
+    ret2, adv2, stats = gae(torch.from_numpy(r), torch.from_numpy(d), torch.from_numpy(v).cuda(),
+                            None if lv is None else torch.from_numpy(lv).cuda())
+    if T * E > 1:
+        a_n, mean, std = ogae.normalize(a_o)
+        np.testing.assert_allclose(adv2.cpu().numpy(), a_n, rtol=1e-5, atol=2e-6)
+        np.testing.assert_allclose(stats.cpu().numpy(), [mean, std], rtol=1e-6)
+
+
+def test_dropin_uavenv_reproduces_reference(traj_npz):
+    """envs.uav_env.UAVEnv seeded like the reference replays the reference's trajectories:
+    same scenes from the global numpy/random streams, same per-step outputs."""
+    from uavhip.config import cfg, config0_overrides
+    from envs.uav_env import UAVEnv
+    saved = {k: getattr(cfg, k) for k in ("NUM_UAVS", "NUM_TARGETS", "COST_WEIGHT_OMEGA")}
+    try:
+        for c in cases(traj_npz)[:24]:
+            if c["cfg"] != "A":
+                continue
+            s = sub(traj_npz, c["key"])
+            cfg.NUM_UAVS, cfg.NUM_TARGETS, cfg.COST_WEIGHT_OMEGA = c["N"], c["M"], c["omega"]
+            np.random.seed(c["seed"]); random.seed(c["seed"])
+            env = UAVEnv()
+            ep = -1
+            for i, a in enumerate(s["action"]):
+                if s["episode"][i] != ep:
+                    ep = s["episode"][i]
+                    o = env.reset(full_reset=(ep == 0))
+                    np.testing.assert_allclose(o, s["reset_obs"][ep], rtol=2e-6, atol=1e-6)
+                    if ep == 0:
+                        np.testing.assert_array_equal([t.id for t in env.targets], s["tgt_id"])
+                obs, r, d, info = env.step(int(a))
+                assert d == bool(s["done"][i])
+                assert abs(r - s["reward"][i]) <= 1e-9 * max(1e-3, abs(s["reward"][i]))
+                assert info["num_assigned"] == s["num_assigned"][i]
+                iv = s["is_valid"][i]
+                assert info["is_valid_action"] == (None if iv < 0 else bool(iv))
+                assert env.uav_idx == s["uav_idx"][i] and env.target_idx == s["target_idx"][i]
+                if d:
+                    assert obs.shape == (14,) and not obs.any()
+                else:
+                    np.testing.assert_allclose(obs, s["obs"][i], rtol=2e-6, atol=1e-6)
+            np.testing.assert_array_equal([u.assigned_target_id for u in env.uavs], s["assigned"][-1])
+            with pytest.raises(IndexError):
+                env.step(0)
+    finally:
+        for k, v in saved.items():
+            setattr(cfg, k, v)
+    del config0_overrides
+
+
+def test_dropin_ppoagent_loop():
+    """main_train.py:79-146 shape of use: select_action / store_transition / update."""
+    from envs.uav_env import UAVEnv
+    from agents.ppo import PPOAgent
+    from uavhip.config import cfg
+    saved = (cfg.NUM_UAVS, cfg.NUM_TARGETS)
+    try:
+        cfg.NUM_UAVS, cfg.NUM_TARGETS = 8, 8
+        np.random.seed(0); random.seed(0); torch.manual_seed(0)
+        env, agent = UAVEnv(), PPOAgent()
+        for ep in range(1, 30):
+            state = env.reset(full_reset=(ep == 1))
+            done = False
+            while not done:
+                a = agent.select_action(state)
+                state, r, done, info = env.step(a)
+                agent.store_transition(r, done)
+            if len(agent.buffer["states"]) >= 64:
+                stats = agent.update()
+                assert stats is not None and all(np.isfinite(list(stats.values())))
+                assert len(agent.buffer["states"]) == 0
+                break
+        else:
+            pytest.fail("no update happened")
+        # policy_old got the new weights and the fused path picked them up
+        x = torch.zeros(1, 5, 14, device="cuda"); x[0, -1, 0] = 0.5
+        a1 = agent.policy_old.fused_forward(x, actions=torch.zeros(1, dtype=torch.long, device="cuda"))[1]
+        lp, _, _ = agent.policy.evaluate(x, torch.zeros(1, dtype=torch.long, device="cuda"))
+        torch.testing.assert_close(a1, lp.detach(), rtol=1e-4, atol=2e-5)
+    finally:
+        cfg.NUM_UAVS, cfg.NUM_TARGETS = saved
+
+
+def test_rollout_engine_invariants():
+    from uavhip import _lib
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.rollout import RolloutEngine
+    from uavhip.vec_env import VecUAVEnv
+    torch.manual_seed(0)
+    E, T = 512, 40
+    env = VecUAVEnv(E, 16, 32, 1, 1, seed=5)
+    pol = TransformerActorCritic().cuda()
+    eng = RolloutEngine(env, pol, T, seed=11)
+    eng.start()
+    tr = eng.collect()
+    torch.cuda.synchronize()
+    d = tr.dones.cpu().numpy().astype(bool)
+    r = tr.rewards.cpu().numpy()
+    assert d.any() and (r >= 0).all() and np.isfinite(r).all()
+    obs_next = tr.obs[1:].cpu().numpy()
+    # after a done the next window is a fresh episode: 4 zero rows then the first feature row
+    assert (obs_next[d][:, :4] == 0).all() and (obs_next[d][:, 4, 13] == 1.0).all()
+    info = tr.info.cpu().numpy()
+    assert (info[..., _lib.INFO["IS_VALID"]][tr.actions.cpu().numpy() == 0] == -1).all()
+    ret, adv = tr.ret.cpu().numpy(), tr.adv.cpu().numpy()
+    assert np.isfinite(ret).all() and abs(adv.mean()) < 1e-4 and abs(adv.std(ddof=1) - 1) < 1e-3
+    eng.roll()
+    eng.collect()
+    assert int(env.errors().max()) == 0

@@ -1,0 +1,156 @@
+"""CPU-only checks of the product's host side and of the C-ABI library (no GPU compute):
+library loads and exports every symbol include/uavhip.h declares; ctypes mirrors match the
+header; the host scene generator reproduces the reference's scenes; the policy module matches the
+reference's initialisation and state_dict; the packed-weight layout covers every parameter."""
+import os
+import random
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, cases, sub
+
+HEADER = os.path.join(ROOT, "include", "uavhip.h")
+
+
+def _header_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|const char\*)\s+(uavhip_\w+)\s*\(", txt, re.M)))
+
+
+def _header_enum(name):
+    txt = open(HEADER).read()
+    body = re.search(r"enum " + name + r" \{(.*?)\};", txt, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    out, val = {}, -1
+    for item in [x.strip() for x in body.split(",") if x.strip()]:
+        if "=" in item:
+            k, v = [y.strip() for y in item.split("=")]
+            val = int(v)
+        else:
+            k = item
+            val += 1
+        out[k] = val
+    return out
+
+
+def test_library_exports_every_header_symbol():
+    from uavhip import _lib
+    fns = _header_functions()
+    assert len(fns) >= 12
+    for f in fns:
+        assert hasattr(_lib.LIB, f), f
+    assert set(fns) == set(_lib.EXPORTS)
+    assert _lib.LIB.uavhip_abi_version() == 1
+
+
+def test_ctypes_mirrors_header_enums():
+    from uavhip import _lib
+    for enum, table, prefix in [("uavhip_info", _lib.INFO, "UAVHIP_INFO_"), ("uavhip_ist", _lib.IST, "UAVHIP_IST_"),
+                                ("uavhip_dst", _lib.DST, "UAVHIP_DST_"), ("uavhip_param", _lib.PRM, "UAVHIP_PRM_"),
+                                ("uavhip_gen", _lib.GEN, "UAVHIP_GEN_")]:
+        h = _header_enum(enum)
+        for k, v in table.items():
+            assert h[prefix + k] == v, (enum, k)
+    assert _header_enum("uavhip_info")["UAVHIP_INFO_COUNT"] == _lib.INFO_COUNT
+    assert _header_enum("uavhip_param")["UAVHIP_PRM_COUNT"] == _lib.PRM_COUNT
+    # struct field order: pointer fields in the header's order
+    txt = open(HEADER).read()
+    body = re.search(r"typedef struct uavhip_env \{(.*?)\} uavhip_env;", txt, re.S).group(1)
+    names = re.findall(r"\*\s*(\w+);", body)
+    assert names == [f[0] for f in _lib.EnvDesc._fields_[9:]]
+
+
+def test_error_path_without_gpu():
+    """A bad descriptor is rejected by argument validation with a message, before any HIP call."""
+    from uavhip import _lib
+    d = _lib.EnvDesc()
+    d.E, d.N, d.M = 1, 100, 4
+    rc = _lib.LIB.uavhip_score_pairs(d, None, None)
+    assert rc == -1 and b"bad env dims" in _lib.LIB.uavhip_last_error()
+    with pytest.raises(_lib.UavHipError):
+        _lib.check(rc, "uavhip_score_pairs")
+
+
+def test_host_scene_generator_matches_reference(traj_npz):
+    from uavhip.config import Config, config0_overrides
+    from uavhip.scene import generate_scene
+    for c in cases(traj_npz):
+        s = sub(traj_npz, c["key"])
+        cf = Config()
+        if c["cfg"] == "0":
+            for k, v in config0_overrides().items():
+                setattr(cf, k, v)
+        cf.NUM_UAVS, cf.NUM_TARGETS = c["N"], c["M"]
+        np.random.seed(c["seed"]); random.seed(c["seed"])
+        g = generate_scene(cf)
+        for k in ("uav_pos", "uav_vel", "uav_load", "uav_cost", "uav_type", "tgt_pos", "tgt_vel", "tgt_value",
+                  "tgt_id", "nfz_pos", "icp_pos", "icp_vel"):
+            np.testing.assert_array_equal(g[k], s[k], err_msg=f"{c['key']} {k}")
+        assert g["total_swarm_cost"] == float(s["total_swarm_cost"])
+
+
+def test_policy_init_matches_reference(policy_npz):
+    from uavhip.policy import TransformerActorCritic
+    torch.manual_seed(0)
+    net = TransformerActorCritic()
+    sd = net.state_dict()
+    assert sum(p.numel() for p in net.parameters()) == int(policy_npz["nparams"]) == 419267
+    import json
+    assert list(sd.keys()) == json.loads(str(policy_npz["keys"]))
+    for k, v in sd.items():
+        np.testing.assert_array_equal(v.numpy(), policy_npz["a/w/" + k], err_msg=k)
+
+
+def test_policy_torch_path_matches_reference(policy_npz):
+    """evaluate() (torch path used by the PPO update) reproduces the reference outputs on CPU."""
+    from uavhip.policy import TransformerActorCritic
+    net = TransformerActorCritic()
+    net.load_state_dict({k[4:]: torch.from_numpy(policy_npz[k].copy()) for k in policy_npz.files
+                         if k.startswith("b/w/")})
+    x = torch.from_numpy(policy_npz["states"])
+    a = torch.from_numpy(policy_npz["actions"])
+    with torch.no_grad():
+        logp, v, ent = net.evaluate(x, a)
+    np.testing.assert_allclose(logp.numpy(), policy_npz["b/logp"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(v.numpy()[:, 0], policy_npz["b/value"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ent.numpy(), policy_npz["b/entropy"], rtol=1e-5, atol=1e-6)
+
+
+def test_packed_layout_covers_state_dict():
+    from uavhip.policy import TransformerActorCritic, layout, pack_weights
+    offs, n = layout()
+    net = TransformerActorCritic()
+    sd = net.state_dict()
+    sizes = [v.numel() for v in sd.values()]
+    ends = offs[1:] + [n]
+    for (k, v), o, e in zip(sd.items(), offs, ends):
+        assert o % 4 == 0 and e - o >= v.numel() and e - o - v.numel() < 4, k
+    buf = pack_weights(sd)
+    for (k, v), o in zip(sd.items(), offs):
+        assert torch.equal(buf[o:o + v.numel()], v.reshape(-1)), k
+    assert n == sum((s + 3) // 4 * 4 for s in sizes)
+
+
+def test_config_matches_reference_constants(traj_npz):
+    from uavhip.config import cfg, params_vector
+    s = sub(traj_npz, "c0")
+    np.testing.assert_array_equal(params_vector(cfg), s["params"])
+    assert (cfg.GAMMA, cfg.GAE_LAMBDA, cfg.K_EPOCHS, cfg.EPS_CLIP, cfg.BATCH_SIZE) == (0.998, 0.95, 5, 0.2, 64)
+
+
+def test_product_refuses_cpu():
+    """No silent CPU fallback: the product env and agent refuse to run without a GPU."""
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from uavhip.vec_env import VecUAVEnv
+    from uavhip.ppo import PPOAgent
+    from uavhip.policy import TransformerActorCritic
+    with pytest.raises(RuntimeError):
+        VecUAVEnv(4, 4, 4, device="cpu")
+    with pytest.raises(RuntimeError):
+        PPOAgent()
+    with pytest.raises(RuntimeError):
+        TransformerActorCritic().get_action(torch.zeros(1, 5, 14))
