@@ -191,10 +191,12 @@ int uavhip_adv_partials(const float* adv, int64_t n, double* partials, int32_t n
 
 /* adv <- (adv - mean) / (std_unbiased + 1e-7) over n elements (ppo.py:94), mean/std folded in
  * fp64 from partials[2 * n_partials] (uavhip_gae or uavhip_adv_partials) in a fixed order, then
- * rounded to fp32 as the reference's fp32 tensors are. stats_out[2] = {mean, std} (nullable,
- * device f64). */
-int uavhip_adv_normalize(float* adv, int64_t n, const double* partials, int32_t n_partials, double* stats_out,
-                         uavhip_stream_t stream);
+ * rounded to fp32 as the reference's fp32 tensors are. n_total = element count the partials
+ * describe (0 -> n); with data-parallel ranks pass all-reduced partials and the global count so
+ * every rank normalises with the statistics of the whole gathered batch. stats_out[2] =
+ * {mean, std} (nullable, device f64). */
+int uavhip_adv_normalize(float* adv, int64_t n, const double* partials, int32_t n_partials, int64_t n_total,
+                         double* stats_out, uavhip_stream_t stream);
 
 /* ---------------------------------------------------------------- policy forward (K4) */
 

@@ -91,13 +91,13 @@ __global__ __launch_bounds__(kRedBlock) void k_adv_partials(const float* __restr
 // Every block folds the (few) partials in the same fixed order, then normalises its slice.
 __global__ __launch_bounds__(kRedBlock) void k_adv_normalize(float* __restrict__ adv, long long n,
                                                              const double* __restrict__ partials, int np,
-                                                             double* __restrict__ stats) {
+                                                             long long n_total, double* __restrict__ stats) {
     __shared__ float sm[2];
     if (threadIdx.x == 0) {
         double S = 0.0, S2 = 0.0;
         for (int i = 0; i < np; ++i) { S += partials[2 * i]; S2 += partials[2 * i + 1]; }
-        const double mean = S / (double)n;
-        double var = n > 1 ? (S2 - S * mean) / (double)(n - 1) : __builtin_nan("");
+        const double mean = S / (double)n_total;
+        double var = n_total > 1 ? (S2 - S * mean) / (double)(n_total - 1) : __builtin_nan("");
         if (var < 0.0) var = 0.0;
         const double sd = sqrt(var);
         sm[0] = (float)mean;
@@ -146,7 +146,7 @@ extern "C" int uavhip_adv_partials(const float* adv, int64_t n, double* partials
 }
 
 extern "C" int uavhip_adv_normalize(float* adv, int64_t n, const double* partials, int32_t n_partials,
-                                    double* stats_out, uavhip_stream_t stream) {
+                                    int64_t n_total, double* stats_out, uavhip_stream_t stream) {
     if (!adv || !partials || n <= 0 || n_partials <= 0) {
         set_error("uavhip_adv_normalize: bad args n=%lld np=%d", (long long)n, n_partials);
         return UAVHIP_EINVAL;
@@ -155,6 +155,6 @@ extern "C" int uavhip_adv_normalize(float* adv, int64_t n, const double* partial
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_adv_normalize, dim3((unsigned)blocks), dim3(kRedBlock), 0, (hipStream_t)stream, adv,
-                       (long long)n, partials, (int)n_partials, stats_out);
+                       (long long)n, partials, (int)n_partials, (long long)(n_total > 0 ? n_total : n), stats_out);
     return check_launch("k_adv_normalize");
 }

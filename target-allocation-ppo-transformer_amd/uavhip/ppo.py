@@ -45,7 +45,7 @@ def gae(rewards, dones, values, last_values=None, gamma=None, lam=None, normaliz
     check(LIB.uavhip_gae(ptr(r), ptr(d), ptr(v), ptr(lv), T, E, ctypes.c_double(gamma), ctypes.c_double(lam),
                          ptr(ret), ptr(adv), ptr(partials), s), "uavhip_gae")
     if normalize:
-        check(LIB.uavhip_adv_normalize(ptr(adv), adv.numel(), ptr(partials), npart, ptr(stats), s),
+        check(LIB.uavhip_adv_normalize(ptr(adv), adv.numel(), ptr(partials), npart, 0, ptr(stats), s),
               "uavhip_adv_normalize")
     return ret, adv, stats
 

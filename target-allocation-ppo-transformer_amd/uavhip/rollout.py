@@ -78,16 +78,10 @@ class RolloutEngine:
         self.traj.obs[0].copy_(self.traj.obs[self.T])
 
     def gather(self, group=None):
-        """All-gather the per-rank trajectories over RCCL (one flat fp32 payload per rank):
-        window tokens, action, logp, value, return, advantage, reward, done."""
-        import torch.distributed as dist
+        """All-gather the per-rank trajectories over RCCL as one flat fp32 payload per rank
+        (uavhip.dist.pack_trajectory); returns the [world * T * E, RECORD_FLOATS] batch."""
+        from .dist import all_gather_rows, pack_trajectory
         tr = self.traj
-        T, E = tr.T, tr.E
-        payload = torch.cat([tr.obs[:T].reshape(T * E, -1), tr.actions.reshape(-1, 1).float(),
-                             tr.logp.reshape(-1, 1), tr.values.reshape(-1, 1), tr.ret.reshape(-1, 1),
-                             tr.adv.reshape(-1, 1), tr.rewards.reshape(-1, 1).float(),
-                             tr.dones.reshape(-1, 1).float()], dim=1).contiguous()
-        world = dist.get_world_size(group)
-        out = torch.empty(world * payload.shape[0], payload.shape[1], dtype=payload.dtype, device=payload.device)
-        dist.all_gather_into_tensor(out, payload, group=group)
-        return out
+        payload = pack_trajectory(tr.obs[:tr.T], tr.actions, tr.logp, tr.values, tr.ret, tr.adv, tr.rewards,
+                                  tr.dones)
+        return all_gather_rows(payload, group)
