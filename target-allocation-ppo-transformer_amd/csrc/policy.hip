@@ -28,10 +28,13 @@ namespace pol {
 constexpr int S = 5, D = 128, NH = 8, HD = 16, FF = 256, IN = 14, HID = 64;
 constexpr int SPW = 16;         // samples per workgroup
 constexpr int TOK = S * SPW;    // 80
-constexpr int NTHR = 256;
+constexpr int NW = 8;            // waves per workgroup: two per SIMD
+constexpr int NTHR = NW * 64;
 constexpr int LDH = D + 4;      // 132: row pad of 16 B -> conflict-free float4 column reads
 constexpr int LDB = 3 * 64 + 4; // 196: [Q 64 | K 64 | V 64] for a chunk of 4 heads
 constexpr int LDF = D + 4;
+constexpr int LDX = 16;         // input rows padded 14 -> 16 (one MFMA k-block)
+constexpr int LDZ = HID + 4;
 
 // ---- packed parameter table, in state_dict key order (transformer_net.py module order)
 constexpr int kLayerParams = 12;
@@ -64,22 +67,26 @@ __host__ __device__ constexpr int layer_param(int trunk, int l, int which) { ret
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct Smem {
-    float x[SPW * S * IN];      // input windows [p][s][k]
+    float x[TOK * LDX];         // input windows [tok = s*16 + p][k], k < 14 valid
     float h[TOK * LDH];         // residual stream [tok][128]
     float big[TOK * LDB];       // QKV chunk / out-proj result / FFN hidden chunk
     float ctx[TOK * LDH];       // attention output / FFN output
-    float z[SPW * HID];         // head hidden
+    float z[SPW * LDZ];         // head hidden
     float logits[SPW * 2];
     float value[SPW];
     int mask[SPW * S];          // key padding mask (transformer_net.py:52-54)
 };
 
 // ------------------------------------------------------------------ GEMM building blocks
-// acc[nt][ct] += W[wrow[nt] + i][kw0 + k] * X[xtok0 + 16 ct + j][k]  over k in [0, K)
-template <int NT, int CT>
+// acc[nt][ct] += W[wrow[nt] + i][kw0 + k] * X[xtok0 + 16 ct + j][k]  over k in [0, 128)
+// Fully unrolled over the 8 k-blocks of 16; the loads of block i + D (weights from L2 as float4,
+// activations from LDS as float4) are issued before the MFMAs of block i, so with D = 2 the
+// load latency hides under 4*NT*CT MFMAs of the previous block and with D = 4 (single column
+// tile, only 4*NT MFMAs per block) under several blocks.
+constexpr int KB = 128 / 16;
+template <int NT, int CT, int D>
 __device__ __forceinline__ void gemm_acc(f32x4 (&acc)[NT][CT], const float* __restrict__ W, int ldw,
-                                         const int (&wrow)[NT], int kw0, int K, const float* X, int ldx,
-                                         int xtok0) {
+                                         const int (&wrow)[NT], int kw0, const float* X, int ldx, int xtok0) {
     const int l = lane_id(), i16 = l & 15, g = l >> 4;
     const float* wp[NT];
 #pragma unroll
@@ -87,22 +94,34 @@ __device__ __forceinline__ void gemm_acc(f32x4 (&acc)[NT][CT], const float* __re
     const float* xp[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) xp[ct] = X + (xtok0 + 16 * ct + i16) * ldx + 4 * g;
-#pragma unroll 2
-    for (int kk = 0; kk < K; kk += 16) {
-        f32x4 a[NT], b[CT];
+    f32x4 a[KB][NT], b[KB][CT];
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) a[nt] = *reinterpret_cast<const f32x4*>(wp[nt] + kk);
+    for (int i = 0; i < KB; ++i) {
+        if (i == 0) {
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) b[ct] = *reinterpret_cast<const f32x4*>(xp[ct] + kk);
+            for (int p = 0; p < D && p < KB; ++p) {
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) a[p][nt] = *reinterpret_cast<const f32x4*>(wp[nt] + 16 * p);
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) b[p][ct] = *reinterpret_cast<const f32x4*>(xp[ct] + 16 * p);
+            }
+        }
+        if (i + D < KB) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) a[i + D][nt] = *reinterpret_cast<const f32x4*>(wp[nt] + 16 * (i + D));
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) b[i + D][ct] = *reinterpret_cast<const f32x4*>(xp[ct] + 16 * (i + D));
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
                 for (int ct = 0; ct < CT; ++ct)
-                    acc[nt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[nt][j], b[ct][j], acc[nt][ct], 0, 0, 0);
+                    acc[nt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][nt][j], b[i][ct][j], acc[nt][ct], 0, 0, 0);
     }
 }
+template <int CT> constexpr int depth() { return CT == 1 ? 4 : 2; }
 
 template <int NT, int CT>
 __device__ __forceinline__ void zero(f32x4 (&acc)[NT][CT]) {
@@ -132,23 +151,16 @@ __device__ __forceinline__ void store_acc(const f32x4 (&acc)[NT][CT], const floa
     }
 }
 
-// Y = epi(W[rows] . X^T + b) for one contiguous block of 64*NT... output features split over waves:
-// wave w handles features [f0 + w*16*NT, f0 + (w+1)*16*NT).
-template <int NT, int CT, bool RELU>
-__device__ __forceinline__ void linear(const float* W, int ldw, int kw0, const float* bias, int f0, int K,
-                                       const float* X, int ldx, int xtok0, float* Y, int ldy, int ycol0,
-                                       int ytok0) {
-    const int w = threadIdx.x >> 6;
-    int rows[NT], cols[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        rows[nt] = f0 + (w * NT + nt) * 16;
-        cols[nt] = ycol0 + (w * NT + nt) * 16;
-    }
-    f32x4 acc[NT][CT];
+// One 16-row output tile per wave: Y[tok][ycol + i] = epi(W[row + i] . X[tok]^T + b[row + i]).
+template <int CT, bool RELU>
+__device__ __forceinline__ void linear1(const float* W, int ldw, int kw0, const float* bias, int row, const float* X,
+                                        int ldx, int xtok0, float* Y, int ldy, int ycol, int ytok0) {
+    const int rows[1] = {row};
+    const int cols[1] = {ycol};
+    f32x4 acc[1][CT];
     zero(acc);
-    gemm_acc<NT, CT>(acc, W, ldw, rows, kw0, K, X, ldx, xtok0);
-    store_acc<NT, CT, RELU>(acc, bias, rows, Y, ldy, cols, ytok0);
+    gemm_acc<1, CT, depth<CT>()>(acc, W, ldw, rows, kw0, X, ldx, xtok0);
+    store_acc<1, CT, RELU>(acc, bias, rows, Y, ldy, cols, ytok0);
 }
 
 // ------------------------------------------------------------------ VALU pieces
@@ -158,12 +170,12 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-// h[tok] = LN(h[tok] + a[tok]) * w + b for tok in [tok0, tok0 + ntok) (post-LN, eps 1e-5)
+// h[tok] = LN(h[tok] + a[tok]) * w + b for tok in [tok0, tok0 + ntok) (post-LN, eps 1e-5); one wave per token
 __device__ void add_layernorm(float* h, const float* a, int lda, int tok0, int ntok, const float* __restrict__ w,
                               const float* __restrict__ b) {
     const int l = lane_id(), wv = threadIdx.x >> 6;
     const float w0 = w[2 * l], w1 = w[2 * l + 1], b0 = b[2 * l], b1 = b[2 * l + 1];
-    for (int t = tok0 + wv; t < tok0 + ntok; t += NTHR / kWave) {
+    for (int t = tok0 + wv; t < tok0 + ntok; t += NW) {
         const float v0 = h[t * LDH + 2 * l] + a[t * lda + 2 * l];
         const float v1 = h[t * LDH + 2 * l + 1] + a[t * lda + 2 * l + 1];
         const float mean = wave_sum(v0 + v1) * (1.0f / D);
@@ -175,32 +187,27 @@ __device__ void add_layernorm(float* h, const float* a, int lda, int tok0, int n
     }
 }
 
-// scaled-dot-product attention for heads [4c, 4c+4) of the query positions [qs0, qs0 + nqs),
-// keys/values of all 5 positions; reads sm.big (Q|K|V of the chunk), writes sm.ctx.
+// Scaled-dot-product attention for heads [4c, 4c+4) of the query positions [qs0, qs0 + nqs) over
+// the keys/values of all 5 positions; reads sm.big (Q|K|V of the chunk), writes sm.ctx.
+// One (query, head) task per 4 consecutive lanes, each lane owning 4 of the 16 head dims
+// (dot products reduced over the quad with two xor-shuffles).
 __device__ void attention_chunk(Smem& sm, int c, int qs0, int nqs) {
     const int ntask = nqs * SPW * 4;
-    for (int task = threadIdx.x; task < ntask; task += NTHR) {
+    const int q4 = threadIdx.x & 3;
+    for (int task = threadIdx.x >> 2; task < ntask; task += NTHR / 4) {
         const int hh = task & 3, rest = task >> 2, p = rest & 15, si = qs0 + (rest >> 4);
         const int ti = si * SPW + p;
-        const float* qrow = sm.big + ti * LDB + hh * HD;
-        float q[HD];
-#pragma unroll
-        for (int d = 0; d < HD; d += 4) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(qrow + d);
-            q[d] = v.x; q[d + 1] = v.y; q[d + 2] = v.z; q[d + 3] = v.w;
-        }
+        const int d0 = hh * HD + 4 * q4;
+        const f32x4 q = *reinterpret_cast<const f32x4*>(sm.big + ti * LDB + d0);
         float sc[S];
         float mx = -INFINITY;
 #pragma unroll
         for (int j = 0; j < S; ++j) {
-            const float* krow = sm.big + (j * SPW + p) * LDB + 64 + hh * HD;
-            float acc = 0.f;
-#pragma unroll
-            for (int d = 0; d < HD; d += 4) {
-                const f32x4 v = *reinterpret_cast<const f32x4*>(krow + d);
-                acc += q[d] * v.x + q[d + 1] * v.y + q[d + 2] * v.z + q[d + 3] * v.w;
-            }
-            sc[j] = sm.mask[p * S + j] ? -INFINITY : acc * 0.25f;  // 1/sqrt(16)
+            const f32x4 k = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 64 + d0);
+            float part = q.x * k.x + q.y * k.y + q.z * k.z + q.w * k.w;
+            part += __shfl_xor(part, 1);
+            part += __shfl_xor(part, 2);
+            sc[j] = sm.mask[p * S + j] ? -INFINITY : part * 0.25f;  // 1/sqrt(16)
             mx = fmaxf(mx, sc[j]);
         }
         float den = 0.f;
@@ -210,47 +217,52 @@ __device__ void attention_chunk(Smem& sm, int c, int qs0, int nqs) {
             den += sc[j];
         }
         const float inv = 1.0f / den;
-        float o[HD];
-#pragma unroll
-        for (int d = 0; d < HD; ++d) o[d] = 0.f;
+        f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < S; ++j) {
-            const float pj = sc[j] * inv;
-            const float* vrow = sm.big + (j * SPW + p) * LDB + 128 + hh * HD;
-#pragma unroll
-            for (int d = 0; d < HD; d += 4) {
-                const f32x4 v = *reinterpret_cast<const f32x4*>(vrow + d);
-                o[d] += pj * v.x; o[d + 1] += pj * v.y; o[d + 2] += pj * v.z; o[d + 3] += pj * v.w;
-            }
+            const f32x4 v = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 128 + d0);
+            o += (sc[j] * inv) * v;
         }
-        float* crow = sm.ctx + ti * LDH + (4 * c + hh) * HD;
-#pragma unroll
-        for (int d = 0; d < HD; d += 4) *reinterpret_cast<f32x4*>(crow + d) = f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]};
+        *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o;
     }
 }
 
-// embedding (transformer_net.py:57-59): h[s*16+p] = relu(W_e x[p][s] + b_e) + pos[s]
+// Embedding (transformer_net.py:57-59) on the MFMA, K = 14 padded to 16 with zeros:
+// h[s*16+p][f] = relu(W_e x[p][s] + b_e)[f] + pos[s][f]; wave w computes features [16w, 16w+16).
 template <int trunk>
 __device__ void embed(Smem& sm, const float* __restrict__ P) {
     const float* We = P + kOffs.o[trunk + EMB_W];
     const float* be = P + kOffs.o[trunk + EMB_B];
     const float* pos = P + kOffs.o[trunk + POS];
-    const int f = threadIdx.x & (D - 1);
-    float wr[IN];
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
+    const int f = 16 * wv + i16;
+    f32x4 a;
+    a.x = 4 * g + 0 < IN ? We[f * IN + 4 * g + 0] : 0.f;
+    a.y = 4 * g + 1 < IN ? We[f * IN + 4 * g + 1] : 0.f;
+    a.z = 4 * g + 2 < IN ? We[f * IN + 4 * g + 2] : 0.f;
+    a.w = 4 * g + 3 < IN ? We[f * IN + 4 * g + 3] : 0.f;
+    f32x4 acc[S];
 #pragma unroll
-    for (int k = 0; k < IN; ++k) wr[k] = We[f * IN + k];
-    const float bf = be[f];
-    for (int t = threadIdx.x >> 7; t < TOK; t += NTHR / D) {
-        const int s = t / SPW, p = t - s * SPW;
-        const float* xr = sm.x + (p * S + s) * IN;
-        float acc = bf;
+    for (int ct = 0; ct < S; ++ct) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(sm.x + (ct * SPW + i16) * LDX + 4 * g);
+        acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < IN; ++k) acc += wr[k] * xr[k];
-        sm.h[t * LDH + f] = fmaxf(acc, 0.f) + pos[s * D + f];
+        for (int j = 0; j < 4; ++j) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc[ct], 0, 0, 0);
+    }
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(be + 16 * wv + 4 * g);
+#pragma unroll
+    for (int ct = 0; ct < S; ++ct) {
+        const f32x4 pp = *reinterpret_cast<const f32x4*>(pos + ct * D + 16 * wv + 4 * g);
+        f32x4 v = acc[ct] + bb;
+        v.x = fmaxf(v.x, 0.f) + pp.x; v.y = fmaxf(v.y, 0.f) + pp.y;
+        v.z = fmaxf(v.z, 0.f) + pp.z; v.w = fmaxf(v.w, 0.f) + pp.w;
+        *reinterpret_cast<f32x4*>(sm.h + (ct * SPW + i16) * LDH + 16 * wv + 4 * g) = v;
     }
 }
 
 // One post-LN nn.TransformerEncoderLayer (relu FFN 256, 8 heads). last: prune to column tile 4.
+// Work split: 8 waves, wave w and w+4 share a SIMD (and its MFMA pipe); every GEMM gives each
+// SIMD the same number of 16-row output tiles.
 template <int trunk, int layer, bool last>
 __device__ void encoder_layer(Smem& sm, const float* __restrict__ P) {
     const float* Win = P + kOffs.o[layer_param(trunk, layer, INW)];
@@ -262,107 +274,61 @@ __device__ void encoder_layer(Smem& sm, const float* __restrict__ P) {
     const float* W2 = P + kOffs.o[layer_param(trunk, layer, L2W)];
     const float* b2 = P + kOffs.o[layer_param(trunk, layer, L2B)];
     const int wv = threadIdx.x >> 6;
-    const int qtok0 = last ? (S - 1) * SPW : 0;   // first query token
-    const int nqs = last ? 1 : S;                  // query positions
+    constexpr int CTQ = last ? 1 : S;              // column tiles that need Q / out / LN / FFN
+    constexpr int qtok0 = last ? (S - 1) * SPW : 0;
+    constexpr int nqs = last ? 1 : S;
 
-    // --- self-attention, in two chunks of 4 heads (LDS budget)
-    for (int c = 0; c < 2; ++c) {
-        // K, V of the chunk for all 80 tokens: 8 row tiles (K 4, V 4) -> 2 per wave
+    for (int c = 0; c < 2; ++c) {  // two chunks of 4 heads (LDS budget)
+        // K (waves 0-3) / V (waves 4-7) of the chunk for all 80 tokens, one 16-row tile each
         {
-            int rows[2], cols[2];
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-                const int tile = wv * 2 + nt;              // 0..7
-                const int part = 1 + (tile >> 2);          // 1 = K, 2 = V
-                rows[nt] = part * D + 64 * c + 16 * (tile & 3);
-                cols[nt] = part * 64 + 16 * (tile & 3);
-            }
-            f32x4 acc[2][S];
-            zero(acc);
-            gemm_acc<2, S>(acc, Win, D, rows, 0, D, sm.h, LDH, 0);
-            store_acc<2, S, false>(acc, bin, rows, sm.big, LDB, cols, 0);
+            const int part = 1 + (wv >> 2), tt = wv & 3;
+            linear1<S, false>(Win, D, 0, bin, part * D + 64 * c + 16 * tt, sm.h, LDH, 0, sm.big, LDB,
+                              part * 64 + 16 * tt, 0);
         }
-        // Q of the chunk for the query tokens: 4 row tiles -> 1 per wave
-        {
-            int rows[1] = {64 * c + 16 * wv};
-            int cols[1] = {16 * wv};
-            if constexpr (last) {
-                f32x4 acc[1][1];
-                zero(acc);
-                gemm_acc<1, 1>(acc, Win, D, rows, 0, D, sm.h, LDH, qtok0);
-                store_acc<1, 1, false>(acc, bin, rows, sm.big, LDB, cols, qtok0);
-            } else {
-                f32x4 acc[1][S];
-                zero(acc);
-                gemm_acc<1, S>(acc, Win, D, rows, 0, D, sm.h, LDH, 0);
-                store_acc<1, S, false>(acc, bin, rows, sm.big, LDB, cols, 0);
-            }
-        }
+        // Q of the chunk for the query tokens, waves 0-3 (their SIMD partners did V)
+        if (wv < 4) linear1<CTQ, false>(Win, D, 0, bin, 64 * c + 16 * wv, sm.h, LDH, qtok0, sm.big, LDB, 16 * wv, qtok0);
         __syncthreads();
         attention_chunk(sm, c, last ? S - 1 : 0, nqs);
         __syncthreads();
     }
-    // --- out projection -> big, then h = LN1(h + attn)
-    if constexpr (last) linear<2, 1, false>(Wo, D, 0, bo, 0, D, sm.ctx, LDH, qtok0, sm.big, LDB, 0, qtok0);
-    else linear<2, S, false>(Wo, D, 0, bo, 0, D, sm.ctx, LDH, 0, sm.big, LDB, 0, 0);
+    // out projection -> big, then h = LN1(h + attn)
+    linear1<CTQ, false>(Wo, D, 0, bo, 16 * wv, sm.ctx, LDH, qtok0, sm.big, LDB, 16 * wv, qtok0);
     __syncthreads();
     add_layernorm(sm.h, sm.big, LDB, qtok0, nqs * SPW, P + kOffs.o[layer_param(trunk, layer, N1W)],
                   P + kOffs.o[layer_param(trunk, layer, N1B)]);
     __syncthreads();
-    // --- FFN: hidden 256 in two chunks of 128, second GEMM accumulated in registers
-    if constexpr (last) {
-        f32x4 acc2[2][1];
-        zero(acc2);
-        int rows2[2] = {32 * wv, 32 * wv + 16};
-        for (int hc = 0; hc < 2; ++hc) {
-            linear<2, 1, true>(W1, D, 0, b1, 128 * hc, D, sm.h, LDH, qtok0, sm.big, LDF, 0, qtok0);
-            __syncthreads();
-            gemm_acc<2, 1>(acc2, W2, FF, rows2, 128 * hc, 128, sm.big, LDF, qtok0);
-            __syncthreads();
-        }
-        store_acc<2, 1, false>(acc2, b2, rows2, sm.ctx, LDH, rows2, qtok0);
-    } else {
-        f32x4 acc2[2][S];
-        zero(acc2);
-        int rows2[2] = {32 * wv, 32 * wv + 16};
-        for (int hc = 0; hc < 2; ++hc) {
-            linear<2, S, true>(W1, D, 0, b1, 128 * hc, D, sm.h, LDH, 0, sm.big, LDF, 0, 0);
-            __syncthreads();
-            gemm_acc<2, S>(acc2, W2, FF, rows2, 128 * hc, 128, sm.big, LDF, 0);
-            __syncthreads();
-        }
-        store_acc<2, S, false>(acc2, b2, rows2, sm.ctx, LDH, rows2, 0);
+    // FFN: hidden 256 in two chunks of 128, second GEMM accumulated in registers
+    f32x4 acc2[1][CTQ];
+    zero(acc2);
+    const int rows2[1] = {16 * wv};
+    for (int hc = 0; hc < 2; ++hc) {
+        linear1<CTQ, true>(W1, D, 0, b1, 128 * hc + 16 * wv, sm.h, LDH, qtok0, sm.big, LDF, 16 * wv, qtok0);
+        __syncthreads();
+        gemm_acc<1, CTQ, depth<CTQ>()>(acc2, W2, FF, rows2, 128 * hc, sm.big, LDF, qtok0);
+        __syncthreads();
     }
+    store_acc<1, CTQ, false>(acc2, b2, rows2, sm.ctx, LDH, rows2, qtok0);
     __syncthreads();
     add_layernorm(sm.h, sm.ctx, LDH, qtok0, nqs * SPW, P + kOffs.o[layer_param(trunk, layer, N2W)],
                   P + kOffs.o[layer_param(trunk, layer, N2B)]);
     __syncthreads();
 }
 
-// 128 -> 64 -> relu -> nout on the last-position rows of sm.h (transformer_net.py:77-91)
+// 128 -> 64 (MFMA, waves 0-3) -> relu -> nout (VALU) on the last-position rows (transformer_net.py:77-91)
 template <int head, int nout>
 __device__ void head_mlp(Smem& sm, const float* __restrict__ P, float* out) {
     const float* W0 = P + kOffs.o[head + 0];
     const float* b0 = P + kOffs.o[head + 1];
     const float* W2 = P + kOffs.o[head + 2];
     const float* b2 = P + kOffs.o[head + 3];
-    for (int i = threadIdx.x; i < SPW * HID; i += NTHR) {
-        const int p = i / HID, o = i - p * HID;
-        const float* hr = sm.h + ((S - 1) * SPW + p) * LDH;
-        const float* wr = W0 + o * D;
-        float acc = 0.f;
-        for (int k = 0; k < D; k += 4) {
-            const f32x4 hv = *reinterpret_cast<const f32x4*>(hr + k);
-            const f32x4 wv = *reinterpret_cast<const f32x4*>(wr + k);
-            acc += hv.x * wv.x + hv.y * wv.y + hv.z * wv.z + hv.w * wv.w;
-        }
-        sm.z[p * HID + o] = fmaxf(acc + b0[o], 0.f);
-    }
+    const int wv = threadIdx.x >> 6;
+    if (wv < HID / 16) linear1<1, true>(W0, D, 0, b0, 16 * wv, sm.h, LDH, (S - 1) * SPW, sm.z, LDZ, 16 * wv, 0);
     __syncthreads();
     if (threadIdx.x < SPW * nout) {
         const int p = threadIdx.x / nout, a = threadIdx.x - p * nout;
         float acc = 0.f;
-        for (int o = 0; o < HID; ++o) acc += W2[a * HID + o] * sm.z[p * HID + o];
+#pragma unroll 8
+        for (int o = 0; o < HID; ++o) acc += W2[a * HID + o] * sm.z[p * LDZ + o];
         out[p * nout + a] = acc + b2[a];
     }
     __syncthreads();
@@ -375,19 +341,18 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
                                                          float* __restrict__ ent_out, float* __restrict__ logits_out) {
     __shared__ __attribute__((aligned(16))) Smem sm;
     const int b0 = blockIdx.x * SPW;
-    // load 16 windows [p][s][k] (zero-fill the batch tail)
-    for (int i = threadIdx.x; i < SPW * S * IN; i += NTHR) {
-        const int p = i / (S * IN);
-        sm.x[i] = (b0 + p < B) ? states[(size_t)b0 * S * IN + i] : 0.f;
+    // windows -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch tail zero-filled)
+    for (int i = threadIdx.x; i < TOK * LDX; i += NTHR) {
+        const int t = i / LDX, k = i - t * LDX, s = t / SPW, p = t - s * SPW;
+        sm.x[i] = (k < IN && b0 + p < B) ? states[((size_t)(b0 + p) * S + s) * IN + k] : 0.f;
     }
     __syncthreads();
     if (threadIdx.x < SPW * S) {  // key padding mask: all-zero rows, last row never masked
         const int p = threadIdx.x / S, s = threadIdx.x - p * S;
         bool z = true;
-        for (int k = 0; k < IN; ++k) z = z && (sm.x[(p * S + s) * IN + k] == 0.f);
+        for (int k = 0; k < IN; ++k) z = z && (sm.x[(s * SPW + p) * LDX + k] == 0.f);
         sm.mask[p * S + s] = (s < S - 1) && z;
     }
-    __syncthreads();
     // actor trunk (1 layer) + head
     embed<kActorTrunk>(sm, P);
     __syncthreads();
