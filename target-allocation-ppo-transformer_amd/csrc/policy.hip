@@ -30,11 +30,12 @@ constexpr int SPW = 16;         // samples per workgroup
 constexpr int TOK = S * SPW;    // 80
 constexpr int NW = 8;            // waves per workgroup: two per SIMD
 constexpr int NTHR = NW * 64;
-constexpr int LDH = D + 4;      // 132: row pad of 16 B -> conflict-free float4 column reads
-constexpr int LDB = 3 * 64 + 4; // 196: [Q 64 | K 64 | V 64] for a chunk of 4 heads
-constexpr int LDF = D + 4;
+constexpr int LDH = D + 8;      // 136: row stride = 2 mod 16 slots of 16 B -> the MFMA operand
+                                // reads/writes (lane = row i + 16 * k-group g) hit 16 distinct slots
+constexpr int LDB = 3 * 64 + 8; // 200: [Q 64 | K 64 | V 64] for a chunk of 4 heads
+constexpr int LDF = D + 8;
 constexpr int LDX = 16;         // input rows padded 14 -> 16 (one MFMA k-block)
-constexpr int LDZ = HID + 4;
+constexpr int LDZ = HID + 8;
 
 // ---- packed parameter table, in state_dict key order (transformer_net.py module order)
 constexpr int kLayerParams = 12;
@@ -170,20 +171,38 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-// h[tok] = LN(h[tok] + a[tok]) * w + b for tok in [tok0, tok0 + ntok) (post-LN, eps 1e-5); one wave per token
+// h[tok] = LN(h[tok] + a[tok]) * w + b for tok in [tok0, tok0 + ntok) (post-LN, eps 1e-5).
+// 8 consecutive lanes per token (16 features each, 4 float4), sums reduced with 3 xor-shuffles
+// inside the octet: a wave normalises 8 tokens at once.
 __device__ void add_layernorm(float* h, const float* a, int lda, int tok0, int ntok, const float* __restrict__ w,
                               const float* __restrict__ b) {
-    const int l = lane_id(), wv = threadIdx.x >> 6;
-    const float w0 = w[2 * l], w1 = w[2 * l + 1], b0 = b[2 * l], b1 = b[2 * l + 1];
-    for (int t = tok0 + wv; t < tok0 + ntok; t += NW) {
-        const float v0 = h[t * LDH + 2 * l] + a[t * lda + 2 * l];
-        const float v1 = h[t * LDH + 2 * l + 1] + a[t * lda + 2 * l + 1];
-        const float mean = wave_sum(v0 + v1) * (1.0f / D);
-        const float d0 = v0 - mean, d1 = v1 - mean;
-        const float var = wave_sum(d0 * d0 + d1 * d1) * (1.0f / D);
-        const float rs = 1.0f / sqrtf(var + 1e-5f);
-        h[t * LDH + 2 * l] = d0 * rs * w0 + b0;
-        h[t * LDH + 2 * l + 1] = d1 * rs * w1 + b1;
+    const int o8 = threadIdx.x & 7;
+    const int f0 = 16 * o8;
+    for (int t = tok0 + (threadIdx.x >> 3); t < tok0 + ntok; t += NTHR / 8) {
+        f32x4 v[4];
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[i] = *reinterpret_cast<const f32x4*>(h + t * LDH + f0 + 4 * i) +
+                   *reinterpret_cast<const f32x4*>(a + t * lda + f0 + 4 * i);
+            s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+        }
+        s += __shfl_xor(s, 1); s += __shfl_xor(s, 2); s += __shfl_xor(s, 4);
+        const float mean = s * (1.0f / D);
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[i] -= mean;
+            q += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
+        }
+        q += __shfl_xor(q, 1); q += __shfl_xor(q, 2); q += __shfl_xor(q, 4);
+        const float rs = 1.0f / sqrtf(q * (1.0f / D) + 1e-5f);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f32x4 ww = *reinterpret_cast<const f32x4*>(w + f0 + 4 * i);
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(b + f0 + 4 * i);
+            *reinterpret_cast<f32x4*>(h + t * LDH + f0 + 4 * i) = v[i] * rs * ww + bb;
+        }
     }
 }
 
