@@ -79,89 +79,93 @@ struct Smem {
 };
 
 // ------------------------------------------------------------------ GEMM building blocks
-// acc[nt][ct] += W[wrow[nt] + i][kw0 + k] * X[xtok0 + 16 ct + j][k]  over k in [0, 128)
-// Fully unrolled over the 8 k-blocks of 16; the loads of block i + D (weights from L2 as float4,
-// activations from LDS as float4) are issued before the MFMAs of block i, so with D = 2 the
-// load latency hides under 4*NT*CT MFMAs of the previous block and with D = 4 (single column
-// tile, only 4*NT MFMAs per block) under several blocks.
 constexpr int KB = 128 / 16;
-template <int NT, int CT, int D>
-__device__ __forceinline__ void gemm_acc(f32x4 (&acc)[NT][CT], const float* __restrict__ W, int ldw,
-                                         const int (&wrow)[NT], int kw0, const float* X, int ldx, int xtok0) {
+
+// The first D k-blocks of a single 16-row weight tile, loaded ahead of time (typically before the
+// __syncthreads that precedes the GEMM: the barrier only drains LDS traffic, lgkmcnt(0), so these
+// global loads stay in flight across it and their latency hides under the preceding phase).
+template <int D>
+struct APre {
+    f32x4 a[D];
+};
+template <int D>
+__device__ __forceinline__ APre<D> prefetch(const float* __restrict__ W, int ldw, int row, int kw0) {
     const int l = lane_id(), i16 = l & 15, g = l >> 4;
-    const float* wp[NT];
+    const float* wp = W + (size_t)(row + i16) * ldw + kw0 + 4 * g;
+    APre<D> r;
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) wp[nt] = W + (size_t)(wrow[nt] + i16) * ldw + kw0 + 4 * g;
+    for (int p = 0; p < D; ++p) r.a[p] = *reinterpret_cast<const f32x4*>(wp + 16 * p);
+    return r;
+}
+
+// acc[ct] += W[row + i][kw0 + k] * X[xtok0 + 16 ct + j][k]  over k in [0, 128), one 16-row tile.
+// Fully unrolled over the 8 k-blocks of 16; the loads of block i + D (weights from L2 as float4,
+// activations from LDS as float4) are issued before the MFMAs of block i; blocks < D come from
+// `pre`. Both operands use the same k permutation (k = 16 i + 4 (lane >> 4) + j for MFMA j).
+template <int CT, int D>
+__device__ __forceinline__ void gemm_tile(f32x4 (&acc)[CT], const APre<D>& pre, const float* __restrict__ W, int ldw,
+                                          int row, int kw0, const float* X, int ldx, int xtok0) {
+    const int l = lane_id(), i16 = l & 15, g = l >> 4;
+    const float* wp = W + (size_t)(row + i16) * ldw + kw0 + 4 * g;
     const float* xp[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) xp[ct] = X + (xtok0 + 16 * ct + i16) * ldx + 4 * g;
-    f32x4 a[KB][NT], b[KB][CT];
+    f32x4 a[KB], b[KB][CT];
+#pragma unroll
+    for (int p = 0; p < D; ++p) {
+        a[p] = pre.a[p];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) b[p][ct] = *reinterpret_cast<const f32x4*>(xp[ct] + 16 * p);
+    }
 #pragma unroll
     for (int i = 0; i < KB; ++i) {
-        if (i == 0) {
-#pragma unroll
-            for (int p = 0; p < D && p < KB; ++p) {
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) a[p][nt] = *reinterpret_cast<const f32x4*>(wp[nt] + 16 * p);
-#pragma unroll
-                for (int ct = 0; ct < CT; ++ct) b[p][ct] = *reinterpret_cast<const f32x4*>(xp[ct] + 16 * p);
-            }
-        }
         if (i + D < KB) {
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) a[i + D][nt] = *reinterpret_cast<const f32x4*>(wp[nt] + 16 * (i + D));
+            a[i + D] = *reinterpret_cast<const f32x4*>(wp + 16 * (i + D));
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) b[i + D][ct] = *reinterpret_cast<const f32x4*>(xp[ct] + 16 * (i + D));
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                for (int ct = 0; ct < CT; ++ct)
-                    acc[nt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][nt][j], b[i][ct][j], acc[nt][ct], 0, 0, 0);
+            for (int ct = 0; ct < CT; ++ct)
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], b[i][ct][j], acc[ct], 0, 0, 0);
+        // keep the scheduler from hoisting every later block's loads (register pressure at 2
+        // waves / SIMD): at most D blocks of operands are in flight
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 template <int CT> constexpr int depth() { return CT == 1 ? 4 : 2; }
 
-template <int NT, int CT>
-__device__ __forceinline__ void zero(f32x4 (&acc)[NT][CT]) {
+template <int CT>
+__device__ __forceinline__ void zero(f32x4 (&acc)[CT]) {
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) acc[nt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ct = 0; ct < CT; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-// Y[ytok0 + 16 ct + j][ycol[nt] + i] = epi(acc + bias[brow[nt] + i])
-template <int NT, int CT, bool RELU>
-__device__ __forceinline__ void store_acc(const f32x4 (&acc)[NT][CT], const float* __restrict__ bias,
-                                          const int (&brow)[NT], float* Y, int ldy, const int (&ycol)[NT],
-                                          int ytok0) {
+// Y[ytok0 + 16 ct + j][ycol + i] = epi(acc + bias[brow + i]); lane (j, g) holds rows 4g..4g+3
+template <int CT, bool RELU>
+__device__ __forceinline__ void store_tile(const f32x4 (&acc)[CT], const float* __restrict__ bias, int brow, float* Y,
+                                           int ldy, int ycol, int ytok0) {
     const int l = lane_id(), i16 = l & 15, g = l >> 4;
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + brow + 4 * g);
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + brow[nt] + 4 * g);
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-            f32x4 v = acc[nt][ct] + bb;
-            if (RELU) {
-                v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-            }
-            *reinterpret_cast<f32x4*>(Y + (ytok0 + 16 * ct + i16) * ldy + ycol[nt] + 4 * g) = v;
+    for (int ct = 0; ct < CT; ++ct) {
+        f32x4 v = acc[ct] + bb;
+        if (RELU) {
+            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         }
+        *reinterpret_cast<f32x4*>(Y + (ytok0 + 16 * ct + i16) * ldy + ycol + 4 * g) = v;
     }
 }
 
 // One 16-row output tile per wave: Y[tok][ycol + i] = epi(W[row + i] . X[tok]^T + b[row + i]).
-template <int CT, bool RELU>
-__device__ __forceinline__ void linear1(const float* W, int ldw, int kw0, const float* bias, int row, const float* X,
-                                        int ldx, int xtok0, float* Y, int ldy, int ycol, int ytok0) {
-    const int rows[1] = {row};
-    const int cols[1] = {ycol};
-    f32x4 acc[1][CT];
+template <int CT, bool RELU, int D>
+__device__ __forceinline__ void linear1(const APre<D>& pre, const float* W, int ldw, const float* bias, int row,
+                                        const float* X, int ldx, int xtok0, float* Y, int ldy, int ycol, int ytok0) {
+    f32x4 acc[CT];
     zero(acc);
-    gemm_acc<1, CT, depth<CT>()>(acc, W, ldw, rows, kw0, X, ldx, xtok0);
-    store_acc<1, CT, RELU>(acc, bias, rows, Y, ldy, cols, ytok0);
+    gemm_tile<CT, D>(acc, pre, W, ldw, row, 0, X, ldx, xtok0);
+    store_tile<CT, RELU>(acc, bias, row, Y, ldy, ycol, ytok0);
 }
 
 // ------------------------------------------------------------------ VALU pieces
@@ -279,11 +283,15 @@ __device__ void embed(Smem& sm, const float* __restrict__ P) {
     }
 }
 
+// K/V weight row of wave wv for chunk c: waves 0-3 K tiles, waves 4-7 V tiles
+__device__ __forceinline__ int kv_row(int wv, int c) { return (1 + (wv >> 2)) * D + 64 * c + 16 * (wv & 3); }
+
 // One post-LN nn.TransformerEncoderLayer (relu FFN 256, 8 heads). last: prune to column tile 4.
 // Work split: 8 waves, wave w and w+4 share a SIMD (and its MFMA pipe); every GEMM gives each
-// SIMD the same number of 16-row output tiles.
+// SIMD the same number of 16-row output tiles. `pkv` = the caller's prefetch of this layer's first
+// K/V weight blocks. Ends WITHOUT a final barrier: the caller prefetches its next weights, then syncs.
 template <int trunk, int layer, bool last>
-__device__ void encoder_layer(Smem& sm, const float* __restrict__ P) {
+__device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv) {
     const float* Win = P + kOffs.o[layer_param(trunk, layer, INW)];
     const float* bin = P + kOffs.o[layer_param(trunk, layer, INB)];
     const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
@@ -294,54 +302,59 @@ __device__ void encoder_layer(Smem& sm, const float* __restrict__ P) {
     const float* b2 = P + kOffs.o[layer_param(trunk, layer, L2B)];
     const int wv = threadIdx.x >> 6;
     constexpr int CTQ = last ? 1 : S;              // column tiles that need Q / out / LN / FFN
+    constexpr int DQ = depth<CTQ>();
     constexpr int qtok0 = last ? (S - 1) * SPW : 0;
     constexpr int nqs = last ? 1 : S;
 
+    APre<DQ> po;
+#pragma unroll
     for (int c = 0; c < 2; ++c) {  // two chunks of 4 heads (LDS budget)
+        APre<DQ> pq;
+        if (wv < 4) pq = prefetch<DQ>(Win, D, 64 * c + 16 * wv, 0);
         // K (waves 0-3) / V (waves 4-7) of the chunk for all 80 tokens, one 16-row tile each
-        {
-            const int part = 1 + (wv >> 2), tt = wv & 3;
-            linear1<S, false>(Win, D, 0, bin, part * D + 64 * c + 16 * tt, sm.h, LDH, 0, sm.big, LDB,
-                              part * 64 + 16 * tt, 0);
-        }
+        linear1<S, false, 2>(pkv, Win, D, bin, kv_row(wv, c), sm.h, LDH, 0, sm.big, LDB, (1 + (wv >> 2)) * 64 + 16 * (wv & 3), 0);
         // Q of the chunk for the query tokens, waves 0-3 (their SIMD partners did V)
-        if (wv < 4) linear1<CTQ, false>(Win, D, 0, bin, 64 * c + 16 * wv, sm.h, LDH, qtok0, sm.big, LDB, 16 * wv, qtok0);
+        if (wv < 4) linear1<CTQ, false, DQ>(pq, Win, D, bin, 64 * c + 16 * wv, sm.h, LDH, qtok0, sm.big, LDB, 16 * wv, qtok0);
+        if (c == 0) pkv = prefetch<2>(Win, D, kv_row(wv, 1), 0);
+        else po = prefetch<DQ>(Wo, D, 16 * wv, 0);
         __syncthreads();
         attention_chunk(sm, c, last ? S - 1 : 0, nqs);
         __syncthreads();
     }
     // out projection -> big, then h = LN1(h + attn)
-    linear1<CTQ, false>(Wo, D, 0, bo, 16 * wv, sm.ctx, LDH, qtok0, sm.big, LDB, 16 * wv, qtok0);
+    linear1<CTQ, false, DQ>(po, Wo, D, bo, 16 * wv, sm.ctx, LDH, qtok0, sm.big, LDB, 16 * wv, qtok0);
+    const APre<DQ> pf1a = prefetch<DQ>(W1, D, 16 * wv, 0);
+    const APre<DQ> pf1b = prefetch<DQ>(W1, D, 128 + 16 * wv, 0);
     __syncthreads();
     add_layernorm(sm.h, sm.big, LDB, qtok0, nqs * SPW, P + kOffs.o[layer_param(trunk, layer, N1W)],
                   P + kOffs.o[layer_param(trunk, layer, N1B)]);
     __syncthreads();
-    // FFN: hidden 256 in two chunks of 128, second GEMM accumulated in registers
-    f32x4 acc2[1][CTQ];
+    // FFN: hidden features 0-127 -> big, 128-255 -> ctx (both free now), then one K=256 GEMM
+    linear1<CTQ, true, DQ>(pf1a, W1, D, b1, 16 * wv, sm.h, LDH, qtok0, sm.big, LDF, 16 * wv, qtok0);
+    linear1<CTQ, true, DQ>(pf1b, W1, D, b1, 128 + 16 * wv, sm.h, LDH, qtok0, sm.ctx, LDF, 16 * wv, qtok0);
+    const APre<DQ> pf2a = prefetch<DQ>(W2, FF, 16 * wv, 0);
+    __syncthreads();
+    f32x4 acc2[CTQ];
     zero(acc2);
-    const int rows2[1] = {16 * wv};
-    for (int hc = 0; hc < 2; ++hc) {
-        linear1<CTQ, true>(W1, D, 0, b1, 128 * hc + 16 * wv, sm.h, LDH, qtok0, sm.big, LDF, 16 * wv, qtok0);
-        __syncthreads();
-        gemm_acc<1, CTQ, depth<CTQ>()>(acc2, W2, FF, rows2, 128 * hc, sm.big, LDF, qtok0);
-        __syncthreads();
-    }
-    store_acc<1, CTQ, false>(acc2, b2, rows2, sm.ctx, LDH, rows2, qtok0);
+    const APre<DQ> pf2b = prefetch<DQ>(W2, FF, 16 * wv, 128);
+    gemm_tile<CTQ, DQ>(acc2, pf2a, W2, FF, 16 * wv, 0, sm.big, LDF, qtok0);
+    gemm_tile<CTQ, DQ>(acc2, pf2b, W2, FF, 16 * wv, 128, sm.ctx, LDF, qtok0);
     __syncthreads();
-    add_layernorm(sm.h, sm.ctx, LDH, qtok0, nqs * SPW, P + kOffs.o[layer_param(trunk, layer, N2W)],
+    store_tile<CTQ, false>(acc2, b2, 16 * wv, sm.big, LDF, 16 * wv, qtok0);
+    __syncthreads();
+    add_layernorm(sm.h, sm.big, LDF, qtok0, nqs * SPW, P + kOffs.o[layer_param(trunk, layer, N2W)],
                   P + kOffs.o[layer_param(trunk, layer, N2B)]);
-    __syncthreads();
 }
 
 // 128 -> 64 (MFMA, waves 0-3) -> relu -> nout (VALU) on the last-position rows (transformer_net.py:77-91)
 template <int head, int nout>
-__device__ void head_mlp(Smem& sm, const float* __restrict__ P, float* out) {
+__device__ void head_mlp(Smem& sm, const float* __restrict__ P, const APre<4>& pw, float* out) {
     const float* W0 = P + kOffs.o[head + 0];
     const float* b0 = P + kOffs.o[head + 1];
     const float* W2 = P + kOffs.o[head + 2];
     const float* b2 = P + kOffs.o[head + 3];
     const int wv = threadIdx.x >> 6;
-    if (wv < HID / 16) linear1<1, true>(W0, D, 0, b0, 16 * wv, sm.h, LDH, (S - 1) * SPW, sm.z, LDZ, 16 * wv, 0);
+    if (wv < HID / 16) linear1<1, true, 4>(pw, W0, D, b0, 16 * wv, sm.h, LDH, (S - 1) * SPW, sm.z, LDZ, 16 * wv, 0);
     __syncthreads();
     if (threadIdx.x < SPW * nout) {
         const int p = threadIdx.x / nout, a = threadIdx.x - p * nout;
@@ -372,17 +385,29 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         for (int k = 0; k < IN; ++k) z = z && (sm.x[(s * SPW + p) * LDX + k] == 0.f);
         sm.mask[p * S + s] = (s < S - 1) && z;
     }
+    const int wv = threadIdx.x >> 6;
+    const float* headw_a = P + kOffs.o[kActorHead];
+    const float* headw_c = P + kOffs.o[kCriticHead];
     // actor trunk (1 layer) + head
     embed<kActorTrunk>(sm, P);
+    APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
     __syncthreads();
-    encoder_layer<kActorTrunk, 0, true>(sm, P);
-    head_mlp<kActorHead, 2>(sm, P, sm.logits);
+    encoder_layer<kActorTrunk, 0, true>(sm, P, pkv);
+    APre<4> ph;
+    if (wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
+    __syncthreads();
+    head_mlp<kActorHead, 2>(sm, P, ph, sm.logits);
     // critic trunk (2 layers) + head
     embed<kCriticTrunk>(sm, P);
+    pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
     __syncthreads();
-    encoder_layer<kCriticTrunk, 0, false>(sm, P);
-    encoder_layer<kCriticTrunk, 1, true>(sm, P);
-    head_mlp<kCriticHead, 1>(sm, P, sm.value);
+    encoder_layer<kCriticTrunk, 0, false>(sm, P, pkv);
+    pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
+    __syncthreads();
+    encoder_layer<kCriticTrunk, 1, true>(sm, P, pkv);
+    if (wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
+    __syncthreads();
+    head_mlp<kCriticHead, 1>(sm, P, ph, sm.value);
     // Categorical(softmax(logits)): sample / log_prob / entropy (transformer_net.py:118-122)
     if (threadIdx.x < SPW) {
         const int p = threadIdx.x, b = b0 + p;
