@@ -36,6 +36,21 @@ MFMA_F32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: fp32 MFMA = vector 
 HBM_PEAK_GBS = 8000.0
 
 
+def profiled_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN_pmc.json, written by scripts/summarize_profile.py from separate rocprofv3
+    --pmc FETCH_SIZE / WRITE_SIZE passes of this benchmark; FETCH doubled per the gfx950 note)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    for k, v in d.get("pmc", {}).items():
+        if k.endswith(kernel) and "hbm_bytes_per_launch" in v:
+            return v["hbm_bytes_per_launch"], os.path.basename(files[-1])
+    return None, None
+
+
 def env_bytes_per_step(M):
     return 24 * M + 490
 
@@ -204,6 +219,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, policy.state_dict(), args.cpu_seconds)
 
+    pol_traffic, pol_src = profiled_traffic("k_policy_forward")
+    env_traffic, _ = profiled_traffic("k_env_step<1>")
     if rank == 0:
         line = {
             "metric": "env-steps/sec (whole node), full PPO rollout, 4096 envs x 16 UAV x 32 tgt per GPU",
@@ -218,9 +235,11 @@ def main():
                        "full_reset_period": 200},
             "roofline": {"kernel": "k_policy_forward", "bound": "mfma", "achieved": achieved_tf,
                          "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / MFMA_F32_PEAK_TFLOPS,
-                         "traffic": None, "avg_launch_ms": pol_ms, "flop_per_launch": POLICY_FLOP_PER_SAMPLE * E},
+                         "traffic": pol_traffic, "traffic_unit": "bytes/launch (PMC)", "traffic_source": pol_src,
+                         "avg_launch_ms": pol_ms, "flop_per_launch": POLICY_FLOP_PER_SAMPLE * E},
             "env_roofline": {"kernel": "k_env_step", "bound": "hbm", "achieved": env_gbs, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS, "avg_launch_ms": env_ms,
+                             "traffic": env_traffic,
                              "bytes_per_env_step": env_bytes_per_step(args.targets)},
             "ppo_samples_per_s": ppo,
             "cpu_baseline": cpu,
