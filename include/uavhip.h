@@ -89,8 +89,12 @@ enum uavhip_ist {
     UAVHIP_IST_N_COVERED,   /* N0: targets with >= 1 lock    */
     UAVHIP_IST_N_ASSIGNED,  /* locked (uav, target) pairs    */
     UAVHIP_IST_EPISODE,     /* 1-based episode counter (main_train.py:77-79 cadence) */
-    UAVHIP_IST_ERROR,       /* set to 1 when a finished env is stepped without auto-reset */
-    UAVHIP_IST_PAD0, UAVHIP_IST_PAD1,
+    UAVHIP_IST_ERROR,       /* bit 0: a finished env was stepped without auto-reset;
+                               bit 1: a full reset found no fresh spare scene (state-only reset done) */
+    UAVHIP_IST_SCENE_SEL,   /* active scene buffer (0/1) when scene_buffers == 2 */
+    UAVHIP_IST_SCENE_STALE, /* 1: the spare buffer still holds a used scene (uavhip_scene_refresh) */
+    UAVHIP_IST_SCENE_GEN,   /* number of on-device scenes generated for this env (Philox counter) */
+    UAVHIP_IST_PAD0, UAVHIP_IST_PAD1, UAVHIP_IST_PAD2,
     UAVHIP_IST_COUNT
 };
 
@@ -113,8 +117,13 @@ enum uavhip_dst {
  */
 typedef struct uavhip_env {
     int32_t E, N, M, Kn, Ki;
-    int32_t full_reset_period; /* auto-reset: regenerate the scene when episode % period == 0
-                                  (200 in main_train.py:79); 0 = state-only resets          */
+    int32_t full_reset_period; /* auto-reset: switch to a fresh scene when episode % period == 0
+                                  (200 in main_train.py:79); 0 = state-only resets. Needs
+                                  scene_buffers == 2.                                         */
+    int32_t scene_buffers;     /* 1, or 2 = every scene array and pair table below is
+                                  [2][E]...: buffer istate[SCENE_SEL] is active, the other a
+                                  pre-generated spare a full reset flips to                  */
+    int32_t pad_;
     uint64_t seed;             /* Philox key for on-device scene generation                 */
     double prm[UAVHIP_PRM_COUNT];
     double gen[UAVHIP_GEN_COUNT];
@@ -147,14 +156,20 @@ typedef struct uavhip_env {
 
 /* ---------------------------------------------------------------- env (K1, K2, reset, gen) */
 
-/* K1. Dense pair tables p_dmg[E][N][M], p_pen[E][N] from the scene arrays, for the envs with
- * mask[e] != 0 (mask NULL = all). Replaces calc_advantage's per-call recomputation
+/* K1. Dense pair tables p_dmg[E][N][M], p_pen[E][N] of the ACTIVE scene buffer from the scene
+ * arrays, for the envs with mask[e] != 0 (mask NULL = all). Replaces calc_advantage's per-call recomputation
  * (mechanics.py:93-181; called ~42x per env step by uav_env.py:184-435). */
 int uavhip_score_pairs(const uavhip_env* env, const uint8_t* mask, uavhip_stream_t stream);
 
 /* Philox4x32-10 scene generation on device (distribution of uav_env.py:65-173, not its
- * MT19937 stream) for masked envs, followed by K1 for them. `episode` feeds the counter. */
+ * MT19937 stream) into the ACTIVE buffer of masked envs (and the spare, when scene_buffers == 2),
+ * followed by K1 for them; the counter is (env, istate[SCENE_GEN]). */
 int uavhip_scene_generate(const uavhip_env* env, const uint8_t* mask, uavhip_stream_t stream);
+
+/* Regenerate (Philox + K1) the spare scene buffer of every env whose istate[SCENE_STALE] is set,
+ * i.e. that flipped to its spare at a full reset. Call once per rollout iteration (full resets
+ * are >= full_reset_period episodes apart). No-op unless scene_buffers == 2. */
+int uavhip_scene_refresh(const uavhip_env* env, uavhip_stream_t stream);
 
 /* UAVEnv.reset(full_reset=False) (uav_env.py:42-63,175-182) for masked envs: clears the
  * allocation, recomputes the scene totals, writes the first window to obs_out[E][5][14]

@@ -22,8 +22,9 @@ GEN = dict(UAV_X0=0, UAV_X1=1, TGT_X0=2, TGT_X1=3, MAP_H=4, WEATHER_SPEED=5, WEA
 GEN_COUNT = 16
 INFO = dict(J=0, NUM_ASSIGNED=1, IS_VALID=2, AVG_P_DMG=3, AVG_P_FINAL=4, UAV_IDX=5, TARGET_IDX=6, EPISODE=7)
 INFO_COUNT = 8
-IST = dict(UAV_IDX=0, TARGET_IDX=1, N_COVERED=2, N_ASSIGNED=3, EPISODE=4, ERROR=5)
-IST_COUNT = 8
+IST = dict(UAV_IDX=0, TARGET_IDX=1, N_COVERED=2, N_ASSIGNED=3, EPISODE=4, ERROR=5, SCENE_SEL=6, SCENE_STALE=7,
+           SCENE_GEN=8)
+IST_COUNT = 12
 DST = dict(R=0, J=1, ASG_COST=2, COV_VALUE=3, TOTAL_COST=4, TOTAL_VALUE=5)
 DST_COUNT = 8
 
@@ -34,7 +35,7 @@ _i32 = ctypes.c_int32
 class EnvDesc(ctypes.Structure):
     """Mirror of `struct uavhip_env` (include/uavhip.h)."""
     _fields_ = [("E", _i32), ("N", _i32), ("M", _i32), ("Kn", _i32), ("Ki", _i32),
-                ("full_reset_period", _i32), ("seed", ctypes.c_uint64),
+                ("full_reset_period", _i32), ("scene_buffers", _i32), ("pad_", _i32), ("seed", ctypes.c_uint64),
                 ("prm", ctypes.c_double * PRM_COUNT), ("gen", ctypes.c_double * GEN_COUNT)] + \
               [(n, _vp) for n in ("uav_pos", "uav_vel", "uav_load", "uav_cost", "uav_type", "tgt_pos", "tgt_vel",
                                   "tgt_value", "tgt_id", "nfz_pos", "icp_pos", "icp_vel", "p_dmg", "p_pen",
@@ -52,6 +53,7 @@ class PolicyDesc(ctypes.Structure):
 _SIGS = {
     "uavhip_score_pairs": (ctypes.c_int, [ctypes.POINTER(EnvDesc), _vp, _vp]),
     "uavhip_scene_generate": (ctypes.c_int, [ctypes.POINTER(EnvDesc), _vp, _vp]),
+    "uavhip_scene_refresh": (ctypes.c_int, [ctypes.POINTER(EnvDesc), _vp]),
     "uavhip_env_reset": (ctypes.c_int, [ctypes.POINTER(EnvDesc), _vp, _i32, _vp, _vp]),
     "uavhip_env_step": (ctypes.c_int, [ctypes.POINTER(EnvDesc), _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "uavhip_gae": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp,

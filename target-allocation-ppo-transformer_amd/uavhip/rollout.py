@@ -71,6 +71,7 @@ class RolloutEngine:
                               seed=self.seed, offset=self._step_counter * E)
             last = tr.last_values
         gae(tr.rewards, tr.dones, tr.values, last_values=last, out=(tr.ret, tr.adv, tr.partials, tr.stats))
+        env.refresh_scenes()  # regenerate spare scenes consumed by full resets (off the step path)
         return tr
 
     def roll(self):

@@ -18,7 +18,7 @@ SCENE_KEYS_F64 = ("uav_pos", "uav_vel", "uav_load", "uav_cost", "tgt_pos", "tgt_
 
 class VecUAVEnv:
     def __init__(self, num_envs, num_uavs=None, num_targets=None, num_nfz=None, num_interceptors=None, config=None,
-                 device="cuda", seed=0, full_reset_period=None):
+                 device="cuda", seed=0, full_reset_period=None, scene_buffers=None):
         c = config or default_cfg
         self.cfg = c
         self.E = int(num_envs)
@@ -33,36 +33,38 @@ class VecUAVEnv:
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise RuntimeError("VecUAVEnv runs on the GPU (HIP) only; the CPU oracle lives in oracle/ (tests)")
+        period = c.FULL_RESET_PERIOD if full_reset_period is None else int(full_reset_period)
+        B = (2 if period > 0 else 1) if scene_buffers is None else int(scene_buffers)
+        self.period, self.B = period, B
         E, N, M, Kn, Ki = self.E, self.N, self.M, self.Kn, self.Ki
         f64 = dict(dtype=torch.float64, device=self.device)
         i32 = dict(dtype=torch.int32, device=self.device)
         z = torch.zeros
-        self.uav_pos, self.uav_vel = z(E, N, 2, **f64), z(E, N, 2, **f64)
-        self.uav_load, self.uav_cost = z(E, N, **f64), z(E, N, **f64)
-        self.uav_type = z(E, N, **i32)
-        self.tgt_pos, self.tgt_vel = z(E, M, 2, **f64), z(E, M, 2, **f64)
-        self.tgt_value, self.tgt_id = z(E, M, **f64), z(E, M, **i32)
-        self.nfz_pos = z(E, max(Kn, 1), 2, **f64)
-        self.icp_pos, self.icp_vel = z(E, max(Ki, 1), 2, **f64), z(E, max(Ki, 1), 2, **f64)
-        self.p_dmg, self.p_pen = z(E, N, M, **f64), z(E, N, **f64)
+        # scene arrays and pair tables: [B * E, ...]; env e's active scene is row sel * E + e
+        self._scene = dict(
+            uav_pos=z(B * E, N, 2, **f64), uav_vel=z(B * E, N, 2, **f64), uav_load=z(B * E, N, **f64),
+            uav_cost=z(B * E, N, **f64), uav_type=z(B * E, N, **i32), tgt_pos=z(B * E, M, 2, **f64),
+            tgt_vel=z(B * E, M, 2, **f64), tgt_value=z(B * E, M, **f64), tgt_id=z(B * E, M, **i32),
+            nfz_pos=z(B * E, max(Kn, 1), 2, **f64), icp_pos=z(B * E, max(Ki, 1), 2, **f64),
+            icp_vel=z(B * E, max(Ki, 1), 2, **f64), p_dmg=z(B * E, N, M, **f64), p_pen=z(B * E, N, **f64))
         self.nh_final, self.nh_pure = z(E, M, **f64), z(E, M, **f64)
         self.t_cost, self.n_lock = z(E, M, **f64), z(E, M, **i32)
         self.assigned = torch.full((E, N), -1, **i32)
         self.istate = z(E, _lib.IST_COUNT, **i32)
         self.dstate = z(E, _lib.DST_COUNT, **f64)
         self.window = z(E, _lib.SEQ_LEN, _lib.STATE_DIM, dtype=torch.float32, device=self.device)
-        period = c.FULL_RESET_PERIOD if full_reset_period is None else full_reset_period
         d = _lib.EnvDesc()
         d.E, d.N, d.M, d.Kn, d.Ki = E, N, M, Kn, Ki
-        d.full_reset_period = int(period)
+        d.full_reset_period = period
+        d.scene_buffers = B
         d.seed = int(seed) & (2 ** 64 - 1)
         for i, v in enumerate(params_vector(c)):
             d.prm[i] = float(v)
         for i, v in enumerate(gen_vector(c)):
             d.gen[i] = float(v)
-        for name in ("uav_pos", "uav_vel", "uav_load", "uav_cost", "uav_type", "tgt_pos", "tgt_vel", "tgt_value",
-                     "tgt_id", "nfz_pos", "icp_pos", "icp_vel", "p_dmg", "p_pen", "nh_final", "nh_pure", "t_cost",
-                     "n_lock", "assigned", "istate", "dstate", "window"):
+        for name, t in self._scene.items():
+            setattr(d, name, t.data_ptr())
+        for name in ("nh_final", "nh_pure", "t_cost", "n_lock", "assigned", "istate", "dstate", "window"):
             setattr(d, name, getattr(self, name).data_ptr())
         self.desc = d
         # per-step output buffers (reused; [E] views of the T=1 case)
@@ -72,26 +74,47 @@ class VecUAVEnv:
         self._info = torch.zeros(E, _lib.INFO_COUNT, **f64)
 
     # ------------------------------------------------------------------ scenes
+    def scene_sel(self):
+        return (self.istate[:, _lib.IST["SCENE_SEL"]] & 1).long() if self.B == 2 else \
+            torch.zeros(self.E, dtype=torch.long, device=self.device)
+
+    def active(self, name):
+        """Env-indexed [E, ...] copy of scene array `name` from each env's active buffer."""
+        t = self._scene[name]
+        if self.B == 1:
+            return t
+        rows = self.scene_sel() * self.E + torch.arange(self.E, device=self.device)
+        return t[rows]
+
+    def __getattr__(self, name):
+        scene = self.__dict__.get("_scene")
+        if scene is not None and name in scene:
+            return self.active(name)
+        raise AttributeError(name)
+
     def set_params(self, params):
         for i, v in enumerate(np.asarray(params, np.float64)):
             self.desc.prm[i] = float(v)
 
     def load_scenes(self, scenes, env_ids=None):
-        """Copy host scenes (dicts in the tests/golden / scene.generate_scene layout) into envs
-        `env_ids` (default 0..len-1), then rescore their pair tables."""
+        """Copy host scenes (dicts in the tests/golden / scene.generate_scene layout) into buffer 0
+        of envs `env_ids` (default 0..len-1), make it their active scene, rescore it. With two
+        buffers the spare is marked stale (uavhip_scene_refresh fills it on device)."""
         if isinstance(scenes, dict):
             scenes = [scenes]
         ids = list(range(len(scenes))) if env_ids is None else list(env_ids)
         mask = torch.zeros(self.E, dtype=torch.uint8)
         for e, s in zip(ids, scenes):
             for k in SCENE_KEYS_F64:
-                dst = getattr(self, k)[e]
+                dst = self._scene[k][e]
                 src = torch.as_tensor(np.asarray(s[k], np.float64).reshape(dst.shape) if np.size(s[k]) else
                                       np.zeros(dst.shape))
                 dst.copy_(src)
-            self.tgt_id[e].copy_(torch.as_tensor(np.asarray(s["tgt_id"], np.int32)))
+            self._scene["tgt_id"][e].copy_(torch.as_tensor(np.asarray(s["tgt_id"], np.int32)))
             if "uav_type" in s:
-                self.uav_type[e].copy_(torch.as_tensor(np.asarray(s["uav_type"], np.int32)))
+                self._scene["uav_type"][e].copy_(torch.as_tensor(np.asarray(s["uav_type"], np.int32)))
+            self.istate[e, _lib.IST["SCENE_SEL"]] = 0
+            self.istate[e, _lib.IST["SCENE_STALE"]] = 1 if self.B == 2 else 0
             mask[e] = 1
         self.score_pairs(mask.to(self.device))
         return mask
@@ -100,8 +123,13 @@ class VecUAVEnv:
         check(LIB.uavhip_score_pairs(self.desc, ptr(mask), stream_handle()), "uavhip_score_pairs")
 
     def generate_scenes(self, mask=None):
-        """On-device Philox scenes (distribution of uav_env.py:65-173) + pair tables."""
+        """On-device Philox scenes (distribution of uav_env.py:65-173) + pair tables, for the
+        active buffer and (double-buffered) the spare."""
         check(LIB.uavhip_scene_generate(self.desc, ptr(mask), stream_handle()), "uavhip_scene_generate")
+
+    def refresh_scenes(self):
+        """Regenerate spares consumed by full resets (call once per rollout iteration)."""
+        check(LIB.uavhip_scene_refresh(self.desc, stream_handle()), "uavhip_scene_refresh")
 
     # ------------------------------------------------------------------ reset / step
     def reset(self, mask=None, episode=-1, obs_out=None):

@@ -235,7 +235,6 @@ def test_scene_generation_properties(N, M, Kn, Ki):
     from uavhip.config import cfg, params_vector
     E = 64
     v = _venv(E, N, M, Kn, Ki, seed=1234)
-    v.istate[:, 4] = torch.arange(E, dtype=torch.int32, device="cuda") + 1
     v.generate_scenes()
     torch.cuda.synchronize()
     up = v.uav_pos.cpu().numpy(); uv = v.uav_vel.cpu().numpy(); ut = v.uav_type.cpu().numpy()
@@ -263,14 +262,21 @@ def test_scene_generation_properties(N, M, Kn, Ki):
         np.testing.assert_allclose(v.p_pen[e].cpu().numpy(), pp, rtol=RTOL_P, atol=ATOL_P)
     # determinism: same seed and episode -> same scene
     w = _venv(E, N, M, Kn, Ki, seed=1234)
-    w.istate[:, 4] = torch.arange(E, dtype=torch.int32, device="cuda") + 1
     w.generate_scenes()
     assert torch.equal(w.uav_pos, v.uav_pos) and torch.equal(w.p_dmg, v.p_dmg)
+    assert (v.istate[:, 8] == 1).all()  # one scene generated per env
+    v.generate_scenes()
+    assert not torch.equal(w.uav_pos, v.uav_pos)  # the next generation differs
 
 
 def test_auto_full_reset_regenerates_scene():
-    """With full_reset_period P the scene changes exactly when the episode index hits a multiple of P."""
+    """With full_reset_period P the scene changes exactly when the episode index hits a multiple of
+    P: the step kernel flips to the pre-generated spare, whose pair tables match the oracle's, and
+    uavhip_scene_refresh regenerates the consumed spare off the step path."""
+    import oracle
+    from uavhip.config import cfg, params_vector
     v = _venv(8, 4, 4, 1, 1, period=3, seed=7)
+    assert v.B == 2
     v.istate[:, 4] = 1
     v.generate_scenes()
     v.reset(episode=1)
@@ -278,12 +284,42 @@ def test_auto_full_reset_regenerates_scene():
     pos_prev = v.uav_pos.clone()
     for ep in range(2, 8):
         for _ in range(4):  # 4 UAVs x assign = 4 steps per episode
-            v.step(one, auto_reset=True)
+            obs, r, d, _ = v.step(one, auto_reset=True)
         torch.cuda.synchronize()
-        assert (v.episodes() == ep).all()
+        assert d.all() and (v.episodes() == ep).all()
         changed = not torch.equal(v.uav_pos, pos_prev)
         assert changed == (ep % 3 == 0), ep
+        if changed:
+            assert (v.istate[:, 7] == 1).all()  # spare consumed
+            s = dict(uav_pos=v.uav_pos[0].cpu().numpy(), uav_vel=v.uav_vel[0].cpu().numpy(),
+                     uav_load=v.uav_load[0].cpu().numpy(), tgt_pos=v.tgt_pos[0].cpu().numpy(),
+                     tgt_vel=v.tgt_vel[0].cpu().numpy(), nfz_pos=v.nfz_pos[0].cpu().numpy(),
+                     icp_pos=v.icp_pos[0].cpu().numpy(), icp_vel=v.icp_vel[0].cpu().numpy(),
+                     tgt_value=v.tgt_value[0].cpu().numpy())
+            pd, pp = oracle.score_pairs(s, params_vector(cfg))
+            np.testing.assert_allclose(v.p_dmg[0].cpu().numpy(), pd, rtol=RTOL_P, atol=ATOL_P)
+            # the first window of the new episode is built from the new scene
+            assert obs[0, 4, 1].item() == np.float32(v.tgt_value[0, 0].item()) / 16
+            v.refresh_scenes()
+            torch.cuda.synchronize()
+            assert (v.istate[:, 7] == 0).all()
         pos_prev = v.uav_pos.clone()
+    assert int(v.errors().max()) == 0
+
+
+def test_full_reset_without_refresh_flags_error():
+    """A second full reset before the spare was refreshed keeps the scene and sets error bit 1."""
+    v = _venv(4, 4, 4, 1, 1, period=1, seed=9)
+    v.generate_scenes()
+    v.reset(episode=1)
+    one = torch.ones(4, dtype=torch.int8, device="cuda")
+    for _ in range(4):
+        v.step(one, auto_reset=True)   # episode 2: flips to the spare
+    p1 = v.uav_pos.clone()
+    for _ in range(4):
+        v.step(one, auto_reset=True)   # episode 3: no fresh spare
+    torch.cuda.synchronize()
+    assert torch.equal(v.uav_pos, p1) and ((v.errors() & 2) == 2).all()
 
 
 def test_c5_stress_dims_run():

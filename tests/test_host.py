@@ -60,7 +60,7 @@ def test_ctypes_mirrors_header_enums():
     txt = open(HEADER).read()
     body = re.search(r"typedef struct uavhip_env \{(.*?)\} uavhip_env;", txt, re.S).group(1)
     names = re.findall(r"\*\s*(\w+);", body)
-    assert names == [f[0] for f in _lib.EnvDesc._fields_[9:]]
+    assert names == [f[0] for f in _lib.EnvDesc._fields_[11:]]
 
 
 def test_error_path_without_gpu():
