@@ -68,6 +68,7 @@ def parse():
     ap.add_argument("--no-ppo", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--eager", action="store_true", help="launch kernels eagerly instead of replaying a hipGraph")
     return ap.parse_args()
 
 
@@ -141,51 +142,38 @@ def main():
     eng = RolloutEngine(env, policy, T, want_info=True, bootstrap=True, seed=1000 + rank)
     eng.start()
 
-    # HIP events around every policy launch (same stream as the launch)
-    ev = []
-    orig = policy.fused_forward
+    # The iteration is captured once into a hipGraph and replayed. HIP events (recorded on the
+    # launch stream around every policy / env launch) cannot live inside a ROCm graph, so the LAST
+    # timed iteration runs the same body as eager launches and carries the events: the kernel
+    # timings are live, from inside the timed region.
+    use_graph = not args.eager
+    mode = "hipGraph replay (last iteration eager, with HIP events)" if use_graph else "eager launches"
+    eng.enable_events(external=False)
+    if use_graph:
+        try:
+            eng.capture()
+        except Exception as exc:  # graph capture unavailable: measure eager launches instead
+            print(f"[bench] graph capture failed ({exc!r}); falling back to eager launches", file=sys.stderr)
+            eng.graph = None
+            mode = "eager launches (graph capture failed)"
 
-    def timed_forward(*a, **k):
-        s0 = torch.cuda.Event(enable_timing=True); s1 = torch.cuda.Event(enable_timing=True)
-        s0.record(); out = orig(*a, **k); s1.record()
-        if timing[0]:
-            ev.append((s0, s1))
-        return out
-
-    timing = [False]
-    policy.fused_forward = timed_forward
-    env_ev = []
-    orig_step = env.step
-
-    def timed_step(*a, **k):
-        s0 = torch.cuda.Event(enable_timing=True); s1 = torch.cuda.Event(enable_timing=True)
-        s0.record(); out = orig_step(*a, **k); s1.record()
-        if timing[0]:
-            env_ev.append((s0, s1))
-        return out
-
-    env.step = timed_step
-
-    def iteration():
-        eng.collect()
+    def iteration(eager=False):
+        eng.collect(eager=eager)
         if dist is not None:
             eng.gather()
-        eng.roll()
 
     for _ in range(args.warmup):
         iteration()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    timing[0] = True
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        iteration()
+    for i in range(args.steps):
+        iteration(eager=(i == args.steps - 1))
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     t1 = time.perf_counter()
-    timing[0] = False
     elapsed = t1 - t0
     if dist is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -194,8 +182,9 @@ def main():
     env_steps = E * T * args.steps * world
     value = env_steps / elapsed
 
-    pol_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    env_ms = float(np.mean([a.elapsed_time(b) for a, b in env_ev]))
+    pol_list, env_list = eng.event_ms()   # the last timed iteration's T+1 policy and T env launches
+    pol_ms = float(np.mean(pol_list))
+    env_ms = float(np.mean(env_list))
     achieved_tf = POLICY_FLOP_PER_SAMPLE * E / (pol_ms * 1e-3) / 1e12
     env_gbs = env_bytes_per_step(args.targets) * E / (env_ms * 1e-3) / 1e9
 
@@ -232,11 +221,12 @@ def main():
                        + (" + RCCL trajectory all-gather" if world > 1 else ""),
                        "envs_per_gpu": E, "uavs": args.uavs, "targets": args.targets, "horizon": T,
                        "env_steps_per_step": E * T * world, "parallelism": f"env-sharded x{world}",
-                       "full_reset_period": 200},
+                       "full_reset_period": 200, "launch": mode},
             "roofline": {"kernel": "k_policy_forward", "bound": "mfma", "achieved": achieved_tf,
                          "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / MFMA_F32_PEAK_TFLOPS,
                          "traffic": pol_traffic, "traffic_unit": "bytes/launch (PMC)", "traffic_source": pol_src,
-                         "avg_launch_ms": pol_ms, "flop_per_launch": POLICY_FLOP_PER_SAMPLE * E},
+                         "avg_launch_ms": pol_ms, "flop_per_launch": POLICY_FLOP_PER_SAMPLE * E,
+                         "timing": "HIP events around each of the T+1 launches of the last timed iteration"},
             "env_roofline": {"kernel": "k_env_step", "bound": "hbm", "achieved": env_gbs, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS, "avg_launch_ms": env_ms,
                              "traffic": env_traffic,

@@ -229,12 +229,13 @@ typedef struct uavhip_policy {
 int32_t uavhip_policy_layout(int32_t* offsets, int32_t max_offsets);
 
 /* get_action / evaluate (transformer_net.py:96-144) for B windows states[B][5][14]:
- * actions_in NULL -> sample a ~ Categorical(softmax(logits)) with Philox(seed, offset + b);
- * else evaluate the given actions. Outputs (nullable except where noted): action_out [B] int8,
- * logp [B], value [B], entropy [B], logits [B][2] (all f32). */
+ * actions_in NULL -> sample a ~ Categorical(softmax(logits)) with Philox(seed, c), counter
+ * c = offset + (offset_dev ? *offset_dev : 0) + b (offset_dev: device u64, lets a captured
+ * hipGraph draw fresh numbers on every replay); else evaluate the given actions. Outputs
+ * (nullable): action_out [B] int8, logp [B], value [B], entropy [B], logits [B][2] (all f32). */
 int uavhip_policy_forward(const uavhip_policy* policy, const float* states, int32_t B, const int8_t* actions_in,
-                          uint64_t seed, uint64_t offset, int8_t* action_out, float* logp, float* value,
-                          float* entropy, float* logits, uavhip_stream_t stream);
+                          uint64_t seed, uint64_t offset, const uint64_t* offset_dev, int8_t* action_out,
+                          float* logp, float* value, float* entropy, float* logits, uavhip_stream_t stream);
 
 /* ---------------------------------------------------------------- misc */
 const char* uavhip_last_error(void);

@@ -368,7 +368,8 @@ __device__ void head_mlp(Smem& sm, const float* __restrict__ P, const APre<4>& p
 
 __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict__ P, const float* __restrict__ states,
                                                          int B, const int8_t* __restrict__ actions_in, uint64_t seed,
-                                                         uint64_t offset, int8_t* __restrict__ action_out,
+                                                         uint64_t offset, const uint64_t* __restrict__ offset_dev,
+                                                         int8_t* __restrict__ action_out,
                                                          float* __restrict__ logp_out, float* __restrict__ value_out,
                                                          float* __restrict__ ent_out, float* __restrict__ logits_out) {
     __shared__ __attribute__((aligned(16))) Smem sm;
@@ -421,7 +422,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
             if (actions_in) {
                 a = actions_in[b] != 0;
             } else {
-                const unsigned long long c = offset + (unsigned long long)b;
+                const unsigned long long c = offset + (offset_dev ? *offset_dev : 0ull) + (unsigned long long)b;
                 const u32x4 r = philox(u32x4{(uint32_t)c, (uint32_t)(c >> 32), 0x5eedu, 0x9e37u}, (uint32_t)seed,
                                        (uint32_t)(seed >> 32));
                 a = u01f(r.x) < p0 ? 0 : 1;
@@ -447,9 +448,9 @@ extern "C" int32_t uavhip_policy_layout(int32_t* offsets, int32_t max_offsets) {
 }
 
 extern "C" int uavhip_policy_forward(const uavhip_policy* policy, const float* states, int32_t B,
-                                     const int8_t* actions_in, uint64_t seed, uint64_t offset, int8_t* action_out,
-                                     float* logp, float* value, float* entropy, float* logits,
-                                     uavhip_stream_t stream) {
+                                     const int8_t* actions_in, uint64_t seed, uint64_t offset,
+                                     const uint64_t* offset_dev, int8_t* action_out, float* logp, float* value,
+                                     float* entropy, float* logits, uavhip_stream_t stream) {
     if (!policy || !policy->weights || !states || B <= 0) {
         set_error("uavhip_policy_forward: NULL policy/weights/states or B=%d", B);
         return UAVHIP_EINVAL;
@@ -463,6 +464,6 @@ extern "C" int uavhip_policy_forward(const uavhip_policy* policy, const float* s
     }
     const int grid = (B + pol::SPW - 1) / pol::SPW;
     hipLaunchKernelGGL(pol::k_policy_forward, dim3(grid), dim3(pol::NTHR), 0, (hipStream_t)stream, policy->weights,
-                       states, (int)B, actions_in, seed, offset, action_out, logp, value, entropy, logits);
+                       states, (int)B, actions_in, seed, offset, offset_dev, action_out, logp, value, entropy, logits);
     return check_launch("k_policy_forward");
 }

@@ -63,7 +63,7 @@ _SIGS = {
     "uavhip_adv_normalize": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _i32, ctypes.c_int64, _vp, _vp]),
     "uavhip_policy_layout": (_i32, [ctypes.POINTER(_i32), _i32]),
     "uavhip_policy_forward": (ctypes.c_int, [ctypes.POINTER(PolicyDesc), _vp, _i32, _vp, ctypes.c_uint64,
-                                             ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp]),
+                                             ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "uavhip_last_error": (ctypes.c_char_p, []),
     "uavhip_abi_version": (_i32, []),
 }

@@ -92,7 +92,11 @@ class TransformerActorCritic(nn.Module):
         key = (dev, tuple(p._version for p in params), tuple(p.data_ptr() for p in params))
         if self._packed is not None and self._packed_key == key:
             return self._packed
-        self._packed = pack_weights(self.state_dict(), device=dev)
+        fresh = pack_weights(self.state_dict(), device=dev)
+        if self._packed is not None and self._packed.device == dev and self._packed.numel() == fresh.numel():
+            self._packed.copy_(fresh)  # in place: a captured hipGraph keeps pointing at this buffer
+        else:
+            self._packed = fresh
         self._packed_key = key
         d = _lib.PolicyDesc()
         d.weights = self._packed.data_ptr()
@@ -103,15 +107,18 @@ class TransformerActorCritic(nn.Module):
         return self._packed
 
     def fused_forward(self, states, actions=None, action_out=None, logp=None, value=None, entropy=None,
-                      logits=None, seed=None, offset=None):
-        """Raw fused forward on [B, 5, 14] fp32 device windows; returns the output tensors."""
+                      logits=None, seed=None, offset=None, offset_dev=None, check_weights=True):
+        """Raw fused forward on [B, 5, 14] fp32 device windows; returns the output tensors.
+        offset_dev: optional device uint64 [1] added to the sampling counter (graph replays);
+        check_weights=False skips the repack check (caller guarantees the pack is current)."""
         if states.device.type != "cuda":
             raise RuntimeError("the fused policy forward runs on the GPU (HIP) only")
         states = states.contiguous()
         if states.dtype != torch.float32:
             states = states.float()
         B = states.shape[0]
-        self.packed_weights()
+        if check_weights or self._packed is None:
+            self.packed_weights()
         dev = states.device
         action_out = torch.empty(B, dtype=torch.int8, device=dev) if action_out is None else action_out
         logp = torch.empty(B, dtype=torch.float32, device=dev) if logp is None else logp
@@ -123,7 +130,7 @@ class TransformerActorCritic(nn.Module):
             self._sample_offset += B
         seed = self.sample_seed if seed is None else seed
         check(LIB.uavhip_policy_forward(self._desc, ptr(states), B, ptr(actions), ctypes.c_uint64(seed),
-                                        ctypes.c_uint64(offset), ptr(action_out), ptr(logp), ptr(value),
+                                        ctypes.c_uint64(offset), ptr(offset_dev), ptr(action_out), ptr(logp), ptr(value),
                                         ptr(entropy), ptr(logits), stream_handle()), "uavhip_policy_forward")
         return action_out, logp, value, entropy, logits
 

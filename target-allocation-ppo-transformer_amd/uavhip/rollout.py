@@ -1,10 +1,14 @@
 """Batched PPO rollout on one GPU: the hot path of BASELINE.json's north_star.
 
 One iteration = T steps of {fused policy forward -> Philox sample -> fused env step} over E
-envs (all on device, no host sync), a bootstrap value pass, GAE + advantage normalisation, and,
-with world_size > 1, one all-gather of the trajectory over RCCL. It replaces the
-reference's per-transition loop (main_train.py:109-117 -> ppo.py:52-66 -> uav_env.py:295) and its
-Python GAE loop (ppo.py:81-89).
+envs (all on device, no host sync), a bootstrap value pass, GAE + advantage normalisation, the
+refresh of spare scenes consumed by full resets, and (caller) with world_size > 1 one all-gather
+of the trajectory over RCCL. It replaces the reference's per-transition loop
+(main_train.py:109-117 -> ppo.py:52-66 -> uav_env.py:295) and its Python GAE loop (ppo.py:81-89).
+
+The iteration can be captured once into a hipGraph (`capture()`) and replayed: the sampling
+counter then lives on the device (advanced by the graph itself), and the policy weights are
+repacked in place, so replays stay valid across PPO updates.
 
 Departure from the reference (flagged): the rollout is truncated at a fixed horizon T and the
 step after T-1 is bootstrapped with V(s_T) (the reference only ever updates on complete episodes,
@@ -44,39 +48,93 @@ class RolloutEngine:
         self.bootstrap = bootstrap
         self.seed = int(seed)
         self.traj = Trajectory(self.T, env.E, env.device, want_info)
-        self._step_counter = 0
+        self.counter = torch.zeros(1, dtype=torch.int64, device=env.device)  # sampling counter base
+        self.graph = None
+        self.policy_events = None   # [(start, end)] HIP events around each policy launch (optional)
+        self.env_events = None
 
     def start(self, generate=True):
         """Fresh scenes on device (Philox) for every env, episode counter 1, first windows."""
-        E = self.env.E
         if generate:
             self.env.istate[:, _lib.IST["EPISODE"]] = 1
             self.env.generate_scenes()
-        self.env.reset(episode=1, obs_out=self.traj.obs[0])
+        self.env.reset(episode=1, obs_out=self.traj.obs[self.T])  # moved to obs[0] by the first _body
 
-    @torch.no_grad()
-    def collect(self):
-        tr, env, pol = self.traj, self.env, self.policy
-        E = env.E
+    def _forward(self, t, obs, actions, logp, value):
+        ev = self.policy_events
+        if ev is not None:
+            ev[t][0].record()
+        self.policy.fused_forward(obs, action_out=actions, logp=logp, value=value, seed=self.seed,
+                                  offset=t * self.env.E, offset_dev=self.counter, check_weights=False)
+        if ev is not None:
+            ev[t][1].record()
+
+    def _body(self):
+        tr, env = self.traj, self.env
+        tr.obs[0].copy_(tr.obs[self.T])  # carry the previous iteration's last window
+        eev = self.env_events
         for t in range(self.T):
-            pol.fused_forward(tr.obs[t], action_out=tr.actions[t], logp=tr.logp[t], value=tr.values[t],
-                              seed=self.seed, offset=self._step_counter * E)
-            self._step_counter += 1
+            self._forward(t, tr.obs[t], tr.actions[t], tr.logp[t], tr.values[t])
+            if eev is not None:
+                eev[t][0].record()
             env.step(tr.actions[t], auto_reset=True, obs_out=tr.obs[t + 1], reward_out=tr.rewards[t],
                      done_out=tr.dones[t], info_out=None if tr.info is None else tr.info[t],
                      want_info=tr.info is not None)
+            if eev is not None:
+                eev[t][1].record()
         last = None
         if self.bootstrap:
-            pol.fused_forward(tr.obs[self.T], action_out=tr.last_actions, logp=tr.last_logp, value=tr.last_values,
-                              seed=self.seed, offset=self._step_counter * E)
+            self._forward(self.T, tr.obs[self.T], tr.last_actions, tr.last_logp, tr.last_values)
             last = tr.last_values
         gae(tr.rewards, tr.dones, tr.values, last_values=last, out=(tr.ret, tr.adv, tr.partials, tr.stats))
         env.refresh_scenes()  # regenerate spare scenes consumed by full resets (off the step path)
-        return tr
+        self.counter.add_((self.T + 1) * env.E)
+
+    @torch.no_grad()
+    def collect(self, eager=False):
+        """One rollout iteration: a graph replay when captured (unless eager=True), else eager
+        launches (which also record the HIP events, if enabled). Both advance the same device state."""
+        self.policy.packed_weights()  # repack in place if the weights changed (e.g. after an update)
+        if self.graph is not None and not eager:
+            self.graph.replay()
+        else:
+            self._body()
+        return self.traj
 
     def roll(self):
-        """Carry the last observation window into the next iteration's obs[0]."""
-        self.traj.obs[0].copy_(self.traj.obs[self.T])
+        """Kept for API compatibility: each iteration starts by carrying obs[T] into obs[0]."""
+
+    def enable_events(self, external=False):
+        """HIP events around every policy / env launch (external=True: graph-capturable nodes)."""
+        kw = dict(enable_timing=True)
+        if external:
+            kw["external"] = True
+        self.policy_events = [(torch.cuda.Event(**kw), torch.cuda.Event(**kw)) for _ in range(self.T + 1)]
+        self.env_events = [(torch.cuda.Event(**kw), torch.cuda.Event(**kw)) for _ in range(self.T)]
+
+    def event_ms(self):
+        """(policy launch ms list, env launch ms list) of the most recent iteration."""
+        return ([a.elapsed_time(b) for a, b in self.policy_events], [a.elapsed_time(b) for a, b in self.env_events])
+
+    @torch.no_grad()
+    def capture(self):
+        """Capture one iteration into a hipGraph. The state it advances lives on the device,
+        so every replay is the next iteration. HIP events are not captured (ROCm disallows
+        external events in graphs); eager iterations still record them."""
+        events = (self.policy_events, self.env_events)
+        self.policy_events = self.env_events = None
+        self.policy.packed_weights()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up outside capture (allocator / lazy init)
+            self._body()
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._body()
+        self.graph = g
+        self.policy_events, self.env_events = events
+        return g
 
     def gather(self, group=None):
         """All-gather the per-rank trajectories over RCCL as one flat fp32 payload per rank

@@ -204,3 +204,42 @@ def test_rollout_engine_invariants():
     eng.roll()
     eng.collect()
     assert int(env.errors().max()) == 0
+
+
+def test_rollout_graph_replay_matches_eager():
+    """The captured hipGraph iteration reproduces eager launches bit for bit (same device state,
+    same sampling counters), across several replays and a weight change in between."""
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.rollout import RolloutEngine
+    from uavhip.vec_env import VecUAVEnv
+    outs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        env = VecUAVEnv(256, 8, 16, 1, 1, seed=3, full_reset_period=2)
+        pol = TransformerActorCritic().cuda()
+        eng = RolloutEngine(env, pol, 16, seed=4)
+        eng.start()
+        if graph:
+            eng.capture()
+            eng.counter.zero_()
+            # capture ran the body once on a side stream: rewind the device state
+            env2 = VecUAVEnv(256, 8, 16, 1, 1, seed=3, full_reset_period=2)
+            env2.istate[:, 4] = 1
+            env2.generate_scenes()
+            for name in ("nh_final", "nh_pure", "t_cost", "n_lock", "assigned", "istate", "dstate", "window"):
+                getattr(env, name).copy_(getattr(env2, name))
+            for k in env._scene:
+                env._scene[k].copy_(env2._scene[k])
+            env.reset(episode=1, obs_out=eng.traj.obs[eng.T])
+        res = []
+        for it in range(4):
+            if it == 2:
+                with torch.no_grad():
+                    pol.actor_head[2].bias.add_(0.5)   # weights change between iterations
+            tr = eng.collect()
+            torch.cuda.synchronize()
+            res.append([x.clone() for x in (tr.actions, tr.rewards, tr.dones, tr.obs, tr.adv, tr.values)])
+        outs.append(res)
+    for a, b in zip(*outs):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
