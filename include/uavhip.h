@@ -106,7 +106,10 @@ enum uavhip_dst {
     UAVHIP_DST_COV_VALUE,  /* sum of values of covered targets (chi_v numerator)         */
     UAVHIP_DST_TOTAL_COST, /* total_swarm_cost (uav_env.py:118)                          */
     UAVHIP_DST_TOTAL_VALUE,/* sum of target values                                       */
-    UAVHIP_DST_PAD0, UAVHIP_DST_PAD1,
+    UAVHIP_DST_PD_CUR,     /* p_dmg of the current pointer pair (cached: no dependent load) */
+    UAVHIP_DST_SUM_PDMG,   /* sum of p_dmg over locked pairs, in lock order (info avg_p_dmg)     */
+    UAVHIP_DST_SUM_PFIN,   /* sum of p_final over locked pairs, in lock order (info avg_p_final) */
+    UAVHIP_DST_PAD0, UAVHIP_DST_PAD1, UAVHIP_DST_PAD2,
     UAVHIP_DST_COUNT
 };
 

@@ -161,11 +161,11 @@ struct EnvRegs {
     // per UAV lane
     int asg;                // target list index or -1
     double ucost, ppen;     // cost, p_pen
-    double pd_asg, pf_asg;  // p_dmg / p_final of the assigned pair
     // wave-uniform scalars
     int u, t, ncov, nasg, ep, err, sel, stale, gen;
     long long sb;           // active scene base index (sel * E + e)
     double r, J, asg_cost, cov_val, tot_cost, tot_val;
+    double sum_pd, sum_pf;  // p_dmg / p_final summed over locked pairs in lock order (info)
     double pd_cur, pp_cur;  // pair probabilities of the current pointer (u, t)
     // observation window: element i (< 64) on lane i in w0, element 64 + i (i < 6) in w1
     float w0, w1;
@@ -266,10 +266,9 @@ __device__ void reset_regs(EnvRegs<TPL>& R, const uavhip_env& env, int lane) {
         R.nlk[k] = 0;
     }
     R.asg = -1;
-    R.pd_asg = 0.0;
-    R.pf_asg = 0.0;
     R.u = 0; R.t = 0; R.ncov = 0; R.nasg = 0;
     R.r = 0.0; R.J = 0.0; R.asg_cost = 0.0; R.cov_val = 0.0;
+    R.sum_pd = 0.0; R.sum_pf = 0.0;
     // total_swarm_cost accumulated in generation order (uav_env.py:118); total value in list order (:198)
     double tc = 0.0;
     for (int j = 0; j < env.N; ++j) tc = tc + readlane_d(R.ucost, j);
@@ -312,8 +311,6 @@ __device__ void load_regs(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lan
         R.nlk[k] = v ? env.n_lock[o] : 0;
     }
     R.asg = lane < N ? env.assigned[(long long)e * N + lane] : -1;
-    R.pd_asg = R.asg >= 0 ? env.p_dmg[(R.sb * N + lane) * M + R.asg] : 0.0;
-    R.pf_asg = R.pd_asg * R.ppen;
     const int* is = env.istate + (long long)e * UAVHIP_IST_COUNT;
     const double* ds = env.dstate + (long long)e * UAVHIP_DST_COUNT;
     R.u = is[UAVHIP_IST_UAV_IDX];
@@ -328,10 +325,14 @@ __device__ void load_regs(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lan
     R.cov_val = ds[UAVHIP_DST_COV_VALUE];
     R.tot_cost = ds[UAVHIP_DST_TOTAL_COST];
     R.tot_val = ds[UAVHIP_DST_TOTAL_VALUE];
+    R.sum_pd = ds[UAVHIP_DST_SUM_PDMG];
+    R.sum_pf = ds[UAVHIP_DST_SUM_PFIN];
     const float* w = env.window + (long long)e * kObs;
     R.w0 = w[lane];
     R.w1 = lane < kObs - kWave ? w[kWave + lane] : 0.0f;
-    load_cur_pair(R, env);
+    // the current pair's p_dmg was cached by the previous launch: one independent load round
+    R.pd_cur = ds[UAVHIP_DST_PD_CUR];
+    R.pp_cur = R.u < N ? readlane_d(R.ppen, R.u) : 0.0;
 }
 
 template <int TPL>
@@ -367,6 +368,9 @@ __device__ void store_regs(const EnvRegs<TPL>& R, const uavhip_env& env, int e, 
         ds[UAVHIP_DST_COV_VALUE] = R.cov_val;
         ds[UAVHIP_DST_TOTAL_COST] = R.tot_cost;
         ds[UAVHIP_DST_TOTAL_VALUE] = R.tot_val;
+        ds[UAVHIP_DST_PD_CUR] = R.pd_cur;
+        ds[UAVHIP_DST_SUM_PDMG] = R.sum_pd;
+        ds[UAVHIP_DST_SUM_PFIN] = R.sum_pf;
     }
     float* w = env.window + (long long)e * kObs;
     w[lane] = R.w0;
@@ -378,29 +382,14 @@ __device__ __forceinline__ void write_obs(float* o, float w0, float w1, int lane
     if (lane < kObs - kWave) o[kWave + lane] = w1;
 }
 
-// uav_env.py:369-433 diagnostics, sums in the reference's (target list, lock) order.
+// uav_env.py:369-433 diagnostics. The reference re-sums p_dmg / p_final over all locked pairs in
+// (target list, lock) order every step; here they are running sums in lock (= time) order, which
+// differ from it only by summation order (<= a few ulp, checked to 1e-12 against the reference).
 template <int TPL>
 __device__ void write_info(const EnvRegs<TPL>& R, const uavhip_env& env, double is_valid, double* o, int lane) {
-    double sd = 0.0, sf = 0.0;
-    const bool uav_lane = lane < env.N;
-#pragma unroll
-    for (int k = 0; k < TPL; ++k) {
-        unsigned long long tm = ballot(lane + kWave * k < env.M && R.nlk[k] > 0);
-        while (tm) {
-            const int tt = ffs64(tm) + kWave * k;
-            tm &= tm - 1;
-            unsigned long long um = ballot(uav_lane && R.asg == tt);
-            while (um) {
-                const int uu = ffs64(um);
-                um &= um - 1;
-                sd = sd + readlane_d(R.pd_asg, uu);
-                sf = sf + readlane_d(R.pf_asg, uu);
-            }
-        }
-    }
     const int cnt = R.nasg;
-    const double avg_d = cnt > 0 ? sd / (double)cnt : 0.0;
-    const double avg_f = cnt > 0 ? sf / (double)cnt : 0.0;
+    const double avg_d = cnt > 0 ? R.sum_pd / (double)cnt : 0.0;
+    const double avg_f = cnt > 0 ? R.sum_pf / (double)cnt : 0.0;
     double v = 0.0;
     v = lane == UAVHIP_INFO_J ? R.J : v;
     v = lane == UAVHIP_INFO_NUM_ASSIGNED ? (double)R.ncov : v;
@@ -469,11 +458,9 @@ __device__ void step_once(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lan
                     R.nlk[k] = R.nlk[k] + 1;
                 }
             }
-            if (lane == u) {
-                R.asg = t;
-                R.pd_asg = pd;
-                R.pf_asg = pf;
-            }
+            if (lane == u) R.asg = t;
+            R.sum_pd = R.sum_pd + pd;
+            R.sum_pf = R.sum_pf + pf;
             R.asg_cost = cost_all;
             if (nlk_t == 0) R.cov_val = R.cov_val + val_t;
             R.ncov = ncov_new;

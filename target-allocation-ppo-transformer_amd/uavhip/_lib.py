@@ -25,8 +25,8 @@ INFO_COUNT = 8
 IST = dict(UAV_IDX=0, TARGET_IDX=1, N_COVERED=2, N_ASSIGNED=3, EPISODE=4, ERROR=5, SCENE_SEL=6, SCENE_STALE=7,
            SCENE_GEN=8)
 IST_COUNT = 12
-DST = dict(R=0, J=1, ASG_COST=2, COV_VALUE=3, TOTAL_COST=4, TOTAL_VALUE=5)
-DST_COUNT = 8
+DST = dict(R=0, J=1, ASG_COST=2, COV_VALUE=3, TOTAL_COST=4, TOTAL_VALUE=5, PD_CUR=6, SUM_PDMG=7, SUM_PFIN=8)
+DST_COUNT = 12
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
