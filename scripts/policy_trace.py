@@ -1,0 +1,56 @@
+"""Phase timeline of k_policy_forward from a TRACE=1 build (make -C .../csrc TRACE=1).
+
+Runs the fused forward at B windows, reads the s_memtime stamps of waves 0 and 4 of the first
+256 workgroups and prints the median cycles spent between consecutive phase boundaries.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "target-allocation-ppo-transformer_amd"))
+import torch  # noqa: E402
+from uavhip import _lib  # noqa: E402
+from uavhip.policy import TransformerActorCritic  # noqa: E402
+
+NAMES = {0: "start", 1: "x+mask", 2: "a.embed", 3: "a.layer+sync", 4: "a.head", 5: "c.layers+sync", 6: "c.head",
+         7: "sample"}
+LAYER = ["start", "c0 gemm", "c0 sync", "c0 attn+sync", "c1 gemm", "c1 sync", "c1 attn+sync", "outproj", "sync",
+         "LN1+sync", "FFN1", "sync", "FFN2+sync", "store+sync", "LN2"]
+for li, tag in enumerate(["A", "C0", "C1"]):
+    for j, n in enumerate(LAYER):
+        NAMES[8 + 16 * li + j] = f"{tag}.{n}"
+
+B = int(os.environ.get("B", "4096"))
+torch.manual_seed(0)
+net = TransformerActorCritic().cuda()
+x = torch.randn(B, 5, 14, device="cuda")
+x[: B // 4, :2] = 0
+a = torch.empty(B, dtype=torch.int8, device="cuda")
+lp = torch.empty(B, device="cuda")
+v = torch.empty(B, device="cuda")
+fn = _lib.LIB.uavhip_policy_trace
+fn.restype = ctypes.c_int
+fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+for _ in range(5):
+    net.fused_forward(x, action_out=a, logp=lp, value=v)
+torch.cuda.synchronize()
+buf = np.zeros(256 * 2 * 64, np.uint64)
+assert fn(buf.ctypes.data, buf.size) == 0
+t = buf.reshape(256, 2, 64).astype(np.int64)
+slots = sorted(k for k in NAMES if (t[:, 0, k] != 0).all())
+base = t[:, :, 0:1]
+rel = t - base
+print(f"B={B}; median cycles since block start (wave0 / wave4) and per-phase delta (wave0)")
+prev = 0
+for k in slots:
+    m0 = int(np.median(rel[:, 0, k]))
+    m4 = int(np.median(rel[:, 1, k])) if (t[:, 1, k] != 0).all() else -1
+    print(f"{k:3d} {NAMES[k]:18s} {m0:8d} {m4:8d}  +{m0 - prev:6d}")
+    prev = m0
+start = t[:, 0, 0]
+end = t[:, 0, 7]
+print(f"block start spread {int(start.max() - start.min())} cycles; end spread {int(end.max() - end.min())};"
+      f" kernel span {int(end.max() - start.min())} cycles")

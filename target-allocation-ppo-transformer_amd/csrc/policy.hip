@@ -60,6 +60,15 @@ constexpr Offs make_offs() {
     return r;
 }
 constexpr Offs kOffs = make_offs();
+// In-features K of the parameters stored in MFMA fragment order ([out][in] weights the kernel
+// streams as the A operand: in_proj, out_proj, linear1, linear2 of every layer, head.0); 0 = plain.
+// Fragment order of an [R][K] matrix: index ((r/16 * K/16 + k/16) * 64 + (r%16 + 16 * (k%16)/4)) * 4 + k%4.
+constexpr int kTileK[kNumParams] = {
+    0, 0, 0, D, 0, D, 0, D, 0, FF, 0, 0, 0, 0, 0,
+    D, 0, 0, 0,
+    0, 0, 0, D, 0, D, 0, D, 0, FF, 0, 0, 0, 0, 0,
+    D, 0, D, 0, D, 0, FF, 0, 0, 0, 0, 0,
+    D, 0, 0, 0};
 constexpr int kActorTrunk = 0, kActorHead = 15, kCriticTrunk = 19, kCriticHead = 46;
 enum { POS = 0, EMB_W = 1, EMB_B = 2 };
 enum { INW = 0, INB, OUTW, OUTB, L1W, L1B, L2W, L2B, N1W, N1B, N2W, N2B };
@@ -67,12 +76,29 @@ __host__ __device__ constexpr int layer_param(int trunk, int l, int which) { ret
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Phase tracing (make TRACE=1 only): waves 0 and 4 of the first 256 workgroups stamp s_memtime at
+// the phase boundaries below; uavhip_policy_trace copies the stamps out. Off in the product build.
+#ifdef UAVHIP_POLICY_TRACE
+constexpr int kTraceSlots = 64;
+__device__ unsigned long long g_ptrace[256 * 2 * kTraceSlots];
+#define PTR(id)                                                                                  \
+    do {                                                                                         \
+        if ((threadIdx.x & 255) == 0 && blockIdx.x < 256)                                        \
+            g_ptrace[(blockIdx.x * 2 + (threadIdx.x >> 8)) * kTraceSlots + (id)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define PTR(id) do {} while (0)
+#endif
+
 struct Smem {
     float x[TOK * LDX];         // input windows [tok = s*16 + p][k], k < 14 valid
     float h[TOK * LDH];         // residual stream [tok][128]
     float big[TOK * LDB];       // QKV chunk / out-proj result / FFN hidden chunk
     float ctx[TOK * LDH];       // attention output / FFN output
-    float z[SPW * LDZ];         // head hidden
+    union {
+        float z[SPW * LDZ];     // head hidden
+        float2 red[NW * TOK];   // LayerNorm partials (mean, M2) per wave and token
+    };
     float logits[SPW * 2];
     float value[SPW];
     int mask[SPW * S];          // key padding mask (transformer_net.py:52-54)
@@ -88,13 +114,19 @@ template <int D>
 struct APre {
     f32x4 a[D];
 };
+// GEMM weights are stored in MFMA fragment order (see kTileK): the A operand of 16-row tile
+// `row / 16`, k-block kb is 1 KiB contiguous, lane l's float4 at 4 l. One wave instruction then
+// reads 1 KiB of consecutive lines instead of 16 half-lines of 16 rows (3.3x the per-CU L2 rate
+// measured on MI355X: scripts/micro/l2bw.hip).
+__device__ __forceinline__ const float* frag_ptr(const float* W, int ldw, int row, int kw0) {
+    return W + ((size_t)(row >> 4) * (ldw >> 4) + (kw0 >> 4)) * 256 + 4 * lane_id();
+}
 template <int D>
 __device__ __forceinline__ APre<D> prefetch(const float* __restrict__ W, int ldw, int row, int kw0) {
-    const int l = lane_id(), i16 = l & 15, g = l >> 4;
-    const float* wp = W + (size_t)(row + i16) * ldw + kw0 + 4 * g;
+    const float* wp = frag_ptr(W, ldw, row, kw0);
     APre<D> r;
 #pragma unroll
-    for (int p = 0; p < D; ++p) r.a[p] = *reinterpret_cast<const f32x4*>(wp + 16 * p);
+    for (int p = 0; p < D; ++p) r.a[p] = *reinterpret_cast<const f32x4*>(wp + 256 * p);
     return r;
 }
 
@@ -106,7 +138,7 @@ template <int CT, int D>
 __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[CT], const APre<D>& pre, const float* __restrict__ W, int ldw,
                                           int row, int kw0, const float* X, int ldx, int xtok0) {
     const int l = lane_id(), i16 = l & 15, g = l >> 4;
-    const float* wp = W + (size_t)(row + i16) * ldw + kw0 + 4 * g;
+    const float* wp = frag_ptr(W, ldw, row, kw0);
     const float* xp[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) xp[ct] = X + (xtok0 + 16 * ct + i16) * ldx + 4 * g;
@@ -120,7 +152,7 @@ __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[CT], const APre<D>& pre, 
 #pragma unroll
     for (int i = 0; i < KB; ++i) {
         if (i + D < KB) {
-            a[i + D] = *reinterpret_cast<const f32x4*>(wp + 16 * (i + D));
+            a[i + D] = *reinterpret_cast<const f32x4*>(wp + 256 * (i + D));
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) b[i + D][ct] = *reinterpret_cast<const f32x4*>(xp[ct] + 16 * (i + D));
         }
@@ -169,43 +201,114 @@ __device__ __forceinline__ void linear1(const APre<D>& pre, const float* W, int 
 }
 
 // ------------------------------------------------------------------ VALU pieces
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+// Cross-lane sums without the LDS crossbar (__shfl_xor lowers to ds_bpermute on gfx950):
+// DPP quad permutes inside a quad, v_permlane16/32_swap across rows / halves. Both lanes of a
+// pair compute the same a + b, so the results are bitwise equal across the group.
+__device__ __forceinline__ float add_xor1(float v) {
+    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));  // [1,0,3,2]
+}
+__device__ __forceinline__ float add_xor2(float v) {
+    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));  // [2,3,0,1]
+}
+__device__ __forceinline__ float add_xor16(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float add_xor32(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// h[tok] = LN(h[tok] + a[tok]) * w + b for tok in [tok0, tok0 + ntok) (post-LN, eps 1e-5).
-// 8 consecutive lanes per token (16 features each, 4 float4), sums reduced with 3 xor-shuffles
-// inside the octet: a wave normalises 8 tokens at once.
-__device__ void add_layernorm(float* h, const float* a, int lda, int tok0, int ntok, const float* __restrict__ w,
-                              const float* __restrict__ b) {
-    const int o8 = threadIdx.x & 7;
-    const int f0 = 16 * o8;
-    for (int t = tok0 + (threadIdx.x >> 3); t < tok0 + ntok; t += NTHR / 8) {
-        f32x4 v[4];
-        float s = 0.f;
+// Fused GEMM epilogue + post-LN (nn.TransformerEncoderLayer norm1 / norm2, eps 1e-5):
+//   h[tok][f] = LN(h[tok] + acc + bias)[f] * w[f] + b[f]
+// for this wave's 16 output features f = [16 wv, 16 wv + 16) of CT column tiles from ytok0. The
+// token statistics combine per-wave (mean, M2) pairs over 16 features each (Chan et al.), so one
+// barrier suffices and the variance is two-pass accurate. Ends WITHOUT a barrier after writing h.
+template <int CT>
+__device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[CT], const float* __restrict__ bias,
+                                                   const float* __restrict__ w, const float* __restrict__ b, int ytok0) {
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
+    const int f0 = 16 * wv + 4 * g;
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + f0);
+    f32x4 v[CT];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            v[i] = *reinterpret_cast<const f32x4*>(h + t * LDH + f0 + 4 * i) +
-                   *reinterpret_cast<const f32x4*>(a + t * lda + f0 + 4 * i);
-            s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    for (int ct = 0; ct < CT; ++ct) {
+        const int tok = ytok0 + 16 * ct + i16;
+        v[ct] = acc[ct] + bb + *reinterpret_cast<const f32x4*>(sm.h + tok * LDH + f0);
+        float s = (v[ct].x + v[ct].y) + (v[ct].z + v[ct].w);
+        s = add_xor32(add_xor16(s));
+        const float m = s * (1.0f / 16);
+        const f32x4 d = v[ct] - m;
+        float q = (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+        q = add_xor32(add_xor16(q));
+        if (g == 0) sm.red[wv * TOK + tok] = make_float2(m, q);
+    }
+    __syncthreads();
+    const f32x4 ww = *reinterpret_cast<const f32x4*>(w + f0);
+    const f32x4 lb = *reinterpret_cast<const f32x4*>(b + f0);
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+        const int tok = ytok0 + 16 * ct + i16;
+        float2 pr[NW];
+        float ms = 0.f;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            pr[k] = sm.red[k * TOK + tok];
+            ms += pr[k].x;
         }
-        s += __shfl_xor(s, 1); s += __shfl_xor(s, 2); s += __shfl_xor(s, 4);
-        const float mean = s * (1.0f / D);
-        float q = 0.f;
+        const float mean = ms * (1.0f / NW);
+        float m2 = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            v[i] -= mean;
-            q += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
+        for (int k = 0; k < NW; ++k) {
+            const float dm = pr[k].x - mean;
+            m2 += pr[k].y + 16.0f * dm * dm;
         }
-        q += __shfl_xor(q, 1); q += __shfl_xor(q, 2); q += __shfl_xor(q, 4);
-        const float rs = 1.0f / sqrtf(q * (1.0f / D) + 1e-5f);
+        const float rs = 1.0f / sqrtf(m2 * (1.0f / D) + 1e-5f);
+        *reinterpret_cast<f32x4*>(sm.h + tok * LDH + f0) = (v[ct] - mean) * rs * ww + lb;
+    }
+}
+
+// Full-layer attention for heads [4c, 4c+4): one (sample, head, query group) task per 4 lanes,
+// each lane owning 4 of the 16 head dims; the task loads the 5 keys / values once for all its
+// queries (group 0: positions 0-2 on waves 0-3, group 1: positions 3-4 on waves 4-7).
+__device__ void attention_full(Smem& sm, int c) {
+    const int q4 = threadIdx.x & 3, task = threadIdx.x >> 2;
+    const int hh = task & 3, p = (task >> 2) & 15, grp = task >> 6;
+    const int d0 = hh * HD + 4 * q4;
+    f32x4 k[S], v[S];
+    bool msk[S];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const f32x4 ww = *reinterpret_cast<const f32x4*>(w + f0 + 4 * i);
-            const f32x4 bb = *reinterpret_cast<const f32x4*>(b + f0 + 4 * i);
-            *reinterpret_cast<f32x4*>(h + t * LDH + f0 + 4 * i) = v[i] * rs * ww + bb;
+    for (int j = 0; j < S; ++j) {
+        k[j] = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 64 + d0);
+        v[j] = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 128 + d0);
+        msk[j] = sm.mask[p * S + j] != 0;
+    }
+    const int qs0 = grp ? 3 : 0, nq = grp ? 2 : 3;
+#pragma unroll
+    for (int qi = 0; qi < 3; ++qi) {
+        if (qi < nq) {
+            const int ti = (qs0 + qi) * SPW + p;
+            const f32x4 q = *reinterpret_cast<const f32x4*>(sm.big + ti * LDB + d0);
+            float sc[S];
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                float part = q.x * k[j].x + q.y * k[j].y + q.z * k[j].z + q.w * k[j].w;
+                part = add_xor2(add_xor1(part));
+                sc[j] = msk[j] ? -INFINITY : part * 0.25f;  // 1/sqrt(16)
+                mx = fmaxf(mx, sc[j]);
+            }
+            float den = 0.f;
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                sc[j] = __expf(sc[j] - mx);
+                den += sc[j];
+            }
+            const float inv = 1.0f / den;
+            f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < S; ++j) o += (sc[j] * inv) * v[j];
+            *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o;
         }
     }
 }
@@ -228,8 +331,7 @@ __device__ void attention_chunk(Smem& sm, int c, int qs0, int nqs) {
         for (int j = 0; j < S; ++j) {
             const f32x4 k = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 64 + d0);
             float part = q.x * k.x + q.y * k.y + q.z * k.z + q.w * k.w;
-            part += __shfl_xor(part, 1);
-            part += __shfl_xor(part, 2);
+            part = add_xor2(add_xor1(part));
             sc[j] = sm.mask[p * S + j] ? -INFINITY : part * 0.25f;  // 1/sqrt(16)
             mx = fmaxf(mx, sc[j]);
         }
@@ -292,6 +394,8 @@ __device__ __forceinline__ int kv_row(int wv, int c) { return (1 + (wv >> 2)) * 
 // K/V weight blocks. Ends WITHOUT a final barrier: the caller prefetches its next weights, then syncs.
 template <int trunk, int layer, bool last>
 __device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv) {
+    [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
+    PTR(tb);
     const float* Win = P + kOffs.o[layer_param(trunk, layer, INW)];
     const float* bin = P + kOffs.o[layer_param(trunk, layer, INB)];
     const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
@@ -304,7 +408,6 @@ __device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv
     constexpr int CTQ = last ? 1 : S;              // column tiles that need Q / out / LN / FFN
     constexpr int DQ = depth<CTQ>();
     constexpr int qtok0 = last ? (S - 1) * SPW : 0;
-    constexpr int nqs = last ? 1 : S;
 
     APre<DQ> po;
 #pragma unroll
@@ -317,33 +420,45 @@ __device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv
         if (wv < 4) linear1<CTQ, false, DQ>(pq, Win, D, bin, 64 * c + 16 * wv, sm.h, LDH, qtok0, sm.big, LDB, 16 * wv, qtok0);
         if (c == 0) pkv = prefetch<2>(Win, D, kv_row(wv, 1), 0);
         else po = prefetch<DQ>(Wo, D, 16 * wv, 0);
+        PTR(tb + 1 + 3 * c);
         __syncthreads();
-        attention_chunk(sm, c, last ? S - 1 : 0, nqs);
+        PTR(tb + 2 + 3 * c);
+        if (last) attention_chunk(sm, c, S - 1, 1);
+        else attention_full(sm, c);
         __syncthreads();
+        PTR(tb + 3 + 3 * c);
     }
-    // out projection -> big, then h = LN1(h + attn)
-    linear1<CTQ, false, DQ>(po, Wo, D, bo, 16 * wv, sm.ctx, LDH, qtok0, sm.big, LDB, 16 * wv, qtok0);
-    const APre<DQ> pf1a = prefetch<DQ>(W1, D, 16 * wv, 0);
-    const APre<DQ> pf1b = prefetch<DQ>(W1, D, 128 + 16 * wv, 0);
+    // out projection, h = LN1(h + attn) in its epilogue
+    APre<DQ> pf1a, pf1b;
+    {
+        f32x4 acc[CTQ];
+        zero(acc);
+        gemm_tile<CTQ, DQ>(acc, po, Wo, D, 16 * wv, 0, sm.ctx, LDH, qtok0);
+        PTR(tb + 7);
+        pf1a = prefetch<DQ>(W1, D, 16 * wv, 0);
+        pf1b = prefetch<DQ>(W1, D, 128 + 16 * wv, 0);
+        residual_layernorm<CTQ>(sm, acc, bo, P + kOffs.o[layer_param(trunk, layer, N1W)],
+                                P + kOffs.o[layer_param(trunk, layer, N1B)], qtok0);
+    }
+    PTR(tb + 8);
     __syncthreads();
-    add_layernorm(sm.h, sm.big, LDB, qtok0, nqs * SPW, P + kOffs.o[layer_param(trunk, layer, N1W)],
-                  P + kOffs.o[layer_param(trunk, layer, N1B)]);
-    __syncthreads();
+    PTR(tb + 9);
     // FFN: hidden features 0-127 -> big, 128-255 -> ctx (both free now), then one K=256 GEMM
     linear1<CTQ, true, DQ>(pf1a, W1, D, b1, 16 * wv, sm.h, LDH, qtok0, sm.big, LDF, 16 * wv, qtok0);
     linear1<CTQ, true, DQ>(pf1b, W1, D, b1, 128 + 16 * wv, sm.h, LDH, qtok0, sm.ctx, LDF, 16 * wv, qtok0);
     const APre<DQ> pf2a = prefetch<DQ>(W2, FF, 16 * wv, 0);
+    PTR(tb + 10);
     __syncthreads();
+    PTR(tb + 11);
     f32x4 acc2[CTQ];
     zero(acc2);
     const APre<DQ> pf2b = prefetch<DQ>(W2, FF, 16 * wv, 128);
     gemm_tile<CTQ, DQ>(acc2, pf2a, W2, FF, 16 * wv, 0, sm.big, LDF, qtok0);
     gemm_tile<CTQ, DQ>(acc2, pf2b, W2, FF, 16 * wv, 128, sm.ctx, LDF, qtok0);
-    __syncthreads();
-    store_tile<CTQ, false>(acc2, b2, 16 * wv, sm.big, LDF, 16 * wv, qtok0);
-    __syncthreads();
-    add_layernorm(sm.h, sm.big, LDF, qtok0, nqs * SPW, P + kOffs.o[layer_param(trunk, layer, N2W)],
-                  P + kOffs.o[layer_param(trunk, layer, N2B)]);
+    PTR(tb + 12);
+    residual_layernorm<CTQ>(sm, acc2, b2, P + kOffs.o[layer_param(trunk, layer, N2W)],
+                            P + kOffs.o[layer_param(trunk, layer, N2B)], qtok0);
+    PTR(tb + 14);
 }
 
 // 128 -> 64 (MFMA, waves 0-3) -> relu -> nout (VALU) on the last-position rows (transformer_net.py:77-91)
@@ -374,6 +489,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
                                                          float* __restrict__ ent_out, float* __restrict__ logits_out) {
     __shared__ __attribute__((aligned(16))) Smem sm;
     const int b0 = blockIdx.x * SPW;
+    PTR(0);
     // windows -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch tail zero-filled)
     for (int i = threadIdx.x; i < TOK * LDX; i += NTHR) {
         const int t = i / LDX, k = i - t * LDX, s = t / SPW, p = t - s * SPW;
@@ -386,18 +502,22 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         for (int k = 0; k < IN; ++k) z = z && (sm.x[(s * SPW + p) * LDX + k] == 0.f);
         sm.mask[p * S + s] = (s < S - 1) && z;
     }
+    PTR(1);
     const int wv = threadIdx.x >> 6;
     const float* headw_a = P + kOffs.o[kActorHead];
     const float* headw_c = P + kOffs.o[kCriticHead];
     // actor trunk (1 layer) + head
     embed<kActorTrunk>(sm, P);
+    PTR(2);
     APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
     __syncthreads();
     encoder_layer<kActorTrunk, 0, true>(sm, P, pkv);
     APre<4> ph;
     if (wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
     __syncthreads();
+    PTR(3);
     head_mlp<kActorHead, 2>(sm, P, ph, sm.logits);
+    PTR(4);
     // critic trunk (2 layers) + head
     embed<kCriticTrunk>(sm, P);
     pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
@@ -408,7 +528,9 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     encoder_layer<kCriticTrunk, 1, true>(sm, P, pkv);
     if (wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
     __syncthreads();
+    PTR(5);
     head_mlp<kCriticHead, 1>(sm, P, ph, sm.value);
+    PTR(6);
     // Categorical(softmax(logits)): sample / log_prob / entropy (transformer_net.py:118-122)
     if (threadIdx.x < SPW) {
         const int p = threadIdx.x, b = b0 + p;
@@ -434,6 +556,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
             if (logits_out) { logits_out[2 * b] = l0; logits_out[2 * b + 1] = l1; }
         }
     }
+    PTR(7);
 }
 
 }  // namespace pol
@@ -446,6 +569,20 @@ extern "C" int32_t uavhip_policy_layout(int32_t* offsets, int32_t max_offsets) {
         for (int i = 0; i < pol::kNumParams && i < max_offsets; ++i) offsets[i] = pol::kOffs.o[i];
     return pol::kOffs.o[pol::kNumParams];
 }
+
+extern "C" int32_t uavhip_policy_tiling(int32_t* kcols, int32_t max_params) {
+    if (kcols)
+        for (int i = 0; i < pol::kNumParams && i < max_params; ++i) kcols[i] = pol::kTileK[i];
+    return pol::kNumParams;
+}
+
+#ifdef UAVHIP_POLICY_TRACE
+extern "C" int uavhip_policy_trace(unsigned long long* out, int n) {
+    const int total = 256 * 2 * pol::kTraceSlots;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pol::g_ptrace), sizeof(unsigned long long) * (n < total ? n : total), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int uavhip_policy_forward(const uavhip_policy* policy, const float* states, int32_t B,
                                      const int8_t* actions_in, uint64_t seed, uint64_t offset,

@@ -77,10 +77,11 @@ class TransformerActorCritic(nn.Module):
         value = self.critic_head(self.critic_net(state)[:, -1, :])
         return logits, value
 
-    def evaluate(self, state, action):
-        """transformer_net.py:124-144 -> (log_prob(action), value [B, 1], entropy)."""
+    def evaluate(self, state, action, validate=True):
+        """transformer_net.py:124-144 -> (log_prob(action), value [B, 1], entropy).
+        validate=False skips Categorical's argument check (a host sync; graph capture)."""
         logits, value = self.heads(state)
-        dist = Categorical(torch.softmax(logits, dim=-1))
+        dist = Categorical(torch.softmax(logits, dim=-1), validate_args=None if validate else False)
         return dist.log_prob(action), value, dist.entropy()
 
     # ------------------------------------------------------------------ fused HIP path
@@ -152,17 +153,43 @@ def layout():
     return [offs[i] for i in range(50)], int(n)
 
 
+def tiling():
+    """In-features K of each parameter stored in MFMA fragment order (0 = flat), key order."""
+    kc = (ctypes.c_int32 * 64)()
+    np_ = LIB.uavhip_policy_tiling(kc, 64)
+    return [kc[i] for i in range(np_)]
+
+
+def to_fragment_order(w, K):
+    """[R][K] -> MFMA fragment order (include/uavhip.h uavhip_policy_tiling): blocks of 16 rows x
+    16 k, inside a block lane = r%16 + 16 * ((k%16)//4) holds k%4 = 0..3."""
+    R = w.shape[0]
+    return w.reshape(R // 16, 16, K // 16, 4, 4).permute(0, 2, 3, 1, 4).reshape(-1)
+
+
+def from_fragment_order(flat, R, K):
+    return flat.reshape(R // 16, K // 16, 4, 16, 4).permute(0, 3, 1, 2, 4).reshape(R, K)
+
+
 def pack_weights(state_dict, device=None):
-    """Flatten the 50-key state_dict into the kernel's packed buffer (state_dict key order)."""
+    """Lay the 50-key state_dict out as the kernel's packed buffer (state_dict key order; GEMM
+    weights in MFMA fragment order)."""
     offs, n = layout()
+    kcols = tiling()
     items = list(state_dict.items())
-    if len(items) != len(offs):
+    if len(items) != len(offs) or len(kcols) != len(offs):
         raise ValueError(f"expected {len(offs)} state_dict entries, got {len(items)}")
     dev = device if device is not None else items[0][1].device
     buf = torch.zeros(n, dtype=torch.float32, device=dev)
     ends = offs[1:] + [n]
-    for (k, v), o, e in zip(items, offs, ends):
-        flat = v.detach().reshape(-1).to(device=dev, dtype=torch.float32)
+    for (k, v), o, e, K in zip(items, offs, ends, kcols):
+        v = v.detach().to(device=dev, dtype=torch.float32)
+        if K:
+            if v.dim() != 2 or v.shape[1] != K or v.shape[0] % 16:
+                raise ValueError(f"{k}: shape {tuple(v.shape)} is not [16 r][{K}]")
+            flat = to_fragment_order(v, K)
+        else:
+            flat = v.reshape(-1)
         if flat.numel() > e - o:
             raise ValueError(f"{k}: {flat.numel()} floats do not fit the packed slot {e - o}")
         buf[o:o + flat.numel()] = flat

@@ -95,14 +95,18 @@ def ppo_epochs(policy, optimizer, states, actions, old_logprobs, old_values, ret
     return sa, sc, se, cnt
 
 
-def make_optimizer(policy):
-    """Adam with the reference's four parameter groups (ppo.py:17-22)."""
-    return optim.Adam([
+def make_optimizer(policy, capturable=False):
+    """Adam with the reference's four parameter groups (ppo.py:17-22); capturable=True keeps the
+    step counters on device so the step can live in a captured graph (GraphPPOUpdater)."""
+    groups = [
         {"params": policy.actor_head.parameters(), "lr": cfg.LR_ACTOR},
         {"params": policy.actor_net.parameters(), "lr": cfg.LR_ACTOR},
         {"params": policy.critic_head.parameters(), "lr": cfg.LR_CRITIC},
         {"params": policy.critic_net.parameters(), "lr": cfg.LR_CRITIC},
-    ])
+    ]
+    if capturable:
+        return optim.Adam(groups, capturable=True, foreach=True)
+    return optim.Adam(groups)
 
 
 class PPOAgent:
@@ -154,3 +158,95 @@ class PPOAgent:
 
     def clear_buffer(self):
         self.buffer = {k: [] for k in self.buffer}
+
+
+class GraphPPOUpdater:
+    """The clipped-PPO minibatch step of ppo_epochs (ppo.py:96-169), captured once into a hipGraph
+    and replayed per minibatch: evaluate -> losses -> backward -> clip_grad_norm_ -> Adam, with the
+    minibatch gathered on device from the (fixed) trajectory buffers by a static index tensor.
+
+    Same ops and op order as ppo_epochs on the same minibatch order (torch.randperm of the CPU
+    generator, SubsetRandomSampler's draw), so a replay reproduces an eager step up to atomics in
+    the backward kernels. The optimizer must be Adam built with capturable=True (make_optimizer(
+    policy, capturable=True)). Buffers must keep their storage for the updater's lifetime."""
+
+    def __init__(self, policy, optimizer, states, actions, old_logprobs, old_values, returns, advantages,
+                 batch_size, eps_clip=None, grad_clip=None):
+        self.policy, self.opt = policy, optimizer
+        self.bufs = (states, actions, old_logprobs, old_values, returns, advantages)
+        self.n = states.shape[0]
+        self.bs = int(batch_size)
+        self.eps = cfg.EPS_CLIP if eps_clip is None else eps_clip
+        self.gclip = cfg.GRAD_NORM_CLIP if grad_clip is None else grad_clip
+        dev = states.device
+        self.idx = torch.zeros(self.bs, dtype=torch.long, device=dev)
+        self.acc = torch.zeros(3, dtype=torch.float64, device=dev)
+        self.graph = None
+
+    def _step(self):
+        states, actions, old_logprobs, old_values, returns, advantages = self.bufs
+        idx, eps = self.idx, self.eps
+        logp, v, ent = self.policy.evaluate(states[idx], actions[idx], validate=False)
+        v = torch.squeeze(v)
+        ratios = torch.exp(logp - old_logprobs[idx])
+        adv = advantages[idx]
+        surr1 = ratios * adv
+        surr2 = torch.clamp(ratios, 1 - eps, 1 + eps) * adv
+        loss_actor = -torch.min(surr1, surr2).mean()
+        bov = old_values[idx]
+        ret = returns[idx]
+        v_clip = bov + torch.clamp(v - bov, -eps, eps)
+        loss_critic = torch.max(torch.mean((v - ret) ** 2), torch.mean((v_clip - ret) ** 2))
+        ent_mean = ent.mean()
+        loss = loss_actor + 0.5 * loss_critic - 0.01 * ent_mean
+        self.opt.zero_grad(set_to_none=False)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.policy.parameters(), self.gclip)
+        self.acc += torch.stack([loss_actor.detach(), loss_critic.detach(), ent_mean.detach()]).double()
+        self.opt.step()
+
+    def capture(self, warmup=2):
+        """Warm up (allocates grads / optimizer state) on a side stream, then capture one step."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        snapshot = [p.detach().clone() for p in self.policy.parameters()]
+        opt_state = {k: {kk: (vv.clone() if torch.is_tensor(vv) else vv) for kk, vv in st.items()}
+                     for k, st in self.opt.state.items()}
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._step()
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._step()
+        # undo the warm-up / capture side effects on weights and optimizer state
+        with torch.no_grad():
+            for p, q in zip(self.policy.parameters(), snapshot):
+                p.copy_(q)
+            for p, st in self.opt.state.items():
+                old = opt_state.get(p)
+                for k, v in st.items():
+                    if torch.is_tensor(v):
+                        if old is not None and k in old:
+                            v.copy_(old[k])
+                        else:
+                            v.zero_()
+        self.acc.zero_()
+
+    def run(self, epochs=None, generator=None):
+        """K epochs over the buffers -> (mean actor loss, critic loss, entropy, n_steps)."""
+        epochs = cfg.K_EPOCHS if epochs is None else epochs
+        if self.graph is None:
+            self.capture()
+        self.acc.zero_()
+        cnt = 0
+        for _ in range(epochs):
+            perm = torch.randperm(self.n, generator=generator).to(self.idx.device, non_blocking=True)
+            for b in range(self.n // self.bs):
+                self.idx.copy_(perm[b * self.bs:(b + 1) * self.bs])
+                self.graph.replay()
+                cnt += 1
+        if cnt == 0:
+            return 0.0, 0.0, 0.0, 0
+        sa, sc, se = (self.acc / cnt).tolist()
+        return sa, sc, se, cnt

@@ -243,3 +243,29 @@ def test_rollout_graph_replay_matches_eager():
     for a, b in zip(*outs):
         for x, y in zip(a, b):
             assert torch.equal(x, y)
+
+
+def test_graph_ppo_update_matches_eager():
+    """GraphPPOUpdater replays == ppo_epochs eager steps (same minibatch order, same Adam)."""
+    import copy
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.ppo import GraphPPOUpdater, make_optimizer, ppo_epochs
+    torch.manual_seed(3)
+    base = TransformerActorCritic().cuda()
+    n, bs = 1024, 256
+    g = torch.Generator(device="cpu").manual_seed(11)
+    states = torch.randn(n, 5, 14, generator=g).cuda()
+    states[: n // 4, :2] = 0
+    acts = torch.randint(0, 2, (n,), generator=g).cuda()
+    logp = -torch.rand(n, generator=g).cuda()
+    vals, ret, adv = (torch.randn(n, generator=g).cuda() for _ in range(3))
+    pe, pg = copy.deepcopy(base), copy.deepcopy(base)
+    oe, og = make_optimizer(pe, capturable=True), make_optimizer(pg, capturable=True)
+    se = ppo_epochs(pe, oe, states, acts, logp, vals, ret, adv, epochs=2, batch_size=bs,
+                    generator=torch.Generator().manual_seed(7))
+    up = GraphPPOUpdater(pg, og, states, acts, logp, vals, ret, adv, bs)
+    sg = up.run(epochs=2, generator=torch.Generator().manual_seed(7))
+    assert se[3] == sg[3] == 2 * (n // bs)
+    np.testing.assert_allclose(sg[:3], se[:3], rtol=1e-5, atol=1e-6)
+    for (k, a), b in zip(pe.state_dict().items(), pg.state_dict().values()):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6, msg=k)

@@ -120,7 +120,7 @@ def test_policy_torch_path_matches_reference(policy_npz):
 
 
 def test_packed_layout_covers_state_dict():
-    from uavhip.policy import TransformerActorCritic, layout, pack_weights
+    from uavhip.policy import TransformerActorCritic, from_fragment_order, layout, pack_weights, tiling
     offs, n = layout()
     net = TransformerActorCritic()
     sd = net.state_dict()
@@ -129,8 +129,19 @@ def test_packed_layout_covers_state_dict():
     for (k, v), o, e in zip(sd.items(), offs, ends):
         assert o % 4 == 0 and e - o >= v.numel() and e - o - v.numel() < 4, k
     buf = pack_weights(sd)
-    for (k, v), o in zip(sd.items(), offs):
-        assert torch.equal(buf[o:o + v.numel()], v.reshape(-1)), k
+    kcols = tiling()
+    assert sum(1 for K in kcols if K) == 14  # in_proj, out_proj, linear1, linear2 x 3 layers + 2 head.0
+    for (k, v), o, K in zip(sd.items(), offs, kcols):
+        got = buf[o:o + v.numel()]
+        if K:
+            assert k.endswith("weight") and v.shape[1] == K, k
+            assert torch.equal(from_fragment_order(got, v.shape[0], K), v), k
+            # spot-check the documented index formula (include/uavhip.h)
+            r, c = v.shape[0] - 3, K - 6
+            idx = ((r // 16 * (K // 16) + c // 16) * 64 + r % 16 + 16 * ((c % 16) // 4)) * 4 + c % 4
+            assert got[idx] == v[r, c], k
+        else:
+            assert torch.equal(got, v.reshape(-1)), k
     assert n == sum((s + 3) // 4 * 4 for s in sizes)
 
 
