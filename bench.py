@@ -66,7 +66,8 @@ def parse():
     ap.add_argument("--horizon", type=int, default=64)
     ap.add_argument("--ppo-minibatch", type=int, default=4096)
     ap.add_argument("--no-ppo", action="store_true")
-    ap.add_argument("--ppo-eager", action="store_true", help="time the eager update instead of graph replays")
+    ap.add_argument("--ppo-impl", choices=["fused", "torch-graph", "torch-eager"], default="fused",
+                    help="PPO update implementation timed for ppo_samples_per_s")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--eager", action="store_true", help="launch kernels eagerly instead of replaying a hipGraph")
@@ -196,16 +197,23 @@ def main():
         states = tr.obs[:T].reshape(n, 5, 14)
         acts = tr.actions.reshape(n).long()
         bufs = (states, acts, tr.logp.reshape(n), tr.values.reshape(n), tr.ret.reshape(n), tr.adv.reshape(n))
-        if args.ppo_eager:
+        if args.ppo_impl == "torch-eager":
             opt = make_optimizer(policy)
             impl = "torch autograd on GPU, eager launches"
             run = lambda: ppo_epochs(policy, opt, *bufs, batch_size=args.ppo_minibatch)  # noqa: E731
-        else:
+        elif args.ppo_impl == "torch-graph":
             opt = make_optimizer(policy, capturable=True)
             upd = GraphPPOUpdater(policy, opt, *bufs, args.ppo_minibatch)
             upd.capture()  # once per buffer set (not timed): replays cover every later update
             impl = "torch autograd on GPU, minibatch step captured in a hipGraph"
             run = upd.run
+        else:
+            from uavhip.train import FusedPPOTrainer
+            trainer = FusedPPOTrainer(policy, args.ppo_minibatch)
+            trainer.set_buffers(*bufs)
+            trainer.capture()  # once per buffer set (not timed): replays cover every later update
+            impl = "HIP training step (uavhip_ppo_step: grouped fp32 MFMA GEMMs + fused kernels), hipGraph replay"
+            run = trainer.run
         torch.cuda.synchronize()
         p0 = time.perf_counter()
         _, _, _, cnt = run()

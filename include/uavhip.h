@@ -247,6 +247,40 @@ int uavhip_policy_forward(const uavhip_policy* policy, const float* states, int3
                           uint64_t seed, uint64_t offset, const uint64_t* offset_dev, int8_t* action_out,
                           float* logp, float* value, float* entropy, float* logits, uavhip_stream_t stream);
 
+/* ---------------------------------------------------------------- PPO update (K5) */
+
+/* One clipped-PPO minibatch step of agents/ppo.py:96-169 (evaluate -> surrogate / clipped value
+ * / entropy loss -> backward -> clip_grad_norm_(1.0) -> Adam with the four parameter groups of
+ * ppo.py:17-22), as hand-written kernels: grouped fp32 MFMA GEMMs for every linear layer
+ * (forward, input gradients, split-K weight gradients), fused residual+LayerNorm, attention,
+ * heads+loss, and a fused clip+Adam. Parameters, gradients and the Adam moments are FLAT
+ * buffers in the plain (not fragment-order) uavhip_policy_layout() layout; the torch module's
+ * parameters can be views of `params`. */
+typedef struct uavhip_ppo {
+    float* params;       /* [n_floats] */
+    float* grads;        /* [n_floats] (written; mode 1: raw gradients before clipping) */
+    float* adam_m;       /* [n_floats] exp_avg */
+    float* adam_v;       /* [n_floats] exp_avg_sq */
+    double* adam_step;   /* [1] device step counter (shared by all groups) */
+    float* workspace;    /* [uavhip_ppo_workspace_floats(minibatch)] */
+    double* stats;       /* [4] += loss_actor, loss_critic, entropy, 1 per step (nullable) */
+    int32_t n_floats;
+    int32_t minibatch;   /* samples per step, multiple of 64 */
+    float lr_actor, lr_critic, beta1, beta2, adam_eps; /* 2e-4, 1e-3, 0.9, 0.999, 1e-8 */
+    float eps_clip, max_grad_norm, value_coef, entropy_coef; /* 0.2, 1.0, 0.5, 0.01 */
+} uavhip_ppo;
+
+/* Floats of workspace one step needs at `minibatch` samples. */
+int64_t uavhip_ppo_workspace_floats(int32_t minibatch);
+
+/* Minibatch rows idx[minibatch] (int32, into the trajectory buffers) of states[n][5][14],
+ * actions[n] (int8), old_logp / old_values / returns / advantages [n] (f32).
+ * mode 0: full step (parameters and Adam moments updated); mode 1: forward + backward only
+ * (raw gradients in ppo->grads, loss stats accumulated). */
+int uavhip_ppo_step(const uavhip_ppo* ppo, const float* states, const int8_t* actions, const float* old_logp,
+                    const float* old_values, const float* returns, const float* advantages, const int32_t* idx,
+                    int32_t mode, uavhip_stream_t stream);
+
 /* ---------------------------------------------------------------- misc */
 const char* uavhip_last_error(void);
 int32_t uavhip_abi_version(void);

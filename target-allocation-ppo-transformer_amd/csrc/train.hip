@@ -1,0 +1,1185 @@
+// train.hip -- K5: one clipped-PPO minibatch step (agents/ppo.py:96-169) of TransformerActorCritic
+// (networks/transformer_net.py) on gfx950, fp32 throughout.
+//
+// Layout: a minibatch of Bm samples is R = 5 Bm token rows, row = b * 5 + s, features contiguous.
+// Every linear layer is one problem of a grouped fp32 MFMA GEMM (v_mfma_f32_16x16x4_f32, 64 x 64
+// tiles, LDS double buffering):
+//    forward   Y[row][out]  = X[row][in] W[out][in]^T + b         (L_FWD)
+//    input gr. dX[row][in]  = dY[row][out] W[out][in]             (L_DX)
+//    weight gr dW[out][in]  = sum_row dY[row][out] X[row][in]     (L_DW, split-K partial slabs + the
+//                                                                  bias gradient as row sums of dY)
+// The last encoder layer of each trunk is pruned to the token the heads read (s = 4): K and V for
+// all rows, everything else for Bm rows (compact [Bm][...] tensors), so its gradients are exactly
+// the dense model's. Attention (5 keys, 8 heads x 16), residual + LayerNorm, heads + loss and the
+// fused clip_grad_norm_ + Adam are VALU kernels. The host side (uavhip_ppo_step) sequences ~40
+// launches on one stream: the whole step is graph-capturable (no host sync, no allocation).
+#include <cmath>
+#include <initializer_list>
+#include <utility>
+
+#include "common.hpp"
+#include "policy_layout.hpp"
+
+namespace uavhip {
+namespace tr {
+using namespace pol;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ cross-lane sums (no LDS)
+__device__ __forceinline__ float add_xor1(float v) {
+    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float add_xor2(float v) {
+    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float add_ror4(float v) {  // row_ror:4 inside each row of 16
+    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float add_ror8(float v) {
+    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float add_xor16(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float add_xor32(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// sum over the 4 lanes of a quad / over the whole wave (same value in every lane)
+__device__ __forceinline__ float quad_sum(float v) { return add_xor2(add_xor1(v)); }
+__device__ __forceinline__ float wave_sum(float v) {
+    return add_xor32(add_xor16(add_ror8(add_ror4(add_xor2(add_xor1(v))))));
+}
+
+// ================================================================== grouped GEMM
+enum Layout { L_FWD = 0, L_DX = 1, L_DW = 2 };
+enum Epi { E_STORE = 0, E_BIAS, E_BIAS_RELU, E_ACCUM, E_RELU_MASK, E_SPLIT };
+
+struct GemmProb {
+    const float* A;
+    const float* B;
+    float* C;            // output (E_SPLIT: partial slabs [splits][M][N])
+    const float* bias;   // E_BIAS*: [N]
+    const float* aux;    // E_RELU_MASK: C = acc * (aux[m][n] > 0)
+    float* bias_part;    // E_SPLIT: [splits][M] row sums of A over the split (the bias gradient)
+    int M, N, K, lda, ldb, ldc, ldaux;
+    int epi, kchunk, splits, tiles_n, tile_begin;
+};
+constexpr int kMaxProbs = 16;
+struct GemmBatch {
+    GemmProb p[kMaxProbs];
+    int n;
+};
+
+constexpr int BM = 64, BN = 64, BK = 32, LDS_K = BK + 4;  // 36-float rows: conflict-free float4 reads
+
+// A(m, k): L_FWD / L_DX row-major [M][K] (lda); L_DW "column" [K][M] (lda).
+// B(k, n): L_FWD = W[n][k] (ldb = K-stride); L_DX / L_DW row-major [K][N] (ldb).
+// LDS images are k-contiguous: As[m][k], Bs[n][k].
+template <int LAYOUT>
+__device__ __forceinline__ void load_slab(const GemmProb& P, int m0, int n0, int k0, f32x4 (&ra)[2], f32x4 (&rb)[2]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int q = t + 256 * h;  // 512 float4 per operand slab (64 x 32)
+        if (LAYOUT == L_DW) {
+            const int k = q >> 4, mq = (q & 15) * 4;
+            ra[h] = *reinterpret_cast<const f32x4*>(P.A + (size_t)(k0 + k) * P.lda + m0 + mq);
+        } else {
+            const int m = q >> 3, kq = (q & 7) * 4;
+            ra[h] = *reinterpret_cast<const f32x4*>(P.A + (size_t)(m0 + m) * P.lda + k0 + kq);
+        }
+        if (LAYOUT == L_FWD) {
+            const int n = q >> 3, kq = (q & 7) * 4;
+            rb[h] = *reinterpret_cast<const f32x4*>(P.B + (size_t)(n0 + n) * P.ldb + k0 + kq);
+        } else {
+            const int k = q >> 4, nq = (q & 15) * 4;
+            rb[h] = *reinterpret_cast<const f32x4*>(P.B + (size_t)(k0 + k) * P.ldb + n0 + nq);
+        }
+    }
+}
+
+template <int LAYOUT>
+__device__ __forceinline__ void store_slab(float* As, float* Bs, const f32x4 (&ra)[2], const f32x4 (&rb)[2]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int q = t + 256 * h;
+        if (LAYOUT == L_DW) {
+            const int k = q >> 4, mq = (q & 15) * 4;
+            As[(mq + 0) * LDS_K + k] = ra[h].x;
+            As[(mq + 1) * LDS_K + k] = ra[h].y;
+            As[(mq + 2) * LDS_K + k] = ra[h].z;
+            As[(mq + 3) * LDS_K + k] = ra[h].w;
+        } else {
+            const int m = q >> 3, kq = (q & 7) * 4;
+            *reinterpret_cast<f32x4*>(As + m * LDS_K + kq) = ra[h];
+        }
+        if (LAYOUT == L_FWD) {
+            const int n = q >> 3, kq = (q & 7) * 4;
+            *reinterpret_cast<f32x4*>(Bs + n * LDS_K + kq) = rb[h];
+        } else {
+            const int k = q >> 4, nq = (q & 15) * 4;
+            Bs[(nq + 0) * LDS_K + k] = rb[h].x;
+            Bs[(nq + 1) * LDS_K + k] = rb[h].y;
+            Bs[(nq + 2) * LDS_K + k] = rb[h].z;
+            Bs[(nq + 3) * LDS_K + k] = rb[h].w;
+        }
+    }
+}
+
+// One 64 x 64 output tile per 256-thread workgroup; wave w computes rows 32 (w & 1) + [0, 32) and
+// columns 32 (w >> 1) + [0, 32) as 2 x 2 MFMA 16 x 16 tiles. Both operands use the k permutation
+// k = 16 h + 4 (lane >> 4) + j for MFMA j of float4 read h (as in policy.hip).
+template <int LAYOUT>
+__global__ __launch_bounds__(256) void k_gemm(const GemmBatch gb) {
+    __shared__ __attribute__((aligned(16))) float As[2][BM * LDS_K];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDS_K];
+    int pi = 0;
+    while (pi + 1 < gb.n && (int)blockIdx.x >= gb.p[pi + 1].tile_begin) ++pi;
+    const GemmProb& P = gb.p[pi];
+    int t = blockIdx.x - P.tile_begin;
+    const int tiles_m = P.M / BM;
+    const int per_split = tiles_m * P.tiles_n;
+    const int split = t / per_split;
+    t -= split * per_split;
+    const int tmi = t / P.tiles_n, tni = t - tmi * P.tiles_n;
+    const int m0 = tmi * BM, n0 = tni * BN;
+    const int kb = split * P.kchunk;
+    const int ke = min(P.K, kb + P.kchunk);
+    const int nslab = (ke - kb) / BK;
+
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
+    const int wm = (wv & 1) * 32, wn = (wv >> 1) * 32;
+    const bool rowsum = P.epi == E_SPLIT && P.bias_part && tni == 0;
+    float rs = 0.f;  // row sum of A for row m0 + threadIdx.x (threads < 64)
+
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    f32x4 ra[2], rb[2];
+    load_slab<LAYOUT>(P, m0, n0, kb, ra, rb);
+    store_slab<LAYOUT>(As[0], Bs[0], ra, rb);
+    __syncthreads();
+    for (int s = 0; s < nslab; ++s) {
+        const int cur = s & 1;
+        if (s + 1 < nslab) load_slab<LAYOUT>(P, m0, n0, kb + (s + 1) * BK, ra, rb);
+        const float* as = As[cur];
+        const float* bs = Bs[cur];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            f32x4 fa[2], fb[2];
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                fa[x] = *reinterpret_cast<const f32x4*>(as + (wm + 16 * x + i16) * LDS_K + 16 * h + 4 * g);
+                fb[x] = *reinterpret_cast<const f32x4*>(bs + (wn + 16 * x + i16) * LDS_K + 16 * h + 4 * g);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a][j], fb[b][j], acc[a][b], 0, 0, 0);
+        }
+        if (rowsum && threadIdx.x < BM) {
+            const float* row = as + threadIdx.x * LDS_K;
+#pragma unroll
+            for (int k = 0; k < BK; k += 4) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(row + k);
+                rs += (v.x + v.y) + (v.z + v.w);
+            }
+        }
+        if (s + 1 < nslab) store_slab<LAYOUT>(As[cur ^ 1], Bs[cur ^ 1], ra, rb);
+        __syncthreads();
+    }
+    if (rowsum && threadIdx.x < BM) P.bias_part[(size_t)split * P.M + m0 + threadIdx.x] = rs;
+
+    // epilogue: lane (i16, g) of tile (a, b) holds C[m0 + wm + 16a + 4g + r][n0 + wn + 16b + i16]
+    float* C = P.epi == E_SPLIT ? P.C + (size_t)split * P.M * P.N : P.C;
+    const int ldc = P.epi == E_SPLIT ? P.N : P.ldc;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int n = n0 + wn + 16 * b + i16;
+        const float bv = (P.epi == E_BIAS || P.epi == E_BIAS_RELU) ? P.bias[n] : 0.f;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm + 16 * a + 4 * g + r;
+                float v = acc[a][b][r];
+                float* cp = C + (size_t)m * ldc + n;
+                switch (P.epi) {
+                    case E_BIAS: v = v + bv; break;
+                    case E_BIAS_RELU: v = fmaxf(v + bv, 0.f); break;
+                    case E_ACCUM: v = *cp + v; break;
+                    case E_RELU_MASK: v = P.aux[(size_t)m * P.ldaux + n] > 0.f ? v : 0.f; break;
+                    default: break;
+                }
+                *cp = v;
+            }
+        }
+    }
+}
+
+// ================================================================== forward pieces
+// Gather the minibatch rows, key padding mask (transformer_net.py:52-54), both embeddings
+// (transformer_net.py:57-59): e = relu(x We^T + be), h0 = e + pos[s]. One block per token row:
+// threads [0, 128) actor features, [128, 256) critic features.
+struct EmbedArgs {
+    const float* states;
+    const int32_t* idx;
+    const float* P;  // params
+    float* xg;       // [R][16]
+    float* mask;     // [R] 1 = padded key
+    float *e_a, *h0_a, *e_c, *h0_c;  // [R][128]
+    const int8_t* act_in;
+    const float *oldlp_in, *oldv_in, *ret_in, *adv_in;
+    float* smp;  // [Bm][8]: action, old_logp, old_value, return, advantage
+};
+__global__ __launch_bounds__(256) void k_embed_fwd(const EmbedArgs a) {
+    __shared__ float xs[16];
+    const int r = blockIdx.x, b = r / S, s = r - b * S;
+    const long long src = (long long)a.idx[b];
+    if (threadIdx.x < 16) {
+        const float v = threadIdx.x < IN ? a.states[(src * S + s) * IN + threadIdx.x] : 0.f;
+        xs[threadIdx.x] = v;
+        a.xg[(size_t)r * 16 + threadIdx.x] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float sa = 0.f;
+        for (int k = 0; k < IN; ++k) sa += fabsf(xs[k]);
+        a.mask[r] = (s < S - 1 && sa == 0.f) ? 1.f : 0.f;
+        if (s == 0) {
+            float* o = a.smp + (size_t)b * 8;
+            o[0] = (float)(a.act_in[src] != 0);
+            o[1] = a.oldlp_in[src];
+            o[2] = a.oldv_in[src];
+            o[3] = a.ret_in[src];
+            o[4] = a.adv_in[src];
+        }
+    }
+    const int trunk = threadIdx.x >> 7, f = threadIdx.x & 127;
+    const int base = trunk ? kCriticTrunk : kActorTrunk;
+    const float* We = a.P + kOffs.o[base + EMB_W] + f * IN;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < IN; ++k) acc += We[k] * xs[k];
+    const float e = fmaxf(acc + a.P[kOffs.o[base + EMB_B] + f], 0.f);
+    const float h = e + a.P[kOffs.o[base + POS] + s * D + f];
+    (trunk ? a.e_c : a.e_a)[(size_t)r * D + f] = e;
+    (trunk ? a.h0_c : a.h0_a)[(size_t)r * D + f] = h;
+}
+
+// Self-attention over the 5 keys of each sample: one (sample, head) per 4 lanes, each lane owning
+// 4 of the 16 head dims. qkv [R][384] (in_proj output), mask [R]; `last`: query s = 4 only, the
+// output o is compact [Bm][128]; else all 5 queries, o is [R][128].
+__global__ __launch_bounds__(256) void k_attn_fwd(const float* __restrict__ qkv, const float* __restrict__ mask,
+                                                  float* __restrict__ o, int Bm, int last) {
+    const int gt = blockIdx.x * 256 + threadIdx.x;
+    const int q4 = gt & 3, hh = (gt >> 2) & 7, b = gt >> 5;
+    if (b >= Bm) return;
+    const int d0 = hh * HD + 4 * q4;
+    f32x4 k[S], v[S];
+    bool msk[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        const float* row = qkv + (size_t)(b * S + j) * 3 * D;
+        k[j] = *reinterpret_cast<const f32x4*>(row + D + d0);
+        v[j] = *reinterpret_cast<const f32x4*>(row + 2 * D + d0);
+        msk[j] = mask[b * S + j] != 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        if (last && i < S - 1) continue;
+        const f32x4 q = *reinterpret_cast<const f32x4*>(qkv + (size_t)(b * S + i) * 3 * D + d0);
+        float sc[S];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            const float part = quad_sum(q.x * k[j].x + q.y * k[j].y + q.z * k[j].z + q.w * k[j].w);
+            sc[j] = msk[j] ? -INFINITY : part * 0.25f;
+            mx = fmaxf(mx, sc[j]);
+        }
+        float den = 0.f;
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            sc[j] = __expf(sc[j] - mx);
+            den += sc[j];
+        }
+        const float inv = 1.0f / den;
+        f32x4 out = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < S; ++j) out += (sc[j] * inv) * v[j];
+        const int orow = last ? b : b * S + i;
+        *reinterpret_cast<f32x4*>(o + (size_t)orow * D + d0) = out;
+    }
+}
+
+// Post-LN residual block: z = hin[row(i)] + a[i]; out[i] = LN(z) * w + b (eps 1e-5), saving
+// xhat[i] = (z - mean) * rstd and rstd[i]. One wave per row, 2 features per lane. hin rows are
+// hin_stride * i + hin_off (token-4 rows of a full tensor for the pruned layers).
+__global__ __launch_bounds__(256) void k_resln_fwd(const float* __restrict__ hin, int hin_stride, int hin_off,
+                                                   const float* __restrict__ a, const float* __restrict__ w,
+                                                   const float* __restrict__ bb, float* __restrict__ xhat,
+                                                   float* __restrict__ rstd, float* __restrict__ out, int rows) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= rows) return;
+    const int l = lane_id();
+    const float2 hv = *reinterpret_cast<const float2*>(hin + (size_t)(i * hin_stride + hin_off) * D + 2 * l);
+    const float2 av = *reinterpret_cast<const float2*>(a + (size_t)i * D + 2 * l);
+    const float z0 = hv.x + av.x, z1 = hv.y + av.y;
+    const float mean = wave_sum(z0 + z1) * (1.0f / D);
+    const float d0 = z0 - mean, d1 = z1 - mean;
+    const float var = wave_sum(d0 * d0 + d1 * d1) * (1.0f / D);
+    const float rs = 1.0f / sqrtf(var + 1e-5f);
+    const float x0 = d0 * rs, x1 = d1 * rs;
+    *reinterpret_cast<float2*>(xhat + (size_t)i * D + 2 * l) = make_float2(x0, x1);
+    const float2 ww = *reinterpret_cast<const float2*>(w + 2 * l);
+    const float2 bv = *reinterpret_cast<const float2*>(bb + 2 * l);
+    *reinterpret_cast<float2*>(out + (size_t)i * D + 2 * l) = make_float2(x0 * ww.x + bv.x, x1 * ww.y + bv.y);
+    if (l == 0) rstd[i] = rs;
+}
+
+// ================================================================== heads + loss
+// 16 samples per 1024-thread block (one wave per sample). Head weights staged in LDS with a
+// 129-float row stride (lane j reads row j: conflict-free).
+constexpr int kHeadSamples = 16;
+constexpr int kWs = D + 1;
+constexpr int kHeadPartN = 2 * HID + 2 + HID + 1;  // dW/db of actor_head.2 and critic_head.2
+constexpr int kHeadPart = 196;                     // padded
+
+struct HeadArgs {
+    const float* P;
+    const float* h_a;   // [Bm][128] actor trunk output (token 4)
+    const float* h_c;   // [Bm][128] critic trunk output (token 4)
+    float* z_a;         // [Bm][64] relu(head.0) actor
+    float* z_c;         // [Bm][64]
+    float* smp;         // [Bm][8]: 5 logits0, 6 logits1, 7 value
+    float* part;        // [nblk][4]: sum min(s1,s2), sum (v-R)^2, sum (vc-R)^2, sum entropy
+    float eps_clip;
+    int Bm;
+};
+
+__device__ void head_hidden(const float* Wl, const float* hs, const float* b0, float* z, int p, int l) {
+    float acc = 0.f;
+    const float* wr = Wl + l * kWs;
+    const float* hr = hs + p * D;
+#pragma unroll 8
+    for (int k = 0; k < D; ++k) acc += wr[k] * hr[k];
+    z[l] = fmaxf(acc + b0[l], 0.f);
+}
+
+// Categorical(softmax(logits)) of transformer_net.py:124-144 as torch.distributions evaluates it:
+// p = softmax(l); p /= sum(p); lc = log(clamp(p, eps, 1 - eps)); logp = lc[a]; ent = -sum(lc * p).
+struct CatVals {
+    float y0, y1, s, p0, p1, c0, c1, lc0, lc1;
+};
+__device__ __forceinline__ CatVals categorical(float l0, float l1) {
+    CatVals c;
+    const float m = fmaxf(l0, l1);
+    const float e0 = expf(l0 - m), e1 = expf(l1 - m);
+    const float den = e0 + e1;
+    c.y0 = e0 / den;
+    c.y1 = e1 / den;
+    c.s = c.y0 + c.y1;
+    c.p0 = c.y0 / c.s;
+    c.p1 = c.y1 / c.s;
+    const float eps = 1.1920928955078125e-07f;
+    c.c0 = fminf(fmaxf(c.p0, eps), 1.f - eps);
+    c.c1 = fminf(fmaxf(c.p1, eps), 1.f - eps);
+    c.lc0 = logf(c.c0);
+    c.lc1 = logf(c.c1);
+    return c;
+}
+
+__global__ __launch_bounds__(1024) void k_heads_fwd(const HeadArgs a) {
+    __shared__ float Wl[HID * kWs];
+    __shared__ float hs[kHeadSamples * D];
+    __shared__ float red[kHeadSamples][4];
+    const int p = threadIdx.x >> 6, l = lane_id();
+    const int b = blockIdx.x * kHeadSamples + p;
+    for (int trunk = 0; trunk < 2; ++trunk) {
+        const int head = trunk ? kCriticHead : kActorHead;
+        const float* W0 = a.P + kOffs.o[head];
+        for (int i = threadIdx.x; i < HID * D; i += 1024) Wl[(i >> 7) * kWs + (i & 127)] = W0[i];
+        const float* h = trunk ? a.h_c : a.h_a;
+        for (int i = threadIdx.x; i < kHeadSamples * D; i += 1024)
+            hs[i] = h[(size_t)(blockIdx.x * kHeadSamples + (i >> 7)) * D + (i & 127)];
+        __syncthreads();
+        float* z = (trunk ? a.z_c : a.z_a) + (size_t)b * HID;
+        head_hidden(Wl, hs, a.P + kOffs.o[head + 1], z, p, l);
+        const float zl = z[l];
+        const float* W2 = a.P + kOffs.o[head + 2];
+        const float* b2 = a.P + kOffs.o[head + 3];
+        float* o = a.smp + (size_t)b * 8;
+        if (trunk == 0) {
+            const float l0 = wave_sum(W2[l] * zl) + b2[0];
+            const float l1 = wave_sum(W2[HID + l] * zl) + b2[1];
+            if (l == 0) { o[5] = l0; o[6] = l1; }
+        } else {
+            const float v = wave_sum(W2[l] * zl) + b2[0];
+            if (l == 0) o[7] = v;
+        }
+        __syncthreads();
+    }
+    if (l == 0) {
+        const float* o = a.smp + (size_t)b * 8;
+        const int act = o[0] != 0.f;
+        const CatVals c = categorical(o[5], o[6]);
+        const float logp = act ? c.lc1 : c.lc0;
+        const float ent = -(c.lc0 * c.p0 + c.lc1 * c.p1);
+        const float ratio = expf(logp - o[1]);
+        const float A = o[4];
+        const float s1 = ratio * A;
+        const float s2 = fminf(fmaxf(ratio, 1.f - a.eps_clip), 1.f + a.eps_clip) * A;
+        const float v = o[7], R = o[3], ov = o[2];
+        const float vc = ov + fminf(fmaxf(v - ov, -a.eps_clip), a.eps_clip);
+        red[p][0] = fminf(s1, s2);
+        red[p][1] = (v - R) * (v - R);
+        red[p][2] = (vc - R) * (vc - R);
+        red[p][3] = ent;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        float s = 0.f;
+        for (int i = 0; i < kHeadSamples; ++i) s += red[i][threadIdx.x];
+        a.part[blockIdx.x * 4 + threadIdx.x] = s;
+    }
+}
+
+struct HeadBwdArgs {
+    const float* P;
+    const float* h_a;
+    const float* h_c;
+    const float* z_a;
+    const float* z_c;
+    const float* smp;
+    const float* part;  // forward partials [nblk][4]
+    float* dz_a;        // [Bm][64] d(head.0 pre-activation), relu-masked
+    float* dz_c;
+    float* dh_a;        // [Bm][128] gradient wrt the actor trunk output (token 4)
+    float* dh_c;
+    float* hpart;       // [nblk][kHeadPart] head.2 weight / bias gradient partials
+    double* stats;      // += loss_actor, loss_critic, entropy, 1
+    float eps_clip, value_coef, entropy_coef;
+    int Bm;
+};
+
+// Loss gradients of ppo.py:148-169 per sample (torch's min / max / clamp backward conventions:
+// ties send half the gradient to each side, clamp passes it on the closed interval), then the
+// heads' backward.
+__global__ __launch_bounds__(1024) void k_heads_bwd(const HeadBwdArgs a) {
+    __shared__ float Wl[HID * kWs];
+    __shared__ float dzs[kHeadSamples * HID];
+    __shared__ float tot[4];
+    __shared__ float gsm[kHeadSamples][3];  // dlogit0, dlogit1, dvalue
+    __shared__ float hp[kHeadSamples][kHeadPart];
+    const int p = threadIdx.x >> 6, l = lane_id();
+    const int b = blockIdx.x * kHeadSamples + p;
+    const int nblk = a.Bm / kHeadSamples;
+    if (threadIdx.x < 64) {  // reduce the forward partials of every block (same order in all blocks)
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int i = l; i < nblk; i += 64)
+            for (int c = 0; c < 4; ++c) s[c] += a.part[i * 4 + c];
+        for (int c = 0; c < 4; ++c) {
+            const float w = wave_sum(s[c]);
+            if (l == 0) tot[c] = w;
+        }
+    }
+    __syncthreads();
+    const float inv = 1.0f / (float)a.Bm;
+    const float L1 = tot[1] * inv, L2 = tot[2] * inv;
+    if (l == 0) {
+        const float* o = a.smp + (size_t)b * 8;
+        const int act = o[0] != 0.f;
+        const CatVals c = categorical(o[5], o[6]);
+        const float logp = act ? c.lc1 : c.lc0;
+        const float ratio = expf(logp - o[1]);
+        const float A = o[4], lo = 1.f - a.eps_clip, hi = 1.f + a.eps_clip;
+        const float s1 = ratio * A;
+        const float s2 = fminf(fmaxf(ratio, lo), hi) * A;
+        const float gmin = -inv;  // d(-mean(min)) / d min_i
+        const float g1 = s1 < s2 ? gmin : (s1 == s2 ? 0.5f * gmin : 0.f);
+        const float g2 = s2 < s1 ? gmin : (s1 == s2 ? 0.5f * gmin : 0.f);
+        const float gr = g1 * A + ((ratio >= lo && ratio <= hi) ? g2 * A : 0.f);
+        const float glogp = gr * ratio;
+        const float gent = -a.entropy_coef * inv;
+        // back through lc = log(clamp(p)), ent = -sum(lc * p), p = y / s, s = y0 + y1, y = softmax
+        float glc0 = -gent * c.p0, glc1 = -gent * c.p1;
+        if (act) glc1 += glogp; else glc0 += glogp;
+        const float eps = 1.1920928955078125e-07f;
+        float gp0 = -gent * c.lc0 + ((c.p0 >= eps && c.p0 <= 1.f - eps) ? glc0 / c.c0 : 0.f);
+        float gp1 = -gent * c.lc1 + ((c.p1 >= eps && c.p1 <= 1.f - eps) ? glc1 / c.c1 : 0.f);
+        const float gs = -(gp0 * c.y0 + gp1 * c.y1) / (c.s * c.s);
+        const float gy0 = gp0 / c.s + gs, gy1 = gp1 / c.s + gs;
+        const float dot = gy0 * c.y0 + gy1 * c.y1;
+        const float gl0 = c.y0 * (gy0 - dot), gl1 = c.y1 * (gy1 - dot);
+        // value: 0.5 * max(mean((v-R)^2), mean((vc-R)^2))
+        const float v = o[7], R = o[3], ov = o[2];
+        const float dv = v - ov;
+        const float vc = ov + fminf(fmaxf(dv, -a.eps_clip), a.eps_clip);
+        const float w1 = L1 > L2 ? 1.f : (L1 == L2 ? 0.5f : 0.f);
+        const float w2 = L2 > L1 ? 1.f : (L1 == L2 ? 0.5f : 0.f);
+        const float gv = a.value_coef * (w1 * 2.f * (v - R) * inv +
+                                         ((dv >= -a.eps_clip && dv <= a.eps_clip) ? w2 * 2.f * (vc - R) * inv : 0.f));
+        gsm[p][0] = gl0;
+        gsm[p][1] = gl1;
+        gsm[p][2] = gv;
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.stats) {
+        a.stats[0] += (double)(-tot[0] * inv);
+        a.stats[1] += (double)fmaxf(L1, L2);
+        a.stats[2] += (double)(tot[3] * inv);
+        a.stats[3] += 1.0;
+    }
+    for (int trunk = 0; trunk < 2; ++trunk) {
+        const int head = trunk ? kCriticHead : kActorHead;
+        const float* W0 = a.P + kOffs.o[head];
+        const float* W2 = a.P + kOffs.o[head + 2];
+        const float* z = (trunk ? a.z_c : a.z_a) + (size_t)b * HID;
+        const float zl = z[l];
+        float g;
+        if (trunk == 0) g = W2[l] * gsm[p][0] + W2[HID + l] * gsm[p][1];
+        else g = W2[l] * gsm[p][2];
+        const float dz = zl > 0.f ? g : 0.f;
+        (trunk ? a.dz_c : a.dz_a)[(size_t)b * HID + l] = dz;
+        dzs[p * HID + l] = dz;
+        // head.2 gradient partials: dW2[o][j] = sum_b g_o z_j, db2[o] = sum_b g_o
+        if (trunk == 0) {
+            hp[p][l] = gsm[p][0] * zl;
+            hp[p][HID + l] = gsm[p][1] * zl;
+            if (l < 2) hp[p][2 * HID + l] = gsm[p][l];
+        } else {
+            hp[p][2 * HID + 2 + l] = gsm[p][2] * zl;
+            if (l == 0) hp[p][3 * HID + 2] = gsm[p][2];
+        }
+        for (int i = threadIdx.x; i < HID * D; i += 1024) Wl[(i >> 7) * kWs + (i & 127)] = W0[i];
+        __syncthreads();
+        // dh[k] = sum_j W0[j][k] dz[j]: lane l owns k = l and l + 64
+        float* dh = (trunk ? a.dh_c : a.dh_a) + (size_t)b * D;
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll 8
+        for (int j = 0; j < HID; ++j) {
+            const float d = dzs[p * HID + j];
+            s0 += Wl[j * kWs + l] * d;
+            s1 += Wl[j * kWs + 64 + l] * d;
+        }
+        dh[l] = s0;
+        dh[64 + l] = s1;
+        __syncthreads();
+    }
+    for (int i = threadIdx.x; i < kHeadPart; i += 1024) {
+        float s = 0.f;
+        if (i < kHeadPartN)
+            for (int q = 0; q < kHeadSamples; ++q) s += hp[q][i];
+        a.hpart[(size_t)blockIdx.x * kHeadPart + i] = s;
+    }
+}
+
+// ================================================================== backward pieces
+// LayerNorm backward (torch's formula) for `rows` rows, one wave per row:
+//   g = gout * w; gin = rstd * (g - mean(g) - xhat * mean(g * xhat))
+// gin goes to dst1[row] and, if dst2, to dst2[row * dst2_stride + dst2_off] (the residual branch).
+// Per-block partials of dw = sum gout * xhat and db = sum gout: part[blk][0..127], [128..255].
+constexpr int kLnBlocks = 256;
+__global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ gout, const float* __restrict__ xhat,
+                                                const float* __restrict__ rstd, const float* __restrict__ w,
+                                                float* __restrict__ dst1, float* __restrict__ dst2, int dst2_stride,
+                                                int dst2_off, float* __restrict__ part, int rows) {
+    __shared__ float pw[4][D], pb[4][D];
+    const int wv = threadIdx.x >> 6, l = lane_id();
+    const float2 ww = *reinterpret_cast<const float2*>(w + 2 * l);
+    float aw0 = 0.f, aw1 = 0.f, ab0 = 0.f, ab1 = 0.f;
+    for (int i = blockIdx.x * 4 + wv; i < rows; i += gridDim.x * 4) {
+        const float2 go = *reinterpret_cast<const float2*>(gout + (size_t)i * D + 2 * l);
+        const float2 xh = *reinterpret_cast<const float2*>(xhat + (size_t)i * D + 2 * l);
+        aw0 += go.x * xh.x; aw1 += go.y * xh.y;
+        ab0 += go.x; ab1 += go.y;
+        const float g0 = go.x * ww.x, g1 = go.y * ww.y;
+        const float mg = wave_sum(g0 + g1) * (1.0f / D);
+        const float mgx = wave_sum(g0 * xh.x + g1 * xh.y) * (1.0f / D);
+        const float rs = rstd[i];
+        const float2 gi = make_float2(rs * (g0 - mg - xh.x * mgx), rs * (g1 - mg - xh.y * mgx));
+        *reinterpret_cast<float2*>(dst1 + (size_t)i * D + 2 * l) = gi;
+        if (dst2) *reinterpret_cast<float2*>(dst2 + (size_t)(i * dst2_stride + dst2_off) * D + 2 * l) = gi;
+    }
+    pw[wv][2 * l] = aw0; pw[wv][2 * l + 1] = aw1;
+    pb[wv][2 * l] = ab0; pb[wv][2 * l + 1] = ab1;
+    __syncthreads();
+    if (threadIdx.x < D) {
+        const int f = threadIdx.x;
+        part[(size_t)blockIdx.x * 2 * D + f] = (pw[0][f] + pw[1][f]) + (pw[2][f] + pw[3][f]);
+        part[(size_t)blockIdx.x * 2 * D + D + f] = (pb[0][f] + pb[1][f]) + (pb[2][f] + pb[3][f]);
+    }
+}
+
+// Attention backward. P recomputed from q, k; with g = do (query rows):
+//   dv_j = sum_i P_ij g_i; dP_ij = g_i . v_j; dS_ij = P_ij (dP_ij - sum_k P_ik dP_ik);
+//   dq_i = sum_j dS_ij k_j / 4; dk_j = sum_i dS_ij q_i / 4.
+// dqkv [R][384] gets all rows (dq zero on rows that were not queries).
+__global__ __launch_bounds__(256) void k_attn_bwd(const float* __restrict__ qkv, const float* __restrict__ mask,
+                                                  const float* __restrict__ dout, float* __restrict__ dqkv, int Bm,
+                                                  int last) {
+    const int gt = blockIdx.x * 256 + threadIdx.x;
+    const int q4 = gt & 3, hh = (gt >> 2) & 7, b = gt >> 5;
+    if (b >= Bm) return;
+    const int d0 = hh * HD + 4 * q4;
+    f32x4 k[S], v[S], dk[S], dv[S];
+    bool msk[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        const float* row = qkv + (size_t)(b * S + j) * 3 * D;
+        k[j] = *reinterpret_cast<const f32x4*>(row + D + d0);
+        v[j] = *reinterpret_cast<const f32x4*>(row + 2 * D + d0);
+        msk[j] = mask[b * S + j] != 0.f;
+        dk[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+        if (!(last && i < S - 1)) {
+            const f32x4 q = *reinterpret_cast<const f32x4*>(qkv + (size_t)(b * S + i) * 3 * D + d0);
+            const int grow = last ? b : b * S + i;
+            const f32x4 g = *reinterpret_cast<const f32x4*>(dout + (size_t)grow * D + d0);
+            float pr[S], dp[S];
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                const float part = quad_sum(q.x * k[j].x + q.y * k[j].y + q.z * k[j].z + q.w * k[j].w);
+                pr[j] = msk[j] ? -INFINITY : part * 0.25f;
+                mx = fmaxf(mx, pr[j]);
+            }
+            float den = 0.f;
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                pr[j] = __expf(pr[j] - mx);
+                den += pr[j];
+            }
+            const float inv = 1.0f / den;
+            float sdp = 0.f;
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                pr[j] *= inv;
+                dp[j] = quad_sum(g.x * v[j].x + g.y * v[j].y + g.z * v[j].z + g.w * v[j].w);
+                sdp += pr[j] * dp[j];
+            }
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                const float ds = pr[j] * (dp[j] - sdp) * 0.25f;
+                dq += ds * k[j];
+                dk[j] += ds * q;
+                dv[j] += pr[j] * g;
+            }
+        }
+        *reinterpret_cast<f32x4*>(dqkv + (size_t)(b * S + i) * 3 * D + d0) = dq;
+    }
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        float* row = dqkv + (size_t)(b * S + j) * 3 * D;
+        *reinterpret_cast<f32x4*>(row + D + d0) = dk[j];
+        *reinterpret_cast<f32x4*>(row + 2 * D + d0) = dv[j];
+    }
+}
+
+// Embedding backward for both trunks, 16 samples (80 rows) per block; thread = (trunk, feature).
+// Partials per block and trunk in parameter order: We [128][14] | be [128] | pos [5][128].
+constexpr int kEmbPart = D * IN + D + S * D;  // 2560
+__global__ __launch_bounds__(256) void k_embed_bwd(const float* __restrict__ dh_a, const float* __restrict__ dh_c,
+                                                   const float* __restrict__ e_a, const float* __restrict__ e_c,
+                                                   const float* __restrict__ xg, float* __restrict__ part) {
+    __shared__ float xs[16 * S * 16];
+    const int r0 = blockIdx.x * 16 * S;
+    for (int i = threadIdx.x; i < 16 * S * 16; i += 256) xs[i] = xg[(size_t)r0 * 16 + i];
+    __syncthreads();
+    const int trunk = threadIdx.x >> 7, f = threadIdx.x & 127;
+    const float* dh = trunk ? dh_c : dh_a;
+    const float* e = trunk ? e_c : e_a;
+    float dw[IN], dbv = 0.f, dp[S];
+#pragma unroll
+    for (int k = 0; k < IN; ++k) dw[k] = 0.f;
+#pragma unroll
+    for (int s = 0; s < S; ++s) dp[s] = 0.f;
+    for (int rr = 0; rr < 16 * S; ++rr) {
+        const int s = rr % S;
+        const float g = dh[(size_t)(r0 + rr) * D + f];
+        dp[s] += g;
+        const float gp = e[(size_t)(r0 + rr) * D + f] > 0.f ? g : 0.f;
+        dbv += gp;
+#pragma unroll
+        for (int k = 0; k < IN; ++k) dw[k] += gp * xs[rr * 16 + k];
+    }
+    float* o = part + ((size_t)blockIdx.x * 2 + trunk) * kEmbPart;
+#pragma unroll
+    for (int k = 0; k < IN; ++k) o[f * IN + k] = dw[k];
+    o[D * IN + f] = dbv;
+#pragma unroll
+    for (int s = 0; s < S; ++s) o[D * IN + D + s * D + f] = dp[s];
+}
+
+// ================================================================== gradient reduction + Adam
+// grads[dst + i] = sum_p src[p * part_stride + i] for each segment; block partial sums of g^2.
+struct Segment {
+    const float* src;
+    int dst, count, parts, part_stride, block_begin;
+};
+constexpr int kMaxSegs = 64;
+struct SegBatch {
+    Segment s[kMaxSegs];
+    int n;
+};
+__global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* __restrict__ grads,
+                                                      float* __restrict__ sq_part, double* __restrict__ step) {
+    __shared__ float red[4];
+    int si = 0;
+    while (si + 1 < sb.n && (int)blockIdx.x >= sb.s[si + 1].block_begin) ++si;
+    const Segment& S_ = sb.s[si];
+    const int i = (blockIdx.x - S_.block_begin) * 256 + threadIdx.x;
+    float sq = 0.f;
+    if (i < S_.count) {
+        // four independent chains keep four loads in flight per thread
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        const float* src = S_.src + i;
+        const size_t ps = S_.part_stride;
+        int p = 0;
+        for (; p + 4 <= S_.parts; p += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] += src[(size_t)(p + u) * ps];
+        }
+        for (; p < S_.parts; ++p) acc[0] += src[(size_t)p * ps];
+        const float tot = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        grads[S_.dst + i] = tot;
+        sq = tot * tot;
+    }
+    sq = wave_sum(sq);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) sq_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (step && blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1.0;
+}
+
+// clip_grad_norm_(max_norm) + torch.optim.Adam (ppo.py:17-22 groups: actor params < critic trunk
+// offset use lr_actor, the rest lr_critic), elementwise over the flat buffers.
+struct AdamArgs {
+    float* params;
+    float* grads;
+    float* m;
+    float* v;
+    const double* step;
+    const float* sq_part;
+    int n_sq, n, critic_begin;
+    float lr_actor, lr_critic, beta1, beta2, eps, max_norm;
+};
+__global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
+    __shared__ float red[4];
+    __shared__ float coef_s;
+    float s = 0.f;
+    for (int i = threadIdx.x; i < a.n_sq; i += 256) s += a.sq_part[i];
+    s = wave_sum(s);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float total = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+        const float c = a.max_norm / (total + 1e-6f);
+        coef_s = fminf(c, 1.0f);
+    }
+    __syncthreads();
+    const float coef = coef_s;
+    const double t = a.step[0];
+    const double bc1 = 1.0 - pow((double)a.beta1, t);
+    const double bc2 = 1.0 - pow((double)a.beta2, t);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < a.n; i += gridDim.x * 256) {
+        const float lr = i < a.critic_begin ? a.lr_actor : a.lr_critic;
+        const float ss = (float)((double)lr / bc1);
+        const float bs = (float)sqrt(bc2);
+        const float g = a.grads[i] * coef;
+        a.grads[i] = g;
+        float m = a.m[i];
+        m = m + (1.f - a.beta1) * (g - m);
+        const float v = a.v[i] * a.beta2 + (1.f - a.beta2) * (g * g);
+        a.m[i] = m;
+        a.v[i] = v;
+        const float denom = sqrtf(v) / bs + a.eps;
+        a.params[i] = a.params[i] + (-ss) * (m / denom);
+    }
+}
+
+// ================================================================== host orchestration
+struct WS {  // workspace carve-up (floats), identical for sizing and for the step
+    size_t off = 0;
+    float* base = nullptr;
+    float* take(size_t n) {
+        float* p = base ? base + off : nullptr;
+        off += (n + 63) & ~(size_t)63;
+        return p;
+    }
+};
+
+struct LayerBufs {  // one encoder layer (pruned: tail tensors are [Bm] rows)
+    float *qkv, *o, *a, *xhat1, *rstd1, *h1, *u, *f, *xhat2, *rstd2, *h2;
+    float *dqkv, *dz1, *dout, *dh1, *du, *df, *dhin;
+    float *ln1_part, *ln2_part;
+};
+
+struct Plan {
+    int Bm, R;
+    float *xg, *mask, *smp, *e_a, *h0_a, *e_c, *h0_c;
+    LayerBufs la, lc0, lc1;
+    float *z_a, *z_c, *dz_a, *dz_c, *dh_a, *dh_c, *fpart, *hpart, *epart, *sq_part;
+    float* split_ws;
+    size_t split_floats;
+    size_t total;  // workspace floats
+};
+
+constexpr int kSplitRows = 2048;  // K rows per split of the weight-gradient GEMMs
+
+inline int splits_for(int K) { return (K + kSplitRows - 1) / kSplitRows; }
+
+inline size_t dw_split_floats(int Bm) {
+    const int R = Bm * S;
+    auto slab = [&](int M, int N, int K) { return (size_t)splits_for(K) * ((size_t)M * N + M); };
+    size_t n = 0;
+    // actor L0 (pruned), critic L0 (full), critic L1 (pruned), both head.0
+    n += slab(3 * D, D, R) + slab(D, D, Bm) + slab(FF, D, Bm) + slab(D, FF, Bm);
+    n += slab(3 * D, D, R) + slab(D, D, R) + slab(FF, D, R) + slab(D, FF, R);
+    n += slab(3 * D, D, R) + slab(D, D, Bm) + slab(FF, D, Bm) + slab(D, FF, Bm);
+    n += 2 * slab(HID, D, Bm);
+    return n;
+}
+
+inline void carve_layer(WS& w, LayerBufs& L, int R, int rows) {
+    L.qkv = w.take((size_t)R * 3 * D);
+    L.o = w.take((size_t)rows * D);
+    L.a = w.take((size_t)rows * D);
+    L.xhat1 = w.take((size_t)rows * D);
+    L.rstd1 = w.take(rows);
+    L.h1 = w.take((size_t)rows * D);
+    L.u = w.take((size_t)rows * FF);
+    L.f = w.take((size_t)rows * D);
+    L.xhat2 = w.take((size_t)rows * D);
+    L.rstd2 = w.take(rows);
+    L.h2 = w.take((size_t)rows * D);
+    L.dqkv = w.take((size_t)R * 3 * D);
+    L.dz1 = w.take((size_t)rows * D);
+    L.dout = w.take((size_t)rows * D);
+    L.dh1 = w.take((size_t)rows * D);
+    L.du = w.take((size_t)rows * FF);
+    L.df = w.take((size_t)rows * D);
+    L.dhin = w.take((size_t)R * D);
+    L.ln1_part = w.take((size_t)kLnBlocks * 2 * D);
+    L.ln2_part = w.take((size_t)kLnBlocks * 2 * D);
+}
+
+inline Plan make_plan(int Bm, float* base) {
+    Plan p{};
+    WS w;
+    w.base = base;
+    p.Bm = Bm;
+    p.R = Bm * S;
+    const int R = p.R;
+    p.xg = w.take((size_t)R * 16);
+    p.mask = w.take(R);
+    p.smp = w.take((size_t)Bm * 8);
+    p.e_a = w.take((size_t)R * D);
+    p.h0_a = w.take((size_t)R * D);
+    p.e_c = w.take((size_t)R * D);
+    p.h0_c = w.take((size_t)R * D);
+    carve_layer(w, p.la, R, Bm);
+    carve_layer(w, p.lc0, R, R);
+    carve_layer(w, p.lc1, R, Bm);
+    p.z_a = w.take((size_t)Bm * HID);
+    p.z_c = w.take((size_t)Bm * HID);
+    p.dz_a = w.take((size_t)Bm * HID);
+    p.dz_c = w.take((size_t)Bm * HID);
+    p.dh_a = w.take((size_t)Bm * D);
+    p.dh_c = w.take((size_t)Bm * D);
+    p.fpart = w.take((size_t)(Bm / kHeadSamples) * 4);
+    p.hpart = w.take((size_t)(Bm / kHeadSamples) * kHeadPart);
+    p.epart = w.take((size_t)(Bm / kHeadSamples) * 2 * kEmbPart);
+    p.sq_part = w.take(1 << 16);
+    p.split_floats = dw_split_floats(Bm);
+    p.split_ws = w.take(p.split_floats);
+    p.total = w.off;
+    return p;
+}
+
+struct GemmBuilder {
+    GemmBatch gb{};
+    int tiles = 0;
+    void add(const float* A, int lda, const float* B, int ldb, float* C, int ldc, int M, int N, int K, int epi,
+             const float* bias = nullptr, const float* aux = nullptr, int ldaux = 0, float* bias_part = nullptr,
+             int kchunk = 0) {
+        GemmProb& P = gb.p[gb.n++];
+        P.A = A; P.B = B; P.C = C; P.bias = bias; P.aux = aux; P.bias_part = bias_part;
+        P.M = M; P.N = N; P.K = K; P.lda = lda; P.ldb = ldb; P.ldc = ldc; P.ldaux = ldaux;
+        P.epi = epi;
+        P.kchunk = kchunk > 0 ? kchunk : K;
+        P.splits = (K + P.kchunk - 1) / P.kchunk;
+        P.tiles_n = N / BN;
+        P.tile_begin = tiles;
+        tiles += P.splits * (M / BM) * P.tiles_n;
+    }
+};
+
+template <int LAYOUT>
+int launch_gemm(const GemmBuilder& g, hipStream_t st) {
+    if (g.gb.n == 0) return UAVHIP_OK;
+    hipLaunchKernelGGL(k_gemm<LAYOUT>, dim3(g.tiles), dim3(256), 0, st, g.gb);
+    return check_launch("k_gemm");
+}
+
+inline const float* prm(const uavhip_ppo* c, int i) { return c->params + kOffs.o[i]; }
+
+}  // namespace tr
+}  // namespace uavhip
+
+using namespace uavhip;
+using namespace uavhip::tr;
+
+extern "C" int64_t uavhip_ppo_workspace_floats(int32_t minibatch) {
+    if (minibatch <= 0 || minibatch % 64) return -1;
+    return (int64_t)make_plan(minibatch, nullptr).total;
+}
+
+#define TR_CHECK(x)          \
+    do {                     \
+        const int rc_ = (x); \
+        if (rc_) return rc_; \
+    } while (0)
+
+extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const int8_t* actions,
+                               const float* old_logp, const float* old_values, const float* returns,
+                               const float* advantages, const int32_t* idx, int32_t mode, uavhip_stream_t stream) {
+    if (!c || !c->params || !c->grads || !c->workspace || !states || !actions || !old_logp || !old_values ||
+        !returns || !advantages || !idx) {
+        set_error("uavhip_ppo_step: NULL pointer");
+        return UAVHIP_EINVAL;
+    }
+    if (c->minibatch <= 0 || c->minibatch % 64 || c->n_floats != kOffs.o[kNumParams] ||
+        (mode == 0 && (!c->adam_m || !c->adam_v || !c->adam_step))) {
+        set_error("uavhip_ppo_step: minibatch %d (multiple of 64), n_floats %d (expected %d), mode %d", c->minibatch,
+                  c->n_floats, kOffs.o[kNumParams], mode);
+        return UAVHIP_EINVAL;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const Plan p = make_plan(c->minibatch, c->workspace);
+    const int Bm = p.Bm, R = p.R, nblk = Bm / kHeadSamples;
+    const LayerBufs &A = p.la, &C0 = p.lc0, &C1 = p.lc1;
+    auto L = [&](int trunk, int layer, int which) { return prm(c, layer_param(trunk, layer, which)); };
+    const int ta = kActorTrunk, tc = kCriticTrunk;
+
+    // ---------------------------------------------------------------- forward
+    {
+        EmbedArgs ea{states, idx, c->params, p.xg, p.mask, p.e_a, p.h0_a, p.e_c, p.h0_c, actions, old_logp,
+                     old_values, returns, advantages, p.smp};
+        hipLaunchKernelGGL(k_embed_fwd, dim3(R), dim3(256), 0, st, ea);
+        TR_CHECK(check_launch("k_embed_fwd"));
+    }
+    {   // layer 0 QKV of both trunks
+        GemmBuilder g;
+        g.add(p.h0_a, D, L(ta, 0, INW), D, A.qkv, 3 * D, R, 3 * D, D, E_BIAS, L(ta, 0, INB));
+        g.add(p.h0_c, D, L(tc, 0, INW), D, C0.qkv, 3 * D, R, 3 * D, D, E_BIAS, L(tc, 0, INB));
+        TR_CHECK(launch_gemm<L_FWD>(g, st));
+    }
+    hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, A.qkv, p.mask, A.o, Bm, 1);
+    hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, C0.qkv, p.mask, C0.o, Bm, 0);
+    TR_CHECK(check_launch("k_attn_fwd"));
+    auto tail_fwd = [&](std::initializer_list<std::pair<const LayerBufs*, std::pair<int, int>>> layers,
+                        std::initializer_list<const float*> hins) -> int {
+        // layers: (buffers, (trunk, layer)); rows = R for the full layer (critic L0), Bm otherwise
+        GemmBuilder g1, g2, g3;
+        int i = 0;
+        const float* hin_arr[4];
+        for (const float* h : hins) hin_arr[i++] = h;
+        i = 0;
+        for (auto& lt : layers) {
+            const LayerBufs& B = *lt.first;
+            const int tr_ = lt.second.first, ly = lt.second.second;
+            const int rows = (&B == &C0) ? R : Bm;
+            g1.add(B.o, D, L(tr_, ly, OUTW), D, B.a, D, rows, D, D, E_BIAS, L(tr_, ly, OUTB));
+            ++i;
+        }
+        TR_CHECK(launch_gemm<L_FWD>(g1, st));
+        i = 0;
+        for (auto& lt : layers) {
+            const LayerBufs& B = *lt.first;
+            const int tr_ = lt.second.first, ly = lt.second.second;
+            const int rows = (&B == &C0) ? R : Bm;
+            const int hs = rows == R ? 1 : S, ho = rows == R ? 0 : S - 1;
+            hipLaunchKernelGGL(k_resln_fwd, dim3((rows + 3) / 4), dim3(256), 0, st, hin_arr[i], hs, ho, B.a,
+                               L(tr_, ly, N1W), L(tr_, ly, N1B), B.xhat1, B.rstd1, B.h1, rows);
+            TR_CHECK(check_launch("k_resln_fwd"));
+            g2.add(B.h1, D, L(tr_, ly, L1W), D, B.u, FF, rows, FF, D, E_BIAS_RELU, L(tr_, ly, L1B));
+            g3.add(B.u, FF, L(tr_, ly, L2W), FF, B.f, D, rows, D, FF, E_BIAS, L(tr_, ly, L2B));
+            ++i;
+        }
+        TR_CHECK(launch_gemm<L_FWD>(g2, st));
+        TR_CHECK(launch_gemm<L_FWD>(g3, st));
+        for (auto& lt : layers) {
+            const LayerBufs& B = *lt.first;
+            const int tr_ = lt.second.first, ly = lt.second.second;
+            const int rows = (&B == &C0) ? R : Bm;
+            hipLaunchKernelGGL(k_resln_fwd, dim3((rows + 3) / 4), dim3(256), 0, st, B.h1, 1, 0, B.f,
+                               L(tr_, ly, N2W), L(tr_, ly, N2B), B.xhat2, B.rstd2, B.h2, rows);
+            TR_CHECK(check_launch("k_resln_fwd"));
+        }
+        return UAVHIP_OK;
+    };
+    TR_CHECK(tail_fwd({{&A, {ta, 0}}, {&C0, {tc, 0}}}, {p.h0_a, p.h0_c}));
+    {   // critic layer 1 (pruned)
+        GemmBuilder g;
+        g.add(C0.h2, D, L(tc, 1, INW), D, C1.qkv, 3 * D, R, 3 * D, D, E_BIAS, L(tc, 1, INB));
+        TR_CHECK(launch_gemm<L_FWD>(g, st));
+        hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, C1.qkv, p.mask, C1.o, Bm, 1);
+        TR_CHECK(check_launch("k_attn_fwd"));
+        TR_CHECK(tail_fwd({{&C1, {tc, 1}}}, {C0.h2}));
+    }
+    {
+        HeadArgs ha{c->params, A.h2, C1.h2, p.z_a, p.z_c, p.smp, p.fpart, c->eps_clip, Bm};
+        hipLaunchKernelGGL(k_heads_fwd, dim3(nblk), dim3(1024), 0, st, ha);
+        TR_CHECK(check_launch("k_heads_fwd"));
+    }
+    // ---------------------------------------------------------------- backward
+    {
+        HeadBwdArgs hb{c->params, A.h2, C1.h2, p.z_a, p.z_c, p.smp, p.fpart, p.dz_a, p.dz_c, p.dh_a, p.dh_c,
+                       p.hpart, c->stats, c->eps_clip, c->value_coef, c->entropy_coef, Bm};
+        hipLaunchKernelGGL(k_heads_bwd, dim3(nblk), dim3(1024), 0, st, hb);
+        TR_CHECK(check_launch("k_heads_bwd"));
+    }
+    // tail backward of a set of layers: gout = gradient wrt the layer output rows (compact for
+    // pruned layers), then dh_in (full [R][128]) = residual + Win^T dqkv
+    auto tail_bwd = [&](std::initializer_list<std::pair<const LayerBufs*, std::pair<int, int>>> layers,
+                        std::initializer_list<const float*> gouts) -> int {
+        const float* go[4];
+        int i = 0;
+        for (const float* gp : gouts) go[i++] = gp;
+        GemmBuilder g1, g2, g3, g4;
+        i = 0;
+        for (auto& lt : layers) {
+            const LayerBufs& B = *lt.first;
+            const int tr_ = lt.second.first, ly = lt.second.second;
+            const int rows = (&B == &C0) ? R : Bm;
+            hipLaunchKernelGGL(k_ln_bwd, dim3(kLnBlocks), dim3(256), 0, st, go[i], B.xhat2, B.rstd2, L(tr_, ly, N2W),
+                               B.df, B.dh1, 1, 0, B.ln2_part, rows);
+            TR_CHECK(check_launch("k_ln_bwd"));
+            g1.add(B.df, D, L(tr_, ly, L2W), FF, B.du, FF, rows, FF, D, E_RELU_MASK, nullptr, B.u, FF);
+            g2.add(B.du, FF, L(tr_, ly, L1W), D, B.dh1, D, rows, D, FF, E_ACCUM);
+            ++i;
+        }
+        TR_CHECK(launch_gemm<L_DX>(g1, st));
+        TR_CHECK(launch_gemm<L_DX>(g2, st));
+        for (auto& lt : layers) {
+            const LayerBufs& B = *lt.first;
+            const int tr_ = lt.second.first, ly = lt.second.second;
+            const int rows = (&B == &C0) ? R : Bm;
+            if (rows != R) {
+                if (hipMemsetAsync(B.dhin, 0, (size_t)R * D * sizeof(float), st) != hipSuccess) {
+                    set_error("hipMemsetAsync failed");
+                    return UAVHIP_EHIP;
+                }
+            }
+            hipLaunchKernelGGL(k_ln_bwd, dim3(kLnBlocks), dim3(256), 0, st, B.dh1, B.xhat1, B.rstd1, L(tr_, ly, N1W),
+                               B.dz1, B.dhin, rows == R ? 1 : S, rows == R ? 0 : S - 1, B.ln1_part, rows);
+            TR_CHECK(check_launch("k_ln_bwd"));
+            g3.add(B.dz1, D, L(tr_, ly, OUTW), D, B.dout, D, rows, D, D, E_STORE);
+        }
+        TR_CHECK(launch_gemm<L_DX>(g3, st));
+        for (auto& lt : layers) {
+            const LayerBufs& B = *lt.first;
+            const int tr_ = lt.second.first, ly = lt.second.second;
+            const int rows = (&B == &C0) ? R : Bm;
+            hipLaunchKernelGGL(k_attn_bwd, dim3(Bm * 32 / 256), dim3(256), 0, st, B.qkv, p.mask, B.dout, B.dqkv, Bm,
+                               rows == R ? 0 : 1);
+            TR_CHECK(check_launch("k_attn_bwd"));
+            g4.add(B.dqkv, 3 * D, L(tr_, ly, INW), D, B.dhin, D, R, D, 3 * D, E_ACCUM);
+        }
+        TR_CHECK(launch_gemm<L_DX>(g4, st));
+        return UAVHIP_OK;
+    };
+    TR_CHECK(tail_bwd({{&C1, {tc, 1}}}, {p.dh_c}));
+    TR_CHECK(tail_bwd({{&A, {ta, 0}}, {&C0, {tc, 0}}}, {p.dh_a, C1.dhin}));
+    hipLaunchKernelGGL(k_embed_bwd, dim3(nblk), dim3(256), 0, st, A.dhin, C0.dhin, p.e_a, p.e_c, p.xg, p.epart);
+    TR_CHECK(check_launch("k_embed_bwd"));
+
+    // ---------------------------------------------------------------- weight gradients
+    SegBatch sb{};
+    int seg_blocks = 0;
+    auto seg = [&](const float* src, int dst, int count, int parts, int part_stride) {
+        Segment& s = sb.s[sb.n++];
+        s.src = src; s.dst = dst; s.count = count; s.parts = parts; s.part_stride = part_stride;
+        s.block_begin = seg_blocks;
+        seg_blocks += (count + 255) / 256;
+    };
+    {
+        GemmBuilder g;
+        float* ws = p.split_ws;
+        auto dw = [&](const float* dY, int ldy, const float* X, int ldx, int M, int N, int K, int pw, int pb) {
+            const int sp = splits_for(K);
+            float* slab = ws;
+            float* bpart = ws + (size_t)sp * M * N;
+            ws += (size_t)sp * ((size_t)M * N + M);
+            g.add(dY, ldy, X, ldx, slab, N, M, N, K, E_SPLIT, nullptr, nullptr, 0, bpart, kSplitRows);
+            seg(slab, kOffs.o[pw], M * N, sp, M * N);
+            seg(bpart, kOffs.o[pb], M, sp, M);
+        };
+        auto layer_dw = [&](const LayerBufs& B, int tr_, int ly, const float* hin, int rows) {
+            dw(B.dqkv, 3 * D, hin, D, 3 * D, D, R, layer_param(tr_, ly, INW), layer_param(tr_, ly, INB));
+            dw(B.dz1, D, B.o, D, D, D, rows, layer_param(tr_, ly, OUTW), layer_param(tr_, ly, OUTB));
+            dw(B.du, FF, B.h1, D, FF, D, rows, layer_param(tr_, ly, L1W), layer_param(tr_, ly, L1B));
+            dw(B.df, D, B.u, FF, D, FF, rows, layer_param(tr_, ly, L2W), layer_param(tr_, ly, L2B));
+        };
+        layer_dw(A, ta, 0, p.h0_a, Bm);
+        layer_dw(C0, tc, 0, p.h0_c, R);
+        layer_dw(C1, tc, 1, C0.h2, Bm);
+        dw(p.dz_a, HID, A.h2, D, HID, D, Bm, kActorHead, kActorHead + 1);
+        dw(p.dz_c, HID, C1.h2, D, HID, D, Bm, kCriticHead, kCriticHead + 1);
+        TR_CHECK(launch_gemm<L_DW>(g, st));
+    }
+    // LayerNorm weights / biases
+    auto ln_seg = [&](const float* part, int pw, int pb) {
+        seg(part, kOffs.o[pw], D, kLnBlocks, 2 * D);
+        seg(part + D, kOffs.o[pb], D, kLnBlocks, 2 * D);
+    };
+    ln_seg(A.ln1_part, layer_param(ta, 0, N1W), layer_param(ta, 0, N1B));
+    ln_seg(A.ln2_part, layer_param(ta, 0, N2W), layer_param(ta, 0, N2B));
+    ln_seg(C0.ln1_part, layer_param(tc, 0, N1W), layer_param(tc, 0, N1B));
+    ln_seg(C0.ln2_part, layer_param(tc, 0, N2W), layer_param(tc, 0, N2B));
+    ln_seg(C1.ln1_part, layer_param(tc, 1, N1W), layer_param(tc, 1, N1B));
+    ln_seg(C1.ln2_part, layer_param(tc, 1, N2W), layer_param(tc, 1, N2B));
+    // embeddings (We | be | pos per trunk), head.2 weights / biases
+    for (int trunk = 0; trunk < 2; ++trunk) {
+        const int base = trunk ? kCriticTrunk : kActorTrunk;
+        const float* src = p.epart + (size_t)trunk * kEmbPart;
+        seg(src, kOffs.o[base + EMB_W], D * IN, nblk, 2 * kEmbPart);
+        seg(src + D * IN, kOffs.o[base + EMB_B], D, nblk, 2 * kEmbPart);
+        seg(src + D * IN + D, kOffs.o[base + POS], S * D, nblk, 2 * kEmbPart);
+    }
+    seg(p.hpart, kOffs.o[kActorHead + 2], 2 * HID, nblk, kHeadPart);
+    seg(p.hpart + 2 * HID, kOffs.o[kActorHead + 3], 2, nblk, kHeadPart);
+    seg(p.hpart + 2 * HID + 2, kOffs.o[kCriticHead + 2], HID, nblk, kHeadPart);
+    seg(p.hpart + 3 * HID + 2, kOffs.o[kCriticHead + 3], 1, nblk, kHeadPart);
+    if (sb.n > kMaxSegs || seg_blocks > (1 << 16)) {
+        set_error("uavhip_ppo_step: too many gradient segments (%d) / blocks (%d)", sb.n, seg_blocks);
+        return UAVHIP_EINVAL;
+    }
+    // padding floats between parameters stay zero
+    hipLaunchKernelGGL(k_reduce_grads, dim3(seg_blocks), dim3(256), 0, st, sb, c->grads, p.sq_part,
+                       mode == 0 ? c->adam_step : nullptr);
+    TR_CHECK(check_launch("k_reduce_grads"));
+    if (mode == 0) {
+        AdamArgs aa{c->params, c->grads, c->adam_m, c->adam_v, c->adam_step, p.sq_part, seg_blocks, c->n_floats,
+                    kOffs.o[kCriticTrunk], c->lr_actor, c->lr_critic, c->beta1, c->beta2, c->adam_eps,
+                    c->max_grad_norm};
+        hipLaunchKernelGGL(k_adam, dim3(512), dim3(256), 0, st, aa);
+        TR_CHECK(check_launch("k_adam"));
+    }
+    return UAVHIP_OK;
+}

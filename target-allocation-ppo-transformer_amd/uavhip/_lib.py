@@ -49,6 +49,14 @@ class PolicyDesc(ctypes.Structure):
                 ("d_head_hidden", _i32), ("actor_layers", _i32), ("critic_layers", _i32)]
 
 
+class PPODesc(ctypes.Structure):
+    """Mirror of `struct uavhip_ppo`."""
+    _fields_ = [("params", _vp), ("grads", _vp), ("adam_m", _vp), ("adam_v", _vp), ("adam_step", _vp),
+                ("workspace", _vp), ("stats", _vp), ("n_floats", _i32), ("minibatch", _i32)] + \
+              [(n, ctypes.c_float) for n in ("lr_actor", "lr_critic", "beta1", "beta2", "adam_eps", "eps_clip",
+                                             "max_grad_norm", "value_coef", "entropy_coef")]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "uavhip_score_pairs": (ctypes.c_int, [ctypes.POINTER(EnvDesc), _vp, _vp]),
@@ -65,6 +73,8 @@ _SIGS = {
     "uavhip_policy_tiling": (_i32, [ctypes.POINTER(_i32), _i32]),
     "uavhip_policy_forward": (ctypes.c_int, [ctypes.POINTER(PolicyDesc), _vp, _i32, _vp, ctypes.c_uint64,
                                              ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "uavhip_ppo_workspace_floats": (ctypes.c_int64, [_i32]),
+    "uavhip_ppo_step": (ctypes.c_int, [ctypes.POINTER(PPODesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
     "uavhip_last_error": (ctypes.c_char_p, []),
     "uavhip_abi_version": (_i32, []),
 }

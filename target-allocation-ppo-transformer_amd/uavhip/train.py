@@ -1,0 +1,117 @@
+"""FusedPPOTrainer: the clipped-PPO update of agents/ppo.py:96-169 on the HIP training step of
+libuavhip.so (uavhip_ppo_step, csrc/train.hip) -- grouped fp32 MFMA GEMMs, fused LayerNorm /
+attention / heads+loss kernels and a fused clip_grad_norm_ + Adam.
+
+The policy's parameters become views of one flat buffer (the uavhip_policy_layout() order), so
+state_dict(), load_state_dict() and the torch `evaluate` path keep working on the same storage the
+kernels update. One minibatch step is one C call; `run` captures it once into a hipGraph and
+replays it per minibatch, drawing minibatches like SubsetRandomSampler (torch.randperm of the
+given CPU generator, ppo.py:97-99).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import LIB, check, ptr, stream_handle
+from .config import cfg
+from .policy import layout
+
+
+class FusedPPOTrainer:
+    def __init__(self, policy, minibatch, lr_actor=None, lr_critic=None, eps_clip=None, max_grad_norm=None,
+                 value_coef=0.5, entropy_coef=0.01, betas=(0.9, 0.999), adam_eps=1e-8):
+        if minibatch <= 0 or minibatch % 64:
+            raise ValueError("minibatch must be a positive multiple of 64")
+        dev = next(policy.parameters()).device
+        if dev.type != "cuda":
+            raise RuntimeError("FusedPPOTrainer runs on the GPU (HIP) only")
+        self.policy, self.minibatch, self.device = policy, int(minibatch), dev
+        offs, n = layout()
+        params = list(policy.state_dict(keep_vars=True).values())
+        if len(params) != len(offs):
+            raise ValueError("unexpected state_dict layout")
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.params = torch.zeros(n, **f32)
+        with torch.no_grad():
+            for p, o in zip(params, offs):
+                self.params[o:o + p.numel()].copy_(p.detach().reshape(-1))
+                p.data = self.params[o:o + p.numel()].view_as(p)
+        self.grads = torch.zeros(n, **f32)
+        self.adam_m = torch.zeros(n, **f32)
+        self.adam_v = torch.zeros(n, **f32)
+        self.adam_step = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.stats = torch.zeros(4, dtype=torch.float64, device=dev)
+        ws = LIB.uavhip_ppo_workspace_floats(self.minibatch)
+        self.workspace = torch.zeros(int(ws), **f32)
+        self.idx = torch.zeros(self.minibatch, dtype=torch.int32, device=dev)
+        d = _lib.PPODesc()
+        d.params, d.grads = self.params.data_ptr(), self.grads.data_ptr()
+        d.adam_m, d.adam_v, d.adam_step = self.adam_m.data_ptr(), self.adam_v.data_ptr(), self.adam_step.data_ptr()
+        d.workspace, d.stats = self.workspace.data_ptr(), self.stats.data_ptr()
+        d.n_floats, d.minibatch = n, self.minibatch
+        d.lr_actor = cfg.LR_ACTOR if lr_actor is None else lr_actor
+        d.lr_critic = cfg.LR_CRITIC if lr_critic is None else lr_critic
+        d.beta1, d.beta2, d.adam_eps = betas[0], betas[1], adam_eps
+        d.eps_clip = cfg.EPS_CLIP if eps_clip is None else eps_clip
+        d.max_grad_norm = cfg.GRAD_NORM_CLIP if max_grad_norm is None else max_grad_norm
+        d.value_coef, d.entropy_coef = value_coef, entropy_coef
+        self.desc = d
+        self.bufs = None
+        self.graph = None
+
+    def set_buffers(self, states, actions, old_logprobs, old_values, returns, advantages):
+        """Trajectory buffers the minibatches are drawn from (kept by reference: a captured graph
+        reads them at their current addresses)."""
+        n = states.shape[0]
+        dev = self.device
+        self.bufs = (states.to(device=dev, dtype=torch.float32).contiguous().reshape(n, cfg.SEQ_LEN, cfg.STATE_DIM),
+                     actions.to(device=dev, dtype=torch.int8).contiguous().reshape(n),
+                     old_logprobs.to(device=dev, dtype=torch.float32).contiguous().reshape(n),
+                     old_values.to(device=dev, dtype=torch.float32).contiguous().reshape(n),
+                     returns.to(device=dev, dtype=torch.float32).contiguous().reshape(n),
+                     advantages.to(device=dev, dtype=torch.float32).contiguous().reshape(n))
+        self.n = n
+        self.graph = None
+
+    def step(self, mode=0):
+        """One minibatch step on rows self.idx (mode 1: gradients only, no parameter update)."""
+        s, a, lp, v, r, adv = self.bufs
+        check(LIB.uavhip_ppo_step(self.desc, ptr(s), ptr(a), ptr(lp), ptr(v), ptr(r), ptr(adv), ptr(self.idx),
+                                  int(mode), stream_handle()), "uavhip_ppo_step")
+
+    def gradients(self, idx):
+        """Raw gradients (before clipping) of the PPO loss on rows idx, as a flat tensor."""
+        self.idx.copy_(torch.as_tensor(idx, dtype=torch.int32, device=self.device))
+        self.step(mode=1)
+        return self.grads
+
+    def capture(self):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=s):
+            self.step(mode=0)
+        torch.cuda.current_stream().wait_stream(s)
+
+    def run(self, epochs=None, generator=None, use_graph=True):
+        """K epochs of minibatch steps over the buffers -> (mean actor loss, critic loss, entropy, n_steps)."""
+        epochs = cfg.K_EPOCHS if epochs is None else epochs
+        if use_graph and self.graph is None:
+            self.capture()
+        self.stats.zero_()
+        cnt = 0
+        for _ in range(epochs):
+            perm = torch.randperm(self.n, generator=generator).to(device=self.device, dtype=torch.int32)
+            for b in range(self.n // self.minibatch):
+                self.idx.copy_(perm[b * self.minibatch:(b + 1) * self.minibatch])
+                if use_graph:
+                    self.graph.replay()
+                else:
+                    self.step(mode=0)
+                cnt += 1
+        self.policy._packed_key = None  # parameters changed under torch's version counters: repack
+        if cnt == 0:
+            return 0.0, 0.0, 0.0, 0
+        st = self.stats.tolist()
+        return st[0] / st[3], st[1] / st[3], st[2] / st[3], cnt

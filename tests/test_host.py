@@ -17,7 +17,7 @@ HEADER = os.path.join(ROOT, "include", "uavhip.h")
 
 def _header_functions():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|int32_t|const char\*)\s+(uavhip_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|const char\*)\s+(uavhip_\w+)\s*\(", txt, re.M)))
 
 
 def _header_enum(name):
@@ -61,6 +61,29 @@ def test_ctypes_mirrors_header_enums():
     body = re.search(r"typedef struct uavhip_env \{(.*?)\} uavhip_env;", txt, re.S).group(1)
     names = re.findall(r"\*\s*(\w+);", body)
     assert names == [f[0] for f in _lib.EnvDesc._fields_[11:]]
+    assert _header_enum("uavhip_ist")["UAVHIP_IST_COUNT"] == _lib.IST_COUNT
+    assert _header_enum("uavhip_dst")["UAVHIP_DST_COUNT"] == _lib.DST_COUNT
+
+
+def _struct_fields(name):
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), txt, re.S).group(1)
+    out = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        out += [re.findall(r"\w+", part)[-1] for part in decl.replace("*", " ").split(",")]
+    return out
+
+
+def test_ctypes_mirrors_header_structs():
+    from uavhip import _lib
+    assert _struct_fields("uavhip_ppo") == [f[0] for f in _lib.PPODesc._fields_]
+    assert _struct_fields("uavhip_policy") == [f[0] for f in _lib.PolicyDesc._fields_]
+    assert _lib.LIB.uavhip_ppo_workspace_floats(64) > 0
+    assert _lib.LIB.uavhip_ppo_workspace_floats(4096) > _lib.LIB.uavhip_ppo_workspace_floats(64)
+    assert _lib.LIB.uavhip_ppo_workspace_floats(65) == -1
 
 
 def test_error_path_without_gpu():
