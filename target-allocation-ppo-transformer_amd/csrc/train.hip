@@ -19,12 +19,11 @@
 
 #include "common.hpp"
 #include "policy_layout.hpp"
+#include "gemm.hpp"
 
 namespace uavhip {
 namespace tr {
 using namespace pol;
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------ cross-lane sums (no LDS)
 __device__ __forceinline__ float add_xor1(float v) {
@@ -53,184 +52,10 @@ __device__ __forceinline__ float wave_sum(float v) {
     return add_xor32(add_xor16(add_ror8(add_ror4(add_xor2(add_xor1(v))))));
 }
 
-// ================================================================== grouped GEMM
-enum Layout { L_FWD = 0, L_DX = 1, L_DW = 2 };
-enum Epi { E_STORE = 0, E_BIAS, E_BIAS_RELU, E_ACCUM, E_RELU_MASK, E_SPLIT };
-
-struct GemmProb {
-    const float* A;
-    const float* B;
-    float* C;            // output (E_SPLIT: partial slabs [splits][M][N])
-    const float* bias;   // E_BIAS*: [N]
-    const float* aux;    // E_RELU_MASK: C = acc * (aux[m][n] > 0)
-    float* bias_part;    // E_SPLIT: [splits][M] row sums of A over the split (the bias gradient)
-    int M, N, K, lda, ldb, ldc, ldaux;
-    int epi, kchunk, splits, tiles_n, tile_begin;
-};
-constexpr int kMaxProbs = 16;
-struct GemmBatch {
-    GemmProb p[kMaxProbs];
-    int n;
-};
-
-constexpr int BM = 64, BN = 64, BK = 32, LDS_K = BK + 4;  // 36-float rows: conflict-free float4 reads
-
-// A(m, k): L_FWD / L_DX row-major [M][K] (lda); L_DW "column" [K][M] (lda).
-// B(k, n): L_FWD = W[n][k] (ldb = K-stride); L_DX / L_DW row-major [K][N] (ldb).
-// LDS images are k-contiguous: As[m][k], Bs[n][k].
-template <int LAYOUT>
-__device__ __forceinline__ void load_slab(const GemmProb& P, int m0, int n0, int k0, f32x4 (&ra)[2], f32x4 (&rb)[2]) {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int q = t + 256 * h;  // 512 float4 per operand slab (64 x 32)
-        if (LAYOUT == L_DW) {
-            const int k = q >> 4, mq = (q & 15) * 4;
-            ra[h] = *reinterpret_cast<const f32x4*>(P.A + (size_t)(k0 + k) * P.lda + m0 + mq);
-        } else {
-            const int m = q >> 3, kq = (q & 7) * 4;
-            ra[h] = *reinterpret_cast<const f32x4*>(P.A + (size_t)(m0 + m) * P.lda + k0 + kq);
-        }
-        if (LAYOUT == L_FWD) {
-            const int n = q >> 3, kq = (q & 7) * 4;
-            rb[h] = *reinterpret_cast<const f32x4*>(P.B + (size_t)(n0 + n) * P.ldb + k0 + kq);
-        } else {
-            const int k = q >> 4, nq = (q & 15) * 4;
-            rb[h] = *reinterpret_cast<const f32x4*>(P.B + (size_t)(k0 + k) * P.ldb + n0 + nq);
-        }
-    }
-}
-
-template <int LAYOUT>
-__device__ __forceinline__ void store_slab(float* As, float* Bs, const f32x4 (&ra)[2], const f32x4 (&rb)[2]) {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int q = t + 256 * h;
-        if (LAYOUT == L_DW) {
-            const int k = q >> 4, mq = (q & 15) * 4;
-            As[(mq + 0) * LDS_K + k] = ra[h].x;
-            As[(mq + 1) * LDS_K + k] = ra[h].y;
-            As[(mq + 2) * LDS_K + k] = ra[h].z;
-            As[(mq + 3) * LDS_K + k] = ra[h].w;
-        } else {
-            const int m = q >> 3, kq = (q & 7) * 4;
-            *reinterpret_cast<f32x4*>(As + m * LDS_K + kq) = ra[h];
-        }
-        if (LAYOUT == L_FWD) {
-            const int n = q >> 3, kq = (q & 7) * 4;
-            *reinterpret_cast<f32x4*>(Bs + n * LDS_K + kq) = rb[h];
-        } else {
-            const int k = q >> 4, nq = (q & 15) * 4;
-            Bs[(nq + 0) * LDS_K + k] = rb[h].x;
-            Bs[(nq + 1) * LDS_K + k] = rb[h].y;
-            Bs[(nq + 2) * LDS_K + k] = rb[h].z;
-            Bs[(nq + 3) * LDS_K + k] = rb[h].w;
-        }
-    }
-}
-
-// One 64 x 64 output tile per 256-thread workgroup; wave w computes rows 32 (w & 1) + [0, 32) and
-// columns 32 (w >> 1) + [0, 32) as 2 x 2 MFMA 16 x 16 tiles. Both operands use the k permutation
-// k = 16 h + 4 (lane >> 4) + j for MFMA j of float4 read h (as in policy.hip).
-template <int LAYOUT>
-__global__ __launch_bounds__(256) void k_gemm(const GemmBatch gb) {
-    __shared__ __attribute__((aligned(16))) float As[2][BM * LDS_K];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDS_K];
-    int pi = 0;
-    while (pi + 1 < gb.n && (int)blockIdx.x >= gb.p[pi + 1].tile_begin) ++pi;
-    const GemmProb& P = gb.p[pi];
-    int t = blockIdx.x - P.tile_begin;
-    const int tiles_m = P.M / BM;
-    const int per_split = tiles_m * P.tiles_n;
-    const int split = t / per_split;
-    t -= split * per_split;
-    const int tmi = t / P.tiles_n, tni = t - tmi * P.tiles_n;
-    const int m0 = tmi * BM, n0 = tni * BN;
-    const int kb = split * P.kchunk;
-    const int ke = min(P.K, kb + P.kchunk);
-    const int nslab = (ke - kb) / BK;
-
-    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
-    const int wm = (wv & 1) * 32, wn = (wv >> 1) * 32;
-    const bool rowsum = P.epi == E_SPLIT && P.bias_part && tni == 0;
-    float rs = 0.f;  // row sum of A for row m0 + threadIdx.x (threads < 64)
-
-    f32x4 acc[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    f32x4 ra[2], rb[2];
-    load_slab<LAYOUT>(P, m0, n0, kb, ra, rb);
-    store_slab<LAYOUT>(As[0], Bs[0], ra, rb);
-    __syncthreads();
-    for (int s = 0; s < nslab; ++s) {
-        const int cur = s & 1;
-        if (s + 1 < nslab) load_slab<LAYOUT>(P, m0, n0, kb + (s + 1) * BK, ra, rb);
-        const float* as = As[cur];
-        const float* bs = Bs[cur];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            f32x4 fa[2], fb[2];
-#pragma unroll
-            for (int x = 0; x < 2; ++x) {
-                fa[x] = *reinterpret_cast<const f32x4*>(as + (wm + 16 * x + i16) * LDS_K + 16 * h + 4 * g);
-                fb[x] = *reinterpret_cast<const f32x4*>(bs + (wn + 16 * x + i16) * LDS_K + 16 * h + 4 * g);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int a = 0; a < 2; ++a)
-#pragma unroll
-                    for (int b = 0; b < 2; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a][j], fb[b][j], acc[a][b], 0, 0, 0);
-        }
-        if (rowsum && threadIdx.x < BM) {
-            const float* row = as + threadIdx.x * LDS_K;
-#pragma unroll
-            for (int k = 0; k < BK; k += 4) {
-                const f32x4 v = *reinterpret_cast<const f32x4*>(row + k);
-                rs += (v.x + v.y) + (v.z + v.w);
-            }
-        }
-        if (s + 1 < nslab) store_slab<LAYOUT>(As[cur ^ 1], Bs[cur ^ 1], ra, rb);
-        __syncthreads();
-    }
-    if (rowsum && threadIdx.x < BM) P.bias_part[(size_t)split * P.M + m0 + threadIdx.x] = rs;
-
-    // epilogue: lane (i16, g) of tile (a, b) holds C[m0 + wm + 16a + 4g + r][n0 + wn + 16b + i16]
-    float* C = P.epi == E_SPLIT ? P.C + (size_t)split * P.M * P.N : P.C;
-    const int ldc = P.epi == E_SPLIT ? P.N : P.ldc;
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-        const int n = n0 + wn + 16 * b + i16;
-        const float bv = (P.epi == E_BIAS || P.epi == E_BIAS_RELU) ? P.bias[n] : 0.f;
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + wm + 16 * a + 4 * g + r;
-                float v = acc[a][b][r];
-                float* cp = C + (size_t)m * ldc + n;
-                switch (P.epi) {
-                    case E_BIAS: v = v + bv; break;
-                    case E_BIAS_RELU: v = fmaxf(v + bv, 0.f); break;
-                    case E_ACCUM: v = *cp + v; break;
-                    case E_RELU_MASK: v = P.aux[(size_t)m * P.ldaux + n] > 0.f ? v : 0.f; break;
-                    default: break;
-                }
-                *cp = v;
-            }
-        }
-    }
-}
-
 // ================================================================== forward pieces
 // Gather the minibatch rows, key padding mask (transformer_net.py:52-54), both embeddings
-// (transformer_net.py:57-59): e = relu(x We^T + be), h0 = e + pos[s]. One block per token row:
-// threads [0, 128) actor features, [128, 256) critic features.
+// (transformer_net.py:57-59): e = relu(x We^T + be), h0 = e + pos[s]. 16 samples (80 rows) per
+// block; thread = (trunk, feature) keeps its We row in registers and walks the rows.
 struct EmbedArgs {
     const float* states;
     const int32_t* idx;
@@ -242,39 +67,54 @@ struct EmbedArgs {
     const float *oldlp_in, *oldv_in, *ret_in, *adv_in;
     float* smp;  // [Bm][8]: action, old_logp, old_value, return, advantage
 };
+constexpr int kEmbRows = 16 * S;
 __global__ __launch_bounds__(256) void k_embed_fwd(const EmbedArgs a) {
-    __shared__ float xs[16];
-    const int r = blockIdx.x, b = r / S, s = r - b * S;
-    const long long src = (long long)a.idx[b];
+    __shared__ float xs[kEmbRows * 16];
+    const int r0 = blockIdx.x * kEmbRows, b0 = blockIdx.x * 16;
+    for (int i = threadIdx.x; i < kEmbRows * 16; i += 256) {
+        const int rr = i >> 4, k = i & 15, b = b0 + rr / S, s = rr % S;
+        const long long src = (long long)a.idx[b];
+        const float v = k < IN ? a.states[(src * S + s) * IN + k] : 0.f;
+        xs[i] = v;
+        a.xg[(size_t)r0 * 16 + i] = v;
+    }
     if (threadIdx.x < 16) {
-        const float v = threadIdx.x < IN ? a.states[(src * S + s) * IN + threadIdx.x] : 0.f;
-        xs[threadIdx.x] = v;
-        a.xg[(size_t)r * 16 + threadIdx.x] = v;
+        const int b = b0 + threadIdx.x;
+        const long long src = (long long)a.idx[b];
+        float* o = a.smp + (size_t)b * 8;
+        o[0] = (float)(a.act_in[src] != 0);
+        o[1] = a.oldlp_in[src];
+        o[2] = a.oldv_in[src];
+        o[3] = a.ret_in[src];
+        o[4] = a.adv_in[src];
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < kEmbRows) {
+        const int rr = threadIdx.x, s = rr % S;
         float sa = 0.f;
-        for (int k = 0; k < IN; ++k) sa += fabsf(xs[k]);
-        a.mask[r] = (s < S - 1 && sa == 0.f) ? 1.f : 0.f;
-        if (s == 0) {
-            float* o = a.smp + (size_t)b * 8;
-            o[0] = (float)(a.act_in[src] != 0);
-            o[1] = a.oldlp_in[src];
-            o[2] = a.oldv_in[src];
-            o[3] = a.ret_in[src];
-            o[4] = a.adv_in[src];
-        }
+        for (int k = 0; k < IN; ++k) sa += fabsf(xs[rr * 16 + k]);
+        a.mask[r0 + rr] = (s < S - 1 && sa == 0.f) ? 1.f : 0.f;
     }
     const int trunk = threadIdx.x >> 7, f = threadIdx.x & 127;
     const int base = trunk ? kCriticTrunk : kActorTrunk;
-    const float* We = a.P + kOffs.o[base + EMB_W] + f * IN;
-    float acc = 0.f;
+    float w[IN];
 #pragma unroll
-    for (int k = 0; k < IN; ++k) acc += We[k] * xs[k];
-    const float e = fmaxf(acc + a.P[kOffs.o[base + EMB_B] + f], 0.f);
-    const float h = e + a.P[kOffs.o[base + POS] + s * D + f];
-    (trunk ? a.e_c : a.e_a)[(size_t)r * D + f] = e;
-    (trunk ? a.h0_c : a.h0_a)[(size_t)r * D + f] = h;
+    for (int k = 0; k < IN; ++k) w[k] = a.P[kOffs.o[base + EMB_W] + f * IN + k];
+    const float be = a.P[kOffs.o[base + EMB_B] + f];
+    float pos[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) pos[s] = a.P[kOffs.o[base + POS] + s * D + f];
+    float* eo = trunk ? a.e_c : a.e_a;
+    float* ho = trunk ? a.h0_c : a.h0_a;
+#pragma unroll 5
+    for (int rr = 0; rr < kEmbRows; ++rr) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < IN; ++k) acc += w[k] * xs[rr * 16 + k];
+        const float e = fmaxf(acc + be, 0.f);
+        eo[(size_t)(r0 + rr) * D + f] = e;
+        ho[(size_t)(r0 + rr) * D + f] = e + pos[rr % S];
+    }
 }
 
 // Self-attention over the 5 keys of each sample: one (sample, head) per 4 lanes, each lane owning
@@ -589,7 +429,7 @@ __global__ __launch_bounds__(1024) void k_heads_bwd(const HeadBwdArgs a) {
 //   g = gout * w; gin = rstd * (g - mean(g) - xhat * mean(g * xhat))
 // gin goes to dst1[row] and, if dst2, to dst2[row * dst2_stride + dst2_off] (the residual branch).
 // Per-block partials of dw = sum gout * xhat and db = sum gout: part[blk][0..127], [128..255].
-constexpr int kLnBlocks = 256;
+constexpr int kLnBlocks = 512;
 __global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ gout, const float* __restrict__ xhat,
                                                 const float* __restrict__ rstd, const float* __restrict__ w,
                                                 float* __restrict__ dst1, float* __restrict__ dst2, int dst2_stride,
@@ -708,6 +548,7 @@ __global__ __launch_bounds__(256) void k_embed_bwd(const float* __restrict__ dh_
     for (int k = 0; k < IN; ++k) dw[k] = 0.f;
 #pragma unroll
     for (int s = 0; s < S; ++s) dp[s] = 0.f;
+#pragma unroll 5
     for (int rr = 0; rr < 16 * S; ++rr) {
         const int s = rr % S;
         const float g = dh[(size_t)(r0 + rr) * D + f];
@@ -729,9 +570,10 @@ __global__ __launch_bounds__(256) void k_embed_bwd(const float* __restrict__ dh_
 // grads[dst + i] = sum_p src[p * part_stride + i] for each segment; block partial sums of g^2.
 struct Segment {
     const float* src;
-    int dst, count, parts, part_stride, block_begin;
+    int dst, count, parts, part_stride, block_begin, wave_mode;
 };
 constexpr int kMaxSegs = 64;
+constexpr int kWaveModeParts = 16;  // more parts than this: one wave per element
 struct SegBatch {
     Segment s[kMaxSegs];
     int n;
@@ -742,22 +584,35 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
     int si = 0;
     while (si + 1 < sb.n && (int)blockIdx.x >= sb.s[si + 1].block_begin) ++si;
     const Segment& S_ = sb.s[si];
-    const int i = (blockIdx.x - S_.block_begin) * 256 + threadIdx.x;
+    const size_t ps = S_.part_stride;
     float sq = 0.f;
-    if (i < S_.count) {
-        // four independent chains keep four loads in flight per thread
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        const float* src = S_.src + i;
-        const size_t ps = S_.part_stride;
-        int p = 0;
-        for (; p + 4 <= S_.parts; p += 4) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc[u] += src[(size_t)(p + u) * ps];
+    if (S_.wave_mode) {  // element = block * 4 + wave; lanes stride over the parts
+        const int i = (blockIdx.x - S_.block_begin) * 4 + (threadIdx.x >> 6);
+        if (i < S_.count) {
+            float acc = 0.f;
+            for (int p = lane_id(); p < S_.parts; p += 64) acc += S_.src[(size_t)p * ps + i];
+            const float tot = wave_sum(acc);
+            if (lane_id() == 0) {
+                grads[S_.dst + i] = tot;
+                sq = tot * tot;
+            }
         }
-        for (; p < S_.parts; ++p) acc[0] += src[(size_t)p * ps];
-        const float tot = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-        grads[S_.dst + i] = tot;
-        sq = tot * tot;
+    } else {
+        const int i = (blockIdx.x - S_.block_begin) * 256 + threadIdx.x;
+        if (i < S_.count) {
+            // four independent chains keep four loads in flight per thread
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            const float* src = S_.src + i;
+            int p = 0;
+            for (; p + 4 <= S_.parts; p += 4) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[u] += src[(size_t)(p + u) * ps];
+            }
+            for (; p < S_.parts; ++p) acc[0] += src[(size_t)p * ps];
+            const float tot = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+            grads[S_.dst + i] = tot;
+            sq = tot * tot;
+        }
     }
     sq = wave_sum(sq);
     if (lane_id() == 0) red[threadIdx.x >> 6] = sq;
@@ -848,9 +703,9 @@ inline size_t dw_split_floats(int Bm) {
     auto slab = [&](int M, int N, int K) { return (size_t)splits_for(K) * ((size_t)M * N + M); };
     size_t n = 0;
     // actor L0 (pruned), critic L0 (full), critic L1 (pruned), both head.0
-    n += slab(3 * D, D, R) + slab(D, D, Bm) + slab(FF, D, Bm) + slab(D, FF, Bm);
+    const size_t pruned = slab(2 * D, D, R) + slab(D, D, Bm) + slab(D, D, Bm) + slab(FF, D, Bm) + slab(D, FF, Bm);
+    n += 2 * pruned;
     n += slab(3 * D, D, R) + slab(D, D, R) + slab(FF, D, R) + slab(D, FF, R);
-    n += slab(3 * D, D, R) + slab(D, D, Bm) + slab(FF, D, Bm) + slab(D, FF, Bm);
     n += 2 * slab(HID, D, Bm);
     return n;
 }
@@ -911,28 +766,19 @@ inline Plan make_plan(int Bm, float* base) {
     return p;
 }
 
-struct GemmBuilder {
-    GemmBatch gb{};
-    int tiles = 0;
-    void add(const float* A, int lda, const float* B, int ldb, float* C, int ldc, int M, int N, int K, int epi,
-             const float* bias = nullptr, const float* aux = nullptr, int ldaux = 0, float* bias_part = nullptr,
-             int kchunk = 0) {
-        GemmProb& P = gb.p[gb.n++];
-        P.A = A; P.B = B; P.C = C; P.bias = bias; P.aux = aux; P.bias_part = bias_part;
-        P.M = M; P.N = N; P.K = K; P.lda = lda; P.ldb = ldb; P.ldc = ldc; P.ldaux = ldaux;
-        P.epi = epi;
-        P.kchunk = kchunk > 0 ? kchunk : K;
-        P.splits = (K + P.kchunk - 1) / P.kchunk;
-        P.tiles_n = N / BN;
-        P.tile_begin = tiles;
-        tiles += P.splits * (M / BM) * P.tiles_n;
-    }
-};
+// in_proj of a pruned layer: K and V for all R rows, Q only for the Bm token-4 rows (row 5b + 4)
+inline void qkv_pruned(GemmBuilder& g, const float* hin, const float* Win, const float* bin, float* qkv, int R, int Bm) {
+    g.add(hin, D, Win + D * D, D, qkv + D, 3 * D, R, 2 * D, D, E_BIAS, bin + D);
+    g.add(hin + (S - 1) * D, S * D, Win, D, qkv + (S - 1) * 3 * D, S * 3 * D, Bm, D, D, E_BIAS, bin);
+}
 
 template <int LAYOUT>
-int launch_gemm(const GemmBuilder& g, hipStream_t st) {
-    if (g.gb.n == 0) return UAVHIP_OK;
-    hipLaunchKernelGGL(k_gemm<LAYOUT>, dim3(g.tiles), dim3(256), 0, st, g.gb);
+int run_gemm(const GemmBuilder& g, hipStream_t st) {
+    if (!g.valid()) {
+        set_error("k_gemm: problem shape not a multiple of the %d x %d x %d tile", g.bm, BN, BK);
+        return UAVHIP_EINVAL;
+    }
+    launch_gemm<LAYOUT>(g, st);
     return check_launch("k_gemm");
 }
 
@@ -980,14 +826,14 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
     {
         EmbedArgs ea{states, idx, c->params, p.xg, p.mask, p.e_a, p.h0_a, p.e_c, p.h0_c, actions, old_logp,
                      old_values, returns, advantages, p.smp};
-        hipLaunchKernelGGL(k_embed_fwd, dim3(R), dim3(256), 0, st, ea);
+        hipLaunchKernelGGL(k_embed_fwd, dim3(Bm / 16), dim3(256), 0, st, ea);
         TR_CHECK(check_launch("k_embed_fwd"));
     }
     {   // layer 0 QKV of both trunks
         GemmBuilder g;
-        g.add(p.h0_a, D, L(ta, 0, INW), D, A.qkv, 3 * D, R, 3 * D, D, E_BIAS, L(ta, 0, INB));
+        qkv_pruned(g, p.h0_a, L(ta, 0, INW), L(ta, 0, INB), A.qkv, R, Bm);
         g.add(p.h0_c, D, L(tc, 0, INW), D, C0.qkv, 3 * D, R, 3 * D, D, E_BIAS, L(tc, 0, INB));
-        TR_CHECK(launch_gemm<L_FWD>(g, st));
+        TR_CHECK(run_gemm<L_FWD>(g, st));
     }
     hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, A.qkv, p.mask, A.o, Bm, 1);
     hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, C0.qkv, p.mask, C0.o, Bm, 0);
@@ -1007,7 +853,7 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
             g1.add(B.o, D, L(tr_, ly, OUTW), D, B.a, D, rows, D, D, E_BIAS, L(tr_, ly, OUTB));
             ++i;
         }
-        TR_CHECK(launch_gemm<L_FWD>(g1, st));
+        TR_CHECK(run_gemm<L_FWD>(g1, st));
         i = 0;
         for (auto& lt : layers) {
             const LayerBufs& B = *lt.first;
@@ -1021,8 +867,8 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
             g3.add(B.u, FF, L(tr_, ly, L2W), FF, B.f, D, rows, D, FF, E_BIAS, L(tr_, ly, L2B));
             ++i;
         }
-        TR_CHECK(launch_gemm<L_FWD>(g2, st));
-        TR_CHECK(launch_gemm<L_FWD>(g3, st));
+        TR_CHECK(run_gemm<L_FWD>(g2, st));
+        TR_CHECK(run_gemm<L_FWD>(g3, st));
         for (auto& lt : layers) {
             const LayerBufs& B = *lt.first;
             const int tr_ = lt.second.first, ly = lt.second.second;
@@ -1036,8 +882,8 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
     TR_CHECK(tail_fwd({{&A, {ta, 0}}, {&C0, {tc, 0}}}, {p.h0_a, p.h0_c}));
     {   // critic layer 1 (pruned)
         GemmBuilder g;
-        g.add(C0.h2, D, L(tc, 1, INW), D, C1.qkv, 3 * D, R, 3 * D, D, E_BIAS, L(tc, 1, INB));
-        TR_CHECK(launch_gemm<L_FWD>(g, st));
+        qkv_pruned(g, C0.h2, L(tc, 1, INW), L(tc, 1, INB), C1.qkv, R, Bm);
+        TR_CHECK(run_gemm<L_FWD>(g, st));
         hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, C1.qkv, p.mask, C1.o, Bm, 1);
         TR_CHECK(check_launch("k_attn_fwd"));
         TR_CHECK(tail_fwd({{&C1, {tc, 1}}}, {C0.h2}));
@@ -1068,30 +914,25 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
             const int tr_ = lt.second.first, ly = lt.second.second;
             const int rows = (&B == &C0) ? R : Bm;
             hipLaunchKernelGGL(k_ln_bwd, dim3(kLnBlocks), dim3(256), 0, st, go[i], B.xhat2, B.rstd2, L(tr_, ly, N2W),
-                               B.df, B.dh1, 1, 0, B.ln2_part, rows);
+                               B.df, nullptr, 1, 0, B.ln2_part, rows);
             TR_CHECK(check_launch("k_ln_bwd"));
             g1.add(B.df, D, L(tr_, ly, L2W), FF, B.du, FF, rows, FF, D, E_RELU_MASK, nullptr, B.u, FF);
-            g2.add(B.du, FF, L(tr_, ly, L1W), D, B.dh1, D, rows, D, FF, E_ACCUM);
+            // dh1 = d(LN2 input) (the residual branch, = df) + W1^T du
+            g2.add_res(B.du, FF, L(tr_, ly, L1W), D, B.dh1, D, rows, D, FF, B.df, D, 0, 0);
             ++i;
         }
-        TR_CHECK(launch_gemm<L_DX>(g1, st));
-        TR_CHECK(launch_gemm<L_DX>(g2, st));
+        TR_CHECK(run_gemm<L_DX>(g1, st));
+        TR_CHECK(run_gemm<L_DX>(g2, st));
         for (auto& lt : layers) {
             const LayerBufs& B = *lt.first;
             const int tr_ = lt.second.first, ly = lt.second.second;
             const int rows = (&B == &C0) ? R : Bm;
-            if (rows != R) {
-                if (hipMemsetAsync(B.dhin, 0, (size_t)R * D * sizeof(float), st) != hipSuccess) {
-                    set_error("hipMemsetAsync failed");
-                    return UAVHIP_EHIP;
-                }
-            }
             hipLaunchKernelGGL(k_ln_bwd, dim3(kLnBlocks), dim3(256), 0, st, B.dh1, B.xhat1, B.rstd1, L(tr_, ly, N1W),
-                               B.dz1, B.dhin, rows == R ? 1 : S, rows == R ? 0 : S - 1, B.ln1_part, rows);
+                               B.dz1, nullptr, 1, 0, B.ln1_part, rows);
             TR_CHECK(check_launch("k_ln_bwd"));
             g3.add(B.dz1, D, L(tr_, ly, OUTW), D, B.dout, D, rows, D, D, E_STORE);
         }
-        TR_CHECK(launch_gemm<L_DX>(g3, st));
+        TR_CHECK(run_gemm<L_DX>(g3, st));
         for (auto& lt : layers) {
             const LayerBufs& B = *lt.first;
             const int tr_ = lt.second.first, ly = lt.second.second;
@@ -1099,9 +940,10 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
             hipLaunchKernelGGL(k_attn_bwd, dim3(Bm * 32 / 256), dim3(256), 0, st, B.qkv, p.mask, B.dout, B.dqkv, Bm,
                                rows == R ? 0 : 1);
             TR_CHECK(check_launch("k_attn_bwd"));
-            g4.add(B.dqkv, 3 * D, L(tr_, ly, INW), D, B.dhin, D, R, D, 3 * D, E_ACCUM);
+            // dh_in = Win^T dqkv + d(LN1 input) on the rows that carried the residual (token 4 if pruned)
+            g4.add_res(B.dqkv, 3 * D, L(tr_, ly, INW), D, B.dhin, D, R, D, 3 * D, B.dz1, D, rows == R ? 0 : S, S - 1);
         }
-        TR_CHECK(launch_gemm<L_DX>(g4, st));
+        TR_CHECK(run_gemm<L_DX>(g4, st));
         return UAVHIP_OK;
     };
     TR_CHECK(tail_bwd({{&C1, {tc, 1}}}, {p.dh_c}));
@@ -1116,22 +958,33 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
         Segment& s = sb.s[sb.n++];
         s.src = src; s.dst = dst; s.count = count; s.parts = parts; s.part_stride = part_stride;
         s.block_begin = seg_blocks;
-        seg_blocks += (count + 255) / 256;
+        s.wave_mode = parts > kWaveModeParts;
+        seg_blocks += s.wave_mode ? (count + 3) / 4 : (count + 255) / 256;
     };
     {
         GemmBuilder g;
         float* ws = p.split_ws;
-        auto dw = [&](const float* dY, int ldy, const float* X, int ldx, int M, int N, int K, int pw, int pb) {
+        // dW[out][in] = sum_rows dY[row][out] X[row][in] into grads at (dst_w, dst_b) float offsets
+        auto dwo = [&](const float* dY, int ldy, const float* X, int ldx, int M, int N, int K, int dst_w, int dst_b) {
             const int sp = splits_for(K);
             float* slab = ws;
             float* bpart = ws + (size_t)sp * M * N;
             ws += (size_t)sp * ((size_t)M * N + M);
             g.add(dY, ldy, X, ldx, slab, N, M, N, K, E_SPLIT, nullptr, nullptr, 0, bpart, kSplitRows);
-            seg(slab, kOffs.o[pw], M * N, sp, M * N);
-            seg(bpart, kOffs.o[pb], M, sp, M);
+            seg(slab, dst_w, M * N, sp, M * N);
+            seg(bpart, dst_b, M, sp, M);
+        };
+        auto dw = [&](const float* dY, int ldy, const float* X, int ldx, int M, int N, int K, int pw, int pb) {
+            dwo(dY, ldy, X, ldx, M, N, K, kOffs.o[pw], kOffs.o[pb]);
         };
         auto layer_dw = [&](const LayerBufs& B, int tr_, int ly, const float* hin, int rows) {
-            dw(B.dqkv, 3 * D, hin, D, 3 * D, D, R, layer_param(tr_, ly, INW), layer_param(tr_, ly, INB));
+            const int pw = kOffs.o[layer_param(tr_, ly, INW)], pb = kOffs.o[layer_param(tr_, ly, INB)];
+            if (rows == R) {
+                dwo(B.dqkv, 3 * D, hin, D, 3 * D, D, R, pw, pb);
+            } else {  // pruned: K/V rows over all R rows, Q rows over the Bm token-4 rows
+                dwo(B.dqkv + D, 3 * D, hin, D, 2 * D, D, R, pw + D * D, pb + D);
+                dwo(B.dqkv + (S - 1) * 3 * D, S * 3 * D, hin + (S - 1) * D, S * D, D, D, Bm, pw, pb);
+            }
             dw(B.dz1, D, B.o, D, D, D, rows, layer_param(tr_, ly, OUTW), layer_param(tr_, ly, OUTB));
             dw(B.du, FF, B.h1, D, FF, D, rows, layer_param(tr_, ly, L1W), layer_param(tr_, ly, L1B));
             dw(B.df, D, B.u, FF, D, FF, rows, layer_param(tr_, ly, L2W), layer_param(tr_, ly, L2B));
@@ -1141,7 +994,7 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
         layer_dw(C1, tc, 1, C0.h2, Bm);
         dw(p.dz_a, HID, A.h2, D, HID, D, Bm, kActorHead, kActorHead + 1);
         dw(p.dz_c, HID, C1.h2, D, HID, D, Bm, kCriticHead, kCriticHead + 1);
-        TR_CHECK(launch_gemm<L_DW>(g, st));
+        TR_CHECK(run_gemm<L_DW>(g, st));
     }
     // LayerNorm weights / biases
     auto ln_seg = [&](const float* part, int pw, int pb) {
