@@ -12,7 +12,9 @@ Also reported (same JSON line):
                 FLOP/sample (last-token-pruned forward) x E per launch / its average
                 HIP-event duration over the timed region
   env_roofline  k_env_step against HBM, algorithmic 24*M + 490 B per env-step
-  ppo_samples_per_s  one update() over the rank's E*T batch (5 epochs, minibatch --ppo-minibatch)
+  ppo_samples_per_s  one PPO update (5 epochs) over the iteration's batch on the HIP training step
+                (uavhip_ppo_step); N > 1: over the all-gathered batch, data parallel (each rank a
+                1/N slice of every global minibatch, RCCL all-reduce of loss sums and gradients)
   cpu_baseline  the CPU port (C oracle env.step + torch-CPU fp32 policy + numpy GAE) on host cores,
                 rank 0 at N = 1 only, bounded sample
 Launch for N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -117,6 +119,61 @@ def cpu_baseline(args, state_dict, seconds):
                       f"policy forward ({cores} threads) + C oracle UAVEnv.step (1 thread) + numpy GAE"}
 
 
+def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
+    """Time one PPO update (5 epochs) over the iteration's trajectories; see the module docstring."""
+    from uavhip.ppo import GraphPPOUpdater, make_optimizer, ppo_epochs
+    tr = eng.traj
+    n = E * T
+    states = tr.obs[:T].reshape(n, 5, 14)
+    acts = tr.actions.reshape(n).long()
+    bufs = (states, acts, tr.logp.reshape(n), tr.values.reshape(n), tr.ret.reshape(n), tr.adv.reshape(n))
+    if world > 1:  # the update runs on the all-gathered batch, data parallel over the ranks
+        from uavhip.dist import unpack_trajectory
+        g = unpack_trajectory(eng.gather())
+        bufs = (g["obs"], g["actions"], g["logp"], g["values"], g["returns"], g["advantages"])
+        n = bufs[0].shape[0]
+    if args.ppo_impl == "torch-eager":
+        opt = make_optimizer(policy)
+        impl = "torch autograd on GPU, eager launches"
+        run = lambda: ppo_epochs(policy, opt, *bufs, batch_size=args.ppo_minibatch)  # noqa: E731
+    elif args.ppo_impl == "torch-graph":
+        opt = make_optimizer(policy, capturable=True)
+        upd = GraphPPOUpdater(policy, opt, *bufs, args.ppo_minibatch)
+        upd.capture()  # once per buffer set (not timed): replays cover every later update
+        impl = "torch autograd on GPU, minibatch step captured in a hipGraph"
+        run = upd.run
+    else:
+        from uavhip.train import FusedPPOTrainer
+        # global minibatch = per-GPU minibatch x world (each rank runs its slice of every step)
+        trainer = FusedPPOTrainer(policy, args.ppo_minibatch * world)
+        trainer.set_buffers(*bufs)
+        if world == 1:
+            trainer.capture()  # once per buffer set (not timed): replays cover every later update
+            impl = "HIP training step (uavhip_ppo_step: grouped fp32 MFMA GEMMs + fused kernels), hipGraph replay"
+        else:
+            impl = ("HIP training step, data parallel: forward / all-reduce loss sums / backward / "
+                    "all-reduce grads (RCCL) / clip+Adam per global minibatch")
+        gen = torch.Generator().manual_seed(1234)  # same minibatch order on every rank
+        run = lambda: trainer.run(generator=gen)  # noqa: E731
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    p0 = time.perf_counter()
+    _, _, _, cnt = run()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    pdt = time.perf_counter() - p0
+    if dist is not None:
+        t = torch.tensor([pdt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        pdt = t.item()
+    return {"value": n / pdt, "unit": "PPO samples/s (whole node: transitions in the update batch / update "
+           "wall time, 5 epochs)", "epochs": 5, "minibatch_per_gpu": args.ppo_minibatch,
+           "global_minibatch": args.ppo_minibatch * world, "optimizer_steps": cnt, "batch": n,
+           "sample_epochs_per_s": n * 5 / pdt, "impl": impl}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,14 +183,19 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # BENCH_DIST_BACKEND=gloo rehearses the N > 1 code path with several ranks on one GPU
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from uavhip.policy import TransformerActorCritic
-    from uavhip.ppo import GraphPPOUpdater, make_optimizer, ppo_epochs
     from uavhip.rollout import RolloutEngine
     from uavhip.vec_env import VecUAVEnv
 
@@ -192,35 +254,11 @@ def main():
 
     ppo = None
     if not args.no_ppo:
-        tr = eng.traj
-        n = E * T
-        states = tr.obs[:T].reshape(n, 5, 14)
-        acts = tr.actions.reshape(n).long()
-        bufs = (states, acts, tr.logp.reshape(n), tr.values.reshape(n), tr.ret.reshape(n), tr.adv.reshape(n))
-        if args.ppo_impl == "torch-eager":
-            opt = make_optimizer(policy)
-            impl = "torch autograd on GPU, eager launches"
-            run = lambda: ppo_epochs(policy, opt, *bufs, batch_size=args.ppo_minibatch)  # noqa: E731
-        elif args.ppo_impl == "torch-graph":
-            opt = make_optimizer(policy, capturable=True)
-            upd = GraphPPOUpdater(policy, opt, *bufs, args.ppo_minibatch)
-            upd.capture()  # once per buffer set (not timed): replays cover every later update
-            impl = "torch autograd on GPU, minibatch step captured in a hipGraph"
-            run = upd.run
-        else:
-            from uavhip.train import FusedPPOTrainer
-            trainer = FusedPPOTrainer(policy, args.ppo_minibatch)
-            trainer.set_buffers(*bufs)
-            trainer.capture()  # once per buffer set (not timed): replays cover every later update
-            impl = "HIP training step (uavhip_ppo_step: grouped fp32 MFMA GEMMs + fused kernels), hipGraph replay"
-            run = trainer.run
-        torch.cuda.synchronize()
-        p0 = time.perf_counter()
-        _, _, _, cnt = run()
-        torch.cuda.synchronize()
-        pdt = time.perf_counter() - p0
-        ppo = {"value": n / pdt, "unit": "PPO samples/s (per GPU)", "epochs": 5, "minibatch": args.ppo_minibatch,
-               "optimizer_steps": cnt, "sample_epochs_per_s": n * 5 / pdt, "impl": impl}
+        try:
+            ppo = ppo_update_rate(args, eng, policy, world, dist, dev, E, T)
+        except Exception as exc:  # the headline rollout line must still print
+            print(f"[bench] PPO update measurement failed: {exc!r}", file=sys.stderr)
+            ppo = {"value": None, "error": repr(exc)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -258,28 +258,41 @@ int uavhip_policy_forward(const uavhip_policy* policy, const float* states, int3
  * parameters can be views of `params`. */
 typedef struct uavhip_ppo {
     float* params;       /* [n_floats] */
-    float* grads;        /* [n_floats] (written; mode 1: raw gradients before clipping) */
+    float* grads;        /* [n_floats] this rank's gradient contribution (written by BACKWARD) */
     float* adam_m;       /* [n_floats] exp_avg */
     float* adam_v;       /* [n_floats] exp_avg_sq */
     double* adam_step;   /* [1] device step counter (shared by all groups) */
     float* workspace;    /* [uavhip_ppo_workspace_floats(minibatch)] */
+    float* loss_sums;    /* [4] written by FORWARD: sums over this rank's samples of min(s1, s2),
+                            (v - R)^2, (v_clip - R)^2, entropy; BACKWARD reads them (all-reduced) */
     double* stats;       /* [4] += loss_actor, loss_critic, entropy, 1 per step (nullable) */
     int32_t n_floats;
-    int32_t minibatch;   /* samples per step, multiple of 64 */
+    int32_t minibatch;   /* samples per step on this rank, multiple of 64 */
+    int32_t global_minibatch; /* samples per step over all ranks (0: = minibatch) */
     float lr_actor, lr_critic, beta1, beta2, adam_eps; /* 2e-4, 1e-3, 0.9, 0.999, 1e-8 */
     float eps_clip, max_grad_norm, value_coef, entropy_coef; /* 0.2, 1.0, 0.5, 0.01 */
 } uavhip_ppo;
+
+/* uavhip_ppo_step phases (bit mask). A data-parallel step over R ranks runs FORWARD,
+ * all-reduces loss_sums (sum), runs BACKWARD (gradients scaled by 1 / global_minibatch, so their
+ * sum over ranks is the global minibatch's gradient), all-reduces grads (sum), runs UPDATE. */
+enum uavhip_ppo_phase {
+    UAVHIP_PPO_FORWARD = 1,
+    UAVHIP_PPO_BACKWARD = 2,
+    UAVHIP_PPO_UPDATE = 4,   /* clip_grad_norm_ on grads + Adam */
+    UAVHIP_PPO_FULL = 7
+};
 
 /* Floats of workspace one step needs at `minibatch` samples. */
 int64_t uavhip_ppo_workspace_floats(int32_t minibatch);
 
 /* Minibatch rows idx[minibatch] (int32, into the trajectory buffers) of states[n][5][14],
- * actions[n] (int8), old_logp / old_values / returns / advantages [n] (f32).
- * mode 0: full step (parameters and Adam moments updated); mode 1: forward + backward only
- * (raw gradients in ppo->grads, loss stats accumulated). */
+ * actions[n] (int8), old_logp / old_values / returns / advantages [n] (f32); `phases` a mask of
+ * uavhip_ppo_phase (UAVHIP_PPO_FULL on one GPU; FORWARD | BACKWARD leaves the raw gradients in
+ * ppo->grads). BACKWARD needs the workspace FORWARD filled for the same rows. */
 int uavhip_ppo_step(const uavhip_ppo* ppo, const float* states, const int8_t* actions, const float* old_logp,
                     const float* old_values, const float* returns, const float* advantages, const int32_t* idx,
-                    int32_t mode, uavhip_stream_t stream);
+                    int32_t phases, uavhip_stream_t stream);
 
 /* ---------------------------------------------------------------- misc */
 const char* uavhip_last_error(void);

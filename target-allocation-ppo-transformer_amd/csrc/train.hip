@@ -294,6 +294,18 @@ __global__ __launch_bounds__(1024) void k_heads_fwd(const HeadArgs a) {
     }
 }
 
+// Sum the per-block loss partials of k_heads_fwd into loss_sums[4] (one wave, fixed order).
+__global__ __launch_bounds__(64) void k_loss_sums(const float* __restrict__ part, int nblk, float* __restrict__ out) {
+    const int l = lane_id();
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = l; i < nblk; i += 64)
+        for (int c = 0; c < 4; ++c) s[c] += part[i * 4 + c];
+    for (int c = 0; c < 4; ++c) {
+        const float w = wave_sum(s[c]);
+        if (l == 0) out[c] = w;
+    }
+}
+
 struct HeadBwdArgs {
     const float* P;
     const float* h_a;
@@ -301,7 +313,7 @@ struct HeadBwdArgs {
     const float* z_a;
     const float* z_c;
     const float* smp;
-    const float* part;  // forward partials [nblk][4]
+    const float* tot;   // [4] loss sums over the global minibatch (loss_sums, all-reduced)
     float* dz_a;        // [Bm][64] d(head.0 pre-activation), relu-masked
     float* dz_c;
     float* dh_a;        // [Bm][128] gradient wrt the actor trunk output (token 4)
@@ -309,7 +321,7 @@ struct HeadBwdArgs {
     float* hpart;       // [nblk][kHeadPart] head.2 weight / bias gradient partials
     double* stats;      // += loss_actor, loss_critic, entropy, 1
     float eps_clip, value_coef, entropy_coef;
-    int Bm;
+    int Bm, Bg;  // samples on this rank / in the global minibatch
 };
 
 // Loss gradients of ppo.py:148-169 per sample (torch's min / max / clamp backward conventions:
@@ -318,23 +330,12 @@ struct HeadBwdArgs {
 __global__ __launch_bounds__(1024) void k_heads_bwd(const HeadBwdArgs a) {
     __shared__ float Wl[HID * kWs];
     __shared__ float dzs[kHeadSamples * HID];
-    __shared__ float tot[4];
     __shared__ float gsm[kHeadSamples][3];  // dlogit0, dlogit1, dvalue
     __shared__ float hp[kHeadSamples][kHeadPart];
     const int p = threadIdx.x >> 6, l = lane_id();
     const int b = blockIdx.x * kHeadSamples + p;
-    const int nblk = a.Bm / kHeadSamples;
-    if (threadIdx.x < 64) {  // reduce the forward partials of every block (same order in all blocks)
-        float s[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int i = l; i < nblk; i += 64)
-            for (int c = 0; c < 4; ++c) s[c] += a.part[i * 4 + c];
-        for (int c = 0; c < 4; ++c) {
-            const float w = wave_sum(s[c]);
-            if (l == 0) tot[c] = w;
-        }
-    }
-    __syncthreads();
-    const float inv = 1.0f / (float)a.Bm;
+    const float tot[4] = {a.tot[0], a.tot[1], a.tot[2], a.tot[3]};
+    const float inv = 1.0f / (float)a.Bg;
     const float L1 = tot[1] * inv, L2 = tot[2] * inv;
     if (l == 0) {
         const float* o = a.smp + (size_t)b * 8;
@@ -579,7 +580,7 @@ struct SegBatch {
     int n;
 };
 __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* __restrict__ grads,
-                                                      float* __restrict__ sq_part, double* __restrict__ step) {
+                                                      float* __restrict__ sq_part) {
     __shared__ float red[4];
     int si = 0;
     while (si + 1 < sb.n && (int)blockIdx.x >= sb.s[si + 1].block_begin) ++si;
@@ -618,8 +619,24 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
     if (lane_id() == 0) red[threadIdx.x >> 6] = sq;
     __syncthreads();
     if (threadIdx.x == 0) sq_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
-    if (step && blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1.0;
 }
+
+// Block partial sums of g^2 over the flat gradient (the norm clip_grad_norm_ needs, taken after
+// any cross-rank all-reduce of grads); block 0 advances Adam's step counter.
+__global__ __launch_bounds__(256) void k_grad_sq(const float* __restrict__ grads, int n, float* __restrict__ sq_part,
+                                                 double* __restrict__ step) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) s += grads[i] * grads[i];
+    s = wave_sum(s);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        sq_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+        if (blockIdx.x == 0) step[0] += 1.0;
+    }
+}
+constexpr int kSqBlocks = 512;
 
 // clip_grad_norm_(max_norm) + torch.optim.Adam (ppo.py:17-22 groups: actor params < critic trunk
 // offset use lr_actor, the rest lr_critic), elementwise over the flat buffers.
@@ -801,18 +818,22 @@ extern "C" int64_t uavhip_ppo_workspace_floats(int32_t minibatch) {
         if (rc_) return rc_; \
     } while (0)
 
+static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int Bg);
+
 extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const int8_t* actions,
                                const float* old_logp, const float* old_values, const float* returns,
-                               const float* advantages, const int32_t* idx, int32_t mode, uavhip_stream_t stream) {
-    if (!c || !c->params || !c->grads || !c->workspace || !states || !actions || !old_logp || !old_values ||
-        !returns || !advantages || !idx) {
+                               const float* advantages, const int32_t* idx, int32_t phases, uavhip_stream_t stream) {
+    const bool fwd = phases & UAVHIP_PPO_FORWARD, bwd = phases & UAVHIP_PPO_BACKWARD, upd = phases & UAVHIP_PPO_UPDATE;
+    if (!c || !c->params || !c->grads || !c->workspace || !c->loss_sums ||
+        ((fwd || bwd) && (!states || !actions || !old_logp || !old_values || !returns || !advantages || !idx))) {
         set_error("uavhip_ppo_step: NULL pointer");
         return UAVHIP_EINVAL;
     }
-    if (c->minibatch <= 0 || c->minibatch % 64 || c->n_floats != kOffs.o[kNumParams] ||
-        (mode == 0 && (!c->adam_m || !c->adam_v || !c->adam_step))) {
-        set_error("uavhip_ppo_step: minibatch %d (multiple of 64), n_floats %d (expected %d), mode %d", c->minibatch,
-                  c->n_floats, kOffs.o[kNumParams], mode);
+    const int Bg = c->global_minibatch > 0 ? c->global_minibatch : c->minibatch;
+    if (c->minibatch <= 0 || c->minibatch % 64 || Bg < c->minibatch || c->n_floats != kOffs.o[kNumParams] ||
+        phases <= 0 || phases > UAVHIP_PPO_FULL || (upd && (!c->adam_m || !c->adam_v || !c->adam_step))) {
+        set_error("uavhip_ppo_step: minibatch %d (multiple of 64), global %d, n_floats %d (expected %d), phases %d",
+                  c->minibatch, Bg, c->n_floats, kOffs.o[kNumParams], phases);
         return UAVHIP_EINVAL;
     }
     hipStream_t st = (hipStream_t)stream;
@@ -821,37 +842,18 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
     const LayerBufs &A = p.la, &C0 = p.lc0, &C1 = p.lc1;
     auto L = [&](int trunk, int layer, int which) { return prm(c, layer_param(trunk, layer, which)); };
     const int ta = kActorTrunk, tc = kCriticTrunk;
-
-    // ---------------------------------------------------------------- forward
-    {
-        EmbedArgs ea{states, idx, c->params, p.xg, p.mask, p.e_a, p.h0_a, p.e_c, p.h0_c, actions, old_logp,
-                     old_values, returns, advantages, p.smp};
-        hipLaunchKernelGGL(k_embed_fwd, dim3(Bm / 16), dim3(256), 0, st, ea);
-        TR_CHECK(check_launch("k_embed_fwd"));
-    }
-    {   // layer 0 QKV of both trunks
-        GemmBuilder g;
-        qkv_pruned(g, p.h0_a, L(ta, 0, INW), L(ta, 0, INB), A.qkv, R, Bm);
-        g.add(p.h0_c, D, L(tc, 0, INW), D, C0.qkv, 3 * D, R, 3 * D, D, E_BIAS, L(tc, 0, INB));
-        TR_CHECK(run_gemm<L_FWD>(g, st));
-    }
-    hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, A.qkv, p.mask, A.o, Bm, 1);
-    hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, C0.qkv, p.mask, C0.o, Bm, 0);
-    TR_CHECK(check_launch("k_attn_fwd"));
     auto tail_fwd = [&](std::initializer_list<std::pair<const LayerBufs*, std::pair<int, int>>> layers,
                         std::initializer_list<const float*> hins) -> int {
         // layers: (buffers, (trunk, layer)); rows = R for the full layer (critic L0), Bm otherwise
         GemmBuilder g1, g2, g3;
-        int i = 0;
         const float* hin_arr[4];
+        int i = 0;
         for (const float* h : hins) hin_arr[i++] = h;
-        i = 0;
         for (auto& lt : layers) {
             const LayerBufs& B = *lt.first;
             const int tr_ = lt.second.first, ly = lt.second.second;
             const int rows = (&B == &C0) ? R : Bm;
             g1.add(B.o, D, L(tr_, ly, OUTW), D, B.a, D, rows, D, D, E_BIAS, L(tr_, ly, OUTB));
-            ++i;
         }
         TR_CHECK(run_gemm<L_FWD>(g1, st));
         i = 0;
@@ -879,24 +881,58 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
         }
         return UAVHIP_OK;
     };
-    TR_CHECK(tail_fwd({{&A, {ta, 0}}, {&C0, {tc, 0}}}, {p.h0_a, p.h0_c}));
-    {   // critic layer 1 (pruned)
+
+    // ---------------------------------------------------------------- forward
+    if (fwd) {
+        EmbedArgs ea{states, idx, c->params, p.xg, p.mask, p.e_a, p.h0_a, p.e_c, p.h0_c, actions, old_logp,
+                     old_values, returns, advantages, p.smp};
+        hipLaunchKernelGGL(k_embed_fwd, dim3(Bm / 16), dim3(256), 0, st, ea);
+        TR_CHECK(check_launch("k_embed_fwd"));
+        // layer 0 QKV of both trunks
         GemmBuilder g;
-        qkv_pruned(g, C0.h2, L(tc, 1, INW), L(tc, 1, INB), C1.qkv, R, Bm);
+        qkv_pruned(g, p.h0_a, L(ta, 0, INW), L(ta, 0, INB), A.qkv, R, Bm);
+        g.add(p.h0_c, D, L(tc, 0, INW), D, C0.qkv, 3 * D, R, 3 * D, D, E_BIAS, L(tc, 0, INB));
         TR_CHECK(run_gemm<L_FWD>(g, st));
+        hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, A.qkv, p.mask, A.o, Bm, 1);
+        hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, C0.qkv, p.mask, C0.o, Bm, 0);
+        TR_CHECK(check_launch("k_attn_fwd"));
+        TR_CHECK(tail_fwd({{&A, {ta, 0}}, {&C0, {tc, 0}}}, {p.h0_a, p.h0_c}));
+        // critic layer 1 (pruned)
+        GemmBuilder g1;
+        qkv_pruned(g1, C0.h2, L(tc, 1, INW), L(tc, 1, INB), C1.qkv, R, Bm);
+        TR_CHECK(run_gemm<L_FWD>(g1, st));
         hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, C1.qkv, p.mask, C1.o, Bm, 1);
         TR_CHECK(check_launch("k_attn_fwd"));
         TR_CHECK(tail_fwd({{&C1, {tc, 1}}}, {C0.h2}));
-    }
-    {
         HeadArgs ha{c->params, A.h2, C1.h2, p.z_a, p.z_c, p.smp, p.fpart, c->eps_clip, Bm};
         hipLaunchKernelGGL(k_heads_fwd, dim3(nblk), dim3(1024), 0, st, ha);
         TR_CHECK(check_launch("k_heads_fwd"));
+        hipLaunchKernelGGL(k_loss_sums, dim3(1), dim3(64), 0, st, p.fpart, nblk, c->loss_sums);
+        TR_CHECK(check_launch("k_loss_sums"));
     }
-    // ---------------------------------------------------------------- backward
+    if (bwd) TR_CHECK(ppo_backward(c, p, st, Bg));
+    if (upd) {
+        hipLaunchKernelGGL(k_grad_sq, dim3(kSqBlocks), dim3(256), 0, st, c->grads, c->n_floats, p.sq_part,
+                           c->adam_step);
+        TR_CHECK(check_launch("k_grad_sq"));
+        AdamArgs aa{c->params, c->grads, c->adam_m, c->adam_v, c->adam_step, p.sq_part, kSqBlocks, c->n_floats,
+                    kOffs.o[kCriticTrunk], c->lr_actor, c->lr_critic, c->beta1, c->beta2, c->adam_eps,
+                    c->max_grad_norm};
+        hipLaunchKernelGGL(k_adam, dim3(512), dim3(256), 0, st, aa);
+        TR_CHECK(check_launch("k_adam"));
+    }
+    return UAVHIP_OK;
+}
+
+// Backward + weight gradients of one minibatch (the workspace holds the forward's activations).
+static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int Bg) {
+    const int Bm = p.Bm, R = p.R, nblk = Bm / kHeadSamples;
+    const LayerBufs &A = p.la, &C0 = p.lc0, &C1 = p.lc1;
+    auto L = [&](int trunk, int layer, int which) { return prm(c, layer_param(trunk, layer, which)); };
+    const int ta = kActorTrunk, tc = kCriticTrunk;
     {
-        HeadBwdArgs hb{c->params, A.h2, C1.h2, p.z_a, p.z_c, p.smp, p.fpart, p.dz_a, p.dz_c, p.dh_a, p.dh_c,
-                       p.hpart, c->stats, c->eps_clip, c->value_coef, c->entropy_coef, Bm};
+        HeadBwdArgs hb{c->params, A.h2, C1.h2, p.z_a, p.z_c, p.smp, c->loss_sums, p.dz_a, p.dz_c, p.dh_a, p.dh_c,
+                       p.hpart, c->stats, c->eps_clip, c->value_coef, c->entropy_coef, Bm, Bg};
         hipLaunchKernelGGL(k_heads_bwd, dim3(nblk), dim3(1024), 0, st, hb);
         TR_CHECK(check_launch("k_heads_bwd"));
     }
@@ -1024,15 +1060,6 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
         return UAVHIP_EINVAL;
     }
     // padding floats between parameters stay zero
-    hipLaunchKernelGGL(k_reduce_grads, dim3(seg_blocks), dim3(256), 0, st, sb, c->grads, p.sq_part,
-                       mode == 0 ? c->adam_step : nullptr);
-    TR_CHECK(check_launch("k_reduce_grads"));
-    if (mode == 0) {
-        AdamArgs aa{c->params, c->grads, c->adam_m, c->adam_v, c->adam_step, p.sq_part, seg_blocks, c->n_floats,
-                    kOffs.o[kCriticTrunk], c->lr_actor, c->lr_critic, c->beta1, c->beta2, c->adam_eps,
-                    c->max_grad_norm};
-        hipLaunchKernelGGL(k_adam, dim3(512), dim3(256), 0, st, aa);
-        TR_CHECK(check_launch("k_adam"));
-    }
-    return UAVHIP_OK;
+    hipLaunchKernelGGL(k_reduce_grads, dim3(seg_blocks), dim3(256), 0, st, sb, c->grads, p.sq_part);
+    return check_launch("k_reduce_grads");
 }

@@ -27,6 +27,7 @@ IST = dict(UAV_IDX=0, TARGET_IDX=1, N_COVERED=2, N_ASSIGNED=3, EPISODE=4, ERROR=
 IST_COUNT = 12
 DST = dict(R=0, J=1, ASG_COST=2, COV_VALUE=3, TOTAL_COST=4, TOTAL_VALUE=5, PD_CUR=6, SUM_PDMG=7, SUM_PFIN=8)
 DST_COUNT = 12
+PPO_FORWARD, PPO_BACKWARD, PPO_UPDATE, PPO_FULL = 1, 2, 4, 7
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -52,7 +53,8 @@ class PolicyDesc(ctypes.Structure):
 class PPODesc(ctypes.Structure):
     """Mirror of `struct uavhip_ppo`."""
     _fields_ = [("params", _vp), ("grads", _vp), ("adam_m", _vp), ("adam_v", _vp), ("adam_step", _vp),
-                ("workspace", _vp), ("stats", _vp), ("n_floats", _i32), ("minibatch", _i32)] + \
+                ("workspace", _vp), ("loss_sums", _vp), ("stats", _vp), ("n_floats", _i32), ("minibatch", _i32),
+                ("global_minibatch", _i32)] + \
               [(n, ctypes.c_float) for n in ("lr_actor", "lr_critic", "beta1", "beta2", "adam_eps", "eps_clip",
                                              "max_grad_norm", "value_coef", "entropy_coef")]
 

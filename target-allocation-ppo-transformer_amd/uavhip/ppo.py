@@ -113,12 +113,16 @@ class PPOAgent:
     """agents/ppo.py:12-184 API: select_action / store_transition / update / clear_buffer,
     attributes device, policy, policy_old, optimizer, buffer, mse_loss."""
 
-    def __init__(self):
+    def __init__(self, fused_update=True):
+        """fused_update: update() runs the HIP training step (uavhip.train.FusedPPOTrainer, its own
+        Adam moments in `self.trainer`); False runs ppo_epochs with torch autograd + self.optimizer."""
         if not torch.cuda.is_available():
             raise RuntimeError("PPOAgent (uavhip) needs an MI355X: the rollout forward is a HIP kernel")
         self.device = torch.device("cuda")
         self.policy = TransformerActorCritic().to(self.device)
         self.optimizer = make_optimizer(self.policy)
+        self.fused_update = bool(fused_update) and cfg.BATCH_SIZE % 64 == 0
+        self.trainer = None
         self.policy_old = TransformerActorCritic().to(self.device)
         self.policy_old.load_state_dict(self.policy.state_dict())
         self.buffer = {"states": [], "actions": [], "logprobs": [], "rewards": [], "is_terminals": [], "values": []}
@@ -148,8 +152,15 @@ class PPOAgent:
         old_states = torch.cat(self.buffer["states"], dim=0)
         old_actions = torch.cat(self.buffer["actions"], dim=0)
         old_logprobs = torch.cat(self.buffer["logprobs"], dim=0)
-        sa, sc, se, cnt = ppo_epochs(self.policy, self.optimizer, old_states, old_actions, old_logprobs,
-                                     values.detach(), returns, advantages)
+        if self.fused_update:
+            from .train import FusedPPOTrainer
+            if self.trainer is None:
+                self.trainer = FusedPPOTrainer(self.policy, cfg.BATCH_SIZE)
+            self.trainer.set_buffers(old_states, old_actions, old_logprobs, values.detach(), returns, advantages)
+            sa, sc, se, cnt = self.trainer.run(use_graph=False)
+        else:
+            sa, sc, se, cnt = ppo_epochs(self.policy, self.optimizer, old_states, old_actions, old_logprobs,
+                                         values.detach(), returns, advantages)
         self.policy_old.load_state_dict(self.policy.state_dict())
         self.clear_buffer()
         if cnt == 0:

@@ -7,6 +7,12 @@ state_dict(), load_state_dict() and the torch `evaluate` path keep working on th
 kernels update. One minibatch step is one C call; `run` captures it once into a hipGraph and
 replays it per minibatch, drawing minibatches like SubsetRandomSampler (torch.randperm of the
 given CPU generator, ppo.py:97-99).
+
+Data parallel (world > 1, every rank holding the same all-gathered buffers and generator seed):
+each rank takes its 1/world slice of every global minibatch; FORWARD, an all-reduce of the four
+loss sums (the clipped value loss picks max(...) over the GLOBAL minibatch), BACKWARD (gradients
+scaled by 1/global minibatch), an all-reduce of the flat gradient (1.68 MB over RCCL/xGMI), then
+the same clip + Adam on every rank: the result is the single-GPU step on the global minibatch.
 """
 import ctypes
 
@@ -20,13 +26,24 @@ from .policy import layout
 
 class FusedPPOTrainer:
     def __init__(self, policy, minibatch, lr_actor=None, lr_critic=None, eps_clip=None, max_grad_norm=None,
-                 value_coef=0.5, entropy_coef=0.01, betas=(0.9, 0.999), adam_eps=1e-8):
-        if minibatch <= 0 or minibatch % 64:
-            raise ValueError("minibatch must be a positive multiple of 64")
+                 value_coef=0.5, entropy_coef=0.01, betas=(0.9, 0.999), adam_eps=1e-8, world=None, rank=None,
+                 group=None, allreduce=None):
+        """minibatch: samples per optimizer step over all ranks (each rank runs minibatch / world).
+        world / rank default to torch.distributed's (1 / 0 when not initialised); allreduce(t)
+        sums a device tensor over the ranks in place (default: torch.distributed.all_reduce)."""
+        import torch.distributed as tdist
+        ddp = tdist.is_available() and tdist.is_initialized()
+        self.world = int(world if world is not None else (tdist.get_world_size(group) if ddp else 1))
+        self.rank = int(rank if rank is not None else (tdist.get_rank(group) if ddp else 0))
+        if minibatch <= 0 or minibatch % (64 * self.world):
+            raise ValueError("minibatch must be a positive multiple of 64 x world")
+        self.allreduce = allreduce or (lambda t: tdist.all_reduce(t, group=group))
         dev = next(policy.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("FusedPPOTrainer runs on the GPU (HIP) only")
-        self.policy, self.minibatch, self.device = policy, int(minibatch), dev
+        self.policy, self.device = policy, dev
+        self.global_minibatch = int(minibatch)
+        self.minibatch = self.global_minibatch // self.world  # rows per rank and step
         offs, n = layout()
         params = list(policy.state_dict(keep_vars=True).values())
         if len(params) != len(offs):
@@ -42,14 +59,15 @@ class FusedPPOTrainer:
         self.adam_v = torch.zeros(n, **f32)
         self.adam_step = torch.zeros(1, dtype=torch.float64, device=dev)
         self.stats = torch.zeros(4, dtype=torch.float64, device=dev)
+        self.loss_sums = torch.zeros(4, **f32)
         ws = LIB.uavhip_ppo_workspace_floats(self.minibatch)
         self.workspace = torch.zeros(int(ws), **f32)
         self.idx = torch.zeros(self.minibatch, dtype=torch.int32, device=dev)
         d = _lib.PPODesc()
         d.params, d.grads = self.params.data_ptr(), self.grads.data_ptr()
         d.adam_m, d.adam_v, d.adam_step = self.adam_m.data_ptr(), self.adam_v.data_ptr(), self.adam_step.data_ptr()
-        d.workspace, d.stats = self.workspace.data_ptr(), self.stats.data_ptr()
-        d.n_floats, d.minibatch = n, self.minibatch
+        d.workspace, d.stats, d.loss_sums = self.workspace.data_ptr(), self.stats.data_ptr(), self.loss_sums.data_ptr()
+        d.n_floats, d.minibatch, d.global_minibatch = n, self.minibatch, self.global_minibatch
         d.lr_actor = cfg.LR_ACTOR if lr_actor is None else lr_actor
         d.lr_critic = cfg.LR_CRITIC if lr_critic is None else lr_critic
         d.beta1, d.beta2, d.adam_eps = betas[0], betas[1], adam_eps
@@ -74,41 +92,55 @@ class FusedPPOTrainer:
         self.n = n
         self.graph = None
 
-    def step(self, mode=0):
-        """One minibatch step on rows self.idx (mode 1: gradients only, no parameter update)."""
+    def step(self, phases=_lib.PPO_FULL):
+        """uavhip_ppo_step phases (bit mask) on this rank's rows self.idx."""
         s, a, lp, v, r, adv = self.bufs
         check(LIB.uavhip_ppo_step(self.desc, ptr(s), ptr(a), ptr(lp), ptr(v), ptr(r), ptr(adv), ptr(self.idx),
-                                  int(mode), stream_handle()), "uavhip_ppo_step")
+                                  int(phases), stream_handle()), "uavhip_ppo_step")
+
+    def ddp_step(self):
+        """One data-parallel optimizer step (see the module docstring)."""
+        self.step(_lib.PPO_FORWARD)
+        self.allreduce(self.loss_sums)
+        self.step(_lib.PPO_BACKWARD)
+        self.allreduce(self.grads)
+        self.step(_lib.PPO_UPDATE)
 
     def gradients(self, idx):
         """Raw gradients (before clipping) of the PPO loss on rows idx, as a flat tensor."""
         self.idx.copy_(torch.as_tensor(idx, dtype=torch.int32, device=self.device))
-        self.step(mode=1)
+        self.step(_lib.PPO_FORWARD | _lib.PPO_BACKWARD)
         return self.grads
 
     def capture(self):
+        if self.world > 1:
+            raise RuntimeError("graph capture is single-GPU; the data-parallel step has collectives between phases")
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, stream=s):
-            self.step(mode=0)
+            self.step(_lib.PPO_FULL)
         torch.cuda.current_stream().wait_stream(s)
 
     def run(self, epochs=None, generator=None, use_graph=True):
         """K epochs of minibatch steps over the buffers -> (mean actor loss, critic loss, entropy, n_steps)."""
         epochs = cfg.K_EPOCHS if epochs is None else epochs
+        use_graph = use_graph and self.world == 1
         if use_graph and self.graph is None:
             self.capture()
         self.stats.zero_()
         cnt = 0
+        Bg, Bl = self.global_minibatch, self.minibatch
         for _ in range(epochs):
             perm = torch.randperm(self.n, generator=generator).to(device=self.device, dtype=torch.int32)
-            for b in range(self.n // self.minibatch):
-                self.idx.copy_(perm[b * self.minibatch:(b + 1) * self.minibatch])
+            for b in range(self.n // Bg):
+                self.idx.copy_(perm[b * Bg + self.rank * Bl:b * Bg + (self.rank + 1) * Bl])
                 if use_graph:
                     self.graph.replay()
+                elif self.world == 1:
+                    self.step(_lib.PPO_FULL)
                 else:
-                    self.step(mode=0)
+                    self.ddp_step()
                 cnt += 1
         self.policy._packed_key = None  # parameters changed under torch's version counters: repack
         if cnt == 0:

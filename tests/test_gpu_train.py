@@ -121,3 +121,42 @@ def test_fused_graph_replay_matches_direct_steps():
     lp_fused = n2.fused_forward(x, actions=bufs[1][:64])[1]
     lp_torch = n2.evaluate(x, bufs[1][:64])[0]
     torch.testing.assert_close(lp_fused, lp_torch.detach(), rtol=1e-4, atol=2e-5)
+
+
+def test_data_parallel_phases_match_single_gpu_step():
+    """Two ranks simulated on one GPU (phases + summed loss_sums / grads in place of the RCCL
+    all-reduces) reproduce the single-GPU step on the global minibatch."""
+    from uavhip import _lib
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.train import FusedPPOTrainer
+    torch.manual_seed(9)
+    base = TransformerActorCritic().cuda()
+    nets = [copy.deepcopy(base) for _ in range(3)]
+    bufs = _buffers(512, seed=12)
+    Bg = 256
+    single = FusedPPOTrainer(nets[0], Bg)
+    ranks = [FusedPPOTrainer(nets[1 + r], Bg, world=2, rank=r, allreduce=lambda t: None) for r in range(2)]
+    for t in [single] + ranks:
+        t.set_buffers(*bufs)
+    perm = torch.randperm(512, generator=torch.Generator().manual_seed(2)).to(torch.int32).cuda()
+    for b in range(2):
+        rows = perm[b * Bg:(b + 1) * Bg]
+        single.idx.copy_(rows)
+        single.step(_lib.PPO_FORWARD | _lib.PPO_BACKWARD)
+        for r, t in enumerate(ranks):
+            t.idx.copy_(rows[r * 128:(r + 1) * 128])
+            t.step(_lib.PPO_FORWARD)
+        tot = ranks[0].loss_sums + ranks[1].loss_sums
+        for t in ranks:
+            t.loss_sums.copy_(tot)
+            t.step(_lib.PPO_BACKWARD)
+        g = ranks[0].grads + ranks[1].grads
+        torch.testing.assert_close(g, single.grads, rtol=1e-4, atol=2e-7)
+        single.step(_lib.PPO_UPDATE)
+        for t in ranks:
+            t.grads.copy_(g)
+            t.step(_lib.PPO_UPDATE)
+    torch.testing.assert_close(ranks[0].params, ranks[1].params, rtol=0, atol=0)
+    d = (ranks[0].params - single.params).abs()
+    assert float(d.max()) <= 0.05 * 2 * 1e-3, float(d.max())  # Adam-normalised: a fraction of lr x steps
+    np.testing.assert_allclose(ranks[0].stats.cpu().numpy(), single.stats.cpu().numpy(), rtol=1e-5)
