@@ -12,6 +12,8 @@ Also reported (same JSON line):
                 FLOP/sample (last-token-pruned forward) x E per launch / its average
                 HIP-event duration over the timed region
   env_roofline  k_env_step against HBM, algorithmic 24*M + 490 B per env-step
+  env_fused     env-only K2 with T = 64 steps per launch (state in registers): BASELINE configs[1]
+                (1024 envs x 8 x 16) and the headline shape, env-steps/s and algorithmic GB/s
   ppo_samples_per_s  one PPO update (5 epochs) over the iteration's batch on the HIP training step
                 (uavhip_ppo_step); N > 1: over the all-gathered batch, data parallel (each rank a
                 1/N slice of every global minibatch, RCCL all-reduce of loss sums and gradients)
@@ -43,7 +45,7 @@ def profiled_traffic(kernel):
     (profiles/rNN_pmc.json, written by scripts/summarize_profile.py from separate rocprofv3
     --pmc FETCH_SIZE / WRITE_SIZE passes of this benchmark; FETCH doubled per the gfx950 note)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")) if "train" not in f)
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -68,6 +70,7 @@ def parse():
     ap.add_argument("--horizon", type=int, default=64)
     ap.add_argument("--ppo-minibatch", type=int, default=4096)
     ap.add_argument("--no-ppo", action="store_true")
+    ap.add_argument("--no-env-fused", action="store_true", help="skip the env-only fused multi-step lines")
     ap.add_argument("--ppo-impl", choices=["fused", "torch-graph", "torch-eager"], default="fused",
                     help="PPO update implementation timed for ppo_samples_per_s")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -117,6 +120,40 @@ def cpu_baseline(args, state_dict, seconds):
     return {"value": steps / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "sample": f"{E} envs x {steps // E} steps of {args.uavs}x{args.targets} ({dt:.1f} s): torch-CPU fp32 "
                       f"policy forward ({cores} threads) + C oracle UAVEnv.step (1 thread) + numpy GAE"}
+
+
+def env_fused_rate(E, N, M, T, dev, reps=5):
+    """Env-only K2 (BASELINE configs[1] shape): one launch steps E envs T times with state in
+    registers (Bernoulli(0.5) actions drawn on device beforehand, auto-reset, obs / reward / done /
+    info written every step). Returns env-steps/s and algorithmic GB/s (SURVEY 8d units)."""
+    from uavhip.vec_env import VecUAVEnv
+    env = VecUAVEnv(E, N, M, 1, 1, seed=77, full_reset_period=200)
+    env.generate_scenes()
+    env.reset(episode=1)
+    g = torch.Generator(device=dev).manual_seed(5)
+    acts = torch.randint(0, 2, (T, E), generator=g, device=dev, dtype=torch.int8)
+    obs = torch.empty(T, E, 5, 14, device=dev)
+    rew = torch.empty(T, E, dtype=torch.float64, device=dev)
+    done = torch.empty(T, E, dtype=torch.uint8, device=dev)
+    info = torch.empty(T, E, 8, dtype=torch.float64, device=dev)
+    for _ in range(2):
+        env.step(acts, obs_out=obs, reward_out=rew, done_out=done, info_out=info)
+        env.refresh_scenes()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ms = []
+    for _ in range(reps):
+        e0.record()
+        env.step(acts, obs_out=obs, reward_out=rew, done_out=done, info_out=info)
+        e1.record()
+        env.refresh_scenes()
+        torch.cuda.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    t = float(np.median(ms)) * 1e-3
+    rate = E * T / t
+    gbs = env_bytes_per_step(M) * rate / 1e9
+    return {"workload": f"{E} envs x {N} UAV x {M} tgt, {T} fused steps per launch", "value": rate,
+            "unit": "env-steps/s", "ms_per_launch": t * 1e3, "achieved": gbs, "peak": HBM_PEAK_GBS,
+            "unit_roofline": "GB/s (algorithmic 24*M + 490 B per env-step)", "frac": gbs / HBM_PEAK_GBS}
 
 
 def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
@@ -252,6 +289,10 @@ def main():
     achieved_tf = POLICY_FLOP_PER_SAMPLE * E / (pol_ms * 1e-3) / 1e12
     env_gbs = env_bytes_per_step(args.targets) * E / (env_ms * 1e-3) / 1e9
 
+    env_fused = None
+    if rank == 0 and world == 1 and not args.no_env_fused:
+        env_fused = [env_fused_rate(1024, 8, 16, 64, dev), env_fused_rate(E, args.uavs, args.targets, 64, dev)]
+
     ppo = None
     if not args.no_ppo:
         try:
@@ -287,6 +328,7 @@ def main():
                              "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS, "avg_launch_ms": env_ms,
                              "traffic": env_traffic,
                              "bytes_per_env_step": env_bytes_per_step(args.targets)},
+            "env_fused": env_fused,
             "ppo_samples_per_s": ppo,
             "cpu_baseline": cpu,
         }

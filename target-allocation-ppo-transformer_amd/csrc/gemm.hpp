@@ -93,13 +93,28 @@ __device__ __forceinline__ TileInfo decode_tile(const GemmBatch& gb, int tile) {
     int pi = 0;
     while (pi + 1 < gb.n && tile >= gb.p[pi + 1].tile_begin) ++pi;
     const GemmProb& P = gb.p[pi];
-    int t = tile - P.tile_begin;
-    const int per_split = (P.M / BM) * P.tiles_n;
+    const int u = tile - P.tile_begin;
+    const int tm_n = P.M / BM, tn_n = P.tiles_n, per_split = tm_n * tn_n;
     ti.pi = pi;
-    ti.split = t / per_split;
-    t -= ti.split * per_split;
-    const int tmi = t / P.tiles_n;
-    ti.tni = t - tmi * P.tiles_n;
+    // XCD-aware order (workgroup b runs on XCD b % 8, the persistent grid is a multiple of 8, so
+    // tile u lands on XCD (tile_begin + u) % 8): the tiles that read the same operand slabs share
+    // an XCD and its L2 -- all tiles of one K-split (split-K), or all column tiles of one row
+    // block (the A slab). Groups of 8 splits / row blocks interleave over the 8 XCDs.
+    int tmi;
+    if (P.splits > 1) {
+        const int g = u / (8 * per_split), r = u - g * 8 * per_split;
+        const int gsz = min(8, P.splits - 8 * g);
+        ti.split = 8 * g + r % gsz;
+        const int j = r / gsz;
+        tmi = j / tn_n;
+        ti.tni = j - tmi * tn_n;
+    } else {
+        const int g = u / (8 * tn_n), r = u - g * 8 * tn_n;
+        const int gsz = min(8, tm_n - 8 * g);
+        ti.split = 0;
+        tmi = 8 * g + r % gsz;
+        ti.tni = r / gsz;
+    }
     ti.m0 = tmi * BM;
     ti.n0 = ti.tni * BN;
     ti.kb = ti.split * P.kchunk;
