@@ -68,6 +68,12 @@ class TransformerActorCritic(nn.Module):
     def forward(self, state):
         raise NotImplementedError("Please use get_action or evaluate.")
 
+    def __getstate__(self):
+        # the packed-weight cache and its ctypes descriptor are per-instance device state
+        state = self.__dict__.copy()
+        state["_packed"] = state["_packed_key"] = state["_desc"] = None
+        return state
+
     # ------------------------------------------------------------------ torch path
     def heads(self, state):
         """-> logits [B, 2], value [B, 1] via the torch modules (autograd-capable)."""
