@@ -294,6 +294,34 @@ int uavhip_ppo_step(const uavhip_ppo* ppo, const float* states, const int8_t* ac
                     const float* old_values, const float* returns, const float* advantages, const int32_t* idx,
                     int32_t phases, uavhip_stream_t stream);
 
+/* ---------------------------------------------------------------- episode metrics */
+
+/* Per-episode sums main_train.py logs (:122-136, :161-195), one record per finished episode. */
+enum uavhip_ep {
+    UAVHIP_EP_ENV = 0,       /* env index                                              */
+    UAVHIP_EP_EPISODE,       /* info EPISODE of the finishing step                     */
+    UAVHIP_EP_STEPS,         /* ep_steps                                               */
+    UAVHIP_EP_REWARD,        /* current_ep_reward (sum of rewards)                     */
+    UAVHIP_EP_Q0,            /* value of the episode's first state (current_q0)        */
+    UAVHIP_EP_J_SUM,         /* ep_total_J (sum of info J_val)                         */
+    UAVHIP_EP_MAX_COV,       /* ep_max_cov (max num_assigned)                          */
+    UAVHIP_EP_ACTION1,       /* ep_action1_cnt                                         */
+    UAVHIP_EP_VALID,         /* ep_valid_cnt (action 1 and is_valid_action)            */
+    UAVHIP_EP_PDMG_SUM,      /* ep_total_p_dmg (steps with num_assigned > 0)           */
+    UAVHIP_EP_PFINAL_SUM,    /* ep_total_p_final                                       */
+    UAVHIP_EP_ASSIGN_STEPS,  /* ep_steps_with_assign                                   */
+    UAVHIP_EP_COUNT
+};
+
+/* Walk a [T][E] rollout chunk (reward f64, done u8, action i8, info [T][E][UAVHIP_INFO_COUNT],
+ * value f32 = V(obs[t])) per env in time order, continuing the episodes in acc[E][UAVHIP_EP_COUNT]
+ * (zero-initialised once; carries unfinished episodes across chunks). Every finished episode is
+ * appended to records[max_records][UAVHIP_EP_COUNT] at slot atomicAdd(n_records, 1) (slots past
+ * max_records are counted but dropped). Sums run in step order in fp64, as the reference's. */
+int uavhip_episode_stats(const double* reward, const uint8_t* done, const int8_t* action, const double* info,
+                         const float* value, int32_t T, int32_t E, double* acc, double* records,
+                         int32_t max_records, uint32_t* n_records, uavhip_stream_t stream);
+
 /* ---------------------------------------------------------------- misc */
 const char* uavhip_last_error(void);
 int32_t uavhip_abi_version(void);

@@ -6,6 +6,7 @@
 #include <vector>
 #include <cmath>
 #include "../../target-allocation-ppo-transformer_amd/csrc/gemm.hpp"
+#include "../../target-allocation-ppo-transformer_amd/csrc/rowgemm.hpp"
 
 using namespace uavhip::tr;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -144,6 +145,85 @@ int main() {
         printf("bm=%3d DW  9 probs  (split-K %d): %7.1f us  %6.1f TF/s  tiles %d\n", bm, kc, us, flops(g) / us / 1e6, g.tiles);
         check<L_DW>("dw", g.gb.p[0]);
     }
+    }
+    // ---- weights-resident row GEMM
+    auto rtime = [&](const RowBuilder& g, int grid) {
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+        for (int i = 0; i < 3; ++i) launch_rowgemm(g, 0, grid);
+        CK(hipEventRecord(e0));
+        for (int i = 0; i < 20; ++i) launch_rowgemm(g, 0, grid);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+        CK(hipGetLastError());
+        return ms * 1e3 / 20;
+    };
+    auto rflops = [&](const RowBuilder& g) {
+        double f = 0;
+        for (int i = 0; i < g.rb.n; ++i) f += 2.0 * g.rb.p[i].M * g.rb.p[i].N * g.rb.p[i].K;
+        return f;
+    };
+    float* xh = dalloc((size_t)R * D);
+    float* rsd = dalloc(R);
+    float* lnw = dalloc(D);
+    for (int grid : {256, 512}) {
+        {
+            RowBuilder g; g.K = 128;
+            RowProb p{}; p.A = h; p.lda = D; p.B = win; p.ldb = D; p.C = qkv; p.ldc = 3 * D; p.bias = bias;
+            p.M = R; p.N = 3 * D; p.K = D; p.epi = R_BIAS; g.add(p);
+            RowProb q = p; q.A = h2; q.B = win2; q.C = qkv2; g.add(q);
+            const double us = rtime(g, grid);
+            printf("grid %d ROW FWD qkv x2 (M=%d N=384 K=128): %7.1f us %6.1f TF/s valid %d\n", grid, R, us, rflops(g) / us / 1e6, (int)g.valid());
+            if (grid == 256) {
+                GemmProb c{}; c.A = h; c.lda = D; c.B = win; c.ldb = D; c.C = qkv; c.ldc = 3 * D; c.M = R; c.N = 3 * D; c.K = D; c.epi = E_STORE;
+                // recompute with bias-free store for the check
+                RowBuilder g2; g2.K = 128; RowProb p2 = p; p2.epi = R_STORE; g2.add(p2); launch_rowgemm(g2, 0, grid); CK(hipDeviceSynchronize());
+                check<L_FWD>("row fwd", c);
+            }
+        }
+        {
+            RowBuilder g; g.K = 128;
+            RowProb p{}; p.A = f; p.lda = D; p.B = win; p.ldb = D; p.C = dh; p.ldc = D; p.bias = bias; p.aux = h; p.ldaux = D;
+            p.lnw = lnw; p.lnb = bias; p.xhat = xh; p.rstd = rsd; p.rmod = 1; p.rrem = 0;
+            p.M = R; p.N = D; p.K = D; p.epi = R_BIAS_RES_LN; g.add(p);
+            const double us = rtime(g, grid);
+            printf("grid %d ROW FWD out+LN (M=%d N=128 K=128): %7.1f us %6.1f TF/s\n", grid, R, us, rflops(g) / us / 1e6);
+        }
+        {
+            RowBuilder g; g.K = 128;
+            RowProb p{}; p.A = h; p.lda = D; p.B = w1; p.ldb = D; p.C = u; p.ldc = FF; p.bias = bias;
+            p.M = R; p.N = FF; p.K = D; p.epi = R_BIAS_RELU; g.add(p);
+            const double us = rtime(g, grid);
+            printf("grid %d ROW FWD ffn1 (M=%d N=256 K=128): %7.1f us %6.1f TF/s\n", grid, R, us, rflops(g) / us / 1e6);
+        }
+        {
+            RowBuilder g; g.K = 256;
+            RowProb p{}; p.A = u; p.lda = FF; p.B = w2; p.ldb = FF; p.C = f; p.ldc = D; p.bias = bias; p.aux = h; p.ldaux = D;
+            p.lnw = lnw; p.lnb = bias; p.xhat = xh; p.rstd = rsd; p.rmod = 1; p.rrem = 0;
+            p.M = R; p.N = D; p.K = FF; p.epi = R_BIAS_RES_LN; g.add(p);
+            const double us = rtime(g, grid);
+            printf("grid %d ROW FWD ffn2+LN (M=%d N=128 K=256): %7.1f us %6.1f TF/s\n", grid, R, us, rflops(g) / us / 1e6);
+        }
+        {
+            RowBuilder g; g.K = 128; g.rb.bt = 1;
+            RowProb p{}; p.A = f; p.lda = D; p.B = w2; p.ldb = FF; p.C = u; p.ldc = FF; p.aux = u; p.ldaux = FF;
+            p.M = R; p.N = FF; p.K = D; p.epi = R_RELU_MASK; g.add(p);
+            const double us = rtime(g, grid);
+            printf("grid %d ROW DX w2 relu (M=%d N=256 K=128): %7.1f us %6.1f TF/s\n", grid, R, us, rflops(g) / us / 1e6);
+            if (grid == 256) {
+                RowBuilder g2; g2.K = 128; g2.rb.bt = 1; RowProb p2 = p; p2.epi = R_STORE; g2.add(p2); launch_rowgemm(g2, 0, grid); CK(hipDeviceSynchronize());
+                GemmProb c{}; c.A = f; c.lda = D; c.B = w2; c.ldb = FF; c.C = u; c.ldc = FF; c.M = R; c.N = FF; c.K = D; c.epi = E_STORE;
+                check<L_DX>("row dx", c);
+            }
+        }
+        {
+            RowBuilder g; g.K = 256; g.rb.bt = 1;
+            RowProb p{}; p.A = u; p.lda = FF; p.B = w1; p.ldb = D; p.C = dh; p.ldc = D; p.aux = f; p.ldaux = D;
+            p.M = R; p.N = D; p.K = FF; p.epi = R_ADD_RES; g.add(p);
+            const double us = rtime(g, grid);
+            printf("grid %d ROW DX w1 +res (M=%d N=128 K=256): %7.1f us %6.1f TF/s\n", grid, R, us, rflops(g) / us / 1e6);
+        }
     }
     return 0;
 }

@@ -28,6 +28,9 @@ IST_COUNT = 12
 DST = dict(R=0, J=1, ASG_COST=2, COV_VALUE=3, TOTAL_COST=4, TOTAL_VALUE=5, PD_CUR=6, SUM_PDMG=7, SUM_PFIN=8)
 DST_COUNT = 12
 PPO_FORWARD, PPO_BACKWARD, PPO_UPDATE, PPO_FULL = 1, 2, 4, 7
+EP = dict(ENV=0, EPISODE=1, STEPS=2, REWARD=3, Q0=4, J_SUM=5, MAX_COV=6, ACTION1=7, VALID=8, PDMG_SUM=9,
+          PFINAL_SUM=10, ASSIGN_STEPS=11)
+EP_COUNT = 12
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -77,6 +80,7 @@ _SIGS = {
                                              ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "uavhip_ppo_workspace_floats": (ctypes.c_int64, [_i32]),
     "uavhip_ppo_step": (ctypes.c_int, [ctypes.POINTER(PPODesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
+    "uavhip_episode_stats": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _i32, _vp, _vp]),
     "uavhip_last_error": (ctypes.c_char_p, []),
     "uavhip_abi_version": (_i32, []),
 }

@@ -188,3 +188,19 @@ def test_product_refuses_cpu():
         PPOAgent()
     with pytest.raises(RuntimeError):
         TransformerActorCritic().get_action(torch.zeros(1, 5, 14))
+
+
+def test_csv_rows_follow_main_train_columns():
+    """metrics.csv_rows: main_train.py:56-61 columns, :165-173 ratios (denominators clamped to 1)."""
+    from uavhip import _lib
+    from uavhip.metrics import CSV_HEADER, csv_rows
+    E = _lib.EP
+    rec = np.zeros((2, _lib.EP_COUNT))
+    rec[0, [E["STEPS"], E["REWARD"], E["Q0"], E["J_SUM"], E["MAX_COV"], E["ACTION1"], E["VALID"]]] = [4, 2.0, 0.5, 8.0, 3, 2, 1]
+    rec[0, [E["PDMG_SUM"], E["PFINAL_SUM"], E["ASSIGN_STEPS"]]] = [1.2, 0.6, 3]
+    rec[1, [E["STEPS"], E["REWARD"], E["Q0"]]] = [1, 4.0, 1.5]          # no assigns, no action 1
+    rows = csv_rows(rec, losses=(0.25, -0.5, 0.69))
+    assert len(CSV_HEADER) == 12
+    assert rows[0][:9] == [1, "2.0000", "0.5000", "2.0000", 3, "0.5000", "0.5000", "0.4000", "0.2000"]
+    assert rows[1][:9] == [2, "3.0000", "1.0000", "0.0000", 0, "0.0000", "0.0000", "0.0000", "0.0000"]
+    assert rows[1][9:] == ["0.250000", "-0.500000", "0.690000"]
