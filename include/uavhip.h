@@ -232,6 +232,10 @@ typedef struct uavhip_policy {
  * (see policy.py). Returns the total number of floats; offsets may be NULL. */
 int32_t uavhip_policy_layout(int32_t* offsets, int32_t max_offsets);
 
+/* flat (state_dict order, uavhip_policy_layout offsets, every parameter row-major) -> packed
+ * (the same with the uavhip_policy_tiling weights in MFMA fragment order), on the device. */
+int uavhip_policy_pack(const float* flat, float* packed, uavhip_stream_t stream);
+
 /* Per parameter (state_dict key order): the in-features K of the weight matrices stored in MFMA
  * fragment order, 0 for parameters stored flat. An [R][K] matrix W in fragment order puts
  * W[r][k] at ((r/16 * K/16 + k/16) * 64 + r%16 + 16 * ((k%16)/4)) * 4 + k%4, so each 16 x 16

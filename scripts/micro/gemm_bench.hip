@@ -6,7 +6,7 @@
 #include <vector>
 #include <cmath>
 #include "../../target-allocation-ppo-transformer_amd/csrc/gemm.hpp"
-#include "../../target-allocation-ppo-transformer_amd/csrc/rowgemm.hpp"
+#include "rowgemm.hpp"
 
 using namespace uavhip::tr;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)

@@ -22,6 +22,7 @@
 //    parity is defined on logits / logp / value / entropy for given actions).
 #include "common.hpp"
 #include "policy_layout.hpp"
+#include "policy_train.hpp"
 
 namespace uavhip {
 namespace pol {
@@ -187,9 +188,21 @@ __device__ __forceinline__ float add_xor32(float v) {
 // for this wave's 16 output features f = [16 wv, 16 wv + 16) of CT column tiles from ytok0. The
 // token statistics combine per-wave (mean, M2) pairs over 16 features each (Chan et al.), so one
 // barrier suffices and the variance is two-pass accurate. Ends WITHOUT a barrier after writing h.
-template <int CT>
+// Training-mode outputs of a LayerNorm: normalised rows, output rows, 1/std per row, in the
+// workspace layout (compact [b] rows for the pruned tail, [b * 5 + s] rows otherwise).
+struct LnOut {
+    float *x, *h, *rs;
+    int b0, compact;
+};
+__device__ __forceinline__ int trow(int tok, int b0) { return (b0 + (tok & (SPW - 1))) * S + tok / SPW; }
+__device__ __forceinline__ int orow(int tok, int b0, bool compact) {
+    return compact ? b0 + (tok & (SPW - 1)) : trow(tok, b0);
+}
+
+template <int CT, bool TR = false>
 __device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[CT], const float* __restrict__ bias,
-                                                   const float* __restrict__ w, const float* __restrict__ b, int ytok0) {
+                                                   const float* __restrict__ w, const float* __restrict__ b, int ytok0,
+                                                   const LnOut& lo = LnOut{}) {
     const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
     const int f0 = 16 * wv + 4 * g;
     const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + f0);
@@ -227,7 +240,27 @@ __device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[
             m2 += pr[k].y + 16.0f * dm * dm;
         }
         const float rs = 1.0f / sqrtf(m2 * (1.0f / D) + 1e-5f);
-        *reinterpret_cast<f32x4*>(sm.h + tok * LDH + f0) = (v[ct] - mean) * rs * ww + lb;
+        const f32x4 xh = (v[ct] - mean) * rs;
+        const f32x4 out = xh * ww + lb;
+        *reinterpret_cast<f32x4*>(sm.h + tok * LDH + f0) = out;
+        if (TR) {
+            const size_t r = (size_t)orow(tok, lo.b0, lo.compact);
+            *reinterpret_cast<f32x4*>(lo.x + r * D + f0) = xh;
+            *reinterpret_cast<f32x4*>(lo.h + r * D + f0) = out;
+            if (wv == 0 && g == 0) lo.rs[r] = rs;
+        }
+    }
+}
+
+// Training mode: copy [tok][cols] rows from LDS (stride lds) to workspace rows (stride ldo, column
+// offset c0) for tokens [t0, TOK), all 512 threads, float4 granules.
+__device__ __forceinline__ void store_rows(const float* src, int lds, float* dst, int ldo, int c0, int ncols, int t0,
+                                           int b0, bool compact) {
+    const int n4 = ncols / 4, items = (TOK - t0) * n4;
+    for (int i = threadIdx.x; i < items; i += NTHR) {
+        const int tok = t0 + i / n4, q = i % n4;
+        *reinterpret_cast<f32x4*>(dst + (size_t)orow(tok, b0, compact) * ldo + c0 + 4 * q) =
+            *reinterpret_cast<const f32x4*>(src + tok * lds + 4 * q);
     }
 }
 
@@ -317,8 +350,9 @@ __device__ void attention_chunk(Smem& sm, int c, int qs0, int nqs) {
 
 // Embedding (transformer_net.py:57-59) on the MFMA, K = 14 padded to 16 with zeros:
 // h[s*16+p][f] = relu(W_e x[p][s] + b_e)[f] + pos[s][f]; wave w computes features [16w, 16w+16).
-template <int trunk>
-__device__ void embed(Smem& sm, const float* __restrict__ P) {
+template <int trunk, bool TR = false>
+__device__ void embed(Smem& sm, const float* __restrict__ P, float* e_out = nullptr, float* h_out = nullptr,
+                      int b0 = 0) {
     const float* We = P + kOffs.o[trunk + EMB_W];
     const float* be = P + kOffs.o[trunk + EMB_B];
     const float* pos = P + kOffs.o[trunk + POS];
@@ -341,10 +375,15 @@ __device__ void embed(Smem& sm, const float* __restrict__ P) {
 #pragma unroll
     for (int ct = 0; ct < S; ++ct) {
         const f32x4 pp = *reinterpret_cast<const f32x4*>(pos + ct * D + 16 * wv + 4 * g);
-        f32x4 v = acc[ct] + bb;
-        v.x = fmaxf(v.x, 0.f) + pp.x; v.y = fmaxf(v.y, 0.f) + pp.y;
-        v.z = fmaxf(v.z, 0.f) + pp.z; v.w = fmaxf(v.w, 0.f) + pp.w;
+        f32x4 e = acc[ct] + bb;
+        e.x = fmaxf(e.x, 0.f); e.y = fmaxf(e.y, 0.f); e.z = fmaxf(e.z, 0.f); e.w = fmaxf(e.w, 0.f);
+        const f32x4 v = e + pp;
         *reinterpret_cast<f32x4*>(sm.h + (ct * SPW + i16) * LDH + 16 * wv + 4 * g) = v;
+        if (TR) {
+            const size_t r = (size_t)trow(ct * SPW + i16, b0);
+            *reinterpret_cast<f32x4*>(e_out + r * D + 16 * wv + 4 * g) = e;
+            *reinterpret_cast<f32x4*>(h_out + r * D + 16 * wv + 4 * g) = v;
+        }
     }
 }
 
@@ -355,8 +394,9 @@ __device__ __forceinline__ int kv_row(int wv, int c) { return (1 + (wv >> 2)) * 
 // Work split: 8 waves, wave w and w+4 share a SIMD (and its MFMA pipe); every GEMM gives each
 // SIMD the same number of 16-row output tiles. `pkv` = the caller's prefetch of this layer's first
 // K/V weight blocks. Ends WITHOUT a final barrier: the caller prefetches its next weights, then syncs.
-template <int trunk, int layer, bool last>
-__device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv) {
+template <int trunk, int layer, bool last, bool TR = false>
+__device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv,
+                              const TrainLayerIO& io = TrainLayerIO{}, int b0 = 0) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
     PTR(tb);
     const float* Win = P + kOffs.o[layer_param(trunk, layer, INW)];
@@ -386,11 +426,20 @@ __device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv
         PTR(tb + 1 + 3 * c);
         __syncthreads();
         PTR(tb + 2 + 3 * c);
+        if (TR) {  // this chunk's Q (query tokens) / K / V -> qkv[row][part * 128 + 64 c + d]
+            for (int i = threadIdx.x; i < TOK * 48; i += NTHR) {
+                const int tok = i / 48, r = i - tok * 48, part = r >> 4, q = r & 15;
+                if (part == 0 && tok < qtok0) continue;
+                *reinterpret_cast<f32x4*>(io.qkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q) =
+                    *reinterpret_cast<const f32x4*>(sm.big + tok * LDB + part * 64 + 4 * q);
+            }
+        }
         if (last) attention_chunk(sm, c, S - 1, 1);
         else attention_full(sm, c);
         __syncthreads();
         PTR(tb + 3 + 3 * c);
     }
+    if (TR) store_rows(sm.ctx, LDH, io.o, D, 0, D, qtok0, b0, last);  // attention output
     // out projection, h = LN1(h + attn) in its epilogue
     APre<DQ> pf1a, pf1b;
     {
@@ -400,8 +449,9 @@ __device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv
         PTR(tb + 7);
         pf1a = prefetch<DQ>(W1, D, 16 * wv, 0);
         pf1b = prefetch<DQ>(W1, D, 128 + 16 * wv, 0);
-        residual_layernorm<CTQ>(sm, acc, bo, P + kOffs.o[layer_param(trunk, layer, N1W)],
-                                P + kOffs.o[layer_param(trunk, layer, N1B)], qtok0);
+        residual_layernorm<CTQ, TR>(sm, acc, bo, P + kOffs.o[layer_param(trunk, layer, N1W)],
+                                    P + kOffs.o[layer_param(trunk, layer, N1B)], qtok0,
+                                    LnOut{io.xhat1, io.h1, io.rstd1, b0, last});
     }
     PTR(tb + 8);
     __syncthreads();
@@ -413,14 +463,19 @@ __device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv
     PTR(tb + 10);
     __syncthreads();
     PTR(tb + 11);
+    if (TR) {  // FFN hidden (post-ReLU): features 0-127 in big, 128-255 in ctx
+        store_rows(sm.big, LDF, io.u, FF, 0, D, qtok0, b0, last);
+        store_rows(sm.ctx, LDF, io.u, FF, D, D, qtok0, b0, last);
+    }
     f32x4 acc2[CTQ];
     zero(acc2);
     const APre<DQ> pf2b = prefetch<DQ>(W2, FF, 16 * wv, 128);
     gemm_tile<CTQ, DQ>(acc2, pf2a, W2, FF, 16 * wv, 0, sm.big, LDF, qtok0);
     gemm_tile<CTQ, DQ>(acc2, pf2b, W2, FF, 16 * wv, 128, sm.ctx, LDF, qtok0);
     PTR(tb + 12);
-    residual_layernorm<CTQ>(sm, acc2, b2, P + kOffs.o[layer_param(trunk, layer, N2W)],
-                            P + kOffs.o[layer_param(trunk, layer, N2B)], qtok0);
+    residual_layernorm<CTQ, TR>(sm, acc2, b2, P + kOffs.o[layer_param(trunk, layer, N2W)],
+                                P + kOffs.o[layer_param(trunk, layer, N2B)], qtok0,
+                                LnOut{io.xhat2, io.h2, io.rstd2, b0, last});
     PTR(tb + 14);
 }
 
@@ -444,19 +499,35 @@ __device__ void head_mlp(Smem& sm, const float* __restrict__ P, const APre<4>& p
     __syncthreads();
 }
 
+template <bool TR>
 __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict__ P, const float* __restrict__ states,
                                                          int B, const int8_t* __restrict__ actions_in, uint64_t seed,
                                                          uint64_t offset, const uint64_t* __restrict__ offset_dev,
                                                          int8_t* __restrict__ action_out,
                                                          float* __restrict__ logp_out, float* __restrict__ value_out,
-                                                         float* __restrict__ ent_out, float* __restrict__ logits_out) {
+                                                         float* __restrict__ ent_out, float* __restrict__ logits_out,
+                                                         const TrainIO io) {
     __shared__ __attribute__((aligned(16))) Smem sm;
     const int b0 = blockIdx.x * SPW;
     PTR(0);
-    // windows -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch tail zero-filled)
+    // windows -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch tail zero-filled);
+    // training mode gathers minibatch row idx[b] of the trajectory buffer
     for (int i = threadIdx.x; i < TOK * LDX; i += NTHR) {
         const int t = i / LDX, k = i - t * LDX, s = t / SPW, p = t - s * SPW;
-        sm.x[i] = (k < IN && b0 + p < B) ? states[((size_t)(b0 + p) * S + s) * IN + k] : 0.f;
+        const size_t src = TR ? (size_t)io.idx[b0 + p] : (size_t)(b0 + p);
+        const float v = (k < IN && b0 + p < B) ? states[(src * S + s) * IN + k] : 0.f;
+        sm.x[i] = v;
+        if (TR) io.xg[(size_t)trow(t, b0) * 16 + k] = v;
+    }
+    if (TR && threadIdx.x < SPW) {  // per-sample loss inputs
+        const int b = b0 + threadIdx.x;
+        const size_t src = (size_t)io.idx[b];
+        float* o = io.smp + (size_t)b * 8;
+        o[0] = (float)(io.act_in[src] != 0);
+        o[1] = io.oldlp_in[src];
+        o[2] = io.oldv_in[src];
+        o[3] = io.ret_in[src];
+        o[4] = io.adv_in[src];
     }
     __syncthreads();
     if (threadIdx.x < SPW * S) {  // key padding mask: all-zero rows, last row never masked
@@ -464,31 +535,33 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         bool z = true;
         for (int k = 0; k < IN; ++k) z = z && (sm.x[(s * SPW + p) * LDX + k] == 0.f);
         sm.mask[p * S + s] = (s < S - 1) && z;
+        if (TR) io.mask[(size_t)(b0 + p) * S + s] = ((s < S - 1) && z) ? 1.f : 0.f;
     }
     PTR(1);
     const int wv = threadIdx.x >> 6;
     const float* headw_a = P + kOffs.o[kActorHead];
     const float* headw_c = P + kOffs.o[kCriticHead];
     // actor trunk (1 layer) + head
-    embed<kActorTrunk>(sm, P);
+    embed<kActorTrunk, TR>(sm, P, io.e[0], io.h0[0], b0);
     PTR(2);
     APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
     __syncthreads();
-    encoder_layer<kActorTrunk, 0, true>(sm, P, pkv);
+    encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0);
     APre<4> ph;
-    if (wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
+    if (!TR && wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
     __syncthreads();
     PTR(3);
-    head_mlp<kActorHead, 2>(sm, P, ph, sm.logits);
+    if (!TR) head_mlp<kActorHead, 2>(sm, P, ph, sm.logits);
     PTR(4);
     // critic trunk (2 layers) + head
-    embed<kCriticTrunk>(sm, P);
+    embed<kCriticTrunk, TR>(sm, P, io.e[1], io.h0[1], b0);
     pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
     __syncthreads();
-    encoder_layer<kCriticTrunk, 0, false>(sm, P, pkv);
+    encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv, io.L[1], b0);
     pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
     __syncthreads();
-    encoder_layer<kCriticTrunk, 1, true>(sm, P, pkv);
+    encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0);
+    if (TR) return;  // heads + loss run in train.hip's k_heads_fwd on the stored trunk outputs
     if (wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
     __syncthreads();
     PTR(5);
@@ -527,6 +600,44 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
 
 using namespace uavhip;
 
+namespace uavhip {
+namespace pol {
+int policy_forward_train(const float* packed, const float* states, const TrainIO& io, int Bm, hipStream_t st) {
+    hipLaunchKernelGGL(k_policy_forward<true>, dim3(Bm / SPW), dim3(NTHR), 0, st, packed, states, Bm, nullptr, 0ull,
+                       0ull, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, io);
+    return check_launch("k_policy_forward<train>");
+}
+
+// flat (state_dict order, plain layout) -> packed (GEMM weights in MFMA fragment order)
+__global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ flat, float* __restrict__ packed) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= kOffs.o[kNumParams]) return;
+    int q = 0;
+    while (q + 1 < kNumParams && i >= kOffs.o[q + 1]) ++q;
+    const int local = i - kOffs.o[q], K = kTileK[q];
+    if (K == 0 || local >= kSizes[q]) {
+        packed[i] = flat[i];
+        return;
+    }
+    // packed index ((r/16 * K/16 + k/16) * 64 + r%16 + 16 * ((k%16)/4)) * 4 + k%4 (uavhip.h)
+    const int j = local & 3, lane = (local >> 2) & 63, blk = local >> 8, KB = K / 16;
+    const int kb = blk % KB, rt = blk / KB;
+    const int r = 16 * rt + (lane & 15), k = 16 * kb + 4 * (lane >> 4) + j;
+    packed[i] = flat[kOffs.o[q] + r * K + k];
+}
+}  // namespace pol
+}  // namespace uavhip
+
+extern "C" int uavhip_policy_pack(const float* flat, float* packed, uavhip_stream_t stream) {
+    if (!flat || !packed) {
+        set_error("uavhip_policy_pack: NULL pointer");
+        return UAVHIP_EINVAL;
+    }
+    const int n = pol::kOffs.o[pol::kNumParams];
+    hipLaunchKernelGGL(pol::k_policy_pack, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, flat, packed);
+    return check_launch("k_policy_pack");
+}
+
 extern "C" int32_t uavhip_policy_layout(int32_t* offsets, int32_t max_offsets) {
     if (offsets)
         for (int i = 0; i < pol::kNumParams && i < max_offsets; ++i) offsets[i] = pol::kOffs.o[i];
@@ -563,7 +674,8 @@ extern "C" int uavhip_policy_forward(const uavhip_policy* policy, const float* s
         return UAVHIP_EINVAL;
     }
     const int grid = (B + pol::SPW - 1) / pol::SPW;
-    hipLaunchKernelGGL(pol::k_policy_forward, dim3(grid), dim3(pol::NTHR), 0, (hipStream_t)stream, policy->weights,
-                       states, (int)B, actions_in, seed, offset, offset_dev, action_out, logp, value, entropy, logits);
+    hipLaunchKernelGGL(pol::k_policy_forward<false>, dim3(grid), dim3(pol::NTHR), 0, (hipStream_t)stream,
+                       policy->weights, states, (int)B, actions_in, seed, offset, offset_dev, action_out, logp, value,
+                       entropy, logits, pol::TrainIO{});
     return check_launch("k_policy_forward");
 }

@@ -20,6 +20,7 @@
 #include "common.hpp"
 #include "policy_layout.hpp"
 #include "gemm.hpp"
+#include "policy_train.hpp"
 
 namespace uavhip {
 namespace tr {
@@ -50,141 +51,6 @@ __device__ __forceinline__ float add_xor32(float v) {
 __device__ __forceinline__ float quad_sum(float v) { return add_xor2(add_xor1(v)); }
 __device__ __forceinline__ float wave_sum(float v) {
     return add_xor32(add_xor16(add_ror8(add_ror4(add_xor2(add_xor1(v))))));
-}
-
-// ================================================================== forward pieces
-// Gather the minibatch rows, key padding mask (transformer_net.py:52-54), both embeddings
-// (transformer_net.py:57-59): e = relu(x We^T + be), h0 = e + pos[s]. 16 samples (80 rows) per
-// block; thread = (trunk, feature) keeps its We row in registers and walks the rows.
-struct EmbedArgs {
-    const float* states;
-    const int32_t* idx;
-    const float* P;  // params
-    float* xg;       // [R][16]
-    float* mask;     // [R] 1 = padded key
-    float *e_a, *h0_a, *e_c, *h0_c;  // [R][128]
-    const int8_t* act_in;
-    const float *oldlp_in, *oldv_in, *ret_in, *adv_in;
-    float* smp;  // [Bm][8]: action, old_logp, old_value, return, advantage
-};
-constexpr int kEmbRows = 16 * S;
-__global__ __launch_bounds__(256) void k_embed_fwd(const EmbedArgs a) {
-    __shared__ float xs[kEmbRows * 16];
-    const int r0 = blockIdx.x * kEmbRows, b0 = blockIdx.x * 16;
-    for (int i = threadIdx.x; i < kEmbRows * 16; i += 256) {
-        const int rr = i >> 4, k = i & 15, b = b0 + rr / S, s = rr % S;
-        const long long src = (long long)a.idx[b];
-        const float v = k < IN ? a.states[(src * S + s) * IN + k] : 0.f;
-        xs[i] = v;
-        a.xg[(size_t)r0 * 16 + i] = v;
-    }
-    if (threadIdx.x < 16) {
-        const int b = b0 + threadIdx.x;
-        const long long src = (long long)a.idx[b];
-        float* o = a.smp + (size_t)b * 8;
-        o[0] = (float)(a.act_in[src] != 0);
-        o[1] = a.oldlp_in[src];
-        o[2] = a.oldv_in[src];
-        o[3] = a.ret_in[src];
-        o[4] = a.adv_in[src];
-    }
-    __syncthreads();
-    if (threadIdx.x < kEmbRows) {
-        const int rr = threadIdx.x, s = rr % S;
-        float sa = 0.f;
-        for (int k = 0; k < IN; ++k) sa += fabsf(xs[rr * 16 + k]);
-        a.mask[r0 + rr] = (s < S - 1 && sa == 0.f) ? 1.f : 0.f;
-    }
-    const int trunk = threadIdx.x >> 7, f = threadIdx.x & 127;
-    const int base = trunk ? kCriticTrunk : kActorTrunk;
-    float w[IN];
-#pragma unroll
-    for (int k = 0; k < IN; ++k) w[k] = a.P[kOffs.o[base + EMB_W] + f * IN + k];
-    const float be = a.P[kOffs.o[base + EMB_B] + f];
-    float pos[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) pos[s] = a.P[kOffs.o[base + POS] + s * D + f];
-    float* eo = trunk ? a.e_c : a.e_a;
-    float* ho = trunk ? a.h0_c : a.h0_a;
-#pragma unroll 5
-    for (int rr = 0; rr < kEmbRows; ++rr) {
-        float acc = 0.f;
-#pragma unroll
-        for (int k = 0; k < IN; ++k) acc += w[k] * xs[rr * 16 + k];
-        const float e = fmaxf(acc + be, 0.f);
-        eo[(size_t)(r0 + rr) * D + f] = e;
-        ho[(size_t)(r0 + rr) * D + f] = e + pos[rr % S];
-    }
-}
-
-// Self-attention over the 5 keys of each sample: one (sample, head) per 4 lanes, each lane owning
-// 4 of the 16 head dims. qkv [R][384] (in_proj output), mask [R]; `last`: query s = 4 only, the
-// output o is compact [Bm][128]; else all 5 queries, o is [R][128].
-__global__ __launch_bounds__(256) void k_attn_fwd(const float* __restrict__ qkv, const float* __restrict__ mask,
-                                                  float* __restrict__ o, int Bm, int last) {
-    const int gt = blockIdx.x * 256 + threadIdx.x;
-    const int q4 = gt & 3, hh = (gt >> 2) & 7, b = gt >> 5;
-    if (b >= Bm) return;
-    const int d0 = hh * HD + 4 * q4;
-    f32x4 k[S], v[S];
-    bool msk[S];
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-        const float* row = qkv + (size_t)(b * S + j) * 3 * D;
-        k[j] = *reinterpret_cast<const f32x4*>(row + D + d0);
-        v[j] = *reinterpret_cast<const f32x4*>(row + 2 * D + d0);
-        msk[j] = mask[b * S + j] != 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-        if (last && i < S - 1) continue;
-        const f32x4 q = *reinterpret_cast<const f32x4*>(qkv + (size_t)(b * S + i) * 3 * D + d0);
-        float sc[S];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            const float part = quad_sum(q.x * k[j].x + q.y * k[j].y + q.z * k[j].z + q.w * k[j].w);
-            sc[j] = msk[j] ? -INFINITY : part * 0.25f;
-            mx = fmaxf(mx, sc[j]);
-        }
-        float den = 0.f;
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            sc[j] = __expf(sc[j] - mx);
-            den += sc[j];
-        }
-        const float inv = 1.0f / den;
-        f32x4 out = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < S; ++j) out += (sc[j] * inv) * v[j];
-        const int orow = last ? b : b * S + i;
-        *reinterpret_cast<f32x4*>(o + (size_t)orow * D + d0) = out;
-    }
-}
-
-// Post-LN residual block: z = hin[row(i)] + a[i]; out[i] = LN(z) * w + b (eps 1e-5), saving
-// xhat[i] = (z - mean) * rstd and rstd[i]. One wave per row, 2 features per lane. hin rows are
-// hin_stride * i + hin_off (token-4 rows of a full tensor for the pruned layers).
-__global__ __launch_bounds__(256) void k_resln_fwd(const float* __restrict__ hin, int hin_stride, int hin_off,
-                                                   const float* __restrict__ a, const float* __restrict__ w,
-                                                   const float* __restrict__ bb, float* __restrict__ xhat,
-                                                   float* __restrict__ rstd, float* __restrict__ out, int rows) {
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i >= rows) return;
-    const int l = lane_id();
-    const float2 hv = *reinterpret_cast<const float2*>(hin + (size_t)(i * hin_stride + hin_off) * D + 2 * l);
-    const float2 av = *reinterpret_cast<const float2*>(a + (size_t)i * D + 2 * l);
-    const float z0 = hv.x + av.x, z1 = hv.y + av.y;
-    const float mean = wave_sum(z0 + z1) * (1.0f / D);
-    const float d0 = z0 - mean, d1 = z1 - mean;
-    const float var = wave_sum(d0 * d0 + d1 * d1) * (1.0f / D);
-    const float rs = 1.0f / sqrtf(var + 1e-5f);
-    const float x0 = d0 * rs, x1 = d1 * rs;
-    *reinterpret_cast<float2*>(xhat + (size_t)i * D + 2 * l) = make_float2(x0, x1);
-    const float2 ww = *reinterpret_cast<const float2*>(w + 2 * l);
-    const float2 bv = *reinterpret_cast<const float2*>(bb + 2 * l);
-    *reinterpret_cast<float2*>(out + (size_t)i * D + 2 * l) = make_float2(x0 * ww.x + bv.x, x1 * ww.y + bv.y);
-    if (l == 0) rstd[i] = rs;
 }
 
 // ================================================================== heads + loss
@@ -708,7 +574,8 @@ struct Plan {
     float *z_a, *z_c, *dz_a, *dz_c, *dh_a, *dh_c, *fpart, *hpart, *epart, *sq_part;
     float* split_ws;
     size_t split_floats;
-    size_t total;  // workspace floats
+    float* packed;  // fragment-order copy of the parameters for the fused forward
+    size_t total;   // workspace floats
 };
 
 constexpr int kSplitRows = 2048;  // K rows per split of the weight-gradient GEMMs
@@ -779,14 +646,9 @@ inline Plan make_plan(int Bm, float* base) {
     p.sq_part = w.take(1 << 16);
     p.split_floats = dw_split_floats(Bm);
     p.split_ws = w.take(p.split_floats);
+    p.packed = w.take(kOffs.o[kNumParams]);
     p.total = w.off;
     return p;
-}
-
-// in_proj of a pruned layer: K and V for all R rows, Q only for the Bm token-4 rows (row 5b + 4)
-inline void qkv_pruned(GemmBuilder& g, const float* hin, const float* Win, const float* bin, float* qkv, int R, int Bm) {
-    g.add(hin, D, Win + D * D, D, qkv + D, 3 * D, R, 2 * D, D, E_BIAS, bin + D);
-    g.add(hin + (S - 1) * D, S * D, Win, D, qkv + (S - 1) * 3 * D, S * 3 * D, Bm, D, D, E_BIAS, bin);
 }
 
 template <int LAYOUT>
@@ -838,72 +700,31 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
     }
     hipStream_t st = (hipStream_t)stream;
     const Plan p = make_plan(c->minibatch, c->workspace);
-    const int Bm = p.Bm, R = p.R, nblk = Bm / kHeadSamples;
+    const int Bm = p.Bm, nblk = Bm / kHeadSamples;
     const LayerBufs &A = p.la, &C0 = p.lc0, &C1 = p.lc1;
-    auto L = [&](int trunk, int layer, int which) { return prm(c, layer_param(trunk, layer, which)); };
-    const int ta = kActorTrunk, tc = kCriticTrunk;
-    auto tail_fwd = [&](std::initializer_list<std::pair<const LayerBufs*, std::pair<int, int>>> layers,
-                        std::initializer_list<const float*> hins) -> int {
-        // layers: (buffers, (trunk, layer)); rows = R for the full layer (critic L0), Bm otherwise
-        GemmBuilder g1, g2, g3;
-        const float* hin_arr[4];
-        int i = 0;
-        for (const float* h : hins) hin_arr[i++] = h;
-        for (auto& lt : layers) {
-            const LayerBufs& B = *lt.first;
-            const int tr_ = lt.second.first, ly = lt.second.second;
-            const int rows = (&B == &C0) ? R : Bm;
-            g1.add(B.o, D, L(tr_, ly, OUTW), D, B.a, D, rows, D, D, E_BIAS, L(tr_, ly, OUTB));
-        }
-        TR_CHECK(run_gemm<L_FWD>(g1, st));
-        i = 0;
-        for (auto& lt : layers) {
-            const LayerBufs& B = *lt.first;
-            const int tr_ = lt.second.first, ly = lt.second.second;
-            const int rows = (&B == &C0) ? R : Bm;
-            const int hs = rows == R ? 1 : S, ho = rows == R ? 0 : S - 1;
-            hipLaunchKernelGGL(k_resln_fwd, dim3((rows + 3) / 4), dim3(256), 0, st, hin_arr[i], hs, ho, B.a,
-                               L(tr_, ly, N1W), L(tr_, ly, N1B), B.xhat1, B.rstd1, B.h1, rows);
-            TR_CHECK(check_launch("k_resln_fwd"));
-            g2.add(B.h1, D, L(tr_, ly, L1W), D, B.u, FF, rows, FF, D, E_BIAS_RELU, L(tr_, ly, L1B));
-            g3.add(B.u, FF, L(tr_, ly, L2W), FF, B.f, D, rows, D, FF, E_BIAS, L(tr_, ly, L2B));
-            ++i;
-        }
-        TR_CHECK(run_gemm<L_FWD>(g2, st));
-        TR_CHECK(run_gemm<L_FWD>(g3, st));
-        for (auto& lt : layers) {
-            const LayerBufs& B = *lt.first;
-            const int tr_ = lt.second.first, ly = lt.second.second;
-            const int rows = (&B == &C0) ? R : Bm;
-            hipLaunchKernelGGL(k_resln_fwd, dim3((rows + 3) / 4), dim3(256), 0, st, B.h1, 1, 0, B.f,
-                               L(tr_, ly, N2W), L(tr_, ly, N2B), B.xhat2, B.rstd2, B.h2, rows);
-            TR_CHECK(check_launch("k_resln_fwd"));
-        }
-        return UAVHIP_OK;
-    };
 
     // ---------------------------------------------------------------- forward
+    // The rollout's fused forward kernel (policy.hip) in training mode: one workgroup per 16
+    // samples, every activation the backward needs written to the workspace.
     if (fwd) {
-        EmbedArgs ea{states, idx, c->params, p.xg, p.mask, p.e_a, p.h0_a, p.e_c, p.h0_c, actions, old_logp,
-                     old_values, returns, advantages, p.smp};
-        hipLaunchKernelGGL(k_embed_fwd, dim3(Bm / 16), dim3(256), 0, st, ea);
-        TR_CHECK(check_launch("k_embed_fwd"));
-        // layer 0 QKV of both trunks
-        GemmBuilder g;
-        qkv_pruned(g, p.h0_a, L(ta, 0, INW), L(ta, 0, INB), A.qkv, R, Bm);
-        g.add(p.h0_c, D, L(tc, 0, INW), D, C0.qkv, 3 * D, R, 3 * D, D, E_BIAS, L(tc, 0, INB));
-        TR_CHECK(run_gemm<L_FWD>(g, st));
-        hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, A.qkv, p.mask, A.o, Bm, 1);
-        hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, C0.qkv, p.mask, C0.o, Bm, 0);
-        TR_CHECK(check_launch("k_attn_fwd"));
-        TR_CHECK(tail_fwd({{&A, {ta, 0}}, {&C0, {tc, 0}}}, {p.h0_a, p.h0_c}));
-        // critic layer 1 (pruned)
-        GemmBuilder g1;
-        qkv_pruned(g1, C0.h2, L(tc, 1, INW), L(tc, 1, INB), C1.qkv, R, Bm);
-        TR_CHECK(run_gemm<L_FWD>(g1, st));
-        hipLaunchKernelGGL(k_attn_fwd, dim3(Bm * 32 / 256), dim3(256), 0, st, C1.qkv, p.mask, C1.o, Bm, 1);
-        TR_CHECK(check_launch("k_attn_fwd"));
-        TR_CHECK(tail_fwd({{&C1, {tc, 1}}}, {C0.h2}));
+        TR_CHECK(uavhip_policy_pack(c->params, p.packed, stream));
+        pol::TrainIO io{};
+        io.idx = idx;
+        io.act_in = actions;
+        io.oldlp_in = old_logp;
+        io.oldv_in = old_values;
+        io.ret_in = returns;
+        io.adv_in = advantages;
+        io.smp = p.smp;
+        io.xg = p.xg;
+        io.mask = p.mask;
+        io.e[0] = p.e_a; io.e[1] = p.e_c;
+        io.h0[0] = p.h0_a; io.h0[1] = p.h0_c;
+        const LayerBufs* lb[3] = {&A, &C0, &C1};
+        for (int i = 0; i < 3; ++i)
+            io.L[i] = pol::TrainLayerIO{lb[i]->qkv, lb[i]->o, lb[i]->xhat1, lb[i]->rstd1, lb[i]->h1, lb[i]->u,
+                                        lb[i]->xhat2, lb[i]->rstd2, lb[i]->h2};
+        TR_CHECK(pol::policy_forward_train(p.packed, states, io, Bm, st));
         HeadArgs ha{c->params, A.h2, C1.h2, p.z_a, p.z_c, p.smp, p.fpart, c->eps_clip, Bm};
         hipLaunchKernelGGL(k_heads_fwd, dim3(nblk), dim3(1024), 0, st, ha);
         TR_CHECK(check_launch("k_heads_fwd"));

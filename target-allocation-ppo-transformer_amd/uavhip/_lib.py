@@ -76,6 +76,7 @@ _SIGS = {
     "uavhip_adv_normalize": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _i32, ctypes.c_int64, _vp, _vp]),
     "uavhip_policy_layout": (_i32, [ctypes.POINTER(_i32), _i32]),
     "uavhip_policy_tiling": (_i32, [ctypes.POINTER(_i32), _i32]),
+    "uavhip_policy_pack": (ctypes.c_int, [_vp, _vp, _vp]),
     "uavhip_policy_forward": (ctypes.c_int, [ctypes.POINTER(PolicyDesc), _vp, _i32, _vp, ctypes.c_uint64,
                                              ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "uavhip_ppo_workspace_floats": (ctypes.c_int64, [_i32]),

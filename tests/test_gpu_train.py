@@ -160,3 +160,18 @@ def test_data_parallel_phases_match_single_gpu_step():
     d = (ranks[0].params - single.params).abs()
     assert float(d.max()) <= 0.05 * 2 * 1e-3, float(d.max())  # Adam-normalised: a fraction of lr x steps
     np.testing.assert_allclose(ranks[0].stats.cpu().numpy(), single.stats.cpu().numpy(), rtol=1e-5)
+
+
+def test_device_pack_matches_host_pack():
+    """uavhip_policy_pack (device) == policy.pack_weights (host) bit for bit."""
+    from uavhip import _lib
+    from uavhip.policy import TransformerActorCritic, layout, pack_weights
+    torch.manual_seed(1)
+    net = TransformerActorCritic().cuda()
+    offs, n = layout()
+    flat = torch.zeros(n, device="cuda")
+    for p, o in zip(net.state_dict().values(), offs):
+        flat[o:o + p.numel()] = p.reshape(-1)
+    packed = torch.full((n,), float("nan"), device="cuda")
+    _lib.check(_lib.LIB.uavhip_policy_pack(_lib.ptr(flat), _lib.ptr(packed), _lib.stream_handle()), "pack")
+    assert torch.equal(packed, pack_weights(net.state_dict(), device="cuda"))
