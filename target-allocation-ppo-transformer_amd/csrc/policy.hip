@@ -98,7 +98,7 @@ __device__ __forceinline__ APre<D> prefetch(const float* __restrict__ W, int ldw
 // Fully unrolled over the 8 k-blocks of 16; the loads of block i + D (weights from L2 as float4,
 // activations from LDS as float4) are issued before the MFMAs of block i; blocks < D come from
 // `pre`. Both operands use the same k permutation (k = 16 i + 4 (lane >> 4) + j for MFMA j).
-template <int CT, int D>
+template <int CT, int D, int NKB = KB>
 __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[CT], const APre<D>& pre, const float* __restrict__ W, int ldw,
                                           int row, int kw0, const float* X, int ldx, int xtok0) {
     const int l = lane_id(), i16 = l & 15, g = l >> 4;
@@ -106,7 +106,7 @@ __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[CT], const APre<D>& pre, 
     const float* xp[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) xp[ct] = X + (xtok0 + 16 * ct + i16) * ldx + 4 * g;
-    f32x4 a[KB], b[KB][CT];
+    f32x4 a[NKB], b[NKB][CT];
 #pragma unroll
     for (int p = 0; p < D; ++p) {
         a[p] = pre.a[p];
@@ -114,8 +114,8 @@ __device__ __forceinline__ void gemm_tile(f32x4 (&acc)[CT], const APre<D>& pre, 
         for (int ct = 0; ct < CT; ++ct) b[p][ct] = *reinterpret_cast<const f32x4*>(xp[ct] + 16 * p);
     }
 #pragma unroll
-    for (int i = 0; i < KB; ++i) {
-        if (i + D < KB) {
+    for (int i = 0; i < NKB; ++i) {
+        if (i + D < NKB) {
             a[i + D] = *reinterpret_cast<const f32x4*>(wp + 256 * (i + D));
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) b[i + D][ct] = *reinterpret_cast<const f32x4*>(xp[ct] + 16 * (i + D));
@@ -595,6 +595,309 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     PTR(7);
 }
 
+// ================================================================== K6: fused training backward
+// Mirror of the forward for one 16-sample workgroup: gradients flow through the LDS-resident
+// [tok][feature] rows, the dX GEMMs run transposed on the MFMA with the transposed weights
+// (policy_pack_transposed) as A operands, and only the dY operands of the weight-gradient GEMMs
+// (df, du, dz1, dqkv) plus per-workgroup LayerNorm / embedding partials go to HBM.
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ float add_ror4(float v) {  // row_ror:4 inside each row of 16 lanes
+    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float add_ror8(float v) {
+    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row16_sum(float v) { return add_ror8(add_ror4(add_xor2(add_xor1(v)))); }
+__device__ __forceinline__ float hsum(f32x4 v) { return (v.x + v.y) + (v.z + v.w); }
+
+// LayerNorm backward (torch's formula) on LDS rows, tokens [t0, TOK), 16 lanes per token and 8
+// features per lane: g = src * w; dz = rstd * (g - mean(g) - xhat * mean(g * xhat)) -> dst (LDS)
+// and gout (workspace rows). Per-workgroup partials of dw = sum src * xhat, db = sum src -> part
+// [0..127], [128..255], reduced over the 32 lane groups through `scratch` (8 KiB floats). Ends
+// without a barrier after the partials are written (scratch is read until then).
+__device__ void ln_bwd_lds(const float* src, float* dst, const float* __restrict__ xhat,
+                           const float* __restrict__ rstd, const float* __restrict__ w, float* __restrict__ gout,
+                           float* __restrict__ part, int t0, int b0, bool compact, float* scratch) {
+    const int j = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int f0 = 8 * j;
+    const f32x4 w0 = ld4(w + f0), w1 = ld4(w + f0 + 4);
+    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 pw0 = zero4, pw1 = zero4, pb0 = zero4, pb1 = zero4;
+    for (int tok = t0 + grp; tok < TOK; tok += NTHR / 16) {
+        const size_t r = (size_t)orow(tok, b0, compact);
+        const f32x4 g0 = ld4(src + tok * LDH + f0), g1 = ld4(src + tok * LDH + f0 + 4);
+        const f32x4 x0 = ld4(xhat + r * D + f0), x1 = ld4(xhat + r * D + f0 + 4);
+        const float rs = rstd[r];
+        const f32x4 gw0 = g0 * w0, gw1 = g1 * w1;
+        const float m1 = row16_sum(hsum(gw0) + hsum(gw1)) * (1.0f / D);
+        const float m2 = row16_sum(hsum(gw0 * x0) + hsum(gw1 * x1)) * (1.0f / D);
+        const f32x4 d0 = rs * (gw0 - m1 - x0 * m2), d1 = rs * (gw1 - m1 - x1 * m2);
+        st4(dst + tok * LDH + f0, d0);
+        st4(dst + tok * LDH + f0 + 4, d1);
+        st4(gout + r * D + f0, d0);
+        st4(gout + r * D + f0 + 4, d1);
+        pw0 += g0 * x0; pw1 += g1 * x1;
+        pb0 += g0; pb1 += g1;
+    }
+    float* sc = scratch + grp * 2 * D;
+    st4(sc + f0, pw0); st4(sc + f0 + 4, pw1);
+    st4(sc + D + f0, pb0); st4(sc + D + f0 + 4, pb1);
+    __syncthreads();
+    if (threadIdx.x < 2 * D) {
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < NTHR / 16; ++q) s[q & 3] += scratch[q * 2 * D + threadIdx.x];
+        part[threadIdx.x] = (s[0] + s[1]) + (s[2] + s[3]);
+    }
+}
+
+// Attention backward for heads [4c, 4c+4), P recomputed from q, k (from the workspace qkv rows);
+// with g = d(attention output) of the query rows (sm.ctx):
+//   dv_j = sum_i P_ij g_i; dP_ij = g_i . v_j; dS_ij = P_ij (dP_ij - sum_k P_ik dP_ik);
+//   dq_i = sum_j dS_ij k_j / 4; dk_j = sum_i dS_ij q_i / 4.
+// One (sample, head) task per 4 lanes (threads 0-255). dq | dk | dv -> sm.big [tok][3 x 64] (the
+// forward's chunk layout) and dqkv rows (pruned layers: dq only for the token-4 query rows; the
+// LDS copy is zero on the other rows).
+template <bool last>
+__device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, float* __restrict__ dqkv, int c, int b0) {
+    if (threadIdx.x >= 256) return;
+    const int q4 = threadIdx.x & 3, hh = (threadIdx.x >> 2) & 3, p = threadIdx.x >> 4;
+    const int d0 = hh * HD + 4 * q4, col = 64 * c + d0;
+    const size_t rb = (size_t)(b0 + p) * S;
+    f32x4 k[S], v[S], dk[S], dv[S];
+    bool msk[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        k[j] = ld4(qkv + (rb + j) * 3 * D + D + col);
+        v[j] = ld4(qkv + (rb + j) * 3 * D + 2 * D + col);
+        msk[j] = sm.mask[p * S + j] != 0;
+        dk[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+        if (!last || i == S - 1) {
+            const f32x4 q = ld4(qkv + (rb + i) * 3 * D + col);
+            const f32x4 g = ld4(sm.ctx + (i * SPW + p) * LDH + col);
+            float pr[S], dp[S];
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                const float part = add_xor2(add_xor1(q.x * k[j].x + q.y * k[j].y + q.z * k[j].z + q.w * k[j].w));
+                pr[j] = msk[j] ? -INFINITY : part * 0.25f;
+                mx = fmaxf(mx, pr[j]);
+            }
+            float den = 0.f;
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                pr[j] = __expf(pr[j] - mx);
+                den += pr[j];
+            }
+            const float inv = 1.0f / den;
+            float sdp = 0.f;
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                pr[j] *= inv;
+                dp[j] = add_xor2(add_xor1(g.x * v[j].x + g.y * v[j].y + g.z * v[j].z + g.w * v[j].w));
+                sdp += pr[j] * dp[j];
+            }
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                const float ds = pr[j] * (dp[j] - sdp) * 0.25f;
+                dq += ds * k[j];
+                dk[j] += ds * q;
+                dv[j] += pr[j] * g;
+            }
+            st4(dqkv + (rb + i) * 3 * D + col, dq);
+        }
+        st4(sm.big + (i * SPW + p) * LDB + d0, dq);
+    }
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        st4(sm.big + (j * SPW + p) * LDB + 64 + d0, dk[j]);
+        st4(sm.big + (j * SPW + p) * LDB + 128 + d0, dv[j]);
+        st4(dqkv + (rb + j) * 3 * D + D + col, dk[j]);
+        st4(dqkv + (rb + j) * 3 * D + 2 * D + col, dv[j]);
+    }
+}
+
+// Backward of one post-LN encoder layer. On entry sm.h holds dL/d(layer output) for the tokens
+// >= qtok0; on exit sm.h holds dL/d(layer input) for all 80 tokens. Ends with a barrier.
+template <int trunk, int layer, bool last>
+__device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __restrict__ PT, const BwdLayerIO& io,
+                          int b0) {
+    constexpr int CTQ = last ? 1 : S;
+    constexpr int DQ = depth<CTQ>();
+    constexpr int qtok0 = last ? (S - 1) * SPW : 0;
+    const float* WinT = PT + kTWin;
+    const float* WoT = PT + kTWo;
+    const float* W1T = PT + kTW1;
+    const float* W2T = PT + kTW2;
+    const int wv = threadIdx.x >> 6, l = lane_id(), i16 = l & 15, g = l >> 4;
+    const int fo = 16 * wv + 4 * g;  // this lane's 4 output features of a 16-row tile of wave wv
+
+    // LN2 backward: sm.h -> sm.ctx (= df)
+    APre<DQ> pa = prefetch<DQ>(W2T, D, 16 * wv, 0);
+    ln_bwd_lds(sm.h, sm.ctx, io.xhat2, io.rstd2, P + kOffs.o[layer_param(trunk, layer, N2W)], io.df, io.ln2_part + (size_t)blockIdx.x * 2 * D,
+               qtok0, b0, last, sm.big);
+    __syncthreads();
+    // du = relu'(u) (W2^T df): 256 hidden features, wave wv owns tiles 16 wv (-> big) and 128 + 16 wv (-> h)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int row = 128 * t + 16 * wv;
+        f32x4 acc[CTQ];
+        zero(acc);
+        if (t == 0) gemm_tile<CTQ, DQ>(acc, pa, W2T, D, row, 0, sm.ctx, LDH, qtok0);
+        else gemm_tile<CTQ, DQ>(acc, prefetch<DQ>(W2T, D, row, 0), W2T, D, row, 0, sm.ctx, LDH, qtok0);
+        float* lds = t ? sm.h : sm.big;
+#pragma unroll
+        for (int ct = 0; ct < CTQ; ++ct) {
+            const int tok = qtok0 + 16 * ct + i16;
+            const size_t r = (size_t)orow(tok, b0, last);
+            const f32x4 u = ld4(io.u + r * FF + row + 4 * g);
+            f32x4 d = acc[ct];
+            d.x = u.x > 0.f ? d.x : 0.f; d.y = u.y > 0.f ? d.y : 0.f;
+            d.z = u.z > 0.f ? d.z : 0.f; d.w = u.w > 0.f ? d.w : 0.f;
+            st4(io.du + r * FF + row + 4 * g, d);
+            st4(lds + tok * LDH + fo, d);
+        }
+    }
+    pa = prefetch<DQ>(W1T, FF, 16 * wv, 0);
+    __syncthreads();
+    // dh1 = df + W1^T du (K = 256: hidden 0-127 in big, 128-255 in h) -> sm.ctx in place
+    {
+        f32x4 acc[CTQ];
+        zero(acc);
+        gemm_tile<CTQ, DQ>(acc, pa, W1T, FF, 16 * wv, 0, sm.big, LDF, qtok0);
+        gemm_tile<CTQ, DQ>(acc, prefetch<DQ>(W1T, FF, 16 * wv, 128), W1T, FF, 16 * wv, 128, sm.h, LDH, qtok0);
+#pragma unroll
+        for (int ct = 0; ct < CTQ; ++ct) {
+            float* q = sm.ctx + (qtok0 + 16 * ct + i16) * LDH + fo;
+            st4(q, acc[ct] + ld4(q));
+        }
+    }
+    pa = prefetch<DQ>(WoT, D, 16 * wv, 0);
+    __syncthreads();
+    // LN1 backward: sm.ctx -> sm.h (= dz1)
+    ln_bwd_lds(sm.ctx, sm.h, io.xhat1, io.rstd1, P + kOffs.o[layer_param(trunk, layer, N1W)], io.dz1, io.ln1_part + (size_t)blockIdx.x * 2 * D,
+               qtok0, b0, last, sm.big);
+    __syncthreads();
+    // d(attention output) = Wo^T dz1 -> sm.ctx
+    {
+        f32x4 acc[CTQ];
+        zero(acc);
+        gemm_tile<CTQ, DQ>(acc, pa, WoT, D, 16 * wv, 0, sm.h, LDH, qtok0);
+#pragma unroll
+        for (int ct = 0; ct < CTQ; ++ct) st4(sm.ctx + (qtok0 + 16 * ct + i16) * LDH + fo, acc[ct]);
+    }
+    __syncthreads();
+    // attention backward per chunk of 4 heads, dh_in += Win^T [dq | dk | dv] of the chunk (K = 3 x 64)
+    f32x4 acc[S];
+    zero(acc);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        APre<2> pw = prefetch<2>(WinT, 3 * D, 16 * wv, 64 * c);
+        attn_bwd_chunk<last>(sm, io.qkv, io.dqkv, c, b0);
+        __syncthreads();
+#pragma unroll
+        for (int part = 0; part < 3; ++part) {
+            const int kw = part * D + 64 * c;
+            if (part) pw = prefetch<2>(WinT, 3 * D, 16 * wv, kw);
+            gemm_tile<S, 2, 4>(acc, pw, WinT, 3 * D, 16 * wv, kw, sm.big + part * 64, LDB, 0);
+        }
+        if (c == 0) __syncthreads();  // big is rewritten by chunk 1
+    }
+    // + dz1 on the rows that carried the residual -> sm.h
+#pragma unroll
+    for (int ct = 0; ct < S; ++ct) {
+        const int tok = 16 * ct + i16;
+        float* q = sm.h + tok * LDH + fo;
+        st4(q, tok >= qtok0 ? acc[ct] + ld4(q) : acc[ct]);
+    }
+    __syncthreads();
+}
+
+// Embedding backward from sm.h = dL/d(h0) (80 tokens): h0 = relu(We x + be) + pos. Thread =
+// (feature, token group of 20); partials reduced over the 4 groups through sm.big -> part [2560].
+__device__ void embed_bwd(Smem& sm, const float* __restrict__ e, float* __restrict__ part, int b0) {
+    const int f = threadIdx.x & (D - 1), grp = threadIdx.x >> 7;
+    float acc[IN + 1 + S];
+#pragma unroll
+    for (int v = 0; v < IN + 1 + S; ++v) acc[v] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TOK / 4; ++i) {
+        const int tok = grp + 4 * i;  // position tok / 16 = i / 4
+        const float gv = sm.h[tok * LDH + f];
+        acc[IN + 1 + i / 4] += gv;
+        const float gp = e[(size_t)trow(tok, b0) * D + f] > 0.f ? gv : 0.f;
+        acc[IN] += gp;
+#pragma unroll
+        for (int k = 0; k < IN; ++k) acc[k] += gp * sm.x[tok * LDX + k];
+    }
+    constexpr int NV = IN + 1 + S;  // 20
+#pragma unroll
+    for (int v = 0; v < NV; ++v) sm.big[(grp * NV + v) * D + f] = acc[v];
+    __syncthreads();
+    for (int o = threadIdx.x; o < NV * D; o += NTHR) {
+        const int v = o >> 7, ff = o & (D - 1);
+        const float s = (sm.big[v * D + ff] + sm.big[(NV + v) * D + ff]) +
+                        (sm.big[(2 * NV + v) * D + ff] + sm.big[(3 * NV + v) * D + ff]);
+        const int dst = v < IN ? ff * IN + v : (v == IN ? D * IN + ff : D * IN + D + (v - IN - 1) * D + ff);
+        part[dst] = s;
+    }
+}
+
+__device__ __forceinline__ void load_top_grad(Smem& sm, const float* __restrict__ dh, int b0) {
+    for (int i = threadIdx.x; i < SPW * D / 4; i += NTHR) {
+        const int p = i / (D / 4), q = i % (D / 4);
+        st4(sm.h + ((S - 1) * SPW + p) * LDH + 4 * q, ld4(dh + (size_t)(b0 + p) * D + 4 * q));
+    }
+}
+
+__global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restrict__ P, const float* __restrict__ PT,
+                                                          const BwdIO io) {
+    __shared__ __attribute__((aligned(16))) Smem sm;
+    const int b0 = blockIdx.x * SPW;
+    for (int i = threadIdx.x; i < TOK * LDX / 4; i += NTHR) {
+        const int t = i / (LDX / 4), q = i % (LDX / 4);
+        st4(sm.x + t * LDX + 4 * q, ld4(io.xg + (size_t)trow(t, b0) * 16 + 4 * q));
+    }
+    if (threadIdx.x < SPW * S) sm.mask[threadIdx.x] = io.mask[(size_t)b0 * S + threadIdx.x] != 0.f;
+    // critic: layer 1 (pruned), layer 0, embedding
+    load_top_grad(sm, io.dh_top[1], b0);
+    __syncthreads();
+    bwd_layer<kCriticTrunk, 1, true>(sm, P, PT + 2 * kLayerT, io.L[2], b0);
+    bwd_layer<kCriticTrunk, 0, false>(sm, P, PT + 1 * kLayerT, io.L[1], b0);
+    embed_bwd(sm, io.e[1], io.epart + ((size_t)blockIdx.x * 2 + 1) * kEmbPart, b0);
+    __syncthreads();
+    // actor: layer 0 (pruned), embedding
+    load_top_grad(sm, io.dh_top[0], b0);
+    __syncthreads();
+    bwd_layer<kActorTrunk, 0, true>(sm, P, PT, io.L[0], b0);
+    embed_bwd(sm, io.e[0], io.epart + (size_t)blockIdx.x * 2 * kEmbPart, b0);
+}
+
+// flat (state_dict order) -> per layer [in_proj^T | out_proj^T | linear1^T | linear2^T] in
+// fragment order: packedT[((r/16) * K/16 + k/16) * 256 + (r%16 + 16 ((k%16)/4)) * 4 + k%4] = W[k][r]
+__global__ __launch_bounds__(256) void k_policy_pack_t(const float* __restrict__ flat, float* __restrict__ pt) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= kPackedTFloats) return;
+    const int li = i / kLayerT, loc = i - li * kLayerT;
+    const int trunk = li == 0 ? kActorTrunk : kCriticTrunk, layer = li == 2 ? 1 : 0;
+    int which, base, Rt, Kt;
+    if (loc < kTWo) { which = INW; base = kTWin; Rt = D; Kt = 3 * D; }
+    else if (loc < kTW1) { which = OUTW; base = kTWo; Rt = D; Kt = D; }
+    else if (loc < kTW2) { which = L1W; base = kTW1; Rt = D; Kt = FF; }
+    else { which = L2W; base = kTW2; Rt = FF; Kt = D; }
+    const int m = loc - base;
+    const int j = m & 3, lane = (m >> 2) & 63, blk = m >> 8, KBt = Kt / 16;
+    const int kb = blk % KBt, rt = blk / KBt;
+    const int r = 16 * rt + (lane & 15), k = 16 * kb + 4 * (lane >> 4) + j;
+    pt[i] = flat[kOffs.o[layer_param(trunk, layer, which)] + k * Rt + r];
+}
+
 }  // namespace pol
 }  // namespace uavhip
 
@@ -606,6 +909,16 @@ int policy_forward_train(const float* packed, const float* states, const TrainIO
     hipLaunchKernelGGL(k_policy_forward<true>, dim3(Bm / SPW), dim3(NTHR), 0, st, packed, states, Bm, nullptr, 0ull,
                        0ull, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, io);
     return check_launch("k_policy_forward<train>");
+}
+
+int policy_backward_train(const float* packed, const float* packedT, const BwdIO& io, int Bm, hipStream_t st) {
+    hipLaunchKernelGGL(k_policy_backward, dim3(Bm / SPW), dim3(NTHR), 0, st, packed, packedT, io);
+    return check_launch("k_policy_backward");
+}
+
+int policy_pack_transposed(const float* flat, float* packedT, hipStream_t st) {
+    hipLaunchKernelGGL(k_policy_pack_t, dim3((kPackedTFloats + 255) / 256), dim3(256), 0, st, flat, packedT);
+    return check_launch("k_policy_pack_t");
 }
 
 // flat (state_dict order, plain layout) -> packed (GEMM weights in MFMA fragment order)

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "policy_layout.hpp"
+
 namespace uavhip {
 namespace pol {
 
@@ -22,6 +24,33 @@ struct TrainIO {
     float *e[2], *h0[2];         // [R][128] actor, critic embeddings (post-ReLU) and layer inputs
     TrainLayerIO L[3];           // actor L0 (pruned), critic L0 (full), critic L1 (pruned)
 };
+
+// ---- K6: fused backward of the three encoder layers + embeddings (policy.hip), one workgroup per
+// 16 samples like the forward. Inputs are the forward's activations; outputs are the dY operands of
+// the weight-gradient GEMMs and per-workgroup partials of the LayerNorm / embedding gradients.
+struct BwdLayerIO {
+    const float *qkv, *xhat1, *rstd1, *u, *xhat2, *rstd2;  // forward activations (TrainLayerIO)
+    float *dqkv;                 // [R][384] (pruned layers: Q part on token-4 rows only)
+    float *dz1, *du, *df;        // d(LN1 input), d(FFN hidden pre-ReLU), d(LN2 input) rows
+    float *ln1_part, *ln2_part;  // [Bm/16][256]: dgamma | dbeta partials per workgroup
+};
+constexpr int kEmbPart = D * IN + D + S * D;  // 2560: We [128][14] | be [128] | pos [5][128]
+struct BwdIO {
+    const float* dh_top[2];  // [Bm][128] gradient wrt the actor / critic trunk outputs (token 4)
+    const float* xg;         // [R][16] input windows (TrainIO::xg)
+    const float* mask;       // [R] key padding mask
+    const float* e[2];       // [R][128] embeddings after ReLU
+    float* epart;            // [Bm/16][2][kEmbPart] embedding gradient partials
+    BwdLayerIO L[3];         // actor L0 (pruned), critic L0 (full), critic L1 (pruned)
+};
+// Transposed copies of each layer's GEMM weights in fragment order (the dX GEMMs' A operands):
+// in_proj^T [128][384] | out_proj^T [128][128] | linear1^T [128][256] | linear2^T [256][128].
+constexpr int kTWin = 0, kTWo = 3 * D * D, kTW1 = kTWo + D * D, kTW2 = kTW1 + FF * D;
+constexpr int kLayerT = kTW2 + D * FF;  // 131072 floats per layer
+constexpr int kPackedTFloats = 3 * kLayerT;
+
+int policy_pack_transposed(const float* flat, float* packedT, hipStream_t st);
+int policy_backward_train(const float* packed, const float* packedT, const BwdIO& io, int Bm, hipStream_t st);
 
 // Launch the training-mode forward over Bm samples (multiple of 16) with fragment-order packed
 // weights `packed` (uavhip_policy_pack) and trajectory windows `states` [n][5][14].

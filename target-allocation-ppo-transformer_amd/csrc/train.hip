@@ -2,20 +2,19 @@
 // (networks/transformer_net.py) on gfx950, fp32 throughout.
 //
 // Layout: a minibatch of Bm samples is R = 5 Bm token rows, row = b * 5 + s, features contiguous.
-// Every linear layer is one problem of a grouped fp32 MFMA GEMM (v_mfma_f32_16x16x4_f32, 64 x 64
-// tiles, LDS double buffering):
-//    forward   Y[row][out]  = X[row][in] W[out][in]^T + b         (L_FWD)
-//    input gr. dX[row][in]  = dY[row][out] W[out][in]             (L_DX)
-//    weight gr dW[out][in]  = sum_row dY[row][out] X[row][in]     (L_DW, split-K partial slabs + the
-//                                                                  bias gradient as row sums of dY)
+// One step is 11 launches on one stream (graph-capturable: no host sync, no allocation):
+//    forward   k_policy_forward<TR> (policy.hip, the rollout's fused kernel writing activations),
+//              k_heads_fwd + k_loss_sums (heads, losses, the four loss sums)
+//    backward  k_heads_bwd (loss + head gradients), k_policy_backward (K6, policy.hip: dX of the
+//              encoder layers and embeddings, one workgroup per 16 samples), then every weight
+//              gradient dW[out][in] = sum_row dY[row][out] X[row][in] as one grouped fp32 MFMA GEMM
+//              (gemm.hpp, L_DW, split-K partial slabs + bias gradients as row sums of dY) and one
+//              k_reduce_grads over all partials
+//    update    k_grad_sq + k_adam (clip_grad_norm_ + Adam)
 // The last encoder layer of each trunk is pruned to the token the heads read (s = 4): K and V for
 // all rows, everything else for Bm rows (compact [Bm][...] tensors), so its gradients are exactly
-// the dense model's. Attention (5 keys, 8 heads x 16), residual + LayerNorm, heads + loss and the
-// fused clip_grad_norm_ + Adam are VALU kernels. The host side (uavhip_ppo_step) sequences ~40
-// launches on one stream: the whole step is graph-capturable (no host sync, no allocation).
+// the dense model's.
 #include <cmath>
-#include <initializer_list>
-#include <utility>
 
 #include "common.hpp"
 #include "policy_layout.hpp"
@@ -291,147 +290,9 @@ __global__ __launch_bounds__(1024) void k_heads_bwd(const HeadBwdArgs a) {
     }
 }
 
-// ================================================================== backward pieces
-// LayerNorm backward (torch's formula) for `rows` rows, one wave per row:
-//   g = gout * w; gin = rstd * (g - mean(g) - xhat * mean(g * xhat))
-// gin goes to dst1[row] and, if dst2, to dst2[row * dst2_stride + dst2_off] (the residual branch).
-// Per-block partials of dw = sum gout * xhat and db = sum gout: part[blk][0..127], [128..255].
-constexpr int kLnBlocks = 512;
-__global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ gout, const float* __restrict__ xhat,
-                                                const float* __restrict__ rstd, const float* __restrict__ w,
-                                                float* __restrict__ dst1, float* __restrict__ dst2, int dst2_stride,
-                                                int dst2_off, float* __restrict__ part, int rows) {
-    __shared__ float pw[4][D], pb[4][D];
-    const int wv = threadIdx.x >> 6, l = lane_id();
-    const float2 ww = *reinterpret_cast<const float2*>(w + 2 * l);
-    float aw0 = 0.f, aw1 = 0.f, ab0 = 0.f, ab1 = 0.f;
-    for (int i = blockIdx.x * 4 + wv; i < rows; i += gridDim.x * 4) {
-        const float2 go = *reinterpret_cast<const float2*>(gout + (size_t)i * D + 2 * l);
-        const float2 xh = *reinterpret_cast<const float2*>(xhat + (size_t)i * D + 2 * l);
-        aw0 += go.x * xh.x; aw1 += go.y * xh.y;
-        ab0 += go.x; ab1 += go.y;
-        const float g0 = go.x * ww.x, g1 = go.y * ww.y;
-        const float mg = wave_sum(g0 + g1) * (1.0f / D);
-        const float mgx = wave_sum(g0 * xh.x + g1 * xh.y) * (1.0f / D);
-        const float rs = rstd[i];
-        const float2 gi = make_float2(rs * (g0 - mg - xh.x * mgx), rs * (g1 - mg - xh.y * mgx));
-        *reinterpret_cast<float2*>(dst1 + (size_t)i * D + 2 * l) = gi;
-        if (dst2) *reinterpret_cast<float2*>(dst2 + (size_t)(i * dst2_stride + dst2_off) * D + 2 * l) = gi;
-    }
-    pw[wv][2 * l] = aw0; pw[wv][2 * l + 1] = aw1;
-    pb[wv][2 * l] = ab0; pb[wv][2 * l + 1] = ab1;
-    __syncthreads();
-    if (threadIdx.x < D) {
-        const int f = threadIdx.x;
-        part[(size_t)blockIdx.x * 2 * D + f] = (pw[0][f] + pw[1][f]) + (pw[2][f] + pw[3][f]);
-        part[(size_t)blockIdx.x * 2 * D + D + f] = (pb[0][f] + pb[1][f]) + (pb[2][f] + pb[3][f]);
-    }
-}
-
-// Attention backward. P recomputed from q, k; with g = do (query rows):
-//   dv_j = sum_i P_ij g_i; dP_ij = g_i . v_j; dS_ij = P_ij (dP_ij - sum_k P_ik dP_ik);
-//   dq_i = sum_j dS_ij k_j / 4; dk_j = sum_i dS_ij q_i / 4.
-// dqkv [R][384] gets all rows (dq zero on rows that were not queries).
-__global__ __launch_bounds__(256) void k_attn_bwd(const float* __restrict__ qkv, const float* __restrict__ mask,
-                                                  const float* __restrict__ dout, float* __restrict__ dqkv, int Bm,
-                                                  int last) {
-    const int gt = blockIdx.x * 256 + threadIdx.x;
-    const int q4 = gt & 3, hh = (gt >> 2) & 7, b = gt >> 5;
-    if (b >= Bm) return;
-    const int d0 = hh * HD + 4 * q4;
-    f32x4 k[S], v[S], dk[S], dv[S];
-    bool msk[S];
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-        const float* row = qkv + (size_t)(b * S + j) * 3 * D;
-        k[j] = *reinterpret_cast<const f32x4*>(row + D + d0);
-        v[j] = *reinterpret_cast<const f32x4*>(row + 2 * D + d0);
-        msk[j] = mask[b * S + j] != 0.f;
-        dk[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-        f32x4 dq = {0.f, 0.f, 0.f, 0.f};
-        if (!(last && i < S - 1)) {
-            const f32x4 q = *reinterpret_cast<const f32x4*>(qkv + (size_t)(b * S + i) * 3 * D + d0);
-            const int grow = last ? b : b * S + i;
-            const f32x4 g = *reinterpret_cast<const f32x4*>(dout + (size_t)grow * D + d0);
-            float pr[S], dp[S];
-            float mx = -INFINITY;
-#pragma unroll
-            for (int j = 0; j < S; ++j) {
-                const float part = quad_sum(q.x * k[j].x + q.y * k[j].y + q.z * k[j].z + q.w * k[j].w);
-                pr[j] = msk[j] ? -INFINITY : part * 0.25f;
-                mx = fmaxf(mx, pr[j]);
-            }
-            float den = 0.f;
-#pragma unroll
-            for (int j = 0; j < S; ++j) {
-                pr[j] = __expf(pr[j] - mx);
-                den += pr[j];
-            }
-            const float inv = 1.0f / den;
-            float sdp = 0.f;
-#pragma unroll
-            for (int j = 0; j < S; ++j) {
-                pr[j] *= inv;
-                dp[j] = quad_sum(g.x * v[j].x + g.y * v[j].y + g.z * v[j].z + g.w * v[j].w);
-                sdp += pr[j] * dp[j];
-            }
-#pragma unroll
-            for (int j = 0; j < S; ++j) {
-                const float ds = pr[j] * (dp[j] - sdp) * 0.25f;
-                dq += ds * k[j];
-                dk[j] += ds * q;
-                dv[j] += pr[j] * g;
-            }
-        }
-        *reinterpret_cast<f32x4*>(dqkv + (size_t)(b * S + i) * 3 * D + d0) = dq;
-    }
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-        float* row = dqkv + (size_t)(b * S + j) * 3 * D;
-        *reinterpret_cast<f32x4*>(row + D + d0) = dk[j];
-        *reinterpret_cast<f32x4*>(row + 2 * D + d0) = dv[j];
-    }
-}
-
-// Embedding backward for both trunks, 16 samples (80 rows) per block; thread = (trunk, feature).
-// Partials per block and trunk in parameter order: We [128][14] | be [128] | pos [5][128].
-constexpr int kEmbPart = D * IN + D + S * D;  // 2560
-__global__ __launch_bounds__(256) void k_embed_bwd(const float* __restrict__ dh_a, const float* __restrict__ dh_c,
-                                                   const float* __restrict__ e_a, const float* __restrict__ e_c,
-                                                   const float* __restrict__ xg, float* __restrict__ part) {
-    __shared__ float xs[16 * S * 16];
-    const int r0 = blockIdx.x * 16 * S;
-    for (int i = threadIdx.x; i < 16 * S * 16; i += 256) xs[i] = xg[(size_t)r0 * 16 + i];
-    __syncthreads();
-    const int trunk = threadIdx.x >> 7, f = threadIdx.x & 127;
-    const float* dh = trunk ? dh_c : dh_a;
-    const float* e = trunk ? e_c : e_a;
-    float dw[IN], dbv = 0.f, dp[S];
-#pragma unroll
-    for (int k = 0; k < IN; ++k) dw[k] = 0.f;
-#pragma unroll
-    for (int s = 0; s < S; ++s) dp[s] = 0.f;
-#pragma unroll 5
-    for (int rr = 0; rr < 16 * S; ++rr) {
-        const int s = rr % S;
-        const float g = dh[(size_t)(r0 + rr) * D + f];
-        dp[s] += g;
-        const float gp = e[(size_t)(r0 + rr) * D + f] > 0.f ? g : 0.f;
-        dbv += gp;
-#pragma unroll
-        for (int k = 0; k < IN; ++k) dw[k] += gp * xs[rr * 16 + k];
-    }
-    float* o = part + ((size_t)blockIdx.x * 2 + trunk) * kEmbPart;
-#pragma unroll
-    for (int k = 0; k < IN; ++k) o[f * IN + k] = dw[k];
-    o[D * IN + f] = dbv;
-#pragma unroll
-    for (int s = 0; s < S; ++s) o[D * IN + D + s * D + f] = dp[s];
-}
+// ================================================================== backward
+// dX of the encoder layers + embeddings: k_policy_backward (policy.hip, K6), one fused kernel.
+using pol::kEmbPart;
 
 // ================================================================== gradient reduction + Adam
 // grads[dst + i] = sum_p src[p * part_stride + i] for each segment; block partial sums of g^2.
@@ -562,8 +423,8 @@ struct WS {  // workspace carve-up (floats), identical for sizing and for the st
 };
 
 struct LayerBufs {  // one encoder layer (pruned: tail tensors are [Bm] rows)
-    float *qkv, *o, *a, *xhat1, *rstd1, *h1, *u, *f, *xhat2, *rstd2, *h2;
-    float *dqkv, *dz1, *dout, *dh1, *du, *df, *dhin;
+    float *qkv, *o, *xhat1, *rstd1, *h1, *u, *xhat2, *rstd2, *h2;
+    float *dqkv, *dz1, *du, *df;
     float *ln1_part, *ln2_part;
 };
 
@@ -575,6 +436,7 @@ struct Plan {
     float* split_ws;
     size_t split_floats;
     float* packed;  // fragment-order copy of the parameters for the fused forward
+    float* packedT; // transposed GEMM weights for the fused backward
     size_t total;   // workspace floats
 };
 
@@ -597,24 +459,20 @@ inline size_t dw_split_floats(int Bm) {
 inline void carve_layer(WS& w, LayerBufs& L, int R, int rows) {
     L.qkv = w.take((size_t)R * 3 * D);
     L.o = w.take((size_t)rows * D);
-    L.a = w.take((size_t)rows * D);
     L.xhat1 = w.take((size_t)rows * D);
     L.rstd1 = w.take(rows);
     L.h1 = w.take((size_t)rows * D);
     L.u = w.take((size_t)rows * FF);
-    L.f = w.take((size_t)rows * D);
     L.xhat2 = w.take((size_t)rows * D);
     L.rstd2 = w.take(rows);
     L.h2 = w.take((size_t)rows * D);
     L.dqkv = w.take((size_t)R * 3 * D);
     L.dz1 = w.take((size_t)rows * D);
-    L.dout = w.take((size_t)rows * D);
-    L.dh1 = w.take((size_t)rows * D);
     L.du = w.take((size_t)rows * FF);
     L.df = w.take((size_t)rows * D);
-    L.dhin = w.take((size_t)R * D);
-    L.ln1_part = w.take((size_t)kLnBlocks * 2 * D);
-    L.ln2_part = w.take((size_t)kLnBlocks * 2 * D);
+    const size_t parts = (size_t)R / (S * 16);  // one partial per 16-sample workgroup of K6
+    L.ln1_part = w.take(parts * 2 * D);
+    L.ln2_part = w.take(parts * 2 * D);
 }
 
 inline Plan make_plan(int Bm, float* base) {
@@ -647,6 +505,7 @@ inline Plan make_plan(int Bm, float* base) {
     p.split_floats = dw_split_floats(Bm);
     p.split_ws = w.take(p.split_floats);
     p.packed = w.take(kOffs.o[kNumParams]);
+    p.packedT = w.take(pol::kPackedTFloats);
     p.total = w.off;
     return p;
 }
@@ -749,7 +608,6 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
 static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int Bg) {
     const int Bm = p.Bm, R = p.R, nblk = Bm / kHeadSamples;
     const LayerBufs &A = p.la, &C0 = p.lc0, &C1 = p.lc1;
-    auto L = [&](int trunk, int layer, int which) { return prm(c, layer_param(trunk, layer, which)); };
     const int ta = kActorTrunk, tc = kCriticTrunk;
     {
         HeadBwdArgs hb{c->params, A.h2, C1.h2, p.z_a, p.z_c, p.smp, c->loss_sums, p.dz_a, p.dz_c, p.dh_a, p.dh_c,
@@ -757,56 +615,23 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         hipLaunchKernelGGL(k_heads_bwd, dim3(nblk), dim3(1024), 0, st, hb);
         TR_CHECK(check_launch("k_heads_bwd"));
     }
-    // tail backward of a set of layers: gout = gradient wrt the layer output rows (compact for
-    // pruned layers), then dh_in (full [R][128]) = residual + Win^T dqkv
-    auto tail_bwd = [&](std::initializer_list<std::pair<const LayerBufs*, std::pair<int, int>>> layers,
-                        std::initializer_list<const float*> gouts) -> int {
-        const float* go[4];
-        int i = 0;
-        for (const float* gp : gouts) go[i++] = gp;
-        GemmBuilder g1, g2, g3, g4;
-        i = 0;
-        for (auto& lt : layers) {
-            const LayerBufs& B = *lt.first;
-            const int tr_ = lt.second.first, ly = lt.second.second;
-            const int rows = (&B == &C0) ? R : Bm;
-            hipLaunchKernelGGL(k_ln_bwd, dim3(kLnBlocks), dim3(256), 0, st, go[i], B.xhat2, B.rstd2, L(tr_, ly, N2W),
-                               B.df, nullptr, 1, 0, B.ln2_part, rows);
-            TR_CHECK(check_launch("k_ln_bwd"));
-            g1.add(B.df, D, L(tr_, ly, L2W), FF, B.du, FF, rows, FF, D, E_RELU_MASK, nullptr, B.u, FF);
-            // dh1 = d(LN2 input) (the residual branch, = df) + W1^T du
-            g2.add_res(B.du, FF, L(tr_, ly, L1W), D, B.dh1, D, rows, D, FF, B.df, D, 0, 0);
-            ++i;
-        }
-        TR_CHECK(run_gemm<L_DX>(g1, st));
-        TR_CHECK(run_gemm<L_DX>(g2, st));
-        for (auto& lt : layers) {
-            const LayerBufs& B = *lt.first;
-            const int tr_ = lt.second.first, ly = lt.second.second;
-            const int rows = (&B == &C0) ? R : Bm;
-            hipLaunchKernelGGL(k_ln_bwd, dim3(kLnBlocks), dim3(256), 0, st, B.dh1, B.xhat1, B.rstd1, L(tr_, ly, N1W),
-                               B.dz1, nullptr, 1, 0, B.ln1_part, rows);
-            TR_CHECK(check_launch("k_ln_bwd"));
-            g3.add(B.dz1, D, L(tr_, ly, OUTW), D, B.dout, D, rows, D, D, E_STORE);
-        }
-        TR_CHECK(run_gemm<L_DX>(g3, st));
-        for (auto& lt : layers) {
-            const LayerBufs& B = *lt.first;
-            const int tr_ = lt.second.first, ly = lt.second.second;
-            const int rows = (&B == &C0) ? R : Bm;
-            hipLaunchKernelGGL(k_attn_bwd, dim3(Bm * 32 / 256), dim3(256), 0, st, B.qkv, p.mask, B.dout, B.dqkv, Bm,
-                               rows == R ? 0 : 1);
-            TR_CHECK(check_launch("k_attn_bwd"));
-            // dh_in = Win^T dqkv + d(LN1 input) on the rows that carried the residual (token 4 if pruned)
-            g4.add_res(B.dqkv, 3 * D, L(tr_, ly, INW), D, B.dhin, D, R, D, 3 * D, B.dz1, D, rows == R ? 0 : S, S - 1);
-        }
-        TR_CHECK(run_gemm<L_DX>(g4, st));
-        return UAVHIP_OK;
-    };
-    TR_CHECK(tail_bwd({{&C1, {tc, 1}}}, {p.dh_c}));
-    TR_CHECK(tail_bwd({{&A, {ta, 0}}, {&C0, {tc, 0}}}, {p.dh_a, C1.dhin}));
-    hipLaunchKernelGGL(k_embed_bwd, dim3(nblk), dim3(256), 0, st, A.dhin, C0.dhin, p.e_a, p.e_c, p.xg, p.epart);
-    TR_CHECK(check_launch("k_embed_bwd"));
+    {
+        TR_CHECK(pol::policy_pack_transposed(c->params, p.packedT, st));
+        pol::BwdIO io{};
+        io.dh_top[0] = p.dh_a;
+        io.dh_top[1] = p.dh_c;
+        io.xg = p.xg;
+        io.mask = p.mask;
+        io.e[0] = p.e_a;
+        io.e[1] = p.e_c;
+        io.epart = p.epart;
+        const LayerBufs* lb[3] = {&A, &C0, &C1};
+        for (int i = 0; i < 3; ++i)
+            io.L[i] = pol::BwdLayerIO{lb[i]->qkv, lb[i]->xhat1, lb[i]->rstd1, lb[i]->u, lb[i]->xhat2, lb[i]->rstd2,
+                                      lb[i]->dqkv, lb[i]->dz1, lb[i]->du, lb[i]->df, lb[i]->ln1_part,
+                                      lb[i]->ln2_part};
+        TR_CHECK(pol::policy_backward_train(p.packed, p.packedT, io, Bm, st));
+    }
 
     // ---------------------------------------------------------------- weight gradients
     SegBatch sb{};
@@ -855,8 +680,8 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
     }
     // LayerNorm weights / biases
     auto ln_seg = [&](const float* part, int pw, int pb) {
-        seg(part, kOffs.o[pw], D, kLnBlocks, 2 * D);
-        seg(part + D, kOffs.o[pb], D, kLnBlocks, 2 * D);
+        seg(part, kOffs.o[pw], D, nblk, 2 * D);
+        seg(part + D, kOffs.o[pb], D, nblk, 2 * D);
     };
     ln_seg(A.ln1_part, layer_param(ta, 0, N1W), layer_param(ta, 0, N1B));
     ln_seg(A.ln2_part, layer_param(ta, 0, N2W), layer_param(ta, 0, N2B));
