@@ -53,25 +53,41 @@ __global__ __launch_bounds__(256) void k_score_pairs(uavhip_env env, const uint8
 }
 
 // ================================================================== wave-per-env kernels
-template <int TPL>
+// LT (multi-step launches whose tables fit): each wave copies its env's p_dmg table to LDS once
+// and the actions of 64 steps to one register, so nothing on the step-to-step dependency chain
+// waits for global memory.
+template <int TPL, bool LT>
 __global__ __launch_bounds__(kBlock) void k_env_step(uavhip_env env, const int8_t* __restrict__ actions, int T,
                                                      int auto_reset, float* __restrict__ obs_out,
                                                      double* __restrict__ reward_out, uint8_t* __restrict__ done_out,
                                                      double* __restrict__ info_out) {
+    extern __shared__ double s_tab[];
     const int lane = lane_id();
     const int e = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (e >= env.E) return;
     EnvRegs<TPL> R;
+    R.tab = s_tab + (threadIdx.x >> 6) * env.N * env.M;
     load_regs(R, env, e, lane);
+    if (LT) load_table(R, env, lane);
     const long long E = env.E;
-    for (int s = 0; s < T; ++s) {
-        const long long se = (long long)s * E + e;
-        step_once(R, env, e, lane, actions[se], auto_reset, obs_out ? obs_out + se * kObs : nullptr,
-                  reward_out ? reward_out + se : nullptr, done_out ? done_out + se : nullptr,
-                  info_out ? info_out + se * UAVHIP_INFO_COUNT : nullptr);
+    for (int s0 = 0; s0 < T; s0 += kWave) {
+        const int na = min(kWave, T - s0);
+        // action == 1 (assign) bits of the next 64 steps in an SGPR pair: the wait for this load
+        // happens here, not inside the step loop (where it would also wait for every store)
+        const int av = lane < na ? actions[(long long)(s0 + lane) * E + e] : 0;
+        const unsigned long long abits = ballot(av == 1);
+        for (int i = 0; i < na; ++i) {
+            const long long se = (long long)(s0 + i) * E + e;
+            step_once<TPL, LT>(R, env, e, lane, (int)((abits >> i) & 1ull), auto_reset,
+                               obs_out ? obs_out + se * kObs : nullptr, reward_out ? reward_out + se : nullptr,
+                               done_out ? done_out + se : nullptr,
+                               info_out ? info_out + se * UAVHIP_INFO_COUNT : nullptr);
+        }
     }
     store_regs(R, env, e, lane);
 }
+constexpr int kTableMinSteps = 4;                // below this the LDS table costs more than it saves
+constexpr size_t kTableMaxBytes = 64 * 1024;     // per workgroup (4 envs)
 
 template <int TPL>
 __global__ __launch_bounds__(kBlock) void k_env_reset(uavhip_env env, const uint8_t* __restrict__ mask, int episode,
@@ -222,6 +238,16 @@ extern "C" int uavhip_env_step(const uavhip_env* env, const int8_t* actions, int
     int rc = validate(env, true);
     if (rc) return rc;
     if (!actions || T <= 0) { set_error("actions NULL or T <= 0 (T=%d)", T); return UAVHIP_EINVAL; }
-    UAVHIP_LAUNCH_TPL(k_env_step, *env, actions, (int)T, (int)auto_reset, obs_out, reward, done, info);
+    const size_t tab = (size_t)kWavesPerBlock * env->N * env->M * sizeof(double);
+    const bool lt = T >= kTableMinSteps && tab <= kTableMaxBytes;
+    const dim3 grid(wave_grid(env->E)), block(kBlock);
+    hipStream_t st = (hipStream_t)stream;
+    if (env->M <= kWave) {
+        if (lt) hipLaunchKernelGGL((k_env_step<1, true>), grid, block, tab, st, *env, actions, (int)T, (int)auto_reset, obs_out, reward, done, info);
+        else hipLaunchKernelGGL((k_env_step<1, false>), grid, block, 0, st, *env, actions, (int)T, (int)auto_reset, obs_out, reward, done, info);
+    } else {
+        if (lt) hipLaunchKernelGGL((k_env_step<2, true>), grid, block, tab, st, *env, actions, (int)T, (int)auto_reset, obs_out, reward, done, info);
+        else hipLaunchKernelGGL((k_env_step<2, false>), grid, block, 0, st, *env, actions, (int)T, (int)auto_reset, obs_out, reward, done, info);
+    }
     return check_launch("k_env_step");
 }

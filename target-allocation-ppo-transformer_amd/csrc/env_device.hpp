@@ -169,7 +169,34 @@ struct EnvRegs {
     double pd_cur, pp_cur;  // pair probabilities of the current pointer (u, t)
     // observation window: element i (< 64) on lane i in w0, element 64 + i (i < 6) in w1
     float w0, w1;
+    // multi-step launches (LT = true): this wave's LDS copy of the active scene's p_dmg table
+    double* tab;
+    // loop-invariant divisors and their correctly rounded reciprocals (div_by)
+    double den_c, rcp_c, den_v, rcp_v, rcp_m;
+    double rcp_n;  // lane l: RN(1 / (l + 1)), the info averages' divisors 1..64
 };
+
+// a / b, correctly rounded, from y = RN(1 / b) (Markstein's theorem: q = RN(a y) is within 1 ulp
+// of a / b, r = a - b q is exact by FMA, and RN(q + r y) = RN(a / b) without over/underflow). Three
+// VALU ops instead of the ~10 of an IEEE fp64 division -- the step kernel is VALU-issue bound.
+__device__ __forceinline__ double div_by(double a, double b, double y) {
+    const double q = a * y;
+    const double r = fma(-b, q, a);
+    return fma(r, y, q);
+}
+
+template <int TPL>
+__device__ __forceinline__ void set_scene_divisors(EnvRegs<TPL>& R) {
+    R.den_c = R.tot_cost + 1e-6;
+    R.rcp_c = 1.0 / R.den_c;
+    R.den_v = R.tot_val + 1e-6;
+    R.rcp_v = 1.0 / R.den_v;
+}
+template <int TPL>
+__device__ __forceinline__ void set_step_divisors(EnvRegs<TPL>& R, const uavhip_env& env, int lane) {
+    R.rcp_m = 1.0 / (double)env.M;
+    R.rcp_n = 1.0 / (double)(lane + 1);
+}
 
 template <int TPL>
 __device__ __forceinline__ double pick(const double (&a)[TPL], int k, int l) {
@@ -184,6 +211,11 @@ __device__ __forceinline__ int pick(const int (&a)[TPL], int k, int l) {
     return v;
 }
 
+// Wait for this wave's outstanding memory operations. Called where register state was just
+// loaded: a load still in flight at a loop back-edge makes the compiler wait for vmcnt(0) (all
+// stores included) at every later use inside the step loop.
+__device__ __forceinline__ void drain_loads() { __builtin_amdgcn_s_waitcnt(0); }
+
 // Scene-dependent per-lane values (after a reset or a scene switch).
 template <int TPL>
 __device__ void load_scene_regs(EnvRegs<TPL>& R, const uavhip_env& env, int lane) {
@@ -194,6 +226,7 @@ __device__ void load_scene_regs(EnvRegs<TPL>& R, const uavhip_env& env, int lane
     }
     R.ucost = lane < env.N ? env.uav_cost[R.sb * env.N + lane] : 0.0;
     R.ppen = lane < env.N ? env.p_pen[R.sb * env.N + lane] : 0.0;
+    drain_loads();
 }
 
 __device__ __forceinline__ float sel14(const float (&f)[kDim], int j) {
@@ -213,9 +246,9 @@ __device__ void push_obs(EnvRegs<TPL>& R, int lane) {
     const double nhf = pick(R.nhf, tk, tl);
     const double nhp = pick(R.nhp, tk, tl);
     const double ucost = readlane_d(R.ucost, R.u);
-    const double chi_c = R.asg_cost / (R.tot_cost + 1e-6);
-    const double chi_v = R.cov_val / (R.tot_val + 1e-6);
-    const double chi_mc = tc / (R.tot_cost + 1e-6);
+    const double chi_c = div_by(R.asg_cost, R.den_c, R.rcp_c);
+    const double chi_v = div_by(R.cov_val, R.den_v, R.rcp_v);
+    const double chi_mc = div_by(tc, R.den_c, R.rcp_c);
     const double pjp = 1.0 - nhf;
     const double pjp_pure = 1.0 - nhp;
     const double prev_rev = pjp * val;
@@ -242,11 +275,12 @@ __device__ void push_obs(EnvRegs<TPL>& R, int lane) {
     R.w1 = lane < kObs - kWave ? nw1 : 0.0f;
 }
 
-// Pair probabilities of the current pointer (u, t).
-template <int TPL>
+// Pair probabilities of the current pointer (u, t). LT: p_dmg from the wave's LDS table (a short
+// LDS round trip instead of a global-memory one on the step-to-step dependency chain).
+template <int TPL, bool LT = false>
 __device__ __forceinline__ void load_cur_pair(EnvRegs<TPL>& R, const uavhip_env& env) {
     if (R.u < env.N) {
-        R.pd_cur = env.p_dmg[(R.sb * env.N + R.u) * env.M + R.t];
+        R.pd_cur = LT ? R.tab[R.u * env.M + R.t] : env.p_dmg[(R.sb * env.N + R.u) * env.M + R.t];
         R.pp_cur = readlane_d(R.ppen, R.u);
     } else {
         R.pd_cur = 0.0;
@@ -254,10 +288,23 @@ __device__ __forceinline__ void load_cur_pair(EnvRegs<TPL>& R, const uavhip_env&
     }
 }
 
-// uav_env.py:42-63,175-182: reset allocation and window, first observation at (0, 0).
+// Copy the active scene's p_dmg table [N][M] into the wave's LDS table (wave-private: LDS
+// operations of one wave complete in order, so no barrier is needed before its own reads).
 template <int TPL>
-__device__ void reset_regs(EnvRegs<TPL>& R, const uavhip_env& env, int lane) {
-    load_scene_regs(R, env, lane);
+__device__ void load_table(EnvRegs<TPL>& R, const uavhip_env& env, int lane) {
+    const int NM = env.N * env.M;
+    const double* src = env.p_dmg + R.sb * NM;
+    for (int i = lane; i < NM; i += kWave) R.tab[i] = src[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// uav_env.py:42-63,175-182: reset allocation and window, first observation at (0, 0).
+// scene: (re)load the scene-dependent registers and totals (after a scene switch or when starting
+// from memory); a state-only reset within a launch keeps them.
+template <int TPL, bool LT = false>
+__device__ void reset_regs(EnvRegs<TPL>& R, const uavhip_env& env, int lane, bool scene = true) {
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
         R.nhf[k] = 1.0;
@@ -269,20 +316,24 @@ __device__ void reset_regs(EnvRegs<TPL>& R, const uavhip_env& env, int lane) {
     R.u = 0; R.t = 0; R.ncov = 0; R.nasg = 0;
     R.r = 0.0; R.J = 0.0; R.asg_cost = 0.0; R.cov_val = 0.0;
     R.sum_pd = 0.0; R.sum_pf = 0.0;
-    // total_swarm_cost accumulated in generation order (uav_env.py:118); total value in list order (:198)
-    double tc = 0.0;
-    for (int j = 0; j < env.N; ++j) tc = tc + readlane_d(R.ucost, j);
-    double tv = 0.0;
-    for (int j = 0; j < env.M; ++j) {
-        double v = readlane_d(R.val[0], j & 63);
-        if (TPL > 1 && j >= kWave) v = readlane_d(R.val[TPL - 1], j & 63);
-        tv = tv + v;
+    if (scene) {
+        load_scene_regs(R, env, lane);
+        // total_swarm_cost accumulated in generation order (uav_env.py:118); total value in list order (:198)
+        double tc = 0.0;
+        for (int j = 0; j < env.N; ++j) tc = tc + readlane_d(R.ucost, j);
+        double tv = 0.0;
+        for (int j = 0; j < env.M; ++j) {
+            double v = readlane_d(R.val[0], j & 63);
+            if (TPL > 1 && j >= kWave) v = readlane_d(R.val[TPL - 1], j & 63);
+            tv = tv + v;
+        }
+        R.tot_cost = tc;
+        R.tot_val = tv;
+        set_scene_divisors(R);
     }
-    R.tot_cost = tc;
-    R.tot_val = tv;
     R.w0 = 0.0f;
     R.w1 = 0.0f;
-    load_cur_pair(R, env);
+    load_cur_pair<TPL, LT>(R, env);
     push_obs(R, lane);
 }
 
@@ -325,6 +376,8 @@ __device__ void load_regs(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lan
     R.cov_val = ds[UAVHIP_DST_COV_VALUE];
     R.tot_cost = ds[UAVHIP_DST_TOTAL_COST];
     R.tot_val = ds[UAVHIP_DST_TOTAL_VALUE];
+    set_scene_divisors(R);
+    set_step_divisors(R, env, lane);
     R.sum_pd = ds[UAVHIP_DST_SUM_PDMG];
     R.sum_pf = ds[UAVHIP_DST_SUM_PFIN];
     const float* w = env.window + (long long)e * kObs;
@@ -333,6 +386,7 @@ __device__ void load_regs(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lan
     // the current pair's p_dmg was cached by the previous launch: one independent load round
     R.pd_cur = ds[UAVHIP_DST_PD_CUR];
     R.pp_cur = R.u < N ? readlane_d(R.ppen, R.u) : 0.0;
+    drain_loads();
 }
 
 template <int TPL>
@@ -388,8 +442,9 @@ __device__ __forceinline__ void write_obs(float* o, float w0, float w1, int lane
 template <int TPL>
 __device__ void write_info(const EnvRegs<TPL>& R, const uavhip_env& env, double is_valid, double* o, int lane) {
     const int cnt = R.nasg;
-    const double avg_d = cnt > 0 ? R.sum_pd / (double)cnt : 0.0;
-    const double avg_f = cnt > 0 ? R.sum_pf / (double)cnt : 0.0;
+    const double y = cnt > 0 ? readlane_d(R.rcp_n, cnt - 1) : 0.0;
+    const double avg_d = cnt > 0 ? div_by(R.sum_pd, (double)cnt, y) : 0.0;
+    const double avg_f = cnt > 0 ? div_by(R.sum_pf, (double)cnt, y) : 0.0;
     double v = 0.0;
     v = lane == UAVHIP_INFO_J ? R.J : v;
     v = lane == UAVHIP_INFO_NUM_ASSIGNED ? (double)R.ncov : v;
@@ -404,7 +459,7 @@ __device__ void write_info(const EnvRegs<TPL>& R, const uavhip_env& env, double 
 
 // One UAVEnv.step (uav_env.py:295-435) on register state. No scene generation on this path: a
 // full reset flips to the pre-generated spare scene (scene_buffers == 2).
-template <int TPL>
+template <int TPL, bool LT = false>
 __device__ void step_once(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lane, int a, int auto_reset,
                           float* obs_o, double* rew_o, uint8_t* done_o, double* info_o) {
     const int N = env.N, M = env.M;
@@ -446,7 +501,7 @@ __device__ void step_once(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lan
         const double ucost_u = readlane_d(R.ucost, u);
         const double cost_all = R.asg_cost + ucost_u;  // exact for costs in {1, 1.25}
         const double J = rev - (env.prm[UAVHIP_PRM_OMEGA] * cost_all);
-        const double new_r = (ncov_new == M) ? 2.0 * J : J * ((double)ncov_new / (double)M);
+        const double new_r = (ncov_new == M) ? 2.0 * J : J * div_by((double)ncov_new, (double)M, R.rcp_m);
         if (new_r >= prev_r) {
             const double val_t = pick(R.val, tk, tl);
 #pragma unroll
@@ -488,22 +543,25 @@ __device__ void step_once(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lan
         if (done_o) *done_o = done ? 1 : 0;
     }
     if (!done) {
-        load_cur_pair(R, env);
+        load_cur_pair<TPL, LT>(R, env);
         push_obs(R, lane);
         if (obs_o) write_obs(obs_o, R.w0, R.w1, lane);
     } else if (auto_reset) {
         R.ep += 1;
         const int P = env.full_reset_period;
+        bool flipped = false;
         if (P > 0 && (R.ep % P) == 0) {  // main_train.py:79 full_reset cadence
             if (env.scene_buffers == 2 && !R.stale) {
                 R.sel ^= 1;
                 R.stale = 1;
                 R.sb = (long long)R.sel * env.E + e;
+                if (LT) load_table(R, env, lane);
+                flipped = true;
             } else {
                 R.err |= 2;  // no fresh spare: keep the scene (state-only reset)
             }
         }
-        reset_regs(R, env, lane);
+        reset_regs<TPL, LT>(R, env, lane, flipped);
         if (obs_o) write_obs(obs_o, R.w0, R.w1, lane);
     } else {
         if (obs_o) write_obs(obs_o, 0.0f, 0.0f, lane);  // _get_obs returns zeros when done (:188-189)
