@@ -266,7 +266,7 @@ typedef struct uavhip_ppo {
     float* adam_m;       /* [n_floats] exp_avg */
     float* adam_v;       /* [n_floats] exp_avg_sq */
     double* adam_step;   /* [1] device step counter (shared by all groups) */
-    float* workspace;    /* [uavhip_ppo_workspace_floats(minibatch)] */
+    float* workspace;    /* [uavhip_ppo_workspace_floats(minibatch)], zero-filled before first use */
     float* loss_sums;    /* [4] written by FORWARD: sums over this rank's samples of min(s1, s2),
                             (v - R)^2, (v_clip - R)^2, entropy; BACKWARD reads them (all-reduced) */
     double* stats;       /* [4] += loss_actor, loss_critic, entropy, 1 per step (nullable) */

@@ -91,7 +91,11 @@ template <int BM>
 __device__ __forceinline__ TileInfo decode_tile(const GemmBatch& gb, int tile) {
     TileInfo ti;
     int pi = 0;
-    while (pi + 1 < gb.n && tile >= gb.p[pi + 1].tile_begin) ++pi;
+    for (int hi = gb.n; hi - pi > 1;) {  // binary search: each probe is a kernarg load
+        const int mid = (pi + hi) >> 1;
+        if (tile >= gb.p[mid].tile_begin) pi = mid;
+        else hi = mid;
+    }
     const GemmProb& P = gb.p[pi];
     const int u = tile - P.tile_begin;
     const int tm_n = P.M / BM, tn_n = P.tiles_n, per_split = tm_n * tn_n;

@@ -499,6 +499,71 @@ __device__ void head_mlp(Smem& sm, const float* __restrict__ P, const APre<4>& p
     __syncthreads();
 }
 
+// Categorical(softmax(logits)) as torch.distributions evaluates it (transformer_net.py:124-144):
+// p = softmax(l); p /= sum(p); lc = log(clamp(p, eps, 1 - eps)); logp = lc[a]; ent = -sum(lc * p).
+struct CatVals {
+    float y0, y1, s, p0, p1, c0, c1, lc0, lc1;
+};
+__device__ __forceinline__ CatVals categorical(float l0, float l1) {
+    CatVals c;
+    const float m = fmaxf(l0, l1);
+    const float e0 = expf(l0 - m), e1 = expf(l1 - m);
+    const float den = e0 + e1;
+    c.y0 = e0 / den;
+    c.y1 = e1 / den;
+    c.s = c.y0 + c.y1;
+    c.p0 = c.y0 / c.s;
+    c.p1 = c.y1 / c.s;
+    const float eps = 1.1920928955078125e-07f;
+    c.c0 = fminf(fmaxf(c.p0, eps), 1.f - eps);
+    c.c1 = fminf(fmaxf(c.p1, eps), 1.f - eps);
+    c.lc0 = logf(c.c0);
+    c.lc1 = logf(c.c1);
+    return c;
+}
+
+// Training mode: relu(head.0) rows of the 16 samples (sm.z) -> z [Bm][64].
+__device__ __forceinline__ void store_hidden(const Smem& sm, float* __restrict__ z, int b0) {
+    if (threadIdx.x < SPW * HID / 4) {
+        const int p = threadIdx.x / (HID / 4), q = threadIdx.x % (HID / 4);
+        *reinterpret_cast<f32x4*>(z + (size_t)(b0 + p) * HID + 4 * q) =
+            *reinterpret_cast<const f32x4*>(sm.z + p * LDZ + 4 * q);
+    }
+}
+
+// Training mode: per-sample PPO loss terms of ppo.py:148-160 (Categorical as torch evaluates it,
+// transformer_net.py:124-144) and their workgroup sums in sample order -> fpart[blk][4];
+// logits / value -> smp[b][5..7] for the backward.
+__device__ void loss_partials(Smem& sm, const TrainIO& io, int b0) {
+    float* red = sm.x;  // free after the embeddings
+    if (threadIdx.x < SPW) {
+        const int p = threadIdx.x;
+        float* o = io.smp + (size_t)(b0 + p) * 8;  // o[0..4] written by this thread at kernel start
+        const float l0 = sm.logits[2 * p], l1 = sm.logits[2 * p + 1], v = sm.value[p];
+        o[5] = l0;
+        o[6] = l1;
+        o[7] = v;
+        const CatVals c = categorical(l0, l1);
+        const float logp = o[0] != 0.f ? c.lc1 : c.lc0;
+        const float ratio = expf(logp - o[1]);
+        const float A = o[4];
+        const float s1 = ratio * A;
+        const float s2 = fminf(fmaxf(ratio, 1.f - io.eps_clip), 1.f + io.eps_clip) * A;
+        const float R = o[3], ov = o[2];
+        const float vc = ov + fminf(fmaxf(v - ov, -io.eps_clip), io.eps_clip);
+        red[4 * p + 0] = fminf(s1, s2);
+        red[4 * p + 1] = (v - R) * (v - R);
+        red[4 * p + 2] = (vc - R) * (vc - R);
+        red[4 * p + 3] = -(c.lc0 * c.p0 + c.lc1 * c.p1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        float acc = 0.f;
+        for (int i = 0; i < SPW; ++i) acc += red[4 * i + threadIdx.x];
+        io.fpart[blockIdx.x * 4 + threadIdx.x] = acc;
+    }
+}
+
 template <bool TR>
 __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict__ P, const float* __restrict__ states,
                                                          int B, const int8_t* __restrict__ actions_in, uint64_t seed,
@@ -548,10 +613,11 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     __syncthreads();
     encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0);
     APre<4> ph;
-    if (!TR && wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
+    if (wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
     __syncthreads();
     PTR(3);
-    if (!TR) head_mlp<kActorHead, 2>(sm, P, ph, sm.logits);
+    head_mlp<kActorHead, 2>(sm, P, ph, sm.logits);
+    if (TR) store_hidden(sm, io.z[0], b0);  // before the critic's LayerNorm partials reuse sm.z
     PTR(4);
     // critic trunk (2 layers) + head
     embed<kCriticTrunk, TR>(sm, P, io.e[1], io.h0[1], b0);
@@ -561,12 +627,16 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
     __syncthreads();
     encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0);
-    if (TR) return;  // heads + loss run in train.hip's k_heads_fwd on the stored trunk outputs
     if (wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
     __syncthreads();
     PTR(5);
     head_mlp<kCriticHead, 1>(sm, P, ph, sm.value);
     PTR(6);
+    if (TR) {
+        store_hidden(sm, io.z[1], b0);
+        loss_partials(sm, io, b0);
+        return;
+    }
     // Categorical(softmax(logits)): sample / log_prob / entropy (transformer_net.py:118-122)
     if (threadIdx.x < SPW) {
         const int p = threadIdx.x, b = b0 + p;
@@ -849,11 +919,95 @@ __device__ void embed_bwd(Smem& sm, const float* __restrict__ e, float* __restri
     }
 }
 
-__device__ __forceinline__ void load_top_grad(Smem& sm, const float* __restrict__ dh, int b0) {
-    for (int i = threadIdx.x; i < SPW * D / 4; i += NTHR) {
-        const int p = i / (D / 4), q = i % (D / 4);
-        st4(sm.h + ((S - 1) * SPW + p) * LDH + 4 * q, ld4(dh + (size_t)(b0 + p) * D + 4 * q));
+// Loss gradients of ppo.py:148-169 per sample (torch's min / max / clamp backward conventions:
+// ties send half the gradient to each side, clamp passes it on the closed interval), then the
+// heads' backward: dz = relu'(z) (W2^T g) for both heads -> io.dz, LDS (actor: sm.z, critic:
+// sm.ctx + 64, both [16][LDZ]), and the head.2 weight / bias partials of the 16 samples.
+__device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io, int b0) {
+    float* gs = sm.ctx;                  // [16][4]: dlogit0, dlogit1, dvalue
+    float* dzc = sm.ctx + 64;            // critic dz rows
+    const float inv = 1.0f / (float)io.Bg;
+    const float tot0 = io.tot[0], tot1 = io.tot[1], tot2 = io.tot[2], tot3 = io.tot[3];
+    if (threadIdx.x < SPW) {
+        const int p = threadIdx.x;
+        const float* o = io.smp + (size_t)(b0 + p) * 8;
+        const int act = o[0] != 0.f;
+        const CatVals c = categorical(o[5], o[6]);
+        const float logp = act ? c.lc1 : c.lc0;
+        const float ratio = expf(logp - o[1]);
+        const float A = o[4], lo = 1.f - io.eps_clip, hi = 1.f + io.eps_clip;
+        const float s1 = ratio * A;
+        const float s2 = fminf(fmaxf(ratio, lo), hi) * A;
+        const float gmin = -inv;  // d(-mean(min)) / d min_i
+        const float g1 = s1 < s2 ? gmin : (s1 == s2 ? 0.5f * gmin : 0.f);
+        const float g2 = s2 < s1 ? gmin : (s1 == s2 ? 0.5f * gmin : 0.f);
+        const float gr = g1 * A + ((ratio >= lo && ratio <= hi) ? g2 * A : 0.f);
+        const float glogp = gr * ratio;
+        const float gent = -io.entropy_coef * inv;
+        // back through lc = log(clamp(p)), ent = -sum(lc * p), p = y / s, s = y0 + y1, y = softmax
+        float glc0 = -gent * c.p0, glc1 = -gent * c.p1;
+        if (act) glc1 += glogp; else glc0 += glogp;
+        const float eps = 1.1920928955078125e-07f;
+        const float gp0 = -gent * c.lc0 + ((c.p0 >= eps && c.p0 <= 1.f - eps) ? glc0 / c.c0 : 0.f);
+        const float gp1 = -gent * c.lc1 + ((c.p1 >= eps && c.p1 <= 1.f - eps) ? glc1 / c.c1 : 0.f);
+        const float gsum = -(gp0 * c.y0 + gp1 * c.y1) / (c.s * c.s);
+        const float gy0 = gp0 / c.s + gsum, gy1 = gp1 / c.s + gsum;
+        const float dot = gy0 * c.y0 + gy1 * c.y1;
+        // value: 0.5 * max(mean((v-R)^2), mean((vc-R)^2))
+        const float L1 = tot1 * inv, L2 = tot2 * inv;
+        const float v = o[7], R = o[3], ov = o[2];
+        const float dv = v - ov;
+        const float vc = ov + fminf(fmaxf(dv, -io.eps_clip), io.eps_clip);
+        const float w1 = L1 > L2 ? 1.f : (L1 == L2 ? 0.5f : 0.f);
+        const float w2 = L2 > L1 ? 1.f : (L1 == L2 ? 0.5f : 0.f);
+        gs[4 * p + 0] = c.y0 * (gy0 - dot);
+        gs[4 * p + 1] = c.y1 * (gy1 - dot);
+        gs[4 * p + 2] = io.value_coef * (w1 * 2.f * (v - R) * inv +
+                                         ((dv >= -io.eps_clip && dv <= io.eps_clip) ? w2 * 2.f * (vc - R) * inv : 0.f));
+        if (p == 0 && blockIdx.x == 0 && io.stats) {
+            io.stats[0] += (double)(-tot0 * inv);
+            io.stats[1] += (double)fmaxf(L1, L2);
+            io.stats[2] += (double)(tot3 * inv);
+            io.stats[3] += 1.0;
+        }
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * SPW * HID; i += NTHR) {
+        const int trunk = i / (SPW * HID), p = (i / HID) % SPW, j = i % HID;
+        const float* W2 = P + kOffs.o[(trunk ? kCriticHead : kActorHead) + 2];
+        const float z = io.z[trunk][(size_t)(b0 + p) * HID + j];
+        const float g = trunk ? W2[j] * gs[4 * p + 2] : W2[j] * gs[4 * p] + W2[HID + j] * gs[4 * p + 1];
+        const float dz = z > 0.f ? g : 0.f;
+        io.dz[trunk][(size_t)(b0 + p) * HID + j] = dz;
+        (trunk ? dzc : sm.z)[p * LDZ + j] = dz;
+    }
+    // head.2 partials, summed over the 16 samples in order: dW2[o][j] = sum g_o z_j, db2[o] = sum g_o
+    if (threadIdx.x < kHeadPart) {
+        const int i = threadIdx.x;
+        float acc = 0.f;
+        if (i < 2 * HID) {
+            const int o = i / HID, j = i % HID;
+            for (int p = 0; p < SPW; ++p) acc += gs[4 * p + o] * io.z[0][(size_t)(b0 + p) * HID + j];
+        } else if (i < 2 * HID + 2) {
+            for (int p = 0; p < SPW; ++p) acc += gs[4 * p + i - 2 * HID];
+        } else if (i < 3 * HID + 2) {
+            const int j = i - 2 * HID - 2;
+            for (int p = 0; p < SPW; ++p) acc += gs[4 * p + 2] * io.z[1][(size_t)(b0 + p) * HID + j];
+        } else if (i < kHeadPartN) {
+            for (int p = 0; p < SPW; ++p) acc += gs[4 * p + 2];
+        }
+        io.hpart[(size_t)blockIdx.x * kHeadPart + i] = acc;
+    }
+}
+
+// dL/d(trunk output) of the 16 samples = head.0^T dz (MFMA, K = 64; one 16-feature tile per
+// wave) -> sm.h rows of column tile 4, the top gradient of the trunk's last layer.
+__device__ __forceinline__ void head_input_grad(Smem& sm, const float* __restrict__ W0T, const float* dz) {
+    const int wv = threadIdx.x >> 6, l = lane_id(), i16 = l & 15, g = l >> 4;
+    f32x4 acc[1];
+    zero(acc);
+    gemm_tile<1, 4, 4>(acc, prefetch<4>(W0T, HID, 16 * wv, 0), W0T, HID, 16 * wv, 0, dz, LDZ, 0);
+    st4(sm.h + ((S - 1) * SPW + i16) * LDH + 16 * wv + 4 * g, acc[0]);
 }
 
 __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restrict__ P, const float* __restrict__ PT,
@@ -865,38 +1019,22 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
         st4(sm.x + t * LDX + 4 * q, ld4(io.xg + (size_t)trow(t, b0) * 16 + 4 * q));
     }
     if (threadIdx.x < SPW * S) sm.mask[threadIdx.x] = io.mask[(size_t)b0 * S + threadIdx.x] != 0.f;
-    // critic: layer 1 (pruned), layer 0, embedding
-    load_top_grad(sm, io.dh_top[1], b0);
+    heads_bwd(sm, P, io, b0);
+    __syncthreads();
+    // critic: head.0, layer 1 (pruned), layer 0, embedding
+    head_input_grad(sm, PT + kHeadT + D * HID, sm.ctx + 64);
     __syncthreads();
     bwd_layer<kCriticTrunk, 1, true>(sm, P, PT + 2 * kLayerT, io.L[2], b0);
     bwd_layer<kCriticTrunk, 0, false>(sm, P, PT + 1 * kLayerT, io.L[1], b0);
     embed_bwd(sm, io.e[1], io.epart + ((size_t)blockIdx.x * 2 + 1) * kEmbPart, b0);
     __syncthreads();
-    // actor: layer 0 (pruned), embedding
-    load_top_grad(sm, io.dh_top[0], b0);
+    // actor: head.0, layer 0 (pruned), embedding
+    head_input_grad(sm, PT + kHeadT, sm.z);
     __syncthreads();
     bwd_layer<kActorTrunk, 0, true>(sm, P, PT, io.L[0], b0);
     embed_bwd(sm, io.e[0], io.epart + (size_t)blockIdx.x * 2 * kEmbPart, b0);
 }
 
-// flat (state_dict order) -> per layer [in_proj^T | out_proj^T | linear1^T | linear2^T] in
-// fragment order: packedT[((r/16) * K/16 + k/16) * 256 + (r%16 + 16 ((k%16)/4)) * 4 + k%4] = W[k][r]
-__global__ __launch_bounds__(256) void k_policy_pack_t(const float* __restrict__ flat, float* __restrict__ pt) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= kPackedTFloats) return;
-    const int li = i / kLayerT, loc = i - li * kLayerT;
-    const int trunk = li == 0 ? kActorTrunk : kCriticTrunk, layer = li == 2 ? 1 : 0;
-    int which, base, Rt, Kt;
-    if (loc < kTWo) { which = INW; base = kTWin; Rt = D; Kt = 3 * D; }
-    else if (loc < kTW1) { which = OUTW; base = kTWo; Rt = D; Kt = D; }
-    else if (loc < kTW2) { which = L1W; base = kTW1; Rt = D; Kt = FF; }
-    else { which = L2W; base = kTW2; Rt = FF; Kt = D; }
-    const int m = loc - base;
-    const int j = m & 3, lane = (m >> 2) & 63, blk = m >> 8, KBt = Kt / 16;
-    const int kb = blk % KBt, rt = blk / KBt;
-    const int r = 16 * rt + (lane & 15), k = 16 * kb + 4 * (lane >> 4) + j;
-    pt[i] = flat[kOffs.o[layer_param(trunk, layer, which)] + k * Rt + r];
-}
 
 }  // namespace pol
 }  // namespace uavhip
@@ -916,27 +1054,64 @@ int policy_backward_train(const float* packed, const float* packedT, const BwdIO
     return check_launch("k_policy_backward");
 }
 
-int policy_pack_transposed(const float* flat, float* packedT, hipStream_t st) {
-    hipLaunchKernelGGL(k_policy_pack_t, dim3((kPackedTFloats + 255) / 256), dim3(256), 0, st, flat, packedT);
-    return check_launch("k_policy_pack_t");
-}
 
-// flat (state_dict order, plain layout) -> packed (GEMM weights in MFMA fragment order)
-__global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ flat, float* __restrict__ packed) {
+// flat (state_dict order, plain layout) -> packed (GEMM weights in MFMA fragment order) and, when
+// packedT is given, the backward's transposed copies: per layer [in_proj^T | out_proj^T |
+// linear1^T | linear2^T], then head.0^T of both heads, with packedT[((r/16) * K/16 + k/16) * 256 +
+// (r%16 + 16 ((k%16)/4)) * 4 + k%4] = W[k][r]. One thread per output float4.
+__global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ flat, float* __restrict__ packed,
+                                                     float* __restrict__ packedT) {
+    constexpr int nq = kOffs.o[kNumParams] / 4;
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= kOffs.o[kNumParams]) return;
-    int q = 0;
-    while (q + 1 < kNumParams && i >= kOffs.o[q + 1]) ++q;
-    const int local = i - kOffs.o[q], K = kTileK[q];
-    if (K == 0 || local >= kSizes[q]) {
-        packed[i] = flat[i];
+    if (i < nq) {
+        const int f = 4 * i;
+        int lo = 0, hi = kNumParams;  // parameter q: kOffs.o[q] <= f < kOffs.o[q + 1]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (f >= kOffs.o[mid]) lo = mid;
+            else hi = mid;
+        }
+        const int local = f - kOffs.o[lo], K = kTileK[lo];
+        int src = f;
+        if (K != 0 && local < kSizes[lo]) {  // fragment order of [R][K]: float4 = 4 consecutive k
+            const int lane = (local >> 2) & 63, blk = local >> 8, KB = K / 16;
+            const int kb = blk % KB, rt = blk / KB;
+            src = kOffs.o[lo] + (16 * rt + (lane & 15)) * K + 16 * kb + 4 * (lane >> 4);
+        }
+        *reinterpret_cast<f32x4*>(packed + f) = *reinterpret_cast<const f32x4*>(flat + src);
         return;
     }
-    // packed index ((r/16 * K/16 + k/16) * 64 + r%16 + 16 * ((k%16)/4)) * 4 + k%4 (uavhip.h)
-    const int j = local & 3, lane = (local >> 2) & 63, blk = local >> 8, KB = K / 16;
-    const int kb = blk % KB, rt = blk / KB;
-    const int r = 16 * rt + (lane & 15), k = 16 * kb + 4 * (lane >> 4) + j;
-    packed[i] = flat[kOffs.o[q] + r * K + k];
+    if (!packedT || i >= nq + kPackedTFloats / 4) return;
+    const int idx = 4 * (i - nq);
+    int src, m, Rt, Kt;
+    if (idx < kHeadT) {
+        const int li = idx / kLayerT, loc = idx - li * kLayerT;
+        const int trunk = li == 0 ? kActorTrunk : kCriticTrunk, layer = li == 2 ? 1 : 0;
+        int which, base;
+        if (loc < kTWo) { which = INW; base = kTWin; Rt = D; Kt = 3 * D; }
+        else if (loc < kTW1) { which = OUTW; base = kTWo; Rt = D; Kt = D; }
+        else if (loc < kTW2) { which = L1W; base = kTW1; Rt = D; Kt = FF; }
+        else { which = L2W; base = kTW2; Rt = FF; Kt = D; }
+        src = kOffs.o[layer_param(trunk, layer, which)];
+        m = loc - base;
+    } else {  // head.0 weight [64][128] of the actor / critic head, transposed
+        const int h = (idx - kHeadT) / (D * HID);
+        src = kOffs.o[h ? kCriticHead : kActorHead];
+        m = idx - kHeadT - h * D * HID;
+        Rt = D;
+        Kt = HID;
+    }
+    const int lane = (m >> 2) & 63, blk = m >> 8, KBt = Kt / 16;
+    const int kb = blk % KBt, rt = blk / KBt;
+    const int r = 16 * rt + (lane & 15), k = 16 * kb + 4 * (lane >> 4);
+    const float* w = flat + src + r;
+    *reinterpret_cast<f32x4*>(packedT + idx) = f32x4{w[k * Rt], w[(k + 1) * Rt], w[(k + 2) * Rt], w[(k + 3) * Rt]};
+}
+
+int policy_pack_train(const float* flat, float* packed, float* packedT, hipStream_t st) {
+    const int items = kOffs.o[kNumParams] / 4 + kPackedTFloats / 4;
+    hipLaunchKernelGGL(k_policy_pack, dim3((items + 255) / 256), dim3(256), 0, st, flat, packed, packedT);
+    return check_launch("k_policy_pack");
 }
 }  // namespace pol
 }  // namespace uavhip
@@ -946,8 +1121,9 @@ extern "C" int uavhip_policy_pack(const float* flat, float* packed, uavhip_strea
         set_error("uavhip_policy_pack: NULL pointer");
         return UAVHIP_EINVAL;
     }
-    const int n = pol::kOffs.o[pol::kNumParams];
-    hipLaunchKernelGGL(pol::k_policy_pack, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, flat, packed);
+    const int n = pol::kOffs.o[pol::kNumParams] / 4;
+    hipLaunchKernelGGL(pol::k_policy_pack, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, flat, packed,
+                       nullptr);
     return check_launch("k_policy_pack");
 }
 

@@ -1,7 +1,8 @@
 // policy_train.hpp -- the training-mode view of the fused policy forward (policy.hip): the same
 // kernel, instantiated with TR = true, gathers a minibatch of windows by row index and writes every
 // activation the PPO backward (train.hip) reads, in its [row = b * 5 + s][feature] layout
-// (pruned layers' tails as compact [b][feature] rows). Heads and sampling are skipped.
+// (pruned layers' tails as compact [b][feature] rows), runs the heads and writes per-workgroup
+// partial sums of the PPO loss terms. Sampling is skipped.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -23,6 +24,10 @@ struct TrainIO {
     float* mask;                 // [R]
     float *e[2], *h0[2];         // [R][128] actor, critic embeddings (post-ReLU) and layer inputs
     TrainLayerIO L[3];           // actor L0 (pruned), critic L0 (full), critic L1 (pruned)
+    float* z[2];                 // [Bm][64] relu(head.0) of the actor / critic head
+    float* fpart;                // [Bm/16][4] per-workgroup loss partials: sum min(s1, s2),
+                                 // sum (v-R)^2, sum (vc-R)^2, sum entropy (smp[5..7] = logits, value)
+    float eps_clip;
 };
 
 // ---- K6: fused backward of the three encoder layers + embeddings (policy.hip), one workgroup per
@@ -35,8 +40,19 @@ struct BwdLayerIO {
     float *ln1_part, *ln2_part;  // [Bm/16][256]: dgamma | dbeta partials per workgroup
 };
 constexpr int kEmbPart = D * IN + D + S * D;  // 2560: We [128][14] | be [128] | pos [5][128]
+constexpr int kHeadPartN = 2 * HID + 2 + HID + 1;  // dW / db of actor_head.2 and critic_head.2
+constexpr int kHeadPart = 196;                     // padded
 struct BwdIO {
-    const float* dh_top[2];  // [Bm][128] gradient wrt the actor / critic trunk outputs (token 4)
+    // heads + loss (ppo.py:148-169): per-sample inputs / logits / value (TrainIO::smp), the loss
+    // sums over the global minibatch (all-reduced when data parallel), relu(head.0) rows
+    const float* smp;
+    const float* tot;
+    const float* z[2];
+    float* dz[2];            // [Bm][64] d(head.0 pre-activation) (weight-gradient GEMM operand)
+    float* hpart;            // [Bm/16][kHeadPart] head.2 weight / bias gradient partials
+    double* stats;           // += loss_actor, loss_critic, entropy, 1 (workgroup 0)
+    float eps_clip, value_coef, entropy_coef;
+    int Bg;                  // samples in the global minibatch
     const float* xg;         // [R][16] input windows (TrainIO::xg)
     const float* mask;       // [R] key padding mask
     const float* e[2];       // [R][128] embeddings after ReLU
@@ -47,9 +63,12 @@ struct BwdIO {
 // in_proj^T [128][384] | out_proj^T [128][128] | linear1^T [128][256] | linear2^T [256][128].
 constexpr int kTWin = 0, kTWo = 3 * D * D, kTW1 = kTWo + D * D, kTW2 = kTW1 + FF * D;
 constexpr int kLayerT = kTW2 + D * FF;  // 131072 floats per layer
-constexpr int kPackedTFloats = 3 * kLayerT;
+// then head.0^T [128][64] of the actor and the critic head
+constexpr int kHeadT = 3 * kLayerT;
+constexpr int kPackedTFloats = kHeadT + 2 * D * HID;
 
-int policy_pack_transposed(const float* flat, float* packedT, hipStream_t st);
+// flat parameters -> packed (forward) and packedT (backward) in one launch
+int policy_pack_train(const float* flat, float* packed, float* packedT, hipStream_t st);
 int policy_backward_train(const float* packed, const float* packedT, const BwdIO& io, int Bm, hipStream_t st);
 
 // Launch the training-mode forward over Bm samples (multiple of 16) with fragment-order packed

@@ -2,15 +2,16 @@
 // (networks/transformer_net.py) on gfx950, fp32 throughout.
 //
 // Layout: a minibatch of Bm samples is R = 5 Bm token rows, row = b * 5 + s, features contiguous.
-// One step is 11 launches on one stream (graph-capturable: no host sync, no allocation):
+// One step is 7 launches on one stream (graph-capturable: no host sync, no allocation):
 //    forward   k_policy_forward<TR> (policy.hip, the rollout's fused kernel writing activations),
-//              k_heads_fwd + k_loss_sums (heads, losses, the four loss sums)
-//    backward  k_heads_bwd (loss + head gradients), k_policy_backward (K6, policy.hip: dX of the
-//              encoder layers and embeddings, one workgroup per 16 samples), then every weight
+//              with the heads and per-workgroup loss partials, then k_loss_sums (the four sums)
+//    backward  k_policy_backward (K6, policy.hip: loss and head gradients, dX of the encoder
+//              layers and embeddings, one workgroup per 16 samples), then every weight
 //              gradient dW[out][in] = sum_row dY[row][out] X[row][in] as one grouped fp32 MFMA GEMM
 //              (gemm.hpp, L_DW, split-K partial slabs + bias gradients as row sums of dY) and one
 //              k_reduce_grads over all partials
-//    update    k_grad_sq + k_adam (clip_grad_norm_ + Adam)
+//    update    k_adam (clip_grad_norm_ + Adam on the g^2 block partials of k_reduce_grads, or of
+//              k_grad_norm after a data-parallel all-reduce)
 // The last encoder layer of each trunk is pruned to the token the heads read (s = 4): K and V for
 // all rows, everything else for Bm rows (compact [Bm][...] tensors), so its gradients are exactly
 // the dense model's.
@@ -56,110 +57,9 @@ __device__ __forceinline__ float wave_sum(float v) {
 // 16 samples per 1024-thread block (one wave per sample). Head weights staged in LDS with a
 // 129-float row stride (lane j reads row j: conflict-free).
 constexpr int kHeadSamples = 16;
-constexpr int kWs = D + 1;
-constexpr int kHeadPartN = 2 * HID + 2 + HID + 1;  // dW/db of actor_head.2 and critic_head.2
-constexpr int kHeadPart = 196;                     // padded
+using pol::kHeadPart;
 
-struct HeadArgs {
-    const float* P;
-    const float* h_a;   // [Bm][128] actor trunk output (token 4)
-    const float* h_c;   // [Bm][128] critic trunk output (token 4)
-    float* z_a;         // [Bm][64] relu(head.0) actor
-    float* z_c;         // [Bm][64]
-    float* smp;         // [Bm][8]: 5 logits0, 6 logits1, 7 value
-    float* part;        // [nblk][4]: sum min(s1,s2), sum (v-R)^2, sum (vc-R)^2, sum entropy
-    float eps_clip;
-    int Bm;
-};
-
-__device__ void head_hidden(const float* Wl, const float* hs, const float* b0, float* z, int p, int l) {
-    float acc = 0.f;
-    const float* wr = Wl + l * kWs;
-    const float* hr = hs + p * D;
-#pragma unroll 8
-    for (int k = 0; k < D; ++k) acc += wr[k] * hr[k];
-    z[l] = fmaxf(acc + b0[l], 0.f);
-}
-
-// Categorical(softmax(logits)) of transformer_net.py:124-144 as torch.distributions evaluates it:
-// p = softmax(l); p /= sum(p); lc = log(clamp(p, eps, 1 - eps)); logp = lc[a]; ent = -sum(lc * p).
-struct CatVals {
-    float y0, y1, s, p0, p1, c0, c1, lc0, lc1;
-};
-__device__ __forceinline__ CatVals categorical(float l0, float l1) {
-    CatVals c;
-    const float m = fmaxf(l0, l1);
-    const float e0 = expf(l0 - m), e1 = expf(l1 - m);
-    const float den = e0 + e1;
-    c.y0 = e0 / den;
-    c.y1 = e1 / den;
-    c.s = c.y0 + c.y1;
-    c.p0 = c.y0 / c.s;
-    c.p1 = c.y1 / c.s;
-    const float eps = 1.1920928955078125e-07f;
-    c.c0 = fminf(fmaxf(c.p0, eps), 1.f - eps);
-    c.c1 = fminf(fmaxf(c.p1, eps), 1.f - eps);
-    c.lc0 = logf(c.c0);
-    c.lc1 = logf(c.c1);
-    return c;
-}
-
-__global__ __launch_bounds__(1024) void k_heads_fwd(const HeadArgs a) {
-    __shared__ float Wl[HID * kWs];
-    __shared__ float hs[kHeadSamples * D];
-    __shared__ float red[kHeadSamples][4];
-    const int p = threadIdx.x >> 6, l = lane_id();
-    const int b = blockIdx.x * kHeadSamples + p;
-    for (int trunk = 0; trunk < 2; ++trunk) {
-        const int head = trunk ? kCriticHead : kActorHead;
-        const float* W0 = a.P + kOffs.o[head];
-        for (int i = threadIdx.x; i < HID * D; i += 1024) Wl[(i >> 7) * kWs + (i & 127)] = W0[i];
-        const float* h = trunk ? a.h_c : a.h_a;
-        for (int i = threadIdx.x; i < kHeadSamples * D; i += 1024)
-            hs[i] = h[(size_t)(blockIdx.x * kHeadSamples + (i >> 7)) * D + (i & 127)];
-        __syncthreads();
-        float* z = (trunk ? a.z_c : a.z_a) + (size_t)b * HID;
-        head_hidden(Wl, hs, a.P + kOffs.o[head + 1], z, p, l);
-        const float zl = z[l];
-        const float* W2 = a.P + kOffs.o[head + 2];
-        const float* b2 = a.P + kOffs.o[head + 3];
-        float* o = a.smp + (size_t)b * 8;
-        if (trunk == 0) {
-            const float l0 = wave_sum(W2[l] * zl) + b2[0];
-            const float l1 = wave_sum(W2[HID + l] * zl) + b2[1];
-            if (l == 0) { o[5] = l0; o[6] = l1; }
-        } else {
-            const float v = wave_sum(W2[l] * zl) + b2[0];
-            if (l == 0) o[7] = v;
-        }
-        __syncthreads();
-    }
-    if (l == 0) {
-        const float* o = a.smp + (size_t)b * 8;
-        const int act = o[0] != 0.f;
-        const CatVals c = categorical(o[5], o[6]);
-        const float logp = act ? c.lc1 : c.lc0;
-        const float ent = -(c.lc0 * c.p0 + c.lc1 * c.p1);
-        const float ratio = expf(logp - o[1]);
-        const float A = o[4];
-        const float s1 = ratio * A;
-        const float s2 = fminf(fmaxf(ratio, 1.f - a.eps_clip), 1.f + a.eps_clip) * A;
-        const float v = o[7], R = o[3], ov = o[2];
-        const float vc = ov + fminf(fmaxf(v - ov, -a.eps_clip), a.eps_clip);
-        red[p][0] = fminf(s1, s2);
-        red[p][1] = (v - R) * (v - R);
-        red[p][2] = (vc - R) * (vc - R);
-        red[p][3] = ent;
-    }
-    __syncthreads();
-    if (threadIdx.x < 4) {
-        float s = 0.f;
-        for (int i = 0; i < kHeadSamples; ++i) s += red[i][threadIdx.x];
-        a.part[blockIdx.x * 4 + threadIdx.x] = s;
-    }
-}
-
-// Sum the per-block loss partials of k_heads_fwd into loss_sums[4] (one wave, fixed order).
+// Sum the per-workgroup loss partials of the training forward into loss_sums[4] (one wave, fixed order).
 __global__ __launch_bounds__(64) void k_loss_sums(const float* __restrict__ part, int nblk, float* __restrict__ out) {
     const int l = lane_id();
     float s[4] = {0.f, 0.f, 0.f, 0.f};
@@ -171,159 +71,57 @@ __global__ __launch_bounds__(64) void k_loss_sums(const float* __restrict__ part
     }
 }
 
-struct HeadBwdArgs {
-    const float* P;
-    const float* h_a;
-    const float* h_c;
-    const float* z_a;
-    const float* z_c;
-    const float* smp;
-    const float* tot;   // [4] loss sums over the global minibatch (loss_sums, all-reduced)
-    float* dz_a;        // [Bm][64] d(head.0 pre-activation), relu-masked
-    float* dz_c;
-    float* dh_a;        // [Bm][128] gradient wrt the actor trunk output (token 4)
-    float* dh_c;
-    float* hpart;       // [nblk][kHeadPart] head.2 weight / bias gradient partials
-    double* stats;      // += loss_actor, loss_critic, entropy, 1
-    float eps_clip, value_coef, entropy_coef;
-    int Bm, Bg;  // samples on this rank / in the global minibatch
-};
-
-// Loss gradients of ppo.py:148-169 per sample (torch's min / max / clamp backward conventions:
-// ties send half the gradient to each side, clamp passes it on the closed interval), then the
-// heads' backward.
-__global__ __launch_bounds__(1024) void k_heads_bwd(const HeadBwdArgs a) {
-    __shared__ float Wl[HID * kWs];
-    __shared__ float dzs[kHeadSamples * HID];
-    __shared__ float gsm[kHeadSamples][3];  // dlogit0, dlogit1, dvalue
-    __shared__ float hp[kHeadSamples][kHeadPart];
-    const int p = threadIdx.x >> 6, l = lane_id();
-    const int b = blockIdx.x * kHeadSamples + p;
-    const float tot[4] = {a.tot[0], a.tot[1], a.tot[2], a.tot[3]};
-    const float inv = 1.0f / (float)a.Bg;
-    const float L1 = tot[1] * inv, L2 = tot[2] * inv;
-    if (l == 0) {
-        const float* o = a.smp + (size_t)b * 8;
-        const int act = o[0] != 0.f;
-        const CatVals c = categorical(o[5], o[6]);
-        const float logp = act ? c.lc1 : c.lc0;
-        const float ratio = expf(logp - o[1]);
-        const float A = o[4], lo = 1.f - a.eps_clip, hi = 1.f + a.eps_clip;
-        const float s1 = ratio * A;
-        const float s2 = fminf(fmaxf(ratio, lo), hi) * A;
-        const float gmin = -inv;  // d(-mean(min)) / d min_i
-        const float g1 = s1 < s2 ? gmin : (s1 == s2 ? 0.5f * gmin : 0.f);
-        const float g2 = s2 < s1 ? gmin : (s1 == s2 ? 0.5f * gmin : 0.f);
-        const float gr = g1 * A + ((ratio >= lo && ratio <= hi) ? g2 * A : 0.f);
-        const float glogp = gr * ratio;
-        const float gent = -a.entropy_coef * inv;
-        // back through lc = log(clamp(p)), ent = -sum(lc * p), p = y / s, s = y0 + y1, y = softmax
-        float glc0 = -gent * c.p0, glc1 = -gent * c.p1;
-        if (act) glc1 += glogp; else glc0 += glogp;
-        const float eps = 1.1920928955078125e-07f;
-        float gp0 = -gent * c.lc0 + ((c.p0 >= eps && c.p0 <= 1.f - eps) ? glc0 / c.c0 : 0.f);
-        float gp1 = -gent * c.lc1 + ((c.p1 >= eps && c.p1 <= 1.f - eps) ? glc1 / c.c1 : 0.f);
-        const float gs = -(gp0 * c.y0 + gp1 * c.y1) / (c.s * c.s);
-        const float gy0 = gp0 / c.s + gs, gy1 = gp1 / c.s + gs;
-        const float dot = gy0 * c.y0 + gy1 * c.y1;
-        const float gl0 = c.y0 * (gy0 - dot), gl1 = c.y1 * (gy1 - dot);
-        // value: 0.5 * max(mean((v-R)^2), mean((vc-R)^2))
-        const float v = o[7], R = o[3], ov = o[2];
-        const float dv = v - ov;
-        const float vc = ov + fminf(fmaxf(dv, -a.eps_clip), a.eps_clip);
-        const float w1 = L1 > L2 ? 1.f : (L1 == L2 ? 0.5f : 0.f);
-        const float w2 = L2 > L1 ? 1.f : (L1 == L2 ? 0.5f : 0.f);
-        const float gv = a.value_coef * (w1 * 2.f * (v - R) * inv +
-                                         ((dv >= -a.eps_clip && dv <= a.eps_clip) ? w2 * 2.f * (vc - R) * inv : 0.f));
-        gsm[p][0] = gl0;
-        gsm[p][1] = gl1;
-        gsm[p][2] = gv;
-    }
-    __syncthreads();
-    if (blockIdx.x == 0 && threadIdx.x == 0 && a.stats) {
-        a.stats[0] += (double)(-tot[0] * inv);
-        a.stats[1] += (double)fmaxf(L1, L2);
-        a.stats[2] += (double)(tot[3] * inv);
-        a.stats[3] += 1.0;
-    }
-    for (int trunk = 0; trunk < 2; ++trunk) {
-        const int head = trunk ? kCriticHead : kActorHead;
-        const float* W0 = a.P + kOffs.o[head];
-        const float* W2 = a.P + kOffs.o[head + 2];
-        const float* z = (trunk ? a.z_c : a.z_a) + (size_t)b * HID;
-        const float zl = z[l];
-        float g;
-        if (trunk == 0) g = W2[l] * gsm[p][0] + W2[HID + l] * gsm[p][1];
-        else g = W2[l] * gsm[p][2];
-        const float dz = zl > 0.f ? g : 0.f;
-        (trunk ? a.dz_c : a.dz_a)[(size_t)b * HID + l] = dz;
-        dzs[p * HID + l] = dz;
-        // head.2 gradient partials: dW2[o][j] = sum_b g_o z_j, db2[o] = sum_b g_o
-        if (trunk == 0) {
-            hp[p][l] = gsm[p][0] * zl;
-            hp[p][HID + l] = gsm[p][1] * zl;
-            if (l < 2) hp[p][2 * HID + l] = gsm[p][l];
-        } else {
-            hp[p][2 * HID + 2 + l] = gsm[p][2] * zl;
-            if (l == 0) hp[p][3 * HID + 2] = gsm[p][2];
-        }
-        for (int i = threadIdx.x; i < HID * D; i += 1024) Wl[(i >> 7) * kWs + (i & 127)] = W0[i];
-        __syncthreads();
-        // dh[k] = sum_j W0[j][k] dz[j]: lane l owns k = l and l + 64
-        float* dh = (trunk ? a.dh_c : a.dh_a) + (size_t)b * D;
-        float s0 = 0.f, s1 = 0.f;
-#pragma unroll 8
-        for (int j = 0; j < HID; ++j) {
-            const float d = dzs[p * HID + j];
-            s0 += Wl[j * kWs + l] * d;
-            s1 += Wl[j * kWs + 64 + l] * d;
-        }
-        dh[l] = s0;
-        dh[64 + l] = s1;
-        __syncthreads();
-    }
-    for (int i = threadIdx.x; i < kHeadPart; i += 1024) {
-        float s = 0.f;
-        if (i < kHeadPartN)
-            for (int q = 0; q < kHeadSamples; ++q) s += hp[q][i];
-        a.hpart[(size_t)blockIdx.x * kHeadPart + i] = s;
-    }
-}
-
 // ================================================================== backward
 // dX of the encoder layers + embeddings: k_policy_backward (policy.hip, K6), one fused kernel.
 using pol::kEmbPart;
 
 // ================================================================== gradient reduction + Adam
 // grads[dst + i] = sum_p src[p * part_stride + i] for each segment; block partial sums of g^2.
+// Few parts (split-K slabs): one thread per element. Many parts (per-workgroup partials of K6 /
+// the heads): a block takes 64 consecutive elements, each wave every 4th part, so every load is a
+// coalesced 256 B row segment; the 4 wave sums combine in a fixed order (deterministic).
 struct Segment {
     const float* src;
-    int dst, count, parts, part_stride, block_begin, wave_mode;
+    int dst, count, parts, part_stride, block_begin, tile_mode;
 };
 constexpr int kMaxSegs = 64;
-constexpr int kWaveModeParts = 16;  // more parts than this: one wave per element
+constexpr int kTileModeParts = 16;  // more parts than this: tile mode
 struct SegBatch {
     Segment s[kMaxSegs];
     int n;
 };
 __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* __restrict__ grads,
-                                                      float* __restrict__ sq_part) {
+                                                      float* __restrict__ sq_part, double* __restrict__ step) {
     __shared__ float red[4];
-    int si = 0;
-    while (si + 1 < sb.n && (int)blockIdx.x >= sb.s[si + 1].block_begin) ++si;
+    __shared__ float wsum[4][64];
+    int si = 0, hi = sb.n;  // segment of this block: binary search (each probe is a kernarg load)
+    while (hi - si > 1) {
+        const int mid = (si + hi) >> 1;
+        if ((int)blockIdx.x >= sb.s[mid].block_begin) si = mid;
+        else hi = mid;
+    }
     const Segment& S_ = sb.s[si];
     const size_t ps = S_.part_stride;
     float sq = 0.f;
-    if (S_.wave_mode) {  // element = block * 4 + wave; lanes stride over the parts
-        const int i = (blockIdx.x - S_.block_begin) * 4 + (threadIdx.x >> 6);
+    if (S_.tile_mode) {
+        const int wv = threadIdx.x >> 6, l = lane_id();
+        const int i = (blockIdx.x - S_.block_begin) * 64 + l;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
         if (i < S_.count) {
-            float acc = 0.f;
-            for (int p = lane_id(); p < S_.parts; p += 64) acc += S_.src[(size_t)p * ps + i];
-            const float tot = wave_sum(acc);
-            if (lane_id() == 0) {
-                grads[S_.dst + i] = tot;
-                sq = tot * tot;
+            const float* src = S_.src + i;
+            int p = wv;
+            for (; p + 12 < S_.parts; p += 16) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[u] += src[(size_t)(p + 4 * u) * ps];
             }
+            for (; p < S_.parts; p += 4) acc[0] += src[(size_t)p * ps];
+        }
+        wsum[wv][l] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        __syncthreads();
+        if (wv == 0 && i < S_.count) {
+            const float tot = (wsum[0][l] + wsum[1][l]) + (wsum[2][l] + wsum[3][l]);
+            grads[S_.dst + i] = tot;
+            sq = tot * tot;
         }
     } else {
         const int i = (blockIdx.x - S_.block_begin) * 256 + threadIdx.x;
@@ -345,13 +143,16 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
     sq = wave_sum(sq);
     if (lane_id() == 0) red[threadIdx.x >> 6] = sq;
     __syncthreads();
-    if (threadIdx.x == 0) sq_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x == 0) {
+        sq_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+        if (step && blockIdx.x == 0) step[0] += 1.0;  // single-GPU step: these are the final grads
+    }
 }
 
-// Block partial sums of g^2 over the flat gradient (the norm clip_grad_norm_ needs, taken after
-// any cross-rank all-reduce of grads); block 0 advances Adam's step counter.
-__global__ __launch_bounds__(256) void k_grad_sq(const float* __restrict__ grads, int n, float* __restrict__ sq_part,
-                                                 double* __restrict__ step) {
+// Block partial sums of g^2 over the flat gradient after a cross-rank all-reduce (data-parallel
+// UPDATE phase; a single-GPU step takes them from k_reduce_grads); advances Adam's step counter.
+__global__ __launch_bounds__(256) void k_grad_norm(const float* __restrict__ grads, int n, float* __restrict__ sq_part,
+                                                   double* __restrict__ step) {
     __shared__ float red[4];
     float s = 0.f;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) s += grads[i] * grads[i];
@@ -363,7 +164,7 @@ __global__ __launch_bounds__(256) void k_grad_sq(const float* __restrict__ grads
         if (blockIdx.x == 0) step[0] += 1.0;
     }
 }
-constexpr int kSqBlocks = 512;
+constexpr int kSqBlocks = 256;
 
 // clip_grad_norm_(max_norm) + torch.optim.Adam (ppo.py:17-22 groups: actor params < critic trunk
 // offset use lr_actor, the rest lr_critic), elementwise over the flat buffers.
@@ -379,35 +180,32 @@ struct AdamArgs {
 };
 __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     __shared__ float red[4];
-    __shared__ float coef_s;
     float s = 0.f;
     for (int i = threadIdx.x; i < a.n_sq; i += 256) s += a.sq_part[i];
     s = wave_sum(s);
     if (lane_id() == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const float total = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
-        const float c = a.max_norm / (total + 1e-6f);
-        coef_s = fminf(c, 1.0f);
-    }
-    __syncthreads();
-    const float coef = coef_s;
+    const float norm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+    const float coef = fminf(a.max_norm / (norm + 1e-6f), 1.0f);
     const double t = a.step[0];
     const double bc1 = 1.0 - pow((double)a.beta1, t);
-    const double bc2 = 1.0 - pow((double)a.beta2, t);
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < a.n; i += gridDim.x * 256) {
-        const float lr = i < a.critic_begin ? a.lr_actor : a.lr_critic;
-        const float ss = (float)((double)lr / bc1);
-        const float bs = (float)sqrt(bc2);
-        const float g = a.grads[i] * coef;
-        a.grads[i] = g;
-        float m = a.m[i];
+    const float bs = (float)sqrt(1.0 - pow((double)a.beta2, t));
+    const float ss_a = (float)((double)a.lr_actor / bc1), ss_c = (float)((double)a.lr_critic / bc1);
+    for (int i4 = blockIdx.x * 256 + threadIdx.x; 4 * i4 < a.n; i4 += gridDim.x * 256) {
+        const int i = 4 * i4;  // n and critic_begin are multiples of 4 (padded layout)
+        const float ss = i < a.critic_begin ? ss_a : ss_c;
+        f32x4 g = *reinterpret_cast<const f32x4*>(a.grads + i) * coef;
+        f32x4 m = *reinterpret_cast<const f32x4*>(a.m + i);
+        f32x4 v = *reinterpret_cast<const f32x4*>(a.v + i);
+        f32x4 p = *reinterpret_cast<const f32x4*>(a.params + i);
         m = m + (1.f - a.beta1) * (g - m);
-        const float v = a.v[i] * a.beta2 + (1.f - a.beta2) * (g * g);
-        a.m[i] = m;
-        a.v[i] = v;
-        const float denom = sqrtf(v) / bs + a.eps;
-        a.params[i] = a.params[i] + (-ss) * (m / denom);
+        v = v * a.beta2 + (1.f - a.beta2) * (g * g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) p[j] = p[j] + (-ss) * (m[j] / (sqrtf(v[j]) / bs + a.eps));
+        *reinterpret_cast<f32x4*>(a.grads + i) = g;
+        *reinterpret_cast<f32x4*>(a.m + i) = m;
+        *reinterpret_cast<f32x4*>(a.v + i) = v;
+        *reinterpret_cast<f32x4*>(a.params + i) = p;
     }
 }
 
@@ -432,7 +230,7 @@ struct Plan {
     int Bm, R;
     float *xg, *mask, *smp, *e_a, *h0_a, *e_c, *h0_c;
     LayerBufs la, lc0, lc1;
-    float *z_a, *z_c, *dz_a, *dz_c, *dh_a, *dh_c, *fpart, *hpart, *epart, *sq_part;
+    float *z_a, *z_c, *dz_a, *dz_c, *fpart, *hpart, *epart, *sq_part;
     float* split_ws;
     size_t split_floats;
     float* packed;  // fragment-order copy of the parameters for the fused forward
@@ -496,8 +294,6 @@ inline Plan make_plan(int Bm, float* base) {
     p.z_c = w.take((size_t)Bm * HID);
     p.dz_a = w.take((size_t)Bm * HID);
     p.dz_c = w.take((size_t)Bm * HID);
-    p.dh_a = w.take((size_t)Bm * D);
-    p.dh_c = w.take((size_t)Bm * D);
     p.fpart = w.take((size_t)(Bm / kHeadSamples) * 4);
     p.hpart = w.take((size_t)(Bm / kHeadSamples) * kHeadPart);
     p.epart = w.take((size_t)(Bm / kHeadSamples) * 2 * kEmbPart);
@@ -539,7 +335,7 @@ extern "C" int64_t uavhip_ppo_workspace_floats(int32_t minibatch) {
         if (rc_) return rc_; \
     } while (0)
 
-static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int Bg);
+static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int Bg, double* step, int* n_sq);
 
 extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const int8_t* actions,
                                const float* old_logp, const float* old_values, const float* returns,
@@ -566,7 +362,7 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
     // The rollout's fused forward kernel (policy.hip) in training mode: one workgroup per 16
     // samples, every activation the backward needs written to the workspace.
     if (fwd) {
-        TR_CHECK(uavhip_policy_pack(c->params, p.packed, stream));
+        TR_CHECK(pol::policy_pack_train(c->params, p.packed, p.packedT, st));
         pol::TrainIO io{};
         io.idx = idx;
         io.act_in = actions;
@@ -583,43 +379,52 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
         for (int i = 0; i < 3; ++i)
             io.L[i] = pol::TrainLayerIO{lb[i]->qkv, lb[i]->o, lb[i]->xhat1, lb[i]->rstd1, lb[i]->h1, lb[i]->u,
                                         lb[i]->xhat2, lb[i]->rstd2, lb[i]->h2};
+        io.z[0] = p.z_a;
+        io.z[1] = p.z_c;
+        io.fpart = p.fpart;
+        io.eps_clip = c->eps_clip;
         TR_CHECK(pol::policy_forward_train(p.packed, states, io, Bm, st));
-        HeadArgs ha{c->params, A.h2, C1.h2, p.z_a, p.z_c, p.smp, p.fpart, c->eps_clip, Bm};
-        hipLaunchKernelGGL(k_heads_fwd, dim3(nblk), dim3(1024), 0, st, ha);
-        TR_CHECK(check_launch("k_heads_fwd"));
         hipLaunchKernelGGL(k_loss_sums, dim3(1), dim3(64), 0, st, p.fpart, nblk, c->loss_sums);
         TR_CHECK(check_launch("k_loss_sums"));
     }
-    if (bwd) TR_CHECK(ppo_backward(c, p, st, Bg));
+    // single-GPU FULL step: the gradient reduction leaves the g^2 partials of the final grads;
+    // otherwise (UPDATE after an all-reduce of grads) k_grad_norm computes them
+    int n_sq = kSqBlocks;
+    if (bwd) TR_CHECK(ppo_backward(c, p, st, Bg, upd ? c->adam_step : nullptr, &n_sq));
     if (upd) {
-        hipLaunchKernelGGL(k_grad_sq, dim3(kSqBlocks), dim3(256), 0, st, c->grads, c->n_floats, p.sq_part,
-                           c->adam_step);
-        TR_CHECK(check_launch("k_grad_sq"));
-        AdamArgs aa{c->params, c->grads, c->adam_m, c->adam_v, c->adam_step, p.sq_part, kSqBlocks, c->n_floats,
+        if (!bwd) {
+            hipLaunchKernelGGL(k_grad_norm, dim3(kSqBlocks), dim3(256), 0, st, c->grads, c->n_floats, p.sq_part,
+                               c->adam_step);
+            TR_CHECK(check_launch("k_grad_norm"));
+        }
+        AdamArgs aa{c->params, c->grads, c->adam_m, c->adam_v, c->adam_step, p.sq_part, n_sq, c->n_floats,
                     kOffs.o[kCriticTrunk], c->lr_actor, c->lr_critic, c->beta1, c->beta2, c->adam_eps,
                     c->max_grad_norm};
-        hipLaunchKernelGGL(k_adam, dim3(512), dim3(256), 0, st, aa);
+        hipLaunchKernelGGL(k_adam, dim3((c->n_floats / 4 + 255) / 256), dim3(256), 0, st, aa);
         TR_CHECK(check_launch("k_adam"));
     }
     return UAVHIP_OK;
 }
 
 // Backward + weight gradients of one minibatch (the workspace holds the forward's activations).
-static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int Bg) {
+static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int Bg, double* step, int* n_sq) {
     const int Bm = p.Bm, R = p.R, nblk = Bm / kHeadSamples;
     const LayerBufs &A = p.la, &C0 = p.lc0, &C1 = p.lc1;
     const int ta = kActorTrunk, tc = kCriticTrunk;
     {
-        HeadBwdArgs hb{c->params, A.h2, C1.h2, p.z_a, p.z_c, p.smp, c->loss_sums, p.dz_a, p.dz_c, p.dh_a, p.dh_c,
-                       p.hpart, c->stats, c->eps_clip, c->value_coef, c->entropy_coef, Bm, Bg};
-        hipLaunchKernelGGL(k_heads_bwd, dim3(nblk), dim3(1024), 0, st, hb);
-        TR_CHECK(check_launch("k_heads_bwd"));
-    }
-    {
-        TR_CHECK(pol::policy_pack_transposed(c->params, p.packedT, st));
         pol::BwdIO io{};
-        io.dh_top[0] = p.dh_a;
-        io.dh_top[1] = p.dh_c;
+        io.smp = p.smp;
+        io.tot = c->loss_sums;
+        io.z[0] = p.z_a;
+        io.z[1] = p.z_c;
+        io.dz[0] = p.dz_a;
+        io.dz[1] = p.dz_c;
+        io.hpart = p.hpart;
+        io.stats = c->stats;
+        io.eps_clip = c->eps_clip;
+        io.value_coef = c->value_coef;
+        io.entropy_coef = c->entropy_coef;
+        io.Bg = Bg;
         io.xg = p.xg;
         io.mask = p.mask;
         io.e[0] = p.e_a;
@@ -640,8 +445,8 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         Segment& s = sb.s[sb.n++];
         s.src = src; s.dst = dst; s.count = count; s.parts = parts; s.part_stride = part_stride;
         s.block_begin = seg_blocks;
-        s.wave_mode = parts > kWaveModeParts;
-        seg_blocks += s.wave_mode ? (count + 3) / 4 : (count + 255) / 256;
+        s.tile_mode = parts > kTileModeParts;
+        seg_blocks += s.tile_mode ? (count + 63) / 64 : (count + 255) / 256;
     };
     {
         GemmBuilder g;
@@ -706,6 +511,7 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         return UAVHIP_EINVAL;
     }
     // padding floats between parameters stay zero
-    hipLaunchKernelGGL(k_reduce_grads, dim3(seg_blocks), dim3(256), 0, st, sb, c->grads, p.sq_part);
+    hipLaunchKernelGGL(k_reduce_grads, dim3(seg_blocks), dim3(256), 0, st, sb, c->grads, p.sq_part, step);
+    *n_sq = seg_blocks;
     return check_launch("k_reduce_grads");
 }
