@@ -683,17 +683,19 @@ __device__ __forceinline__ float hsum(f32x4 v) { return (v.x + v.y) + (v.z + v.w
 
 // LayerNorm backward (torch's formula) on LDS rows, tokens [t0, TOK), 16 lanes per token and 8
 // features per lane: g = src * w; dz = rstd * (g - mean(g) - xhat * mean(g * xhat)) -> dst (LDS)
-// and gout (workspace rows). Per-workgroup partials of dw = sum src * xhat, db = sum src -> part
-// [0..127], [128..255], reduced over the 32 lane groups through `scratch` (8 KiB floats). Ends
-// without a barrier after the partials are written (scratch is read until then).
+// and gout (workspace rows). Workgroup partials, reduced over the 32 lane groups through `scratch`
+// (12 KiB floats): dw = sum src * xhat, db = sum src -> part[0..127], [128..255]; the bias
+// gradient of the linear that produced the LayerNorm input, sum dz -> bias[0..127]. Ends without a
+// barrier after the partials are written (scratch is read until then).
 __device__ void ln_bwd_lds(const float* src, float* dst, const float* __restrict__ xhat,
                            const float* __restrict__ rstd, const float* __restrict__ w, float* __restrict__ gout,
-                           float* __restrict__ part, int t0, int b0, bool compact, float* scratch) {
+                           float* __restrict__ part, float* __restrict__ bias, int t0, int b0, bool compact,
+                           float* scratch) {
     const int j = threadIdx.x & 15, grp = threadIdx.x >> 4;
     const int f0 = 8 * j;
     const f32x4 w0 = ld4(w + f0), w1 = ld4(w + f0 + 4);
     const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-    f32x4 pw0 = zero4, pw1 = zero4, pb0 = zero4, pb1 = zero4;
+    f32x4 pw0 = zero4, pw1 = zero4, pb0 = zero4, pb1 = zero4, pd0 = zero4, pd1 = zero4;
     for (int tok = t0 + grp; tok < TOK; tok += NTHR / 16) {
         const size_t r = (size_t)orow(tok, b0, compact);
         const f32x4 g0 = ld4(src + tok * LDH + f0), g1 = ld4(src + tok * LDH + f0 + 4);
@@ -709,16 +711,20 @@ __device__ void ln_bwd_lds(const float* src, float* dst, const float* __restrict
         st4(gout + r * D + f0 + 4, d1);
         pw0 += g0 * x0; pw1 += g1 * x1;
         pb0 += g0; pb1 += g1;
+        pd0 += d0; pd1 += d1;
     }
-    float* sc = scratch + grp * 2 * D;
+    float* sc = scratch + grp * 3 * D;
     st4(sc + f0, pw0); st4(sc + f0 + 4, pw1);
     st4(sc + D + f0, pb0); st4(sc + D + f0 + 4, pb1);
+    st4(sc + 2 * D + f0, pd0); st4(sc + 2 * D + f0 + 4, pd1);
     __syncthreads();
-    if (threadIdx.x < 2 * D) {
-        float s[4] = {0.f, 0.f, 0.f, 0.f};
+    if (threadIdx.x < 3 * D) {
+        float s4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < NTHR / 16; ++q) s[q & 3] += scratch[q * 2 * D + threadIdx.x];
-        part[threadIdx.x] = (s[0] + s[1]) + (s[2] + s[3]);
+        for (int q = 0; q < NTHR / 16; ++q) s4[q & 3] += scratch[q * 3 * D + threadIdx.x];
+        const float tot = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        if (threadIdx.x < 2 * D) part[threadIdx.x] = tot;
+        else bias[threadIdx.x - 2 * D] = tot;
     }
 }
 
@@ -730,13 +736,15 @@ __device__ void ln_bwd_lds(const float* src, float* dst, const float* __restrict
 // forward's chunk layout) and dqkv rows (pruned layers: dq only for the token-4 query rows; the
 // LDS copy is zero on the other rows).
 template <bool last>
-__device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, float* __restrict__ dqkv, int c, int b0) {
+__device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, float* __restrict__ dqkv, int c, int b0,
+                               float* scratch) {
     if (threadIdx.x >= 256) return;
     const int q4 = threadIdx.x & 3, hh = (threadIdx.x >> 2) & 3, p = threadIdx.x >> 4;
     const int d0 = hh * HD + 4 * q4, col = 64 * c + d0;
     const size_t rb = (size_t)(b0 + p) * S;
     f32x4 k[S], v[S], dk[S], dv[S];
     bool msk[S];
+    f32x4 sdq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < S; ++j) {
         k[j] = ld4(qkv + (rb + j) * 3 * D + D + col);
@@ -781,15 +789,33 @@ __device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, float* _
                 dv[j] += pr[j] * g;
             }
             st4(dqkv + (rb + i) * 3 * D + col, dq);
+            sdq += dq;
         }
         st4(sm.big + (i * SPW + p) * LDB + d0, dq);
     }
+    f32x4 sk = {0.f, 0.f, 0.f, 0.f}, sv = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < S; ++j) {
         st4(sm.big + (j * SPW + p) * LDB + 64 + d0, dk[j]);
         st4(sm.big + (j * SPW + p) * LDB + 128 + d0, dv[j]);
         st4(dqkv + (rb + j) * 3 * D + D + col, dk[j]);
         st4(dqkv + (rb + j) * 3 * D + 2 * D + col, dv[j]);
+        sk += dk[j];
+        sv += dv[j];
+    }
+    // in_proj bias partials: sums over the wave's 4 samples (lanes 16 apart), one row per wave
+    f32x4 sq = sdq;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        sq[e] = add_xor32(add_xor16(sq[e]));
+        sk[e] = add_xor32(add_xor16(sk[e]));
+        sv[e] = add_xor32(add_xor16(sv[e]));
+    }
+    if ((threadIdx.x & 63) < 16) {
+        float* row = scratch + (threadIdx.x >> 6) * 3 * 64;
+        st4(row + d0, sq);
+        st4(row + 64 + d0, sk);
+        st4(row + 128 + d0, sv);
     }
 }
 
@@ -807,11 +833,12 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
     const float* W2T = PT + kTW2;
     const int wv = threadIdx.x >> 6, l = lane_id(), i16 = l & 15, g = l >> 4;
     const int fo = 16 * wv + 4 * g;  // this lane's 4 output features of a 16-row tile of wave wv
+    float* bias = io.bpart + (size_t)blockIdx.x * kBiasPart;  // this workgroup's bias partials
 
     // LN2 backward: sm.h -> sm.ctx (= df)
     APre<DQ> pa = prefetch<DQ>(W2T, D, 16 * wv, 0);
-    ln_bwd_lds(sm.h, sm.ctx, io.xhat2, io.rstd2, P + kOffs.o[layer_param(trunk, layer, N2W)], io.df, io.ln2_part + (size_t)blockIdx.x * 2 * D,
-               qtok0, b0, last, sm.big);
+    ln_bwd_lds(sm.h, sm.ctx, io.xhat2, io.rstd2, P + kOffs.o[layer_param(trunk, layer, N2W)], io.df,
+               io.ln2_part + (size_t)blockIdx.x * 2 * D, bias + kBiasL2, qtok0, b0, last, sm.big);
     __syncthreads();
     // du = relu'(u) (W2^T df): 256 hidden features, wave wv owns tiles 16 wv (-> big) and 128 + 16 wv (-> h)
 #pragma unroll
@@ -822,6 +849,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         if (t == 0) gemm_tile<CTQ, DQ>(acc, pa, W2T, D, row, 0, sm.ctx, LDH, qtok0);
         else gemm_tile<CTQ, DQ>(acc, prefetch<DQ>(W2T, D, row, 0), W2T, D, row, 0, sm.ctx, LDH, qtok0);
         float* lds = t ? sm.h : sm.big;
+        f32x4 sd = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ct = 0; ct < CTQ; ++ct) {
             const int tok = qtok0 + 16 * ct + i16;
@@ -832,7 +860,12 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
             d.z = u.z > 0.f ? d.z : 0.f; d.w = u.w > 0.f ? d.w : 0.f;
             st4(io.du + r * FF + row + 4 * g, d);
             st4(lds + tok * LDH + fo, d);
+            sd += d;
         }
+        // linear1 bias partial: sum over the tokens (the 16 lanes of a row, then the column tiles)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sd[e] = row16_sum(sd[e]);
+        if (i16 == 0) st4(bias + kBiasL1 + row + 4 * g, sd);
     }
     pa = prefetch<DQ>(W1T, FF, 16 * wv, 0);
     __syncthreads();
@@ -851,8 +884,8 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
     pa = prefetch<DQ>(WoT, D, 16 * wv, 0);
     __syncthreads();
     // LN1 backward: sm.ctx -> sm.h (= dz1)
-    ln_bwd_lds(sm.ctx, sm.h, io.xhat1, io.rstd1, P + kOffs.o[layer_param(trunk, layer, N1W)], io.dz1, io.ln1_part + (size_t)blockIdx.x * 2 * D,
-               qtok0, b0, last, sm.big);
+    ln_bwd_lds(sm.ctx, sm.h, io.xhat1, io.rstd1, P + kOffs.o[layer_param(trunk, layer, N1W)], io.dz1,
+               io.ln1_part + (size_t)blockIdx.x * 2 * D, bias + kBiasOut, qtok0, b0, last, sm.big);
     __syncthreads();
     // d(attention output) = Wo^T dz1 -> sm.ctx
     {
@@ -869,8 +902,13 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         APre<2> pw = prefetch<2>(WinT, 3 * D, 16 * wv, 64 * c);
-        attn_bwd_chunk<last>(sm, io.qkv, io.dqkv, c, b0);
+        attn_bwd_chunk<last>(sm, io.qkv, io.dqkv, c, b0, sm.x);
         __syncthreads();
+        if (threadIdx.x < 3 * 64) {  // in_proj bias partial of the chunk: the 4 wave rows of sm.x
+            const int i = threadIdx.x;
+            const float v = (sm.x[i] + sm.x[192 + i]) + (sm.x[384 + i] + sm.x[576 + i]);
+            bias[kBiasIn + (i >> 6) * D + 64 * c + (i & 63)] = v;
+        }
 #pragma unroll
         for (int part = 0; part < 3; ++part) {
             const int kw = part * D + 64 * c;
@@ -890,8 +928,15 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
 }
 
 // Embedding backward from sm.h = dL/d(h0) (80 tokens): h0 = relu(We x + be) + pos. Thread =
-// (feature, token group of 20); partials reduced over the 4 groups through sm.big -> part [2560].
-__device__ void embed_bwd(Smem& sm, const float* __restrict__ e, float* __restrict__ part, int b0) {
+// (feature, token group of 20); partials reduced over the 4 groups through sm.big -> part [2560]
+// in the parameters' order (pos | We | be).
+__device__ void embed_bwd(Smem& sm, const float* __restrict__ e, const float* __restrict__ xg,
+                          float* __restrict__ part, int b0) {
+    for (int i = threadIdx.x; i < TOK * LDX / 4; i += NTHR) {  // input windows (sm.x was scratch)
+        const int t = i / (LDX / 4), q = i % (LDX / 4);
+        st4(sm.x + t * LDX + 4 * q, ld4(xg + (size_t)trow(t, b0) * 16 + 4 * q));
+    }
+    __syncthreads();
     const int f = threadIdx.x & (D - 1), grp = threadIdx.x >> 7;
     float acc[IN + 1 + S];
 #pragma unroll
@@ -914,7 +959,8 @@ __device__ void embed_bwd(Smem& sm, const float* __restrict__ e, float* __restri
         const int v = o >> 7, ff = o & (D - 1);
         const float s = (sm.big[v * D + ff] + sm.big[(NV + v) * D + ff]) +
                         (sm.big[(2 * NV + v) * D + ff] + sm.big[(3 * NV + v) * D + ff]);
-        const int dst = v < IN ? ff * IN + v : (v == IN ? D * IN + ff : D * IN + D + (v - IN - 1) * D + ff);
+        // state_dict order of the trunk's first parameters: pos [5][128] | We [128][14] | be [128]
+        const int dst = v < IN ? S * D + ff * IN + v : (v == IN ? S * D + D * IN + ff : (v - IN - 1) * D + ff);
         part[dst] = s;
     }
 }
@@ -981,8 +1027,17 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         io.dz[trunk][(size_t)(b0 + p) * HID + j] = dz;
         (trunk ? dzc : sm.z)[p * LDZ + j] = dz;
     }
+    __syncthreads();
+    // head.0 bias partials (sum over the 16 samples of dz, from LDS)
+    if (threadIdx.x < 2 * HID) {
+        const int trunk = threadIdx.x / HID, j = threadIdx.x % HID;
+        const float* d = trunk ? dzc : sm.z;
+        float acc = 0.f;
+        for (int p = 0; p < SPW; ++p) acc += d[p * LDZ + j];
+        io.hpart[(size_t)blockIdx.x * kHeadPart + kHeadB0 + threadIdx.x] = acc;
+    }
     // head.2 partials, summed over the 16 samples in order: dW2[o][j] = sum g_o z_j, db2[o] = sum g_o
-    if (threadIdx.x < kHeadPart) {
+    if (threadIdx.x < kHeadB0) {
         const int i = threadIdx.x;
         float acc = 0.f;
         if (i < 2 * HID) {
@@ -993,7 +1048,7 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         } else if (i < 3 * HID + 2) {
             const int j = i - 2 * HID - 2;
             for (int p = 0; p < SPW; ++p) acc += gs[4 * p + 2] * io.z[1][(size_t)(b0 + p) * HID + j];
-        } else if (i < kHeadPartN) {
+        } else if (i < 3 * HID + 3) {
             for (int p = 0; p < SPW; ++p) acc += gs[4 * p + 2];
         }
         io.hpart[(size_t)blockIdx.x * kHeadPart + i] = acc;
@@ -1014,10 +1069,6 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
                                                           const BwdIO io) {
     __shared__ __attribute__((aligned(16))) Smem sm;
     const int b0 = blockIdx.x * SPW;
-    for (int i = threadIdx.x; i < TOK * LDX / 4; i += NTHR) {
-        const int t = i / (LDX / 4), q = i % (LDX / 4);
-        st4(sm.x + t * LDX + 4 * q, ld4(io.xg + (size_t)trow(t, b0) * 16 + 4 * q));
-    }
     if (threadIdx.x < SPW * S) sm.mask[threadIdx.x] = io.mask[(size_t)b0 * S + threadIdx.x] != 0.f;
     heads_bwd(sm, P, io, b0);
     __syncthreads();
@@ -1026,13 +1077,13 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
     __syncthreads();
     bwd_layer<kCriticTrunk, 1, true>(sm, P, PT + 2 * kLayerT, io.L[2], b0);
     bwd_layer<kCriticTrunk, 0, false>(sm, P, PT + 1 * kLayerT, io.L[1], b0);
-    embed_bwd(sm, io.e[1], io.epart + ((size_t)blockIdx.x * 2 + 1) * kEmbPart, b0);
+    embed_bwd(sm, io.e[1], io.xg, io.epart + ((size_t)blockIdx.x * 2 + 1) * kEmbPart, b0);
     __syncthreads();
     // actor: head.0, layer 0 (pruned), embedding
     head_input_grad(sm, PT + kHeadT, sm.z);
     __syncthreads();
     bwd_layer<kActorTrunk, 0, true>(sm, P, PT, io.L[0], b0);
-    embed_bwd(sm, io.e[0], io.epart + (size_t)blockIdx.x * 2 * kEmbPart, b0);
+    embed_bwd(sm, io.e[0], io.xg, io.epart + (size_t)blockIdx.x * 2 * kEmbPart, b0);
 }
 
 

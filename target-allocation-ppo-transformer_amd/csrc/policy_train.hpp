@@ -38,10 +38,16 @@ struct BwdLayerIO {
     float *dqkv;                 // [R][384] (pruned layers: Q part on token-4 rows only)
     float *dz1, *du, *df;        // d(LN1 input), d(FFN hidden pre-ReLU), d(LN2 input) rows
     float *ln1_part, *ln2_part;  // [Bm/16][256]: dgamma | dbeta partials per workgroup
+    float* bpart;                // this layer's [kBiasLayer] slice of rows [Bm/16][kBiasPart]
 };
-constexpr int kEmbPart = D * IN + D + S * D;  // 2560: We [128][14] | be [128] | pos [5][128]
-constexpr int kHeadPartN = 2 * HID + 2 + HID + 1;  // dW / db of actor_head.2 and critic_head.2
-constexpr int kHeadPart = 196;                     // padded
+constexpr int kEmbPart = S * D + D * IN + D;  // 2560: pos [5][128] | We [128][14] | be [128]
+// per-workgroup head partials: dW / db of actor_head.2 [0, 130) and critic_head.2 [130, 195), then
+// db of actor_head.0 [196, 260) and critic_head.0 [260, 324)
+constexpr int kHeadB0 = 196;
+constexpr int kHeadPart = kHeadB0 + 2 * HID;
+// per-workgroup bias partials of one encoder layer (sums over its rows of the dY operands)
+constexpr int kBiasL1 = 0, kBiasL2 = FF, kBiasOut = FF + D, kBiasIn = FF + 2 * D, kBiasLayer = FF + 5 * D;
+constexpr int kBiasPart = 3 * kBiasLayer;  // 2688: actor L0 | critic L0 | critic L1
 struct BwdIO {
     // heads + loss (ppo.py:148-169): per-sample inputs / logits / value (TrainIO::smp), the loss
     // sums over the global minibatch (all-reduced when data parallel), relu(head.0) rows

@@ -7,9 +7,9 @@
 //              with the heads and per-workgroup loss partials, then k_loss_sums (the four sums)
 //    backward  k_policy_backward (K6, policy.hip: loss and head gradients, dX of the encoder
 //              layers and embeddings, one workgroup per 16 samples), then every weight
-//              gradient dW[out][in] = sum_row dY[row][out] X[row][in] as one grouped fp32 MFMA GEMM
-//              (gemm.hpp, L_DW, split-K partial slabs + bias gradients as row sums of dY) and one
-//              k_reduce_grads over all partials
+//              gradient dW[out][in] = sum_row dY[row][out] X[row][in] as one stream-K fp32 MFMA
+//              launch (wgrad.hpp: per-workgroup partial tiles), and one k_reduce_grads over all
+//              partials (weight tiles, K6's bias / LayerNorm / embedding / head partials)
 //    update    k_adam (clip_grad_norm_ + Adam on the g^2 block partials of k_reduce_grads, or of
 //              k_grad_norm after a data-parallel all-reduce)
 // The last encoder layer of each trunk is pruned to the token the heads read (s = 4): K and V for
@@ -19,7 +19,7 @@
 
 #include "common.hpp"
 #include "policy_layout.hpp"
-#include "gemm.hpp"
+#include "wgrad.hpp"
 #include "policy_train.hpp"
 
 namespace uavhip {
@@ -81,8 +81,10 @@ using pol::kEmbPart;
 // the heads): a block takes 64 consecutive elements, each wave every 4th part, so every load is a
 // coalesced 256 B row segment; the 4 wave sums combine in a fixed order (deterministic).
 struct Segment {
-    const float* src;
+    const float* src;       // part 0
+    const float* src_rest;  // part p >= 1 at src_rest + (p - 1) * part_stride
     int dst, count, parts, part_stride, block_begin, tile_mode;
+    int dst_ld;             // 0: dst + i; else a 128-wide weight tile, dst + (i / 128) * dst_ld + i % 128
 };
 constexpr int kMaxSegs = 64;
 constexpr int kTileModeParts = 16;  // more parts than this: tile mode
@@ -102,12 +104,14 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
     }
     const Segment& S_ = sb.s[si];
     const size_t ps = S_.part_stride;
+    auto part = [&](int p) { return p == 0 ? S_.src : S_.src_rest + (size_t)(p - 1) * ps; };
+    auto dsti = [&](int i) { return S_.dst + (S_.dst_ld ? (i >> 7) * S_.dst_ld + (i & 127) : i); };
     float sq = 0.f;
     if (S_.tile_mode) {
         const int wv = threadIdx.x >> 6, l = lane_id();
         const int i = (blockIdx.x - S_.block_begin) * 64 + l;
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        if (i < S_.count) {
+        if (i < S_.count) {  // uniform part stride in this mode (src_rest = src + part_stride)
             const float* src = S_.src + i;
             int p = wv;
             for (; p + 12 < S_.parts; p += 16) {
@@ -120,7 +124,7 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
         __syncthreads();
         if (wv == 0 && i < S_.count) {
             const float tot = (wsum[0][l] + wsum[1][l]) + (wsum[2][l] + wsum[3][l]);
-            grads[S_.dst + i] = tot;
+            grads[dsti(i)] = tot;
             sq = tot * tot;
         }
     } else {
@@ -128,15 +132,14 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
         if (i < S_.count) {
             // four independent chains keep four loads in flight per thread
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
-            const float* src = S_.src + i;
             int p = 0;
             for (; p + 4 <= S_.parts; p += 4) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) acc[u] += src[(size_t)(p + u) * ps];
+                for (int u = 0; u < 4; ++u) acc[u] += part(p + u)[i];
             }
-            for (; p < S_.parts; ++p) acc[0] += src[(size_t)p * ps];
+            for (; p < S_.parts; ++p) acc[0] += part(p)[i];
             const float tot = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-            grads[S_.dst + i] = tot;
+            grads[dsti(i)] = tot;
             sq = tot * tot;
         }
     }
@@ -231,28 +234,12 @@ struct Plan {
     float *xg, *mask, *smp, *e_a, *h0_a, *e_c, *h0_c;
     LayerBufs la, lc0, lc1;
     float *z_a, *z_c, *dz_a, *dz_c, *fpart, *hpart, *epart, *sq_part;
-    float* split_ws;
-    size_t split_floats;
+    float* wg_part;  // weight-gradient partial tiles [kWgGrid * kWgRuns][kWgSlot]
+    float* bpart;    // [Bm/16][kBiasPart] bias partials of K6
     float* packed;  // fragment-order copy of the parameters for the fused forward
     float* packedT; // transposed GEMM weights for the fused backward
     size_t total;   // workspace floats
 };
-
-constexpr int kSplitRows = 2048;  // K rows per split of the weight-gradient GEMMs
-
-inline int splits_for(int K) { return (K + kSplitRows - 1) / kSplitRows; }
-
-inline size_t dw_split_floats(int Bm) {
-    const int R = Bm * S;
-    auto slab = [&](int M, int N, int K) { return (size_t)splits_for(K) * ((size_t)M * N + M); };
-    size_t n = 0;
-    // actor L0 (pruned), critic L0 (full), critic L1 (pruned), both head.0
-    const size_t pruned = slab(2 * D, D, R) + slab(D, D, Bm) + slab(D, D, Bm) + slab(FF, D, Bm) + slab(D, FF, Bm);
-    n += 2 * pruned;
-    n += slab(3 * D, D, R) + slab(D, D, R) + slab(FF, D, R) + slab(D, FF, R);
-    n += 2 * slab(HID, D, Bm);
-    return n;
-}
 
 inline void carve_layer(WS& w, LayerBufs& L, int R, int rows) {
     L.qkv = w.take((size_t)R * 3 * D);
@@ -298,23 +285,14 @@ inline Plan make_plan(int Bm, float* base) {
     p.hpart = w.take((size_t)(Bm / kHeadSamples) * kHeadPart);
     p.epart = w.take((size_t)(Bm / kHeadSamples) * 2 * kEmbPart);
     p.sq_part = w.take(1 << 16);
-    p.split_floats = dw_split_floats(Bm);
-    p.split_ws = w.take(p.split_floats);
+    p.wg_part = w.take((size_t)kWgGrid * kWgRuns * kWgSlot);
+    p.bpart = w.take((size_t)(Bm / kHeadSamples) * pol::kBiasPart);
     p.packed = w.take(kOffs.o[kNumParams]);
     p.packedT = w.take(pol::kPackedTFloats);
     p.total = w.off;
     return p;
 }
 
-template <int LAYOUT>
-int run_gemm(const GemmBuilder& g, hipStream_t st) {
-    if (!g.valid()) {
-        set_error("k_gemm: problem shape not a multiple of the %d x %d x %d tile", g.bm, BN, BK);
-        return UAVHIP_EINVAL;
-    }
-    launch_gemm<LAYOUT>(g, st);
-    return check_launch("k_gemm");
-}
 
 inline const float* prm(const uavhip_ppo* c, int i) { return c->params + kOffs.o[i]; }
 
@@ -434,78 +412,90 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         for (int i = 0; i < 3; ++i)
             io.L[i] = pol::BwdLayerIO{lb[i]->qkv, lb[i]->xhat1, lb[i]->rstd1, lb[i]->u, lb[i]->xhat2, lb[i]->rstd2,
                                       lb[i]->dqkv, lb[i]->dz1, lb[i]->du, lb[i]->df, lb[i]->ln1_part,
-                                      lb[i]->ln2_part};
+                                      lb[i]->ln2_part, p.bpart + (size_t)i * pol::kBiasLayer};
         TR_CHECK(pol::policy_backward_train(p.packed, p.packedT, io, Bm, st));
     }
 
     // ---------------------------------------------------------------- weight gradients
     SegBatch sb{};
     int seg_blocks = 0;
-    auto seg = [&](const float* src, int dst, int count, int parts, int part_stride) {
+    auto seg = [&](const float* src, int dst, int count, int parts, int part_stride, const float* src_rest = nullptr,
+                   int dst_ld = 0) {
+        if (sb.n >= kMaxSegs) { ++sb.n; return; }
         Segment& s = sb.s[sb.n++];
         s.src = src; s.dst = dst; s.count = count; s.parts = parts; s.part_stride = part_stride;
+        s.src_rest = src_rest ? src_rest : src + part_stride;
+        s.dst_ld = dst_ld;
         s.block_begin = seg_blocks;
-        s.tile_mode = parts > kTileModeParts;
+        s.tile_mode = parts > kTileModeParts && !src_rest;
         seg_blocks += s.tile_mode ? (count + 63) / 64 : (count + 255) / 256;
     };
     {
-        GemmBuilder g;
-        float* ws = p.split_ws;
-        // dW[out][in] = sum_rows dY[row][out] X[row][in] into grads at (dst_w, dst_b) float offsets
-        auto dwo = [&](const float* dY, int ldy, const float* X, int ldx, int M, int N, int K, int dst_w, int dst_b) {
-            const int sp = splits_for(K);
-            float* slab = ws;
-            float* bpart = ws + (size_t)sp * M * N;
-            ws += (size_t)sp * ((size_t)M * N + M);
-            g.add(dY, ldy, X, ldx, slab, N, M, N, K, E_SPLIT, nullptr, nullptr, 0, bpart, kSplitRows);
-            seg(slab, dst_w, M * N, sp, M * N);
-            seg(bpart, dst_b, M, sp, M);
-        };
-        auto dw = [&](const float* dY, int ldy, const float* X, int ldx, int M, int N, int K, int pw, int pb) {
-            dwo(dY, ldy, X, ldx, M, N, K, kOffs.o[pw], kOffs.o[pb]);
+        // dW[out][in] = sum_rows dY[row][out] X[row][in]; dst = the weight's float offset
+        WgPlan wp;
+        int dst[kWgMaxProbs];
+        auto dw = [&](const float* dY, int ldy, const float* X, int ldx, int M, int N, int K, int dst_w) {
+            dst[wp.b.n] = dst_w;
+            wp.add(dY, ldy, X, ldx, M, N, K);
         };
         auto layer_dw = [&](const LayerBufs& B, int tr_, int ly, const float* hin, int rows) {
-            const int pw = kOffs.o[layer_param(tr_, ly, INW)], pb = kOffs.o[layer_param(tr_, ly, INB)];
+            const int pw = kOffs.o[layer_param(tr_, ly, INW)];
             if (rows == R) {
-                dwo(B.dqkv, 3 * D, hin, D, 3 * D, D, R, pw, pb);
+                dw(B.dqkv, 3 * D, hin, D, 3 * D, D, R, pw);
             } else {  // pruned: K/V rows over all R rows, Q rows over the Bm token-4 rows
-                dwo(B.dqkv + D, 3 * D, hin, D, 2 * D, D, R, pw + D * D, pb + D);
-                dwo(B.dqkv + (S - 1) * 3 * D, S * 3 * D, hin + (S - 1) * D, S * D, D, D, Bm, pw, pb);
+                dw(B.dqkv + D, 3 * D, hin, D, 2 * D, D, R, pw + D * D);
+                dw(B.dqkv + (S - 1) * 3 * D, S * 3 * D, hin + (S - 1) * D, S * D, D, D, Bm, pw);
             }
-            dw(B.dz1, D, B.o, D, D, D, rows, layer_param(tr_, ly, OUTW), layer_param(tr_, ly, OUTB));
-            dw(B.du, FF, B.h1, D, FF, D, rows, layer_param(tr_, ly, L1W), layer_param(tr_, ly, L1B));
-            dw(B.df, D, B.u, FF, D, FF, rows, layer_param(tr_, ly, L2W), layer_param(tr_, ly, L2B));
+            dw(B.dz1, D, B.o, D, D, D, rows, kOffs.o[layer_param(tr_, ly, OUTW)]);
+            dw(B.du, FF, B.h1, D, FF, D, rows, kOffs.o[layer_param(tr_, ly, L1W)]);
+            dw(B.df, D, B.u, FF, D, FF, rows, kOffs.o[layer_param(tr_, ly, L2W)]);
         };
+        layer_dw(C0, tc, 0, p.h0_c, R);  // the long problems first
         layer_dw(A, ta, 0, p.h0_a, Bm);
-        layer_dw(C0, tc, 0, p.h0_c, R);
         layer_dw(C1, tc, 1, C0.h2, Bm);
-        dw(p.dz_a, HID, A.h2, D, HID, D, Bm, kActorHead, kActorHead + 1);
-        dw(p.dz_c, HID, C1.h2, D, HID, D, Bm, kCriticHead, kCriticHead + 1);
-        TR_CHECK(run_gemm<L_DW>(g, st));
+        dw(p.dz_a, HID, A.h2, D, HID, D, Bm, kOffs.o[kActorHead]);
+        dw(p.dz_c, HID, C1.h2, D, HID, D, Bm, kOffs.o[kCriticHead]);
+        wp.b.part = p.wg_part;
+        const bool sched = wp.ok && wp.tiles([&](const WgTileRuns& t) {
+            const WgProb& P = wp.b.p[t.prob];
+            seg(p.wg_part + (size_t)t.first_slot * kWgSlot, dst[t.prob] + t.m0 * P.N + t.n0, t.rows * kWgT, t.runs,
+                kWgRuns * kWgSlot, p.wg_part + (size_t)t.rest_slot * kWgSlot, P.N);
+        });
+        if (!sched) {
+            set_error("uavhip_ppo_step: weight-gradient problems do not fit the stream-K schedule");
+            return UAVHIP_EINVAL;
+        }
+        hipLaunchKernelGGL(k_wgrad, dim3(wp.grid), dim3(kWgThreads), 0, st, wp.b);
+        TR_CHECK(check_launch("k_wgrad"));
     }
-    // LayerNorm weights / biases
-    auto ln_seg = [&](const float* part, int pw, int pb) {
-        seg(part, kOffs.o[pw], D, nblk, 2 * D);
-        seg(part + D, kOffs.o[pb], D, nblk, 2 * D);
-    };
-    ln_seg(A.ln1_part, layer_param(ta, 0, N1W), layer_param(ta, 0, N1B));
-    ln_seg(A.ln2_part, layer_param(ta, 0, N2W), layer_param(ta, 0, N2B));
-    ln_seg(C0.ln1_part, layer_param(tc, 0, N1W), layer_param(tc, 0, N1B));
-    ln_seg(C0.ln2_part, layer_param(tc, 0, N2W), layer_param(tc, 0, N2B));
-    ln_seg(C1.ln1_part, layer_param(tc, 1, N1W), layer_param(tc, 1, N1B));
-    ln_seg(C1.ln2_part, layer_param(tc, 1, N2W), layer_param(tc, 1, N2B));
-    // embeddings (We | be | pos per trunk), head.2 weights / biases
-    for (int trunk = 0; trunk < 2; ++trunk) {
-        const int base = trunk ? kCriticTrunk : kActorTrunk;
-        const float* src = p.epart + (size_t)trunk * kEmbPart;
-        seg(src, kOffs.o[base + EMB_W], D * IN, nblk, 2 * kEmbPart);
-        seg(src + D * IN, kOffs.o[base + EMB_B], D, nblk, 2 * kEmbPart);
-        seg(src + D * IN + D, kOffs.o[base + POS], S * D, nblk, 2 * kEmbPart);
+    // biases of the encoder layers (K6's per-workgroup sums of the dY rows)
+    {
+        const int lt[3][2] = {{ta, 0}, {tc, 0}, {tc, 1}};
+        for (int i = 0; i < 3; ++i) {
+            const float* bp = p.bpart + (size_t)i * pol::kBiasLayer;
+            const int tr_ = lt[i][0], ly = lt[i][1];
+            seg(bp + pol::kBiasL1, kOffs.o[layer_param(tr_, ly, L1B)], FF, nblk, pol::kBiasPart);
+            seg(bp + pol::kBiasL2, kOffs.o[layer_param(tr_, ly, L2B)], D, nblk, pol::kBiasPart);
+            seg(bp + pol::kBiasOut, kOffs.o[layer_param(tr_, ly, OUTB)], D, nblk, pol::kBiasPart);
+            seg(bp + pol::kBiasIn, kOffs.o[layer_param(tr_, ly, INB)], 3 * D, nblk, pol::kBiasPart);
+        }
     }
-    seg(p.hpart, kOffs.o[kActorHead + 2], 2 * HID, nblk, kHeadPart);
-    seg(p.hpart + 2 * HID, kOffs.o[kActorHead + 3], 2, nblk, kHeadPart);
-    seg(p.hpart + 2 * HID + 2, kOffs.o[kCriticHead + 2], HID, nblk, kHeadPart);
-    seg(p.hpart + 3 * HID + 2, kOffs.o[kCriticHead + 3], 1, nblk, kHeadPart);
+    // LayerNorm weight | bias (adjacent parameters, as in the partial rows)
+    const LayerBufs* lbs[3] = {&A, &C0, &C1};
+    const int lts[3][2] = {{ta, 0}, {tc, 0}, {tc, 1}};
+    for (int i = 0; i < 3; ++i) {
+        seg(lbs[i]->ln1_part, kOffs.o[layer_param(lts[i][0], lts[i][1], N1W)], 2 * D, nblk, 2 * D);
+        seg(lbs[i]->ln2_part, kOffs.o[layer_param(lts[i][0], lts[i][1], N2W)], 2 * D, nblk, 2 * D);
+    }
+    // embeddings (pos | We | be per trunk, adjacent parameters)
+    for (int trunk = 0; trunk < 2; ++trunk)
+        seg(p.epart + (size_t)trunk * kEmbPart, kOffs.o[(trunk ? kCriticTrunk : kActorTrunk) + POS], kEmbPart, nblk,
+            2 * kEmbPart);
+    // heads: head.2 weight | bias (adjacent), head.0 bias
+    seg(p.hpart, kOffs.o[kActorHead + 2], 2 * HID + 2, nblk, kHeadPart);
+    seg(p.hpart + 2 * HID + 2, kOffs.o[kCriticHead + 2], HID + 1, nblk, kHeadPart);
+    seg(p.hpart + pol::kHeadB0, kOffs.o[kActorHead + 1], HID, nblk, kHeadPart);
+    seg(p.hpart + pol::kHeadB0 + HID, kOffs.o[kCriticHead + 1], HID, nblk, kHeadPart);
     if (sb.n > kMaxSegs || seg_blocks > (1 << 16)) {
         set_error("uavhip_ppo_step: too many gradient segments (%d) / blocks (%d)", sb.n, seg_blocks);
         return UAVHIP_EINVAL;
