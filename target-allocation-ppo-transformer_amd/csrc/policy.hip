@@ -39,6 +39,11 @@ constexpr int LDX = 16;         // input rows padded 14 -> 16 (one MFMA k-block)
 constexpr int LDZ = HID + 8;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+#ifdef UAVHIP_EXP_NOSTORE
+constexpr bool kExpNoStore = true;
+#else
+constexpr bool kExpNoStore = false;
+#endif
 
 // Phase tracing (make TRACE=1 only): waves 0 and 4 of the first 256 workgroups stamp s_memtime at
 // the phase boundaries below; uavhip_policy_trace copies the stamps out. Off in the product build.
@@ -50,12 +55,23 @@ __device__ unsigned long long g_ptrace[256 * 2 * kTraceSlots];
         if ((threadIdx.x & 255) == 0 && blockIdx.x < 256)                                        \
             g_ptrace[(blockIdx.x * 2 + (threadIdx.x >> 8)) * kTraceSlots + (id)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+__device__ unsigned long long g_btrace[256 * 2 * kTraceSlots];
+#define BTR(id)                                                                                  \
+    do {                                                                                         \
+        if ((threadIdx.x & 255) == 0 && blockIdx.x < 256)                                        \
+            g_btrace[(blockIdx.x * 2 + (threadIdx.x >> 8)) * kTraceSlots + (id)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #else
 #define PTR(id) do {} while (0)
+#define BTR(id) do {} while (0)
 #endif
 
+constexpr int kScr = NW * 3 * 64;  // backward scratch: per-wave in_proj bias partial rows
 struct Smem {
-    float x[TOK * LDX];         // input windows [tok = s*16 + p][k], k < 14 valid
+    union {
+        float x[TOK * LDX];     // input windows [tok = s*16 + p][k], k < 14 valid
+        float scr[kScr];        // backward: scratch while the windows are not needed
+    };
     float h[TOK * LDH];         // residual stream [tok][128]
     float big[TOK * LDB];       // QKV chunk / out-proj result / FFN hidden chunk
     float ctx[TOK * LDH];       // attention output / FFN output
@@ -243,7 +259,7 @@ __device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[
         const f32x4 xh = (v[ct] - mean) * rs;
         const f32x4 out = xh * ww + lb;
         *reinterpret_cast<f32x4*>(sm.h + tok * LDH + f0) = out;
-        if (TR) {
+        if (TR && !kExpNoStore) {
             const size_t r = (size_t)orow(tok, lo.b0, lo.compact);
             *reinterpret_cast<f32x4*>(lo.x + r * D + f0) = xh;
             *reinterpret_cast<f32x4*>(lo.h + r * D + f0) = out;
@@ -256,6 +272,9 @@ __device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[
 // offset c0) for tokens [t0, TOK), all 512 threads, float4 granules.
 __device__ __forceinline__ void store_rows(const float* src, int lds, float* dst, int ldo, int c0, int ncols, int t0,
                                            int b0, bool compact) {
+#ifdef UAVHIP_EXP_NOSTORE  // timing experiment only (make NOSTORE=1): activations not written
+    return;
+#endif
     const int n4 = ncols / 4, items = (TOK - t0) * n4;
     for (int i = threadIdx.x; i < items; i += NTHR) {
         const int tok = t0 + i / n4, q = i % n4;
@@ -379,7 +398,7 @@ __device__ void embed(Smem& sm, const float* __restrict__ P, float* e_out = null
         e.x = fmaxf(e.x, 0.f); e.y = fmaxf(e.y, 0.f); e.z = fmaxf(e.z, 0.f); e.w = fmaxf(e.w, 0.f);
         const f32x4 v = e + pp;
         *reinterpret_cast<f32x4*>(sm.h + (ct * SPW + i16) * LDH + 16 * wv + 4 * g) = v;
-        if (TR) {
+        if (TR && !kExpNoStore) {
             const size_t r = (size_t)trow(ct * SPW + i16, b0);
             *reinterpret_cast<f32x4*>(e_out + r * D + 16 * wv + 4 * g) = e;
             *reinterpret_cast<f32x4*>(h_out + r * D + 16 * wv + 4 * g) = v;
@@ -426,7 +445,7 @@ __device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv
         PTR(tb + 1 + 3 * c);
         __syncthreads();
         PTR(tb + 2 + 3 * c);
-        if (TR) {  // this chunk's Q (query tokens) / K / V -> qkv[row][part * 128 + 64 c + d]
+        if (TR && !kExpNoStore) {  // this chunk's Q (query tokens) / K / V -> qkv[row][part * 128 + 64 c + d]
             for (int i = threadIdx.x; i < TOK * 48; i += NTHR) {
                 const int tok = i / 48, r = i - tok * 48, part = r >> 4, q = r & 15;
                 if (part == 0 && tok < qtok0) continue;
@@ -696,11 +715,28 @@ __device__ void ln_bwd_lds(const float* src, float* dst, const float* __restrict
     const f32x4 w0 = ld4(w + f0), w1 = ld4(w + f0 + 4);
     const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
     f32x4 pw0 = zero4, pw1 = zero4, pb0 = zero4, pb1 = zero4, pd0 = zero4, pd1 = zero4;
-    for (int tok = t0 + grp; tok < TOK; tok += NTHR / 16) {
+    // all of this lane group's (<= 3) tokens' global operands in one round trip
+    constexpr int kIt = (TOK + NTHR / 16 - 1) / (NTHR / 16);
+    f32x4 X0[kIt], X1[kIt];
+    float RS[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const int tok = t0 + grp + it * (NTHR / 16);
+        if (tok < TOK) {
+            const size_t r = (size_t)orow(tok, b0, compact);
+            X0[it] = ld4(xhat + r * D + f0);
+            X1[it] = ld4(xhat + r * D + f0 + 4);
+            RS[it] = rstd[r];
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const int tok = t0 + grp + it * (NTHR / 16);
+        if (tok >= TOK) continue;
         const size_t r = (size_t)orow(tok, b0, compact);
         const f32x4 g0 = ld4(src + tok * LDH + f0), g1 = ld4(src + tok * LDH + f0 + 4);
-        const f32x4 x0 = ld4(xhat + r * D + f0), x1 = ld4(xhat + r * D + f0 + 4);
-        const float rs = rstd[r];
+        const f32x4 x0 = X0[it], x1 = X1[it];
+        const float rs = RS[it];
         const f32x4 gw0 = g0 * w0, gw1 = g1 * w1;
         const float m1 = row16_sum(hsum(gw0) + hsum(gw1)) * (1.0f / D);
         const float m2 = row16_sum(hsum(gw0 * x0) + hsum(gw1 * x1)) * (1.0f / D);
@@ -732,38 +768,47 @@ __device__ void ln_bwd_lds(const float* src, float* dst, const float* __restrict
 // with g = d(attention output) of the query rows (sm.ctx):
 //   dv_j = sum_i P_ij g_i; dP_ij = g_i . v_j; dS_ij = P_ij (dP_ij - sum_k P_ik dP_ik);
 //   dq_i = sum_j dS_ij k_j / 4; dk_j = sum_i dS_ij q_i / 4.
-// One (sample, head) task per 4 lanes (threads 0-255). dq | dk | dv -> sm.big [tok][3 x 64] (the
-// forward's chunk layout) and dqkv rows (pruned layers: dq only for the token-4 query rows; the
-// LDS copy is zero on the other rows).
+// One (sample, head) task per 8 lanes, 2 of the 16 head dims each (all 512 threads; dot products
+// reduced over the 8 lanes with two quad permutes and a half-row mirror). dq | dk | dv ->
+// sm.big [tok][3 x 64] (the forward's chunk layout) and dqkv rows (pruned layers: dq only for the
+// token-4 query rows; the LDS copy is zero on the other rows). Per-wave sums over the wave's 2
+// samples of dq, dk, dv -> scratch [wave][192] (in_proj bias partials).
+__device__ __forceinline__ float add_hmirror8(float v) {  // + lane 7 - i within each group of 8
+    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float sum8(float v) { return add_hmirror8(add_xor2(add_xor1(v))); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 ld2(const float* p) { return *reinterpret_cast<const f32x2*>(p); }
+__device__ __forceinline__ void st2(float* p, f32x2 v) { *reinterpret_cast<f32x2*>(p) = v; }
+
 template <bool last>
 __device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, float* __restrict__ dqkv, int c, int b0,
                                float* scratch) {
-    if (threadIdx.x >= 256) return;
-    const int q4 = threadIdx.x & 3, hh = (threadIdx.x >> 2) & 3, p = threadIdx.x >> 4;
-    const int d0 = hh * HD + 4 * q4, col = 64 * c + d0;
+    const int o8 = threadIdx.x & 7, hh = (threadIdx.x >> 3) & 3, p = threadIdx.x >> 5;
+    const int d0 = hh * HD + 2 * o8, col = 64 * c + d0;
     const size_t rb = (size_t)(b0 + p) * S;
-    f32x4 k[S], v[S], dk[S], dv[S];
+    f32x2 k[S], v[S], dk[S], dv[S];
     bool msk[S];
-    f32x4 sdq = {0.f, 0.f, 0.f, 0.f};
+    f32x2 sdq = {0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-        k[j] = ld4(qkv + (rb + j) * 3 * D + D + col);
-        v[j] = ld4(qkv + (rb + j) * 3 * D + 2 * D + col);
+        k[j] = ld2(qkv + (rb + j) * 3 * D + D + col);
+        v[j] = ld2(qkv + (rb + j) * 3 * D + 2 * D + col);
         msk[j] = sm.mask[p * S + j] != 0;
-        dk[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dk[j] = f32x2{0.f, 0.f};
+        dv[j] = f32x2{0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < S; ++i) {
-        f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+        f32x2 dq = {0.f, 0.f};
         if (!last || i == S - 1) {
-            const f32x4 q = ld4(qkv + (rb + i) * 3 * D + col);
-            const f32x4 g = ld4(sm.ctx + (i * SPW + p) * LDH + col);
+            const f32x2 q = ld2(qkv + (rb + i) * 3 * D + col);
+            const f32x2 g = ld2(sm.ctx + (i * SPW + p) * LDH + col);
             float pr[S], dp[S];
             float mx = -INFINITY;
 #pragma unroll
             for (int j = 0; j < S; ++j) {
-                const float part = add_xor2(add_xor1(q.x * k[j].x + q.y * k[j].y + q.z * k[j].z + q.w * k[j].w));
+                const float part = sum8(q.x * k[j].x + q.y * k[j].y);
                 pr[j] = msk[j] ? -INFINITY : part * 0.25f;
                 mx = fmaxf(mx, pr[j]);
             }
@@ -778,7 +823,7 @@ __device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, float* _
 #pragma unroll
             for (int j = 0; j < S; ++j) {
                 pr[j] *= inv;
-                dp[j] = add_xor2(add_xor1(g.x * v[j].x + g.y * v[j].y + g.z * v[j].z + g.w * v[j].w));
+                dp[j] = sum8(g.x * v[j].x + g.y * v[j].y);
                 sdp += pr[j] * dp[j];
             }
 #pragma unroll
@@ -788,42 +833,42 @@ __device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, float* _
                 dk[j] += ds * q;
                 dv[j] += pr[j] * g;
             }
-            st4(dqkv + (rb + i) * 3 * D + col, dq);
+            st2(dqkv + (rb + i) * 3 * D + col, dq);
             sdq += dq;
         }
-        st4(sm.big + (i * SPW + p) * LDB + d0, dq);
+        st2(sm.big + (i * SPW + p) * LDB + d0, dq);
     }
-    f32x4 sk = {0.f, 0.f, 0.f, 0.f}, sv = {0.f, 0.f, 0.f, 0.f};
+    f32x2 sk = {0.f, 0.f}, sv = {0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-        st4(sm.big + (j * SPW + p) * LDB + 64 + d0, dk[j]);
-        st4(sm.big + (j * SPW + p) * LDB + 128 + d0, dv[j]);
-        st4(dqkv + (rb + j) * 3 * D + D + col, dk[j]);
-        st4(dqkv + (rb + j) * 3 * D + 2 * D + col, dv[j]);
+        st2(sm.big + (j * SPW + p) * LDB + 64 + d0, dk[j]);
+        st2(sm.big + (j * SPW + p) * LDB + 128 + d0, dv[j]);
+        st2(dqkv + (rb + j) * 3 * D + D + col, dk[j]);
+        st2(dqkv + (rb + j) * 3 * D + 2 * D + col, dv[j]);
         sk += dk[j];
         sv += dv[j];
     }
-    // in_proj bias partials: sums over the wave's 4 samples (lanes 16 apart), one row per wave
-    f32x4 sq = sdq;
+    // the wave's two samples are lanes 32 apart
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        sq[e] = add_xor32(add_xor16(sq[e]));
-        sk[e] = add_xor32(add_xor16(sk[e]));
-        sv[e] = add_xor32(add_xor16(sv[e]));
+    for (int e = 0; e < 2; ++e) {
+        sdq[e] = add_xor32(sdq[e]);
+        sk[e] = add_xor32(sk[e]);
+        sv[e] = add_xor32(sv[e]);
     }
-    if ((threadIdx.x & 63) < 16) {
+    if ((threadIdx.x & 63) < 32) {
         float* row = scratch + (threadIdx.x >> 6) * 3 * 64;
-        st4(row + d0, sq);
-        st4(row + 64 + d0, sk);
-        st4(row + 128 + d0, sv);
+        st2(row + d0, sdq);
+        st2(row + 64 + d0, sk);
+        st2(row + 128 + d0, sv);
     }
 }
 
 // Backward of one post-LN encoder layer. On entry sm.h holds dL/d(layer output) for the tokens
 // >= qtok0; on exit sm.h holds dL/d(layer input) for all 80 tokens. Ends with a barrier.
-template <int trunk, int layer, bool last>
+template <int trunk, int layer, bool last, int TB>
 __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __restrict__ PT, const BwdLayerIO& io,
                           int b0) {
+    BTR(TB);
     constexpr int CTQ = last ? 1 : S;
     constexpr int DQ = depth<CTQ>();
     constexpr int qtok0 = last ? (S - 1) * SPW : 0;
@@ -839,12 +884,17 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
     APre<DQ> pa = prefetch<DQ>(W2T, D, 16 * wv, 0);
     ln_bwd_lds(sm.h, sm.ctx, io.xhat2, io.rstd2, P + kOffs.o[layer_param(trunk, layer, N2W)], io.df,
                io.ln2_part + (size_t)blockIdx.x * 2 * D, bias + kBiasL2, qtok0, b0, last, sm.big);
+    BTR(TB + 1);
     __syncthreads();
+    BTR(TB + 2);
     // du = relu'(u) (W2^T df): 256 hidden features, wave wv owns tiles 16 wv (-> big) and 128 + 16 wv (-> h)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         const int row = 128 * t + 16 * wv;
-        f32x4 acc[CTQ];
+        f32x4 acc[CTQ], uu[CTQ];  // u (for the ReLU mask) loaded ahead of the GEMM
+#pragma unroll
+        for (int ct = 0; ct < CTQ; ++ct)
+            uu[ct] = ld4(io.u + (size_t)orow(qtok0 + 16 * ct + i16, b0, last) * FF + row + 4 * g);
         zero(acc);
         if (t == 0) gemm_tile<CTQ, DQ>(acc, pa, W2T, D, row, 0, sm.ctx, LDH, qtok0);
         else gemm_tile<CTQ, DQ>(acc, prefetch<DQ>(W2T, D, row, 0), W2T, D, row, 0, sm.ctx, LDH, qtok0);
@@ -854,7 +904,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         for (int ct = 0; ct < CTQ; ++ct) {
             const int tok = qtok0 + 16 * ct + i16;
             const size_t r = (size_t)orow(tok, b0, last);
-            const f32x4 u = ld4(io.u + r * FF + row + 4 * g);
+            const f32x4 u = uu[ct];
             f32x4 d = acc[ct];
             d.x = u.x > 0.f ? d.x : 0.f; d.y = u.y > 0.f ? d.y : 0.f;
             d.z = u.z > 0.f ? d.z : 0.f; d.w = u.w > 0.f ? d.w : 0.f;
@@ -868,7 +918,9 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         if (i16 == 0) st4(bias + kBiasL1 + row + 4 * g, sd);
     }
     pa = prefetch<DQ>(W1T, FF, 16 * wv, 0);
+    BTR(TB + 3);
     __syncthreads();
+    BTR(TB + 4);
     // dh1 = df + W1^T du (K = 256: hidden 0-127 in big, 128-255 in h) -> sm.ctx in place
     {
         f32x4 acc[CTQ];
@@ -882,11 +934,15 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         }
     }
     pa = prefetch<DQ>(WoT, D, 16 * wv, 0);
+    BTR(TB + 5);
     __syncthreads();
+    BTR(TB + 6);
     // LN1 backward: sm.ctx -> sm.h (= dz1)
     ln_bwd_lds(sm.ctx, sm.h, io.xhat1, io.rstd1, P + kOffs.o[layer_param(trunk, layer, N1W)], io.dz1,
                io.ln1_part + (size_t)blockIdx.x * 2 * D, bias + kBiasOut, qtok0, b0, last, sm.big);
+    BTR(TB + 7);
     __syncthreads();
+    BTR(TB + 8);
     // d(attention output) = Wo^T dz1 -> sm.ctx
     {
         f32x4 acc[CTQ];
@@ -895,27 +951,40 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
 #pragma unroll
         for (int ct = 0; ct < CTQ; ++ct) st4(sm.ctx + (qtok0 + 16 * ct + i16) * LDH + fo, acc[ct]);
     }
+    BTR(TB + 9);
     __syncthreads();
+    BTR(TB + 10);
     // attention backward per chunk of 4 heads, dh_in += Win^T [dq | dk | dv] of the chunk (K = 3 x 64)
     f32x4 acc[S];
     zero(acc);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         APre<2> pw = prefetch<2>(WinT, 3 * D, 16 * wv, 64 * c);
-        attn_bwd_chunk<last>(sm, io.qkv, io.dqkv, c, b0, sm.x);
+        attn_bwd_chunk<last>(sm, io.qkv, io.dqkv, c, b0, sm.scr);
         __syncthreads();
-        if (threadIdx.x < 3 * 64) {  // in_proj bias partial of the chunk: the 4 wave rows of sm.x
+        BTR(TB + 11 + 2 * c);
+        if (threadIdx.x < 3 * 64) {  // in_proj bias partial of the chunk: the 8 wave rows of sm.scr
             const int i = threadIdx.x;
-            const float v = (sm.x[i] + sm.x[192 + i]) + (sm.x[384 + i] + sm.x[576 + i]);
+            float v = 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) v += sm.scr[w * 192 + i];
             bias[kBiasIn + (i >> 6) * D + 64 * c + (i & 63)] = v;
         }
+        if (last) {  // dq is zero outside the query tile: Win_q^T dq only for column tile 4
+            f32x4 a1[1] = {acc[S - 1]};
+            gemm_tile<1, 2, 4>(a1, pw, WinT, 3 * D, 16 * wv, 64 * c, sm.big, LDB, (S - 1) * SPW);
+            acc[S - 1] = a1[0];
+        } else {
+            gemm_tile<S, 2, 4>(acc, pw, WinT, 3 * D, 16 * wv, 64 * c, sm.big, LDB, 0);
+        }
 #pragma unroll
-        for (int part = 0; part < 3; ++part) {
+        for (int part = 1; part < 3; ++part) {
             const int kw = part * D + 64 * c;
-            if (part) pw = prefetch<2>(WinT, 3 * D, 16 * wv, kw);
-            gemm_tile<S, 2, 4>(acc, pw, WinT, 3 * D, 16 * wv, kw, sm.big + part * 64, LDB, 0);
+            gemm_tile<S, 2, 4>(acc, prefetch<2>(WinT, 3 * D, 16 * wv, kw), WinT, 3 * D, 16 * wv, kw,
+                               sm.big + part * 64, LDB, 0);
         }
         if (c == 0) __syncthreads();  // big is rewritten by chunk 1
+        BTR(TB + 12 + 2 * c);
     }
     // + dz1 on the rows that carried the residual -> sm.h
 #pragma unroll
@@ -925,6 +994,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         st4(q, tok >= qtok0 ? acc[ct] + ld4(q) : acc[ct]);
     }
     __syncthreads();
+    BTR(TB + 15);
 }
 
 // Embedding backward from sm.h = dL/d(h0) (80 tokens): h0 = relu(We x + be) + pos. Thread =
@@ -932,12 +1002,15 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
 // in the parameters' order (pos | We | be).
 __device__ void embed_bwd(Smem& sm, const float* __restrict__ e, const float* __restrict__ xg,
                           float* __restrict__ part, int b0) {
+    const int f = threadIdx.x & (D - 1), grp = threadIdx.x >> 7;
+    float ev[TOK / 4];  // this thread's embedding values (the ReLU mask), loaded with the windows
+#pragma unroll
+    for (int i = 0; i < TOK / 4; ++i) ev[i] = e[(size_t)trow(grp + 4 * i, b0) * D + f];
     for (int i = threadIdx.x; i < TOK * LDX / 4; i += NTHR) {  // input windows (sm.x was scratch)
         const int t = i / (LDX / 4), q = i % (LDX / 4);
         st4(sm.x + t * LDX + 4 * q, ld4(xg + (size_t)trow(t, b0) * 16 + 4 * q));
     }
     __syncthreads();
-    const int f = threadIdx.x & (D - 1), grp = threadIdx.x >> 7;
     float acc[IN + 1 + S];
 #pragma unroll
     for (int v = 0; v < IN + 1 + S; ++v) acc[v] = 0.f;
@@ -946,7 +1019,7 @@ __device__ void embed_bwd(Smem& sm, const float* __restrict__ e, const float* __
         const int tok = grp + 4 * i;  // position tok / 16 = i / 4
         const float gv = sm.h[tok * LDH + f];
         acc[IN + 1 + i / 4] += gv;
-        const float gp = e[(size_t)trow(tok, b0) * D + f] > 0.f ? gv : 0.f;
+        const float gp = ev[i] > 0.f ? gv : 0.f;
         acc[IN] += gp;
 #pragma unroll
         for (int k = 0; k < IN; ++k) acc[k] += gp * sm.x[tok * LDX + k];
@@ -972,11 +1045,21 @@ __device__ void embed_bwd(Smem& sm, const float* __restrict__ e, const float* __
 __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io, int b0) {
     float* gs = sm.ctx;                  // [16][4]: dlogit0, dlogit1, dvalue
     float* dzc = sm.ctx + 64;            // critic dz rows
+    float* zs = sm.big;                  // relu(head.0) rows of both heads [2][16][64]
     const float inv = 1.0f / (float)io.Bg;
     const float tot0 = io.tot[0], tot1 = io.tot[1], tot2 = io.tot[2], tot3 = io.tot[3];
+    {   // every global input in one round trip: z rows (one float4 per thread), per-sample rows,
+        // the head.2 weights of this thread's hidden unit j = tid % 64 (the dz loop below)
+        const int trunk = threadIdx.x >> 8, p = (threadIdx.x >> 4) & 15, q = threadIdx.x & 15;
+        st4(zs + (trunk * SPW + p) * HID + 4 * q, ld4(io.z[trunk] + (size_t)(b0 + p) * HID + 4 * q));
+    }
+    const int jj = threadIdx.x % HID;
+    const float* W2a = P + kOffs.o[kActorHead + 2];
+    const float w2a0 = W2a[jj], w2a1 = W2a[HID + jj], w2c = P[kOffs.o[kCriticHead + 2] + jj];
     if (threadIdx.x < SPW) {
         const int p = threadIdx.x;
-        const float* o = io.smp + (size_t)(b0 + p) * 8;
+        const f32x4 oa = ld4(io.smp + (size_t)(b0 + p) * 8), ob = ld4(io.smp + (size_t)(b0 + p) * 8 + 4);
+        const float o[8] = {oa.x, oa.y, oa.z, oa.w, ob.x, ob.y, ob.z, ob.w};
         const int act = o[0] != 0.f;
         const CatVals c = categorical(o[5], o[6]);
         const float logp = act ? c.lc1 : c.lc0;
@@ -1018,11 +1101,11 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         }
     }
     __syncthreads();
+    static_assert(NTHR % HID == 0, "dz loop: j = tid % 64 for every i");
     for (int i = threadIdx.x; i < 2 * SPW * HID; i += NTHR) {
         const int trunk = i / (SPW * HID), p = (i / HID) % SPW, j = i % HID;
-        const float* W2 = P + kOffs.o[(trunk ? kCriticHead : kActorHead) + 2];
-        const float z = io.z[trunk][(size_t)(b0 + p) * HID + j];
-        const float g = trunk ? W2[j] * gs[4 * p + 2] : W2[j] * gs[4 * p] + W2[HID + j] * gs[4 * p + 1];
+        const float z = zs[(trunk * SPW + p) * HID + j];
+        const float g = trunk ? w2c * gs[4 * p + 2] : w2a0 * gs[4 * p] + w2a1 * gs[4 * p + 1];
         const float dz = z > 0.f ? g : 0.f;
         io.dz[trunk][(size_t)(b0 + p) * HID + j] = dz;
         (trunk ? dzc : sm.z)[p * LDZ + j] = dz;
@@ -1042,12 +1125,12 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         float acc = 0.f;
         if (i < 2 * HID) {
             const int o = i / HID, j = i % HID;
-            for (int p = 0; p < SPW; ++p) acc += gs[4 * p + o] * io.z[0][(size_t)(b0 + p) * HID + j];
+            for (int p = 0; p < SPW; ++p) acc += gs[4 * p + o] * zs[p * HID + j];
         } else if (i < 2 * HID + 2) {
             for (int p = 0; p < SPW; ++p) acc += gs[4 * p + i - 2 * HID];
         } else if (i < 3 * HID + 2) {
             const int j = i - 2 * HID - 2;
-            for (int p = 0; p < SPW; ++p) acc += gs[4 * p + 2] * io.z[1][(size_t)(b0 + p) * HID + j];
+            for (int p = 0; p < SPW; ++p) acc += gs[4 * p + 2] * zs[(SPW + p) * HID + j];
         } else if (i < 3 * HID + 3) {
             for (int p = 0; p < SPW; ++p) acc += gs[4 * p + 2];
         }
@@ -1070,20 +1153,26 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
     __shared__ __attribute__((aligned(16))) Smem sm;
     const int b0 = blockIdx.x * SPW;
     if (threadIdx.x < SPW * S) sm.mask[threadIdx.x] = io.mask[(size_t)b0 * S + threadIdx.x] != 0.f;
+    BTR(0);
     heads_bwd(sm, P, io, b0);
     __syncthreads();
+    BTR(1);
     // critic: head.0, layer 1 (pruned), layer 0, embedding
     head_input_grad(sm, PT + kHeadT + D * HID, sm.ctx + 64);
     __syncthreads();
-    bwd_layer<kCriticTrunk, 1, true>(sm, P, PT + 2 * kLayerT, io.L[2], b0);
-    bwd_layer<kCriticTrunk, 0, false>(sm, P, PT + 1 * kLayerT, io.L[1], b0);
+    BTR(2);
+    bwd_layer<kCriticTrunk, 1, true, 4>(sm, P, PT + 2 * kLayerT, io.L[2], b0);
+    bwd_layer<kCriticTrunk, 0, false, 20>(sm, P, PT + 1 * kLayerT, io.L[1], b0);
     embed_bwd(sm, io.e[1], io.xg, io.epart + ((size_t)blockIdx.x * 2 + 1) * kEmbPart, b0);
     __syncthreads();
+    BTR(52);
     // actor: head.0, layer 0 (pruned), embedding
     head_input_grad(sm, PT + kHeadT, sm.z);
     __syncthreads();
-    bwd_layer<kActorTrunk, 0, true>(sm, P, PT, io.L[0], b0);
+    BTR(53);
+    bwd_layer<kActorTrunk, 0, true, 36>(sm, P, PT, io.L[0], b0);
     embed_bwd(sm, io.e[0], io.xg, io.epart + (size_t)blockIdx.x * 2 * kEmbPart, b0);
+    BTR(54);
 }
 
 
@@ -1194,6 +1283,11 @@ extern "C" int32_t uavhip_policy_tiling(int32_t* kcols, int32_t max_params) {
 extern "C" int uavhip_policy_trace(unsigned long long* out, int n) {
     const int total = 256 * 2 * pol::kTraceSlots;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(pol::g_ptrace), sizeof(unsigned long long) * (n < total ? n : total), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int uavhip_policy_btrace(unsigned long long* out, int n) {  // k_policy_backward stamps
+    const int total = 256 * 2 * pol::kTraceSlots;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pol::g_btrace), sizeof(unsigned long long) * (n < total ? n : total), 0,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
