@@ -165,8 +165,7 @@ def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
     acts = tr.actions.reshape(n).long()
     bufs = (states, acts, tr.logp.reshape(n), tr.values.reshape(n), tr.ret.reshape(n), tr.adv.reshape(n))
     if world > 1:  # the update runs on the all-gathered batch, data parallel over the ranks
-        from uavhip.dist import unpack_trajectory
-        g = unpack_trajectory(eng.gather())
+        g = eng.gather()  # this iteration's gathered batch (cached by the timed loop's call)
         bufs = (g["obs"], g["actions"], g["logp"], g["values"], g["returns"], g["advantages"])
         n = bufs[0].shape[0]
     if args.ppo_impl == "torch-eager":
@@ -241,7 +240,7 @@ def main():
     torch.manual_seed(0)  # identical initial policy on every rank
     policy = TransformerActorCritic().to(dev)
     env = VecUAVEnv(E, args.uavs, args.targets, 1, 1, seed=1 + rank, full_reset_period=200)
-    eng = RolloutEngine(env, policy, T, want_info=True, bootstrap=True, seed=1000 + rank)
+    eng = RolloutEngine(env, policy, T, want_info=True, bootstrap=True, seed=1000 + rank, normalize=(world == 1))
     eng.start()
 
     # The iteration is captured once into a hipGraph and replayed. HIP events (recorded on the

@@ -216,6 +216,18 @@ int uavhip_adv_partials(const float* adv, int64_t n, double* partials, int32_t n
 int uavhip_adv_normalize(float* adv, int64_t n, const double* partials, int32_t n_partials, int64_t n_total,
                          double* stats_out, uavhip_stream_t stream);
 
+/* Policy-input windows [blocks][T][E][5][14] of a trajectory from its compact all-gather form
+ * (uavhip/dist.py pack_compact; the data-parallel exchange of SURVEY.md 8e): per block, first
+ * windows first[e][70] (the window at step 0), rows[t][e][14] (the row pushed at step t = window
+ * slot 4; row 0 is read from the first window) and done flags done[(t * E + e) * done_stride] (f32,
+ * nonzero = the episode ended at step t, so step t + 1 starts from a zero window,
+ * uav_env.py:42-63,241-242). Blocks are block_stride floats apart in all three arrays (one rank's
+ * payload each). Replaces shipping 70 window floats per transition in the gather: the deque only
+ * shifts, so a window is the last 5 rows of its episode. */
+int uavhip_windows_from_rows(const float* first, const float* rows, const float* done, int32_t done_stride,
+                             int64_t block_stride, int32_t blocks, int32_t T, int32_t E, float* out,
+                             uavhip_stream_t stream);
+
 /* ---------------------------------------------------------------- policy forward (K4) */
 
 /* Packed fp32 weights of TransformerActorCritic (transformer_net.py:67-144), produced by

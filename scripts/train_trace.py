@@ -55,3 +55,25 @@ for k in slots:
     m4 = int(np.median(rel[:, 1, k])) if (t[:, 1, k] != 0).all() else -1
     print(f"{k:3d} {NAMES[k]:16s} {m0:8d} {m4:8d}  +{m0 - prev:6d}")
     prev = m0
+
+# the training forward (k_policy_forward<TR>) of the same steps: stamps of policy_trace.py's slots
+fwd = _lib.LIB.uavhip_policy_trace
+fwd.restype = ctypes.c_int
+fwd.argtypes = [ctypes.c_void_p, ctypes.c_int]
+buf = np.zeros(256 * 2 * 64, np.uint64)
+assert fwd(buf.ctypes.data, buf.size) == 0
+t = buf.reshape(256, 2, 64).astype(np.int64)[:min(256, bs // 16)]
+FN = {0: "start", 1: "x+mask", 2: "a.embed", 3: "a.layer+sync", 4: "a.head", 5: "c.layers+sync", 6: "c.head"}
+FL = ["start", "c0 gemm", "c0 sync", "c0 attn+sync", "c1 gemm", "c1 sync", "c1 attn+sync", "outproj", "sync",
+      "LN1+sync", "FFN1", "sync", "FFN2+sync", "store+sync", "LN2"]
+for li, tag in enumerate(["A", "C0", "C1"]):
+    for j, nm in enumerate(FL):
+        FN[8 + 16 * li + j] = f"{tag}.{nm}"
+slots = sorted(k for k in FN if (t[:, 0, k] != 0).all())
+rel = t - t[:, :, 0:1]
+print("training forward:")
+prev = 0
+for k in slots:
+    m0 = int(np.median(rel[:, 0, k]))
+    print(f"{k:3d} {FN[k]:16s} {m0:8d}  +{m0 - prev:6d}")
+    prev = m0

@@ -111,9 +111,52 @@ __global__ __launch_bounds__(kRedBlock) void k_adv_normalize(float* __restrict__
         adv[i] = (adv[i] - mean) / den;
 }
 
+// Trajectory windows from the compact all-gather format (uavhip/dist.py): thread per (block,
+// step, env, window slot), 14 floats each. Slot s of step t holds the row pushed at step
+// k = t - 4 + s if no episode ended in [k, t - 1] (else zeros, as after UAVEnv.reset); rows of
+// steps k <= 0 come from the block's first window W(0).
+__global__ __launch_bounds__(256) void k_windows_from_rows(const float* __restrict__ first,
+                                                           const float* __restrict__ rows,
+                                                           const float* __restrict__ done, int dstride,
+                                                           long long bstride, int T, int E, float* __restrict__ out,
+                                                           long long total) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total) return;
+    const int s = (int)(i % 5);
+    long long r = i / 5;
+    const int e = (int)(r % E);
+    r /= E;
+    const int t = (int)(r % T);
+    const long long b = r / T;
+    const int k = t - (4 - s);
+    const float* dn = done + b * bstride;
+    bool ok = true;
+    for (int m = k > 0 ? k : 0; m < t; ++m) ok = ok && dn[((long long)m * E + e) * dstride] == 0.f;
+    const float* src = k >= 1 ? rows + b * bstride + ((long long)k * E + e) * 14
+                              : first + b * bstride + (long long)e * 70 + (k + 4) * 14;  // W(0) = first
+    float2* dst = reinterpret_cast<float2*>(out + i * 14);
+#pragma unroll
+    for (int q = 0; q < 7; ++q) dst[q] = ok ? reinterpret_cast<const float2*>(src)[q] : make_float2(0.f, 0.f);
+}
+
 }  // namespace uavhip
 
 using namespace uavhip;
+
+extern "C" int uavhip_windows_from_rows(const float* first, const float* rows, const float* done, int32_t done_stride,
+                                        int64_t block_stride, int32_t blocks, int32_t T, int32_t E, float* out,
+                                        uavhip_stream_t stream) {
+    if (!first || !rows || !done || !out || done_stride <= 0 || blocks <= 0 || T <= 0 || E <= 0 ||
+        (block_stride & 1) || (((uintptr_t)first | (uintptr_t)rows | (uintptr_t)out) & 7)) {
+        set_error("uavhip_windows_from_rows: bad args (blocks=%d T=%d E=%d stride=%lld; 8-byte aligned buffers)",
+                  blocks, T, E, (long long)block_stride);
+        return UAVHIP_EINVAL;
+    }
+    const long long total = (long long)blocks * T * E * 5;
+    hipLaunchKernelGGL(k_windows_from_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       first, rows, done, (int)done_stride, (long long)block_stride, (int)T, (int)E, out, total);
+    return check_launch("k_windows_from_rows");
+}
 
 extern "C" int32_t uavhip_gae_partials(int32_t T, int32_t E) {
     (void)T;

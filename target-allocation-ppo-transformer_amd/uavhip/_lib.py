@@ -74,6 +74,7 @@ _SIGS = {
     "uavhip_gae_partials": (_i32, [_i32, _i32]),
     "uavhip_adv_partials": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _i32, _vp]),
     "uavhip_adv_normalize": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _i32, ctypes.c_int64, _vp, _vp]),
+    "uavhip_windows_from_rows": (ctypes.c_int, [_vp, _vp, _vp, _i32, ctypes.c_int64, _i32, _i32, _i32, _vp, _vp]),
     "uavhip_policy_layout": (_i32, [ctypes.POINTER(_i32), _i32]),
     "uavhip_policy_tiling": (_i32, [ctypes.POINTER(_i32), _i32]),
     "uavhip_policy_pack": (ctypes.c_int, [_vp, _vp, _vp]),

@@ -7,8 +7,13 @@ iteration -- an all-gather of the trajectory records over RCCL (backend "nccl" o
 import torch
 import torch.distributed as dist
 
-# per-transition record: 70 window floats + action, logp, value, return, advantage, reward, done
-RECORD_FLOATS = 70 + 7
+# Compact exchange format (one flat fp32 payload per rank): the row each step pushes into the
+# observation window ([T][E][14], = window slot 4), the per-transition scalars ([T][E][6]: action,
+# logp, value, return, advantage, done) and the window at step 0 ([E][70]). A window is the last 5
+# rows of its episode (zeros before the episode's first step), so the receivers rebuild all T
+# windows on the GPU (uavhip_windows_from_rows): 20 floats per transition instead of 76.
+ROW_FLOATS = 14
+SCALARS = ("actions", "logp", "values", "returns", "advantages", "dones")
 
 
 def shard(total, world, rank):
@@ -18,23 +23,46 @@ def shard(total, world, rank):
     return start, base + (1 if rank < extra else 0)
 
 
-def pack_trajectory(obs, actions, logp, values, returns, advantages, rewards, dones):
-    """[T, E, ...] buffers -> one fp32 [T*E, RECORD_FLOATS] payload (single collective)."""
+def compact_floats(T, E):
+    """Floats of one rank's payload."""
+    return T * E * (ROW_FLOATS + len(SCALARS)) + E * 70
+
+
+def pack_compact(obs, actions, logp, values, returns, advantages, dones):
+    """obs [>=T, E, 5, 14] policy inputs and [T, E] per-step tensors -> flat fp32 payload."""
     T, E = actions.shape[:2]
-    n = T * E
-    return torch.cat([obs.reshape(n, -1).float(), actions.reshape(n, 1).float(), logp.reshape(n, 1).float(),
-                      values.reshape(n, 1).float(), returns.reshape(n, 1).float(), advantages.reshape(n, 1).float(),
-                      rewards.reshape(n, 1).float(), dones.reshape(n, 1).float()], dim=1).contiguous()
+    rows = obs[:T, :, 4, :].reshape(-1)
+    scal = torch.stack([actions.float(), logp.float(), values.float(), returns.float(), advantages.float(),
+                        dones.float()], dim=-1).reshape(-1)
+    return torch.cat([rows.float(), scal, obs[0].reshape(-1).float()]).contiguous()
 
 
-def unpack_trajectory(payload):
-    o = payload
-    return dict(obs=o[:, :70].reshape(-1, 5, 14), actions=o[:, 70].long(), logp=o[:, 71], values=o[:, 72],
-                returns=o[:, 73], advantages=o[:, 74], rewards=o[:, 75], dones=o[:, 76])
+def unpack_compact(payloads, T, E):
+    """[world, compact_floats] gathered payloads -> dict of [world * T * E, ...] tensors in (rank,
+    step, env) order; obs rebuilt on the GPU (uavhip_windows_from_rows; the HIP library is
+    required -- there is no host fallback)."""
+    from ._lib import LIB, check, ptr, stream_handle
+    world = payloads.shape[0]
+    F = compact_floats(T, E)
+    if payloads.shape[1] != F or payloads.dtype != torch.float32 or not payloads.is_contiguous():
+        raise ValueError("payloads must be a contiguous fp32 [world, compact_floats(T, E)] tensor")
+    nr = T * E * ROW_FLOATS
+    ns = T * E * len(SCALARS)
+    scal = payloads[:, nr:nr + ns].reshape(world * T * E, len(SCALARS))
+    obs = torch.empty(world * T * E, 5, 14, dtype=torch.float32, device=payloads.device)
+    base = payloads.data_ptr()
+    check(LIB.uavhip_windows_from_rows(base + 4 * (nr + ns), base, base + 4 * (nr + len(SCALARS) - 1),
+                                       len(SCALARS), F, world, T, E, ptr(obs), stream_handle()),
+          "uavhip_windows_from_rows")
+    out = {k: scal[:, i] for i, k in enumerate(SCALARS)}
+    out["actions"] = out["actions"].to(torch.int8)
+    out["obs"] = obs
+    return out
 
 
 def all_gather_rows(payload, group=None):
-    """Concatenate every rank's [rows, F] payload in rank order (equal rows per rank)."""
+    """Concatenate every rank's [rows, F] payload in rank order (equal rows per rank); one
+    all_gather_into_tensor over RCCL."""
     world = dist.get_world_size(group)
     if world == 1:
         return payload

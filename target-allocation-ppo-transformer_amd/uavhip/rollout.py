@@ -41,8 +41,13 @@ class Trajectory:
 
 
 class RolloutEngine:
-    def __init__(self, env, policy, horizon, want_info=True, bootstrap=True, seed=0):
+    def __init__(self, env, policy, horizon, want_info=True, bootstrap=True, seed=0, normalize=True):
+        """normalize=False leaves the advantages raw after GAE: a data-parallel caller normalises
+        them with the moments of the whole gathered batch in gather() (ppo.py:94)."""
         self.env = env
+        self.normalize = normalize
+        self.iteration = 0
+        self._gathered = (-1, None)  # (iteration, batch) of the last gather()
         self.policy = policy
         self.T = int(horizon)
         self.bootstrap = bootstrap
@@ -86,7 +91,8 @@ class RolloutEngine:
         if self.bootstrap:
             self._forward(self.T, tr.obs[self.T], tr.last_actions, tr.last_logp, tr.last_values)
             last = tr.last_values
-        gae(tr.rewards, tr.dones, tr.values, last_values=last, out=(tr.ret, tr.adv, tr.partials, tr.stats))
+        gae(tr.rewards, tr.dones, tr.values, last_values=last, normalize=self.normalize,
+            out=(tr.ret, tr.adv, tr.partials, tr.stats))
         env.refresh_scenes()  # regenerate spare scenes consumed by full resets (off the step path)
         self.counter.add_((self.T + 1) * env.E)
 
@@ -95,6 +101,7 @@ class RolloutEngine:
         """One rollout iteration: a graph replay when captured (unless eager=True), else eager
         launches (which also record the HIP events, if enabled). Both advance the same device state."""
         self.policy.packed_weights()  # repack in place if the weights changed (e.g. after an update)
+        self.iteration += 1
         if self.graph is not None and not eager:
             self.graph.replay()
         else:
@@ -137,10 +144,20 @@ class RolloutEngine:
         return g
 
     def gather(self, group=None):
-        """All-gather the per-rank trajectories over RCCL as one flat fp32 payload per rank
-        (uavhip.dist.pack_trajectory); returns the [world * T * E, RECORD_FLOATS] batch."""
-        from .dist import all_gather_rows, pack_trajectory
+        """The data-parallel exchange of one iteration: a 3-double all-reduce of the
+        advantage moments and normalisation with them (when the engine left the advantages raw),
+        then ONE all-gather over RCCL of every rank's compact payload (uavhip.dist.pack_compact:
+        20 floats per transition) and the GPU rebuild of the windows. Returns the gathered batch
+        as a dict of [world * T * E, ...] tensors (obs, actions, logp, values, returns, advantages,
+        dones) in (rank, step, env) order."""
+        from .dist import all_gather_rows, global_moments, normalize_global, pack_compact, unpack_compact
+        if self._gathered[0] == self.iteration:  # once per iteration (normalises in place)
+            return self._gathered[1]
         tr = self.traj
-        payload = pack_trajectory(tr.obs[:tr.T], tr.actions, tr.logp, tr.values, tr.ret, tr.adv, tr.rewards,
-                                  tr.dones)
-        return all_gather_rows(payload, group)
+        if not self.normalize:
+            normalize_global(tr.adv, global_moments(tr.partials, tr.adv.numel(), group))
+        payload = pack_compact(tr.obs, tr.actions, tr.logp, tr.values, tr.ret, tr.adv, tr.dones)
+        gathered = all_gather_rows(payload.view(1, -1), group)
+        batch = unpack_compact(gathered, tr.T, tr.E)
+        self._gathered = (self.iteration, batch)
+        return batch

@@ -1,6 +1,8 @@
 """Multi-process (world_size 2 and 3, gloo on CPU) checks of the data-parallel plumbing in
-uavhip.dist: env sharding, the single trajectory all-gather (rank order, record layout) and the
-global advantage moments all-reduce. The RCCL path runs the same functions with backend "nccl"."""
+uavhip.dist: env sharding, the single trajectory all-gather of the compact format (rank order,
+record layout; every rank's windows rebuilt exactly from its rows / done flags / first windows by
+the oracle's deque restatement) and the global advantage moments all-reduce. The RCCL path runs
+the same functions with backend "nccl"; the GPU rebuild kernel is checked in test_gpu_policy_gae."""
 import os
 import socket
 
@@ -18,6 +20,25 @@ def _free_port():
     return p
 
 
+def _deque_windows(T, E, g):
+    """Windows as UAVEnv's deque produces them (zeros after a reset, shift + append per step),
+    T + 1 steps (the rollout buffer keeps the next window), with random rows and done flags."""
+    dones = (torch.rand(T, E, generator=g) < 0.25).to(torch.uint8)
+    obs = torch.zeros(T + 1, E, 5, 14)
+    w = torch.randn(E, 5, 14, generator=g)
+    w[: E // 2, :2] = 0  # some envs mid-way through their first 5 steps
+    for t in range(T + 1):
+        if t > 0:
+            nxt = torch.zeros_like(w)
+            for e in range(E):
+                if not dones[t - 1, e]:
+                    nxt[e, :4] = w[e, 1:]
+            nxt[:, 4] = torch.randn(E, 14, generator=g)
+            w = nxt
+        obs[t] = w
+    return obs, dones
+
+
 def _worker(rank, world, port, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -30,26 +51,18 @@ def _worker(rank, world, port, q):
     try:
         T, E_total = 6, 10
         start, cnt = udist.shard(E_total, world, rank)
+        E = (E_total + world - 1) // world  # equal payloads per rank (the last shard padded)
         g = torch.Generator().manual_seed(1000 + rank)
-        obs = torch.randn(T, cnt, 5, 14, generator=g)
-        actions = torch.randint(0, 2, (T, cnt), generator=g, dtype=torch.int8)
-        f = [torch.randn(T, cnt, generator=g) for _ in range(4)]
-        rewards = torch.rand(T, cnt, generator=g, dtype=torch.float64)
-        dones = (torch.rand(T, cnt, generator=g) < 0.2).to(torch.uint8)
-        payload = udist.pack_trajectory(obs, actions, f[0], f[1], f[2], f[3], rewards, dones)
-        # equal-size payloads per rank (pad the smaller shard's rows for the collective)
-        rows = T * ((E_total + world - 1) // world)
-        padded = torch.zeros(rows, payload.shape[1])
-        padded[:payload.shape[0]] = payload
-        out = udist.all_gather_rows(padded)
-        rec = udist.unpack_trajectory(payload)
-        ok_roundtrip = (torch.equal(rec["obs"], obs.reshape(-1, 5, 14)) and
-                        torch.equal(rec["actions"], actions.reshape(-1).long()) and
-                        torch.equal(rec["advantages"], f[3].reshape(-1)))
-        adv = f[3].reshape(-1).double()
+        obs, dones = _deque_windows(T, E, g)
+        actions = torch.randint(0, 2, (T, E), generator=g, dtype=torch.int8)
+        f = [torch.randn(T, E, generator=g) for _ in range(4)]
+        payload = udist.pack_compact(obs, actions, f[0], f[1], f[2], f[3], dones)
+        assert payload.numel() == udist.compact_floats(T, E)
+        out = udist.all_gather_rows(payload.view(1, -1))
+        adv = f[3][:, :cnt].reshape(-1).double()
         partials = torch.stack([adv.sum(), (adv * adv).sum()])
         mom = udist.global_moments(partials, adv.numel())
-        q.put((rank, start, cnt, out.numpy(), payload.numpy(), ok_roundtrip, mom.numpy(), adv.numpy()))
+        q.put((rank, start, cnt, out.numpy(), payload.numpy(), obs.numpy(), dones.numpy(), mom.numpy(), adv.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -70,16 +83,26 @@ def test_gloo_gather_and_moments(world):
     starts = [r[1] for r in res]; cnts = [r[2] for r in res]
     assert starts[0] == 0 and all(starts[i] + cnts[i] == starts[i + 1] for i in range(world - 1))
     assert sum(cnts) == 10
-    rows = res[0][3].shape[0] // world
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle.windows import windows_from_rows
+    T, E = 6, res[0][5].shape[1]
     for r in res:
-        assert r[5]
+        gathered = r[3]
+        assert gathered.shape == (world, res[0][4].size)
         for k in range(world):   # every rank sees every rank's payload at slot k
-            pay = res[k][4]
-            np.testing.assert_array_equal(r[3][k * rows:k * rows + pay.shape[0]], pay)
+            np.testing.assert_array_equal(gathered[k], res[k][4])
+            # the compact record rebuilds rank k's windows exactly (deque semantics)
+            nr, ns = T * E * 14, T * E * 6
+            rows = gathered[k][:nr].reshape(T, E, 14)
+            scal = gathered[k][nr:nr + ns].reshape(T, E, 6)
+            first = gathered[k][nr + ns:].reshape(E, 5, 14)
+            np.testing.assert_array_equal(windows_from_rows(first, rows, scal[..., 5]), res[k][5][:T])
+            np.testing.assert_array_equal(scal[..., 5], res[k][6])
     # global moments equal the moments of the union of all ranks' advantages
-    allv = np.concatenate([r[7] for r in res])
+    allv = np.concatenate([r[8] for r in res])
     for r in res:
-        np.testing.assert_allclose(r[6], [allv.sum(), (allv * allv).sum(), allv.size], rtol=1e-12)
+        np.testing.assert_allclose(r[7], [allv.sum(), (allv * allv).sum(), allv.size], rtol=1e-12)
 
 
 def test_shard_covers_all():

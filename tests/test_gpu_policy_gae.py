@@ -206,6 +206,47 @@ def test_rollout_engine_invariants():
     assert int(env.errors().max()) == 0
 
 
+def test_compact_exchange_rebuilds_rollout_windows():
+    """The data-parallel exchange format (uavhip/dist.py): a real rollout's windows come back
+    bit-exactly from the rows / done flags / first windows (uavhip_windows_from_rows), for several
+    iterations (windows carried across the iteration boundary) and several payload blocks, and the
+    GPU rebuild equals the oracle's step-by-step deque restatement on random inputs."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle.windows import windows_from_rows
+    from uavhip import dist as udist
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.rollout import RolloutEngine
+    from uavhip.vec_env import VecUAVEnv
+    torch.manual_seed(0)
+    E, T = 192, 24
+    env = VecUAVEnv(E, 4, 6, 1, 1, seed=9)  # short episodes: many boundaries inside a window
+    eng = RolloutEngine(env, TransformerActorCritic().cuda(), T, seed=3)
+    eng.start()
+    pays, wins = [], []
+    for _ in range(3):
+        tr = eng.collect()
+        assert tr.dones.any()
+        pays.append(udist.pack_compact(tr.obs, tr.actions, tr.logp, tr.values, tr.ret, tr.adv, tr.dones))
+        wins.append(tr.obs[:T].clone())
+    got = udist.unpack_compact(torch.stack(pays), T, E)
+    torch.cuda.synchronize()
+    assert torch.equal(got["obs"], torch.cat(wins).reshape(-1, 5, 14))
+    assert torch.equal(got["dones"].reshape(3, T, E).to(torch.uint8).cpu(), torch.stack(
+        [udist_p[T * E * 14:T * E * 20].reshape(T, E, 6)[..., 5].cpu().to(torch.uint8) for udist_p in pays]))
+    # random inputs against the oracle (zero rows included)
+    g = torch.Generator().manual_seed(4)
+    first = torch.randn(2, E, 5, 14, generator=g)
+    rows = torch.randn(2, T, E, 14, generator=g)
+    dn = (torch.rand(2, T, E, generator=g) < 0.3)
+    pay = torch.stack([torch.cat([rows[b].reshape(-1), torch.stack([torch.zeros(T, E)] * 5 + [dn[b].float()], -1)
+                                  .reshape(-1), first[b].reshape(-1)]) for b in range(2)]).cuda()
+    got = udist.unpack_compact(pay, T, E)["obs"].reshape(2, T, E, 5, 14).cpu().numpy()
+    for b in range(2):
+        np.testing.assert_array_equal(got[b], windows_from_rows(first[b].numpy(), rows[b].numpy(), dn[b].numpy()))
+
+
 def test_rollout_graph_replay_matches_eager():
     """The captured hipGraph iteration reproduces eager launches bit for bit (same device state,
     same sampling counters), across several replays and a weight change in between."""

@@ -50,7 +50,7 @@ def _grad_scale_check(name, got, ref, rtol):
     assert err <= rtol * scale + 1e-7, f"{name}: max|d| {err:.3e} vs scale {scale:.3e}"
 
 
-@pytest.mark.parametrize("Bm", [64, 256])
+@pytest.mark.parametrize("Bm", [64, 256, 4096])
 def test_fused_gradients_match_autograd(Bm):
     from uavhip.policy import TransformerActorCritic, layout
     from uavhip.train import FusedPPOTrainer
