@@ -62,11 +62,13 @@ __global__ __launch_bounds__(kBlock) void k_env_step(uavhip_env env, const int8_
                                                      double* __restrict__ reward_out, uint8_t* __restrict__ done_out,
                                                      double* __restrict__ info_out) {
     extern __shared__ double s_tab[];
+    __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock * 16];
     const int lane = lane_id();
     const int e = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (e >= env.E) return;
     EnvRegs<TPL> R;
     R.tab = s_tab + (threadIdx.x >> 6) * env.N * env.M;
+    R.row = s_row + (threadIdx.x >> 6) * 16;
     load_regs(R, env, e, lane);
     if (LT) load_table(R, env, lane);
     const long long E = env.E;
@@ -96,7 +98,9 @@ __global__ __launch_bounds__(kBlock) void k_env_reset(uavhip_env env, const uint
     const int e = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (e >= env.E) return;
     if (mask && !mask[e]) return;
+    __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock * 16];
     EnvRegs<TPL> R;
+    R.row = s_row + (threadIdx.x >> 6) * 16;
     load_scene_index(env, e, R.sel, R.stale, R.gen, R.sb);
     const int* is = env.istate + (long long)e * UAVHIP_IST_COUNT;
     R.ep = episode >= 0 ? episode : is[UAVHIP_IST_EPISODE];

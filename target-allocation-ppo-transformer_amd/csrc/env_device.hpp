@@ -171,6 +171,8 @@ struct EnvRegs {
     float w0, w1;
     // multi-step launches (LT = true): this wave's LDS copy of the active scene's p_dmg table
     double* tab;
+    // the wave's 16-float LDS scratch: the new observation row on its way to its lanes
+    float* row;
     // loop-invariant divisors and their correctly rounded reciprocals (div_by)
     double den_c, rcp_c, den_v, rcp_v, rcp_m;
     double rcp_n;  // lane l: RN(1 / (l + 1)), the info averages' divisors 1..64
@@ -229,13 +231,6 @@ __device__ void load_scene_regs(EnvRegs<TPL>& R, const uavhip_env& env, int lane
     drain_loads();
 }
 
-__device__ __forceinline__ float sel14(const float (&f)[kDim], int j) {
-    float v = 0.0f;
-#pragma unroll
-    for (int i = 0; i < kDim; ++i) v = (j == i) ? f[i] : v;
-    return v;
-}
-
 // mechanics.py:185-241 get_state_vector + uav_env.py:194-237 (_get_obs context) for the current
 // pointer; pushes the row into the window (uav_env.py:241-242).
 template <int TPL>
@@ -260,19 +255,29 @@ __device__ void push_obs(EnvRegs<TPL>& R, int lane) {
     const double d_pkm = p_pure - p_km;
     const double d_pm = hat_pp - hat_p;
     const double d_G = (hat_pp * val) - hat_G;
-    float f[kDim] = {(float)ucost / 2.0f, (float)val / 16.0f, (float)chi_c, (float)chi_v, (float)chi_mc,
-                     (float)p_km, (float)pjp, (float)hat_p, (float)prev_rev / 16.0f, (float)hat_G / 16.0f,
-                     (float)d_pkm, (float)d_pm, (float)d_G / 16.0f, 1.0f};
+    // the new row goes through the wave's LDS scratch (lane 0 writes, lanes 56..63 and 0..5 read
+    // their element): 6 LDS instructions instead of two 14-way VALU select chains. LDS operations
+    // of one wave complete in order, so the reads see the write.
+    if (lane == 0) {
+        typedef float f32x4 __attribute__((ext_vector_type(4)));
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<f32x4*>(R.row) = f32x4{(float)ucost / 2.0f, (float)val / 16.0f, (float)chi_c, (float)chi_v};
+        *reinterpret_cast<f32x4*>(R.row + 4) = f32x4{(float)chi_mc, (float)p_km, (float)pjp, (float)hat_p};
+        *reinterpret_cast<f32x4*>(R.row + 8) =
+            f32x4{(float)prev_rev / 16.0f, (float)hat_G / 16.0f, (float)d_pkm, (float)d_pm};
+        *reinterpret_cast<f32x2*>(R.row + 12) = f32x2{(float)d_G / 16.0f, 1.0f};
+    }
     // shift the deque by one row (14 floats) and append
     const float a = __shfl(R.w0, (lane + kDim) & 63);
     const float b = __shfl(R.w1, (lane + kDim - kWave) & 63);
+    const float r0 = R.row[(lane - (kObs - kDim)) & 15];           // new row, elements 56..63
+    const float r1 = R.row[(lane + kWave - (kObs - kDim)) & 15];   // new row, elements 64..69 (lane < 6)
     float nw0;
     if (lane < kWave - kDim) nw0 = a;             // elements 14..63 -> 0..49
     else if (lane < kObs - kDim) nw0 = b;         // elements 64..69 -> 50..55
-    else nw0 = sel14(f, lane - (kObs - kDim));    // new row, elements 56..63
-    const float nw1 = sel14(f, lane + kWave - (kObs - kDim));  // new row, elements 64..69 (lane < 6)
+    else nw0 = r0;
     R.w0 = nw0;
-    R.w1 = lane < kObs - kWave ? nw1 : 0.0f;
+    R.w1 = lane < kObs - kWave ? r1 : 0.0f;
 }
 
 // Pair probabilities of the current pointer (u, t). LT: p_dmg from the wave's LDS table (a short
@@ -441,20 +446,21 @@ __device__ __forceinline__ void write_obs(float* o, float w0, float w1, int lane
 // differ from it only by summation order (<= a few ulp, checked to 1e-12 against the reference).
 template <int TPL>
 __device__ void write_info(const EnvRegs<TPL>& R, const uavhip_env& env, double is_valid, double* o, int lane) {
+    static_assert(UAVHIP_INFO_COUNT == 8 && UAVHIP_INFO_J == 0 && UAVHIP_INFO_NUM_ASSIGNED == 1 &&
+                  UAVHIP_INFO_IS_VALID == 2 && UAVHIP_INFO_AVG_P_DMG == 3 && UAVHIP_INFO_AVG_P_FINAL == 4 &&
+                  UAVHIP_INFO_UAV_IDX == 5 && UAVHIP_INFO_TARGET_IDX == 6 && UAVHIP_INFO_EPISODE == 7,
+                  "info record layout");
     const int cnt = R.nasg;
     const double y = cnt > 0 ? readlane_d(R.rcp_n, cnt - 1) : 0.0;
     const double avg_d = cnt > 0 ? div_by(R.sum_pd, (double)cnt, y) : 0.0;
     const double avg_f = cnt > 0 ? div_by(R.sum_pf, (double)cnt, y) : 0.0;
-    double v = 0.0;
-    v = lane == UAVHIP_INFO_J ? R.J : v;
-    v = lane == UAVHIP_INFO_NUM_ASSIGNED ? (double)R.ncov : v;
-    v = lane == UAVHIP_INFO_IS_VALID ? is_valid : v;
-    v = lane == UAVHIP_INFO_AVG_P_DMG ? avg_d : v;
-    v = lane == UAVHIP_INFO_AVG_P_FINAL ? avg_f : v;
-    v = lane == UAVHIP_INFO_UAV_IDX ? (double)R.u : v;
-    v = lane == UAVHIP_INFO_TARGET_IDX ? (double)R.t : v;
-    v = lane == UAVHIP_INFO_EPISODE ? (double)R.ep : v;
-    if (lane < UAVHIP_INFO_COUNT) o[lane] = v;
+    if (lane == 0) {  // the 64-byte record from one lane: 4 stores, no per-lane selection
+        double2* q = reinterpret_cast<double2*>(o);
+        q[0] = make_double2(R.J, (double)R.ncov);
+        q[1] = make_double2(is_valid, avg_d);
+        q[2] = make_double2(avg_f, (double)R.u);
+        q[3] = make_double2((double)R.t, (double)R.ep);
+    }
 }
 
 // One UAVEnv.step (uav_env.py:295-435) on register state. No scene generation on this path: a

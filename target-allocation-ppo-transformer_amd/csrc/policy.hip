@@ -596,22 +596,44 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     PTR(0);
     // windows -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch tail zero-filled);
     // training mode gathers minibatch row idx[b] of the trajectory buffer
-    for (int i = threadIdx.x; i < TOK * LDX; i += NTHR) {
-        const int t = i / LDX, k = i - t * LDX, s = t / SPW, p = t - s * SPW;
-        const size_t src = TR ? (size_t)io.idx[b0 + p] : (size_t)(b0 + p);
-        const float v = (k < IN && b0 + p < B) ? states[(src * S + s) * IN + k] : 0.f;
-        sm.x[i] = v;
-        if (TR) io.xg[(size_t)trow(t, b0) * 16 + k] = v;
-    }
-    if (TR && threadIdx.x < SPW) {  // per-sample loss inputs
-        const int b = b0 + threadIdx.x;
-        const size_t src = (size_t)io.idx[b];
-        float* o = io.smp + (size_t)b * 8;
-        o[0] = (float)(io.act_in[src] != 0);
-        o[1] = io.oldlp_in[src];
-        o[2] = io.oldv_in[src];
-        o[3] = io.ret_in[src];
-        o[4] = io.adv_in[src];
+    {   // <= 3 elements per thread, every load of a round issued before any is used: the
+        // training gather is two dependent rounds (row index, then window / loss inputs)
+        constexpr int kEl = (TOK * LDX + NTHR - 1) / NTHR;
+        size_t src[kEl];
+#pragma unroll
+        for (int u = 0; u < kEl; ++u) {
+            const int i = threadIdx.x + u * NTHR, p = (i / LDX) % SPW;
+            src[u] = (size_t)(b0 + p);
+            if (TR && i < TOK * LDX) src[u] = (size_t)io.idx[b0 + p];
+        }
+        size_t ssrc = 0;
+        if (TR && threadIdx.x < SPW) ssrc = (size_t)io.idx[b0 + threadIdx.x];
+        float v[kEl];
+#pragma unroll
+        for (int u = 0; u < kEl; ++u) {
+            const int i = threadIdx.x + u * NTHR;
+            const int t = i / LDX, k = i - t * LDX, s = t / SPW, p = t - s * SPW;
+            v[u] = (i < TOK * LDX && k < IN && b0 + p < B) ? states[(src[u] * S + s) * IN + k] : 0.f;
+        }
+        float ld[5];
+        if (TR && threadIdx.x < SPW) {  // per-sample loss inputs
+            ld[0] = (float)(io.act_in[ssrc] != 0);
+            ld[1] = io.oldlp_in[ssrc];
+            ld[2] = io.oldv_in[ssrc];
+            ld[3] = io.ret_in[ssrc];
+            ld[4] = io.adv_in[ssrc];
+        }
+#pragma unroll
+        for (int u = 0; u < kEl; ++u) {
+            const int i = threadIdx.x + u * NTHR;
+            if (i >= TOK * LDX) continue;
+            sm.x[i] = v[u];
+            if (TR) io.xg[(size_t)trow(i / LDX, b0) * 16 + (i % LDX)] = v[u];
+        }
+        if (TR && threadIdx.x < SPW) {
+            float* o = io.smp + (size_t)(b0 + threadIdx.x) * 8;
+            for (int c = 0; c < 5; ++c) o[c] = ld[c];
+        }
     }
     __syncthreads();
     if (threadIdx.x < SPW * S) {  // key padding mask: all-zero rows, last row never masked
