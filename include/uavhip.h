@@ -36,6 +36,8 @@ typedef void* uavhip_stream_t; /* hipStream_t */
 #define UAVHIP_MAX_N 64     /* UAVs per env (one wave lane each)          */
 #define UAVHIP_MAX_M 128    /* targets per env (<= 2 per wave lane)       */
 #define UAVHIP_MAX_OBSTACLES 8
+/* uavhip_env.flags */
+#define UAVHIP_ENV_ONE_PER_WAVE 1  /* multi-step launches: never pack two envs into one wave */
 
 enum uavhip_status {
     UAVHIP_OK = 0,
@@ -126,7 +128,7 @@ typedef struct uavhip_env {
     int32_t scene_buffers;     /* 1, or 2 = every scene array and pair table below is
                                   [2][E]...: buffer istate[SCENE_SEL] is active, the other a
                                   pre-generated spare a full reset flips to                  */
-    int32_t pad_;
+    int32_t flags;              /* UAVHIP_ENV_* bits (0 = defaults)                    */
     uint64_t seed;             /* Philox key for on-device scene generation                 */
     double prm[UAVHIP_PRM_COUNT];
     double gen[UAVHIP_GEN_COUNT];

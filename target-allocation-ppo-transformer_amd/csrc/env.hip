@@ -9,6 +9,7 @@
 //    rollout call, T > 1 the env-only multi-step launch (BASELINE config 2). It never generates a
 //    scene itself (register budget: 4 waves / SIMD); full resets flip to the spare buffer.
 #include "env_device.hpp"
+#include "env_group.hpp"
 
 #pragma clang fp contract(off)
 
@@ -88,7 +89,41 @@ __global__ __launch_bounds__(kBlock) void k_env_step(uavhip_env env, const int8_
     }
     store_regs(R, env, e, lane);
 }
+// Two envs per wave (env_group.hpp) for multi-step launches with N, M <= 32 and E even: the same
+// step, half the VALU instructions per env-step (the wave-uniform fp64 work serves two envs).
+__global__ __launch_bounds__(kBlock) void k_env_step_g(uavhip_env env, const int8_t* __restrict__ actions, int T,
+                                                       int auto_reset, float* __restrict__ obs_out,
+                                                       double* __restrict__ reward_out, uint8_t* __restrict__ done_out,
+                                                       double* __restrict__ info_out) {
+    extern __shared__ double s_tab[];  // [wave][group][N * M]
+    __shared__ __attribute__((aligned(16))) float s_win[kWavesPerBlock * 2 * envgrp::kWin];
+    const int lane = lane_id(), j = lane & 31, wv = threadIdx.x >> 6;
+    const int slot = wv * 2 + (lane >> 5);
+    const int e = blockIdx.x * kWavesPerBlock * 2 + slot;
+    if (e >= env.E) return;  // E is even: both groups of a wave leave together
+    envgrp::GRegs R;
+    R.tab = s_tab + slot * env.N * env.M;
+    R.win = s_win + slot * envgrp::kWin;
+    envgrp::gload_regs(R, env, e, j);
+    envgrp::gload_table(R, env, j);
+    const long long E = env.E;
+    for (int s0 = 0; s0 < T; s0 += envgrp::L) {
+        const int na = min(envgrp::L, T - s0);
+        // this env's action == 1 bits of the next 32 steps
+        const int av = j < na ? actions[(long long)(s0 + j) * E + e] : 0;
+        const unsigned abits = envgrp::gbits(ballot(av == 1));
+        for (int i = 0; i < na; ++i) {
+            const long long se = (long long)(s0 + i) * E + e;
+            envgrp::gstep(R, env, e, j, (int)((abits >> i) & 1u), auto_reset,
+                          obs_out ? obs_out + se * kObs : nullptr, reward_out ? reward_out + se : nullptr,
+                          done_out ? done_out + se : nullptr, info_out ? info_out + se * UAVHIP_INFO_COUNT : nullptr);
+        }
+    }
+    envgrp::gstore_regs(R, env, e, j);
+}
+
 constexpr int kTableMinSteps = 4;                // below this the LDS table costs more than it saves
+constexpr int kGroupMinEnvs = 4096;
 constexpr size_t kTableMaxBytes = 64 * 1024;     // per workgroup (4 envs)
 
 template <int TPL>
@@ -246,6 +281,15 @@ extern "C" int uavhip_env_step(const uavhip_env* env, const int8_t* actions, int
     const bool lt = T >= kTableMinSteps && tab <= kTableMaxBytes;
     const dim3 grid(wave_grid(env->E)), block(kBlock);
     hipStream_t st = (hipStream_t)stream;
+    // two envs per wave pays once there are >= 2 such waves per SIMD (E >= 4096 on 1024 SIMDs);
+    // below that the launch is latency-bound and one env per wave keeps more waves in flight
+    if (lt && env->N <= envgrp::L && env->M <= envgrp::L && env->E % 2 == 0 && env->E >= kGroupMinEnvs &&
+        !(env->flags & UAVHIP_ENV_ONE_PER_WAVE)) {
+        const int per_block = kWavesPerBlock * 2;
+        hipLaunchKernelGGL(k_env_step_g, dim3((env->E + per_block - 1) / per_block), block, 2 * tab, st, *env, actions,
+                           (int)T, (int)auto_reset, obs_out, reward, done, info);
+        return check_launch("k_env_step_g");
+    }
     if (env->M <= kWave) {
         if (lt) hipLaunchKernelGGL((k_env_step<1, true>), grid, block, tab, st, *env, actions, (int)T, (int)auto_reset, obs_out, reward, done, info);
         else hipLaunchKernelGGL((k_env_step<1, false>), grid, block, 0, st, *env, actions, (int)T, (int)auto_reset, obs_out, reward, done, info);

@@ -39,7 +39,7 @@ _i32 = ctypes.c_int32
 class EnvDesc(ctypes.Structure):
     """Mirror of `struct uavhip_env` (include/uavhip.h)."""
     _fields_ = [("E", _i32), ("N", _i32), ("M", _i32), ("Kn", _i32), ("Ki", _i32),
-                ("full_reset_period", _i32), ("scene_buffers", _i32), ("pad_", _i32), ("seed", ctypes.c_uint64),
+                ("full_reset_period", _i32), ("scene_buffers", _i32), ("flags", _i32), ("seed", ctypes.c_uint64),
                 ("prm", ctypes.c_double * PRM_COUNT), ("gen", ctypes.c_double * GEN_COUNT)] + \
               [(n, _vp) for n in ("uav_pos", "uav_vel", "uav_load", "uav_cost", "uav_type", "tgt_pos", "tgt_vel",
                                   "tgt_value", "tgt_id", "nfz_pos", "icp_pos", "icp_vel", "p_dmg", "p_pen",

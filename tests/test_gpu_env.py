@@ -335,3 +335,32 @@ def test_c5_stress_dims_run():
     torch.cuda.synchronize()
     assert torch.isfinite(obs).all() and torch.isfinite(r).all() and (r >= 0).all()
     assert int(v.errors().max()) == 0
+
+
+@pytest.mark.parametrize("N,M,period", [(16, 32, 3), (8, 16, 2), (4, 4, 5), (32, 32, 0)])
+def test_two_envs_per_wave_matches_one_per_wave(N, M, period):
+    """Multi-step launches pack two envs into a wave when N, M <= 32 (env_group.hpp). Against the
+    one-env-per-wave kernel (checked against the reference above) on the same scenes and actions:
+    every output and the whole carried state bitwise, over several launches with auto-reset and
+    full resets that flip to refreshed spare scenes."""
+    E, T = 4096, 40  # the grouped kernel's minimum batch
+    outs = []
+    for flags in (0, 1):
+        v = _venv(E, N, M, 1, 1, period=period, seed=21)
+        v.desc.flags = flags
+        v.istate[:, 4] = 1
+        v.generate_scenes()
+        v.reset(episode=1)
+        g = torch.Generator(device="cuda").manual_seed(7)
+        res = []
+        for _ in range(3):
+            a = (torch.rand(T, E, device="cuda", generator=g) < 0.6).to(torch.int8)
+            obs, r, d, info = v.step(a)
+            v.refresh_scenes()
+            res += [obs.clone(), r.clone(), d.clone(), info.clone()]
+        res += [v.istate.clone(), v.dstate.clone(), v.window.clone(), v.nh_final.clone(), v.nh_pure.clone(),
+                v.t_cost.clone(), v.n_lock.clone(), v.assigned.clone()]
+        assert int((v.errors() & 1).max()) == 0  # bit 2 (a second full reset before a refresh) may occur
+        outs.append(res)
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
