@@ -12,7 +12,7 @@ Also reported (same JSON line):
                 FLOP/sample (last-token-pruned forward) x E per launch / its average
                 HIP-event duration over the timed region
   env_roofline  k_env_step against HBM, algorithmic 24*M + 490 B per env-step
-  env_fused     env-only K2 with T = 64 steps per launch (state in registers): BASELINE configs[1]
+  env_fused     env-only K2 with T = 256 steps per launch (state in registers): BASELINE configs[1]
                 (1024 envs x 8 x 16) and the headline shape, env-steps/s and algorithmic GB/s
   ppo_samples_per_s  one PPO update (5 epochs) over the iteration's batch on the HIP training step
                 (uavhip_ppo_step); N > 1: over the all-gathered batch, data parallel (each rank a
@@ -291,7 +291,7 @@ def main():
 
     env_fused = None
     if rank == 0 and world == 1 and not args.no_env_fused:
-        env_fused = [env_fused_rate(1024, 8, 16, 64, dev), env_fused_rate(E, args.uavs, args.targets, 64, dev)]
+        env_fused = [env_fused_rate(1024, 8, 16, 256, dev), env_fused_rate(E, args.uavs, args.targets, 256, dev)]
 
     ppo = None
     if not args.no_ppo:
