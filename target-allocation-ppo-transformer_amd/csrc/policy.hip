@@ -446,7 +446,9 @@ __device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv
         __syncthreads();
         PTR(tb + 2 + 3 * c);
         if (TR && !kExpNoStore) {  // this chunk's Q (query tokens) / K / V -> qkv[row][part * 128 + 64 c + d]
-            for (int i = threadIdx.x; i < TOK * 48; i += NTHR) {
+            // by waves 4-7 (V tiles: less MFMA work than the K + Q waves sharing their SIMDs)
+            for (int i = (int)threadIdx.x - NTHR / 2; i < TOK * 48; i += NTHR / 2) {
+                if (i < 0) break;
                 const int tok = i / 48, r = i - tok * 48, part = r >> 4, q = r & 15;
                 if (part == 0 && tok < qtok0) continue;
                 *reinterpret_cast<f32x4*>(io.qkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q) =
@@ -648,9 +650,9 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     const float* headw_a = P + kOffs.o[kActorHead];
     const float* headw_c = P + kOffs.o[kCriticHead];
     // actor trunk (1 layer) + head
+    APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
     embed<kActorTrunk, TR>(sm, P, io.e[0], io.h0[0], b0);
     PTR(2);
-    APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
     __syncthreads();
     encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0);
     APre<4> ph;
@@ -661,8 +663,8 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     if (TR) store_hidden(sm, io.z[0], b0);  // before the critic's LayerNorm partials reuse sm.z
     PTR(4);
     // critic trunk (2 layers) + head
-    embed<kCriticTrunk, TR>(sm, P, io.e[1], io.h0[1], b0);
     pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+    embed<kCriticTrunk, TR>(sm, P, io.e[1], io.h0[1], b0);
     __syncthreads();
     encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv, io.L[1], b0);
     pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
@@ -792,9 +794,9 @@ __device__ void ln_bwd_lds(const float* src, float* dst, const float* __restrict
 //   dq_i = sum_j dS_ij k_j / 4; dk_j = sum_i dS_ij q_i / 4.
 // One (sample, head) task per 8 lanes, 2 of the 16 head dims each (all 512 threads; dot products
 // reduced over the 8 lanes with two quad permutes and a half-row mirror). dq | dk | dv ->
-// sm.big [tok][3 x 64] (the forward's chunk layout) and dqkv rows (pruned layers: dq only for the
-// token-4 query rows; the LDS copy is zero on the other rows). Per-wave sums over the wave's 2
-// samples of dq, dk, dv -> scratch [wave][192] (in_proj bias partials).
+// sm.big [tok][3 x 64] (the forward's chunk layout; pruned layers: dq zero outside the token-4
+// query rows); the caller copies them to the dqkv rows. Per-wave sums over the wave's 2 samples of
+// dq, dk, dv -> scratch [wave][192] (in_proj bias partials).
 __device__ __forceinline__ float add_hmirror8(float v) {  // + lane 7 - i within each group of 8
     return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true));
 }
@@ -804,8 +806,7 @@ __device__ __forceinline__ f32x2 ld2(const float* p) { return *reinterpret_cast<
 __device__ __forceinline__ void st2(float* p, f32x2 v) { *reinterpret_cast<f32x2*>(p) = v; }
 
 template <bool last>
-__device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, float* __restrict__ dqkv, int c, int b0,
-                               float* scratch) {
+__device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, int c, int b0, float* scratch) {
     const int o8 = threadIdx.x & 7, hh = (threadIdx.x >> 3) & 3, p = threadIdx.x >> 5;
     const int d0 = hh * HD + 2 * o8, col = 64 * c + d0;
     const size_t rb = (size_t)(b0 + p) * S;
@@ -855,7 +856,6 @@ __device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, float* _
                 dk[j] += ds * q;
                 dv[j] += pr[j] * g;
             }
-            st2(dqkv + (rb + i) * 3 * D + col, dq);
             sdq += dq;
         }
         st2(sm.big + (i * SPW + p) * LDB + d0, dq);
@@ -865,8 +865,6 @@ __device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, float* _
     for (int j = 0; j < S; ++j) {
         st2(sm.big + (j * SPW + p) * LDB + 64 + d0, dk[j]);
         st2(sm.big + (j * SPW + p) * LDB + 128 + d0, dv[j]);
-        st2(dqkv + (rb + j) * 3 * D + D + col, dk[j]);
-        st2(dqkv + (rb + j) * 3 * D + 2 * D + col, dv[j]);
         sk += dk[j];
         sv += dv[j];
     }
@@ -982,7 +980,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         APre<2> pw = prefetch<2>(WinT, 3 * D, 16 * wv, 64 * c);
-        attn_bwd_chunk<last>(sm, io.qkv, io.dqkv, c, b0, sm.scr);
+        attn_bwd_chunk<last>(sm, io.qkv, c, b0, sm.scr);
         __syncthreads();
         BTR(TB + 11 + 2 * c);
         if (threadIdx.x < 3 * 64) {  // in_proj bias partial of the chunk: the 8 wave rows of sm.scr
@@ -992,6 +990,17 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
             for (int w = 0; w < NW; ++w) v += sm.scr[w * 192 + i];
             bias[kBiasIn + (i >> 6) * D + 64 * c + (i & 63)] = v;
         }
+        // first weight blocks of the chunk's K and V parts, loaded ahead of the stores below (the
+        // vector memory counter retires in order: loads behind a store burst wait for it)
+        APre<2> pw1 = prefetch<2>(WinT, 3 * D, 16 * wv, D + 64 * c);
+        APre<2> pw2 = prefetch<2>(WinT, 3 * D, 16 * wv, 2 * D + 64 * c);
+        // dq | dk | dv of the chunk -> dqkv rows: 256-byte row segments, float4 per thread
+        for (int i = threadIdx.x; i < TOK * 48; i += NTHR) {
+            const int tok = i / 48, r = i - tok * 48, part = r >> 4, q = r & 15;
+            if (part == 0 && tok < qtok0) continue;  // pruned: dq only on the query rows
+            st4(io.dqkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q,
+                ld4(sm.big + tok * LDB + part * 64 + 4 * q));
+        }
         if (last) {  // dq is zero outside the query tile: Win_q^T dq only for column tile 4
             f32x4 a1[1] = {acc[S - 1]};
             gemm_tile<1, 2, 4>(a1, pw, WinT, 3 * D, 16 * wv, 64 * c, sm.big, LDB, (S - 1) * SPW);
@@ -999,12 +1008,8 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         } else {
             gemm_tile<S, 2, 4>(acc, pw, WinT, 3 * D, 16 * wv, 64 * c, sm.big, LDB, 0);
         }
-#pragma unroll
-        for (int part = 1; part < 3; ++part) {
-            const int kw = part * D + 64 * c;
-            gemm_tile<S, 2, 4>(acc, prefetch<2>(WinT, 3 * D, 16 * wv, kw), WinT, 3 * D, 16 * wv, kw,
-                               sm.big + part * 64, LDB, 0);
-        }
+        gemm_tile<S, 2, 4>(acc, pw1, WinT, 3 * D, 16 * wv, D + 64 * c, sm.big + 64, LDB, 0);
+        gemm_tile<S, 2, 4>(acc, pw2, WinT, 3 * D, 16 * wv, 2 * D + 64 * c, sm.big + 128, LDB, 0);
         if (c == 0) __syncthreads();  // big is rewritten by chunk 1
         BTR(TB + 12 + 2 * c);
     }
