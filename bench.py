@@ -8,9 +8,10 @@ normalisation, and with N > 1 GPUs the RCCL all-gather of the trajectories (SURV
 value = E * T * K * N / max-over-ranks wall time. Inputs (scenes, windows) are resident in HBM.
 
 Also reported (same JSON line):
-  roofline      dominant kernel = k_policy_forward, MFMA fp32 peak, algorithmic 2,446,208
-                FLOP/sample (last-token-pruned forward) x E per launch / its average
-                HIP-event duration over the timed region
+  roofline      dominant kernel = k_policy_forward, MFMA fp32 peak, algorithmic FLOP per launch of
+                the path the rollout runs (window-row ring: 1,790,848 FLOP/sample; the full-window
+                forward is 2,446,208) x E / its average HIP-event duration over the
+                timed region
   env_roofline  k_env_step against HBM, algorithmic 24*M + 490 B per env-step
   env_fused     env-only K2 with T = 256 steps per launch (state in registers): BASELINE configs[1]
                 (1024 envs x 8 x 16) and the headline shape, env-steps/s and algorithmic GB/s
@@ -35,7 +36,10 @@ for p in (ROOT, os.path.join(ROOT, "target-allocation-ppo-transformer_amd")):
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-POLICY_FLOP_PER_SAMPLE = 2_446_208  # SURVEY.md 8(d), derived in DESIGN.md
+POLICY_FLOP_PER_SAMPLE = 2_446_208  # full-window forward (last-token pruned), DESIGN.md 4
+# the rollout's window-row path (uavhip_policy_forward_rows) forms layer-0 Q|K|V of the new row
+# only: minus 4 rows x (actor K,V 256 + critic Q,K,V 384) x 128 x 2 FLOP
+ROWS_FLOP_PER_SAMPLE = POLICY_FLOP_PER_SAMPLE - 4 * (256 + 384) * 128 * 2  # 1,790,848
 MFMA_F32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: fp32 MFMA = vector peak
 HBM_PEAK_GBS = 8000.0
 
@@ -76,6 +80,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--eager", action="store_true", help="launch kernels eagerly instead of replaying a hipGraph")
+    ap.add_argument("--full-window", action="store_true",
+                    help="policy forward over the full window every step (no window-row ring)")
     return ap.parse_args()
 
 
@@ -240,7 +246,8 @@ def main():
     torch.manual_seed(0)  # identical initial policy on every rank
     policy = TransformerActorCritic().to(dev)
     env = VecUAVEnv(E, args.uavs, args.targets, 1, 1, seed=1 + rank, full_reset_period=200)
-    eng = RolloutEngine(env, policy, T, want_info=True, bootstrap=True, seed=1000 + rank, normalize=(world == 1))
+    eng = RolloutEngine(env, policy, T, want_info=True, bootstrap=True, seed=1000 + rank, normalize=(world == 1),
+                        row_cache=not args.full_window)
     eng.start()
 
     # The iteration is captured once into a hipGraph and replayed. HIP events (recorded on the
@@ -286,7 +293,8 @@ def main():
     pol_list, env_list = eng.event_ms()   # the last timed iteration's T+1 policy and T env launches
     pol_ms = float(np.mean(pol_list))
     env_ms = float(np.mean(env_list))
-    achieved_tf = POLICY_FLOP_PER_SAMPLE * E / (pol_ms * 1e-3) / 1e12
+    flop_sample = ROWS_FLOP_PER_SAMPLE if eng.rowproj is not None else POLICY_FLOP_PER_SAMPLE
+    achieved_tf = flop_sample * E / (pol_ms * 1e-3) / 1e12
     env_gbs = env_bytes_per_step(args.targets) * E / (env_ms * 1e-3) / 1e9
 
     env_fused = None
@@ -322,7 +330,9 @@ def main():
             "roofline": {"kernel": "k_policy_forward", "bound": "mfma", "achieved": achieved_tf,
                          "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / MFMA_F32_PEAK_TFLOPS,
                          "traffic": pol_traffic, "traffic_unit": "bytes/launch (PMC)", "traffic_source": pol_src,
-                         "avg_launch_ms": pol_ms, "flop_per_launch": POLICY_FLOP_PER_SAMPLE * E,
+                         "avg_launch_ms": pol_ms, "flop_per_launch": flop_sample * E,
+                         "path": "window-row ring (layer-0 in_proj of the new row only)" if eng.rowproj is not None
+                         else "full window",
                          "timing": "HIP events around each of the T+1 launches of the last timed iteration"},
             "env_roofline": {"kernel": "k_env_step", "bound": "hbm", "achieved": env_gbs, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS, "avg_launch_ms": env_ms,

@@ -265,6 +265,23 @@ int uavhip_policy_forward(const uavhip_policy* policy, const float* states, int3
                           uint64_t seed, uint64_t offset, const uint64_t* offset_dev, int8_t* action_out,
                           float* logp, float* value, float* entropy, float* logits, uavhip_stream_t stream);
 
+/* Rollout fast path of uavhip_policy_forward for a SEQUENCE of windows in which window g + 1 is
+ * window g shifted by one row plus a new last row (the observation deque, uav_env.py:241-242;
+ * after an episode end the earlier rows are zero padding). rowproj (caller-owned, size
+ * uavhip_policy_rowproj_floats(B)) keeps, per window, the layer-0 in_proj of the embeddings of
+ * its rows (a 5-slot ring indexed by step mod 5) and Win . pos of both trunks, so the forward of
+ * step g projects only the new row (transformer_net.py:57-63 is linear up to the in_proj after
+ * the embedding ReLU). step = g (>= 0, +1 per call along the sequence); fill != 0 rebuilds rows
+ * 0-3 and the pos table from states and the current weights: required on the first call, after
+ * the weights change, and whenever states is not the previous call's window advanced by one
+ * row. Outputs as uavhip_policy_forward, equal to it within fp32 rounding (Win (e + pos) + b is
+ * evaluated as (Win e + b) + Win pos). */
+int64_t uavhip_policy_rowproj_floats(int32_t B);
+int uavhip_policy_forward_rows(const uavhip_policy* policy, const float* states, int32_t B, float* rowproj,
+                               int32_t step, int32_t fill, const int8_t* actions_in, uint64_t seed, uint64_t offset,
+                               const uint64_t* offset_dev, int8_t* action_out, float* logp, float* value,
+                               float* entropy, float* logits, uavhip_stream_t stream);
+
 /* ---------------------------------------------------------------- PPO update (K5) */
 
 /* One clipped-PPO minibatch step of agents/ppo.py:96-169 (evaluate -> surrogate / clipped value

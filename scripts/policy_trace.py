@@ -22,6 +22,7 @@ LAYER = ["start", "c0 gemm", "c0 sync", "c0 attn+sync", "c1 gemm", "c1 sync", "c
 for li, tag in enumerate(["A", "C0", "C1"]):
     for j, n in enumerate(LAYER):
         NAMES[8 + 16 * li + j] = f"{tag}.{n}"
+    NAMES[8 + 16 * li + 13] = f"{tag}.ring gemm"
 
 B = int(os.environ.get("B", "4096"))
 torch.manual_seed(0)
@@ -34,13 +35,20 @@ v = torch.empty(B, device="cuda")
 fn = _lib.LIB.uavhip_policy_trace
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-for _ in range(5):
-    net.fused_forward(x, action_out=a, logp=lp, value=v)
+ROWS = os.environ.get("ROWS", "0") == "1"  # window-row ring path (uavhip_policy_forward_rows)
+kw = {}
+if ROWS:
+    from uavhip.policy import rowproj_buffer
+    rp = rowproj_buffer(B)
+for i in range(5):
+    if ROWS:  # timing only: the same windows replayed as a sequence
+        kw = dict(rowproj=rp, step=i, fill=i == 0)
+    net.fused_forward(x, action_out=a, logp=lp, value=v, **kw)
 torch.cuda.synchronize()
 buf = np.zeros(256 * 2 * 64, np.uint64)
 assert fn(buf.ctypes.data, buf.size) == 0
 t = buf.reshape(256, 2, 64).astype(np.int64)
-slots = sorted(k for k in NAMES if (t[:, 0, k] != 0).all())
+slots = sorted((k for k in NAMES if (t[:, 0, k] != 0).all()), key=lambda k: np.median(t[:, 0, k] - t[:, 0, 0]))
 base = t[:, :, 0:1]
 rel = t - base
 print(f"B={B}; median cycles since block start (wave0 / wave4) and per-phase delta (wave0)")

@@ -369,35 +369,53 @@ __device__ void attention_chunk(Smem& sm, int c, int qs0, int nqs) {
 
 // Embedding (transformer_net.py:57-59) on the MFMA, K = 14 padded to 16 with zeros:
 // h[s*16+p][f] = relu(W_e x[p][s] + b_e)[f] + pos[s][f]; wave w computes features [16w, 16w+16).
-template <int trunk, bool TR = false>
-__device__ void embed(Smem& sm, const float* __restrict__ P, float* e_out = nullptr, float* h_out = nullptr,
-                      int b0 = 0) {
+// The global operands (weights, bias, position rows) are loaded up front (embed_load), so a caller
+// can issue later loads behind them without the embedding waiting for those (in-order vmcnt).
+struct EmbPre {
+    f32x4 a, bb, pp[S];
+};
+template <int trunk>
+__device__ __forceinline__ EmbPre embed_load(const float* __restrict__ P) {
     const float* We = P + kOffs.o[trunk + EMB_W];
     const float* be = P + kOffs.o[trunk + EMB_B];
     const float* pos = P + kOffs.o[trunk + POS];
     const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
     const int f = 16 * wv + i16;
-    f32x4 a;
-    a.x = 4 * g + 0 < IN ? We[f * IN + 4 * g + 0] : 0.f;
-    a.y = 4 * g + 1 < IN ? We[f * IN + 4 * g + 1] : 0.f;
-    a.z = 4 * g + 2 < IN ? We[f * IN + 4 * g + 2] : 0.f;
-    a.w = 4 * g + 3 < IN ? We[f * IN + 4 * g + 3] : 0.f;
-    f32x4 acc[S];
+    EmbPre r;
+    r.a.x = 4 * g + 0 < IN ? We[f * IN + 4 * g + 0] : 0.f;
+    r.a.y = 4 * g + 1 < IN ? We[f * IN + 4 * g + 1] : 0.f;
+    r.a.z = 4 * g + 2 < IN ? We[f * IN + 4 * g + 2] : 0.f;
+    r.a.w = 4 * g + 3 < IN ? We[f * IN + 4 * g + 3] : 0.f;
+    r.bb = *reinterpret_cast<const f32x4*>(be + 16 * wv + 4 * g);
 #pragma unroll
-    for (int ct = 0; ct < S; ++ct) {
+    for (int ct = 0; ct < S; ++ct) r.pp[ct] = *reinterpret_cast<const f32x4*>(pos + ct * D + 16 * wv + 4 * g);
+    return r;
+}
+// MODE kEmbH: h = e + pos for all 5 positions (sm.h). kEmbSplit: also e of position 4 (no pos)
+// -> sm.ctx rows 64-79 (the window-row projection path's in_proj input). kEmbRows: only e of
+// positions 0-3 -> sm.ctx (row projection fill).
+enum { kEmbH = 0, kEmbSplit = 1, kEmbRows = 2 };
+template <int trunk, bool TR = false, int MODE = kEmbH>
+__device__ void embed_apply(Smem& sm, const EmbPre& ep, float* e_out = nullptr, float* h_out = nullptr, int b0 = 0) {
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
+    constexpr int NT = MODE == kEmbRows ? S - 1 : S;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) {
         const f32x4 b = *reinterpret_cast<const f32x4*>(sm.x + (ct * SPW + i16) * LDX + 4 * g);
         acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc[ct], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(ep.a[j], b[j], acc[ct], 0, 0, 0);
     }
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(be + 16 * wv + 4 * g);
 #pragma unroll
-    for (int ct = 0; ct < S; ++ct) {
-        const f32x4 pp = *reinterpret_cast<const f32x4*>(pos + ct * D + 16 * wv + 4 * g);
-        f32x4 e = acc[ct] + bb;
+    for (int ct = 0; ct < NT; ++ct) {
+        f32x4 e = acc[ct] + ep.bb;
         e.x = fmaxf(e.x, 0.f); e.y = fmaxf(e.y, 0.f); e.z = fmaxf(e.z, 0.f); e.w = fmaxf(e.w, 0.f);
-        const f32x4 v = e + pp;
-        *reinterpret_cast<f32x4*>(sm.h + (ct * SPW + i16) * LDH + 16 * wv + 4 * g) = v;
+        const int o = (ct * SPW + i16) * LDH + 16 * wv + 4 * g;
+        if (MODE == kEmbRows || (MODE == kEmbSplit && ct == S - 1)) *reinterpret_cast<f32x4*>(sm.ctx + o) = e;
+        if (MODE == kEmbRows) continue;
+        const f32x4 v = e + ep.pp[ct];
+        *reinterpret_cast<f32x4*>(sm.h + o) = v;
         if (TR && !kExpNoStore) {
             const size_t r = (size_t)trow(ct * SPW + i16, b0);
             *reinterpret_cast<f32x4*>(e_out + r * D + 16 * wv + 4 * g) = e;
@@ -405,27 +423,31 @@ __device__ void embed(Smem& sm, const float* __restrict__ P, float* e_out = null
         }
     }
 }
+template <int trunk, bool TR = false>
+__device__ void embed(Smem& sm, const float* __restrict__ P, float* e_out = nullptr, float* h_out = nullptr,
+                      int b0 = 0) {
+    embed_apply<trunk, TR>(sm, embed_load<trunk>(P), e_out, h_out, b0);
+}
 
 // K/V weight row of wave wv for chunk c: waves 0-3 K tiles, waves 4-7 V tiles
 __device__ __forceinline__ int kv_row(int wv, int c) { return (1 + (wv >> 2)) * D + 64 * c + 16 * (wv & 3); }
+
+template <int trunk, int layer, bool last, bool TR>
+__device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P, const APre<depth<last ? 1 : S>()>& po,
+                           const TrainLayerIO& io, int b0);
 
 // One post-LN nn.TransformerEncoderLayer (relu FFN 256, 8 heads). last: prune to column tile 4.
 // Work split: 8 waves, wave w and w+4 share a SIMD (and its MFMA pipe); every GEMM gives each
 // SIMD the same number of 16-row output tiles. `pkv` = the caller's prefetch of this layer's first
 // K/V weight blocks. Ends WITHOUT a final barrier: the caller prefetches its next weights, then syncs.
 template <int trunk, int layer, bool last, bool TR = false>
-__device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv,
+__device__ __forceinline__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv,
                               const TrainLayerIO& io = TrainLayerIO{}, int b0 = 0) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
     PTR(tb);
     const float* Win = P + kOffs.o[layer_param(trunk, layer, INW)];
     const float* bin = P + kOffs.o[layer_param(trunk, layer, INB)];
     const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
-    const float* bo = P + kOffs.o[layer_param(trunk, layer, OUTB)];
-    const float* W1 = P + kOffs.o[layer_param(trunk, layer, L1W)];
-    const float* b1 = P + kOffs.o[layer_param(trunk, layer, L1B)];
-    const float* W2 = P + kOffs.o[layer_param(trunk, layer, L2W)];
-    const float* b2 = P + kOffs.o[layer_param(trunk, layer, L2B)];
     const int wv = threadIdx.x >> 6;
     constexpr int CTQ = last ? 1 : S;              // column tiles that need Q / out / LN / FFN
     constexpr int DQ = depth<CTQ>();
@@ -460,6 +482,25 @@ __device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv
         __syncthreads();
         PTR(tb + 3 + 3 * c);
     }
+    layer_tail<trunk, layer, last, TR>(sm, P, po, io, b0);
+}
+
+// Out-projection + LN1 + FFN + LN2 of an encoder layer, after the attention output is in sm.ctx.
+// `po` = the caller's prefetch of the first out_proj weight blocks.
+template <int trunk, int layer, bool last, bool TR>
+__device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P, const APre<depth<last ? 1 : S>()>& po,
+                           const TrainLayerIO& io, int b0) {
+    [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
+    const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
+    const float* bo = P + kOffs.o[layer_param(trunk, layer, OUTB)];
+    const float* W1 = P + kOffs.o[layer_param(trunk, layer, L1W)];
+    const float* b1 = P + kOffs.o[layer_param(trunk, layer, L1B)];
+    const float* W2 = P + kOffs.o[layer_param(trunk, layer, L2W)];
+    const float* b2 = P + kOffs.o[layer_param(trunk, layer, L2B)];
+    const int wv = threadIdx.x >> 6;
+    constexpr int CTQ = last ? 1 : S;
+    constexpr int DQ = depth<CTQ>();
+    constexpr int qtok0 = last ? (S - 1) * SPW : 0;
     if (TR) store_rows(sm.ctx, LDH, io.o, D, 0, D, qtok0, b0, last);  // attention output
     // out projection, h = LN1(h + attn) in its epilogue
     APre<DQ> pf1a, pf1b;
@@ -498,6 +539,211 @@ __device__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv
                                 P + kOffs.o[layer_param(trunk, layer, N2B)], qtok0,
                                 LnOut{io.xhat2, io.h2, io.rstd2, b0, last});
     PTR(tb + 14);
+}
+
+// ------------------------------------------------------------------ window-row projections
+// Rollout fast path (uavhip_policy_forward_rows). Up to its in_proj, layer 0 of each trunk is
+// token-local and linear after the embedding ReLU: Q|K|V of window row j at position s is
+// Win (e_j + pos_s) + b_in = u_j + Win pos_s with u_j = Win e_j + b_in independent of s
+// (transformer_net.py:57-63; post-LN encoder, so no norm in between). Consecutive rollout windows
+// share 4 of their 5 rows (the observation deque, uav_env.py:241-242), so every env keeps the u
+// rows of its current window in a 5-slot ring -- row r of the window sequence in slot r mod 5 --
+// and the forward at sequence step g computes u for the new row only (slot g mod 5): the two
+// layer-0 in_proj GEMMs shrink from 80 to 16 tokens per workgroup. Rows 0-3 of a window at step g
+// are in slots (g + 1 + s) mod 5. Masked rows (all-zero padding, transformer_net.py:52-54) are
+// keys masked in every layer and never reach the last token, so they read as zero.
+// Ring row: actor K | V (2 x 128), then critic Q | K | V (3 x 128); Win pos_s table in front.
+constexpr int kPposFloats = 2 * S * 3 * D;  // [trunk][s][384]
+constexpr int kRowFloats = 5 * D;
+struct RowIO {
+    float* rp;  // [kPposFloats] Win pos_s, then ring [5][B][kRowFloats]
+    int B, g;   // windows; sequence step of this forward
+};
+constexpr int kPwD = 4;  // in_proj k-blocks of the new-row GEMM loaded ahead (of 8)
+template <int trunk> constexpr int row_parts() { return trunk == kActorTrunk ? 2 : 3; }  // K,V / Q,K,V
+template <int NP>
+struct RowPre {
+    f32x4 v[2][2 * NP];  // per chunk: this thread's ring values of positions 0-3
+    float pp[2][2];      // per chunk: this thread's share of the [5][192] Win pos_s rows
+    f32x4 bias[3];       // in_proj bias of the wave's Q, K, V rows (new-row GEMM epilogue)
+};
+
+// Win pos_s of chunk c ([s][part * 64 + d], d < 64) -> registers; staged into sm.red (free during
+// the chunk loop) by ppos_stage.
+template <int trunk, int NP>
+__device__ __forceinline__ void ppos_load(RowPre<NP>& r, const RowIO& rio) {
+    const float* pp = rio.rp + (trunk == kActorTrunk ? 0 : S * 3 * D);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = (threadIdx.x + NTHR * u) % (S * 192);  // (threads past 960 reload, unused)
+            const int s = i / 192, rr = i - 192 * s, part = rr >> 6, cc = rr & 63;
+            r.pp[c][u] = pp[s * 3 * D + part * D + 64 * c + cc];
+        }
+}
+template <int NP>
+__device__ __forceinline__ void ppos_stage(Smem& sm, const RowPre<NP>& r, int c) {
+    float* pl = reinterpret_cast<float*>(sm.red);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int i = threadIdx.x + NTHR * u;
+        if (i < S * 192) pl[i] = r.pp[c][u];
+    }
+}
+// Item u of chunk c for this thread: float4 q of part `part` (of the NP cached parts) of token tok
+// (position tok >> 4 < 4, sample tok & 15); 16 consecutive lanes read one 256-byte row segment.
+template <int NP>
+__device__ __forceinline__ void ring_item(int u, int& part, int& tok) {
+    const int t2 = (threadIdx.x >> 4) + 32 * u;
+    part = t2 % NP;
+    tok = t2 / NP;
+}
+// Chunk c of the ring rows (the critic loads chunk 1 only after its new-row GEMM: registers).
+template <int trunk, int NP>
+__device__ __forceinline__ void ring_load(RowPre<NP>& r, const Smem& sm, const RowIO& rio, int b0, int c) {
+    constexpr int ROFF = trunk == kActorTrunk ? 0 : 2 * D;
+    const float* slots = rio.rp + kPposFloats;
+    const int q = threadIdx.x & 15;
+    // predicates and offsets first (LDS reads of the mask), then the loads back to back: no LDS
+    // read lands in a register of an outstanding load (that forces a vmcnt(0) drain)
+    int off[2 * NP];
+#pragma unroll
+    for (int u = 0; u < 2 * NP; ++u) {
+        int part, tok;
+        ring_item<NP>(u, part, tok);
+        const int s = tok >> 4, p = tok & 15, b = b0 + p;
+        const bool ok = b < rio.B && !sm.mask[p * S + s];
+        const int slot = (rio.g + 1 + s) % 5;
+        off[u] = ok ? (slot * rio.B + b) * kRowFloats + ROFF + part * D + 64 * c + 4 * q : -1;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // unconditional loads (masked items read ring row 0 and are dropped): a load under a branch
+    // makes the compiler's vmcnt bookkeeping assume it may be missing and wait for everything
+#pragma unroll
+    for (int u = 0; u < 2 * NP; ++u) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(slots + (off[u] >= 0 ? off[u] : 4 * q));
+        r.v[c][u] = off[u] >= 0 ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+
+// acc[r] += W[row[r] + i][k] . X[xtok0 + j][k] over k in [0, 128): R weight tiles against one
+// activation tile (shared B operand), blocks < D from `pre` (D = KB: weights fully preloaded).
+// `issued()` runs right after the last weight load is issued: loads it issues queue behind the
+// GEMM's own (vmcnt retires in order), so none of the GEMM's waits cover them.
+template <int R, int D, class F>
+__device__ __forceinline__ void gemm_rows(f32x4 (&acc)[R], const APre<D> (&pre)[R], const float* __restrict__ W,
+                                          int ldw, const int (&row)[R], const float* X, int ldx, int xtok0,
+                                          F&& issued) {
+    const int l = lane_id(), i16 = l & 15, g = l >> 4;
+    const float* xp = X + (xtok0 + i16) * ldx + 4 * g;
+    f32x4 a[KB][R], b[KB];
+#pragma unroll
+    for (int p = 0; p < D; ++p) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) a[p][r] = pre[r].a[p];
+        b[p] = *reinterpret_cast<const f32x4*>(xp + 16 * p);
+    }
+#pragma unroll
+    for (int i = 0; i < KB; ++i) {
+        if (i + D < KB) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                a[i + D][r] = *reinterpret_cast<const f32x4*>(frag_ptr(W, ldw, row[r], 0) + 256 * (i + D));
+            b[i + D] = *reinterpret_cast<const f32x4*>(xp + 16 * (i + D));
+        }
+        if (i == (D < KB ? KB - D - 1 : 0)) issued();
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][r][j], b[i][j], acc[r], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// Layer 0 of a trunk on the ring: u of the new row (position 4) from `pw` (in_proj rows 128 j +
+// 16 wv: this wave's Q, K and V features, all in chunk wv >> 2) and the ring rows of positions
+// 0-3 from `rp`; then attention and layer_tail as in encoder_layer. Expects sm.ctx rows 64-79 =
+// e of position 4 (embed_apply kEmbSplit), sm.red = Win pos_s of chunk 0 (ppos_stage).
+template <int trunk, int NP>
+__device__ __forceinline__ void encoder_layer_rows(Smem& sm, const float* __restrict__ P, const APre<kPwD> (&pw)[3], RowPre<NP>& rp,
+                                   const RowIO& rio, int b0) {
+    constexpr bool last = trunk == kActorTrunk;  // the actor's layer 0 is its last (pruned) layer
+    constexpr int P0 = 3 - NP, ROFF = trunk == kActorTrunk ? 0 : 2 * D;
+    constexpr int CTQ = last ? 1 : S, DQ = depth<CTQ>();
+    [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1);
+    PTR(tb);
+    const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
+    const float* Wo = P + kOffs.o[layer_param(trunk, 0, OUTW)];
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
+    const int rows[3] = {16 * wv, D + 16 * wv, 2 * D + 16 * wv};
+    f32x4 acc[3] = {};
+    gemm_rows<3, kPwD>(acc, pw, Win, D, rows, sm.ctx, LDH, (S - 1) * SPW, [&] {
+        ring_load<trunk>(rp, sm, rio, b0, 0);
+        if (trunk == kActorTrunk) ring_load<trunk>(rp, sm, rio, b0, 1);
+    });
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[j] += rp.bias[j];  // u = Win e + b
+    if (b0 + i16 < rio.B) {  // the new row -> ring slot g mod 5
+        float* dst = rio.rp + kPposFloats + ((size_t)(rio.g % 5) * rio.B + b0 + i16) * kRowFloats + ROFF + 16 * wv + 4 * g;
+#pragma unroll
+        for (int j = P0; j < 3; ++j) *reinterpret_cast<f32x4*>(dst + (j - P0) * D) = acc[j];
+    }
+    if (trunk != kActorTrunk) ring_load<trunk>(rp, sm, rio, b0, 1);
+    PTR(tb + 13);
+    const float* pl = reinterpret_cast<const float*>(sm.red);
+    const int q = threadIdx.x & 15;
+    APre<DQ> po;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        // Q | K | V of the chunk -> sm.big: positions 0-3 from the ring, position 4 from acc
+#pragma unroll
+        for (int u = 0; u < 2 * NP; ++u) {
+            int part, tok;
+            ring_item<NP>(u, part, tok);
+            const int bp = part + P0, s = tok >> 4;
+            *reinterpret_cast<f32x4*>(sm.big + tok * LDB + bp * 64 + 4 * q) =
+                rp.v[c][u] + *reinterpret_cast<const f32x4*>(pl + s * 192 + bp * 64 + 4 * q);
+        }
+        if ((wv >> 2) == c) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int col = 64 * j + 16 * (wv & 3) + 4 * g;
+                *reinterpret_cast<f32x4*>(sm.big + ((S - 1) * SPW + i16) * LDB + col) =
+                    acc[j] + *reinterpret_cast<const f32x4*>(pl + (S - 1) * 192 + col);
+            }
+        }
+        if (c == 1) po = prefetch<DQ>(Wo, D, 16 * wv, 0);
+        PTR(tb + 1 + 3 * c);
+        __syncthreads();
+        PTR(tb + 2 + 3 * c);
+        if (c == 0) ppos_stage(sm, rp, 1);  // sm.red is read again only by the chunk-1 assembly
+        if (last) attention_chunk(sm, c, S - 1, 1);
+        else attention_full(sm, c);
+        __syncthreads();
+        PTR(tb + 3 + 3 * c);
+    }
+    layer_tail<trunk, 0, last, false>(sm, P, po, TrainLayerIO{}, b0);
+}
+
+// Everything layer 0 of a trunk needs before its new-row GEMM (which then issues the ring loads
+// behind its last weight loads): embedding operands, Win pos_s, the wave's in_proj weight tiles
+// and bias. Ends with the embedding in sm.h / sm.ctx and Win pos_s of
+// chunk 0 in sm.red, without a barrier.
+template <int trunk, int NP>
+__device__ __forceinline__ void rows_prologue(Smem& sm, const float* __restrict__ P, APre<kPwD> (&pw)[3],
+                                              RowPre<NP>& rp, const RowIO& rio, int b0) {
+    const int wv = threadIdx.x >> 6;
+    const EmbPre ep = embed_load<trunk>(P);
+    ppos_load<trunk>(rp, rio);
+    const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) pw[j] = prefetch<kPwD>(Win, D, j * D + 16 * wv, 0);
+    const float* bin = P + kOffs.o[layer_param(trunk, 0, INB)];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) rp.bias[j] = *reinterpret_cast<const f32x4*>(bin + j * D + 16 * wv + 4 * (lane_id() >> 4));
+    embed_apply<trunk, false, kEmbSplit>(sm, ep);
+    ppos_stage(sm, rp, 0);
 }
 
 // 128 -> 64 (MFMA, waves 0-3) -> relu -> nout (VALU) on the last-position rows (transformer_net.py:77-91)
@@ -585,14 +831,16 @@ __device__ void loss_partials(Smem& sm, const TrainIO& io, int b0) {
     }
 }
 
-template <bool TR>
+// ROWS: layer 0 of both trunks on the window-row projection ring (inference only).
+template <bool TR, bool ROWS = false>
 __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict__ P, const float* __restrict__ states,
                                                          int B, const int8_t* __restrict__ actions_in, uint64_t seed,
                                                          uint64_t offset, const uint64_t* __restrict__ offset_dev,
                                                          int8_t* __restrict__ action_out,
                                                          float* __restrict__ logp_out, float* __restrict__ value_out,
                                                          float* __restrict__ ent_out, float* __restrict__ logits_out,
-                                                         const TrainIO io) {
+                                                         const TrainIO io, const RowIO rio) {
+    static_assert(!(TR && ROWS), "the training forward recomputes every row");
     __shared__ __attribute__((aligned(16))) Smem sm;
     const int b0 = blockIdx.x * SPW;
     PTR(0);
@@ -650,11 +898,21 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     const float* headw_a = P + kOffs.o[kActorHead];
     const float* headw_c = P + kOffs.o[kCriticHead];
     // actor trunk (1 layer) + head
-    APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-    embed<kActorTrunk, TR>(sm, P, io.e[0], io.h0[0], b0);
-    PTR(2);
-    __syncthreads();
-    encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0);
+    if constexpr (ROWS) {
+        __syncthreads();  // sm.mask -> ring loads
+        APre<kPwD> pw[3];
+        RowPre<2> rp;
+        rows_prologue<kActorTrunk>(sm, P, pw, rp, rio, b0);
+        PTR(2);
+        __syncthreads();
+        encoder_layer_rows<kActorTrunk>(sm, P, pw, rp, rio, b0);
+    } else {
+        APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+        embed<kActorTrunk, TR>(sm, P, io.e[0], io.h0[0], b0);
+        PTR(2);
+        __syncthreads();
+        encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0);
+    }
     APre<4> ph;
     if (wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
     __syncthreads();
@@ -663,11 +921,19 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     if (TR) store_hidden(sm, io.z[0], b0);  // before the critic's LayerNorm partials reuse sm.z
     PTR(4);
     // critic trunk (2 layers) + head
-    pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-    embed<kCriticTrunk, TR>(sm, P, io.e[1], io.h0[1], b0);
-    __syncthreads();
-    encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv, io.L[1], b0);
-    pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
+    if constexpr (ROWS) {
+        APre<kPwD> pw[3];
+        RowPre<3> rp;
+        rows_prologue<kCriticTrunk>(sm, P, pw, rp, rio, b0);
+        __syncthreads();
+        encoder_layer_rows<kCriticTrunk>(sm, P, pw, rp, rio, b0);
+    } else {
+        APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+        embed<kCriticTrunk, TR>(sm, P, io.e[1], io.h0[1], b0);
+        __syncthreads();
+        encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv, io.L[1], b0);
+    }
+    APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
     __syncthreads();
     encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0);
     if (wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
@@ -706,6 +972,78 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         }
     }
     PTR(7);
+}
+
+// Ring fill of one trunk: u rows of positions 0-3 of the workgroup's 16 windows -> slots
+// (g + 1 + s) mod 5, the same GEMM (k order, bias add) as the forward's new-row u.
+template <int trunk>
+__device__ void rows_fill_trunk(Smem& sm, const float* __restrict__ P, const RowIO& rio, int b0) {
+    constexpr int NP = row_parts<trunk>(), P0 = 3 - NP, ROFF = trunk == kActorTrunk ? 0 : 2 * D;
+    const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
+    const float* bin = P + kOffs.o[layer_param(trunk, 0, INB)];
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
+    embed_apply<trunk, false, kEmbRows>(sm, embed_load<trunk>(P));
+    __syncthreads();
+    float* slots = rio.rp + kPposFloats;
+#pragma unroll
+    for (int j = P0; j < 3; ++j) {
+        const int row = j * D + 16 * wv;
+        f32x4 acc[S - 1];
+        zero(acc);
+        gemm_tile<S - 1, 2>(acc, prefetch<2>(Win, D, row, 0), Win, D, row, 0, sm.ctx, LDH, 0);
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(bin + row + 4 * g);
+        const int b = b0 + i16;
+        if (b < rio.B) {
+#pragma unroll
+            for (int s = 0; s < S - 1; ++s)
+                *reinterpret_cast<f32x4*>(slots + ((size_t)((rio.g + 1 + s) % 5) * rio.B + b) * kRowFloats + ROFF +
+                                          (j - P0) * D + 16 * wv + 4 * g) = acc[s] + bb;
+        }
+    }
+    __syncthreads();  // sm.ctx is the next trunk's embedding
+}
+
+// Win pos_s of one trunk -> rp[trunk][s][384] (no bias): pos rows as activation tile columns 0-4.
+template <int trunk>
+__device__ void rows_ppos_trunk(Smem& sm, const float* __restrict__ P, float* out) {
+    const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
+    const float* pos = P + kOffs.o[trunk + POS];
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < SPW * D; i += NTHR) {
+        const int t = i / D, k = i - t * D;
+        sm.h[t * LDH + k] = t < S ? pos[t * D + k] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int row = j * D + 16 * wv;
+        f32x4 acc[1];
+        zero(acc);
+        gemm_tile<1, 2>(acc, prefetch<2>(Win, D, row, 0), Win, D, row, 0, sm.h, LDH, 0);
+        if (i16 < S) *reinterpret_cast<f32x4*>(out + i16 * 3 * D + row + 4 * g) = acc[0];
+    }
+    __syncthreads();
+}
+
+// uavhip_policy_forward_rows with fill: rebuilds the ring rows of positions 0-3 of every window
+// (blocks < nb) and the Win pos_s table (block nb) from the current weights.
+__global__ __launch_bounds__(NTHR) void k_policy_rows_fill(const float* __restrict__ P,
+                                                           const float* __restrict__ states, const RowIO rio) {
+    __shared__ __attribute__((aligned(16))) Smem sm;
+    const int nb = (rio.B + SPW - 1) / SPW;
+    if ((int)blockIdx.x == nb) {
+        rows_ppos_trunk<kActorTrunk>(sm, P, rio.rp);
+        rows_ppos_trunk<kCriticTrunk>(sm, P, rio.rp + S * 3 * D);
+        return;
+    }
+    const int b0 = blockIdx.x * SPW;
+    for (int i = threadIdx.x; i < (S - 1) * SPW * LDX; i += NTHR) {  // positions 0-3 only
+        const int t = i / LDX, k = i - t * LDX, s = t / SPW, p = t - s * SPW;
+        sm.x[i] = (k < IN && b0 + p < rio.B) ? states[((size_t)(b0 + p) * S + s) * IN + k] : 0.f;
+    }
+    __syncthreads();
+    rows_fill_trunk<kActorTrunk>(sm, P, rio, b0);
+    rows_fill_trunk<kCriticTrunk>(sm, P, rio, b0);
 }
 
 // ================================================================== K6: fused training backward
@@ -1212,7 +1550,7 @@ namespace uavhip {
 namespace pol {
 int policy_forward_train(const float* packed, const float* states, const TrainIO& io, int Bm, hipStream_t st) {
     hipLaunchKernelGGL(k_policy_forward<true>, dim3(Bm / SPW), dim3(NTHR), 0, st, packed, states, Bm, nullptr, 0ull,
-                       0ull, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, io);
+                       0ull, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, io, RowIO{});
     return check_launch("k_policy_forward<train>");
 }
 
@@ -1319,24 +1657,57 @@ extern "C" int uavhip_policy_btrace(unsigned long long* out, int n) {  // k_poli
 }
 #endif
 
-extern "C" int uavhip_policy_forward(const uavhip_policy* policy, const float* states, int32_t B,
-                                     const int8_t* actions_in, uint64_t seed, uint64_t offset,
-                                     const uint64_t* offset_dev, int8_t* action_out, float* logp, float* value,
-                                     float* entropy, float* logits, uavhip_stream_t stream) {
+static int check_policy(const char* fn, const uavhip_policy* policy, const float* states, int32_t B) {
     if (!policy || !policy->weights || !states || B <= 0) {
-        set_error("uavhip_policy_forward: NULL policy/weights/states or B=%d", B);
+        set_error("%s: NULL policy/weights/states or B=%d", fn, B);
         return UAVHIP_EINVAL;
     }
     if (policy->n_floats != pol::kOffs.o[pol::kNumParams] || policy->d_model != pol::D || policy->n_heads != pol::NH ||
         policy->d_ff != pol::FF || policy->d_head_hidden != pol::HID || policy->actor_layers != 1 ||
         policy->critic_layers != 2) {
-        set_error("uavhip_policy_forward: unsupported architecture / packed size %d (expected %d)", policy->n_floats,
+        set_error("%s: unsupported architecture / packed size %d (expected %d)", fn, policy->n_floats,
                   pol::kOffs.o[pol::kNumParams]);
         return UAVHIP_EINVAL;
     }
+    return UAVHIP_OK;
+}
+
+extern "C" int uavhip_policy_forward(const uavhip_policy* policy, const float* states, int32_t B,
+                                     const int8_t* actions_in, uint64_t seed, uint64_t offset,
+                                     const uint64_t* offset_dev, int8_t* action_out, float* logp, float* value,
+                                     float* entropy, float* logits, uavhip_stream_t stream) {
+    if (const int rc = check_policy("uavhip_policy_forward", policy, states, B)) return rc;
     const int grid = (B + pol::SPW - 1) / pol::SPW;
     hipLaunchKernelGGL(pol::k_policy_forward<false>, dim3(grid), dim3(pol::NTHR), 0, (hipStream_t)stream,
                        policy->weights, states, (int)B, actions_in, seed, offset, offset_dev, action_out, logp, value,
-                       entropy, logits, pol::TrainIO{});
+                       entropy, logits, pol::TrainIO{}, pol::RowIO{});
     return check_launch("k_policy_forward");
+}
+
+extern "C" int64_t uavhip_policy_rowproj_floats(int32_t B) {
+    return B > 0 ? pol::kPposFloats + (int64_t)pol::S * B * pol::kRowFloats : -1;
+}
+
+extern "C" int uavhip_policy_forward_rows(const uavhip_policy* policy, const float* states, int32_t B,
+                                          float* rowproj, int32_t step, int32_t fill, const int8_t* actions_in,
+                                          uint64_t seed, uint64_t offset, const uint64_t* offset_dev,
+                                          int8_t* action_out, float* logp, float* value, float* entropy,
+                                          float* logits, uavhip_stream_t stream) {
+    if (const int rc = check_policy("uavhip_policy_forward_rows", policy, states, B)) return rc;
+    if (!rowproj || step < 0 || (int64_t)B * pol::S * pol::kRowFloats >= (int64_t)1 << 31) {
+        set_error("uavhip_policy_forward_rows: NULL rowproj, step=%d < 0 or B=%d above the ring's 32-bit offsets",
+                  step, B);
+        return UAVHIP_EINVAL;
+    }
+    const int grid = (B + pol::SPW - 1) / pol::SPW;
+    const pol::RowIO rio{rowproj, (int)B, (int)step};
+    if (fill) {
+        hipLaunchKernelGGL(pol::k_policy_rows_fill, dim3(grid + 1), dim3(pol::NTHR), 0, (hipStream_t)stream,
+                           policy->weights, states, rio);
+        if (const int rc = check_launch("k_policy_rows_fill")) return rc;
+    }
+    hipLaunchKernelGGL((pol::k_policy_forward<false, true>), dim3(grid), dim3(pol::NTHR), 0, (hipStream_t)stream,
+                       policy->weights, states, (int)B, actions_in, seed, offset, offset_dev, action_out, logp, value,
+                       entropy, logits, pol::TrainIO{}, rio);
+    return check_launch("k_policy_forward_rows");
 }

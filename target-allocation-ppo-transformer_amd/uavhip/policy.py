@@ -114,10 +114,14 @@ class TransformerActorCritic(nn.Module):
         return self._packed
 
     def fused_forward(self, states, actions=None, action_out=None, logp=None, value=None, entropy=None,
-                      logits=None, seed=None, offset=None, offset_dev=None, check_weights=True):
+                      logits=None, seed=None, offset=None, offset_dev=None, check_weights=True, rowproj=None,
+                      step=0, fill=True):
         """Raw fused forward on [B, 5, 14] fp32 device windows; returns the output tensors.
         offset_dev: optional device uint64 [1] added to the sampling counter (graph replays);
-        check_weights=False skips the repack check (caller guarantees the pack is current)."""
+        check_weights=False skips the repack check (caller guarantees the pack is current).
+        rowproj (a rowproj_buffer(B) tensor) selects the window-sequence fast path
+        (uavhip_policy_forward_rows): step = index of `states` in the sequence, fill = rebuild the
+        cached rows (first call, new weights, or windows not advanced by one row)."""
         if states.device.type != "cuda":
             raise RuntimeError("the fused policy forward runs on the GPU (HIP) only")
         states = states.contiguous()
@@ -136,6 +140,15 @@ class TransformerActorCritic(nn.Module):
             offset = self._sample_offset
             self._sample_offset += B
         seed = self.sample_seed if seed is None else seed
+        if rowproj is not None:
+            if rowproj.numel() < LIB.uavhip_policy_rowproj_floats(B) or rowproj.dtype != torch.float32:
+                raise ValueError("rowproj: need a float32 buffer of rowproj_buffer(B) elements")
+            check(LIB.uavhip_policy_forward_rows(self._desc, ptr(states), B, ptr(rowproj), int(step), int(bool(fill)),
+                                                 ptr(actions), ctypes.c_uint64(seed), ctypes.c_uint64(offset),
+                                                 ptr(offset_dev), ptr(action_out), ptr(logp), ptr(value),
+                                                 ptr(entropy), ptr(logits), stream_handle()),
+                  "uavhip_policy_forward_rows")
+            return action_out, logp, value, entropy, logits
         check(LIB.uavhip_policy_forward(self._desc, ptr(states), B, ptr(actions), ctypes.c_uint64(seed),
                                         ctypes.c_uint64(offset), ptr(offset_dev), ptr(action_out), ptr(logp), ptr(value),
                                         ptr(entropy), ptr(logits), stream_handle()), "uavhip_policy_forward")
@@ -150,6 +163,11 @@ class TransformerActorCritic(nn.Module):
         ent = torch.empty(B, dtype=torch.float32, device=state.device)
         a, lp, v, ent, _ = self.fused_forward(state, entropy=ent)
         return a.long(), lp, v.view(B, 1), ent
+
+
+def rowproj_buffer(B, device="cuda"):
+    """Zeroed window-row projection buffer for fused_forward(rowproj=...) over B windows."""
+    return torch.zeros(int(LIB.uavhip_policy_rowproj_floats(int(B))), dtype=torch.float32, device=device)
 
 
 def layout():

@@ -18,6 +18,7 @@ reference's rule.
 import torch
 
 from . import _lib
+from .policy import rowproj_buffer
 from .ppo import gae, gae_workspace
 
 
@@ -41,9 +42,10 @@ class Trajectory:
 
 
 class RolloutEngine:
-    def __init__(self, env, policy, horizon, want_info=True, bootstrap=True, seed=0, normalize=True):
+    def __init__(self, env, policy, horizon, want_info=True, bootstrap=True, seed=0, normalize=True, row_cache=True):
         """normalize=False leaves the advantages raw after GAE: a data-parallel caller normalises
-        them with the moments of the whole gathered batch in gather() (ppo.py:94)."""
+        them with the moments of the whole gathered batch in gather() (ppo.py:94).
+        row_cache=False runs every step on the full-window forward (uavhip_policy_forward)."""
         self.env = env
         self.normalize = normalize
         self.iteration = 0
@@ -54,6 +56,9 @@ class RolloutEngine:
         self.seed = int(seed)
         self.traj = Trajectory(self.T, env.E, env.device, want_info)
         self.counter = torch.zeros(1, dtype=torch.int64, device=env.device)  # sampling counter base
+        # window-row projections of the obs windows (policy.rowproj_buffer): the windows of one
+        # iteration are one deque sequence, so step t projects only its new row (rebuilt at t = 0)
+        self.rowproj = rowproj_buffer(env.E, env.device) if row_cache else None
         self.graph = None
         self.policy_events = None   # [(start, end)] HIP events around each policy launch (optional)
         self.env_events = None
@@ -70,7 +75,8 @@ class RolloutEngine:
         if ev is not None:
             ev[t][0].record()
         self.policy.fused_forward(obs, action_out=actions, logp=logp, value=value, seed=self.seed,
-                                  offset=t * self.env.E, offset_dev=self.counter, check_weights=False)
+                                  offset=t * self.env.E, offset_dev=self.counter, check_weights=False,
+                                  rowproj=self.rowproj, step=t, fill=t == 0)
         if ev is not None:
             ev[t][1].record()
 

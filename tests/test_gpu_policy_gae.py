@@ -24,6 +24,62 @@ def _load_policy(policy_npz, tag):
 
 
 @pytest.mark.parametrize("tag", ["a", "b"])
+def test_row_projection_forward_vs_reference(policy_npz, tag):
+    """uavhip_policy_forward_rows with fill (every window's rows projected afresh) against the
+    reference's outputs on the golden windows, at the full-forward tolerance."""
+    from uavhip.policy import rowproj_buffer
+    net = _load_policy(policy_npz, tag)
+    x = torch.from_numpy(policy_npz["states"]).cuda()
+    a = torch.from_numpy(policy_npz["actions"]).cuda()
+    B = x.shape[0]
+    ent = torch.empty(B, device="cuda")
+    lg = torch.empty(B, 2, device="cuda")
+    _, logp, value, ent, lg = net.fused_forward(x, actions=a, entropy=ent, logits=lg, rowproj=rowproj_buffer(B),
+                                                step=3, fill=True)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(lg.cpu().numpy(), policy_npz[f"{tag}/logits"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(logp.cpu().numpy(), policy_npz[f"{tag}/logp"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(ent.cpu().numpy(), policy_npz[f"{tag}/entropy"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(value.cpu().numpy(), policy_npz[f"{tag}/value"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("B,step0", [(200, 0), (4096, 7)])
+def test_row_projection_sequence(B, step0):
+    """A deque window sequence (oracle.windows restatement: shifts, episode ends -> zero padding)
+    through the ring: each step projects only its new row. Bitwise equal to rebuilding every
+    window's rows at every step (fill), and within fp32 rounding of the full forward."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle.windows import windows_from_rows
+    from uavhip.policy import TransformerActorCritic, rowproj_buffer
+    torch.manual_seed(2)
+    net = TransformerActorCritic().cuda()
+    T = 12
+    g = np.random.default_rng(B)
+    first = g.standard_normal((B, 5, 14)).astype(np.float32)
+    first[: B // 3, :3] = 0
+    first[B // 3: B // 2, :4] = 0
+    rows = g.standard_normal((T, B, 14)).astype(np.float32)
+    dones = g.random((T, B)) < 0.15
+    wins = torch.from_numpy(windows_from_rows(first, rows, dones)).cuda()
+    acts = torch.from_numpy((g.random((T, B)) < 0.5).astype(np.int8)).cuda()
+    ring, fresh = rowproj_buffer(B), rowproj_buffer(B)
+    for t in range(T):
+        outs = []
+        for buf, fill in ((ring, t == 0), (fresh, True), (None, False)):
+            lg = torch.empty(B, 2, device="cuda")
+            kw = dict(rowproj=buf, step=step0 + t, fill=fill) if buf is not None else {}
+            _, lp, v, _, lg = net.fused_forward(wins[t], actions=acts[t], logits=lg, **kw)
+            outs.append((lg, lp, v))
+        torch.cuda.synchronize()
+        for x, y in zip(outs[0], outs[1]):
+            assert torch.equal(x, y), f"step {t}: ring != fill"
+        for x, y in zip(outs[0], outs[2]):
+            torch.testing.assert_close(x, y, rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("tag", ["a", "b"])
 def test_fused_policy_vs_reference(policy_npz, tag):
     net = _load_policy(policy_npz, tag)
     x = torch.from_numpy(policy_npz["states"]).cuda()
@@ -245,6 +301,28 @@ def test_compact_exchange_rebuilds_rollout_windows():
     got = udist.unpack_compact(pay, T, E)["obs"].reshape(2, T, E, 5, 14).cpu().numpy()
     for b in range(2):
         np.testing.assert_array_equal(got[b], windows_from_rows(first[b].numpy(), rows[b].numpy(), dn[b].numpy()))
+
+
+def test_rollout_row_cache_matches_full_forward():
+    """The rollout's window-row path (every step after t = 0 projects one row) against the
+    full-window forward on the recorded windows and actions: logp / value within fp32 rounding."""
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.rollout import RolloutEngine
+    from uavhip.vec_env import VecUAVEnv
+    torch.manual_seed(0)
+    E, T = 256, 24
+    env = VecUAVEnv(E, 4, 6, 1, 1, seed=9)
+    pol = TransformerActorCritic().cuda()
+    eng = RolloutEngine(env, pol, T, seed=3)
+    eng.start()
+    for _ in range(2):
+        tr = eng.collect()
+        assert tr.dones.any()
+        x = tr.obs[:T].reshape(-1, 5, 14)
+        _, lp, v, _, _ = pol.fused_forward(x, actions=tr.actions.reshape(-1))
+        torch.cuda.synchronize()
+        torch.testing.assert_close(lp, tr.logp.reshape(-1), rtol=1e-5, atol=2e-6)
+        torch.testing.assert_close(v, tr.values.reshape(-1), rtol=1e-5, atol=2e-6)
 
 
 def test_rollout_graph_replay_matches_eager():
