@@ -8,10 +8,11 @@ normalisation, and with N > 1 GPUs the RCCL all-gather of the trajectories (SURV
 value = E * T * K * N / max-over-ranks wall time. Inputs (scenes, windows) are resident in HBM.
 
 Also reported (same JSON line):
-  roofline      dominant kernel = k_policy_forward, MFMA fp32 peak, algorithmic FLOP per launch of
-                the path the rollout runs (window-row ring: 1,790,848 FLOP/sample; the full-window
-                forward is 2,446,208) x E / its average HIP-event duration over the
-                timed region
+  roofline      dominant kernel = k_policy_forward, MFMA fp32 peak; achieved = ALGORITHMIC FLOP per
+                launch (2,446,208 FLOP/sample, the last-token-pruned forward of one
+                window) x E / its average HIP-event duration over the timed region. The rollout's
+                window-row ring reuses layer-0 Q/K/V of rows 0-3 from earlier steps, so it EXECUTES
+                1,790,848 FLOP/sample; that rate is reported beside it (executed_*)
   env_roofline  k_env_step against HBM, algorithmic 24*M + 490 B per env-step
   env_fused     env-only K2 with T = 256 steps per launch (state in registers): BASELINE configs[1]
                 (1024 envs x 8 x 16) and the headline shape, env-steps/s and algorithmic GB/s
@@ -54,7 +55,7 @@ def profiled_traffic(kernel):
         return None, None
     d = json.load(open(files[-1]))
     for k, v in d.get("pmc", {}).items():
-        if k.endswith(kernel) and "hbm_bytes_per_launch" in v:
+        if k.replace("uavhip::pol::", "").replace("uavhip::", "") == kernel and "hbm_bytes_per_launch" in v:
             return v["hbm_bytes_per_launch"], os.path.basename(files[-1])
     return None, None
 
@@ -293,8 +294,9 @@ def main():
     pol_list, env_list = eng.event_ms()   # the last timed iteration's T+1 policy and T env launches
     pol_ms = float(np.mean(pol_list))
     env_ms = float(np.mean(env_list))
-    flop_sample = ROWS_FLOP_PER_SAMPLE if eng.rowproj is not None else POLICY_FLOP_PER_SAMPLE
-    achieved_tf = flop_sample * E / (pol_ms * 1e-3) / 1e12
+    flop_exec = ROWS_FLOP_PER_SAMPLE if eng.rowproj is not None else POLICY_FLOP_PER_SAMPLE
+    achieved_tf = POLICY_FLOP_PER_SAMPLE * E / (pol_ms * 1e-3) / 1e12
+    exec_tf = flop_exec * E / (pol_ms * 1e-3) / 1e12
     env_gbs = env_bytes_per_step(args.targets) * E / (env_ms * 1e-3) / 1e9
 
     env_fused = None
@@ -313,8 +315,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, policy.state_dict(), args.cpu_seconds)
 
-    pol_traffic, pol_src = profiled_traffic("k_policy_forward")
-    env_traffic, _ = profiled_traffic("k_env_step<1>")
+    pol_kernel = "k_policy_forward<false, true>" if eng.rowproj is not None else "k_policy_forward<false>"
+    pol_traffic, pol_src = profiled_traffic(pol_kernel)
+    env_traffic, _ = profiled_traffic("k_env_step<1, false>")
     if rank == 0:
         line = {
             "metric": "env-steps/sec (whole node), full PPO rollout, 4096 envs x 16 UAV x 32 tgt per GPU",
@@ -327,10 +330,13 @@ def main():
                        "envs_per_gpu": E, "uavs": args.uavs, "targets": args.targets, "horizon": T,
                        "env_steps_per_step": E * T * world, "parallelism": f"env-sharded x{world}",
                        "full_reset_period": 200, "launch": mode},
-            "roofline": {"kernel": "k_policy_forward", "bound": "mfma", "achieved": achieved_tf,
+            "roofline": {"kernel": pol_kernel, "bound": "mfma", "achieved": achieved_tf,
                          "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / MFMA_F32_PEAK_TFLOPS,
                          "traffic": pol_traffic, "traffic_unit": "bytes/launch (PMC)", "traffic_source": pol_src,
-                         "avg_launch_ms": pol_ms, "flop_per_launch": flop_sample * E,
+                         "avg_launch_ms": pol_ms, "flop_per_launch": POLICY_FLOP_PER_SAMPLE * E,
+                         "flop_per_launch_source": "SURVEY.md 8(d): 2,446,208 FLOP/sample x E",
+                         "executed_flop_per_launch": flop_exec * E, "executed_achieved": exec_tf,
+                         "executed_frac": exec_tf / MFMA_F32_PEAK_TFLOPS,
                          "path": "window-row ring (layer-0 in_proj of the new row only)" if eng.rowproj is not None
                          else "full window",
                          "timing": "HIP events around each of the T+1 launches of the last timed iteration"},
