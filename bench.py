@@ -15,7 +15,9 @@ Also reported (same JSON line):
                 1,790,848 FLOP/sample; that rate is reported beside it (executed_*)
   env_roofline  k_env_step against HBM, algorithmic 24*M + 490 B per env-step
   env_fused     env-only K2 with T = 256 steps per launch (state in registers): BASELINE configs[1]
-                (1024 envs x 8 x 16) and the headline shape, env-steps/s and algorithmic GB/s
+                (1024 envs x 8 x 16) and the headline shape, env-steps/s and algorithmic GB/s; and
+                BASELINE configs[4]'s per-GPU shard (8192 envs x 64 x 128, fp16 obs, T = 64)
+  score_pairs   K1 (LDS-tiled pair scoring) over 8192 fresh 64 x 128 scenes (configs[4])
   ppo_samples_per_s  one PPO update (5 epochs) over the iteration's batch on the HIP training step
                 (uavhip_ppo_step); N > 1: over the all-gathered batch, data parallel (each rank a
                 1/N slice of every global minibatch, RCCL all-reduce of loss sums and gradients)
@@ -129,17 +131,18 @@ def cpu_baseline(args, state_dict, seconds):
                       f"policy forward ({cores} threads) + C oracle UAVEnv.step (1 thread) + numpy GAE"}
 
 
-def env_fused_rate(E, N, M, T, dev, reps=5):
+def env_fused_rate(E, N, M, T, dev, reps=5, obs_dtype=torch.float32):
     """Env-only K2 (BASELINE configs[1] shape): one launch steps E envs T times with state in
     registers (Bernoulli(0.5) actions drawn on device beforehand, auto-reset, obs / reward / done /
-    info written every step). Returns env-steps/s and algorithmic GB/s (SURVEY 8d units)."""
+    info written every step). Returns env-steps/s and algorithmic GB/s (SURVEY 8d units; fp16 obs
+    write 140 B instead of 280 B per env-step)."""
     from uavhip.vec_env import VecUAVEnv
-    env = VecUAVEnv(E, N, M, 1, 1, seed=77, full_reset_period=200)
+    env = VecUAVEnv(E, N, M, 1, 1, seed=77, full_reset_period=200, obs_dtype=obs_dtype)
     env.generate_scenes()
     env.reset(episode=1)
     g = torch.Generator(device=dev).manual_seed(5)
     acts = torch.randint(0, 2, (T, E), generator=g, device=dev, dtype=torch.int8)
-    obs = torch.empty(T, E, 5, 14, device=dev)
+    obs = torch.empty(T, E, 5, 14, device=dev, dtype=obs_dtype)
     rew = torch.empty(T, E, dtype=torch.float64, device=dev)
     done = torch.empty(T, E, dtype=torch.uint8, device=dev)
     info = torch.empty(T, E, 8, dtype=torch.float64, device=dev)
@@ -157,10 +160,36 @@ def env_fused_rate(E, N, M, T, dev, reps=5):
         ms.append(e0.elapsed_time(e1))
     t = float(np.median(ms)) * 1e-3
     rate = E * T / t
-    gbs = env_bytes_per_step(M) * rate / 1e9
-    return {"workload": f"{E} envs x {N} UAV x {M} tgt, {T} fused steps per launch", "value": rate,
-            "unit": "env-steps/s", "ms_per_launch": t * 1e3, "achieved": gbs, "peak": HBM_PEAK_GBS,
-            "unit_roofline": "GB/s (algorithmic 24*M + 490 B per env-step)", "frac": gbs / HBM_PEAK_GBS}
+    f16 = obs_dtype == torch.float16
+    bps = env_bytes_per_step(M) - (140 if f16 else 0)
+    gbs = bps * rate / 1e9
+    return {"workload": f"{E} envs x {N} UAV x {M} tgt, {T} fused steps per launch" + (", fp16 obs" if f16 else ""),
+            "value": rate, "unit": "env-steps/s", "ms_per_launch": t * 1e3, "achieved": gbs, "peak": HBM_PEAK_GBS,
+            "unit_roofline": f"GB/s (algorithmic 24*M + {490 - 140 * f16} B per env-step)", "frac": gbs / HBM_PEAK_GBS}
+
+
+def score_pairs_rate(E, N, M, dev, reps=5):
+    """K1 (LDS-tiled pair scoring, one workgroup per env) over E fresh scenes: pairs/s and the
+    algorithmic 8 + 48/M + 40/N B per pair + 8 B per UAV against HBM. fp64-VALU bound
+    (acos + 2 exp + sqrt + 3 divisions per pair)."""
+    from uavhip.vec_env import VecUAVEnv
+    env = VecUAVEnv(E, N, M, 1, 1, seed=78, full_reset_period=0)
+    env.generate_scenes()
+    env.score_pairs()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ms = []
+    for _ in range(reps):
+        e0.record()
+        env.score_pairs()
+        e1.record()
+        torch.cuda.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    t = float(np.median(ms)) * 1e-3
+    pairs = E * N * M
+    gbs = (pairs * (8 + 48 / M + 40 / N) + 8 * E * N) / t / 1e9
+    return {"workload": f"K1 score_pairs, {E} envs x {N} UAV x {M} tgt", "value": pairs / t, "unit": "pairs/s",
+            "ms_per_launch": t * 1e3, "achieved": gbs, "peak": HBM_PEAK_GBS,
+            "unit_roofline": "GB/s (algorithmic 8 + 48/M + 40/N B per pair + 8 B per UAV)", "frac": gbs / HBM_PEAK_GBS}
 
 
 def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
@@ -299,9 +328,11 @@ def main():
     exec_tf = flop_exec * E / (pol_ms * 1e-3) / 1e12
     env_gbs = env_bytes_per_step(args.targets) * E / (env_ms * 1e-3) / 1e9
 
-    env_fused = None
+    env_fused = stress = None
     if rank == 0 and world == 1 and not args.no_env_fused:
-        env_fused = [env_fused_rate(1024, 8, 16, 256, dev), env_fused_rate(E, args.uavs, args.targets, 256, dev)]
+        env_fused = [env_fused_rate(1024, 8, 16, 256, dev), env_fused_rate(E, args.uavs, args.targets, 256, dev),
+                     env_fused_rate(8192, 64, 128, 64, dev, obs_dtype=torch.float16)]
+        stress = score_pairs_rate(8192, 64, 128, dev)
 
     ppo = None
     if not args.no_ppo:
@@ -345,6 +376,7 @@ def main():
                              "traffic": env_traffic,
                              "bytes_per_env_step": env_bytes_per_step(args.targets)},
             "env_fused": env_fused,
+            "score_pairs": stress,
             "ppo_samples_per_s": ppo,
             "cpu_baseline": cpu,
         }

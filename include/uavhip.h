@@ -38,6 +38,9 @@ typedef void* uavhip_stream_t; /* hipStream_t */
 #define UAVHIP_MAX_OBSTACLES 8
 /* uavhip_env.flags */
 #define UAVHIP_ENV_ONE_PER_WAVE 1  /* multi-step launches: never pack two envs into one wave */
+#define UAVHIP_ENV_OBS_F16 2       /* obs_out of uavhip_env_reset / uavhip_env_step is IEEE binary16
+                                      (round-to-nearest-even of the f32 window; BASELINE config 4)
+                                      instead of f32; the env's own window stays f32          */
 
 enum uavhip_status {
     UAVHIP_OK = 0,

@@ -74,6 +74,38 @@ __device__ __forceinline__ double dist_score(double d, double zeta) {
     return exp(-(q * q));
 }
 
+// Per-UAV terms of angle_score / speed_score every pair of the UAV reuses: speed and unit heading
+// ([1, 0] when the UAV is still, mechanics.py:37-41).
+__device__ __forceinline__ void uav_heading(double uvx, double uvy, double& us, double& hx, double& hy) {
+    us = norm2(uvx, uvy);
+    hx = 1.0;
+    hy = 0.0;
+    if (!(us < 1e-6)) { hx = uvx / us; hy = uvy / us; }
+}
+
+// calc_damage_prob from the per-UAV (us, hx, hy, load) and per-target (ts) terms: the same fp64
+// operations as damage_prob below (|p_u - p_t| and |p_t - p_u| round identically), so bitwise.
+__device__ __forceinline__ double damage_prob_pre(double upx, double upy, double us, double hx, double hy,
+                                                  double load, double tpx, double tpy, double ts, const double* prm) {
+    const double vx = tpx - upx, vy = tpy - upy;
+    const double dist = norm2(vx, vy);
+    double ea = 1.0;
+    if (!(dist < 1e-6)) {
+        const double nx = vx / dist, ny = vy / dist;
+        const double c = nx * hx + ny * hy;
+        const double sigma = acos(clipd(c, -1.0, 1.0));
+        double b = 0.002 * dist;
+        if (b < 1e-6) b = 1e-6;
+        const double q = sigma / (b * M_PI);
+        ea = exp(-(q * q));
+    }
+    const double ed = dist_score(dist, prm[UAVHIP_PRM_ZETA_D]);
+    const double es = speed_score(us, ts, prm[UAVHIP_PRM_K]);
+    const double term = prm[UAVHIP_PRM_C1] * ed + prm[UAVHIP_PRM_C2] * es;
+    const double p = ea * term * load;
+    return clipd(p, 0.0, 1.0);
+}
+
 // mechanics.py:93-114 calc_damage_prob
 __device__ __forceinline__ double damage_prob(double upx, double upy, double uvx, double uvy, double load,
                                               double tpx, double tpy, double tvx, double tvy, const double* prm) {

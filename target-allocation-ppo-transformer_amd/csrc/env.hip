@@ -2,8 +2,8 @@
 // generation / refresh, reset, K2 fused step. Reference: envs/uav_env.py, envs/mechanics.py,
 // envs/entities.py. Device building blocks: env_device.hpp.
 //
-//  * K1: one thread per (env, uav, target) pair over the whole batch + one per (env, uav) for
-//    p_pen (which never depends on the target, mechanics.py:118). fp64 VALU.
+//  * K1: one workgroup per env, entity records + per-entity terms staged in LDS, pairs scored from
+//    LDS with coalesced p_dmg stores; p_pen (target-independent, mechanics.py:118) per UAV. fp64 VALU.
 //  * reset / step / generate / refresh: one wave per env (env_device.hpp).
 //  * K2 keeps the whole env state in registers across T fused steps; T = 1 is the per-step
 //    rollout call, T > 1 the env-only multi-step launch (BASELINE config 2). It never generates a
@@ -22,34 +22,53 @@ constexpr int kBlock = kWavesPerBlock * kWave;
 }  // namespace
 
 // ================================================================== K1: pair tables (active buffer)
-__global__ __launch_bounds__(256) void k_score_pairs(uavhip_env env, const uint8_t* __restrict__ mask) {
-    const int N = env.N, M = env.M;
-    const long long npairs = (long long)env.E * N * M;
-    const long long nuav = (long long)env.E * N;
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < npairs + nuav; i += stride) {
-        const bool pair = i < npairs;
-        const int e = pair ? (int)(i / ((long long)N * M)) : (int)((i - npairs) / N);
-        if (mask && !mask[e]) continue;
-        const int sel = env.scene_buffers == 2 ? (env.istate[(long long)e * UAVHIP_IST_COUNT + UAVHIP_IST_SCENE_SEL] & 1) : 0;
-        const long long sb = (long long)sel * env.E + e;
-        if (pair) {
-            const int r = (int)(i - (long long)e * N * M);
-            const int u = r / M, t = r - u * M;
-            const double* up = env.uav_pos + 2 * (sb * N + u);
-            const double* uv = env.uav_vel + 2 * (sb * N + u);
-            const double* tp = env.tgt_pos + 2 * (sb * M + t);
-            const double* tv = env.tgt_vel + 2 * (sb * M + t);
-            env.p_dmg[sb * N * M + r] =
-                damage_prob(up[0], up[1], uv[0], uv[1], env.uav_load[sb * N + u], tp[0], tp[1], tv[0], tv[1], env.prm);
-        } else {
-            const int u = (int)(i - npairs - (long long)e * N);
-            const double* up = env.uav_pos + 2 * (sb * N + u);
-            const double* uv = env.uav_vel + 2 * (sb * N + u);
-            env.p_pen[sb * N + u] = penetration_prob(up[0], up[1], uv[0], uv[1], env.nfz_pos + 2 * sb * env.Kn, env.Kn,
-                                                     env.icp_pos + 2 * sb * env.Ki, env.icp_vel + 2 * sb * env.Ki,
-                                                     env.Ki, env.prm);
-        }
+// One workgroup per env (LDS-tiled pairwise scoring, BASELINE config 4): the env's UAV and target
+// records are staged in LDS once together with the per-entity terms every pair reuses (UAV speed +
+// unit heading, target speed: uav_heading), then the N x M pairs are scored from LDS broadcasts
+// with coalesced p_dmg stores (p_dmg[e] is one contiguous N*M run); p_pen (target-independent,
+// mechanics.py:118) by one thread per UAV. damage_prob_pre performs damage_prob's fp64 operations,
+// so the tables are bitwise those of the per-wave scene scorer (score_scene_wave).
+constexpr int kScoreThreads = 256;
+static_assert(UAVHIP_MAX_N + UAVHIP_MAX_M <= kScoreThreads, "one staging thread per entity");
+__global__ __launch_bounds__(kScoreThreads) void k_score_pairs(uavhip_env env, const uint8_t* __restrict__ mask) {
+    __shared__ double s_u[6][UAVHIP_MAX_N];  // pos x, pos y, heading x, heading y, speed, load
+    __shared__ double s_t[3][UAVHIP_MAX_M];  // pos x, pos y, speed
+    const int e = blockIdx.x;
+    if (mask && !mask[e]) return;
+    const int N = env.N, M = env.M, tid = threadIdx.x;
+    const int sel = env.scene_buffers == 2 ? (env.istate[(long long)e * UAVHIP_IST_COUNT + UAVHIP_IST_SCENE_SEL] & 1) : 0;
+    const long long sb = (long long)sel * env.E + e;
+    if (tid < N) {
+        const double* up = env.uav_pos + 2 * (sb * N + tid);
+        const double* uv = env.uav_vel + 2 * (sb * N + tid);
+        double us, hx, hy;
+        uav_heading(uv[0], uv[1], us, hx, hy);
+        s_u[0][tid] = up[0];
+        s_u[1][tid] = up[1];
+        s_u[2][tid] = hx;
+        s_u[3][tid] = hy;
+        s_u[4][tid] = us;
+        s_u[5][tid] = env.uav_load[sb * N + tid];
+        env.p_pen[sb * N + tid] = penetration_prob(up[0], up[1], uv[0], uv[1], env.nfz_pos + 2 * sb * env.Kn, env.Kn,
+                                                   env.icp_pos + 2 * sb * env.Ki, env.icp_vel + 2 * sb * env.Ki,
+                                                   env.Ki, env.prm);
+    } else if (tid - UAVHIP_MAX_N < M && tid >= UAVHIP_MAX_N) {
+        const int t = tid - UAVHIP_MAX_N;
+        const double* tp = env.tgt_pos + 2 * (sb * M + t);
+        const double* tv = env.tgt_vel + 2 * (sb * M + t);
+        s_t[0][t] = tp[0];
+        s_t[1][t] = tp[1];
+        s_t[2][t] = norm2(tv[0], tv[1]);
+    }
+    __syncthreads();
+    double prm[UAVHIP_PRM_COUNT];
+#pragma unroll
+    for (int k = 0; k < UAVHIP_PRM_COUNT; ++k) prm[k] = env.prm[k];
+    double* out = env.p_dmg + sb * N * M;
+    for (int i = tid; i < N * M; i += kScoreThreads) {
+        const int u = i / M, t = i - u * M;
+        out[i] = damage_prob_pre(s_u[0][u], s_u[1][u], s_u[4][u], s_u[2][u], s_u[3][u], s_u[5][u], s_t[0][t],
+                                 s_t[1][t], s_t[2][t], prm);
     }
 }
 
@@ -82,7 +101,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(uavhip_env env, const int8_
         for (int i = 0; i < na; ++i) {
             const long long se = (long long)(s0 + i) * E + e;
             step_once<TPL, LT>(R, env, e, lane, (int)((abits >> i) & 1ull), auto_reset,
-                               obs_out ? obs_out + se * kObs : nullptr, reward_out ? reward_out + se : nullptr,
+                               obs_out ? obs_at(obs_out, se, obs_f16(env)) : nullptr, reward_out ? reward_out + se : nullptr,
                                done_out ? done_out + se : nullptr,
                                info_out ? info_out + se * UAVHIP_INFO_COUNT : nullptr);
         }
@@ -115,7 +134,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step_g(uavhip_env env, const int
         for (int i = 0; i < na; ++i) {
             const long long se = (long long)(s0 + i) * E + e;
             envgrp::gstep(R, env, e, j, (int)((abits >> i) & 1u), auto_reset,
-                          obs_out ? obs_out + se * kObs : nullptr, reward_out ? reward_out + se : nullptr,
+                          obs_out ? obs_at(obs_out, se, obs_f16(env)) : nullptr, reward_out ? reward_out + se : nullptr,
                           done_out ? done_out + se : nullptr, info_out ? info_out + se * UAVHIP_INFO_COUNT : nullptr);
         }
     }
@@ -142,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void k_env_reset(uavhip_env env, const uint
     R.err = 0;
     reset_regs(R, env, lane);
     store_regs(R, env, e, lane);
-    if (obs_out) write_obs(obs_out + (long long)e * kObs, R.w0, R.w1, lane);
+    if (obs_out) write_obs(obs_at(obs_out, e, obs_f16(env)), R.w0, R.w1, lane, obs_f16(env));
 }
 
 // Fresh scene(s) for masked envs: the active buffer, plus the spare when double-buffered.
@@ -242,10 +261,7 @@ using namespace uavhip;
 extern "C" int uavhip_score_pairs(const uavhip_env* env, const uint8_t* mask, uavhip_stream_t stream) {
     int rc = validate(env, false);
     if (rc) return rc;
-    const long long work = (long long)env->E * env->N * (env->M + 1);
-    long long blocks = (work + 255) / 256;
-    if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(k_score_pairs, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *env, mask);
+    hipLaunchKernelGGL(k_score_pairs, dim3(env->E), dim3(kScoreThreads), 0, (hipStream_t)stream, *env, mask);
     return check_launch("k_score_pairs");
 }
 

@@ -436,9 +436,21 @@ __device__ void store_regs(const EnvRegs<TPL>& R, const uavhip_env& env, int e, 
     if (lane < kObs - kWave) w[kWave + lane] = R.w1;
 }
 
-__device__ __forceinline__ void write_obs(float* o, float w0, float w1, int lane) {
-    o[lane] = w0;
-    if (lane < kObs - kWave) o[kWave + lane] = w1;
+// obs_out element type: f32, or IEEE binary16 (round to nearest even of the f32 window) under
+// UAVHIP_ENV_OBS_F16 (BASELINE config 4: fp16 obs; the env's own window stays f32)
+__device__ __forceinline__ bool obs_f16(const uavhip_env& env) { return (env.flags & UAVHIP_ENV_OBS_F16) != 0; }
+__device__ __forceinline__ float* obs_at(float* base, long long i, bool h) {
+    return h ? reinterpret_cast<float*>(reinterpret_cast<_Float16*>(base) + i * kObs) : base + i * kObs;
+}
+__device__ __forceinline__ void write_obs(float* o, float w0, float w1, int lane, bool h) {
+    if (h) {
+        _Float16* q = reinterpret_cast<_Float16*>(o);
+        q[lane] = (_Float16)w0;
+        if (lane < kObs - kWave) q[kWave + lane] = (_Float16)w1;
+    } else {
+        o[lane] = w0;
+        if (lane < kObs - kWave) o[kWave + lane] = w1;
+    }
 }
 
 // uav_env.py:369-433 diagnostics. The reference re-sums p_dmg / p_final over all locked pairs in
@@ -471,7 +483,7 @@ __device__ void step_once(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lan
     const int N = env.N, M = env.M;
     if (R.u >= N) {  // stepping a finished env: the reference raises IndexError (:296)
         R.err |= 1;
-        if (obs_o) write_obs(obs_o, 0.0f, 0.0f, lane);
+        if (obs_o) write_obs(obs_o, 0.0f, 0.0f, lane, obs_f16(env));
         if (lane == 0) {
             if (rew_o) *rew_o = 0.0;
             if (done_o) *done_o = 1;
@@ -551,7 +563,7 @@ __device__ void step_once(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lan
     if (!done) {
         load_cur_pair<TPL, LT>(R, env);
         push_obs(R, lane);
-        if (obs_o) write_obs(obs_o, R.w0, R.w1, lane);
+        if (obs_o) write_obs(obs_o, R.w0, R.w1, lane, obs_f16(env));
     } else if (auto_reset) {
         R.ep += 1;
         const int P = env.full_reset_period;
@@ -568,9 +580,9 @@ __device__ void step_once(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lan
             }
         }
         reset_regs<TPL, LT>(R, env, lane, flipped);
-        if (obs_o) write_obs(obs_o, R.w0, R.w1, lane);
+        if (obs_o) write_obs(obs_o, R.w0, R.w1, lane, obs_f16(env));
     } else {
-        if (obs_o) write_obs(obs_o, 0.0f, 0.0f, lane);  // _get_obs returns zeros when done (:188-189)
+        if (obs_o) write_obs(obs_o, 0.0f, 0.0f, lane, obs_f16(env));  // _get_obs returns zeros when done (:188-189)
     }
 }
 

@@ -129,10 +129,18 @@ __device__ void gpush_obs(GRegs& R, int j) {
     R.w2 = j < kObs - 2 * L ? w[16 + 2 * L + j] : 0.0f;
 }
 
-__device__ __forceinline__ void gwrite_obs(float* o, const GRegs& R, int j, bool zero) {
-    o[j] = zero ? 0.0f : R.w0;
-    o[L + j] = zero ? 0.0f : R.w1;
-    if (j < kObs - 2 * L) o[2 * L + j] = zero ? 0.0f : R.w2;
+__device__ __forceinline__ void gwrite_obs(float* o, const GRegs& R, int j, bool zero, bool h) {
+    const float a = zero ? 0.0f : R.w0, b = zero ? 0.0f : R.w1, c = zero ? 0.0f : R.w2;
+    if (h) {  // UAVHIP_ENV_OBS_F16
+        _Float16* q = reinterpret_cast<_Float16*>(o);
+        q[j] = (_Float16)a;
+        q[L + j] = (_Float16)b;
+        if (j < kObs - 2 * L) q[2 * L + j] = (_Float16)c;
+    } else {
+        o[j] = a;
+        o[L + j] = b;
+        if (j < kObs - 2 * L) o[2 * L + j] = c;
+    }
 }
 
 __device__ void gwrite_info(const GRegs& R, double is_valid, double* o, int j) {
@@ -262,7 +270,7 @@ __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int 
     const int N = env.N, M = env.M;
     if (R.u >= N) {  // stepping a finished env: the reference raises IndexError (:296)
         R.err |= 1;
-        if (obs_o) gwrite_obs(obs_o, R, j, true);
+        if (obs_o) gwrite_obs(obs_o, R, j, true, obs_f16(env));
         if (j == 0) {
             if (rew_o) *rew_o = 0.0;
             if (done_o) *done_o = 1;
@@ -338,7 +346,7 @@ __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int 
     if (!done) {
         gload_cur_pair(R, env);
         gpush_obs(R, j);
-        if (obs_o) gwrite_obs(obs_o, R, j, false);
+        if (obs_o) gwrite_obs(obs_o, R, j, false, obs_f16(env));
     } else if (auto_reset) {
         R.ep += 1;
         const int P = env.full_reset_period;
@@ -355,9 +363,9 @@ __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int 
             }
         }
         greset_regs(R, env, j, flipped);
-        if (obs_o) gwrite_obs(obs_o, R, j, false);
+        if (obs_o) gwrite_obs(obs_o, R, j, false, obs_f16(env));
     } else {
-        if (obs_o) gwrite_obs(obs_o, R, j, true);  // _get_obs returns zeros when done (:188-189)
+        if (obs_o) gwrite_obs(obs_o, R, j, true, obs_f16(env));  // _get_obs returns zeros when done (:188-189)
     }
 }
 

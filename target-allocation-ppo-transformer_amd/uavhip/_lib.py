@@ -14,6 +14,7 @@ SEQ_LEN = 5
 STATE_DIM = 14
 OBS_FLOATS = SEQ_LEN * STATE_DIM
 MAX_N, MAX_M, MAX_OBSTACLES = 64, 128, 8
+ENV_ONE_PER_WAVE, ENV_OBS_F16 = 1, 2  # uavhip_env.flags bits
 
 PRM = dict(ZETA_D=0, K=1, C1=2, C2=3, C3=4, C4=5, OMEGA=6, ZETA_OBS=7)
 PRM_COUNT = 8

@@ -18,8 +18,13 @@ SCENE_KEYS_F64 = ("uav_pos", "uav_vel", "uav_load", "uav_cost", "tgt_pos", "tgt_
 
 class VecUAVEnv:
     def __init__(self, num_envs, num_uavs=None, num_targets=None, num_nfz=None, num_interceptors=None, config=None,
-                 device="cuda", seed=0, full_reset_period=None, scene_buffers=None):
+                 device="cuda", seed=0, full_reset_period=None, scene_buffers=None, obs_dtype=torch.float32):
+        """obs_dtype: float32, or float16 (BASELINE config 4: observations emitted as IEEE binary16,
+        UAVHIP_ENV_OBS_F16; the env's own window deque stays f32)."""
         c = config or default_cfg
+        if obs_dtype not in (torch.float32, torch.float16):
+            raise ValueError(f"obs_dtype must be torch.float32 or torch.float16 (got {obs_dtype})")
+        self.obs_dtype = obs_dtype
         self.cfg = c
         self.E = int(num_envs)
         self.N = int(num_uavs if num_uavs is not None else c.NUM_UAVS)
@@ -58,6 +63,7 @@ class VecUAVEnv:
         d.full_reset_period = period
         d.scene_buffers = B
         d.seed = int(seed) & (2 ** 64 - 1)
+        d.flags = _lib.ENV_OBS_F16 if obs_dtype == torch.float16 else 0
         for i, v in enumerate(params_vector(c)):
             d.prm[i] = float(v)
         for i, v in enumerate(gen_vector(c)):
@@ -68,7 +74,7 @@ class VecUAVEnv:
             setattr(d, name, getattr(self, name).data_ptr())
         self.desc = d
         # per-step output buffers (reused; [E] views of the T=1 case)
-        self._obs = torch.zeros(E, _lib.SEQ_LEN, _lib.STATE_DIM, dtype=torch.float32, device=self.device)
+        self._obs = torch.zeros(E, _lib.SEQ_LEN, _lib.STATE_DIM, dtype=obs_dtype, device=self.device)
         self._rew = torch.zeros(E, **f64)
         self._done = torch.zeros(E, dtype=torch.uint8, device=self.device)
         self._info = torch.zeros(E, _lib.INFO_COUNT, **f64)
@@ -132,7 +138,12 @@ class VecUAVEnv:
         check(LIB.uavhip_scene_refresh(self.desc, stream_handle()), "uavhip_scene_refresh")
 
     # ------------------------------------------------------------------ reset / step
+    def _check_obs(self, obs):
+        if obs is not None and obs.dtype != self.obs_dtype:
+            raise TypeError(f"obs_out must be {self.obs_dtype} (got {obs.dtype})")
+
     def reset(self, mask=None, episode=-1, obs_out=None):
+        self._check_obs(obs_out)
         out = self._obs if obs_out is None else obs_out
         check(LIB.uavhip_env_reset(self.desc, ptr(mask), int(episode), ptr(out), stream_handle()), "uavhip_env_reset")
         return out
@@ -141,6 +152,7 @@ class VecUAVEnv:
              want_info=True):
         """actions: int8 tensor [E] (one step) or [T, E] (T fused steps). Returns (obs, reward,
         done, info) device tensors shaped [E, ...] or [T, E, ...]."""
+        self._check_obs(obs_out)
         if actions.dtype != torch.int8 or actions.device != self.device:
             actions = actions.to(device=self.device, dtype=torch.int8)
         actions = actions.contiguous()
@@ -156,7 +168,7 @@ class VecUAVEnv:
         else:
             dev = self.device
             obs = obs_out if obs_out is not None else torch.empty(*lead, _lib.SEQ_LEN, _lib.STATE_DIM,
-                                                                  dtype=torch.float32, device=dev)
+                                                                  dtype=self.obs_dtype, device=dev)
             rew = reward_out if reward_out is not None else torch.empty(*lead, dtype=torch.float64, device=dev)
             done = done_out if done_out is not None else torch.empty(*lead, dtype=torch.uint8, device=dev)
             info = (info_out if info_out is not None else

@@ -364,3 +364,93 @@ def test_two_envs_per_wave_matches_one_per_wave(N, M, period):
         outs.append(res)
     for x, y in zip(*outs):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("N,M,Kn,Ki", [(16, 32, 1, 1), (64, 128, 1, 1), (8, 16, 2, 3), (4, 4, 0, 0), (30, 10, 1, 1)])
+def test_score_pairs_tiled_matches_scene_scorer(N, M, Kn, Ki):
+    """K1 (one workgroup per env, entity terms staged in LDS) against the per-wave scorer that the
+    on-device scene generator runs (the pair math of the reference tests above): bitwise."""
+    v = _venv(96, N, M, Kn, Ki, seed=5)
+    v.generate_scenes()
+    torch.cuda.synchronize()
+    want_d, want_p = v._scene["p_dmg"].clone(), v._scene["p_pen"].clone()
+    v._scene["p_dmg"].fill_(-1.0)
+    v._scene["p_pen"].fill_(-1.0)
+    v.score_pairs()
+    v.istate[:, 6] ^= 1  # the spare buffer too
+    v.score_pairs()
+    v.istate[:, 6] ^= 1
+    torch.cuda.synchronize()
+    assert torch.equal(v._scene["p_dmg"], want_d) and torch.equal(v._scene["p_pen"], want_p)
+
+
+def _device_scene(v, e):
+    keys = ("uav_pos", "uav_vel", "uav_load", "uav_cost", "tgt_pos", "tgt_vel", "tgt_value", "tgt_id", "nfz_pos",
+            "icp_pos", "icp_vel")
+    s = {k: v.active(k)[e].cpu().numpy() for k in keys}
+    s["nfz_pos"] = s["nfz_pos"][:v.Kn]
+    s["icp_pos"], s["icp_vel"] = s["icp_pos"][:v.Ki], s["icp_vel"][:v.Ki]
+    return s
+
+
+def test_c5_trajectories_vs_oracle():
+    """BASELINE config 4 dims (64 UAVs x 128 targets, two targets per lane) against the CPU oracle
+    on the device-generated scenes: one fused 400-step launch per env batch with state-only
+    auto-reset; decisions / done / pointer walk / num_assigned / is_valid bit-exact, rewards and J
+    to 1e-12, obs to the fp32 bar, and the same launch with fp16 observations (UAVHIP_ENV_OBS_F16)
+    emits exactly the fp32 windows rounded to binary16 with every other output bitwise equal."""
+    import oracle
+    from uavhip import _lib
+    E, N, M, T = 6, 64, 128, 400
+    outs = {}
+    for dt in (torch.float32, torch.float16):
+        from uavhip.vec_env import VecUAVEnv
+        v = VecUAVEnv(E, N, M, 1, 1, full_reset_period=0, seed=11, obs_dtype=dt)
+        v.generate_scenes()
+        obs0 = v.reset(episode=1)
+        g = torch.Generator(device="cuda").manual_seed(3)
+        a = (torch.rand(T, E, device="cuda", generator=g) < 0.35).to(torch.int8)
+        obs, r, d, info = v.step(a, auto_reset=True)
+        torch.cuda.synchronize()
+        outs[dt] = (v, obs0.clone(), a.cpu().numpy(), obs.clone(), r.cpu().numpy(), d.cpu().numpy(),
+                    info.cpu().numpy())
+    v, obs0, acts, obs, rew, done, info = outs[torch.float32]
+    obs_np = obs.cpu().numpy()
+    n_done = 0
+    for e in range(E):
+        env = oracle.OracleEnv(_device_scene(v, e), np.array([v.desc.prm[i] for i in range(_lib.PRM_COUNT)]))
+        np.testing.assert_allclose(obs0[e].cpu().numpy(), env.reset(), rtol=2e-6, atol=1e-6)
+        for t in range(T):
+            o_c, r_c, d_c, i_c = env.step(int(acts[t, e]))
+            assert bool(done[t, e]) == d_c, (e, t)
+            assert abs(rew[t, e] - r_c) <= 1e-12 * max(1.0, abs(r_c)), (e, t, rew[t, e], r_c)
+            np.testing.assert_array_equal(info[t, e, [1, 2, 5, 6]], i_c[[1, 2, 5, 6]])
+            assert abs(info[t, e, 0] - i_c[0]) <= 1e-12 * max(1.0, abs(i_c[0]))
+            if d_c:
+                n_done += 1
+                o_c = env.reset()
+            np.testing.assert_allclose(obs_np[t, e], o_c, rtol=2e-6, atol=1e-6)
+    assert n_done >= E  # every env finished at least one episode inside the launch
+    h = outs[torch.float16]
+    assert h[3].dtype == torch.float16
+    assert torch.equal(h[1], obs0.half()) and torch.equal(h[3], obs.half())
+    for i in (2, 4, 5, 6):
+        np.testing.assert_array_equal(h[i], outs[torch.float32][i])
+
+
+def test_fp16_obs_two_envs_per_wave():
+    """UAVHIP_ENV_OBS_F16 on the grouped (two envs per wave) multi-step kernel: fp16 obs = fp32 obs
+    rounded to binary16, all other outputs bitwise equal."""
+    from uavhip.vec_env import VecUAVEnv
+    res = []
+    for dt in (torch.float32, torch.float16):
+        v = VecUAVEnv(4096, 16, 32, 1, 1, full_reset_period=0, seed=4, obs_dtype=dt)
+        v.generate_scenes()
+        v.reset(episode=1)
+        g = torch.Generator(device="cuda").manual_seed(9)
+        a = (torch.rand(40, 4096, device="cuda", generator=g) < 0.5).to(torch.int8)
+        res.append([x.clone() for x in v.step(a, auto_reset=True)])
+    torch.cuda.synchronize()
+    assert res[1][0].dtype == torch.float16 and torch.equal(res[1][0], res[0][0].half())
+    for x, y in zip(res[0][1:], res[1][1:]):
+        assert torch.equal(x, y)
