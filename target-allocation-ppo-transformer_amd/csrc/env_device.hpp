@@ -176,6 +176,13 @@ struct EnvRegs {
     // loop-invariant divisors and their correctly rounded reciprocals (div_by)
     double den_c, rcp_c, den_v, rcp_v, rcp_m;
     double rcp_n;  // lane l: RN(1 / (l + 1)), the info averages' divisors 1..64
+    // pair probabilities the first step of a launch can move the pointer to, loaded by load_regs
+    // ahead of the step (p_dmg of (u, t + 1), (u + 1, 0) and (0, 0) of scene sb): one launch-start
+    // load round instead of a dependent global load at the end of the step
+    bool pc_ok = false;
+    int pc_u, pc_t;
+    long long pc_sb;
+    double pc[3];
 };
 
 // a / b, correctly rounded, from y = RN(1 / b) (Markstein's theorem: q = RN(a y) is within 1 ulp
@@ -285,7 +292,16 @@ __device__ void push_obs(EnvRegs<TPL>& R, int lane) {
 template <int TPL, bool LT = false>
 __device__ __forceinline__ void load_cur_pair(EnvRegs<TPL>& R, const uavhip_env& env) {
     if (R.u < env.N) {
-        R.pd_cur = LT ? R.tab[R.u * env.M + R.t] : env.p_dmg[(R.sb * env.N + R.u) * env.M + R.t];
+        if (LT) {
+            R.pd_cur = R.tab[R.u * env.M + R.t];
+        } else if (R.pc_ok && R.sb == R.pc_sb && R.t == 0 && (R.u == R.pc_u + 1 || R.u == 0)) {
+            R.pd_cur = R.u == 0 ? R.pc[2] : R.pc[1];
+        } else if (R.pc_ok && R.sb == R.pc_sb && R.u == R.pc_u && R.t == R.pc_t + 1) {
+            R.pd_cur = R.pc[0];
+        } else {
+            R.pd_cur = env.p_dmg[(R.sb * env.N + R.u) * env.M + R.t];
+        }
+        R.pc_ok = false;
         R.pp_cur = readlane_d(R.ppen, R.u);
     } else {
         R.pd_cur = 0.0;
@@ -351,11 +367,30 @@ __device__ __forceinline__ void load_scene_index(const uavhip_env& env, int e, i
     sb = (long long)sel * env.E + e;
 }
 
+// Register state from memory in ONE load round: nothing waits for the active-scene index (the
+// scene-dependent values are read from both buffers and selected afterwards); then, without a
+// wait, the pair probabilities the first step can move the pointer to (load_cur_pair).
 template <int TPL>
 __device__ void load_regs(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lane) {
     const int N = env.N, M = env.M;
-    load_scene_index(env, e, R.sel, R.stale, R.gen, R.sb);
-    load_scene_regs(R, env, lane);
+    const int* is = env.istate + (long long)e * UAVHIP_IST_COUNT;
+    const double* ds = env.dstate + (long long)e * UAVHIP_DST_COUNT;
+    const int nb = env.scene_buffers;
+    double valb[2][TPL], ucb[2], ppb[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const long long sb = (long long)(b < nb ? b : 0) * env.E + e;
+#pragma unroll
+        for (int k = 0; k < TPL; ++k) {
+            const int t = lane + kWave * k;
+            valb[b][k] = t < M ? env.tgt_value[sb * M + t] : 0.0;
+        }
+        ucb[b] = lane < N ? env.uav_cost[sb * N + lane] : 0.0;
+        ppb[b] = lane < N ? env.p_pen[sb * N + lane] : 0.0;
+    }
+    const int sel_raw = is[UAVHIP_IST_SCENE_SEL];
+    R.stale = is[UAVHIP_IST_SCENE_STALE];
+    R.gen = is[UAVHIP_IST_SCENE_GEN];
 #pragma unroll
     for (int k = 0; k < TPL; ++k) {
         const int t = lane + kWave * k;
@@ -367,8 +402,6 @@ __device__ void load_regs(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lan
         R.nlk[k] = v ? env.n_lock[o] : 0;
     }
     R.asg = lane < N ? env.assigned[(long long)e * N + lane] : -1;
-    const int* is = env.istate + (long long)e * UAVHIP_IST_COUNT;
-    const double* ds = env.dstate + (long long)e * UAVHIP_DST_COUNT;
     R.u = is[UAVHIP_IST_UAV_IDX];
     R.t = is[UAVHIP_IST_TARGET_IDX];
     R.ncov = is[UAVHIP_IST_N_COVERED];
@@ -381,17 +414,34 @@ __device__ void load_regs(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lan
     R.cov_val = ds[UAVHIP_DST_COV_VALUE];
     R.tot_cost = ds[UAVHIP_DST_TOTAL_COST];
     R.tot_val = ds[UAVHIP_DST_TOTAL_VALUE];
-    set_scene_divisors(R);
-    set_step_divisors(R, env, lane);
     R.sum_pd = ds[UAVHIP_DST_SUM_PDMG];
     R.sum_pf = ds[UAVHIP_DST_SUM_PFIN];
     const float* w = env.window + (long long)e * kObs;
     R.w0 = w[lane];
     R.w1 = lane < kObs - kWave ? w[kWave + lane] : 0.0f;
-    // the current pair's p_dmg was cached by the previous launch: one independent load round
+    // the current pair's p_dmg was cached by the previous launch
     R.pd_cur = ds[UAVHIP_DST_PD_CUR];
-    R.pp_cur = R.u < N ? readlane_d(R.ppen, R.u) : 0.0;
     drain_loads();
+    R.sel = nb == 2 ? (sel_raw & 1) : 0;
+    R.sb = (long long)R.sel * env.E + e;
+#pragma unroll
+    for (int k = 0; k < TPL; ++k) R.val[k] = R.sel ? valb[1][k] : valb[0][k];
+    R.ucost = R.sel ? ucb[1] : ucb[0];
+    R.ppen = R.sel ? ppb[1] : ppb[0];
+    if (R.u < N) {  // candidates for the first step's load_cur_pair, consumed after its compute
+        const double* pt = env.p_dmg + R.sb * N * M;
+        const int u = R.u, t = R.t;
+        R.pc[0] = t + 1 < M ? pt[u * M + t + 1] : 0.0;
+        R.pc[1] = u + 1 < N ? pt[(u + 1) * M] : 0.0;
+        R.pc[2] = pt[0];
+        R.pc_u = u;
+        R.pc_t = t;
+        R.pc_sb = R.sb;
+        R.pc_ok = true;
+    }
+    set_scene_divisors(R);
+    set_step_divisors(R, env, lane);
+    R.pp_cur = R.u < N ? readlane_d(R.ppen, R.u) : 0.0;
 }
 
 template <int TPL>

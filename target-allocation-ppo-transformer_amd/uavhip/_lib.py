@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libuavhip.so")
+# UAVHIP_LIB: an alternative in-tree build (profiling: the TRACE=1 phase-stamp build)
+LIB_PATH = os.environ.get("UAVHIP_LIB") or os.path.join(_HERE, "libuavhip.so")
 
 SEQ_LEN = 5
 STATE_DIM = 14
