@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--eager", action="store_true", help="launch kernels eagerly instead of replaying a hipGraph")
+    ap.add_argument("--unfused", action="store_true",
+                    help="separate policy and env launches per step instead of uavhip_rollout_step")
     ap.add_argument("--full-window", action="store_true",
                     help="policy forward over the full window every step (no window-row ring)")
     return ap.parse_args()
@@ -277,7 +279,7 @@ def main():
     policy = TransformerActorCritic().to(dev)
     env = VecUAVEnv(E, args.uavs, args.targets, 1, 1, seed=1 + rank, full_reset_period=200)
     eng = RolloutEngine(env, policy, T, want_info=True, bootstrap=True, seed=1000 + rank, normalize=(world == 1),
-                        row_cache=not args.full_window)
+                        row_cache=not args.full_window, fused_step=False if args.unfused else None)
     eng.start()
 
     # The iteration is captured once into a hipGraph and replayed. HIP events (recorded on the
@@ -320,9 +322,15 @@ def main():
     env_steps = E * T * args.steps * world
     value = env_steps / elapsed
 
-    pol_list, env_list = eng.event_ms()   # the last timed iteration's T+1 policy and T env launches
-    pol_ms = float(np.mean(pol_list))
-    env_ms = float(np.mean(env_list))
+    # the last timed iteration's launches: T+1 policy and T env launches, or (fused steps) T fused
+    # forward + env-step launches and the bootstrap forward (the same kernel without the env step)
+    pol_list, env_list = eng.event_ms()
+    if eng.fused_step:
+        pol_ms = float(np.mean(pol_list[:T]))
+        env_ms = max(pol_ms - float(pol_list[T]), 1e-6)  # the env step's share of a fused launch
+    else:
+        pol_ms = float(np.mean(pol_list))
+        env_ms = float(np.mean(env_list))
     flop_exec = ROWS_FLOP_PER_SAMPLE if eng.rowproj is not None else POLICY_FLOP_PER_SAMPLE
     achieved_tf = POLICY_FLOP_PER_SAMPLE * E / (pol_ms * 1e-3) / 1e12
     exec_tf = flop_exec * E / (pol_ms * 1e-3) / 1e12
@@ -346,9 +354,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, policy.state_dict(), args.cpu_seconds)
 
-    pol_kernel = "k_policy_forward<false, true>" if eng.rowproj is not None else "k_policy_forward<false>"
+    pol_kernel = ("k_policy_forward<false, true, true>" if eng.fused_step else "k_policy_forward<false, true, false>"
+                  if eng.rowproj is not None else "k_policy_forward<false, false, false>")
     pol_traffic, pol_src = profiled_traffic(pol_kernel)
-    env_traffic, _ = profiled_traffic("k_env_step<1, false>")
+    env_traffic = None if eng.fused_step else profiled_traffic("k_env_step<1, false>")[0]
     if rank == 0:
         line = {
             "metric": "env-steps/sec (whole node), full PPO rollout, 4096 envs x 16 UAV x 32 tgt per GPU",
@@ -368,10 +377,16 @@ def main():
                          "flop_per_launch_source": "SURVEY.md 8(d): 2,446,208 FLOP/sample x E",
                          "executed_flop_per_launch": flop_exec * E, "executed_achieved": exec_tf,
                          "executed_frac": exec_tf / MFMA_F32_PEAK_TFLOPS,
-                         "path": "window-row ring (layer-0 in_proj of the new row only)" if eng.rowproj is not None
-                         else "full window",
-                         "timing": "HIP events around each of the T+1 launches of the last timed iteration"},
-            "env_roofline": {"kernel": "k_env_step", "bound": "hbm", "achieved": env_gbs, "peak": HBM_PEAK_GBS,
+                         "path": ("fused rollout step (window-row forward + sample + env step, one launch)"
+                                  if eng.fused_step else "window-row ring (layer-0 in_proj of the new row only)"
+                                  if eng.rowproj is not None else "full window"),
+                         "timing": ("HIP events around each of the T fused launches of the last timed iteration "
+                                    "(env step included)" if eng.fused_step else
+                                    "HIP events around each of the T+1 launches of the last timed iteration")},
+            "env_roofline": {"kernel": "env step inside the fused rollout launch" if eng.fused_step else "k_env_step",
+                             "timing": ("fused launch minus the bootstrap forward launch" if eng.fused_step else
+                                        "HIP events around each of the T env launches"),
+                             "bound": "hbm", "achieved": env_gbs, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS, "avg_launch_ms": env_ms,
                              "traffic": env_traffic,
                              "bytes_per_env_step": env_bytes_per_step(args.targets)},

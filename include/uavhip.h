@@ -285,6 +285,19 @@ int uavhip_policy_forward_rows(const uavhip_policy* policy, const float* states,
                                const uint64_t* offset_dev, int8_t* action_out, float* logp, float* value,
                                float* entropy, float* logits, uavhip_stream_t stream);
 
+/* One rollout step in ONE launch (main_train.py:109-117: select_action, then env.step): the
+ * window-row forward of uavhip_policy_forward_rows with sampling, followed in the same
+ * workgroups by the env step (uavhip_env_step, T = 1) of env e with the action sampled for
+ * window b = e. B = env->E; the same outputs as the two calls in sequence, bitwise: action_out,
+ * logp, value [E] of the forward, obs_out [E][5][14] (the next windows; f32, or binary16 under
+ * UAVHIP_ENV_OBS_F16), reward [E], done [E], info [E][UAVHIP_INFO_COUNT] (nullable) of the step.
+ * Needs N, M <= 64 (one env per wave). Saves the T = 1 env launch's fixed cost (dispatch, the
+ * state-load round, the store drain: ~7 of its ~10 us at 4096 envs). */
+int uavhip_rollout_step(const uavhip_policy* policy, const uavhip_env* env, const float* states, float* rowproj,
+                        int32_t step, int32_t fill, uint64_t seed, uint64_t offset, const uint64_t* offset_dev,
+                        int8_t* action_out, float* logp, float* value, int32_t auto_reset, float* obs_out,
+                        double* reward, uint8_t* done, double* info, uavhip_stream_t stream);
+
 /* ---------------------------------------------------------------- PPO update (K5) */
 
 /* One clipped-PPO minibatch step of agents/ppo.py:96-169 (evaluate -> surrogate / clipped value

@@ -19,6 +19,7 @@ namespace uavhip {
 // ------------------------------------------------------------------ error plumbing (host)
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+int validate_env(const uavhip_env* env, bool need_state);  // env.hip: descriptor checks of the C ABI
 
 // ------------------------------------------------------------------ wave helpers
 constexpr int kWave = 64;

@@ -213,8 +213,7 @@ __global__ __launch_bounds__(kBlock) void k_scene_refresh(uavhip_env env) {
 }
 
 // ================================================================== C ABI
-namespace {
-int validate(const uavhip_env* env, bool need_state) {
+int validate_env(const uavhip_env* env, bool need_state) {
     if (!env) { set_error("env descriptor is NULL"); return UAVHIP_EINVAL; }
     if (env->E <= 0 || env->N <= 0 || env->N > UAVHIP_MAX_N || env->M <= 0 || env->M > UAVHIP_MAX_M ||
         env->Kn < 0 || env->Kn > UAVHIP_MAX_OBSTACLES || env->Ki < 0 || env->Ki > UAVHIP_MAX_OBSTACLES) {
@@ -243,6 +242,8 @@ int validate(const uavhip_env* env, bool need_state) {
     }
     return UAVHIP_OK;
 }
+namespace {
+int validate(const uavhip_env* env, bool need_state) { return validate_env(env, need_state); }
 inline int wave_grid(int E) { return (E + kWavesPerBlock - 1) / kWavesPerBlock; }
 }  // namespace
 

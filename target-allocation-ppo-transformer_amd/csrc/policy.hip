@@ -21,6 +21,7 @@
 //  * sampling: a = (u < p0) ? 0 : 1 with u ~ Philox(seed, offset + b) (not torch's RNG stream;
 //    parity is defined on logits / logp / value / entropy for given actions).
 #include "common.hpp"
+#include "env_device.hpp"
 #include "policy_layout.hpp"
 #include "policy_train.hpp"
 
@@ -831,16 +832,29 @@ __device__ void loss_partials(Smem& sm, const TrainIO& io, int b0) {
     }
 }
 
+// Fused rollout step (uavhip_rollout_step): the env step of the sampled actions (uav_env.py:295-435)
+// after the forward, on the same workgroup's 16 envs.
+struct EnvOut {
+    int auto_reset;
+    float* obs;     // [E][5][14] next windows (f32, or binary16 under UAVHIP_ENV_OBS_F16)
+    double* rew;    // [E]
+    uint8_t* done;  // [E]
+    double* info;   // [E][UAVHIP_INFO_COUNT] (nullable)
+};
+
 // ROWS: layer 0 of both trunks on the window-row projection ring (inference only).
-template <bool TR, bool ROWS = false>
+// ENV: the env step of the sampled actions follows (needs ROWS; envs b0 .. b0 + 15).
+template <bool TR, bool ROWS = false, bool ENV = false>
 __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict__ P, const float* __restrict__ states,
                                                          int B, const int8_t* __restrict__ actions_in, uint64_t seed,
                                                          uint64_t offset, const uint64_t* __restrict__ offset_dev,
                                                          int8_t* __restrict__ action_out,
                                                          float* __restrict__ logp_out, float* __restrict__ value_out,
                                                          float* __restrict__ ent_out, float* __restrict__ logits_out,
-                                                         const TrainIO io, const RowIO rio) {
+                                                         const TrainIO io, const RowIO rio, const uavhip_env env,
+                                                         const EnvOut eo) {
     static_assert(!(TR && ROWS), "the training forward recomputes every row");
+    static_assert(!ENV || ROWS, "the fused env step follows the rollout forward");
     __shared__ __attribute__((aligned(16))) Smem sm;
     const int b0 = blockIdx.x * SPW;
     PTR(0);
@@ -969,9 +983,35 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
             if (ent_out) ent_out[b] = -(p0 * lp0 + p1 * lp1);
             if (value_out) value_out[b] = sm.value[p];
             if (logits_out) { logits_out[2 * b] = l0; logits_out[2 * b + 1] = l1; }
+            if (ENV) sm.mask[p] = a;  // the key mask is dead after the forward
         }
     }
     PTR(7);
+    if constexpr (ENV) {
+        // UAVEnv.step of this workgroup's 16 envs, two per wave (one env per wave at a time,
+        // envdev::step_once on register state; the wave's row scratch in the dead sm.x). Both envs'
+        // registers are loaded in one round before either steps.
+        __syncthreads();
+        using namespace envdev;
+        const int lane = lane_id(), e0 = b0 + 2 * wv;
+        if (e0 < B) {
+            const bool two = e0 + 1 < B;
+            EnvRegs<1> R0, R1;
+            R0.row = R1.row = sm.x + 16 * wv;
+            load_regs(R0, env, e0, lane);
+            if (two) load_regs(R1, env, e0 + 1, lane);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (k == 1 && !two) break;
+                EnvRegs<1>& R = k ? R1 : R0;
+                const int e = e0 + k;
+                step_once<1, false>(R, env, e, lane, sm.mask[2 * wv + k], eo.auto_reset,
+                                    obs_at(eo.obs, e, obs_f16(env)), eo.rew + e, eo.done + e,
+                                    eo.info ? eo.info + (size_t)e * UAVHIP_INFO_COUNT : nullptr);
+                store_regs(R, env, e, lane);
+            }
+        }
+    }
 }
 
 // Ring fill of one trunk: u rows of positions 0-3 of the workgroup's 16 windows -> slots
@@ -1550,7 +1590,7 @@ namespace uavhip {
 namespace pol {
 int policy_forward_train(const float* packed, const float* states, const TrainIO& io, int Bm, hipStream_t st) {
     hipLaunchKernelGGL(k_policy_forward<true>, dim3(Bm / SPW), dim3(NTHR), 0, st, packed, states, Bm, nullptr, 0ull,
-                       0ull, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, io, RowIO{});
+                       0ull, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, io, RowIO{}, uavhip_env{}, EnvOut{});
     return check_launch("k_policy_forward<train>");
 }
 
@@ -1680,7 +1720,7 @@ extern "C" int uavhip_policy_forward(const uavhip_policy* policy, const float* s
     const int grid = (B + pol::SPW - 1) / pol::SPW;
     hipLaunchKernelGGL(pol::k_policy_forward<false>, dim3(grid), dim3(pol::NTHR), 0, (hipStream_t)stream,
                        policy->weights, states, (int)B, actions_in, seed, offset, offset_dev, action_out, logp, value,
-                       entropy, logits, pol::TrainIO{}, pol::RowIO{});
+                       entropy, logits, pol::TrainIO{}, pol::RowIO{}, uavhip_env{}, pol::EnvOut{});
     return check_launch("k_policy_forward");
 }
 
@@ -1708,6 +1748,38 @@ extern "C" int uavhip_policy_forward_rows(const uavhip_policy* policy, const flo
     }
     hipLaunchKernelGGL((pol::k_policy_forward<false, true>), dim3(grid), dim3(pol::NTHR), 0, (hipStream_t)stream,
                        policy->weights, states, (int)B, actions_in, seed, offset, offset_dev, action_out, logp, value,
-                       entropy, logits, pol::TrainIO{}, rio);
+                       entropy, logits, pol::TrainIO{}, rio, uavhip_env{}, pol::EnvOut{});
     return check_launch("k_policy_forward_rows");
+}
+
+// Fused rollout step: uavhip_policy_forward_rows (sampling) + uavhip_env_step (T = 1) of env e
+// on window b = e, one launch. N, M <= 64 (one env per wave); B = env->E.
+extern "C" int uavhip_rollout_step(const uavhip_policy* policy, const uavhip_env* env, const float* states,
+                                   float* rowproj, int32_t step, int32_t fill, uint64_t seed, uint64_t offset,
+                                   const uint64_t* offset_dev, int8_t* action_out, float* logp, float* value,
+                                   int32_t auto_reset, float* obs_out, double* reward, uint8_t* done, double* info,
+                                   uavhip_stream_t stream) {
+    if (const int rc = validate_env(env, true)) return rc;
+    const int32_t B = env->E;
+    if (const int rc = check_policy("uavhip_rollout_step", policy, states, B)) return rc;
+    if (env->N > 64 || env->M > 64 || !action_out || !obs_out || !reward || !done) {
+        set_error("uavhip_rollout_step: N=%d, M=%d must be <= 64 and action/obs/reward/done non-NULL", env->N, env->M);
+        return UAVHIP_EINVAL;
+    }
+    if (!rowproj || step < 0 || (int64_t)B * pol::S * pol::kRowFloats >= (int64_t)1 << 31) {
+        set_error("uavhip_rollout_step: NULL rowproj, step=%d < 0 or E=%d above the ring's 32-bit offsets", step, B);
+        return UAVHIP_EINVAL;
+    }
+    const int grid = (B + pol::SPW - 1) / pol::SPW;
+    const pol::RowIO rio{rowproj, (int)B, (int)step};
+    if (fill) {
+        hipLaunchKernelGGL(pol::k_policy_rows_fill, dim3(grid + 1), dim3(pol::NTHR), 0, (hipStream_t)stream,
+                           policy->weights, states, rio);
+        if (const int rc = check_launch("k_policy_rows_fill")) return rc;
+    }
+    hipLaunchKernelGGL((pol::k_policy_forward<false, true, true>), dim3(grid), dim3(pol::NTHR), 0, (hipStream_t)stream,
+                       policy->weights, states, (int)B, nullptr, seed, offset, offset_dev, action_out, logp, value,
+                       nullptr, nullptr, pol::TrainIO{}, rio, *env,
+                       pol::EnvOut{(int)auto_reset, obs_out, reward, done, info});
+    return check_launch("k_rollout_step");
 }

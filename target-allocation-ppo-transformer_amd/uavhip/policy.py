@@ -154,6 +154,23 @@ class TransformerActorCritic(nn.Module):
                                         ptr(entropy), ptr(logits), stream_handle()), "uavhip_policy_forward")
         return action_out, logp, value, entropy, logits
 
+    def rollout_step(self, env, states, rowproj, step, fill, action_out, logp, value, obs_out, reward_out, done_out,
+                     info_out=None, auto_reset=True, seed=None, offset=0, offset_dev=None):
+        """uavhip_rollout_step: the window-row forward + sampling over env's E windows `states`
+        and the env step of the sampled actions in one launch (VecUAVEnv `env`, N, M <= 64).
+        The weights must be packed (packed_weights())."""
+        if self._packed is None:
+            self.packed_weights()
+        env._check_obs(obs_out)
+        if rowproj.numel() < LIB.uavhip_policy_rowproj_floats(env.E) or states.dtype != torch.float32:
+            raise ValueError("rowproj: need rowproj_buffer(E); states: float32 windows")
+        seed = self.sample_seed if seed is None else seed
+        check(LIB.uavhip_rollout_step(self._desc, env.desc, ptr(states), ptr(rowproj), int(step), int(bool(fill)),
+                                      ctypes.c_uint64(seed), ctypes.c_uint64(offset), ptr(offset_dev),
+                                      ptr(action_out), ptr(logp), ptr(value), int(bool(auto_reset)), ptr(obs_out),
+                                      ptr(reward_out), ptr(done_out), ptr(info_out), stream_handle()),
+              "uavhip_rollout_step")
+
     @torch.no_grad()
     def get_action(self, state):
         """transformer_net.py:96-122 -> (action [B] int64, log_prob [B], value [B, 1], entropy [B])."""

@@ -42,10 +42,13 @@ class Trajectory:
 
 
 class RolloutEngine:
-    def __init__(self, env, policy, horizon, want_info=True, bootstrap=True, seed=0, normalize=True, row_cache=True):
+    def __init__(self, env, policy, horizon, want_info=True, bootstrap=True, seed=0, normalize=True, row_cache=True,
+                 fused_step=None):
         """normalize=False leaves the advantages raw after GAE: a data-parallel caller normalises
         them with the moments of the whole gathered batch in gather() (ppo.py:94).
-        row_cache=False runs every step on the full-window forward (uavhip_policy_forward)."""
+        row_cache=False runs every step on the full-window forward (uavhip_policy_forward).
+        fused_step: one launch per step (uavhip_rollout_step: forward + sample + env step); default
+        on when the row cache is on and N, M <= 64."""
         self.env = env
         self.normalize = normalize
         self.iteration = 0
@@ -59,6 +62,10 @@ class RolloutEngine:
         # window-row projections of the obs windows (policy.rowproj_buffer): the windows of one
         # iteration are one deque sequence, so step t projects only its new row (rebuilt at t = 0)
         self.rowproj = rowproj_buffer(env.E, env.device) if row_cache else None
+        can_fuse = row_cache and env.N <= 64 and env.M <= 64
+        if fused_step and not can_fuse:
+            raise ValueError("fused_step needs row_cache=True and N, M <= 64")
+        self.fused_step = can_fuse if fused_step is None else bool(fused_step)
         self.graph = None
         self.policy_events = None   # [(start, end)] HIP events around each policy launch (optional)
         self.env_events = None
@@ -85,6 +92,17 @@ class RolloutEngine:
         tr.obs[0].copy_(tr.obs[self.T])  # carry the previous iteration's last window
         eev = self.env_events
         for t in range(self.T):
+            if self.fused_step:
+                ev = self.policy_events
+                if ev is not None:
+                    ev[t][0].record()
+                self.policy.rollout_step(env, tr.obs[t], self.rowproj, t, t == 0, tr.actions[t], tr.logp[t],
+                                         tr.values[t], tr.obs[t + 1], tr.rewards[t], tr.dones[t],
+                                         None if tr.info is None else tr.info[t], seed=self.seed,
+                                         offset=t * env.E, offset_dev=self.counter)
+                if ev is not None:
+                    ev[t][1].record()
+                continue
             self._forward(t, tr.obs[t], tr.actions[t], tr.logp[t], tr.values[t])
             if eev is not None:
                 eev[t][0].record()
@@ -126,8 +144,11 @@ class RolloutEngine:
         self.env_events = [(torch.cuda.Event(**kw), torch.cuda.Event(**kw)) for _ in range(self.T)]
 
     def event_ms(self):
-        """(policy launch ms list, env launch ms list) of the most recent iteration."""
-        return ([a.elapsed_time(b) for a, b in self.policy_events], [a.elapsed_time(b) for a, b in self.env_events])
+        """(policy launch ms list, env launch ms list) of the most recent iteration (fused steps:
+        the policy list holds the T fused launches + the bootstrap forward, the env list is empty)."""
+        pol = [a.elapsed_time(b) for a, b in self.policy_events]
+        env = [] if self.fused_step else [a.elapsed_time(b) for a, b in self.env_events]
+        return pol, env
 
     @torch.no_grad()
     def capture(self):

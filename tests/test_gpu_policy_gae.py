@@ -388,3 +388,37 @@ def test_graph_ppo_update_matches_eager():
     np.testing.assert_allclose(sg[:3], se[:3], rtol=1e-5, atol=1e-6)
     for (k, a), b in zip(pe.state_dict().items(), pg.state_dict().values()):
         torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.parametrize("E,N,M,period", [(4096, 16, 32, 3), (1000, 8, 16, 2), (96, 64, 64, 0), (33, 4, 4, 5)])
+def test_fused_rollout_step_matches_two_launches(E, N, M, period):
+    """uavhip_rollout_step (window-row forward + sampling + env step in one launch) against the
+    separate policy and env launches it replaces (each checked against the reference above), on
+    twin envs from the same seed: every trajectory output, the row cache and the whole env state
+    bitwise over two iterations with auto-reset and full resets flipping to refreshed scenes."""
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.rollout import RolloutEngine
+    from uavhip.vec_env import VecUAVEnv
+    torch.manual_seed(0)
+    pol = TransformerActorCritic().cuda()
+    T = 20
+    res = []
+    for fused in (False, True):
+        env = VecUAVEnv(E, N, M, 1, 1, seed=6, full_reset_period=period)
+        eng = RolloutEngine(env, pol, T, seed=5, fused_step=fused)
+        assert eng.fused_step == fused
+        eng.start()
+        out = []
+        for _ in range(2):
+            tr = eng.collect()
+            out += [x.clone() for x in (tr.obs, tr.actions, tr.logp, tr.values, tr.rewards, tr.dones, tr.info,
+                                        tr.ret, tr.adv, tr.last_values)]
+        out += [eng.rowproj.clone(), env.istate.clone(), env.dstate.clone(), env.window.clone(), env.nh_final.clone(),
+                env.nh_pure.clone(), env.t_cost.clone(), env.n_lock.clone(), env.assigned.clone()]
+        assert int((env.errors() & 1).max()) == 0
+        res.append(out)
+    torch.cuda.synchronize()
+    if N * M <= 512:
+        assert res[1][5].any()  # episodes ended inside the rollout
+    for i, (a, b) in enumerate(zip(*res)):
+        assert torch.equal(a, b), i
