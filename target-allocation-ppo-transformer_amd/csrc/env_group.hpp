@@ -69,7 +69,10 @@ __device__ void gload_scene_regs(GRegs& R, const uavhip_env& env, int j) {
     drain_loads();
 }
 
+// tab == nullptr (single-step use inside the fused rollout launch): pair probabilities are read
+// from the global p_dmg table instead of an LDS copy
 __device__ void gload_table(GRegs& R, const uavhip_env& env, int j) {
+    if (!R.tab) return;
     const int NM = env.N * env.M;
     const double* src = env.p_dmg + R.sb * NM;
     for (int i = j; i < NM; i += L) R.tab[i] = src[i];
@@ -80,7 +83,7 @@ __device__ void gload_table(GRegs& R, const uavhip_env& env, int j) {
 
 __device__ __forceinline__ void gload_cur_pair(GRegs& R, const uavhip_env& env) {
     if (R.u < env.N) {
-        R.pd_cur = R.tab[R.u * env.M + R.t];
+        R.pd_cur = R.tab ? R.tab[R.u * env.M + R.t] : env.p_dmg[(R.sb * env.N + R.u) * env.M + R.t];
         R.pp_cur = gsh_d(R.ppen, R.u);
     } else {
         R.pd_cur = 0.0;
@@ -185,12 +188,28 @@ __device__ void greset_regs(GRegs& R, const uavhip_env& env, int j, bool scene) 
     gpush_obs(R, j);
 }
 
-__device__ void gload_regs(GRegs& R, const uavhip_env& env, int e, int j) {
+// Register state from memory in one load round (scene-dependent values read from both scene
+// buffers and selected after the wait, as envdev::load_regs). gload_issue only issues the loads
+// (the fused rollout launch overlaps them with the critic head); gload_finish consumes them.
+struct GPending {
+    double valb[2], ucb[2], ppb[2];
+    int sel_raw;
+};
+__device__ __forceinline__ void gload_issue(GRegs& R, GPending& q, const uavhip_env& env, int e, int j) {
     const int N = env.N, M = env.M;
-    load_scene_index(env, e, R.sel, R.stale, R.gen, R.sb);
-    R.val = j < M ? env.tgt_value[R.sb * M + j] : 0.0;
-    R.ucost = j < N ? env.uav_cost[R.sb * N + j] : 0.0;
-    R.ppen = j < N ? env.p_pen[R.sb * N + j] : 0.0;
+    const int* is = env.istate + (long long)e * UAVHIP_IST_COUNT;
+    const double* ds = env.dstate + (long long)e * UAVHIP_DST_COUNT;
+    const int nb = env.scene_buffers;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const long long sb = (long long)(b < nb ? b : 0) * env.E + e;
+        q.valb[b] = j < M ? env.tgt_value[sb * M + j] : 0.0;
+        q.ucb[b] = j < N ? env.uav_cost[sb * N + j] : 0.0;
+        q.ppb[b] = j < N ? env.p_pen[sb * N + j] : 0.0;
+    }
+    q.sel_raw = is[UAVHIP_IST_SCENE_SEL];
+    R.stale = is[UAVHIP_IST_SCENE_STALE];
+    R.gen = is[UAVHIP_IST_SCENE_GEN];
     const long long o = (long long)e * M + j;
     const bool v = j < M;
     R.nhf = v ? env.nh_final[o] : 1.0;
@@ -198,8 +217,6 @@ __device__ void gload_regs(GRegs& R, const uavhip_env& env, int e, int j) {
     R.tc = v ? env.t_cost[o] : 0.0;
     R.nlk = v ? env.n_lock[o] : 0;
     R.asg = j < N ? env.assigned[(long long)e * N + j] : -1;
-    const int* is = env.istate + (long long)e * UAVHIP_IST_COUNT;
-    const double* ds = env.dstate + (long long)e * UAVHIP_DST_COUNT;
     R.u = is[UAVHIP_IST_UAV_IDX];
     R.t = is[UAVHIP_IST_TARGET_IDX];
     R.ncov = is[UAVHIP_IST_N_COVERED];
@@ -219,11 +236,24 @@ __device__ void gload_regs(GRegs& R, const uavhip_env& env, int e, int j) {
     R.w0 = w[j];
     R.w1 = w[L + j];
     R.w2 = j < kObs - 2 * L ? w[2 * L + j] : 0.0f;
-    drain_loads();
+}
+__device__ __forceinline__ void gload_finish(GRegs& R, const GPending& q, const uavhip_env& env, int e, int j) {
+    const int N = env.N, M = env.M;
+    R.sel = env.scene_buffers == 2 ? (q.sel_raw & 1) : 0;
+    R.sb = (long long)R.sel * env.E + e;
+    R.val = R.sel ? q.valb[1] : q.valb[0];
+    R.ucost = R.sel ? q.ucb[1] : q.ucb[0];
+    R.ppen = R.sel ? q.ppb[1] : q.ppb[0];
     gset_scene_divisors(R);
     R.rcp_m = 1.0 / (double)M;
     R.rcp_n = 1.0 / (double)(j + 1);
     R.pp_cur = R.u < N ? gsh_d(R.ppen, R.u) : 0.0;
+}
+__device__ void gload_regs(GRegs& R, const uavhip_env& env, int e, int j) {
+    GPending q;
+    gload_issue(R, q, env, e, j);
+    drain_loads();
+    gload_finish(R, q, env, e, j);
 }
 
 __device__ void gstore_regs(const GRegs& R, const uavhip_env& env, int e, int j) {

@@ -22,6 +22,7 @@
 //    parity is defined on logits / logp / value / entropy for given actions).
 #include "common.hpp"
 #include "env_device.hpp"
+#include "env_group.hpp"
 #include "policy_layout.hpp"
 #include "policy_train.hpp"
 
@@ -950,6 +951,15 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
     __syncthreads();
     encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0);
+    // fused env step, two envs per wave side by side: its state loads are issued here and land
+    // while the critic head runs
+    [[maybe_unused]] const bool env_grp =
+        ENV && env.N <= envgrp::L && env.M <= envgrp::L && b0 + 2 * wv + 1 < B;
+    [[maybe_unused]] envgrp::GRegs gR;
+    [[maybe_unused]] envgrp::GPending gq;
+    if constexpr (ENV) {
+        if (env_grp) envgrp::gload_issue(gR, gq, env, b0 + 2 * wv + (lane_id() >> 5), lane_id() & 31);
+    }
     if (wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
     __syncthreads();
     PTR(5);
@@ -994,7 +1004,17 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         __syncthreads();
         using namespace envdev;
         const int lane = lane_id(), e0 = b0 + 2 * wv;
-        if (e0 < B) {
+        if (env_grp) {
+            // both envs side by side, 32 lanes each (env_group.hpp); window scratch in the dead sm.h
+            const int j = lane & 31, g = lane >> 5, e = e0 + g;
+            envgrp::GRegs& R = gR;
+            R.tab = nullptr;
+            R.win = sm.h + (2 * wv + g) * envgrp::kWin;
+            envgrp::gload_finish(R, gq, env, e, j);
+            envgrp::gstep(R, env, e, j, sm.mask[2 * wv + g], eo.auto_reset, obs_at(eo.obs, e, obs_f16(env)),
+                          eo.rew + e, eo.done + e, eo.info ? eo.info + (size_t)e * UAVHIP_INFO_COUNT : nullptr);
+            envgrp::gstore_regs(R, env, e, j);
+        } else if (e0 < B) {
             const bool two = e0 + 1 < B;
             EnvRegs<1> R0, R1;
             R0.row = R1.row = sm.x + 16 * wv;
