@@ -23,6 +23,8 @@ Also reported (same JSON line):
                 1/N slice of every global minibatch, RCCL all-reduce of loss sums and gradients)
   cpu_baseline  the CPU port (C oracle env.step + torch-CPU fp32 policy + numpy GAE) on host cores,
                 rank 0 at N = 1 only, bounded sample
+  cpu_env_baseline  UAVEnv.step alone (C oracle, reference algorithm) on all host cores (one process
+                per core, <= 16), 10 s
 Launch for N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
@@ -131,6 +133,18 @@ def cpu_baseline(args, state_dict, seconds):
     return {"value": steps / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "sample": f"{E} envs x {steps // E} steps of {args.uavs}x{args.targets} ({dt:.1f} s): torch-CPU fp32 "
                       f"policy forward ({cores} threads) + C oracle UAVEnv.step (1 thread) + numpy GAE"}
+
+
+def cpu_env_baseline(args, seconds=10.0):
+    """UAVEnv.step alone on the host cores (north_star: the reference CPU env.step timed on the same
+    box): the C oracle's batched loop in one process per core, run as a child process that never
+    touches the GPU (oracle/cpu_env_bench.py)."""
+    import subprocess
+    procs = max(1, min(16, len(os.sched_getaffinity(0))))
+    out = subprocess.run([sys.executable, "-m", "oracle.cpu_env_bench", "--procs", str(procs), "--seconds",
+                          str(seconds), "--uavs", str(args.uavs), "--targets", str(args.targets)],
+                         cwd=ROOT, capture_output=True, text=True, timeout=seconds + 120, check=True)
+    return json.loads(out.stdout.strip().splitlines()[-1])
 
 
 def env_fused_rate(E, N, M, T, dev, reps=5, obs_dtype=torch.float32):
@@ -350,9 +364,13 @@ def main():
             print(f"[bench] PPO update measurement failed: {exc!r}", file=sys.stderr)
             ppo = {"value": None, "error": repr(exc)}
 
-    cpu = None
+    cpu = cpu_env = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, policy.state_dict(), args.cpu_seconds)
+        try:
+            cpu_env = cpu_env_baseline(args)
+        except Exception as exc:  # the headline line must still print
+            cpu_env = {"value": None, "error": repr(exc)}
 
     pol_kernel = ("k_policy_forward<false, true, true>" if eng.fused_step else "k_policy_forward<false, true, false>"
                   if eng.rowproj is not None else "k_policy_forward<false, false, false>")
@@ -394,6 +412,7 @@ def main():
             "score_pairs": stress,
             "ppo_samples_per_s": ppo,
             "cpu_baseline": cpu,
+            "cpu_env_baseline": cpu_env,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
