@@ -857,6 +857,8 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     static_assert(!(TR && ROWS), "the training forward recomputes every row");
     static_assert(!ENV || ROWS, "the fused env step follows the rollout forward");
     __shared__ __attribute__((aligned(16))) Smem sm;
+    // the younger half (waves 4-7, the arbitration loser of every phase) at priority 1
+    if (threadIdx.x >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
     const int b0 = blockIdx.x * SPW;
     PTR(0);
     // windows -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch tail zero-filled);
@@ -1576,6 +1578,8 @@ __device__ __forceinline__ void head_input_grad(Smem& sm, const float* __restric
 __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restrict__ P, const float* __restrict__ PT,
                                                           const BwdIO io) {
     __shared__ __attribute__((aligned(16))) Smem sm;
+    // the younger half (waves 4-7, the arbitration loser of every phase) at priority 1
+    if (threadIdx.x >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
     const int b0 = blockIdx.x * SPW;
     if (threadIdx.x < SPW * S) sm.mask[threadIdx.x] = io.mask[(size_t)b0 * S + threadIdx.x] != 0.f;
     BTR(0);
