@@ -89,7 +89,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(uavhip_env env, const int8_
     EnvRegs<TPL> R;
     R.tab = s_tab + (threadIdx.x >> 6) * env.N * env.M;
     R.row = s_row + (threadIdx.x >> 6) * 16;
-    load_regs(R, env, e, lane);
+    load_regs<TPL>(R, env, e, lane);
     if (LT) load_table(R, env, lane);
     const long long E = env.E;
     for (int s0 = 0; s0 < T; s0 += kWave) {
@@ -307,6 +307,9 @@ extern "C" int uavhip_env_step(const uavhip_env* env, const int8_t* actions, int
                            (int)T, (int)auto_reset, obs_out, reward, done, info);
         return check_launch("k_env_step_g");
     }
+    // (the single-step load order with prefetched next-pair candidates, load_regs<TPL, true>, runs
+    // inside the fused rollout launch; instantiating it here as well slowed the multi-step kernels
+    // of this code object by ~9 % with byte-identical machine code for them: code placement)
     if (env->M <= kWave) {
         if (lt) hipLaunchKernelGGL((k_env_step<1, true>), grid, block, tab, st, *env, actions, (int)T, (int)auto_reset, obs_out, reward, done, info);
         else hipLaunchKernelGGL((k_env_step<1, false>), grid, block, 0, st, *env, actions, (int)T, (int)auto_reset, obs_out, reward, done, info);

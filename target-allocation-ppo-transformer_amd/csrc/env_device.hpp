@@ -367,12 +367,54 @@ __device__ __forceinline__ void load_scene_index(const uavhip_env& env, int e, i
     sb = (long long)sel * env.E + e;
 }
 
-// Register state from memory in ONE load round: nothing waits for the active-scene index (the
-// scene-dependent values are read from both buffers and selected afterwards); then, without a
-// wait, the pair probabilities the first step can move the pointer to (load_cur_pair).
-template <int TPL>
+// Register state from memory. PF (single-step launches): ONE load round -- nothing waits for the
+// active-scene index (the scene-dependent values are read from both buffers and selected
+// afterwards) -- and then, without a wait, the pair probabilities the first step can move the
+// pointer to (load_cur_pair). Multi-step launches load once per launch and keep the plain order
+// (scene index, scene values, state): fewer live registers in their step loop.
+template <int TPL, bool PF = false>
 __device__ void load_regs(EnvRegs<TPL>& R, const uavhip_env& env, int e, int lane) {
     const int N = env.N, M = env.M;
+    if constexpr (!PF) {
+        load_scene_index(env, e, R.sel, R.stale, R.gen, R.sb);
+        load_scene_regs(R, env, lane);
+#pragma unroll
+        for (int k = 0; k < TPL; ++k) {
+            const int t = lane + kWave * k;
+            const long long o = (long long)e * M + t;
+            const bool v = t < M;
+            R.nhf[k] = v ? env.nh_final[o] : 1.0;
+            R.nhp[k] = v ? env.nh_pure[o] : 1.0;
+            R.tc[k] = v ? env.t_cost[o] : 0.0;
+            R.nlk[k] = v ? env.n_lock[o] : 0;
+        }
+        R.asg = lane < N ? env.assigned[(long long)e * N + lane] : -1;
+        const int* is = env.istate + (long long)e * UAVHIP_IST_COUNT;
+        const double* ds = env.dstate + (long long)e * UAVHIP_DST_COUNT;
+        R.u = is[UAVHIP_IST_UAV_IDX];
+        R.t = is[UAVHIP_IST_TARGET_IDX];
+        R.ncov = is[UAVHIP_IST_N_COVERED];
+        R.nasg = is[UAVHIP_IST_N_ASSIGNED];
+        R.ep = is[UAVHIP_IST_EPISODE];
+        R.err = is[UAVHIP_IST_ERROR];
+        R.r = ds[UAVHIP_DST_R];
+        R.J = ds[UAVHIP_DST_J];
+        R.asg_cost = ds[UAVHIP_DST_ASG_COST];
+        R.cov_val = ds[UAVHIP_DST_COV_VALUE];
+        R.tot_cost = ds[UAVHIP_DST_TOTAL_COST];
+        R.tot_val = ds[UAVHIP_DST_TOTAL_VALUE];
+        set_scene_divisors(R);
+        set_step_divisors(R, env, lane);
+        R.sum_pd = ds[UAVHIP_DST_SUM_PDMG];
+        R.sum_pf = ds[UAVHIP_DST_SUM_PFIN];
+        const float* w = env.window + (long long)e * kObs;
+        R.w0 = w[lane];
+        R.w1 = lane < kObs - kWave ? w[kWave + lane] : 0.0f;
+        R.pd_cur = ds[UAVHIP_DST_PD_CUR];
+        R.pp_cur = R.u < N ? readlane_d(R.ppen, R.u) : 0.0;
+        drain_loads();
+        return;
+    }
     const int* is = env.istate + (long long)e * UAVHIP_IST_COUNT;
     const double* ds = env.dstate + (long long)e * UAVHIP_DST_COUNT;
     const int nb = env.scene_buffers;

@@ -69,10 +69,12 @@ __device__ void gload_scene_regs(GRegs& R, const uavhip_env& env, int j) {
     drain_loads();
 }
 
-// tab == nullptr (single-step use inside the fused rollout launch): pair probabilities are read
-// from the global p_dmg table instead of an LDS copy
+// TAB = false (single-step use inside the fused rollout launch): pair probabilities are read from
+// the global p_dmg table instead of an LDS copy. A compile-time choice: a global load that MAY be
+// in flight in the step loop would make every later use wait for all the step's stores.
+template <bool TAB = true>
 __device__ void gload_table(GRegs& R, const uavhip_env& env, int j) {
-    if (!R.tab) return;
+    if (!TAB) return;
     const int NM = env.N * env.M;
     const double* src = env.p_dmg + R.sb * NM;
     for (int i = j; i < NM; i += L) R.tab[i] = src[i];
@@ -81,9 +83,10 @@ __device__ void gload_table(GRegs& R, const uavhip_env& env, int j) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+template <bool TAB = true>
 __device__ __forceinline__ void gload_cur_pair(GRegs& R, const uavhip_env& env) {
     if (R.u < env.N) {
-        R.pd_cur = R.tab ? R.tab[R.u * env.M + R.t] : env.p_dmg[(R.sb * env.N + R.u) * env.M + R.t];
+        R.pd_cur = TAB ? R.tab[R.u * env.M + R.t] : env.p_dmg[(R.sb * env.N + R.u) * env.M + R.t];
         R.pp_cur = gsh_d(R.ppen, R.u);
     } else {
         R.pd_cur = 0.0;
@@ -161,6 +164,7 @@ __device__ void gwrite_info(const GRegs& R, double is_valid, double* o, int j) {
 }
 
 // uav_env.py:42-63,175-182 (envdev::reset_regs)
+template <bool TAB = true>
 __device__ void greset_regs(GRegs& R, const uavhip_env& env, int j, bool scene) {
     R.nhf = 1.0;
     R.nhp = 1.0;
@@ -184,13 +188,13 @@ __device__ void greset_regs(GRegs& R, const uavhip_env& env, int j, bool scene) 
     R.w0 = 0.0f;
     R.w1 = 0.0f;
     R.w2 = 0.0f;
-    gload_cur_pair(R, env);
+    gload_cur_pair<TAB>(R, env);
     gpush_obs(R, j);
 }
 
-// Register state from memory in one load round (scene-dependent values read from both scene
-// buffers and selected after the wait, as envdev::load_regs). gload_issue only issues the loads
-// (the fused rollout launch overlaps them with the critic head); gload_finish consumes them.
+// Single-step use (the fused rollout launch): register state in one load round, scene-dependent
+// values read from both scene buffers and selected after the wait (as envdev::load_regs<PF>).
+// gload_issue only issues the loads (overlapped with the critic head); gload_finish consumes them.
 struct GPending {
     double valb[2], ucb[2], ppb[2];
     int sel_raw;
@@ -249,11 +253,46 @@ __device__ __forceinline__ void gload_finish(GRegs& R, const GPending& q, const 
     R.rcp_n = 1.0 / (double)(j + 1);
     R.pp_cur = R.u < N ? gsh_d(R.ppen, R.u) : 0.0;
 }
+// Multi-step launches (once per launch): the plain order, scene index first (fewer live registers).
 __device__ void gload_regs(GRegs& R, const uavhip_env& env, int e, int j) {
-    GPending q;
-    gload_issue(R, q, env, e, j);
+    const int N = env.N, M = env.M;
+    load_scene_index(env, e, R.sel, R.stale, R.gen, R.sb);
+    R.val = j < M ? env.tgt_value[R.sb * M + j] : 0.0;
+    R.ucost = j < N ? env.uav_cost[R.sb * N + j] : 0.0;
+    R.ppen = j < N ? env.p_pen[R.sb * N + j] : 0.0;
+    const long long o = (long long)e * M + j;
+    const bool v = j < M;
+    R.nhf = v ? env.nh_final[o] : 1.0;
+    R.nhp = v ? env.nh_pure[o] : 1.0;
+    R.tc = v ? env.t_cost[o] : 0.0;
+    R.nlk = v ? env.n_lock[o] : 0;
+    R.asg = j < N ? env.assigned[(long long)e * N + j] : -1;
+    const int* is = env.istate + (long long)e * UAVHIP_IST_COUNT;
+    const double* ds = env.dstate + (long long)e * UAVHIP_DST_COUNT;
+    R.u = is[UAVHIP_IST_UAV_IDX];
+    R.t = is[UAVHIP_IST_TARGET_IDX];
+    R.ncov = is[UAVHIP_IST_N_COVERED];
+    R.nasg = is[UAVHIP_IST_N_ASSIGNED];
+    R.ep = is[UAVHIP_IST_EPISODE];
+    R.err = is[UAVHIP_IST_ERROR];
+    R.r = ds[UAVHIP_DST_R];
+    R.J = ds[UAVHIP_DST_J];
+    R.asg_cost = ds[UAVHIP_DST_ASG_COST];
+    R.cov_val = ds[UAVHIP_DST_COV_VALUE];
+    R.tot_cost = ds[UAVHIP_DST_TOTAL_COST];
+    R.tot_val = ds[UAVHIP_DST_TOTAL_VALUE];
+    R.sum_pd = ds[UAVHIP_DST_SUM_PDMG];
+    R.sum_pf = ds[UAVHIP_DST_SUM_PFIN];
+    R.pd_cur = ds[UAVHIP_DST_PD_CUR];
+    const float* w = env.window + (long long)e * kObs;
+    R.w0 = w[j];
+    R.w1 = w[L + j];
+    R.w2 = j < kObs - 2 * L ? w[2 * L + j] : 0.0f;
     drain_loads();
-    gload_finish(R, q, env, e, j);
+    gset_scene_divisors(R);
+    R.rcp_m = 1.0 / (double)M;
+    R.rcp_n = 1.0 / (double)(j + 1);
+    R.pp_cur = R.u < N ? gsh_d(R.ppen, R.u) : 0.0;
 }
 
 __device__ void gstore_regs(const GRegs& R, const uavhip_env& env, int e, int j) {
@@ -295,6 +334,7 @@ __device__ void gstore_regs(const GRegs& R, const uavhip_env& env, int e, int j)
 }
 
 // One UAVEnv.step (uav_env.py:295-435) of this group's env (envdev::step_once).
+template <bool TAB = true>
 __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int auto_reset, float* obs_o,
                       double* rew_o, uint8_t* done_o, double* info_o) {
     const int N = env.N, M = env.M;
@@ -374,7 +414,7 @@ __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int 
         if (done_o) *done_o = done ? 1 : 0;
     }
     if (!done) {
-        gload_cur_pair(R, env);
+        gload_cur_pair<TAB>(R, env);
         gpush_obs(R, j);
         if (obs_o) gwrite_obs(obs_o, R, j, false, obs_f16(env));
     } else if (auto_reset) {
@@ -386,13 +426,13 @@ __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int 
                 R.sel ^= 1;
                 R.stale = 1;
                 R.sb = (long long)R.sel * env.E + e;
-                gload_table(R, env, j);
+                gload_table<TAB>(R, env, j);
                 flipped = true;
             } else {
                 R.err |= 2;  // no fresh spare: keep the scene (state-only reset)
             }
         }
-        greset_regs(R, env, j, flipped);
+        greset_regs<TAB>(R, env, j, flipped);
         if (obs_o) gwrite_obs(obs_o, R, j, false, obs_f16(env));
     } else {
         if (obs_o) gwrite_obs(obs_o, R, j, true, obs_f16(env));  // _get_obs returns zeros when done (:188-189)

@@ -1013,15 +1013,15 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
             R.tab = nullptr;
             R.win = sm.h + (2 * wv + g) * envgrp::kWin;
             envgrp::gload_finish(R, gq, env, e, j);
-            envgrp::gstep(R, env, e, j, sm.mask[2 * wv + g], eo.auto_reset, obs_at(eo.obs, e, obs_f16(env)),
+            envgrp::gstep<false>(R, env, e, j, sm.mask[2 * wv + g], eo.auto_reset, obs_at(eo.obs, e, obs_f16(env)),
                           eo.rew + e, eo.done + e, eo.info ? eo.info + (size_t)e * UAVHIP_INFO_COUNT : nullptr);
             envgrp::gstore_regs(R, env, e, j);
         } else if (e0 < B) {
             const bool two = e0 + 1 < B;
             EnvRegs<1> R0, R1;
             R0.row = R1.row = sm.x + 16 * wv;
-            load_regs(R0, env, e0, lane);
-            if (two) load_regs(R1, env, e0 + 1, lane);
+            load_regs<1, true>(R0, env, e0, lane);
+            if (two) load_regs<1, true>(R1, env, e0 + 1, lane);
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
                 if (k == 1 && !two) break;
