@@ -16,7 +16,8 @@ from uavhip import _lib  # noqa: E402
 from uavhip.policy import TransformerActorCritic  # noqa: E402
 from uavhip.train import FusedPPOTrainer  # noqa: E402
 
-NAMES = {0: "start", 1: "heads bwd", 2: "c.head.0", 52: "c.embed", 53: "a.head.0", 54: "a.embed"}
+NAMES = {0: "start", 1: "heads bwd", 2: "c.head.0", 52: "c.embed", 53: "a.head.0", 54: "a.embed",
+         55: "c.emb loads", 56: "c.emb acc", 57: "a.emb loads", 58: "a.emb acc"}
 LAYER = ["start", "LN2", "sync", "du gemm", "sync", "W1 gemm", "sync", "LN1", "sync", "Wo gemm", "sync",
          "attn0+sync", "Win0+sync", "attn1+sync", "Win1", "res+sync"]
 for base, tag in ((4, "C1"), (20, "C0"), (36, "A")):
@@ -46,7 +47,7 @@ buf = np.zeros(256 * 2 * 64, np.uint64)
 assert fn(buf.ctypes.data, buf.size) == 0
 t = buf.reshape(256, 2, 64).astype(np.int64)
 t = t[:min(256, bs // 16)]
-slots = sorted(k for k in NAMES if (t[:, 0, k] != 0).all())
+slots = sorted((k for k in NAMES if (t[:, 0, k] != 0).all()), key=lambda k: np.median(t[:, 0, k] - t[:, 0, 0]))
 rel = t - t[:, :, 0:1]
 print(f"BS={bs}; median cycles since block start (wave0 / wave4) and per-phase delta (wave0)")
 prev = 0

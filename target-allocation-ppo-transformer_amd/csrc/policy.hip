@@ -1285,9 +1285,27 @@ __device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, int c, i
 
 // Backward of one post-LN encoder layer. On entry sm.h holds dL/d(layer output) for the tokens
 // >= qtok0; on exit sm.h holds dL/d(layer input) for all 80 tokens. Ends with a barrier.
+// The embedding backward's global inputs (embed_bwd): this thread's 20 embedding values (the ReLU
+// mask) and one float4 of the input windows, loaded by the layer-0 backward right after its last
+// GEMM (every weight load of the layer issued: nothing waits behind them), so their latency hides
+// under the layer's final residual pass and barrier.
+struct EmbBwdPre {
+    float ev[TOK / 4];
+    f32x4 xv;
+};
+__device__ __forceinline__ void embed_bwd_load(EmbBwdPre& ep, const float* __restrict__ e, const float* __restrict__ xg,
+                                               int b0) {
+    const int f = threadIdx.x & (D - 1), grp = threadIdx.x >> 7;
+#pragma unroll
+    for (int i = 0; i < TOK / 4; ++i) ep.ev[i] = e[(size_t)trow(grp + 4 * i, b0) * D + f];
+    const int i = threadIdx.x;
+    ep.xv = i < TOK * LDX / 4 ? ld4(xg + (size_t)trow(i / (LDX / 4), b0) * 16 + 4 * (i % (LDX / 4)))
+                              : f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
 template <int trunk, int layer, bool last, int TB>
 __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __restrict__ PT, const BwdLayerIO& io,
-                          int b0) {
+                          int b0, EmbBwdPre* ep = nullptr, const float* e_emb = nullptr, const float* xg = nullptr) {
     BTR(TB);
     constexpr int CTQ = last ? 1 : S;
     constexpr int DQ = depth<CTQ>();
@@ -1413,6 +1431,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         if (c == 0) __syncthreads();  // big is rewritten by chunk 1
         BTR(TB + 12 + 2 * c);
     }
+    if (layer == 0 && ep) embed_bwd_load(*ep, e_emb, xg, b0);
     // + dz1 on the rows that carried the residual -> sm.h
 #pragma unroll
     for (int ct = 0; ct < S; ++ct) {
@@ -1427,17 +1446,11 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
 // Embedding backward from sm.h = dL/d(h0) (80 tokens): h0 = relu(We x + be) + pos. Thread =
 // (feature, token group of 20); partials reduced over the 4 groups through sm.big -> part [2560]
 // in the parameters' order (pos | We | be).
-__device__ void embed_bwd(Smem& sm, const float* __restrict__ e, const float* __restrict__ xg,
-                          float* __restrict__ part, int b0) {
+__device__ void embed_bwd(Smem& sm, const EmbBwdPre& ep, float* __restrict__ part, int tb = 55) {
     const int f = threadIdx.x & (D - 1), grp = threadIdx.x >> 7;
-    float ev[TOK / 4];  // this thread's embedding values (the ReLU mask), loaded with the windows
-#pragma unroll
-    for (int i = 0; i < TOK / 4; ++i) ev[i] = e[(size_t)trow(grp + 4 * i, b0) * D + f];
-    for (int i = threadIdx.x; i < TOK * LDX / 4; i += NTHR) {  // input windows (sm.x was scratch)
-        const int t = i / (LDX / 4), q = i % (LDX / 4);
-        st4(sm.x + t * LDX + 4 * q, ld4(xg + (size_t)trow(t, b0) * 16 + 4 * q));
-    }
+    if (threadIdx.x < TOK * LDX / 4) st4(sm.x + 4 * threadIdx.x, ep.xv);  // input windows (sm.x was scratch)
     __syncthreads();
+    BTR(tb);
     float acc[IN + 1 + S];
 #pragma unroll
     for (int v = 0; v < IN + 1 + S; ++v) acc[v] = 0.f;
@@ -1446,15 +1459,22 @@ __device__ void embed_bwd(Smem& sm, const float* __restrict__ e, const float* __
         const int tok = grp + 4 * i;  // position tok / 16 = i / 4
         const float gv = sm.h[tok * LDH + f];
         acc[IN + 1 + i / 4] += gv;
-        const float gp = ev[i] > 0.f ? gv : 0.f;
+        const float gp = ep.ev[i] > 0.f ? gv : 0.f;
         acc[IN] += gp;
+        float xr[LDX];  // the token's window row: 4 broadcast b128 reads
 #pragma unroll
-        for (int k = 0; k < IN; ++k) acc[k] += gp * sm.x[tok * LDX + k];
+        for (int q = 0; q < LDX / 4; ++q) {
+            const f32x4 x4 = ld4(sm.x + tok * LDX + 4 * q);
+            xr[4 * q] = x4.x; xr[4 * q + 1] = x4.y; xr[4 * q + 2] = x4.z; xr[4 * q + 3] = x4.w;
+        }
+#pragma unroll
+        for (int k = 0; k < IN; ++k) acc[k] += gp * xr[k];
     }
     constexpr int NV = IN + 1 + S;  // 20
 #pragma unroll
     for (int v = 0; v < NV; ++v) sm.big[(grp * NV + v) * D + f] = acc[v];
     __syncthreads();
+    BTR(tb + 1);
     for (int o = threadIdx.x; o < NV * D; o += NTHR) {
         const int v = o >> 7, ff = o & (D - 1);
         const float s = (sm.big[v * D + ff] + sm.big[(NV + v) * D + ff]) +
@@ -1591,16 +1611,20 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
     __syncthreads();
     BTR(2);
     bwd_layer<kCriticTrunk, 1, true, 4>(sm, P, PT + 2 * kLayerT, io.L[2], b0);
-    bwd_layer<kCriticTrunk, 0, false, 20>(sm, P, PT + 1 * kLayerT, io.L[1], b0);
-    embed_bwd(sm, io.e[1], io.xg, io.epart + ((size_t)blockIdx.x * 2 + 1) * kEmbPart, b0);
+    {
+        EmbBwdPre ep;
+        bwd_layer<kCriticTrunk, 0, false, 20>(sm, P, PT + 1 * kLayerT, io.L[1], b0, &ep, io.e[1], io.xg);
+        embed_bwd(sm, ep, io.epart + ((size_t)blockIdx.x * 2 + 1) * kEmbPart);
+    }
     __syncthreads();
     BTR(52);
     // actor: head.0, layer 0 (pruned), embedding
     head_input_grad(sm, PT + kHeadT, sm.z);
     __syncthreads();
     BTR(53);
-    bwd_layer<kActorTrunk, 0, true, 36>(sm, P, PT, io.L[0], b0);
-    embed_bwd(sm, io.e[0], io.xg, io.epart + (size_t)blockIdx.x * 2 * kEmbPart, b0);
+    EmbBwdPre ep;
+    bwd_layer<kActorTrunk, 0, true, 36>(sm, P, PT, io.L[0], b0, &ep, io.e[0], io.xg);
+    embed_bwd(sm, ep, io.epart + (size_t)blockIdx.x * 2 * kEmbPart, 57);
     BTR(54);
 }
 
