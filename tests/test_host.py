@@ -204,3 +204,24 @@ def test_csv_rows_follow_main_train_columns():
     assert rows[0][:9] == [1, "2.0000", "0.5000", "2.0000", 3, "0.5000", "0.5000", "0.4000", "0.2000"]
     assert rows[1][:9] == [2, "3.0000", "1.0000", "0.0000", 0, "0.0000", "0.0000", "0.0000", "0.0000"]
     assert rows[1][9:] == ["0.250000", "-0.500000", "0.690000"]
+
+
+def test_rollout_step_argument_checks_without_gpu():
+    """uavhip_rollout_step rejects a bad env descriptor, a policy of another architecture and env
+    dims beyond the one-env-per-wave layout (N, M <= 64) before any HIP call."""
+    import ctypes
+    from uavhip import _lib
+    d = _lib.EnvDesc()
+    d.E, d.N, d.M, d.Kn, d.Ki, d.scene_buffers = 4, 100, 4, 1, 1, 1
+    pol = _lib.PolicyDesc()
+    args = (None, None, 0, 1, ctypes.c_uint64(0), ctypes.c_uint64(0), None, None, None, None, 1, None, None, None,
+            None, None)
+    assert _lib.LIB.uavhip_rollout_step(pol, d, *args) == -1
+    assert b"bad env dims" in _lib.LIB.uavhip_last_error()
+    d.N = 8
+    for name in ("uav_pos", "uav_vel", "uav_load", "uav_cost", "tgt_pos", "tgt_vel", "tgt_value", "tgt_id", "nfz_pos",
+                 "icp_pos", "icp_vel", "p_dmg", "p_pen", "istate", "nh_final", "nh_pure", "t_cost", "n_lock",
+                 "assigned", "dstate", "window"):
+        setattr(d, name, 16)  # non-NULL placeholders: validation never dereferences them
+    assert _lib.LIB.uavhip_rollout_step(pol, d, *args) == -1
+    assert b"uavhip_rollout_step" in _lib.LIB.uavhip_last_error()  # NULL weights / states
