@@ -45,6 +45,8 @@ POLICY_FLOP_PER_SAMPLE = 2_446_208  # full-window forward (last-
 # the rollout's window-row path (uavhip_policy_forward_rows) forms layer-0 Q|K|V of the new row
 # only: minus 4 rows x (actor K,V 256 + critic Q,K,V 384) x 128 x 2 FLOP
 ROWS_FLOP_PER_SAMPLE = POLICY_FLOP_PER_SAMPLE - 4 * (256 + 384) * 128 * 2  # 1,790,848
+TRAIN_FLOP_PER_SAMPLE_EPOCH = 3 * 4_040_000  # training ~ 3 x dense forward
+TRAIN_EXEC_FLOP_PER_SAMPLE_EPOCH = 7_460_000  # pruned forward + dX + dW
 MFMA_F32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: fp32 MFMA = vector peak
 HBM_PEAK_GBS = 8000.0
 
@@ -257,10 +259,23 @@ def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
         t = torch.tensor([pdt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         pdt = t.item()
+    se = n * 5 / pdt
+    # whole-node MFMA rate of the update: SURVEY 8(d)'s algorithmic training work (3 x the dense
+    # forward per sample-epoch) and the work the HIP step executes (last layers pruned: forward 2.45
+    # + input gradients 2.62 + weight gradients 2.39 MFLOP), over all GPUs
+    alg_tf = se * TRAIN_FLOP_PER_SAMPLE_EPOCH / 1e12
+    exe_tf = se * TRAIN_EXEC_FLOP_PER_SAMPLE_EPOCH / 1e12
+    peak = MFMA_F32_PEAK_TFLOPS * world
     return {"value": n / pdt, "unit": "PPO samples/s (whole node: transitions in the update batch / update "
            "wall time, 5 epochs)", "epochs": 5, "minibatch_per_gpu": args.ppo_minibatch,
            "global_minibatch": args.ppo_minibatch * world, "optimizer_steps": cnt, "batch": n,
-           "sample_epochs_per_s": n * 5 / pdt, "impl": impl}
+           "sample_epochs_per_s": se, "impl": impl,
+           "roofline": {"bound": "mfma", "unit": "TFLOP/s", "peak": peak, "achieved": alg_tf, "frac": alg_tf / peak,
+                        "flop_per_sample_epoch": TRAIN_FLOP_PER_SAMPLE_EPOCH,
+                        "flop_source": "SURVEY.md 8(d): 3 x the dense forward (4.04 MFLOP) per sample-epoch",
+                        "executed_flop_per_sample_epoch": TRAIN_EXEC_FLOP_PER_SAMPLE_EPOCH,
+                        "executed_achieved": exe_tf, "executed_frac": exe_tf / peak,
+                        "timing": "update wall time (all kernels of the step, launches included)"}}
 
 
 def main():
