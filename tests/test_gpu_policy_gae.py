@@ -422,3 +422,56 @@ def test_fused_rollout_step_matches_two_launches(E, N, M, period):
         assert res[1][5].any()  # episodes ended inside the rollout
     for i, (a, b) in enumerate(zip(*res)):
         assert torch.equal(a, b), i
+
+
+def test_fused_rollout_step_vs_oracle(traj_npz):
+    """The rollout hot path against the CPU oracle directly: uavhip_rollout_step over the fixture
+    scenes of one shape (several copies each, state-only auto-reset), every sampled action replayed
+    through oracle.OracleEnv -- done flags bit-exact, rewards to 1e-12, next windows to the fp32 bar
+    -- and logp / value against the torch forward of the same windows and actions."""
+    import oracle
+    from uavhip.policy import TransformerActorCritic, rowproj_buffer
+    from uavhip.vec_env import VecUAVEnv
+    groups = {}
+    for c in cases(traj_npz):
+        s = sub(traj_npz, c["key"])
+        key = (c["N"], c["M"], len(s["nfz_pos"]), len(s["icp_pos"]), tuple(s["params"]))
+        groups.setdefault(key, []).append(s)
+    (N, M, Kn, Ki, prm), scenes = max(((k, g) for k, g in groups.items() if k[0] <= 64 and k[1] <= 64),
+                                      key=lambda kv: kv[0][0] * kv[0][1] * len(kv[1]))
+    scenes = (scenes * 8)[:48]
+    E = len(scenes)
+    torch.manual_seed(2)
+    net = TransformerActorCritic().cuda()
+    v = VecUAVEnv(E, N, M, Kn, Ki, full_reset_period=0)
+    v.set_params(np.array(prm))
+    v.load_scenes(scenes)
+    obs = v.reset(episode=1).clone()
+    refs = [oracle.OracleEnv(sc, np.array(prm)) for sc in scenes]
+    for r in refs:
+        r.reset()
+    rp = rowproj_buffer(E)
+    net.packed_weights()
+    n_done = 0
+    for t in range(40):
+        act = torch.empty(E, dtype=torch.int8, device="cuda")
+        lp, val = torch.empty(E, device="cuda"), torch.empty(E, device="cuda")
+        nxt = torch.empty_like(obs)
+        rew = torch.empty(E, dtype=torch.float64, device="cuda")
+        dn = torch.empty(E, dtype=torch.uint8, device="cuda")
+        net.rollout_step(v, obs, rp, t, t == 0, act, lp, val, nxt, rew, dn, seed=9, offset=t * E)
+        with torch.no_grad():
+            lp_t, v_t, _ = net.evaluate(obs, act.long())
+        torch.testing.assert_close(lp, lp_t, rtol=1e-4, atol=2e-5)
+        torch.testing.assert_close(val, v_t[:, 0], rtol=1e-4, atol=1e-4)
+        a_h, r_h, d_h, o_h = act.cpu().numpy(), rew.cpu().numpy(), dn.cpu().numpy(), nxt.cpu().numpy()
+        for e in range(E):
+            o_c, r_c, d_c, _ = refs[e].step(int(a_h[e]))
+            assert bool(d_h[e]) == d_c, (t, e)
+            assert abs(r_h[e] - r_c) <= 1e-12 * max(1.0, abs(r_c)), (t, e, r_h[e], r_c)
+            if d_c:
+                n_done += 1
+                o_c = refs[e].reset()
+            np.testing.assert_allclose(o_h[e], o_c, rtol=2e-6, atol=1e-6)
+        obs = nxt
+    assert n_done > 0
