@@ -302,6 +302,14 @@ inline const float* prm(const uavhip_ppo* c, int i) { return c->params + kOffs.o
 using namespace uavhip;
 using namespace uavhip::tr;
 
+#ifdef UAVHIP_POLICY_TRACE
+extern "C" int uavhip_wgrad_trace(unsigned long long* out, int n) {  // k_wgrad stamps (TRACE build)
+    const int total = kWgGrid * 16;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wtrace), sizeof(unsigned long long) * (n < total ? n : total), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int64_t uavhip_ppo_workspace_floats(int32_t minibatch) {
     if (minibatch <= 0 || minibatch % 64) return -1;
     return (int64_t)make_plan(minibatch, nullptr).total;

@@ -56,6 +56,18 @@ struct WgBatch {
 typedef __attribute__((address_space(3))) void wg_lds_void;
 typedef __attribute__((address_space(1))) void wg_glob_void;
 
+// Stamps (make TRACE=1 only): per workgroup, s_memtime at kernel start and, per run, after the
+// first slab landed / after the k-loop / after the epilogue (uavhip_wgrad_trace copies them out).
+#ifdef UAVHIP_POLICY_TRACE
+__device__ unsigned long long g_wtrace[kWgGrid * 16];
+#define WTR(slot)                                                                                   \
+    do {                                                                                            \
+        if (threadIdx.x == 0 && (slot) < 16) g_wtrace[blockIdx.x * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define WTR(slot) do {} while (0)
+#endif
+
 __device__ __forceinline__ int wg_find(const WgBatch& b, int u) {
     int lo = 0, hi = b.n;
     while (hi - lo > 1) {
@@ -92,6 +104,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
     int u = (int)(blockIdx.x * U / G);
     const int u_end = (int)((blockIdx.x + 1) * U / G);
     int run = 0;
+    WTR(0);
     while (u < u_end) {
         const int pi = wg_find(wb, u);
         const WgProb& P = wb.p[pi];
@@ -107,6 +120,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
         wg_load_slab(P.A, P.lda, s0 * kWgBK, m0, P.M, wg_smem);
         wg_load_slab(P.B, P.ldb, s0 * kWgBK, n0, P.N, wg_smem + kWgBK * kWgT);
         __syncthreads();  // waits vmcnt(0): the first slab has landed
+        WTR(1 + 4 * run);
         for (int s = 0; s < n_slabs; ++s) {
             const int cur = s & 1;
             if (s + 1 < n_slabs) {
@@ -129,6 +143,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
             }
             __syncthreads();  // next slab landed (vmcnt(0)); everyone is done reading this one
         }
+        WTR(2 + 4 * run);
         // k-parity 1 -> LDS, parity 0 adds and stores. Lane (i16, g) of tile (a, b) holds
         // dW[m0 + qm + 16 g + 4 r + a][n0 + qn + 4 i16 + b], r = 0..3.
         float* red = wg_smem + quad * 64 * 64;
@@ -154,6 +169,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
                 }
         }
         __syncthreads();  // LDS is reloaded by the next run
+        WTR(3 + 4 * run);
         u += n_slabs;
         ++run;
     }
