@@ -434,17 +434,23 @@ __device__ void embed(Smem& sm, const float* __restrict__ P, float* e_out = null
 // K/V weight row of wave wv for chunk c: waves 0-3 K tiles, waves 4-7 V tiles
 __device__ __forceinline__ int kv_row(int wv, int c) { return (1 + (wv >> 2)) * D + 64 * c + 16 * (wv & 3); }
 
-template <int trunk, int layer, bool last, bool TR>
+// A caller's hook run inside layer_tail after the FFN2 GEMM, before the LN2 epilogue (training
+// mode: the next phase's global loads issued ahead of LN2's activation stores -- the vector memory
+// counter retires in order, so a load behind a store burst waits for the whole burst).
+struct NoHook {
+    __device__ void operator()() const {}
+};
+template <int trunk, int layer, bool last, bool TR, class F = NoHook>
 __device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P, const APre<depth<last ? 1 : S>()>& po,
-                           const TrainLayerIO& io, int b0);
+                           const TrainLayerIO& io, int b0, F pre_ln2 = F{});
 
 // One post-LN nn.TransformerEncoderLayer (relu FFN 256, 8 heads). last: prune to column tile 4.
 // Work split: 8 waves, wave w and w+4 share a SIMD (and its MFMA pipe); every GEMM gives each
 // SIMD the same number of 16-row output tiles. `pkv` = the caller's prefetch of this layer's first
 // K/V weight blocks. Ends WITHOUT a final barrier: the caller prefetches its next weights, then syncs.
-template <int trunk, int layer, bool last, bool TR = false>
+template <int trunk, int layer, bool last, bool TR = false, class F = NoHook>
 __device__ __forceinline__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv,
-                              const TrainLayerIO& io = TrainLayerIO{}, int b0 = 0) {
+                              const TrainLayerIO& io = TrainLayerIO{}, int b0 = 0, F pre_ln2 = F{}) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
     PTR(tb);
     const float* Win = P + kOffs.o[layer_param(trunk, layer, INW)];
@@ -484,14 +490,14 @@ __device__ __forceinline__ void encoder_layer(Smem& sm, const float* __restrict_
         __syncthreads();
         PTR(tb + 3 + 3 * c);
     }
-    layer_tail<trunk, layer, last, TR>(sm, P, po, io, b0);
+    layer_tail<trunk, layer, last, TR>(sm, P, po, io, b0, pre_ln2);
 }
 
 // Out-projection + LN1 + FFN + LN2 of an encoder layer, after the attention output is in sm.ctx.
 // `po` = the caller's prefetch of the first out_proj weight blocks.
-template <int trunk, int layer, bool last, bool TR>
+template <int trunk, int layer, bool last, bool TR, class F>
 __device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P, const APre<depth<last ? 1 : S>()>& po,
-                           const TrainLayerIO& io, int b0) {
+                           const TrainLayerIO& io, int b0, F pre_ln2) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
     const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
     const float* bo = P + kOffs.o[layer_param(trunk, layer, OUTB)];
@@ -537,6 +543,7 @@ __device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P
     gemm_tile<CTQ, DQ>(acc2, pf2a, W2, FF, 16 * wv, 0, sm.big, LDF, qtok0);
     gemm_tile<CTQ, DQ>(acc2, pf2b, W2, FF, 16 * wv, 128, sm.ctx, LDF, qtok0);
     PTR(tb + 12);
+    pre_ln2();
     residual_layernorm<CTQ, TR>(sm, acc2, b2, P + kOffs.o[layer_param(trunk, layer, N2W)],
                                 P + kOffs.o[layer_param(trunk, layer, N2B)], qtok0,
                                 LnOut{io.xhat2, io.h2, io.rstd2, b0, last});
@@ -923,15 +930,28 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         PTR(2);
         __syncthreads();
         encoder_layer_rows<kActorTrunk>(sm, P, pw, rp, rio, b0);
-    } else {
+    }
+    // training mode: the actor head's and the critic embedding's / first GEMM's operands are loaded
+    // ahead of the actor's LN2 activation stores (layer_tail hook)
+    APre<4> ph;
+    [[maybe_unused]] EmbPre ep_c;
+    [[maybe_unused]] APre<2> pkv_c;
+    if constexpr (!ROWS) {
         APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
         embed<kActorTrunk, TR>(sm, P, io.e[0], io.h0[0], b0);
         PTR(2);
         __syncthreads();
-        encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0);
+        if constexpr (TR) {
+            encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0, [&] {
+                if (wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
+                ep_c = embed_load<kCriticTrunk>(P);
+                pkv_c = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+            });
+        } else {
+            encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0);
+        }
     }
-    APre<4> ph;
-    if (wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
+    if (!TR && wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
     __syncthreads();
     PTR(3);
     head_mlp<kActorHead, 2>(sm, P, ph, sm.logits);
@@ -944,15 +964,31 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         rows_prologue<kCriticTrunk>(sm, P, pw, rp, rio, b0);
         __syncthreads();
         encoder_layer_rows<kCriticTrunk>(sm, P, pw, rp, rio, b0);
-    } else {
-        APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-        embed<kCriticTrunk, TR>(sm, P, io.e[1], io.h0[1], b0);
-        __syncthreads();
-        encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv, io.L[1], b0);
     }
-    APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
+    APre<2> pkv;
+    if constexpr (!ROWS) {
+        if constexpr (TR) {
+            embed_apply<kCriticTrunk, TR>(sm, ep_c, io.e[1], io.h0[1], b0);
+            __syncthreads();
+            encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv_c, io.L[1], b0, [&] {
+                pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
+            });
+        } else {
+            APre<2> pkv0 = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+            embed<kCriticTrunk, TR>(sm, P, io.e[1], io.h0[1], b0);
+            __syncthreads();
+            encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv0, io.L[1], b0);
+        }
+    }
+    if (!TR) pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
     __syncthreads();
-    encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0);
+    if constexpr (TR) {
+        encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0, [&] {
+            if (wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
+        });
+    } else {
+        encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0);
+    }
     // fused env step, two envs per wave side by side: its state loads are issued here and land
     // while the critic head runs
     [[maybe_unused]] const bool env_grp =
@@ -962,7 +998,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     if constexpr (ENV) {
         if (env_grp) envgrp::gload_issue(gR, gq, env, b0 + 2 * wv + (lane_id() >> 5), lane_id() & 31);
     }
-    if (wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
+    if (!TR && wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
     __syncthreads();
     PTR(5);
     head_mlp<kCriticHead, 1>(sm, P, ph, sm.value);
