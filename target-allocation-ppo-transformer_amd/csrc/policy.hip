@@ -533,13 +533,13 @@ __device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P
     PTR(tb + 10);
     __syncthreads();
     PTR(tb + 11);
+    const APre<DQ> pf2b = prefetch<DQ>(W2, FF, 16 * wv, 128);
     if (TR) {  // FFN hidden (post-ReLU): features 0-127 in big, 128-255 in ctx
         store_rows(sm.big, LDF, io.u, FF, 0, D, qtok0, b0, last);
         store_rows(sm.ctx, LDF, io.u, FF, D, D, qtok0, b0, last);
     }
     f32x4 acc2[CTQ];
     zero(acc2);
-    const APre<DQ> pf2b = prefetch<DQ>(W2, FF, 16 * wv, 128);
     gemm_tile<CTQ, DQ>(acc2, pf2a, W2, FF, 16 * wv, 0, sm.big, LDF, qtok0);
     gemm_tile<CTQ, DQ>(acc2, pf2b, W2, FF, 16 * wv, 128, sm.ctx, LDF, qtok0);
     PTR(tb + 12);
