@@ -1362,6 +1362,9 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
     __syncthreads();
     BTR(TB + 2);
     // du = relu'(u) (W2^T df): 256 hidden features, wave wv owns tiles 16 wv (-> big) and 128 + 16 wv (-> h)
+    // the next GEMM's first weight blocks are loaded before each tile's du stores (a load issued
+    // behind a store burst waits for the whole burst)
+    APre<DQ> pb;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         const int row = 128 * t + 16 * wv;
@@ -1370,8 +1373,13 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         for (int ct = 0; ct < CTQ; ++ct)
             uu[ct] = ld4(io.u + (size_t)orow(qtok0 + 16 * ct + i16, b0, last) * FF + row + 4 * g);
         zero(acc);
-        if (t == 0) gemm_tile<CTQ, DQ>(acc, pa, W2T, D, row, 0, sm.ctx, LDH, qtok0);
-        else gemm_tile<CTQ, DQ>(acc, prefetch<DQ>(W2T, D, row, 0), W2T, D, row, 0, sm.ctx, LDH, qtok0);
+        if (t == 0) {
+            gemm_tile<CTQ, DQ>(acc, pa, W2T, D, row, 0, sm.ctx, LDH, qtok0);
+            pb = prefetch<DQ>(W2T, D, 128 + 16 * wv, 0);
+        } else {
+            gemm_tile<CTQ, DQ>(acc, pb, W2T, D, row, 0, sm.ctx, LDH, qtok0);
+            pa = prefetch<DQ>(W1T, FF, 16 * wv, 0);
+        }
         float* lds = t ? sm.h : sm.big;
         f32x4 sd = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1391,7 +1399,6 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         for (int e = 0; e < 4; ++e) sd[e] = row16_sum(sd[e]);
         if (i16 == 0) st4(bias + kBiasL1 + row + 4 * g, sd);
     }
-    pa = prefetch<DQ>(W1T, FF, 16 * wv, 0);
     BTR(TB + 3);
     __syncthreads();
     BTR(TB + 4);
