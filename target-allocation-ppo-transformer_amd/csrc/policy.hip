@@ -868,6 +868,14 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     if (threadIdx.x >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
     const int b0 = blockIdx.x * SPW;
     PTR(0);
+    // training mode: the actor embedding's operands and first K/V weight blocks are loaded before
+    // the minibatch gather stores its rows (a load behind a store burst waits for the burst)
+    [[maybe_unused]] EmbPre ep_a;
+    [[maybe_unused]] APre<2> pkv_a;
+    if constexpr (TR) {
+        ep_a = embed_load<kActorTrunk>(P);
+        pkv_a = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(threadIdx.x >> 6, 0), 0);
+    }
     // windows -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch tail zero-filled);
     // training mode gathers minibatch row idx[b] of the trajectory buffer
     {   // <= 3 elements per thread, every load of a round issued before any is used: the
@@ -937,8 +945,14 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     [[maybe_unused]] EmbPre ep_c;
     [[maybe_unused]] APre<2> pkv_c;
     if constexpr (!ROWS) {
-        APre<2> pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-        embed<kActorTrunk, TR>(sm, P, io.e[0], io.h0[0], b0);
+        APre<2> pkv;
+        if constexpr (TR) {
+            pkv = pkv_a;
+            embed_apply<kActorTrunk, TR>(sm, ep_a, io.e[0], io.h0[0], b0);
+        } else {
+            pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+            embed<kActorTrunk, TR>(sm, P, io.e[0], io.h0[0], b0);
+        }
         PTR(2);
         __syncthreads();
         if constexpr (TR) {
