@@ -158,10 +158,9 @@ __device__ __forceinline__ void zero(f32x4 (&acc)[CT]) {
 
 // Y[ytok0 + 16 ct + j][ycol + i] = epi(acc + bias[brow + i]); lane (j, g) holds rows 4g..4g+3
 template <int CT, bool RELU>
-__device__ __forceinline__ void store_tile(const f32x4 (&acc)[CT], const float* __restrict__ bias, int brow, float* Y,
-                                           int ldy, int ycol, int ytok0) {
+__device__ __forceinline__ void store_tile(const f32x4 (&acc)[CT], const f32x4 bb, float* Y, int ldy, int ycol,
+                                           int ytok0) {
     const int l = lane_id(), i16 = l & 15, g = l >> 4;
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + brow + 4 * g);
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
         f32x4 v = acc[ct] + bb;
@@ -173,13 +172,15 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[CT], const float* 
 }
 
 // One 16-row output tile per wave: Y[tok][ycol + i] = epi(W[row + i] . X[tok]^T + b[row + i]).
+// The bias is loaded ahead of the k-loop, so the epilogue does not wait one more L2 round trip.
 template <int CT, bool RELU, int D>
 __device__ __forceinline__ void linear1(const APre<D>& pre, const float* W, int ldw, const float* bias, int row,
                                         const float* X, int ldx, int xtok0, float* Y, int ldy, int ycol, int ytok0) {
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + row + 4 * (lane_id() >> 4));
     f32x4 acc[CT];
     zero(acc);
     gemm_tile<CT, D>(acc, pre, W, ldw, row, 0, X, ldx, xtok0);
-    store_tile<CT, RELU>(acc, bias, row, Y, ldy, ycol, ytok0);
+    store_tile<CT, RELU>(acc, bb, Y, ldy, ycol, ytok0);
 }
 
 // ------------------------------------------------------------------ VALU pieces
@@ -217,13 +218,23 @@ __device__ __forceinline__ int orow(int tok, int b0, bool compact) {
     return compact ? b0 + (tok & (SPW - 1)) : trow(tok, b0);
 }
 
+// The epilogue's per-feature operands (GEMM bias, LN weight and bias), loaded by the caller right
+// after the GEMM -- ahead of its next prefetches and the barrier, whose latency then covers them.
+struct LnPar {
+    f32x4 bb, ww, lb;
+};
+__device__ __forceinline__ LnPar ln_load(const float* __restrict__ bias, const float* __restrict__ w,
+                                         const float* __restrict__ b) {
+    const int f0 = 16 * (threadIdx.x >> 6) + 4 * (lane_id() >> 4);
+    return LnPar{*reinterpret_cast<const f32x4*>(bias + f0), *reinterpret_cast<const f32x4*>(w + f0),
+                 *reinterpret_cast<const f32x4*>(b + f0)};
+}
 template <int CT, bool TR = false>
-__device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[CT], const float* __restrict__ bias,
-                                                   const float* __restrict__ w, const float* __restrict__ b, int ytok0,
+__device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[CT], const LnPar& lp, int ytok0,
                                                    const LnOut& lo = LnOut{}) {
     const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
     const int f0 = 16 * wv + 4 * g;
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + f0);
+    const f32x4 bb = lp.bb;
     f32x4 v[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
@@ -238,8 +249,7 @@ __device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[
         if (g == 0) sm.red[wv * TOK + tok] = make_float2(m, q);
     }
     __syncthreads();
-    const f32x4 ww = *reinterpret_cast<const f32x4*>(w + f0);
-    const f32x4 lb = *reinterpret_cast<const f32x4*>(b + f0);
+    const f32x4 ww = lp.ww, lb = lp.lb;
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
         const int tok = ytok0 + 16 * ct + i16;
@@ -517,11 +527,10 @@ __device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P
         zero(acc);
         gemm_tile<CTQ, DQ>(acc, po, Wo, D, 16 * wv, 0, sm.ctx, LDH, qtok0);
         PTR(tb + 7);
+        const LnPar lp = ln_load(bo, P + kOffs.o[layer_param(trunk, layer, N1W)], P + kOffs.o[layer_param(trunk, layer, N1B)]);
         pf1a = prefetch<DQ>(W1, D, 16 * wv, 0);
         pf1b = prefetch<DQ>(W1, D, 128 + 16 * wv, 0);
-        residual_layernorm<CTQ, TR>(sm, acc, bo, P + kOffs.o[layer_param(trunk, layer, N1W)],
-                                    P + kOffs.o[layer_param(trunk, layer, N1B)], qtok0,
-                                    LnOut{io.xhat1, io.h1, io.rstd1, b0, last});
+        residual_layernorm<CTQ, TR>(sm, acc, lp, qtok0, LnOut{io.xhat1, io.h1, io.rstd1, b0, last});
     }
     PTR(tb + 8);
     __syncthreads();
@@ -543,10 +552,9 @@ __device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P
     gemm_tile<CTQ, DQ>(acc2, pf2a, W2, FF, 16 * wv, 0, sm.big, LDF, qtok0);
     gemm_tile<CTQ, DQ>(acc2, pf2b, W2, FF, 16 * wv, 128, sm.ctx, LDF, qtok0);
     PTR(tb + 12);
+    const LnPar lp2 = ln_load(b2, P + kOffs.o[layer_param(trunk, layer, N2W)], P + kOffs.o[layer_param(trunk, layer, N2B)]);
     pre_ln2();
-    residual_layernorm<CTQ, TR>(sm, acc2, b2, P + kOffs.o[layer_param(trunk, layer, N2W)],
-                                P + kOffs.o[layer_param(trunk, layer, N2B)], qtok0,
-                                LnOut{io.xhat2, io.h2, io.rstd2, b0, last});
+    residual_layernorm<CTQ, TR>(sm, acc2, lp2, qtok0, LnOut{io.xhat2, io.h2, io.rstd2, b0, last});
     PTR(tb + 14);
 }
 
