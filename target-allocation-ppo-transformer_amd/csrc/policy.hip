@@ -771,14 +771,22 @@ __device__ void head_mlp(Smem& sm, const float* __restrict__ P, const APre<4>& p
     const float* W2 = P + kOffs.o[head + 2];
     const float* b2 = P + kOffs.o[head + 3];
     const int wv = threadIdx.x >> 6;
+    // second layer: 16 lanes per (sample p, output a) = item p * nout + a, 4 hidden features per
+    // lane; its weights and bias are loaded before the first layer's GEMM
+    constexpr int kItems = SPW * nout;
+    const int item = threadIdx.x >> 4, k4 = threadIdx.x & 15;
+    const int p = item / nout, a = (item - p * nout) % nout;  // in range for every thread
+    const f32x4 w2 = *reinterpret_cast<const f32x4*>(W2 + a * HID + 4 * k4);
+    const float bb2 = b2[a];
     if (wv < HID / 16) linear1<1, true, 4>(pw, W0, D, b0, 16 * wv, sm.h, LDH, (S - 1) * SPW, sm.z, LDZ, 16 * wv, 0);
     __syncthreads();
-    if (threadIdx.x < SPW * nout) {
-        const int p = threadIdx.x / nout, a = threadIdx.x - p * nout;
-        float acc = 0.f;
-#pragma unroll 8
-        for (int o = 0; o < HID; ++o) acc += W2[a * HID + o] * sm.z[p * LDZ + o];
-        out[p * nout + a] = acc + b2[a];
+    if (item < kItems) {  // wave-uniform: kItems * 16 is a multiple of 64
+        const f32x4 z = *reinterpret_cast<const f32x4*>(sm.z + p * LDZ + 4 * k4);
+        float acc = (w2.x * z.x + w2.y * z.y) + (w2.z * z.z + w2.w * z.w);
+        acc = add_xor2(add_xor1(acc));
+        acc += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc), 0x141, 0xF, 0xF, true));  // row_half_mirror
+        acc += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc), 0x140, 0xF, 0xF, true));  // row_mirror
+        if (k4 == 0) out[item] = acc + bb2;
     }
     __syncthreads();
 }
