@@ -250,9 +250,8 @@ __device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[
     }
     __syncthreads();
     const f32x4 ww = lp.ww, lb = lp.lb;
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-        const int tok = ytok0 + 16 * ct + i16;
+    // (mean, 1/std) of token tok from the 8 per-wave partials
+    auto stats = [&](int tok, float& mean, float& rs) {
         float2 pr[NW];
         float ms = 0.f;
 #pragma unroll
@@ -260,14 +259,36 @@ __device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[
             pr[k] = sm.red[k * TOK + tok];
             ms += pr[k].x;
         }
-        const float mean = ms * (1.0f / NW);
+        mean = ms * (1.0f / NW);
         float m2 = 0.f;
 #pragma unroll
         for (int k = 0; k < NW; ++k) {
             const float dm = pr[k].x - mean;
             m2 += pr[k].y + 16.0f * dm * dm;
         }
-        const float rs = 1.0f / sqrtf(m2 * (1.0f / D) + 1e-5f);
+        rs = 1.0f / sqrtf(m2 * (1.0f / D) + 1e-5f);
+    };
+    static_assert(CT == 1 || CT == S, "pruned tile or all five");
+    // all five tiles: lane (i16, g) combines the partials of tile g's token, the last tile's in a
+    // second round; the other rows of the wave fetch theirs with ds_bpermute (instead of every row
+    // of the wave redoing every token's combine)
+    float mA, rA, mB, rB;
+    if constexpr (CT == 1) stats(ytok0 + i16, mA, rA);
+    else {
+        stats(ytok0 + 16 * g + i16, mA, rA);
+        stats(ytok0 + 16 * (S - 1) + i16, mB, rB);
+    }
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+        const int tok = ytok0 + 16 * ct + i16;
+        float mean = mA, rs = rA;
+        if (CT > 1 && ct < S - 1) {
+            mean = __shfl(mA, 16 * ct + i16);
+            rs = __shfl(rA, 16 * ct + i16);
+        } else if (CT > 1) {
+            mean = mB;
+            rs = rB;
+        }
         const f32x4 xh = (v[ct] - mean) * rs;
         const f32x4 out = xh * ww + lb;
         *reinterpret_cast<f32x4*>(sm.h + tok * LDH + f0) = out;
