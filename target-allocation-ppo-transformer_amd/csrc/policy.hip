@@ -1292,18 +1292,37 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 ld2(const float* p) { return *reinterpret_cast<const f32x2*>(p); }
 __device__ __forceinline__ void st2(float* p, f32x2 v) { *reinterpret_cast<f32x2*>(p) = v; }
 
+// The chunk's saved Q / K / V values of this thread (2 head dims of one (sample, head)), loaded by
+// the caller well ahead of attn_bwd_chunk: the rows come from HBM (written by the forward long before).
+struct AttnPre {
+    f32x2 k[S], v[S], q[S];
+};
 template <bool last>
-__device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, int c, int b0, float* scratch) {
+__device__ __forceinline__ void attn_bwd_load(AttnPre& a, const float* __restrict__ qkv, int c, int b0) {
     const int o8 = threadIdx.x & 7, hh = (threadIdx.x >> 3) & 3, p = threadIdx.x >> 5;
-    const int d0 = hh * HD + 2 * o8, col = 64 * c + d0;
+    const int col = 64 * c + hh * HD + 2 * o8;
     const size_t rb = (size_t)(b0 + p) * S;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        a.k[j] = ld2(qkv + (rb + j) * 3 * D + D + col);
+        a.v[j] = ld2(qkv + (rb + j) * 3 * D + 2 * D + col);
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+        if (!last || i == S - 1) a.q[i] = ld2(qkv + (rb + i) * 3 * D + col);
+}
+template <bool last>
+__device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch) {
+    const int o8 = threadIdx.x & 7, hh = (threadIdx.x >> 3) & 3, p = threadIdx.x >> 5;
+    const int d0 = hh * HD + 2 * o8;
+    const int col = 64 * c + d0;
     f32x2 k[S], v[S], dk[S], dv[S];
     bool msk[S];
     f32x2 sdq = {0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-        k[j] = ld2(qkv + (rb + j) * 3 * D + D + col);
-        v[j] = ld2(qkv + (rb + j) * 3 * D + 2 * D + col);
+        k[j] = a.k[j];
+        v[j] = a.v[j];
         msk[j] = sm.mask[p * S + j] != 0;
         dk[j] = f32x2{0.f, 0.f};
         dv[j] = f32x2{0.f, 0.f};
@@ -1312,7 +1331,7 @@ __device__ void attn_bwd_chunk(Smem& sm, const float* __restrict__ qkv, int c, i
     for (int i = 0; i < S; ++i) {
         f32x2 dq = {0.f, 0.f};
         if (!last || i == S - 1) {
-            const f32x2 q = ld2(qkv + (rb + i) * 3 * D + col);
+            const f32x2 q = a.q[i];
             const f32x2 g = ld2(sm.ctx + (i * SPW + p) * LDH + col);
             float pr[S], dp[S];
             float mx = -INFINITY;
@@ -1466,6 +1485,9 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         }
     }
     pa = prefetch<DQ>(WoT, D, 16 * wv, 0);
+    // chunk 0's Q / K / V for the attention backward: their HBM latency hides under LN1 backward
+    AttnPre ap;
+    attn_bwd_load<last>(ap, io.qkv, 0, b0);
     BTR(TB + 5);
     __syncthreads();
     BTR(TB + 6);
@@ -1492,7 +1514,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         APre<2> pw = prefetch<2>(WinT, 3 * D, 16 * wv, 64 * c);
-        attn_bwd_chunk<last>(sm, io.qkv, c, b0, sm.scr);
+        attn_bwd_chunk<last>(sm, ap, c, sm.scr);
         __syncthreads();
         BTR(TB + 11 + 2 * c);
         if (threadIdx.x < 3 * 64) {  // in_proj bias partial of the chunk: the 8 wave rows of sm.scr
@@ -1522,6 +1544,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         }
         gemm_tile<S, 2, 4>(acc, pw1, WinT, 3 * D, 16 * wv, D + 64 * c, sm.big + 64, LDB, 0);
         gemm_tile<S, 2, 4>(acc, pw2, WinT, 3 * D, 16 * wv, 2 * D + 64 * c, sm.big + 128, LDB, 0);
+        if (c == 0) attn_bwd_load<last>(ap, io.qkv, 1, b0);  // behind every weight load of the chunk
         if (c == 0) __syncthreads();  // big is rewritten by chunk 1
         BTR(TB + 12 + 2 * c);
     }
