@@ -1217,37 +1217,47 @@ __device__ __forceinline__ float hsum(f32x4 v) { return (v.x + v.y) + (v.z + v.w
 // (12 KiB floats): dw = sum src * xhat, db = sum src -> part[0..127], [128..255]; the bias
 // gradient of the linear that produced the LayerNorm input, sum dz -> bias[0..127]. Ends without a
 // barrier after the partials are written (scratch is read until then).
-__device__ void ln_bwd_lds(const float* src, float* dst, const float* __restrict__ xhat,
-                           const float* __restrict__ rstd, const float* __restrict__ w, float* __restrict__ gout,
+// Its global operands -- the weight and this lane group's (<= 3) tokens' xhat rows and 1/std -- in
+// one round trip, issued by the caller ahead of time (ln_bwd_load) so the HBM latency hides under
+// the preceding phase.
+constexpr int kLnIt = (TOK + NTHR / 16 - 1) / (NTHR / 16);
+struct LnBwdPre {
+    f32x4 w0, w1, X0[kLnIt], X1[kLnIt];
+    float RS[kLnIt];
+};
+__device__ __forceinline__ void ln_bwd_load(LnBwdPre& a, const float* __restrict__ xhat, const float* __restrict__ rstd,
+                                            const float* __restrict__ w, int t0, int b0, bool compact) {
+    const int f0 = 8 * (threadIdx.x & 15), grp = threadIdx.x >> 4;
+    a.w0 = ld4(w + f0);
+    a.w1 = ld4(w + f0 + 4);
+#pragma unroll
+    for (int it = 0; it < kLnIt; ++it) {
+        const int tok = t0 + grp + it * (NTHR / 16);
+        if (tok < TOK) {  // wave-uniform
+            const size_t r = (size_t)orow(tok, b0, compact);
+            a.X0[it] = ld4(xhat + r * D + f0);
+            a.X1[it] = ld4(xhat + r * D + f0 + 4);
+            a.RS[it] = rstd[r];
+        }
+    }
+}
+__device__ void ln_bwd_lds(const float* src, float* dst, const LnBwdPre& a, float* __restrict__ gout,
                            float* __restrict__ part, float* __restrict__ bias, int t0, int b0, bool compact,
                            float* scratch) {
     const int j = threadIdx.x & 15, grp = threadIdx.x >> 4;
     const int f0 = 8 * j;
-    const f32x4 w0 = ld4(w + f0), w1 = ld4(w + f0 + 4);
+    const f32x4 w0 = a.w0, w1 = a.w1;
     const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
     f32x4 pw0 = zero4, pw1 = zero4, pb0 = zero4, pb1 = zero4, pd0 = zero4, pd1 = zero4;
-    // all of this lane group's (<= 3) tokens' global operands in one round trip
-    constexpr int kIt = (TOK + NTHR / 16 - 1) / (NTHR / 16);
-    f32x4 X0[kIt], X1[kIt];
-    float RS[kIt];
-#pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-        const int tok = t0 + grp + it * (NTHR / 16);
-        if (tok < TOK) {
-            const size_t r = (size_t)orow(tok, b0, compact);
-            X0[it] = ld4(xhat + r * D + f0);
-            X1[it] = ld4(xhat + r * D + f0 + 4);
-            RS[it] = rstd[r];
-        }
-    }
+    constexpr int kIt = kLnIt;
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
         const int tok = t0 + grp + it * (NTHR / 16);
         if (tok >= TOK) continue;
         const size_t r = (size_t)orow(tok, b0, compact);
         const f32x4 g0 = ld4(src + tok * LDH + f0), g1 = ld4(src + tok * LDH + f0 + 4);
-        const f32x4 x0 = X0[it], x1 = X1[it];
-        const float rs = RS[it];
+        const f32x4 x0 = a.X0[it], x1 = a.X1[it];
+        const float rs = a.RS[it];
         const f32x4 gw0 = g0 * w0, gw1 = g1 * w1;
         const float m1 = row16_sum(hsum(gw0) + hsum(gw1)) * (1.0f / D);
         const float m2 = row16_sum(hsum(gw0 * x0) + hsum(gw1 * x1)) * (1.0f / D);
@@ -1409,9 +1419,12 @@ __device__ __forceinline__ void embed_bwd_load(EmbBwdPre& ep, const float* __res
                               : f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-template <int trunk, int layer, bool last, int TB>
+// ln2_pre: this layer's LN2-backward operands, already loaded by the caller (nullptr: load here);
+// next_load: issues the next phase's global loads behind this layer's last weight loads.
+template <int trunk, int layer, bool last, int TB, class F = NoHook>
 __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __restrict__ PT, const BwdLayerIO& io,
-                          int b0, EmbBwdPre* ep = nullptr, const float* e_emb = nullptr, const float* xg = nullptr) {
+                          int b0, EmbBwdPre* ep = nullptr, const float* e_emb = nullptr, const float* xg = nullptr,
+                          const LnBwdPre* ln2_pre = nullptr, F next_load = F{}) {
     BTR(TB);
     constexpr int CTQ = last ? 1 : S;
     constexpr int DQ = depth<CTQ>();
@@ -1426,8 +1439,11 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
 
     // LN2 backward: sm.h -> sm.ctx (= df)
     APre<DQ> pa = prefetch<DQ>(W2T, D, 16 * wv, 0);
-    ln_bwd_lds(sm.h, sm.ctx, io.xhat2, io.rstd2, P + kOffs.o[layer_param(trunk, layer, N2W)], io.df,
-               io.ln2_part + (size_t)blockIdx.x * 2 * D, bias + kBiasL2, qtok0, b0, last, sm.big);
+    LnBwdPre lnp;
+    if (ln2_pre) lnp = *ln2_pre;
+    else ln_bwd_load(lnp, io.xhat2, io.rstd2, P + kOffs.o[layer_param(trunk, layer, N2W)], qtok0, b0, last);
+    ln_bwd_lds(sm.h, sm.ctx, lnp, io.df, io.ln2_part + (size_t)blockIdx.x * 2 * D, bias + kBiasL2, qtok0, b0, last,
+               sm.big);
     BTR(TB + 1);
     __syncthreads();
     BTR(TB + 2);
@@ -1485,15 +1501,17 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         }
     }
     pa = prefetch<DQ>(WoT, D, 16 * wv, 0);
-    // chunk 0's Q / K / V for the attention backward: their HBM latency hides under LN1 backward
+    // LN1 backward's operands, then chunk 0's Q / K / V for the attention backward: their HBM
+    // latency hides under the residual pass / barrier and LN1 backward
+    ln_bwd_load(lnp, io.xhat1, io.rstd1, P + kOffs.o[layer_param(trunk, layer, N1W)], qtok0, b0, last);
     AttnPre ap;
     attn_bwd_load<last>(ap, io.qkv, 0, b0);
     BTR(TB + 5);
     __syncthreads();
     BTR(TB + 6);
     // LN1 backward: sm.ctx -> sm.h (= dz1)
-    ln_bwd_lds(sm.ctx, sm.h, io.xhat1, io.rstd1, P + kOffs.o[layer_param(trunk, layer, N1W)], io.dz1,
-               io.ln1_part + (size_t)blockIdx.x * 2 * D, bias + kBiasOut, qtok0, b0, last, sm.big);
+    ln_bwd_lds(sm.ctx, sm.h, lnp, io.dz1, io.ln1_part + (size_t)blockIdx.x * 2 * D, bias + kBiasOut, qtok0, b0, last,
+               sm.big);
     BTR(TB + 7);
     __syncthreads();
     BTR(TB + 8);
@@ -1549,6 +1567,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         BTR(TB + 12 + 2 * c);
     }
     if (layer == 0 && ep) embed_bwd_load(*ep, e_emb, xg, b0);
+    next_load();
     // + dz1 on the rows that carried the residual -> sm.h
 #pragma unroll
     for (int ct = 0; ct < S; ++ct) {
@@ -1727,10 +1746,17 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
     head_input_grad(sm, PT + kHeadT + D * HID, sm.ctx + 64);
     __syncthreads();
     BTR(2);
-    bwd_layer<kCriticTrunk, 1, true, 4>(sm, P, PT + 2 * kLayerT, io.L[2], b0);
     {
+        // layer 0's LN2-backward operands are loaded at the end of layer 1's backward
+        LnBwdPre l2;
+        bwd_layer<kCriticTrunk, 1, true, 4>(sm, P, PT + 2 * kLayerT, io.L[2], b0, nullptr, nullptr, nullptr, nullptr,
+                                            [&] {
+                                                ln_bwd_load(l2, io.L[1].xhat2, io.L[1].rstd2,
+                                                            P + kOffs.o[layer_param(kCriticTrunk, 0, N2W)], 0, b0,
+                                                            false);
+                                            });
         EmbBwdPre ep;
-        bwd_layer<kCriticTrunk, 0, false, 20>(sm, P, PT + 1 * kLayerT, io.L[1], b0, &ep, io.e[1], io.xg);
+        bwd_layer<kCriticTrunk, 0, false, 20>(sm, P, PT + 1 * kLayerT, io.L[1], b0, &ep, io.e[1], io.xg, &l2);
         embed_bwd(sm, ep, io.epart + ((size_t)blockIdx.x * 2 + 1) * kEmbPart);
     }
     __syncthreads();
