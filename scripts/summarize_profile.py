@@ -31,6 +31,17 @@ stats = {}
 for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
     stats[r["Name"].split("(")[0].replace("void ", "")] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                                              "pct": float(r["Percentage"])}
+# steady state: the average of each frequently launched kernel's last 64 launches (the last rollout
+# iteration at T = 64; early iterations run slower while clocks and episode states settle)
+trace_csv = os.path.join(src, "trace", "run_kernel_trace.csv")
+if os.path.exists(trace_csv):
+    durs = defaultdict(list)
+    for r in csv.DictReader(open(trace_csv)):
+        durs[r["Kernel_Name"].split("(")[0].replace("void ", "")].append(
+            int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    for k, v in durs.items():
+        if k in stats and len(v) >= 128:
+            stats[k]["last64_avg_ns"] = sum(v[-64:]) / 64
 json.dump({"pmc": out, "kernel_stats": stats, "source": os.path.basename(src)},
           open(os.path.join(dst, f"{rnd}_pmc.json"), "w"), indent=1)
 print(json.dumps({k: v for k, v in out.items() if "uavhip" in k}, indent=1))
