@@ -16,7 +16,7 @@ from uavhip import _lib  # noqa: E402
 from uavhip.policy import TransformerActorCritic  # noqa: E402
 
 NAMES = {0: "start", 1: "x+mask", 2: "a.embed", 3: "a.layer+sync", 4: "a.head", 5: "c.layers+sync", 6: "c.head",
-         7: "sample"}
+         7: "sample", 60: "env.sync", 61: "env.loads", 62: "env.step", 63: "env.store"}
 LAYER = ["start", "c0 gemm", "c0 sync", "c0 attn+sync", "c1 gemm", "c1 sync", "c1 attn+sync", "outproj", "sync",
          "LN1+sync", "FFN1", "sync", "FFN2+sync", "store+sync", "LN2"]
 for li, tag in enumerate(["A", "C0", "C1"]):
@@ -36,11 +36,23 @@ fn = _lib.LIB.uavhip_policy_trace
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
 ROWS = os.environ.get("ROWS", "0") == "1"  # window-row ring path (uavhip_policy_forward_rows)
+ENV = os.environ.get("ENV", "0") == "1"    # fused rollout step (uavhip_rollout_step), 16 x 32 envs
 kw = {}
-if ROWS:
+if ENV:  # the stamps of the last of 8 fused steps
+    from uavhip import VecUAVEnv
+    from uavhip.rollout import RolloutEngine
+    env = VecUAVEnv(B, 16, 32, 1, 1, seed=1)
+    eng = RolloutEngine(env, net, horizon=8)
+    eng.start()
+    tr = eng.traj
+    tr.obs[0].copy_(tr.obs[8])
+    for t in range(8):
+        net.rollout_step(env, tr.obs[t], eng.rowproj, t, t == 0, tr.actions[t], tr.logp[t], tr.values[t],
+                         tr.obs[t + 1], tr.rewards[t], tr.dones[t], seed=0, offset=t * B, offset_dev=eng.counter)
+elif ROWS:
     from uavhip.policy import rowproj_buffer
     rp = rowproj_buffer(B)
-for i in range(5):
+for i in range(0 if ENV else 5):
     if ROWS:  # timing only: the same windows replayed as a sequence
         kw = dict(rowproj=rp, step=i, fill=i == 0)
     net.fused_forward(x, action_out=a, logp=lp, value=v, **kw)
@@ -59,6 +71,6 @@ for k in slots:
     print(f"{k:3d} {NAMES[k]:18s} {m0:8d} {m4:8d}  +{m0 - prev:6d}")
     prev = m0
 start = t[:, 0, 0]
-end = t[:, 0, 7]
+end = t[:, 0, 63 if ENV else 7]
 print(f"block start spread {int(start.max() - start.min())} cycles; end spread {int(end.max() - end.min())};"
       f" kernel span {int(end.max() - start.min())} cycles")

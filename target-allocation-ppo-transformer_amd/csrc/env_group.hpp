@@ -195,10 +195,17 @@ __device__ void greset_regs(GRegs& R, const uavhip_env& env, int j, bool scene) 
 // Single-step use (the fused rollout launch): register state in one load round, scene-dependent
 // values read from both scene buffers and selected after the wait (as envdev::load_regs<PF>).
 // gload_issue only issues the loads (overlapped with the critic head); gload_finish consumes them.
+// The per-env scalars (istate / dstate rows) arrive as one vector load each -- lane j of a group
+// holds element j -- and are broadcast in gload_finish: 2 memory instructions instead of 18.
 struct GPending {
     double valb[2], ucb[2], ppb[2];
-    int sel_raw;
+    int isv;
+    double dsv;
 };
+__device__ __forceinline__ int grl_i(int v, int jj) {
+    const int a = __builtin_amdgcn_readlane(v, jj), b = __builtin_amdgcn_readlane(v, L + jj);
+    return gbase() ? b : a;
+}
 __device__ __forceinline__ void gload_issue(GRegs& R, GPending& q, const uavhip_env& env, int e, int j) {
     const int N = env.N, M = env.M;
     const int* is = env.istate + (long long)e * UAVHIP_IST_COUNT;
@@ -211,9 +218,8 @@ __device__ __forceinline__ void gload_issue(GRegs& R, GPending& q, const uavhip_
         q.ucb[b] = j < N ? env.uav_cost[sb * N + j] : 0.0;
         q.ppb[b] = j < N ? env.p_pen[sb * N + j] : 0.0;
     }
-    q.sel_raw = is[UAVHIP_IST_SCENE_SEL];
-    R.stale = is[UAVHIP_IST_SCENE_STALE];
-    R.gen = is[UAVHIP_IST_SCENE_GEN];
+    q.isv = is[j < UAVHIP_IST_COUNT ? j : 0];
+    q.dsv = ds[j < UAVHIP_DST_COUNT ? j : 0];
     const long long o = (long long)e * M + j;
     const bool v = j < M;
     R.nhf = v ? env.nh_final[o] : 1.0;
@@ -221,21 +227,6 @@ __device__ __forceinline__ void gload_issue(GRegs& R, GPending& q, const uavhip_
     R.tc = v ? env.t_cost[o] : 0.0;
     R.nlk = v ? env.n_lock[o] : 0;
     R.asg = j < N ? env.assigned[(long long)e * N + j] : -1;
-    R.u = is[UAVHIP_IST_UAV_IDX];
-    R.t = is[UAVHIP_IST_TARGET_IDX];
-    R.ncov = is[UAVHIP_IST_N_COVERED];
-    R.nasg = is[UAVHIP_IST_N_ASSIGNED];
-    R.ep = is[UAVHIP_IST_EPISODE];
-    R.err = is[UAVHIP_IST_ERROR];
-    R.r = ds[UAVHIP_DST_R];
-    R.J = ds[UAVHIP_DST_J];
-    R.asg_cost = ds[UAVHIP_DST_ASG_COST];
-    R.cov_val = ds[UAVHIP_DST_COV_VALUE];
-    R.tot_cost = ds[UAVHIP_DST_TOTAL_COST];
-    R.tot_val = ds[UAVHIP_DST_TOTAL_VALUE];
-    R.sum_pd = ds[UAVHIP_DST_SUM_PDMG];
-    R.sum_pf = ds[UAVHIP_DST_SUM_PFIN];
-    R.pd_cur = ds[UAVHIP_DST_PD_CUR];
     const float* w = env.window + (long long)e * kObs;
     R.w0 = w[j];
     R.w1 = w[L + j];
@@ -243,7 +234,25 @@ __device__ __forceinline__ void gload_issue(GRegs& R, GPending& q, const uavhip_
 }
 __device__ __forceinline__ void gload_finish(GRegs& R, const GPending& q, const uavhip_env& env, int e, int j) {
     const int N = env.N, M = env.M;
-    R.sel = env.scene_buffers == 2 ? (q.sel_raw & 1) : 0;
+    const int sel_raw = grl_i(q.isv, UAVHIP_IST_SCENE_SEL);
+    R.stale = grl_i(q.isv, UAVHIP_IST_SCENE_STALE);
+    R.gen = grl_i(q.isv, UAVHIP_IST_SCENE_GEN);
+    R.u = grl_i(q.isv, UAVHIP_IST_UAV_IDX);
+    R.t = grl_i(q.isv, UAVHIP_IST_TARGET_IDX);
+    R.ncov = grl_i(q.isv, UAVHIP_IST_N_COVERED);
+    R.nasg = grl_i(q.isv, UAVHIP_IST_N_ASSIGNED);
+    R.ep = grl_i(q.isv, UAVHIP_IST_EPISODE);
+    R.err = grl_i(q.isv, UAVHIP_IST_ERROR);
+    R.r = grl_d(q.dsv, UAVHIP_DST_R);
+    R.J = grl_d(q.dsv, UAVHIP_DST_J);
+    R.asg_cost = grl_d(q.dsv, UAVHIP_DST_ASG_COST);
+    R.cov_val = grl_d(q.dsv, UAVHIP_DST_COV_VALUE);
+    R.tot_cost = grl_d(q.dsv, UAVHIP_DST_TOTAL_COST);
+    R.tot_val = grl_d(q.dsv, UAVHIP_DST_TOTAL_VALUE);
+    R.sum_pd = grl_d(q.dsv, UAVHIP_DST_SUM_PDMG);
+    R.sum_pf = grl_d(q.dsv, UAVHIP_DST_SUM_PFIN);
+    R.pd_cur = grl_d(q.dsv, UAVHIP_DST_PD_CUR);
+    R.sel = env.scene_buffers == 2 ? (sel_raw & 1) : 0;
     R.sb = (long long)R.sel * env.E + e;
     R.val = R.sel ? q.valb[1] : q.valb[0];
     R.ucost = R.sel ? q.ucb[1] : q.ucb[0];

@@ -1091,6 +1091,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         // envdev::step_once on register state; the wave's row scratch in the dead sm.x). Both envs'
         // registers are loaded in one round before either steps.
         __syncthreads();
+        PTR(60);
         using namespace envdev;
         const int lane = lane_id(), e0 = b0 + 2 * wv;
         if (env_grp) {
@@ -1100,9 +1101,12 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
             R.tab = nullptr;
             R.win = sm.h + (2 * wv + g) * envgrp::kWin;
             envgrp::gload_finish(R, gq, env, e, j);
+            PTR(61);
             envgrp::gstep<false>(R, env, e, j, sm.mask[2 * wv + g], eo.auto_reset, obs_at(eo.obs, e, obs_f16(env)),
                           eo.rew + e, eo.done + e, eo.info ? eo.info + (size_t)e * UAVHIP_INFO_COUNT : nullptr);
+            PTR(62);
             envgrp::gstore_regs(R, env, e, j);
+            PTR(63);
         } else if (e0 < B) {
             const bool two = e0 + 1 < B;
             EnvRegs<1> R0, R1;
