@@ -315,7 +315,8 @@ typedef struct uavhip_ppo {
     double* adam_step;   /* [1] device step counter (shared by all groups) */
     float* workspace;    /* [uavhip_ppo_workspace_floats(minibatch)], zero-filled before first use */
     float* loss_sums;    /* [4] written by FORWARD: sums over this rank's samples of min(s1, s2),
-                            (v - R)^2, (v_clip - R)^2, entropy; BACKWARD reads them (all-reduced) */
+                            (v - R)^2, (v_clip - R)^2, entropy; BACKWARD reads them (all-reduced);
+                            FORWARD | BACKWARD in one call: summed and written by the backward */
     double* stats;       /* [4] += loss_actor, loss_critic, entropy, 1 per step (nullable) */
     int32_t n_floats;
     int32_t minibatch;   /* samples per step on this rank, multiple of 64 */

@@ -1634,7 +1634,25 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     float* dzc = sm.ctx + 64;            // critic dz rows
     float* zs = sm.big;                  // relu(head.0) rows of both heads [2][16][64]
     const float inv = 1.0f / (float)io.Bg;
-    const float tot0 = io.tot[0], tot1 = io.tot[1], tot2 = io.tot[2], tot3 = io.tot[3];
+    // the four loss sums (used by wave 0 only): from the all-reduced buffer, or summed here from
+    // the forward's workgroup partials with k_loss_sums' exact order (train.hip)
+    float tot0, tot1, tot2, tot3;
+    if (io.fpart) {
+        float s4[4] = {0.f, 0.f, 0.f, 0.f};
+        if (threadIdx.x < 64) {
+            for (int i = threadIdx.x; i < io.nfpart; i += 64)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) s4[c] += io.fpart[i * 4 + c];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                s4[c] = add_xor32(add_xor16(add_ror8(add_ror4(add_xor2(add_xor1(s4[c]))))));
+            if (blockIdx.x == 0 && threadIdx.x == 0 && io.tot_out)
+                for (int c = 0; c < 4; ++c) io.tot_out[c] = s4[c];
+        }
+        tot0 = s4[0]; tot1 = s4[1]; tot2 = s4[2]; tot3 = s4[3];
+    } else {
+        tot0 = io.tot[0]; tot1 = io.tot[1]; tot2 = io.tot[2]; tot3 = io.tot[3];
+    }
     {   // every global input in one round trip: z rows (one float4 per thread), per-sample rows,
         // the head.2 weights of this thread's hidden unit j = tid % 64 (the dz loop below)
         const int trunk = threadIdx.x >> 8, p = (threadIdx.x >> 4) & 15, q = threadIdx.x & 15;

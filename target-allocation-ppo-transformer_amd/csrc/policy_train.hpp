@@ -53,6 +53,11 @@ struct BwdIO {
     // sums over the global minibatch (all-reduced when data parallel), relu(head.0) rows
     const float* smp;
     const float* tot;
+    // FORWARD + BACKWARD in one call: the forward's per-workgroup loss partials [nfpart][4], summed
+    // by every workgroup's wave 0 in k_loss_sums' order (tot unused; workgroup 0 writes tot_out)
+    const float* fpart;
+    int nfpart;
+    float* tot_out;
     const float* z[2];
     float* dz[2];            // [Bm][64] d(head.0 pre-activation) (weight-gradient GEMM operand)
     float* hpart;            // [Bm/16][kHeadPart] head.2 weight / bias gradient partials

@@ -321,7 +321,8 @@ extern "C" int64_t uavhip_ppo_workspace_floats(int32_t minibatch) {
         if (rc_) return rc_; \
     } while (0)
 
-static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int Bg, double* step, int* n_sq);
+static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int Bg, double* step, int* n_sq,
+                        bool fused_sums);
 
 extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const int8_t* actions,
                                const float* old_logp, const float* old_values, const float* returns,
@@ -370,13 +371,15 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
         io.fpart = p.fpart;
         io.eps_clip = c->eps_clip;
         TR_CHECK(pol::policy_forward_train(p.packed, states, io, Bm, st));
-        hipLaunchKernelGGL(k_loss_sums, dim3(1), dim3(64), 0, st, p.fpart, nblk, c->loss_sums);
-        TR_CHECK(check_launch("k_loss_sums"));
+        if (!bwd) {  // with BACKWARD in the same call, K6 sums the partials itself (one launch fewer)
+            hipLaunchKernelGGL(k_loss_sums, dim3(1), dim3(64), 0, st, p.fpart, nblk, c->loss_sums);
+            TR_CHECK(check_launch("k_loss_sums"));
+        }
     }
     // single-GPU FULL step: the gradient reduction leaves the g^2 partials of the final grads;
     // otherwise (UPDATE after an all-reduce of grads) k_grad_norm computes them
     int n_sq = kSqBlocks;
-    if (bwd) TR_CHECK(ppo_backward(c, p, st, Bg, upd ? c->adam_step : nullptr, &n_sq));
+    if (bwd) TR_CHECK(ppo_backward(c, p, st, Bg, upd ? c->adam_step : nullptr, &n_sq, fwd));
     if (upd) {
         if (!bwd) {
             hipLaunchKernelGGL(k_grad_norm, dim3(kSqBlocks), dim3(256), 0, st, c->grads, c->n_floats, p.sq_part,
@@ -393,7 +396,8 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
 }
 
 // Backward + weight gradients of one minibatch (the workspace holds the forward's activations).
-static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int Bg, double* step, int* n_sq) {
+static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int Bg, double* step, int* n_sq,
+                        bool fused_sums) {
     const int Bm = p.Bm, R = p.R, nblk = Bm / kHeadSamples;
     const LayerBufs &A = p.la, &C0 = p.lc0, &C1 = p.lc1;
     const int ta = kActorTrunk, tc = kCriticTrunk;
@@ -401,6 +405,11 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         pol::BwdIO io{};
         io.smp = p.smp;
         io.tot = c->loss_sums;
+        if (fused_sums) {
+            io.fpart = p.fpart;
+            io.nfpart = nblk;
+            io.tot_out = c->loss_sums;
+        }
         io.z[0] = p.z_a;
         io.z[1] = p.z_c;
         io.dz[0] = p.dz_a;
