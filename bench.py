@@ -240,7 +240,7 @@ def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
         if world == 1:
             trainer.capture()  # once per buffer set (not timed): replays cover every later update
             impl = ("HIP training step (uavhip_ppo_step: fused forward / backward kernels, stream-K weight-gradient "
-                    "MFMA GEMM, fused clip + Adam), hipGraph replay")
+                    "MFMA GEMM, fused clip + Adam), one hipGraph replay per epoch")
         else:
             impl = ("HIP training step, data parallel: forward / all-reduce loss sums / backward / "
                     "all-reduce grads (RCCL) / clip+Adam per global minibatch")

@@ -4,9 +4,10 @@ attention / heads+loss kernels and a fused clip_grad_norm_ + Adam.
 
 The policy's parameters become views of one flat buffer (the uavhip_policy_layout() order), so
 state_dict(), load_state_dict() and the torch `evaluate` path keep working on the same storage the
-kernels update. One minibatch step is one C call; `run` captures it once into a hipGraph and
-replays it per minibatch, drawing minibatches like SubsetRandomSampler (torch.randperm of the
-given CPU generator, ppo.py:97-99).
+kernels update. One minibatch step is one C call; `run` captures the steps of a whole epoch into
+one hipGraph (minibatch b reads its rows at a fixed offset of a device permutation buffer) and per
+epoch copies in the permutation and replays it, drawing minibatches like SubsetRandomSampler
+(torch.randperm of the given CPU generator, ppo.py:97-99).
 
 Data parallel (world > 1, every rank holding the same all-gathered buffers and generator seed):
 each rank takes its 1/world slice of every global minibatch; FORWARD, an all-reduce of the four
@@ -90,21 +91,28 @@ class FusedPPOTrainer:
                      returns.to(device=dev, dtype=torch.float32).contiguous().reshape(n),
                      advantages.to(device=dev, dtype=torch.float32).contiguous().reshape(n))
         self.n = n
+        self.perm = torch.zeros(n, dtype=torch.int32, device=dev)  # the epoch's minibatch order
         self.graph = None
 
-    def step(self, phases=_lib.PPO_FULL):
-        """uavhip_ppo_step phases (bit mask) on this rank's rows self.idx."""
+    def step(self, phases=_lib.PPO_FULL, idx=None):
+        """uavhip_ppo_step phases (bit mask) on this rank's rows idx (default self.idx)."""
         s, a, lp, v, r, adv = self.bufs
-        check(LIB.uavhip_ppo_step(self.desc, ptr(s), ptr(a), ptr(lp), ptr(v), ptr(r), ptr(adv), ptr(self.idx),
+        idx = self.idx if idx is None else idx
+        check(LIB.uavhip_ppo_step(self.desc, ptr(s), ptr(a), ptr(lp), ptr(v), ptr(r), ptr(adv), ptr(idx),
                                   int(phases), stream_handle()), "uavhip_ppo_step")
 
-    def ddp_step(self):
+    def _rows(self, perm, b):
+        """This rank's rows of global minibatch b of the permutation perm (a view)."""
+        Bg, Bl = self.global_minibatch, self.minibatch
+        return perm[b * Bg + self.rank * Bl:b * Bg + (self.rank + 1) * Bl]
+
+    def ddp_step(self, idx=None):
         """One data-parallel optimizer step (see the module docstring)."""
-        self.step(_lib.PPO_FORWARD)
+        self.step(_lib.PPO_FORWARD, idx)
         self.allreduce(self.loss_sums)
-        self.step(_lib.PPO_BACKWARD)
+        self.step(_lib.PPO_BACKWARD, idx)
         self.allreduce(self.grads)
-        self.step(_lib.PPO_UPDATE)
+        self.step(_lib.PPO_UPDATE, idx)
 
     def gradients(self, idx):
         """Raw gradients (before clipping) of the PPO loss on rows idx, as a flat tensor."""
@@ -118,8 +126,9 @@ class FusedPPOTrainer:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=s):
-            self.step(_lib.PPO_FULL)
+        with torch.cuda.graph(self.graph, stream=s):  # one epoch: every minibatch step
+            for b in range(self.n // self.global_minibatch):
+                self.step(_lib.PPO_FULL, self._rows(self.perm, b))
         torch.cuda.current_stream().wait_stream(s)
 
     def run(self, epochs=None, generator=None, use_graph=True):
@@ -130,17 +139,18 @@ class FusedPPOTrainer:
             self.capture()
         self.stats.zero_()
         cnt = 0
-        Bg, Bl = self.global_minibatch, self.minibatch
+        steps = self.n // self.global_minibatch
         for _ in range(epochs):
-            perm = torch.randperm(self.n, generator=generator).to(device=self.device, dtype=torch.int32)
-            for b in range(self.n // Bg):
-                self.idx.copy_(perm[b * Bg + self.rank * Bl:b * Bg + (self.rank + 1) * Bl])
-                if use_graph:
-                    self.graph.replay()
-                elif self.world == 1:
-                    self.step(_lib.PPO_FULL)
+            self.perm.copy_(torch.randperm(self.n, generator=generator))
+            if use_graph:
+                self.graph.replay()
+                cnt += steps
+                continue
+            for b in range(steps):
+                if self.world == 1:
+                    self.step(_lib.PPO_FULL, self._rows(self.perm, b))
                 else:
-                    self.ddp_step()
+                    self.ddp_step(self._rows(self.perm, b))
                 cnt += 1
         self.policy._packed_key = None  # parameters changed under torch's version counters: repack
         if cnt == 0:
