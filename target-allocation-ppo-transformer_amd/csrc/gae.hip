@@ -1,7 +1,7 @@
 // gae.hip -- K3: GAE + advantage normalisation over a time-major [T][E] rollout buffer.
 // Reference: agents/ppo.py:70-94 (one Python iteration and a chain of 0-dim fp32 torch ops per
-// transition). Here: one lane per env walks t = T-1..0 with the loads of the next few steps in
-// flight (the recurrence is the only serial part); fp32 arithmetic in the reference's op order,
+// transition). Here: one lane per env walks t = T-1..0 over inputs staged in LDS by its whole
+// workgroup (the recurrence is the only serial part); fp32 arithmetic in the reference's op order,
 // no FMA contraction, so returns are bitwise the reference's. The normalisation statistics are
 // fp64 block partials (fixed reduction order -> run-to-run deterministic, no atomics).
 #include "common.hpp"
@@ -10,7 +10,9 @@
 
 namespace uavhip {
 namespace {
-constexpr int kGaeBlock = 64;  // one wave per block: E = 4096 -> 64 blocks spread over the CUs
+constexpr int kGaeBlock = 64;     // envs per block (E = 4096 -> 64 blocks); one partial pair each
+constexpr int kGaeThreads = 256;  // loaders / storers per block
+constexpr int kGaeT = 64;         // steps staged in LDS per pass
 constexpr int kRedBlock = 256;
 
 // Deterministic fp64 block reduction of (a, b); result valid in thread 0.
@@ -32,40 +34,69 @@ __device__ __forceinline__ void block_sum2(double& a, double& b) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(kGaeBlock) void k_gae(const double* __restrict__ reward, const uint8_t* __restrict__ done,
-                                                   const float* __restrict__ value,
-                                                   const float* __restrict__ last_value, int T, int E, float g,
-                                                   float gl, float* __restrict__ ret, float* __restrict__ adv,
-                                                   double* __restrict__ partials) {
-    const int e = blockIdx.x * kGaeBlock + threadIdx.x;
+// One block per 64 envs: all 256 threads stage the [t][env] inputs of up to kGaeT steps in LDS
+// (coalesced, 4 waves of loads in flight instead of one), wave 0 walks the recurrence from LDS --
+// one lane per env, the serial part -- and all threads store the returns / advantages.
+__global__ __launch_bounds__(kGaeThreads) void k_gae(const double* __restrict__ reward,
+                                                     const uint8_t* __restrict__ done,
+                                                     const float* __restrict__ value,
+                                                     const float* __restrict__ last_value, int T, int E, float g,
+                                                     float gl, float* __restrict__ ret, float* __restrict__ adv,
+                                                     double* __restrict__ partials) {
+    __shared__ float sr[kGaeT][kGaeBlock], sv[kGaeT][kGaeBlock], sret[kGaeT][kGaeBlock], sadv[kGaeT][kGaeBlock];
+    __shared__ uint8_t sd[kGaeT][kGaeBlock];
+    const int e0 = blockIdx.x * kGaeBlock, lane = threadIdx.x & (kGaeBlock - 1);
+    const bool walker = threadIdx.x < kGaeBlock && e0 + lane < E;
     double s = 0.0, s2 = 0.0;
-    if (e < E) {
-        float nv = last_value ? last_value[e] : 0.0f;  // ppo.py:77 next_values[-1] = 0
-        float gae = 0.0f;
-#pragma unroll 8
-        for (int t = T - 1; t >= 0; --t) {
-            const long long i = (long long)t * E + e;
-            const float r = (float)reward[i];  // python float promoted into the fp32 tensor op
-            const float v = value[i];
-            float delta;
-            if (done[i]) {  // v_next = 0.0, carry cut (ppo.py:84-87)
-                delta = r - v;
-                gae = delta;
-            } else {
-                delta = (r + g * nv) - v;
-                gae = delta + gl * gae;
+    float nv = 0.0f, gae = 0.0f;
+    if (walker && last_value) nv = last_value[e0 + lane];  // ppo.py:77 next_values[-1] = 0
+    for (int tend = T - 1; tend >= 0; tend -= kGaeT) {
+        const int tbeg = tend - kGaeT + 1 > 0 ? tend - kGaeT + 1 : 0, nt = tend - tbeg + 1;
+        for (int it = threadIdx.x; it < nt * kGaeBlock; it += kGaeThreads) {
+            const int k = it / kGaeBlock, j = it % kGaeBlock, e = e0 + j;
+            if (e < E) {
+                const long long i = (long long)(tbeg + k) * E + e;
+                sr[k][j] = (float)reward[i];  // python float promoted into the fp32 tensor op
+                sv[k][j] = value[i];
+                sd[k][j] = done[i];
             }
-            const float R = gae + v;
-            const float A = R - v;  // ppo.py:91 advantages = returns - values
-            ret[i] = R;
-            adv[i] = A;
-            s += (double)A;
-            s2 += (double)A * (double)A;
-            nv = v;
         }
+        __syncthreads();
+        if (walker) {
+#pragma unroll 8
+            for (int k = nt - 1; k >= 0; --k) {
+                const float r = sr[k][lane], v = sv[k][lane];
+                float delta;
+                if (sd[k][lane]) {  // v_next = 0.0, carry cut (ppo.py:84-87)
+                    delta = r - v;
+                    gae = delta;
+                } else {
+                    delta = (r + g * nv) - v;
+                    gae = delta + gl * gae;
+                }
+                const float R = gae + v;
+                const float A = R - v;  // ppo.py:91 advantages = returns - values
+                sret[k][lane] = R;
+                sadv[k][lane] = A;
+                s += (double)A;
+                s2 += (double)A * (double)A;
+                nv = v;
+            }
+        }
+        __syncthreads();
+        for (int it = threadIdx.x; it < nt * kGaeBlock; it += kGaeThreads) {
+            const int k = it / kGaeBlock, j = it % kGaeBlock, e = e0 + j;
+            if (e < E) {
+                const long long i = (long long)(tbeg + k) * E + e;
+                ret[i] = sret[k][j];
+                adv[i] = sadv[k][j];
+            }
+        }
+        __syncthreads();  // the next pass rewrites the LDS tiles
     }
     if (partials) {
-        block_sum2<kGaeBlock>(s, s2);
+        // waves 1-3 add zeros: the same value as the per-env-wave reduction of block_sum2<64>
+        block_sum2<kGaeThreads>(s, s2);
         if (threadIdx.x == 0) {
             partials[2 * blockIdx.x] = s;
             partials[2 * blockIdx.x + 1] = s2;
@@ -172,7 +203,7 @@ extern "C" int uavhip_gae(const double* reward, const uint8_t* done, const float
     }
     const float g = (float)gamma;
     const float gl = (float)(gamma * lam);  // cfg.GAMMA * cfg.GAE_LAMBDA is an f64 product (ppo.py:87)
-    hipLaunchKernelGGL(k_gae, dim3((E + kGaeBlock - 1) / kGaeBlock), dim3(kGaeBlock), 0, (hipStream_t)stream, reward,
+    hipLaunchKernelGGL(k_gae, dim3((E + kGaeBlock - 1) / kGaeBlock), dim3(kGaeThreads), 0, (hipStream_t)stream, reward,
                        done, value, last_value, (int)T, (int)E, g, gl, ret, adv, partials);
     return check_launch("k_gae");
 }
