@@ -124,9 +124,20 @@ __global__ __launch_bounds__(kRedBlock) void k_adv_normalize(float* __restrict__
                                                              const double* __restrict__ partials, int np,
                                                              long long n_total, double* __restrict__ stats) {
     __shared__ float sm[2];
+    double S = 0.0, S2 = 0.0;
+    if (threadIdx.x < kWave) {
+        // the partials arrive 64 at a time, one per lane (one load round instead of a chain of
+        // dependent loads), and are added in index order as before; lane 0 finishes
+        for (int c0 = 0; c0 < np; c0 += kWave) {
+            const int i = c0 + threadIdx.x, m = np - c0 < kWave ? np - c0 : kWave;
+            const double a = i < np ? partials[2 * i] : 0.0, b = i < np ? partials[2 * i + 1] : 0.0;
+            for (int k = 0; k < m; ++k) {
+                S += readlane_d(a, k);
+                S2 += readlane_d(b, k);
+            }
+        }
+    }
     if (threadIdx.x == 0) {
-        double S = 0.0, S2 = 0.0;
-        for (int i = 0; i < np; ++i) { S += partials[2 * i]; S2 += partials[2 * i + 1]; }
         const double mean = S / (double)n_total;
         double var = n_total > 1 ? (S2 - S * mean) / (double)(n_total - 1) : __builtin_nan("");
         if (var < 0.0) var = 0.0;
