@@ -945,6 +945,14 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
 #pragma unroll
         for (int u = 0; u < kEl; ++u) {
             const int i = threadIdx.x + u * NTHR;
+            if (!TR) {  // key padding mask from the registers: the 16 lanes of a token row vote
+                static_assert(LDX == 16 && NTHR % LDX == 0, "one token row = 16 lanes");
+                const unsigned long long nz = __ballot(v[u] != 0.f);
+                if (i < TOK * LDX && (i % LDX) == 0) {
+                    const int t = i / LDX, s = t / SPW, p = t - s * SPW;
+                    sm.mask[p * S + s] = (s < S - 1) && ((nz >> (lane_id() & 48)) & 0xFFFFull) == 0;
+                }
+            }
             if (i >= TOK * LDX) continue;
             sm.x[i] = v[u];
             if (TR) io.xg[(size_t)trow(i / LDX, b0) * 16 + (i % LDX)] = v[u];
@@ -955,7 +963,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         }
     }
     __syncthreads();
-    if (threadIdx.x < SPW * S) {  // key padding mask: all-zero rows, last row never masked
+    if (TR && threadIdx.x < SPW * S) {  // key padding mask: all-zero rows, last row never masked
         const int p = threadIdx.x / S, s = threadIdx.x - p * S;
         bool z = true;
         for (int k = 0; k < IN; ++k) z = z && (sm.x[(s * SPW + p) * LDX + k] == 0.f);
@@ -968,7 +976,6 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     const float* headw_c = P + kOffs.o[kCriticHead];
     // actor trunk (1 layer) + head
     if constexpr (ROWS) {
-        __syncthreads();  // sm.mask -> ring loads
         APre<kPwD> pw[3];
         RowPre<2> rp;
         rows_prologue<kActorTrunk>(sm, P, pw, rp, rio, b0);
