@@ -945,12 +945,15 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
 #pragma unroll
         for (int u = 0; u < kEl; ++u) {
             const int i = threadIdx.x + u * NTHR;
-            if (!TR) {  // key padding mask from the registers: the 16 lanes of a token row vote
+            {  // key padding mask (all-zero rows, the last never masked) from the registers: the 16
+               // lanes of a token row vote
                 static_assert(LDX == 16 && NTHR % LDX == 0, "one token row = 16 lanes");
                 const unsigned long long nz = __ballot(v[u] != 0.f);
                 if (i < TOK * LDX && (i % LDX) == 0) {
                     const int t = i / LDX, s = t / SPW, p = t - s * SPW;
-                    sm.mask[p * S + s] = (s < S - 1) && ((nz >> (lane_id() & 48)) & 0xFFFFull) == 0;
+                    const bool m = (s < S - 1) && ((nz >> (lane_id() & 48)) & 0xFFFFull) == 0;
+                    sm.mask[p * S + s] = m;
+                    if (TR) io.mask[(size_t)(b0 + p) * S + s] = m ? 1.f : 0.f;
                 }
             }
             if (i >= TOK * LDX) continue;
@@ -963,13 +966,6 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         }
     }
     __syncthreads();
-    if (TR && threadIdx.x < SPW * S) {  // key padding mask: all-zero rows, last row never masked
-        const int p = threadIdx.x / S, s = threadIdx.x - p * S;
-        bool z = true;
-        for (int k = 0; k < IN; ++k) z = z && (sm.x[(s * SPW + p) * LDX + k] == 0.f);
-        sm.mask[p * S + s] = (s < S - 1) && z;
-        if (TR) io.mask[(size_t)(b0 + p) * S + s] = ((s < S - 1) && z) ? 1.f : 0.f;
-    }
     PTR(1);
     const int wv = threadIdx.x >> 6;
     const float* headw_a = P + kOffs.o[kActorHead];
