@@ -114,6 +114,7 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
         if (i < S_.count) {  // uniform part stride in this mode (src_rest = src + part_stride)
             const float* src = S_.src + i;
             int p = wv;
+#pragma unroll 4
             for (; p + 12 < S_.parts; p += 16) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) acc[u] += src[(size_t)(p + 4 * u) * ps];
@@ -133,6 +134,7 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
             // four independent chains keep four loads in flight per thread
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
             int p = 0;
+#pragma unroll 4
             for (; p + 4 <= S_.parts; p += 4) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) acc[u] += part(p + u)[i];
