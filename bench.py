@@ -306,9 +306,12 @@ def main():
     E, T = args.envs, args.horizon
     torch.manual_seed(0)  # identical initial policy on every rank
     policy = TransformerActorCritic().to(dev)
-    env = VecUAVEnv(E, args.uavs, args.targets, 1, 1, seed=1 + rank, full_reset_period=200)
-    eng = RolloutEngine(env, policy, T, want_info=True, bootstrap=True, seed=1000 + rank, normalize=(world == 1),
-                        row_cache=not args.full_window, fused_step=False if args.unfused else None)
+    # rank r owns envs [r E, (r + 1) E) of the node's world * E: its scenes and action samples are
+    # those of the same envs in a one-process run over all of them (env_base / total_envs)
+    env = VecUAVEnv(E, args.uavs, args.targets, 1, 1, seed=1, full_reset_period=200, env_base=rank * E)
+    eng = RolloutEngine(env, policy, T, want_info=True, bootstrap=True, seed=1000, normalize=(world == 1),
+                        row_cache=not args.full_window, fused_step=False if args.unfused else None,
+                        total_envs=world * E)
     eng.start()
 
     # The iteration is captured once into a hipGraph and replayed. HIP events (recorded on the

@@ -41,6 +41,8 @@ typedef void* uavhip_stream_t; /* hipStream_t */
 #define UAVHIP_ENV_OBS_F16 2       /* obs_out of uavhip_env_reset / uavhip_env_step is IEEE binary16
                                       (round-to-nearest-even of the f32 window; BASELINE config 4)
                                       instead of f32; the env's own window stays f32          */
+#define UAVHIP_ENV_NO_REPLAY 4     /* multi-step launches: never use the omega = 0 replay kernel
+                                      (K2r, env_replay.hpp), always the step-by-step K2 / K2g  */
 
 enum uavhip_status {
     UAVHIP_OK = 0,
@@ -133,6 +135,9 @@ typedef struct uavhip_env {
                                   pre-generated spare a full reset flips to                  */
     int32_t flags;              /* UAVHIP_ENV_* bits (0 = defaults)                    */
     uint64_t seed;             /* Philox key for on-device scene generation                 */
+    uint64_t env_base;         /* global index of env 0: scene counters run on env_base + e, so
+                                  a rank's shard [env_base, env_base + E) draws the scenes the
+                                  same envs draw in one process over the union (0 on one GPU) */
     double prm[UAVHIP_PRM_COUNT];
     double gen[UAVHIP_GEN_COUNT];
     /* scene: entities.py records as SoA */

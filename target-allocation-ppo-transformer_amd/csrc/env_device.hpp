@@ -57,14 +57,15 @@ __device__ __forceinline__ int rank_in_wave(uint32_t key, int lane, int n) {
     return r;
 }
 
-// uav_env.py:65-173 distribution into scene buffer index sb; Philox counter (lane, env, gen, stream).
+// uav_env.py:65-173 distribution into scene buffer index sb; Philox counter (lane, global env index
+// env_base + e, gen, stream): a rank's shard draws the scenes of the same envs of the union.
 template <int TPL>
 __device__ void gen_scene_wave(const uavhip_env& env, long long sb, int e, int gen, int lane) {
     const int N = env.N, M = env.M;
     const uint32_t k0 = (uint32_t)env.seed, k1 = (uint32_t)(env.seed >> 32);
     const double* g = env.gen;
     const double H = g[UAVHIP_GEN_MAP_H];
-    const uint32_t ue = (uint32_t)e, ug = (uint32_t)gen;
+    const uint32_t ue = (uint32_t)(env.env_base + (uint64_t)e), ug = (uint32_t)gen;
     {   // UAVs: N//4 of type 2 at random positions (random.shuffle(uav_types), :81-84)
         const u32x4 rk = philox(u32x4{(uint32_t)lane, ue, ug, 0u}, k0, k1);
         const u32x4 ru = philox(u32x4{(uint32_t)lane, ue, ug, 1u}, k0, k1);

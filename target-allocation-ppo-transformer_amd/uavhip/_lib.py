@@ -15,7 +15,7 @@ SEQ_LEN = 5
 STATE_DIM = 14
 OBS_FLOATS = SEQ_LEN * STATE_DIM
 MAX_N, MAX_M, MAX_OBSTACLES = 64, 128, 8
-ENV_ONE_PER_WAVE, ENV_OBS_F16 = 1, 2  # uavhip_env.flags bits
+ENV_ONE_PER_WAVE, ENV_OBS_F16, ENV_NO_REPLAY = 1, 2, 4  # uavhip_env.flags bits
 
 PRM = dict(ZETA_D=0, K=1, C1=2, C2=3, C3=4, C4=5, OMEGA=6, ZETA_OBS=7)
 PRM_COUNT = 8
@@ -42,6 +42,7 @@ class EnvDesc(ctypes.Structure):
     """Mirror of `struct uavhip_env` (include/uavhip.h)."""
     _fields_ = [("E", _i32), ("N", _i32), ("M", _i32), ("Kn", _i32), ("Ki", _i32),
                 ("full_reset_period", _i32), ("scene_buffers", _i32), ("flags", _i32), ("seed", ctypes.c_uint64),
+                ("env_base", ctypes.c_uint64),
                 ("prm", ctypes.c_double * PRM_COUNT), ("gen", ctypes.c_double * GEN_COUNT)] + \
               [(n, _vp) for n in ("uav_pos", "uav_vel", "uav_load", "uav_cost", "uav_type", "tgt_pos", "tgt_vel",
                                   "tgt_value", "tgt_id", "nfz_pos", "icp_pos", "icp_vel", "p_dmg", "p_pen",

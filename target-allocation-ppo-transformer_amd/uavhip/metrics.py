@@ -55,13 +55,17 @@ def derived(rec):
 
 def csv_rows(rec, first_episode=1, window=50, losses=(0.0, 0.0, 0.0)):
     """One CSV row per record in the given order, columns as main_train.py:56-61 (Avg_Reward and
-    Avg_Q0 are moving averages over the last `window` episodes, :146-157)."""
+    Avg_Q0 are moving averages over the last `window` episodes, :146-157). losses: (critic, actor,
+    entropy) of the update behind every row (main_train.py:176-178; zeros when none ran), or one
+    such triple per record."""
     d = derived(rec)
+    per_row = np.ndim(losses) == 2
     rows = []
     for i in range(len(rec)):
         lo = max(0, i + 1 - window)
+        lc, la, le = losses[i] if per_row else losses
         rows.append([first_episode + i, f"{np.mean(d['reward'][lo:i + 1]):.4f}", f"{np.mean(d['q0'][lo:i + 1]):.4f}",
                      f"{d['avg_J'][i]:.4f}", int(d["max_cov"][i]), f"{d['action1_ratio'][i]:.4f}",
                      f"{d['valid_rate'][i]:.4f}", f"{d['avg_p_dmg'][i]:.4f}", f"{d['avg_p_final'][i]:.4f}",
-                     f"{losses[0]:.6f}", f"{losses[1]:.6f}", f"{losses[2]:.6f}"])
+                     f"{lc:.6f}", f"{la:.6f}", f"{le:.6f}"])
     return rows

@@ -19,6 +19,7 @@ from torch.distributions import Categorical
 from . import _lib
 from ._lib import LIB, check, ptr, stream_handle
 from .config import cfg
+from .vec_env import check_out
 
 
 def _ortho(layer, std=float(np.sqrt(2)), bias=0.0):
@@ -62,7 +63,11 @@ class TransformerActorCritic(nn.Module):
         self._packed = None
         self._packed_key = None
         self._desc = None
-        self.sample_seed = 0x1234ABCD
+        # Philox key of the on-device action sampling, drawn from torch's RNG after the parameters (the
+        # initialisation stays the reference's): torch.manual_seed controls it, as it controls the
+        # reference's Categorical sampling (transformer_net.py:120), and separate instances / runs
+        # sample independently. The counter starts at 0 per instance.
+        self.sample_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         self._sample_offset = 0
 
     def forward(self, state):
@@ -128,6 +133,8 @@ class TransformerActorCritic(nn.Module):
         if states.dtype != torch.float32:
             states = states.float()
         B = states.shape[0]
+        if states.numel() != B * cfg.SEQ_LEN * cfg.STATE_DIM:
+            raise ValueError(f"states must be [B, {cfg.SEQ_LEN}, {cfg.STATE_DIM}] (got {tuple(states.shape)})")
         if check_weights or self._packed is None:
             self.packed_weights()
         dev = states.device
@@ -136,6 +143,11 @@ class TransformerActorCritic(nn.Module):
         value = torch.empty(B, dtype=torch.float32, device=dev) if value is None else value
         if actions is not None:
             actions = actions.to(device=dev, dtype=torch.int8).contiguous()
+            check_out(actions, "actions", torch.int8, (B,), dev)
+        for t, name, dt, tail in ((action_out, "action_out", torch.int8, ()), (logp, "logp", torch.float32, ()),
+                                  (value, "value", torch.float32, ()), (entropy, "entropy", torch.float32, ()),
+                                  (logits, "logits", torch.float32, (2,))):
+            check_out(t, name, dt, (B,), dev, tail)
         if offset is None:
             offset = self._sample_offset
             self._sample_offset += B
@@ -161,9 +173,17 @@ class TransformerActorCritic(nn.Module):
         The weights must be packed (packed_weights())."""
         if self._packed is None:
             self.packed_weights()
+        E, dev = env.E, env.device
         env._check_obs(obs_out)
-        if rowproj.numel() < LIB.uavhip_policy_rowproj_floats(env.E) or states.dtype != torch.float32:
-            raise ValueError("rowproj: need rowproj_buffer(E); states: float32 windows")
+        check_out(states, "states", torch.float32, (E,), dev, (cfg.SEQ_LEN, cfg.STATE_DIM))
+        if rowproj.numel() < LIB.uavhip_policy_rowproj_floats(E) or rowproj.dtype != torch.float32 or \
+                not rowproj.is_contiguous():
+            raise ValueError("rowproj: need a contiguous float32 rowproj_buffer(E)")
+        for t, name, dt, tail in ((action_out, "action_out", torch.int8, ()), (logp, "logp", torch.float32, ()),
+                                  (value, "value", torch.float32, ()), (reward_out, "reward_out", torch.float64, ()),
+                                  (done_out, "done_out", torch.uint8, ()),
+                                  (info_out, "info_out", torch.float64, (_lib.INFO_COUNT,))):
+            check_out(t, name, dt, (E,), dev, tail)
         seed = self.sample_seed if seed is None else seed
         check(LIB.uavhip_rollout_step(self._desc, env.desc, ptr(states), ptr(rowproj), int(step), int(bool(fill)),
                                       ctypes.c_uint64(seed), ctypes.c_uint64(offset), ptr(offset_dev),

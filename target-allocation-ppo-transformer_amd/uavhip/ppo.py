@@ -2,7 +2,8 @@
 PPOAgent with the reference's API (agents/ppo.py:12-184), used by the drop-in agents/ppo.py.
 
 GAE here follows ppo.py:70-94 op for op in fp32 (returns bit-identical to the reference on the
-same buffer); the clipped-PPO epochs (ppo.py:96-181) run as torch autograd on the GPU.
+same buffer); the clipped-PPO epochs (ppo.py:96-181) run on the HIP training step
+(uavhip.train.FusedPPOTrainer), or as torch autograd on the GPU (ppo_epochs, GraphPPOUpdater).
 """
 import ctypes
 
@@ -57,8 +58,10 @@ def gae_workspace(T, E, device):
 
 
 def ppo_epochs(policy, optimizer, states, actions, old_logprobs, old_values, returns, advantages, epochs=None,
-               batch_size=None, eps_clip=None, grad_clip=None, generator=None):
-    """Clipped-PPO minibatch epochs (ppo.py:96-169). Returns (mean actor loss, critic loss, entropy, n)."""
+               batch_size=None, eps_clip=None, grad_clip=None, generator=None, perms=None):
+    """Clipped-PPO minibatch epochs (ppo.py:96-169). Returns (mean actor loss, critic loss, entropy, n).
+    Minibatches: BatchSampler(SubsetRandomSampler(range(n), generator), batch_size, drop_last=True)
+    per epoch as ppo.py:115, or over the given per-epoch row orders `perms` (recorded sampler draws)."""
     epochs = cfg.K_EPOCHS if epochs is None else epochs
     batch_size = cfg.BATCH_SIZE if batch_size is None else batch_size
     eps = cfg.EPS_CLIP if eps_clip is None else eps_clip
@@ -69,8 +72,12 @@ def ppo_epochs(policy, optimizer, states, actions, old_logprobs, old_values, ret
     sa = sc = se = 0.0
     cnt = 0
     acc = torch.zeros(3, dtype=torch.float64, device=dev)
-    for _ in range(epochs):
-        for idx in BatchSampler(SubsetRandomSampler(range(n), generator=generator), batch_size, drop_last=True):
+    if perms is not None:
+        epochs = len(perms)
+    for ep in range(epochs):
+        order = [int(i) for i in perms[ep]] if perms is not None else \
+            SubsetRandomSampler(range(n), generator=generator)
+        for idx in BatchSampler(order, batch_size, drop_last=True):
             idx = torch.as_tensor(idx, device=dev)
             logp, v, ent = policy.evaluate(states[idx], actions[idx])
             v = torch.squeeze(v)
@@ -156,8 +163,10 @@ class PPOAgent:
             from .train import FusedPPOTrainer
             if self.trainer is None:
                 self.trainer = FusedPPOTrainer(self.policy, cfg.BATCH_SIZE)
-            self.trainer.set_buffers(old_states, old_actions, old_logprobs, values.detach(), returns, advantages)
-            sa, sc, se, cnt = self.trainer.run(use_graph=False)
+            # the trainer's own buffers (fixed addresses): one captured hipGraph per epoch length,
+            # reused by every later update with the same number of minibatches
+            self.trainer.stage(old_states, old_actions, old_logprobs, values.detach(), returns, advantages)
+            sa, sc, se, cnt = self.trainer.run(use_graph=True)
         else:
             sa, sc, se, cnt = ppo_epochs(self.policy, self.optimizer, old_states, old_actions, old_logprobs,
                                          values.detach(), returns, advantages)

@@ -42,13 +42,18 @@ class Trajectory:
 
 
 class RolloutEngine:
-    def __init__(self, env, policy, horizon, want_info=True, bootstrap=True, seed=0, normalize=True, row_cache=True,
-                 fused_step=None):
+    def __init__(self, env, policy, horizon, want_info=True, bootstrap=True, seed=None, normalize=True, row_cache=True,
+                 fused_step=None, total_envs=None):
         """normalize=False leaves the advantages raw after GAE: a data-parallel caller normalises
         them with the moments of the whole gathered batch in gather() (ppo.py:94).
         row_cache=False runs every step on the full-window forward (uavhip_policy_forward).
         fused_step: one launch per step (uavhip_rollout_step: forward + sample + env step); default
-        on when the row cache is on and N, M <= 64."""
+        on when the row cache is on and N, M <= 64.
+        seed: Philox key of the action sampling (default: the policy's sample_seed, drawn from
+        torch's RNG). Sampling counters are global env indices: step t of env e draws counter
+        t * total_envs + env.env_base + e, so a rank's shard (VecUAVEnv(env_base=shard start),
+        total_envs = all ranks' envs, the same seed everywhere) samples exactly what the same envs
+        sample in one process over the union, and no two ranks share a counter."""
         self.env = env
         self.normalize = normalize
         self.iteration = 0
@@ -56,7 +61,11 @@ class RolloutEngine:
         self.policy = policy
         self.T = int(horizon)
         self.bootstrap = bootstrap
-        self.seed = int(seed)
+        self.seed = int(policy.sample_seed if seed is None else seed)
+        self.env_base = int(getattr(env, "env_base", 0))
+        self.total = int(env.E if total_envs is None else total_envs)
+        if self.env_base + env.E > self.total:
+            raise ValueError(f"env_base {self.env_base} + E {env.E} exceeds total_envs {self.total}")
         self.traj = Trajectory(self.T, env.E, env.device, want_info)
         self.counter = torch.zeros(1, dtype=torch.int64, device=env.device)  # sampling counter base
         # window-row projections of the obs windows (policy.rowproj_buffer): the windows of one
@@ -77,12 +86,16 @@ class RolloutEngine:
             self.env.generate_scenes()
         self.env.reset(episode=1, obs_out=self.traj.obs[self.T])  # moved to obs[0] by the first _body
 
+    def _offset(self, t):
+        """Sampling counter base of step t (the device counter adds (T + 1) * total per iteration)."""
+        return t * self.total + self.env_base
+
     def _forward(self, t, obs, actions, logp, value):
         ev = self.policy_events
         if ev is not None:
             ev[t][0].record()
         self.policy.fused_forward(obs, action_out=actions, logp=logp, value=value, seed=self.seed,
-                                  offset=t * self.env.E, offset_dev=self.counter, check_weights=False,
+                                  offset=self._offset(t), offset_dev=self.counter, check_weights=False,
                                   rowproj=self.rowproj, step=t, fill=t == 0)
         if ev is not None:
             ev[t][1].record()
@@ -99,7 +112,7 @@ class RolloutEngine:
                 self.policy.rollout_step(env, tr.obs[t], self.rowproj, t, t == 0, tr.actions[t], tr.logp[t],
                                          tr.values[t], tr.obs[t + 1], tr.rewards[t], tr.dones[t],
                                          None if tr.info is None else tr.info[t], seed=self.seed,
-                                         offset=t * env.E, offset_dev=self.counter)
+                                         offset=self._offset(t), offset_dev=self.counter)
                 if ev is not None:
                     ev[t][1].record()
                 continue
@@ -118,7 +131,7 @@ class RolloutEngine:
         gae(tr.rewards, tr.dones, tr.values, last_values=last, normalize=self.normalize,
             out=(tr.ret, tr.adv, tr.partials, tr.stats))
         env.refresh_scenes()  # regenerate spare scenes consumed by full resets (off the step path)
-        self.counter.add_((self.T + 1) * env.E)
+        self.counter.add_((self.T + 1) * self.total)
 
     @torch.no_grad()
     def collect(self, eager=False):

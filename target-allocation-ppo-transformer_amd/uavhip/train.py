@@ -77,7 +77,9 @@ class FusedPPOTrainer:
         d.value_coef, d.entropy_coef = value_coef, entropy_coef
         self.desc = d
         self.bufs = None
-        self.graph = None
+        self.graphs = {}    # steps per epoch -> captured epoch hipGraph over the current buffers
+        self._store = None  # stage(): the trainer's own trajectory buffers
+        self._cap = 0
 
     def set_buffers(self, states, actions, old_logprobs, old_values, returns, advantages):
         """Trajectory buffers the minibatches are drawn from (kept by reference: a captured graph
@@ -92,7 +94,30 @@ class FusedPPOTrainer:
                      advantages.to(device=dev, dtype=torch.float32).contiguous().reshape(n))
         self.n = n
         self.perm = torch.zeros(n, dtype=torch.int32, device=dev)  # the epoch's minibatch order
-        self.graph = None
+        self.graphs = {}
+        self._store = None
+
+    def stage(self, states, actions, old_logprobs, old_values, returns, advantages):
+        """Copy a trajectory into the trainer's own device buffers (capacity grows in powers of two),
+        so the epoch graphs captured for one size stay valid for the next update of any size they
+        cover (PPOAgent.update: every update has a different buffer length)."""
+        n = states.shape[0]
+        dev = self.device
+        if self._store is None or self._cap < n:
+            cap = 1 << max(10, (n - 1).bit_length())
+            f32 = dict(dtype=torch.float32, device=dev)
+            self._store = (torch.zeros(cap, cfg.SEQ_LEN, cfg.STATE_DIM, **f32),
+                           torch.zeros(cap, dtype=torch.int8, device=dev),
+                           *(torch.zeros(cap, **f32) for _ in range(4)))
+            self._cap = cap
+            self.perm = torch.zeros(cap, dtype=torch.int32, device=dev)
+            self.graphs = {}
+        src = (states.reshape(n, cfg.SEQ_LEN, cfg.STATE_DIM), actions.reshape(n), old_logprobs.reshape(n),
+               old_values.reshape(n), returns.reshape(n), advantages.reshape(n))
+        for dst, x in zip(self._store, src):
+            dst[:n].copy_(x)
+        self.bufs = self._store
+        self.n = n
 
     def step(self, phases=_lib.PPO_FULL, idx=None):
         """uavhip_ppo_step phases (bit mask) on this rank's rows idx (default self.idx)."""
@@ -121,29 +146,46 @@ class FusedPPOTrainer:
         return self.grads
 
     def capture(self):
+        """Capture one epoch (every minibatch step of the current buffer length) into a hipGraph."""
         if self.world > 1:
             raise RuntimeError("graph capture is single-GPU; the data-parallel step has collectives between phases")
+        steps = self.n // self.global_minibatch
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=s):  # one epoch: every minibatch step
-            for b in range(self.n // self.global_minibatch):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):  # one epoch: every minibatch step
+            for b in range(steps):
                 self.step(_lib.PPO_FULL, self._rows(self.perm, b))
         torch.cuda.current_stream().wait_stream(s)
+        self.graphs[steps] = g
+        return g
 
-    def run(self, epochs=None, generator=None, use_graph=True):
-        """K epochs of minibatch steps over the buffers -> (mean actor loss, critic loss, entropy, n_steps)."""
+    @property
+    def graph(self):
+        return self.graphs.get(self.n // self.global_minibatch)
+
+    def run(self, epochs=None, generator=None, use_graph=True, perms=None):
+        """K epochs of minibatch steps over the buffers -> (mean actor loss, critic loss, entropy, n_steps).
+        Minibatch order: torch.randperm(n, generator) per epoch (SubsetRandomSampler's draw,
+        ppo.py:115), or the given `perms` ([epochs][n] row orders, e.g. recorded from the reference)."""
         epochs = cfg.K_EPOCHS if epochs is None else epochs
+        if perms is not None:
+            perms = [torch.as_tensor(p, dtype=torch.int32) for p in perms]
+            epochs = len(perms)
+            if any(p.numel() != self.n for p in perms):
+                raise ValueError(f"perms: every epoch's order must list the {self.n} rows")
         use_graph = use_graph and self.world == 1
-        if use_graph and self.graph is None:
-            self.capture()
+        steps = self.n // self.global_minibatch
+        graph = self.graph if use_graph else None
+        if use_graph and graph is None and steps > 0:
+            graph = self.capture()
         self.stats.zero_()
         cnt = 0
-        steps = self.n // self.global_minibatch
-        for _ in range(epochs):
-            self.perm.copy_(torch.randperm(self.n, generator=generator))
-            if use_graph:
-                self.graph.replay()
+        for ep in range(epochs):
+            order = perms[ep] if perms is not None else torch.randperm(self.n, generator=generator)
+            self.perm[:self.n].copy_(order)
+            if graph is not None:
+                graph.replay()
                 cnt += steps
                 continue
             for b in range(steps):

@@ -16,11 +16,34 @@ SCENE_KEYS_F64 = ("uav_pos", "uav_vel", "uav_load", "uav_cost", "tgt_pos", "tgt_
                   "icp_pos", "icp_vel")
 
 
+def _same_device(t, device):
+    return t.device.type == device.type and (device.index is None or t.device.index == device.index)
+
+
+def check_out(t, name, dtype, lead, device, tail=()):
+    """A caller-provided kernel buffer (read or written through a raw pointer): right device and
+    dtype, contiguous, exactly prod(lead + tail) elements -- anything else would be an out-of-bounds
+    or misread device access the C side cannot detect. None passes (NULL = not wanted)."""
+    if t is None:
+        return
+    n = 1
+    for d in tuple(lead) + tuple(tail):
+        n *= int(d)
+    if not isinstance(t, torch.Tensor) or not _same_device(t, device) or t.dtype != dtype or \
+            not t.is_contiguous() or t.numel() != n:
+        got = (f"{t.dtype} {tuple(t.shape)} on {t.device}, contiguous={t.is_contiguous()}"
+               if isinstance(t, torch.Tensor) else type(t).__name__)
+        raise ValueError(f"{name}: need a contiguous {dtype} tensor of {n} elements on {device} (got {got})")
+
+
 class VecUAVEnv:
     def __init__(self, num_envs, num_uavs=None, num_targets=None, num_nfz=None, num_interceptors=None, config=None,
-                 device="cuda", seed=0, full_reset_period=None, scene_buffers=None, obs_dtype=torch.float32):
+                 device="cuda", seed=0, full_reset_period=None, scene_buffers=None, obs_dtype=torch.float32,
+                 env_base=0):
         """obs_dtype: float32, or float16 (BASELINE config 4: observations emitted as IEEE binary16,
-        UAVHIP_ENV_OBS_F16; the env's own window deque stays f32)."""
+        UAVHIP_ENV_OBS_F16; the env's own window deque stays f32).
+        env_base: global index of env 0 when this is one rank's shard of a larger env set -- the
+        on-device scenes of env e are those of env env_base + e of the union (uavhip_env.env_base)."""
         c = config or default_cfg
         if obs_dtype not in (torch.float32, torch.float16):
             raise ValueError(f"obs_dtype must be torch.float32 or torch.float16 (got {obs_dtype})")
@@ -63,6 +86,10 @@ class VecUAVEnv:
         d.full_reset_period = period
         d.scene_buffers = B
         d.seed = int(seed) & (2 ** 64 - 1)
+        self.env_base = int(env_base)
+        if self.env_base < 0:
+            raise ValueError("env_base must be >= 0")
+        d.env_base = self.env_base
         d.flags = _lib.ENV_OBS_F16 if obs_dtype == torch.float16 else 0
         for i, v in enumerate(params_vector(c)):
             d.prm[i] = float(v)
@@ -126,11 +153,13 @@ class VecUAVEnv:
         return mask
 
     def score_pairs(self, mask=None):
+        check_out(mask, "mask", torch.uint8, (self.E,), self.device)
         check(LIB.uavhip_score_pairs(self.desc, ptr(mask), stream_handle()), "uavhip_score_pairs")
 
     def generate_scenes(self, mask=None):
         """On-device Philox scenes (distribution of uav_env.py:65-173) + pair tables, for the
         active buffer and (double-buffered) the spare."""
+        check_out(mask, "mask", torch.uint8, (self.E,), self.device)
         check(LIB.uavhip_scene_generate(self.desc, ptr(mask), stream_handle()), "uavhip_scene_generate")
 
     def refresh_scenes(self):
@@ -138,12 +167,15 @@ class VecUAVEnv:
         check(LIB.uavhip_scene_refresh(self.desc, stream_handle()), "uavhip_scene_refresh")
 
     # ------------------------------------------------------------------ reset / step
-    def _check_obs(self, obs):
+    def _check_obs(self, obs, lead=None):
         if obs is not None and obs.dtype != self.obs_dtype:
             raise TypeError(f"obs_out must be {self.obs_dtype} (got {obs.dtype})")
+        check_out(obs, "obs_out", self.obs_dtype, (self.E,) if lead is None else lead, self.device,
+                  (_lib.SEQ_LEN, _lib.STATE_DIM))
 
     def reset(self, mask=None, episode=-1, obs_out=None):
         self._check_obs(obs_out)
+        check_out(mask, "mask", torch.uint8, (self.E,), self.device)
         out = self._obs if obs_out is None else obs_out
         check(LIB.uavhip_env_reset(self.desc, ptr(mask), int(episode), ptr(out), stream_handle()), "uavhip_env_reset")
         return out
@@ -152,7 +184,6 @@ class VecUAVEnv:
              want_info=True):
         """actions: int8 tensor [E] (one step) or [T, E] (T fused steps). Returns (obs, reward,
         done, info) device tensors shaped [E, ...] or [T, E, ...]."""
-        self._check_obs(obs_out)
         if actions.dtype != torch.int8 or actions.device != self.device:
             actions = actions.to(device=self.device, dtype=torch.int8)
         actions = actions.contiguous()
@@ -173,6 +204,10 @@ class VecUAVEnv:
             done = done_out if done_out is not None else torch.empty(*lead, dtype=torch.uint8, device=dev)
             info = (info_out if info_out is not None else
                     torch.empty(*lead, _lib.INFO_COUNT, dtype=torch.float64, device=dev)) if want_info else None
+        self._check_obs(obs, lead)
+        check_out(rew, "reward_out", torch.float64, lead, self.device)
+        check_out(done, "done_out", torch.uint8, lead, self.device)
+        check_out(info, "info_out", torch.float64, lead, self.device, (_lib.INFO_COUNT,))
         check(LIB.uavhip_env_step(self.desc, ptr(actions), T, int(bool(auto_reset)), ptr(obs), ptr(rew), ptr(done),
                                   ptr(info), stream_handle()), "uavhip_env_step")
         return obs, rew, done, info

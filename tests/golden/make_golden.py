@@ -17,6 +17,9 @@ Outputs (all numpy .npz, loaded with allow_pickle=False):
   policy.npz     TransformerActorCritic state_dicts + state batch -> logits/logp/value/entropy
   gae.npz        PPOAgent.update() GAE returns + normalised advantages (captured in-frame)
   ppo_update.npz one full PPOAgent.update() (seeded sampler) -> losses + final weights
+  main_train.npz main_train.train() itself for 30 episodes: every env.step (action, reward, done,
+                 info), the per-episode statistic accumulators of main_train.py:98-136 read from
+                 train()'s own frame, its CSV rows (:161-195) and the update losses behind them
 
 Usage:  python tests/golden/make_golden.py   (takes ~1 min on CPU)
 """
@@ -444,6 +447,78 @@ def gen_update(policy):
     return out
 
 
+# ----------------------------------------------------------------------------- main_train statistics
+EP_LOCALS = ("current_ep_reward", "current_q0", "ep_total_J", "ep_steps", "ep_max_cov", "ep_action1_cnt",
+             "ep_valid_cnt", "ep_total_p_dmg", "ep_total_p_final", "ep_steps_with_assign")
+
+
+def gen_main_train(episodes=30):
+    """Run the reference's training driver (main_train.train) and record what its statistics are
+    made of and what it computed from them: env.step is wrapped to log each step's action / reward /
+    done / info; the per-episode accumulators are read from train()'s own frame when the next
+    episode's env.reset() is called (and, for the last episode, when its CSV row is written); the
+    CSV writer is wrapped to capture the rows and the update stats behind their loss columns."""
+    import csv
+    import tempfile
+    import main_train as mt
+    steps, eps, rows = [], [], []
+    real_step, real_reset, real_writer = UAVEnv.step, UAVEnv.reset, csv.writer
+
+    def frame_of_train():
+        f = sys._getframe(2)
+        return f.f_locals if f.f_code.co_name == "train" else None
+
+    def snapshot(fl, episode):
+        return [float(episode)] + [float(fl[k]) for k in EP_LOCALS]
+
+    def step(self, action):
+        obs, r, d, info = real_step(self, action)
+        iv = info["is_valid_action"]
+        steps.append([len(eps) + 1, action, r, float(d), info["J_val"], info["num_assigned"],
+                      -1.0 if iv is None else float(bool(iv)), info["avg_p_dmg"], info["avg_p_final"]])
+        return obs, r, d, info
+
+    def reset(self, full_reset=True):
+        fl = frame_of_train()
+        if fl is not None and "ep_total_J" in fl:   # the previous episode's final accumulators
+            eps.append(snapshot(fl, fl["i_episode"] - 1))
+        return real_reset(self, full_reset)
+
+    class Writer:
+        def __init__(self, f):
+            self.w = real_writer(f)
+
+        def writerow(self, row):
+            fl = sys._getframe(1).f_locals
+            if "ep_total_J" in fl:
+                st = fl["ppo_stats"]
+                rows.append(([str(x) for x in row], [st["loss_critic"], st["loss_actor"], st["entropy"]] if st else
+                             [0.0, 0.0, 0.0]))
+                if fl["i_episode"] == episodes:
+                    eps.append(snapshot(fl, fl["i_episode"]))
+            return self.w.writerow(row)
+
+    saved = (cfg.MAX_EPISODES, os.getcwd())
+    UAVEnv.step, UAVEnv.reset, csv.writer = step, reset, Writer
+    try:
+        cfg.MAX_EPISODES = episodes
+        np.random.seed(0); random.seed(0); torch.manual_seed(0)
+        with tempfile.TemporaryDirectory() as d:
+            os.chdir(d)
+            mt.train()
+    finally:
+        UAVEnv.step, UAVEnv.reset, csv.writer = real_step, real_reset, real_writer
+        cfg.MAX_EPISODES = saved[0]
+        os.chdir(saved[1])
+    assert len(eps) == episodes and len(rows) == episodes // 10
+    return {"steps": np.array(steps, np.float64), "episodes": np.array(eps, np.float64),
+            "csv_rows": np.array(json.dumps([r for r, _ in rows])),
+            "csv_losses": np.array([l for _, l in rows], np.float64),
+            "fields": np.array(json.dumps(["episode", "action", "reward", "done", "J_val", "num_assigned", "is_valid",
+                                           "avg_p_dmg", "avg_p_final"])),
+            "episode_fields": np.array(json.dumps(["episode"] + list(EP_LOCALS))), "meta": np.array(json.dumps(meta()))}
+
+
 def main():
     outdir = HERE
     torch.set_num_threads(min(8, os.cpu_count() or 1))
@@ -455,6 +530,7 @@ def main():
     np.savez_compressed(os.path.join(outdir, "policy.npz"), **pol)
     np.savez_compressed(os.path.join(outdir, "gae.npz"), **gen_gae())
     np.savez_compressed(os.path.join(outdir, "ppo_update.npz"), **gen_update(pol))
+    np.savez_compressed(os.path.join(outdir, "main_train.npz"), **gen_main_train())
     print("golden fixtures written to", outdir)
 
 

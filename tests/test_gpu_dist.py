@@ -1,0 +1,146 @@
+"""GPU: BASELINE configs[3]'s code path on the one MI355X -- envs sharded over world = 2 rank
+processes, each rolling out its shard, ONE trajectory all-gather (compact rows + window rebuild on
+the GPU), advantages normalised with the all-reduced global moments (ppo.py:94), then the
+data-parallel PPO update (FORWARD / all-reduce loss sums / BACKWARD / all-reduce gradients / clip +
+Adam per global minibatch). gloo carries the collectives (RCCL will not put two ranks on one
+device); the data path and every kernel are the ones the RCCL run uses (uavhip/dist.py,
+uavhip/rollout.py, uavhip/train.py).
+
+Checked against ONE process stepping the union of the envs with the same seeds (SURVEY.md section
+4): shards draw their scenes and action samples by global env index (VecUAVEnv(env_base=...),
+RolloutEngine(total_envs=...)), so over two iterations -- with episode ends, full resets flipping
+to refreshed scenes and windows carried across the iteration boundary -- the gathered batch equals
+the union's trajectory in (rank, step, env) order bit for bit, the normalised advantages agree to
+1e-6 (the moments are folded in another order), and after 2 epochs of 18 minibatch steps the ranks'
+parameters are identical and equal the single-process update on the global minibatches within the
+Adam tolerance of tests/test_gpu_train.py."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import has_gpu
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs an MI355X")]
+
+WORLD, E, N, M, T = 2, 96, 8, 16, 24
+BG, EPOCHS, PERIOD, ITERS = 256, 2, 3, 2
+KEYS = ("obs", "actions", "logp", "values", "returns", "dones")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _engine(n_envs, env_base, normalize):
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.rollout import RolloutEngine
+    from uavhip.vec_env import VecUAVEnv
+    torch.manual_seed(0)
+    pol = TransformerActorCritic().cuda()
+    env = VecUAVEnv(n_envs, N, M, 1, 1, seed=17, full_reset_period=PERIOD, env_base=env_base)
+    eng = RolloutEngine(env, pol, T, seed=29, normalize=normalize, total_envs=WORLD * E)
+    return pol, eng
+
+
+def _rank(rank, port, q):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "target-allocation-ppo-transformer_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        torch.cuda.set_device(0)
+        from uavhip.train import FusedPPOTrainer
+        pol, eng = _engine(E, rank * E, normalize=False)
+        eng.start()
+        batches = []
+        for _ in range(ITERS):
+            eng.collect(eager=True)
+            b = eng.gather()
+            batches.append({k: v.cpu().numpy().copy() for k, v in b.items()})
+        tr = FusedPPOTrainer(pol, BG)  # world / rank from torch.distributed
+        assert tr.world == WORLD and tr.minibatch == BG // WORLD
+        tr.set_buffers(b["obs"], b["actions"], b["logp"], b["values"], b["returns"], b["advantages"])
+        st = tr.run(epochs=EPOCHS, generator=torch.Generator().manual_seed(3))
+        torch.cuda.synchronize()
+        q.put((rank, batches, tr.params.cpu().numpy(), st))
+    except BaseException as exc:  # report instead of hanging the parent on q.get
+        q.put((rank, repr(exc), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _union_order(x):
+    """[T, WORLD * E, ...] -> [(rank, step, env), ...] flattened: the gathered batch's order."""
+    x = x[:T].reshape(T, WORLD, E, *x.shape[2:]).transpose(0, 1)
+    return x.reshape(WORLD * T * E, *x.shape[3:])
+
+
+def test_world2_sharded_iteration_matches_one_process():
+    import torch.multiprocessing as mp
+    from uavhip.policy import layout
+    from uavhip.train import FusedPPOTrainer
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(WORLD):
+        r, batches, params, st = q.get(timeout=600)
+        assert not isinstance(batches, str), f"rank {r}: {batches}"
+        res[r] = (batches, params, st)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+
+    # one process over the union of the envs, same seeds
+    pol, eng = _engine(WORLD * E, 0, normalize=True)
+    eng.start()
+    for it in range(ITERS):
+        tr = eng.collect(eager=True)
+        ref = {"obs": tr.obs, "actions": tr.actions, "logp": tr.logp, "values": tr.values, "returns": tr.ret,
+               "dones": tr.dones.float(), "advantages": tr.adv}
+        ref = {k: _union_order(v.cpu().numpy()) for k, v in ref.items()}
+        for r in range(WORLD):
+            got = res[r][0][it]
+            for k in KEYS:
+                assert np.array_equal(got[k].astype(ref[k].dtype), ref[k]), (it, r, k)
+            err = float(np.abs(got["advantages"] - ref["advantages"]).max())
+            print(f"iteration {it} rank {r}: max |adv - union adv| = {err:.3e}")
+            assert err <= 1e-6
+        assert ref["dones"].any()
+    assert int(eng.env.istate[:, 8].max()) >= 3  # a full reset flipped to the spare, refreshed on device
+    single = FusedPPOTrainer(pol, BG)
+    single.set_buffers(*(torch.from_numpy(ref[k]).cuda() for k in ("obs", "actions", "logp", "values", "returns",
+                                                                   "advantages")))
+    s1 = single.run(epochs=EPOCHS, generator=torch.Generator().manual_seed(3), use_graph=False)
+    steps = EPOCHS * (WORLD * T * E // BG)
+    assert s1[3] == res[0][2][3] == res[1][2][3] == steps
+    np.testing.assert_allclose(res[0][2][:3], s1[:3], rtol=1e-4)
+    p0, p1 = res[0][1], res[1][1]
+    assert np.array_equal(p0, p1)  # the replicas stay bit-identical
+    ps = single.params.cpu().numpy()
+    offs, n = layout()
+    ends = offs[1:] + [n]
+    worst = 0.0
+    for (k, v), o, e_ in zip(pol.state_dict().items(), offs, ends):
+        d = np.abs(p0[o:o + v.numel()] - ps[o:o + v.numel()])
+        reach = steps * (2e-4 if k.startswith("actor") else 1e-3)  # lr x steps: Adam's reach
+        if k.endswith("in_proj_bias"):  # the key bias: gradient is rounding noise in both
+            assert d[128:256].max() <= 2 * reach, k
+            d = np.concatenate([d[:128], d[256:]])
+        worst = max(worst, float(d.max()) / reach)
+        assert d.max() <= 0.05 * reach and d.mean() <= 2e-3 * reach, (k, float(d.max()), reach)
+    print(f"data-parallel vs single-process parameters: max |d| = {worst:.3e} x lr x steps")

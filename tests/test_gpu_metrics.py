@@ -39,3 +39,24 @@ def test_episode_stats_match_restatement():
     np.testing.assert_array_equal(st.acc.cpu().numpy(), acc)
     rows = csv_rows(got)
     assert len(rows) == len(got) and len(rows[0]) == 12
+
+
+def test_episode_stats_match_main_train():
+    """uavhip_episode_stats against the reference's own main_train.train() (tests/golden/main_train.npz,
+    30 episodes): the per-step info stream as one env's rollout chunks (split at an arbitrary step, so
+    the open episode carries across the chunk boundary) gives exactly the accumulators train() held."""
+    from conftest import load_golden, main_train_chunk, main_train_records
+    from uavhip.metrics import EpisodeStats
+    mt = load_golden("main_train.npz")
+    rew, done, act, info, val = main_train_chunk(mt)
+    st = EpisodeStats(1)
+    cut = len(rew) // 2 + 7
+    for sl in (slice(0, cut), slice(cut, None)):
+        tr = type("Chunk", (), {})()
+        tr.rewards, tr.dones, tr.actions = (torch.from_numpy(np.ascontiguousarray(x[sl])).cuda() for x in (rew, done, act))
+        tr.info = torch.from_numpy(np.ascontiguousarray(info[sl])).cuda()
+        tr.values = torch.from_numpy(np.ascontiguousarray(val[sl])).cuda()
+        st.update(tr)
+    got = st.drain()
+    np.testing.assert_array_equal(got, main_train_records(mt))
+    assert not st.acc.any()

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import cases, has_gpu, sub
+from conftest import assert_close_report, cases, has_gpu, sub
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs an MI355X")]
 
@@ -37,10 +37,10 @@ def test_row_projection_forward_vs_reference(policy_npz, tag):
     _, logp, value, ent, lg = net.fused_forward(x, actions=a, entropy=ent, logits=lg, rowproj=rowproj_buffer(B),
                                                 step=3, fill=True)
     torch.cuda.synchronize()
-    np.testing.assert_allclose(lg.cpu().numpy(), policy_npz[f"{tag}/logits"], rtol=1e-4, atol=2e-5)
-    np.testing.assert_allclose(logp.cpu().numpy(), policy_npz[f"{tag}/logp"], rtol=1e-4, atol=2e-5)
-    np.testing.assert_allclose(ent.cpu().numpy(), policy_npz[f"{tag}/entropy"], rtol=1e-4, atol=2e-5)
-    np.testing.assert_allclose(value.cpu().numpy(), policy_npz[f"{tag}/value"], rtol=1e-4, atol=1e-4)
+    assert_close_report(f"{tag} logits", lg.cpu().numpy(), policy_npz[f"{tag}/logits"], rtol=1e-4, atol=2e-5)
+    assert_close_report(f"{tag} logp", logp.cpu().numpy(), policy_npz[f"{tag}/logp"], rtol=1e-4, atol=2e-5)
+    assert_close_report(f"{tag} entropy", ent.cpu().numpy(), policy_npz[f"{tag}/entropy"], rtol=1e-4, atol=2e-5)
+    assert_close_report(f"{tag} value", value.cpu().numpy(), policy_npz[f"{tag}/value"], rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("B,step0", [(200, 0), (4096, 7)])
@@ -89,10 +89,10 @@ def test_fused_policy_vs_reference(policy_npz, tag):
     lg = torch.empty(B, 2, device="cuda")
     _, logp, value, ent, lg = net.fused_forward(x, actions=a, entropy=ent, logits=lg)
     torch.cuda.synchronize()
-    np.testing.assert_allclose(lg.cpu().numpy(), policy_npz[f"{tag}/logits"], rtol=1e-4, atol=2e-5)
-    np.testing.assert_allclose(logp.cpu().numpy(), policy_npz[f"{tag}/logp"], rtol=1e-4, atol=2e-5)
-    np.testing.assert_allclose(ent.cpu().numpy(), policy_npz[f"{tag}/entropy"], rtol=1e-4, atol=2e-5)
-    np.testing.assert_allclose(value.cpu().numpy(), policy_npz[f"{tag}/value"], rtol=1e-4, atol=1e-4)
+    assert_close_report(f"{tag} logits", lg.cpu().numpy(), policy_npz[f"{tag}/logits"], rtol=1e-4, atol=2e-5)
+    assert_close_report(f"{tag} logp", logp.cpu().numpy(), policy_npz[f"{tag}/logp"], rtol=1e-4, atol=2e-5)
+    assert_close_report(f"{tag} entropy", ent.cpu().numpy(), policy_npz[f"{tag}/entropy"], rtol=1e-4, atol=2e-5)
+    assert_close_report(f"{tag} value", value.cpu().numpy(), policy_npz[f"{tag}/value"], rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("B", [1, 7, 16, 300, 4096])
@@ -110,9 +110,9 @@ def test_fused_policy_vs_torch_module(policy_npz, B):
         logp_t, v_t, ent_t = net.evaluate(x, a)
     ent = torch.empty(B, device="cuda")
     _, logp, value, ent, _ = net.fused_forward(x, actions=a, entropy=ent)
-    np.testing.assert_allclose(logp.cpu().numpy(), logp_t.cpu().numpy(), rtol=1e-4, atol=2e-5)
-    np.testing.assert_allclose(ent.cpu().numpy(), ent_t.cpu().numpy(), rtol=1e-4, atol=2e-5)
-    np.testing.assert_allclose(value.cpu().numpy(), v_t[:, 0].cpu().numpy(), rtol=1e-4, atol=1e-4)
+    assert_close_report(f"B={B} logp", logp.cpu().numpy(), logp_t.cpu().numpy(), rtol=1e-4, atol=2e-5)
+    assert_close_report(f"B={B} entropy", ent.cpu().numpy(), ent_t.cpu().numpy(), rtol=1e-4, atol=2e-5)
+    assert_close_report(f"B={B} value", value.cpu().numpy(), v_t[:, 0].cpu().numpy(), rtol=1e-4, atol=1e-4)
 
 
 def test_fused_sampling_distribution(policy_npz):

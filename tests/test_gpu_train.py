@@ -47,6 +47,7 @@ def _torch_loss(policy, states, acts, logp, vals, ret, adv, eps=0.2):
 def _grad_scale_check(name, got, ref, rtol):
     scale = float(ref.abs().max())
     err = float((got - ref).abs().max())
+    print(f"{name}: max |d| / max |grad| = {err / max(scale, 1e-30):.3e}")
     assert err <= rtol * scale + 1e-7, f"{name}: max|d| {err:.3e} vs scale {scale:.3e}"
 
 
@@ -97,6 +98,7 @@ def test_fused_steps_match_eager_adam():
             d = torch.cat([d[:128], d[256:]])
         # Adam normalises each element's gradient: elements whose gradient is tiny carry its
         # rounding differences into their step, bounded by a small fraction of lr
+        print(f"{k}: max |d| = {float(d.max()) / step:.3e} x lr x steps, mean {float(d.mean()) / step:.3e}")
         assert float(d.max()) <= 0.05 * step, f"{k}: max {float(d.max()):.3e} vs lr*steps {step:.1e}"
         assert float(d.mean()) <= 2e-3 * step, f"{k}: mean {float(d.mean()):.3e} vs lr*steps {step:.1e}"
 
@@ -175,3 +177,47 @@ def test_device_pack_matches_host_pack():
     packed = torch.full((n,), float("nan"), device="cuda")
     _lib.check(_lib.LIB.uavhip_policy_pack(_lib.ptr(flat), _lib.ptr(packed), _lib.stream_handle()), "pack")
     assert torch.equal(packed, pack_weights(net.state_dict(), device="cuda"))
+
+
+def test_fused_update_replays_reference_update():
+    """The HIP training step against the reference's own PPOAgent.update() (tests/golden/ppo_update.npz,
+    agents/ppo.py:68-181): from the fixture's weights w0 and buffers, GAE on the GPU, then the 15
+    minibatch-64 steps in the recorded sampler order (FusedPPOTrainer, minibatch = BATCH_SIZE) must
+    reproduce the reference's mean losses and final weights w1.
+
+    Bars. The kernels sum in another order than torch CPU (MFMA GEMM tiles, split-K weight
+    gradients, LayerNorm / attention reductions): gradients differ at fp32 rounding (~1e-6
+    relative). Adam normalises every element's step to ~lr, so a weight moves by at most lr per step
+    and an element whose gradient is rounding noise can take a step of either sign: the final weights
+    agree to a small fraction of lr x steps (lr x steps = the most any weight can move), the key bias
+    of in_proj (softmax cancels its gradient exactly: pure noise in both implementations) to
+    2 lr x steps. The printed maxima are the measured errors."""
+    from test_ppo_pin import fixture_policy
+    from conftest import load_golden
+    from uavhip.ppo import gae
+    from uavhip.train import FusedPPOTrainer
+    f = load_golden("ppo_update.npz")
+    net = fixture_policy(f).cuda()
+    ret, adv, _ = gae(torch.from_numpy(f["rewards"]), torch.from_numpy(f["dones"]),
+                      torch.from_numpy(f["values"]).cuda())
+    tr = FusedPPOTrainer(net, 64)
+    tr.set_buffers(torch.from_numpy(f["states"]).cuda(), torch.from_numpy(f["actions"]).cuda(),
+                   torch.from_numpy(f["logprobs"]).cuda(), torch.from_numpy(f["values"]).cuda(), ret, adv)
+    sa, sc, se, n = tr.run(perms=f["perms"], use_graph=True)
+    assert n == 15
+    got = np.array([sa, sc, se])
+    want = np.array([f["loss_actor"], f["loss_critic"], f["entropy"]], dtype=np.float64)
+    rel = np.abs(got - want) / np.maximum(np.abs(want), 1e-3)
+    print("losses (actor, critic, entropy) rel err:", rel)
+    assert rel.max() <= 1e-4
+    worst = {}
+    for k, v in net.state_dict().items():
+        reach = n * (2e-4 if k.startswith("actor") else 1e-3)  # lr x steps
+        d = np.abs(v.detach().cpu().numpy() - f["w1/" + k]).reshape(-1)
+        if k.endswith("in_proj_bias"):
+            assert d[128:256].max() <= 2 * reach, k
+            d = np.concatenate([d[:128], d[256:]])
+        worst[k] = float(d.max()) / reach
+        assert d.max() <= 0.02 * reach and d.mean() <= 1e-3 * reach, (k, float(d.max()), reach)
+    k = max(worst, key=worst.get)
+    print(f"max |w1 - reference w1| = {worst[k]:.3e} x lr x steps ({k})")

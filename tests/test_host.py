@@ -43,7 +43,7 @@ def test_library_exports_every_header_symbol():
     for f in fns:
         assert hasattr(_lib.LIB, f), f
     assert set(fns) == set(_lib.EXPORTS)
-    assert _lib.LIB.uavhip_abi_version() == 1
+    assert _lib.LIB.uavhip_abi_version() == 2
 
 
 def test_ctypes_mirrors_header_enums():
@@ -60,7 +60,9 @@ def test_ctypes_mirrors_header_enums():
     txt = open(HEADER).read()
     body = re.search(r"typedef struct uavhip_env \{(.*?)\} uavhip_env;", txt, re.S).group(1)
     names = re.findall(r"\*\s*(\w+);", body)
-    assert names == [f[0] for f in _lib.EnvDesc._fields_[11:]]
+    assert names == [f[0] for f in _lib.EnvDesc._fields_[12:]]
+    scalars = re.findall(r"u?int\w*_t\s+(\w+);", body.split("double prm")[0])
+    assert scalars[-2:] == ["seed", "env_base"] == [f[0] for f in _lib.EnvDesc._fields_[8:10]]
     assert _header_enum("uavhip_ist")["UAVHIP_IST_COUNT"] == _lib.IST_COUNT
     assert _header_enum("uavhip_dst")["UAVHIP_DST_COUNT"] == _lib.DST_COUNT
 
@@ -200,6 +202,7 @@ def test_csv_rows_follow_main_train_columns():
     rec[0, [E["PDMG_SUM"], E["PFINAL_SUM"], E["ASSIGN_STEPS"]]] = [1.2, 0.6, 3]
     rec[1, [E["STEPS"], E["REWARD"], E["Q0"]]] = [1, 4.0, 1.5]          # no assigns, no action 1
     rows = csv_rows(rec, losses=(0.25, -0.5, 0.69))
+    assert csv_rows(rec, losses=[(0.25, -0.5, 0.69), (1.0, 2.0, 3.0)])[1][9:] == ["1.000000", "2.000000", "3.000000"]
     assert len(CSV_HEADER) == 12
     assert rows[0][:9] == [1, "2.0000", "0.5000", "2.0000", 3, "0.5000", "0.5000", "0.4000", "0.2000"]
     assert rows[1][:9] == [2, "3.0000", "1.0000", "0.0000", 0, "0.0000", "0.0000", "0.0000", "0.0000"]

@@ -167,3 +167,24 @@ def test_policy_oracle_matches_reference(policy_npz, tag):
     np.testing.assert_allclose(logp.numpy(), policy_npz[f"{tag}/logp"], rtol=1e-5, atol=2e-6)
     np.testing.assert_allclose(value.numpy(), policy_npz[f"{tag}/value"], rtol=1e-5, atol=2e-5)
     np.testing.assert_allclose(ent.numpy(), policy_npz[f"{tag}/entropy"], rtol=1e-5, atol=2e-6)
+
+
+def test_metrics_restatement_matches_main_train():
+    """oracle/metrics.py (main_train.py:122-136 restated) pinned to the reference's own run
+    (tests/golden/main_train.npz: train() for 30 episodes): fed the same per-step info stream, it
+    reproduces the accumulators train() held at every episode end exactly (fp64 sums in step
+    order), and uavhip.metrics.csv_rows turns them into train()'s own CSV rows (:161-195)."""
+    import json
+    from conftest import load_golden, main_train_chunk, main_train_records
+    from oracle import metrics as om
+    from uavhip.metrics import csv_rows
+    mt = load_golden("main_train.npz")
+    rew, done, act, info, val = main_train_chunk(mt)
+    rec, acc = om.episode_records(rew, done, act, info, val)
+    ref = main_train_records(mt)
+    assert len(rec) == len(ref) == 30 and not acc.any()
+    np.testing.assert_array_equal(rec, ref)
+    rows = csv_rows(rec, losses=np.repeat(mt["csv_losses"], 10, axis=0))
+    want = json.loads(str(mt["csv_rows"]))
+    got = [[str(x) for x in rows[i]] for i in (9, 19, 29)]
+    assert got == want
