@@ -7,6 +7,13 @@ GPU entry point raises if its HIP call fails.
 import ctypes
 import os
 
+# torch first: its bundled HIP runtime (libamdhip64.so.7 / libhsa-runtime64.so.1) is then the one
+# libuavhip.so binds to (same sonames), so the library and torch share ONE runtime, device and set of
+# streams. Loaded the other way round (the drop-in `configs` module imported before anything else,
+# as main_train.py does), /opt/rocm's runtime would come in first and the two runtimes would
+# contend for the device.
+import torch  # noqa: F401,E402
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # UAVHIP_LIB: an alternative in-tree build (profiling: the TRACE=1 phase-stamp build)
 LIB_PATH = os.environ.get("UAVHIP_LIB") or os.path.join(_HERE, "libuavhip.so")

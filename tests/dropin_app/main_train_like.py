@@ -76,8 +76,7 @@ def train(episodes):
             csv_file.flush()
         torch.save(agent.policy.state_dict(), os.path.join("saved_models", "final_model.pth"))
     csv_file.close()
-    mods = {m: sys.modules[m].__file__ for m in ("configs.config", "envs.uav_env", "agents.ppo",
-                                                 "networks.transformer_net")}
+    mods = {m: sys.modules[m].__file__ for m in ("configs.config", "envs.uav_env", "envs.entities", "agents.ppo")}
     return {"episodes": episodes, "updates": updates, "steps": steps_total, "last_stats": last_stats,
             "rewards": [float(r) for r in ep_rewards], "modules": mods}
 

@@ -82,7 +82,7 @@ def _rank(rank, port, q):
 
 def _union_order(x):
     """[T, WORLD * E, ...] -> [(rank, step, env), ...] flattened: the gathered batch's order."""
-    x = x[:T].reshape(T, WORLD, E, *x.shape[2:]).transpose(0, 1)
+    x = np.swapaxes(x[:T].reshape(T, WORLD, E, *x.shape[2:]), 0, 1)
     return x.reshape(WORLD * T * E, *x.shape[3:])
 
 
@@ -142,5 +142,5 @@ def test_world2_sharded_iteration_matches_one_process():
             assert d[128:256].max() <= 2 * reach, k
             d = np.concatenate([d[:128], d[256:]])
         worst = max(worst, float(d.max()) / reach)
-        assert d.max() <= 0.05 * reach and d.mean() <= 2e-3 * reach, (k, float(d.max()), reach)
+        assert d.max() <= 0.01 * reach and d.mean() <= 1e-5 * reach, (k, float(d.max()), reach)
     print(f"data-parallel vs single-process parameters: max |d| = {worst:.3e} x lr x steps")

@@ -2,7 +2,10 @@
 drop-in UAVEnv / PPOAgent and the batched rollout engine. Marked gpu.
 
 Policy tolerance (fp32 vs fp32 in a different summation order, transformer depth 2): logits /
-logp / entropy 2e-5 absolute + 1e-4 relative, value 1e-4 relative. GAE returns bit-exact."""
+logp / entropy 2e-6 absolute + 1e-5 relative, value 1e-5 absolute + 1e-5 relative -- measured on
+MI355X (the tests print them): at most 7e-7 absolute on logits / logp / entropy and 2.4e-6 on
+values of magnitude ~10, i.e. 1e-5 relative is the north_star bar with a 3-10x margin. GAE returns
+bit-exact."""
 import random
 
 import numpy as np
@@ -37,10 +40,10 @@ def test_row_projection_forward_vs_reference(policy_npz, tag):
     _, logp, value, ent, lg = net.fused_forward(x, actions=a, entropy=ent, logits=lg, rowproj=rowproj_buffer(B),
                                                 step=3, fill=True)
     torch.cuda.synchronize()
-    assert_close_report(f"{tag} logits", lg.cpu().numpy(), policy_npz[f"{tag}/logits"], rtol=1e-4, atol=2e-5)
-    assert_close_report(f"{tag} logp", logp.cpu().numpy(), policy_npz[f"{tag}/logp"], rtol=1e-4, atol=2e-5)
-    assert_close_report(f"{tag} entropy", ent.cpu().numpy(), policy_npz[f"{tag}/entropy"], rtol=1e-4, atol=2e-5)
-    assert_close_report(f"{tag} value", value.cpu().numpy(), policy_npz[f"{tag}/value"], rtol=1e-4, atol=1e-4)
+    assert_close_report(f"{tag} logits", lg.cpu().numpy(), policy_npz[f"{tag}/logits"], rtol=1e-5, atol=2e-6)
+    assert_close_report(f"{tag} logp", logp.cpu().numpy(), policy_npz[f"{tag}/logp"], rtol=1e-5, atol=2e-6)
+    assert_close_report(f"{tag} entropy", ent.cpu().numpy(), policy_npz[f"{tag}/entropy"], rtol=1e-5, atol=2e-6)
+    assert_close_report(f"{tag} value", value.cpu().numpy(), policy_npz[f"{tag}/value"], rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("B,step0", [(200, 0), (4096, 7)])
@@ -89,10 +92,10 @@ def test_fused_policy_vs_reference(policy_npz, tag):
     lg = torch.empty(B, 2, device="cuda")
     _, logp, value, ent, lg = net.fused_forward(x, actions=a, entropy=ent, logits=lg)
     torch.cuda.synchronize()
-    assert_close_report(f"{tag} logits", lg.cpu().numpy(), policy_npz[f"{tag}/logits"], rtol=1e-4, atol=2e-5)
-    assert_close_report(f"{tag} logp", logp.cpu().numpy(), policy_npz[f"{tag}/logp"], rtol=1e-4, atol=2e-5)
-    assert_close_report(f"{tag} entropy", ent.cpu().numpy(), policy_npz[f"{tag}/entropy"], rtol=1e-4, atol=2e-5)
-    assert_close_report(f"{tag} value", value.cpu().numpy(), policy_npz[f"{tag}/value"], rtol=1e-4, atol=1e-4)
+    assert_close_report(f"{tag} logits", lg.cpu().numpy(), policy_npz[f"{tag}/logits"], rtol=1e-5, atol=2e-6)
+    assert_close_report(f"{tag} logp", logp.cpu().numpy(), policy_npz[f"{tag}/logp"], rtol=1e-5, atol=2e-6)
+    assert_close_report(f"{tag} entropy", ent.cpu().numpy(), policy_npz[f"{tag}/entropy"], rtol=1e-5, atol=2e-6)
+    assert_close_report(f"{tag} value", value.cpu().numpy(), policy_npz[f"{tag}/value"], rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("B", [1, 7, 16, 300, 4096])
@@ -110,9 +113,9 @@ def test_fused_policy_vs_torch_module(policy_npz, B):
         logp_t, v_t, ent_t = net.evaluate(x, a)
     ent = torch.empty(B, device="cuda")
     _, logp, value, ent, _ = net.fused_forward(x, actions=a, entropy=ent)
-    assert_close_report(f"B={B} logp", logp.cpu().numpy(), logp_t.cpu().numpy(), rtol=1e-4, atol=2e-5)
-    assert_close_report(f"B={B} entropy", ent.cpu().numpy(), ent_t.cpu().numpy(), rtol=1e-4, atol=2e-5)
-    assert_close_report(f"B={B} value", value.cpu().numpy(), v_t[:, 0].cpu().numpy(), rtol=1e-4, atol=1e-4)
+    assert_close_report(f"B={B} logp", logp.cpu().numpy(), logp_t.cpu().numpy(), rtol=1e-5, atol=2e-6)
+    assert_close_report(f"B={B} entropy", ent.cpu().numpy(), ent_t.cpu().numpy(), rtol=1e-5, atol=2e-6)
+    assert_close_report(f"B={B} value", value.cpu().numpy(), v_t[:, 0].cpu().numpy(), rtol=1e-5, atol=1e-5)
 
 
 def test_fused_sampling_distribution(policy_npz):
@@ -229,7 +232,7 @@ def test_dropin_ppoagent_loop():
         x = torch.zeros(1, 5, 14, device="cuda"); x[0, -1, 0] = 0.5
         a1 = agent.policy_old.fused_forward(x, actions=torch.zeros(1, dtype=torch.long, device="cuda"))[1]
         lp, _, _ = agent.policy.evaluate(x, torch.zeros(1, dtype=torch.long, device="cuda"))
-        torch.testing.assert_close(a1, lp.detach(), rtol=1e-4, atol=2e-5)
+        torch.testing.assert_close(a1, lp.detach(), rtol=1e-5, atol=2e-6)
     finally:
         cfg.NUM_UAVS, cfg.NUM_TARGETS = saved
 
@@ -462,8 +465,8 @@ def test_fused_rollout_step_vs_oracle(traj_npz):
         net.rollout_step(v, obs, rp, t, t == 0, act, lp, val, nxt, rew, dn, seed=9, offset=t * E)
         with torch.no_grad():
             lp_t, v_t, _ = net.evaluate(obs, act.long())
-        torch.testing.assert_close(lp, lp_t, rtol=1e-4, atol=2e-5)
-        torch.testing.assert_close(val, v_t[:, 0], rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(lp, lp_t, rtol=1e-5, atol=2e-6)
+        torch.testing.assert_close(val, v_t[:, 0], rtol=1e-5, atol=1e-5)
         a_h, r_h, d_h, o_h = act.cpu().numpy(), rew.cpu().numpy(), dn.cpu().numpy(), nxt.cpu().numpy()
         for e in range(E):
             o_c, r_c, d_c, _ = refs[e].step(int(a_h[e]))

@@ -3,11 +3,12 @@ on the module's own forward (ppo.py:96-169 restated in uavhip/ppo.py): gradients
 then whole optimizer steps against ppo_epochs with torch.optim.Adam. Marked gpu.
 
 Tolerances: the kernels reorder fp32 sums (MFMA GEMMs, split-K weight gradients, LayerNorm /
-attention reductions), so gradients agree to 2e-4 of each tensor's max |grad|. After Adam steps
-(which normalise every element's gradient, so an element with a tiny gradient turns rounding
-differences into step differences) parameters agree to 5 % of lr x steps at most and 0.2 % on
-average; the key bias of in_proj, whose gradient is pure rounding noise in both implementations
-(softmax cancels it exactly), only to 2 lr x steps. Graph replays equal direct calls bitwise."""
+attention reductions), so gradients agree to 5e-5 of each tensor's max |grad| (measured on MI355X:
+at most 8.4e-6). After Adam steps (which normalise every element's gradient, so an element with a
+tiny gradient turns rounding differences into step differences) parameters agree to 1 % of lr x
+steps at most (measured 2.6e-3) and 1e-5 on average (measured 3e-7); the key bias of in_proj, whose
+gradient is pure rounding noise in both implementations (softmax cancels it exactly), only to
+2 lr x steps. Graph replays equal direct calls bitwise. The tests print the errors they measure."""
 import copy
 
 import numpy as np
@@ -70,7 +71,7 @@ def test_fused_gradients_match_autograd(Bm):
     offs, _ = layout()
     for (k, p), o in zip(ref.named_parameters(), offs):
         got = grads[o:o + p.numel()].view_as(p)
-        _grad_scale_check(k, got, p.grad, 2e-4)
+        _grad_scale_check(k, got, p.grad, 5e-5)
 
 
 def test_fused_steps_match_eager_adam():
@@ -99,8 +100,8 @@ def test_fused_steps_match_eager_adam():
         # Adam normalises each element's gradient: elements whose gradient is tiny carry its
         # rounding differences into their step, bounded by a small fraction of lr
         print(f"{k}: max |d| = {float(d.max()) / step:.3e} x lr x steps, mean {float(d.mean()) / step:.3e}")
-        assert float(d.max()) <= 0.05 * step, f"{k}: max {float(d.max()):.3e} vs lr*steps {step:.1e}"
-        assert float(d.mean()) <= 2e-3 * step, f"{k}: mean {float(d.mean()):.3e} vs lr*steps {step:.1e}"
+        assert float(d.max()) <= 0.01 * step, f"{k}: max {float(d.max()):.3e} vs lr*steps {step:.1e}"
+        assert float(d.mean()) <= 1e-5 * step, f"{k}: mean {float(d.mean()):.3e} vs lr*steps {step:.1e}"
 
 
 def test_fused_graph_replay_matches_direct_steps():
@@ -122,7 +123,7 @@ def test_fused_graph_replay_matches_direct_steps():
     x = bufs[0][:64]
     lp_fused = n2.fused_forward(x, actions=bufs[1][:64])[1]
     lp_torch = n2.evaluate(x, bufs[1][:64])[0]
-    torch.testing.assert_close(lp_fused, lp_torch.detach(), rtol=1e-4, atol=2e-5)
+    torch.testing.assert_close(lp_fused, lp_torch.detach(), rtol=1e-5, atol=2e-6)
 
 
 def test_data_parallel_phases_match_single_gpu_step():
@@ -191,7 +192,9 @@ def test_fused_update_replays_reference_update():
     and an element whose gradient is rounding noise can take a step of either sign: the final weights
     agree to a small fraction of lr x steps (lr x steps = the most any weight can move), the key bias
     of in_proj (softmax cancels its gradient exactly: pure noise in both implementations) to
-    2 lr x steps. The printed maxima are the measured errors."""
+    2 lr x steps. Measured on MI355X: losses within 4.7e-5 relative (the actor loss, a mean of
+    terms that cancel to -0.004; 2e-8 for the critic loss), weights within 2.2e-3 lr x steps at most
+    and ~3e-7 on average; the bars are 1e-4, 1 % and 1e-5."""
     from test_ppo_pin import fixture_policy
     from conftest import load_golden
     from uavhip.ppo import gae
@@ -218,6 +221,6 @@ def test_fused_update_replays_reference_update():
             assert d[128:256].max() <= 2 * reach, k
             d = np.concatenate([d[:128], d[256:]])
         worst[k] = float(d.max()) / reach
-        assert d.max() <= 0.02 * reach and d.mean() <= 1e-3 * reach, (k, float(d.max()), reach)
+        assert d.max() <= 0.01 * reach and d.mean() <= 1e-5 * reach, (k, float(d.max()), reach)
     k = max(worst, key=worst.get)
     print(f"max |w1 - reference w1| = {worst[k]:.3e} x lr x steps ({k})")
