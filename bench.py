@@ -19,8 +19,11 @@ Also reported (same JSON line):
                 BASELINE configs[4]'s per-GPU shard (8192 envs x 64 x 128, fp16 obs, T = 64)
   score_pairs   K1 (LDS-tiled pair scoring) over 8192 fresh 64 x 128 scenes (configs[4])
   ppo_samples_per_s  one PPO update (5 epochs) over the iteration's batch on the HIP training step
-                (uavhip_ppo_step); N > 1: over the all-gathered batch, data parallel (each rank a
-                1/N slice of every global minibatch, RCCL all-reduce of loss sums and gradients)
+                (uavhip_ppo_step) at minibatch 4096 per GPU; N > 1: over the all-gathered batch, data
+                parallel (each rank a 1/N slice of every global minibatch, RCCL all-reduce of loss sums
+                and gradients)
+  ppo_samples_per_s_mb64  the same update at the reference's minibatch 64 (parity mode: the
+                reference's optimizer trajectory) over 16,384 of the iteration's transitions, N = 1
   cpu_baseline  the CPU port (C oracle env.step + torch-CPU fp32 policy + numpy GAE) on host cores,
                 rank 0 at N = 1 only, bounded sample
   cpu_env_baseline  UAVEnv.step alone (C oracle, reference algorithm) on all host cores (one process
@@ -278,6 +281,34 @@ def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
                         "timing": "update wall time (all kernels of the step, launches included)"}}
 
 
+def ppo_mb64_rate(policy, eng, E, T, dev, n_sub=16384):
+    """The reference's own minibatch (BATCH_SIZE = 64, ppo.py:110-115) on the HIP training step: one
+    5-epoch update over the first n_sub transitions of the iteration's batch = 5 n_sub / 64 Adam
+    steps, each epoch one captured hipGraph of n_sub / 64 minibatch steps (capture not timed), on a
+    copy of the policy. Parity mode: the same optimizer trajectory as the reference's update."""
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.train import FusedPPOTrainer
+    tr_ = eng.traj
+    n = E * T
+    bufs = (tr_.obs[:T].reshape(n, 5, 14), tr_.actions.reshape(n), tr_.logp.reshape(n), tr_.values.reshape(n),
+            tr_.ret.reshape(n), tr_.adv.reshape(n))
+    n_sub = min(n_sub, n)
+    pol = TransformerActorCritic().to(dev)
+    pol.load_state_dict(policy.state_dict())
+    trainer = FusedPPOTrainer(pol, 64)
+    trainer.stage(*(b[:n_sub] for b in bufs))
+    trainer.capture()
+    gen = torch.Generator().manual_seed(4321)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _, _, _, cnt = trainer.run(generator=gen)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"value": n_sub / dt, "unit": "PPO samples/s (transitions / update wall time, 5 epochs)",
+            "minibatch": 64, "batch": n_sub, "optimizer_steps": cnt, "ms_per_optimizer_step": dt / cnt * 1e3,
+            "impl": "HIP training step at the reference's minibatch 64, one hipGraph replay per epoch"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -374,7 +405,13 @@ def main():
                      env_fused_rate(8192, 64, 128, 64, dev, obs_dtype=torch.float16)]
         stress = score_pairs_rate(8192, 64, 128, dev)
 
-    ppo = None
+    ppo = ppo64 = None
+    if not args.no_ppo and world == 1 and args.ppo_impl == "fused":
+        try:
+            ppo64 = ppo_mb64_rate(policy, eng, E, T, dev)
+        except Exception as exc:  # the headline rollout line must still print
+            print(f"[bench] minibatch-64 PPO measurement failed: {exc!r}", file=sys.stderr)
+            ppo64 = {"value": None, "error": repr(exc)}
     if not args.no_ppo:
         try:
             ppo = ppo_update_rate(args, eng, policy, world, dist, dev, E, T)
@@ -429,6 +466,7 @@ def main():
             "env_fused": env_fused,
             "score_pairs": stress,
             "ppo_samples_per_s": ppo,
+            "ppo_samples_per_s_mb64": ppo64,
             "cpu_baseline": cpu,
             "cpu_env_baseline": cpu_env,
         }

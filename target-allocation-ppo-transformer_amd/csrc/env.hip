@@ -10,6 +10,7 @@
 //    scene itself (register budget: 4 waves / SIMD); full resets flip to the spare buffer.
 #include "env_device.hpp"
 #include "env_group.hpp"
+#include "env_replay.hpp"
 
 #pragma clang fp contract(off)
 
@@ -142,6 +143,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step_g(uavhip_env env, const int
 }
 
 constexpr int kTableMinSteps = 4;                // below this the LDS table costs more than it saves
+constexpr int kReplayMinSteps = 8;               // K2r: below this a chunk's walk / fold overhead does not pay
+constexpr size_t kReplayMaxLds = 150 * 1024;     // per workgroup (4 envs), below the 160 KiB of a CU
 constexpr int kGroupMinEnvs = 4096;
 constexpr size_t kTableMaxBytes = 64 * 1024;     // per workgroup (4 envs)
 
@@ -298,6 +301,25 @@ extern "C" int uavhip_env_step(const uavhip_env* env, const int8_t* actions, int
     const bool lt = T >= kTableMinSteps && tab <= kTableMaxBytes;
     const dim3 grid(wave_grid(env->E)), block(kBlock);
     hipStream_t st = (hipStream_t)stream;
+    // K2r (env_replay.hpp): with omega == 0 the walk is a function of the actions; replay it
+    if (auto_reset && T >= kReplayMinSteps && env->prm[UAVHIP_PRM_OMEGA] == 0.0 && env->M <= envrep::kMaxM &&
+        !(env->flags & UAVHIP_ENV_NO_REPLAY)) {
+        const size_t l64 = (size_t)envrep::kWavesPerBlock * envrep::wave_doubles<64>(env->N, env->M) * sizeof(double);
+        const size_t l32 = (size_t)envrep::kWavesPerBlock * envrep::wave_doubles<32>(env->N, env->M) * sizeof(double);
+        const dim3 rgrid((env->E + envrep::kWavesPerBlock - 1) / envrep::kWavesPerBlock), rblock(envrep::kBlock);
+        if (l64 <= kReplayMaxLds) {
+            (void)hipFuncSetAttribute((const void*)envrep::k_env_replay<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l64);
+            hipLaunchKernelGGL(envrep::k_env_replay<64>, rgrid, rblock, l64, st, *env, actions, (int)T, obs_out, reward,
+                               done, info);
+            return check_launch("k_env_replay");
+        }
+        if (l32 <= kReplayMaxLds) {
+            (void)hipFuncSetAttribute((const void*)envrep::k_env_replay<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l32);
+            hipLaunchKernelGGL(envrep::k_env_replay<32>, rgrid, rblock, l32, st, *env, actions, (int)T, obs_out, reward,
+                               done, info);
+            return check_launch("k_env_replay");
+        }
+    }
     // two envs per wave pays once there are >= 2 such waves per SIMD (E >= 4096 on 1024 SIMDs);
     // below that the launch is latency-bound and one env per wave keeps more waves in flight
     if (lt && env->N <= envgrp::L && env->M <= envgrp::L && env->E % 2 == 0 && env->E >= kGroupMinEnvs &&

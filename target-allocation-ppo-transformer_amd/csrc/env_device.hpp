@@ -239,41 +239,52 @@ __device__ void load_scene_regs(EnvRegs<TPL>& R, const uavhip_env& env, int lane
     drain_loads();
 }
 
-// mechanics.py:185-241 get_state_vector + uav_env.py:194-237 (_get_obs context) for the current
-// pointer; pushes the row into the window (uav_env.py:241-242).
-template <int TPL>
-__device__ void push_obs(EnvRegs<TPL>& R, int lane) {
-    const int tl = R.t & 63, tk = R.t >> 6;
-    const double val = pick(R.val, tk, tl);
-    const double tc = pick(R.tc, tk, tl);
-    const double nhf = pick(R.nhf, tk, tl);
-    const double nhp = pick(R.nhp, tk, tl);
-    const double ucost = readlane_d(R.ucost, R.u);
-    const double chi_c = div_by(R.asg_cost, R.den_c, R.rcp_c);
-    const double chi_v = div_by(R.cov_val, R.den_v, R.rcp_v);
-    const double chi_mc = div_by(tc, R.den_c, R.rcp_c);
+// mechanics.py:185-241 get_state_vector + uav_env.py:194-237 (_get_obs context): the 14 floats of
+// the observation row of pointer (u, t) -- UAV u's cost, target t's value, its locker-cost sum and
+// not-hit products (tc, nhf, nhp), the allocation's cost / covered-value sums, the pair's p_dmg and
+// p_pen, the scene divisors. The one definition of the row's arithmetic (push_obs, the replay kernel).
+struct ObsRow {
+    float v[14];
+};
+__device__ __forceinline__ ObsRow obs_row(double ucost, double val, double tc, double nhf, double nhp, double asg_cost,
+                                          double cov_val, double pd, double pp, double den_c, double rcp_c,
+                                          double den_v, double rcp_v) {
+    const double chi_c = div_by(asg_cost, den_c, rcp_c);
+    const double chi_v = div_by(cov_val, den_v, rcp_v);
+    const double chi_mc = div_by(tc, den_c, rcp_c);
     const double pjp = 1.0 - nhf;
     const double pjp_pure = 1.0 - nhp;
     const double prev_rev = pjp * val;
-    const double p_km = R.pd_cur * R.pp_cur;
-    const double p_pure = R.pd_cur;
+    const double p_km = pd * pp;
+    const double p_pure = pd;
     const double hat_p = 1.0 - (1.0 - pjp) * (1.0 - p_km);
     const double hat_pp = 1.0 - (1.0 - pjp_pure) * (1.0 - p_pure);
     const double hat_G = hat_p * val;
     const double d_pkm = p_pure - p_km;
     const double d_pm = hat_pp - hat_p;
     const double d_G = (hat_pp * val) - hat_G;
+    return ObsRow{{(float)ucost / 2.0f, (float)val / 16.0f, (float)chi_c, (float)chi_v, (float)chi_mc, (float)p_km,
+                   (float)pjp, (float)hat_p, (float)prev_rev / 16.0f, (float)hat_G / 16.0f, (float)d_pkm, (float)d_pm,
+                   (float)d_G / 16.0f, 1.0f}};
+}
+
+// The current pointer's row (obs_row), pushed into the window (uav_env.py:241-242).
+template <int TPL>
+__device__ void push_obs(EnvRegs<TPL>& R, int lane) {
+    const int tl = R.t & 63, tk = R.t >> 6;
+    const ObsRow o = obs_row(readlane_d(R.ucost, R.u), pick(R.val, tk, tl), pick(R.tc, tk, tl), pick(R.nhf, tk, tl),
+                             pick(R.nhp, tk, tl), R.asg_cost, R.cov_val, R.pd_cur, R.pp_cur, R.den_c, R.rcp_c, R.den_v,
+                             R.rcp_v);
     // the new row goes through the wave's LDS scratch (lane 0 writes, lanes 56..63 and 0..5 read
     // their element): 6 LDS instructions instead of two 14-way VALU select chains. LDS operations
     // of one wave complete in order, so the reads see the write.
     if (lane == 0) {
         typedef float f32x4 __attribute__((ext_vector_type(4)));
         typedef float f32x2 __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<f32x4*>(R.row) = f32x4{(float)ucost / 2.0f, (float)val / 16.0f, (float)chi_c, (float)chi_v};
-        *reinterpret_cast<f32x4*>(R.row + 4) = f32x4{(float)chi_mc, (float)p_km, (float)pjp, (float)hat_p};
-        *reinterpret_cast<f32x4*>(R.row + 8) =
-            f32x4{(float)prev_rev / 16.0f, (float)hat_G / 16.0f, (float)d_pkm, (float)d_pm};
-        *reinterpret_cast<f32x2*>(R.row + 12) = f32x2{(float)d_G / 16.0f, 1.0f};
+        *reinterpret_cast<f32x4*>(R.row) = f32x4{o.v[0], o.v[1], o.v[2], o.v[3]};
+        *reinterpret_cast<f32x4*>(R.row + 4) = f32x4{o.v[4], o.v[5], o.v[6], o.v[7]};
+        *reinterpret_cast<f32x4*>(R.row + 8) = f32x4{o.v[8], o.v[9], o.v[10], o.v[11]};
+        *reinterpret_cast<f32x2*>(R.row + 12) = f32x2{o.v[12], o.v[13]};
     }
     // shift the deque by one row (14 floats) and append
     const float a = __shfl(R.w0, (lane + kDim) & 63);

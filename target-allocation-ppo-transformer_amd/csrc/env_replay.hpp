@@ -1,0 +1,340 @@
+// env_replay.hpp -- K2r: the env-only multi-step launch (uavhip_env_step, T > 1, auto-reset) when
+// COST_WEIGHT_OMEGA == 0, the reference's setting (config.py:53) and that of every BASELINE config.
+//
+// Why it can be replayed: with omega = 0 a tentative assign is always accepted (uav_env.py:317).
+// J(X') >= J(X) because the lock multiplies one not-hit product by (1 - p) in [0, 1] and the
+// list-order sum gains no negative term, and IEEE rounding is monotone; N0 never shrinks; so
+// r(X') = J' N0' / M (or 2 J' at full coverage) >= r(X). The pointer walk, the lock sequence and the
+// episode ends are then a function of the action stream alone, and K2's step-to-step dependency
+// chain splits into a cheap integer walk and fp64 work that is independent across steps.
+//
+// One wave per env, chunks of up to C steps (lane i = step i of the chunk):
+//   walk    wave-uniform integer loop: pointer before / after, assign, done, episode, full-reset
+//           scene flips -- a chunk ends right after a flip, the rest runs on the new scene;
+//   fold    lane = target / UAV, in step order, assigns only: the per-target not-hit products, locker
+//           costs and lock counts and the info running sums -- step_once's operations in its order --
+//           with every target's nh_final | nh_pure | t_cost after each assign written to a row of
+//           three LDS tables (row 0: the chunk's starting state);
+//   replay  lane = step: J(X) after its assign as the list-order sum over its table row (unlocked
+//           targets add +0.0, as in _calc_J_X), r(X), reward, info and the observation row of the
+//           pointer after the step (obs_row); rows -> LDS;
+//   store   lane = window element, one step at a time: each step's window out of the row table (an
+//           episode start zeroes the older slots; rows before the chunk come from the carried window).
+// Every output and the carried state are bitwise those of step_once (tests: test_env_replay_*).
+#pragma once
+#include "env_device.hpp"
+
+#pragma clang fp contract(off)
+
+namespace uavhip {
+namespace envrep {
+using namespace envdev;
+
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWavesPerBlock * kWave;
+constexpr int kRowStride = 16;   // floats per observation row in LDS (14 used)
+constexpr int kMaxM = 32;        // targets: the packed step record holds 7-bit pointers, ncov < 256
+constexpr int kSeq = UAVHIP_SEQ_LEN;
+
+// LDS per wave, in doubles, every region an even count (16-byte aligned float4 rows): p_dmg table
+// [N][M], three (C + 1) x (M + 1) column tables (an odd row stride: conflict-free b64 reads of one
+// column by 32 lanes), C observation rows, the carried window (70 floats).
+__host__ __device__ constexpr size_t even(size_t x) { return (x + 1) & ~(size_t)1; }
+template <int C>
+__host__ __device__ constexpr size_t table_doubles(int M) { return even((size_t)(C + 1) * (M + 1)); }
+template <int C>
+__host__ __device__ constexpr size_t wave_doubles(int N, int M) {
+    return even((size_t)N * M) + 3 * table_doubles<C>(M) + (size_t)C * kRowStride / 2 + 36;
+}
+
+__device__ __forceinline__ double shfl_d(double v, int src) {
+    const int lo = __shfl(__double2loint(v), src), hi = __shfl(__double2hiint(v), src);
+    return __hiloint2double(hi, lo);
+}
+// old with lane i's element replaced by the wave-uniform v (a v_cndmask per dword)
+template <class V>
+__device__ __forceinline__ V put_lane(V v, int i, V old) {
+    return lane_id() == i ? v : old;
+}
+__device__ __forceinline__ int top_bit(unsigned long long m) { return m ? 63 - __builtin_clzll(m) : -1; }
+// LDS written by some lanes and read by others of the same wave: complete and order them
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// packed step record (lane i): pointer before (ub, tb), after the action (ua, ta; ua == N at an
+// episode end), assign, done
+__device__ __forceinline__ int rec_pack(int ub, int tb, int ua, int ta, int a, int d) {
+    return ub | (tb << 7) | (ua << 14) | (ta << 21) | (a << 28) | (d << 29);
+}
+
+template <int C>
+__global__ __launch_bounds__(kBlock) void k_env_replay(uavhip_env env, const int8_t* __restrict__ actions, int T,
+                                                       float* __restrict__ obs_out, double* __restrict__ reward_out,
+                                                       uint8_t* __restrict__ done_out, double* __restrict__ info_out) {
+    static_assert(C <= kWave, "one step per lane");
+    extern __shared__ __attribute__((aligned(16))) double s_dyn[];
+    __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock * 16];
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    const int e = blockIdx.x * kWavesPerBlock + wv;
+    if (e >= env.E) return;
+    const int N = env.N, M = env.M, MS = M + 1;
+    double* base = s_dyn + (size_t)wv * wave_doubles<C>(N, M);
+    double* nhT = base + even((size_t)N * M);
+    double* nhpT = nhT + table_doubles<C>(M);
+    double* tcT = nhpT + table_doubles<C>(M);
+    float* rows = reinterpret_cast<float*>(tcT + table_doubles<C>(M));
+    float* carry = rows + C * kRowStride;
+    EnvRegs<1> R;
+    R.tab = base;
+    R.row = s_row + wv * 16;
+    load_regs<1>(R, env, e, lane);
+    load_table(R, env, lane);
+    const long long E = env.E;
+    const bool h = obs_f16(env);
+    if (R.u >= N) {  // finished before the launch (a previous launch without auto-reset): K2's error path
+        for (int s = 0; s < T; ++s) {
+            const long long se = (long long)s * E + e;
+            step_once<1, true>(R, env, e, lane, 0, 1, obs_out ? obs_at(obs_out, se, h) : nullptr,
+                               reward_out ? reward_out + se : nullptr, done_out ? done_out + se : nullptr,
+                               info_out ? info_out + se * UAVHIP_INFO_COUNT : nullptr);
+        }
+        store_regs(R, env, e, lane);
+        return;
+    }
+    // window element handled by this lane in the store phase: element lane, and 64 + lane (lane < 6)
+    const int j0 = lane / kDim, c0 = lane - j0 * kDim;
+    const int j1 = (kWave + lane) / kDim, c1 = kWave + lane - j1 * kDim;
+    for (int s0 = 0; s0 < T;) {
+        // ------------------------------------------------------------ walk
+        const int na = min(C, T - s0);
+        const int av = lane < na ? actions[(long long)(s0 + lane) * E + e] : 0;
+        const unsigned long long abits = ballot(av == 1);
+        int code = 0, epl = 0;
+        int u = R.u, t = R.t, n = na;
+        unsigned long long dbits = 0;
+        bool flip = false;
+        for (int i = 0; i < na; ++i) {
+            const int a = (int)((abits >> i) & 1ull);
+            const int ub = u, tb = t;
+            if (a) {
+                u += 1;
+                t = 0;
+            } else if (++t >= M) {
+                u += 1;
+                t = 0;
+            }
+            const int d = u >= N ? 1 : 0;
+            code = put_lane(rec_pack(ub, tb, u, t, a, d), i, code);
+            epl = put_lane(R.ep, i, epl);
+            if (d) {  // uav_env.py:355-356; auto-reset (main_train.py:79 full-reset cadence)
+                dbits |= 1ull << i;
+                R.ep += 1;
+                u = 0;
+                t = 0;
+                const int P = env.full_reset_period;
+                if (P > 0 && (R.ep % P) == 0) {
+                    if (env.scene_buffers == 2 && !R.stale) {
+                        flip = true;
+                        n = i + 1;
+                        break;
+                    }
+                    R.err |= 2;  // no fresh spare: state-only reset
+                }
+            }
+        }
+        const unsigned long long nmask = n >= 64 ? ~0ull : (1ull << n) - 1;
+        const unsigned long long amask = abits & nmask;
+        dbits &= nmask;
+        const bool act = lane < n;
+        const int ub = code & 127, tb = (code >> 7) & 127, ua = (code >> 14) & 127, ta = (code >> 21) & 127;
+        const bool la = act && ((code >> 28) & 1), ld = act && ((code >> 29) & 1);
+        // the pair each assign locks: p_dmg (this chunk's scene), p_pen and the UAV's cost
+        const double pd_a = la ? R.tab[ub * M + tb] : 0.0;
+        const double pp_a = shfl_d(R.ppen, ub);
+        const double uc_a = shfl_d(R.ucost, ub);
+        // ------------------------------------------------------------ fold
+        const double c_r = R.r, c_J = R.J, c_spd = R.sum_pd, c_spf = R.sum_pf, c_ac = R.asg_cost, c_cv = R.cov_val;
+        const int c_ncov = R.ncov, c_nasg = R.nasg;
+        if (lane < M) {
+            nhT[lane] = R.nhf[0];
+            nhpT[lane] = R.nhp[0];
+            tcT[lane] = R.tc[0];
+        }
+        carry[lane] = R.w0;
+        if (lane < kObs - kWave) carry[kWave + lane] = R.w1;
+        double ev_spd = 0.0, ev_spf = 0.0, ev_ac = 0.0, ev_cv = 0.0;
+        int ev_cnt = 0;  // lane i: (ncov << 8) | nasg after step i's assign
+        for (int i = 0; i < n; ++i) {
+            const int ci = readlane_i(code, i);
+            if ((ci >> 28) & 1) {  // uav_env.py:306-325, as step_once performs it
+                const int ubi = ci & 127, tbi = (ci >> 7) & 127;
+                const double pd = readlane_d(pd_a, i), pp = readlane_d(pp_a, i), uc = readlane_d(uc_a, i);
+                const double pf = pd * pp;
+                const int nlk_t = readlane_i(R.nlk[0], tbi);
+                if (lane == tbi) {
+                    R.nhf[0] = R.nhf[0] * (1.0 - pf);
+                    R.nhp[0] = R.nhp[0] * (1.0 - pd);
+                    R.tc[0] = R.tc[0] + uc;
+                    R.nlk[0] += 1;
+                }
+                if (lane == ubi) R.asg = tbi;
+                R.sum_pd = R.sum_pd + pd;
+                R.sum_pf = R.sum_pf + pf;
+                R.asg_cost = R.asg_cost + uc;
+                if (nlk_t == 0) {
+                    R.cov_val = R.cov_val + readlane_d(R.val[0], tbi);
+                    R.ncov += 1;
+                }
+                R.nasg += 1;
+                if (lane < M) {
+                    const int o = (1 + i) * MS + lane;
+                    nhT[o] = R.nhf[0];
+                    nhpT[o] = R.nhp[0];
+                    tcT[o] = R.tc[0];
+                }
+                ev_spd = put_lane(R.sum_pd, i, ev_spd);
+                ev_spf = put_lane(R.sum_pf, i, ev_spf);
+                ev_ac = put_lane(R.asg_cost, i, ev_ac);
+                ev_cv = put_lane(R.cov_val, i, ev_cv);
+                ev_cnt = put_lane((R.ncov << 8) | R.nasg, i, ev_cnt);
+            }
+            if ((ci >> 29) & 1) {  // episode end: the state part of reset_regs (uav_env.py:175-182)
+                R.nhf[0] = 1.0;
+                R.nhp[0] = 1.0;
+                R.tc[0] = 0.0;
+                R.nlk[0] = 0;
+                R.asg = -1;
+                R.ncov = 0;
+                R.nasg = 0;
+                R.sum_pd = 0.0;
+                R.sum_pf = 0.0;
+                R.asg_cost = 0.0;
+                R.cov_val = 0.0;
+            }
+        }
+        wave_lds_sync();
+        // ------------------------------------------------------------ replay (lane = step)
+        // J(X), r(X) after this step's assign: the list-order revenue sum over its table row
+        double Jv = 0.0, rv = 0.0;
+        if (la) {
+            const double* col = nhT + (1 + lane) * MS;
+            double rev = 0.0;
+            for (int k = 0; k < M; ++k) rev = rev + (1.0 - col[k]) * readlane_d(R.val[0], k);
+            const int ncov = ev_cnt >> 8;
+            Jv = rev - (env.prm[UAVHIP_PRM_OMEGA] * ev_ac);
+            rv = (ncov == M) ? 2.0 * Jv : Jv * div_by((double)ncov, (double)M, R.rcp_m);
+        }
+        // the state after this step (before an episode-end reset): that of the latest assign of its
+        // episode, else the episode's fresh state (it began inside the chunk), else the chunk's start
+        const unsigned long long le = lane == 63 ? ~0ull : (2ull << lane) - 1, lt = (1ull << lane) - 1;
+        const int dprev = top_bit(dbits & lt);
+        const int alast = top_bit(amask & le), aprev = top_bit(amask & lt);
+        const bool fresh = dprev >= 0, has = alast > dprev, hasp = aprev > dprev;
+        const int src = has ? alast : 0;
+        const double s_r = shfl_d(rv, src), s_J = shfl_d(Jv, src), s_spd = shfl_d(ev_spd, src),
+                     s_spf = shfl_d(ev_spf, src), s_ac = shfl_d(ev_ac, src), s_cv = shfl_d(ev_cv, src);
+        const int s_cnt = __shfl(ev_cnt, src);
+        const double p_r = shfl_d(rv, hasp ? aprev : 0);
+        const double r_after = has ? s_r : (fresh ? 0.0 : c_r);
+        const double J_after = has ? s_J : (fresh ? 0.0 : c_J);
+        const double spd = has ? s_spd : (fresh ? 0.0 : c_spd);
+        const double spf = has ? s_spf : (fresh ? 0.0 : c_spf);
+        const double ac = has ? s_ac : (fresh ? 0.0 : c_ac);
+        const double cv = has ? s_cv : (fresh ? 0.0 : c_cv);
+        const int ncov = has ? (s_cnt >> 8) : (fresh ? 0 : c_ncov);
+        const int nasg = has ? (s_cnt & 255) : (fresh ? 0 : c_nasg);
+        const double r_before = hasp ? p_r : (fresh ? 0.0 : c_r);
+        double reward = la ? r_after - r_before : 0.0;  // :321 R = r(X') - r(X)
+        if (ld) reward = reward + r_after;              // :361-363 goal reward r(X_final)
+        const double is_valid = la ? (reward != 0.0 ? 1.0 : 0.0) : -1.0;
+        const double y = nasg > 0 ? shfl_d(R.rcp_n, nasg - 1) : 0.0;
+        const double avg_d = nasg > 0 ? div_by(spd, (double)nasg, y) : 0.0;
+        const double avg_f = nasg > 0 ? div_by(spf, (double)nasg, y) : 0.0;
+        // the row pushed into the window: the pointer after the step, or at an episode end the new
+        // episode's first row at (0, 0) on a fresh state (a flip's row is rebuilt on the new scene)
+        {
+            const int pu = ld ? 0 : ua, pt = ld ? 0 : ta;
+            const int trow = ld ? -1 : (has ? 1 + alast : (fresh ? -1 : 0));
+            const int o = (trow < 0 ? 0 : trow) * MS + pt;
+            const double nhf = trow < 0 ? 1.0 : nhT[o];
+            const double nhp = trow < 0 ? 1.0 : nhpT[o];
+            const double tc = trow < 0 ? 0.0 : tcT[o];
+            const ObsRow row = obs_row(shfl_d(R.ucost, pu), shfl_d(R.val[0], pt), tc, nhf, nhp, ld ? 0.0 : ac,
+                                       ld ? 0.0 : cv, R.tab[pu * M + pt], shfl_d(R.ppen, pu), R.den_c, R.rcp_c,
+                                       R.den_v, R.rcp_v);
+            if (act) {
+                typedef float f32x4 __attribute__((ext_vector_type(4)));
+                typedef float f32x2 __attribute__((ext_vector_type(2)));
+                float* rw = rows + lane * kRowStride;
+                *reinterpret_cast<f32x4*>(rw) = f32x4{row.v[0], row.v[1], row.v[2], row.v[3]};
+                *reinterpret_cast<f32x4*>(rw + 4) = f32x4{row.v[4], row.v[5], row.v[6], row.v[7]};
+                *reinterpret_cast<f32x4*>(rw + 8) = f32x4{row.v[8], row.v[9], row.v[10], row.v[11]};
+                *reinterpret_cast<f32x2*>(rw + 12) = f32x2{row.v[12], row.v[13]};
+            }
+        }
+        if (act) {
+            const long long se = (long long)(s0 + lane) * E + e;
+            if (reward_out) reward_out[se] = reward;
+            if (done_out) done_out[se] = ld ? 1 : 0;
+            if (info_out) {  // uav_env.py:426-433 (write_info's layout)
+                double2* q = reinterpret_cast<double2*>(info_out + se * UAVHIP_INFO_COUNT);
+                q[0] = make_double2(J_after, (double)ncov);
+                q[1] = make_double2(is_valid, avg_d);
+                q[2] = make_double2(avg_f, (double)ua);
+                q[3] = make_double2((double)ta, (double)epl);
+            }
+        }
+        // ------------------------------------------------------------ carried state
+        {
+            const int d_last = top_bit(dbits), a_last = top_bit(amask);
+            if (a_last > d_last) {
+                R.r = readlane_d(rv, a_last);
+                R.J = readlane_d(Jv, a_last);
+            } else if (d_last >= 0) {
+                R.r = 0.0;
+                R.J = 0.0;
+            }
+        }
+        R.u = u;
+        R.t = t;
+        wave_lds_sync();
+        if (flip) {  // the full reset at step n - 1 flips to the pre-generated spare scene
+            R.sel ^= 1;
+            R.stale = 1;
+            R.sb = (long long)R.sel * env.E + e;
+            load_table(R, env, lane);
+            reset_regs<1, true>(R, env, lane, true);  // new scene values; its first row -> R.row
+            wave_lds_sync();
+            if (lane < kDim) rows[(n - 1) * kRowStride + lane] = R.row[lane];
+            wave_lds_sync();
+        } else {
+            R.pd_cur = R.tab[R.u * M + R.t];
+            R.pp_cur = readlane_d(R.ppen, R.u);
+        }
+        // ------------------------------------------------------------ store
+        for (int s = 0; s < n; ++s) {
+            const int d = top_bit(dbits & (s == 63 ? ~0ull : (2ull << s) - 1));  // latest episode start <= s
+            auto elem = [&](int j, int c) -> float {
+                const int k = s - (kSeq - 1) + j;  // chunk step whose row sits in window slot j
+                if (d >= 0) return k >= d ? rows[k * kRowStride + c] : 0.0f;
+                return k >= 0 ? rows[k * kRowStride + c] : carry[(kSeq + k) * kDim + c];
+            };
+            const float v0 = elem(j0, c0);
+            const float v1 = lane < kObs - kWave ? elem(j1, c1) : 0.0f;
+            if (obs_out) write_obs(obs_at(obs_out, (long long)(s0 + s) * E + e, h), v0, v1, lane, h);
+            if (s == n - 1) {
+                R.w0 = v0;
+                R.w1 = v1;
+            }
+        }
+        wave_lds_sync();
+        s0 += n;
+    }
+    store_regs(R, env, e, lane);
+}
+
+}  // namespace envrep
+}  // namespace uavhip

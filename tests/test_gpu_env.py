@@ -345,7 +345,7 @@ def test_two_envs_per_wave_matches_one_per_wave(N, M, period):
     full resets that flip to refreshed spare scenes."""
     E, T = 4096, 40  # the grouped kernel's minimum batch
     outs = []
-    for flags in (0, 1):
+    for flags in (4, 5):  # UAVHIP_ENV_NO_REPLAY (| ONE_PER_WAVE): the step-by-step kernels
         v = _venv(E, N, M, 1, 1, period=period, seed=21)
         v.desc.flags = flags
         v.istate[:, 4] = 1
@@ -454,3 +454,95 @@ def test_fp16_obs_two_envs_per_wave():
     assert res[1][0].dtype == torch.float16 and torch.equal(res[1][0], res[0][0].half())
     for x, y in zip(res[0][1:], res[1][1:]):
         assert torch.equal(x, y)
+
+
+def _replay_twins(E, N, M, period, T, launches, obs_dtype, p_assign, seed, start_done=False):
+    """Outputs of `launches` multi-step launches + the whole carried state, for K2r (flags 0) and the
+    one-env-per-wave step kernel K2 (UAVHIP_ENV_NO_REPLAY | ONE_PER_WAVE) on twin envs."""
+    from uavhip.vec_env import VecUAVEnv
+    outs = []
+    for flags in (0, 5):
+        v = VecUAVEnv(E, N, M, 1, 1, full_reset_period=period, seed=seed, obs_dtype=obs_dtype)
+        v.desc.flags |= flags
+        v.istate[:, 4] = 1
+        v.generate_scenes()
+        v.reset(episode=1)
+        g = torch.Generator(device="cuda").manual_seed(seed)
+        res = []
+        if start_done:  # half the envs finished by a launch without auto-reset: K2's error path
+            one = torch.ones(E, dtype=torch.int8, device="cuda")
+            for _ in range(N):
+                v.step(one[None].expand(1, E).contiguous(), auto_reset=False)
+            v.reset(mask=(torch.arange(E, device="cuda") % 2 == 0).to(torch.uint8))
+        for _ in range(launches):
+            a = (torch.rand(T, E, device="cuda", generator=g) < p_assign).to(torch.int8)
+            obs, r, d, info = v.step(a)
+            v.refresh_scenes()
+            res += [obs.clone(), r.clone(), d.clone(), info.clone()]
+        res += [v.istate.clone(), v.dstate.clone(), v.window.clone(), v.nh_final.clone(), v.nh_pure.clone(),
+                v.t_cost.clone(), v.n_lock.clone(), v.assigned.clone(), v.p_dmg.clone()]
+        outs.append(res)
+    torch.cuda.synchronize()
+    return outs
+
+
+@pytest.mark.parametrize("E,N,M,period,T,p", [(1024, 8, 16, 3, 200, 0.5), (4096, 16, 32, 2, 100, 0.5),
+                                              (300, 4, 4, 5, 131, 0.3), (96, 30, 10, 2, 70, 0.6),
+                                              (64, 64, 32, 0, 90, 0.5), (256, 8, 16, 1, 64, 0.9),
+                                              (128, 16, 32, 3, 257, 0.05)])
+def test_env_replay_matches_sequential_step(E, N, M, period, T, p):
+    """K2r (the omega = 0 replay, env_replay.hpp) against K2 (checked against the reference above):
+    every output -- windows, rewards, done, info -- and the whole carried state bitwise over three
+    launches with auto-reset; full resets flipping to refreshed spares (period 1: a second full reset
+    in one launch is refused, error bit 2); chunk boundaries (T not a multiple of the 64- or 32-step
+    chunk); skip-heavy and assign-heavy action streams; N up to 64, M up to 32."""
+    a, b = _replay_twins(E, N, M, period, T, 3, torch.float32, p, seed=E + N + M)
+    assert a[2].any()  # episodes ended inside the launches
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.equal(x, y), i
+
+
+def test_env_replay_fp16_and_finished_envs():
+    """K2r with binary16 observations (BASELINE config 4), and envs that were already finished
+    before the launch (auto-reset off earlier): those take K2's error path inside K2r."""
+    a, b = _replay_twins(512, 8, 16, 4, 96, 2, torch.float16, 0.5, seed=3, start_done=True)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.equal(x, y), i
+    assert int((a[-9][:, 5] & 1).sum()) == 256  # the finished envs flagged the stepping error
+
+
+def test_env_replay_matches_oracle(traj_npz):
+    """K2r directly against the CPU oracle: the golden scenes of one shape, several copies each, a
+    random action stream in one 150-step launch with state-only auto-reset, every step replayed
+    through oracle.OracleEnv -- done bit-exact, rewards to 1e-12, info to 1e-12, windows to the fp32 bar."""
+    import oracle
+    from uavhip.vec_env import VecUAVEnv
+    groups = {}
+    for c in cases(traj_npz):
+        s = sub(traj_npz, c["key"])
+        if s["params"][6] == 0.0 and len(s["nfz_pos"]) == 1:
+            groups.setdefault((c["N"], c["M"]), []).append(s)
+    (N, M), scenes = max(((k, g) for k, g in groups.items() if k[1] <= 32), key=lambda kv: kv[0][0] * kv[0][1])
+    scenes = (scenes * 8)[:32]
+    E, T = len(scenes), 150
+    v = VecUAVEnv(E, N, M, 1, 1, full_reset_period=0)
+    v.set_params(scenes[0]["params"])
+    v.load_scenes(scenes)
+    v.reset(episode=1)
+    rng = np.random.default_rng(5)
+    acts = (rng.random((T, E)) < 0.5).astype(np.int8)
+    obs, rew, done, info = (x.cpu().numpy() for x in v.step(torch.from_numpy(acts).cuda()))
+    refs = [oracle.OracleEnv(s, s["params"]) for s in scenes]
+    for r in refs:
+        r.reset()
+    for t in range(T):
+        for e in range(E):
+            o_c, r_c, d_c, inf_c = refs[e].step(int(acts[t, e]))
+            assert bool(done[t, e]) == d_c, (t, e)
+            assert abs(rew[t, e] - r_c) <= 1e-12 * max(1.0, abs(r_c)), (t, e)
+            np.testing.assert_allclose(info[t, e, :5], inf_c[:5], rtol=1e-12, atol=1e-15)
+            np.testing.assert_array_equal(info[t, e, 5:7], inf_c[5:7])
+            if d_c:
+                o_c = refs[e].reset()
+            np.testing.assert_allclose(obs[t, e], o_c, rtol=2e-6, atol=1e-6)
+    assert done.any()
