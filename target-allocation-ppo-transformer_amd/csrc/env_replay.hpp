@@ -250,7 +250,9 @@ __global__ __launch_bounds__(kBlock) void k_env_replay(uavhip_env env, const int
         double reward = la ? r_after - r_before : 0.0;  // :321 R = r(X') - r(X)
         if (ld) reward = reward + r_after;              // :361-363 goal reward r(X_final)
         const double is_valid = la ? (reward != 0.0 ? 1.0 : 0.0) : -1.0;
-        const double y = nasg > 0 ? shfl_d(R.rcp_n, nasg - 1) : 0.0;
+        // (every cross-lane read with the whole wave active: ds_bpermute from an inactive lane reads 0)
+        const double rn = shfl_d(R.rcp_n, nasg > 0 ? nasg - 1 : 0);
+        const double y = nasg > 0 ? rn : 0.0;
         const double avg_d = nasg > 0 ? div_by(spd, (double)nasg, y) : 0.0;
         const double avg_f = nasg > 0 ? div_by(spf, (double)nasg, y) : 0.0;
         // the row pushed into the window: the pointer after the step, or at an episode end the new
