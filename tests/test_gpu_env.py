@@ -457,11 +457,12 @@ def test_fp16_obs_two_envs_per_wave():
 
 
 def _replay_twins(E, N, M, period, T, launches, obs_dtype, p_assign, seed, start_done=False):
-    """Outputs of `launches` multi-step launches + the whole carried state, for K2r (flags 0) and the
-    one-env-per-wave step kernel K2 (UAVHIP_ENV_NO_REPLAY | ONE_PER_WAVE) on twin envs."""
+    """Outputs of `launches` multi-step launches + the whole carried state, for K2r (ONE_PER_WAVE: the
+    grouped K2g is not a candidate) and the one-env-per-wave step kernel K2 (NO_REPLAY | ONE_PER_WAVE)
+    on twin envs."""
     from uavhip.vec_env import VecUAVEnv
     outs = []
-    for flags in (0, 5):
+    for flags in (1, 5):
         v = VecUAVEnv(E, N, M, 1, 1, full_reset_period=period, seed=seed, obs_dtype=obs_dtype)
         v.desc.flags |= flags
         v.istate[:, 4] = 1
