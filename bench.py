@@ -69,6 +69,23 @@ def profiled_traffic(kernel):
     return None, None
 
 
+def env_counters(kernel):
+    """The VALU side and the PMC traffic of an env kernel (K1 / K2 / K2g / K2r) from the newest
+    profiles/rNN_env_counters.json (scripts/profile_env_counters.sh + summarize_env_counters.py, the
+    same shapes as the bench's env legs): fp64 FLOP fraction of the 78.6 TFLOP/s fp64 vector peak,
+    VALU busy share of SIMD cycles, HBM bytes per launch (FETCH x 2 + WRITE)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_env_counters.json")))
+    if not files:
+        return None
+    k = json.load(open(files[-1]))["kernels"].get(kernel)
+    if k is None:
+        return None
+    keep = ("avg_ns", "fp64_frac", "fp64_tflops", "valu_busy", "hbm_bytes_per_launch", "valu_insts", "salu_insts")
+    return dict({a: k[a] for a in keep}, kernel=kernel, source=os.path.basename(files[-1]),
+                hbm_frac=k["hbm_bytes_per_launch"] / (k["avg_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS)
+
+
 def env_bytes_per_step(M):
     return 24 * M + 490
 
@@ -403,7 +420,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_env_fused:
         env_fused = [env_fused_rate(1024, 8, 16, 256, dev), env_fused_rate(E, args.uavs, args.targets, 256, dev),
                      env_fused_rate(8192, 64, 128, 64, dev, obs_dtype=torch.float16)]
+        # the kernel uavhip_env_step dispatches for each leg (env.hip): K2r below the grouped kernel's
+        # batch (omega = 0), K2g two envs per wave, K2 one env per wave (M > 32)
+        for leg, kern in zip(env_fused, ("uavhip::envrep::k_env_replay<64>", "uavhip::k_env_step_g",
+                                         "uavhip::k_env_step<2, false>")):
+            leg["kernel"] = kern
+            leg["counters"] = env_counters(kern)
         stress = score_pairs_rate(8192, 64, 128, dev)
+        stress["counters"] = env_counters("uavhip::k_score_pairs")
 
     ppo = ppo64 = None
     if not args.no_ppo and world == 1 and args.ppo_impl == "fused":
