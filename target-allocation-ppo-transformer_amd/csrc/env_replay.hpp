@@ -9,17 +9,18 @@
 // chain splits into a cheap integer walk and fp64 work that is independent across steps.
 //
 // One wave per env, chunks of up to C steps (lane i = step i of the chunk):
-//   walk    wave-uniform integer loop: pointer before / after, assign, done, episode, full-reset
-//           scene flips -- a chunk ends right after a flip, the rest runs on the new scene;
-//   fold    lane = target / UAV, in step order, assigns only: the per-target not-hit products, locker
+//   walk    lane = step, from the chunk's action bits alone (ballots and popcounts): pointer before /
+//           after, assign, done, episode, full-reset scene flips -- a chunk ends right after a flip,
+//           the rest runs on the new scene;
+//   fold    lane = target / UAV, over the assigns in step order: the per-target not-hit products, locker
 //           costs and lock counts and the info running sums -- step_once's operations in its order --
 //           with every target's nh_final | nh_pure | t_cost after each assign written to a row of
 //           three LDS tables (row 0: the chunk's starting state);
 //   replay  lane = step: J(X) after its assign as the list-order sum over its table row (unlocked
 //           targets add +0.0, as in _calc_J_X), r(X), reward, info and the observation row of the
 //           pointer after the step (obs_row); rows -> LDS;
-//   store   lane = window element, one step at a time: each step's window out of the row table (an
-//           episode start zeroes the older slots; rows before the chunk come from the carried window).
+//   store   16 lanes per step, 4 steps at a time: each step's window out of the row table (an episode
+//           start zeroes the older slots; rows before the chunk come from the carried window).
 // Every output and the carried state are bitwise those of step_once (tests: test_env_replay_*).
 #pragma once
 #include "env_device.hpp"
@@ -126,45 +127,48 @@ __global__ __launch_bounds__(kBlock) void k_env_replay(uavhip_env env, const int
         const int na = min(C, T - s0);
         const unsigned long long abits = ballot(av == 1 && lane < na);
         const int av_next = s0 + na + lane < T ? actions[(long long)(s0 + na + lane) * E + e] : 0;
-        int code = 0, epl = 0;
-        int u = R.u, t = R.t, n = na;
-        unsigned long long dbits = 0;
+        // Every lane works out its own step from the chunk's action bits (uav_env.py:306-356): the
+        // pointer ADVANCES to the next UAV (t -> 0) on an assign, or on a skip of the last target.
+        // Between two assigns the target index just counts skips modulo M, so step i's target is
+        // (t at the run start + steps since) mod M, the run starting after the previous assign (at
+        // the carried t for the chunk's first run). An episode is N advances: the UAV index is the
+        // advance count modulo N, and it ends (u reaches N) on every N-th advance.
+        const unsigned long long le = lane == 63 ? ~0ull : (2ull << lane) - 1, lt = (1ull << lane) - 1;
+        const bool lin = lane < na;
+        const int a_i = (int)((abits >> lane) & 1ull);
+        const int p_as = top_bit(abits & lt);                     // previous assign in the chunk
+        const int tb = (((p_as >= 0 ? 0 : R.t) + lane - (p_as + 1)) % M);
+        const bool adv = lin && (a_i || tb + 1 == M);
+        const unsigned long long advbits = ballot(adv);
+        const int ub = (R.u + __popcll(advbits & lt)) % N;
+        const int ua = ub + (adv ? 1 : 0), ta = adv ? 0 : tb + 1;
+        const bool dn = adv && ua == N;                           // uav_env.py:355-356
+        unsigned long long dbits = ballot(dn);
+        const int epl = R.ep + __popcll(dbits & lt);              // the episode step i belongs to
+        // main_train.py:79 full-reset cadence at the episode ends: the first one (spare fresh) flips
+        // to the spare scene and ends the chunk; with the spare already used, a state-only reset
+        const int P = env.full_reset_period;
+        const unsigned long long frbits = ballot(dn && P > 0 && (epl + 1) % P == 0);
+        int n = na;
         bool flip = false;
-        for (int i = 0; i < na; ++i) {
-            const int a = (int)((abits >> i) & 1ull);
-            const int ub = u, tb = t;
-            if (a) {
-                u += 1;
-                t = 0;
-            } else if (++t >= M) {
-                u += 1;
-                t = 0;
-            }
-            const int d = u >= N ? 1 : 0;
-            code = put_lane(rec_pack(ub, tb, u, t, a, d), i, code);
-            epl = put_lane(R.ep, i, epl);
-            if (d) {  // uav_env.py:355-356; auto-reset (main_train.py:79 full-reset cadence)
-                dbits |= 1ull << i;
-                R.ep += 1;
-                u = 0;
-                t = 0;
-                const int P = env.full_reset_period;
-                if (P > 0 && (R.ep % P) == 0) {
-                    if (env.scene_buffers == 2 && !R.stale) {
-                        flip = true;
-                        n = i + 1;
-                        break;
-                    }
-                    R.err |= 2;  // no fresh spare: state-only reset
-                }
+        if (frbits) {
+            if (env.scene_buffers == 2 && !R.stale) {
+                flip = true;
+                n = __builtin_ctzll(frbits) + 1;
+            } else {
+                R.err |= 2;  // no fresh spare: state-only reset
             }
         }
         const unsigned long long nmask = n >= 64 ? ~0ull : (1ull << n) - 1;
+        const int code = rec_pack(ub, tb, ua, ta, a_i, dn ? 1 : 0);
+        // the walk's end state
+        const int u = (R.u + __popcll(advbits & nmask)) % N;
+        const int t = readlane_i(ta, n - 1);
+        R.ep += __popcll(dbits & nmask);
         const unsigned long long amask = abits & nmask;
         dbits &= nmask;
         const bool act = lane < n;
-        const int ub = code & 127, tb = (code >> 7) & 127, ua = (code >> 14) & 127, ta = (code >> 21) & 127;
-        const bool la = act && ((code >> 28) & 1), ld = act && ((code >> 29) & 1);
+        const bool la = act && a_i, ld = act && dn;
         // the pair each assign locks: p_dmg (this chunk's scene), p_pen and the UAV's cost
         const double pd_a = la ? R.tab[ub * M + tb] : 0.0;
         const double pp_a = shfl_d(R.ppen, ub);
@@ -181,7 +185,8 @@ __global__ __launch_bounds__(kBlock) void k_env_replay(uavhip_env env, const int
         if (lane < kObs - kWave) carry[kWave + lane] = R.w1;
         double ev_spd = 0.0, ev_spf = 0.0, ev_ac = 0.0, ev_cv = 0.0;
         int ev_cnt = 0;  // lane i: (ncov << 8) | nasg after step i's assign
-        for (int i = 0; i < n; ++i) {
+        for (unsigned long long ev = (amask | dbits) & nmask; ev; ev &= ev - 1) {  // assigns and episode ends
+            const int i = __builtin_ctzll(ev);
             const int ci = readlane_i(code, i);
             if ((ci >> 28) & 1) {  // uav_env.py:306-325, as step_once performs it
                 const int ubi = ci & 127, tbi = (ci >> 7) & 127;
@@ -243,7 +248,6 @@ __global__ __launch_bounds__(kBlock) void k_env_replay(uavhip_env env, const int
         }
         // the state after this step (before an episode-end reset): that of the latest assign of its
         // episode, else the episode's fresh state (it began inside the chunk), else the chunk's start
-        const unsigned long long le = lane == 63 ? ~0ull : (2ull << lane) - 1, lt = (1ull << lane) - 1;
         const int dprev = top_bit(dbits & lt);
         const int alast = top_bit(amask & le), aprev = top_bit(amask & lt);
         const bool fresh = dprev >= 0, has = alast > dprev, hasp = aprev > dprev;
@@ -330,25 +334,30 @@ __global__ __launch_bounds__(kBlock) void k_env_replay(uavhip_env env, const int
         // window slot j of step s holds the row of chunk step k = s - 4 + j: zero before the latest
         // episode start d <= s (the reset row of step d opens the episode), from the carried
         // window for k < 0 when the episode began before the chunk
-        // lane s writes its own 70 floats, 8 bytes at a time: 35 store instructions per chunk (one
-        // step at a time, 280 contiguous bytes per instruction, measured 7-12 % slower: 10 times the
-        // instructions at one wave per SIMD)
-        if (obs_out && act) {
-            const int d = top_bit(dbits & le);
-            float* o = obs_at(obs_out, (long long)(s0 + lane) * E + e, h);
+        // four steps per store instruction, 16 lanes per step writing float pairs 16 k + j of its
+        // window: 3 instructions cover 4 steps, each touching 4 runs of 128 contiguous bytes (one lane
+        // per step, 8 bytes each, touched 64 lines per instruction: 1.5x slower at configs[1])
+        if (obs_out) {
+            const int g4 = lane >> 4, j16 = lane & 15;
+            for (int s4 = 0; s4 < n; s4 += 4) {
+                const int s = s4 + g4;
+                const int d = top_bit(dbits & (s >= 63 ? ~0ull : (2ull << s) - 1));
+                float* o = obs_at(obs_out, (long long)(s0 + s) * E + e, h);
 #pragma unroll
-            for (int j = 0; j < kSeq; ++j) {
-                const int k = lane - (kSeq - 1) + j;
-                const bool zero = d >= 0 && k < d;
-                const float* src = k >= 0 ? rows + (k >= 0 ? k : 0) * kRowStride : carry + (kSeq + k) * kDim;
-#pragma unroll
-                for (int q = 0; q < kDim / 2; ++q) {
-                    const float2 v = zero ? make_float2(0.0f, 0.0f) : reinterpret_cast<const float2*>(src)[q];
-                    if (h) {  // binary16, round to nearest even (write_obs's conversion)
-                        typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-                        reinterpret_cast<f16x2*>(o)[j * (kDim / 2) + q] = f16x2{(_Float16)v.x, (_Float16)v.y};
-                    } else {
-                        reinterpret_cast<float2*>(o)[j * (kDim / 2) + q] = v;
+                for (int k = 0; k < 3; ++k) {
+                    const int p = 16 * k + j16;  // float pair of the 70-float window
+                    if (s < n && p < kObs / 2) {
+                        const int jj = p / (kDim / 2), qq = p - jj * (kDim / 2);
+                        const int kk = s - (kSeq - 1) + jj;  // chunk step whose row fills slot jj
+                        const float* src = kk >= 0 ? rows + kk * kRowStride : carry + (kSeq + kk) * kDim;
+                        float2 v = reinterpret_cast<const float2*>(src)[qq];
+                        if (d >= 0 && kk < d) v = make_float2(0.0f, 0.0f);
+                        if (h) {  // binary16, round to nearest even (write_obs's conversion)
+                            typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+                            reinterpret_cast<f16x2*>(o)[p] = f16x2{(_Float16)v.x, (_Float16)v.y};
+                        } else {
+                            reinterpret_cast<float2*>(o)[p] = v;
+                        }
                     }
                 }
             }
