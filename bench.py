@@ -14,7 +14,7 @@ Also reported (same JSON line):
                 window-row ring reuses layer-0 Q/K/V of rows 0-3 from earlier steps, so it EXECUTES
                 1,790,848 FLOP/sample; that rate is reported beside it (executed_*)
   env_roofline  k_env_step against HBM, algorithmic 24*M + 490 B per env-step
-  env_fused     env-only K2 with T = 256 steps per launch (state in registers): BASELINE configs[1]
+  env_fused     env-only multi-step launches, T = 256 (K2r omega = 0 replay / K2): BASELINE configs[1]
                 (1024 envs x 8 x 16) and the headline shape, env-steps/s and algorithmic GB/s; and
                 BASELINE configs[4]'s per-GPU shard (8192 envs x 64 x 128, fp16 obs, T = 64)
   score_pairs   K1 (LDS-tiled pair scoring) over 8192 fresh 64 x 128 scenes (configs[4])
@@ -170,8 +170,8 @@ def cpu_env_baseline(args, seconds=10.0):
 
 
 def env_fused_rate(E, N, M, T, dev, reps=5, obs_dtype=torch.float32):
-    """Env-only K2 (BASELINE configs[1] shape): one launch steps E envs T times with state in
-    registers (Bernoulli(0.5) actions drawn on device beforehand, auto-reset, obs / reward / done /
+    """Env-only multi-step launch (BASELINE configs[1] shape; K2r / K2, see env.hip's dispatch): one
+    launch steps E envs T times with state in registers (Bernoulli(0.5) actions drawn on device beforehand, auto-reset, obs / reward / done /
     info written every step). Returns env-steps/s and algorithmic GB/s (SURVEY 8d units; fp16 obs
     write 140 B instead of 280 B per env-step)."""
     from uavhip.vec_env import VecUAVEnv
@@ -420,9 +420,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_env_fused:
         env_fused = [env_fused_rate(1024, 8, 16, 256, dev), env_fused_rate(E, args.uavs, args.targets, 256, dev),
                      env_fused_rate(8192, 64, 128, 64, dev, obs_dtype=torch.float16)]
-        # the kernel uavhip_env_step dispatches for each leg (env.hip): K2r below the grouped kernel's
-        # batch (omega = 0), K2g two envs per wave, K2 one env per wave (M > 32)
-        for leg, kern in zip(env_fused, ("uavhip::envrep::k_env_replay<64>", "uavhip::k_env_step_g",
+        # the kernel uavhip_env_step dispatches for each leg (env.hip): K2r wherever omega = 0 and
+        # M <= 32 (64-step chunks when the LDS tables fit, else 32), K2 one env per wave (M > 32)
+        for leg, kern in zip(env_fused, ("uavhip::envrep::k_env_replay<64>", "uavhip::envrep::k_env_replay<32>",
                                          "uavhip::k_env_step<2, false>")):
             leg["kernel"] = kern
             leg["counters"] = env_counters(kern)

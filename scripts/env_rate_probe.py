@@ -40,8 +40,8 @@ def rate(E, N, M, T, flags, outs=("obs", "rew", "done", "info"), reps=5):
 
 
 QUICK = os.environ.get("PROBE_QUICK") == "1"  # one launch shape, full outputs (counter passes)
-for (E, N, M, T) in [(1024, 8, 16, 256)] + ([] if QUICK else [(4096, 16, 32, 256)]):
-    for name, flags in (("K2r", 0), ("K2g", 4), ("K2", 5)):
+for (E, N, M, T) in [(1024, 8, 16, 256)] + ([] if QUICK else [(4096, 8, 16, 256), (4096, 16, 32, 256)]):
+    for name, flags in (("K2r", 1), ("K2g", 4), ("K2", 5)):  # ONE_PER_WAVE keeps K2g out of the K2r leg
         for outs in (("obs", "rew", "done", "info"),) + (() if QUICK else (("rew", "done", "info"), ("rew", "done"), ())):
             r, ms = rate(E, N, M, T, flags, outs)
             print(f"{E}x{N}x{M} T={T} {name:4s} outs={','.join(outs) or '-':18s} {r / 1e9:6.3f} G env-steps/s  {ms:.4f} ms", flush=True)

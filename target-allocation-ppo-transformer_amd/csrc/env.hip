@@ -301,18 +301,9 @@ extern "C" int uavhip_env_step(const uavhip_env* env, const int8_t* actions, int
     const bool lt = T >= kTableMinSteps && tab <= kTableMaxBytes;
     const dim3 grid(wave_grid(env->E)), block(kBlock);
     hipStream_t st = (hipStream_t)stream;
-    // two envs per wave pays once there are >= 2 such waves per SIMD (E >= 4096 on 1024 SIMDs);
-    // below that the launch is latency-bound and one env per wave keeps more waves in flight
-    if (lt && env->N <= envgrp::L && env->M <= envgrp::L && env->E % 2 == 0 && env->E >= kGroupMinEnvs &&
-        !(env->flags & UAVHIP_ENV_ONE_PER_WAVE)) {
-        const int per_block = kWavesPerBlock * 2;
-        hipLaunchKernelGGL(k_env_step_g, dim3((env->E + per_block - 1) / per_block), block, 2 * tab, st, *env, actions,
-                           (int)T, (int)auto_reset, obs_out, reward, done, info);
-        return check_launch("k_env_step_g");
-    }
-    // K2r (env_replay.hpp): with omega == 0 the walk is a function of the actions; replay it. Below
-    // the grouped kernel's batch it is the fastest (1024 x 8 x 16, T = 256: 2.1 vs 1.1 G env-steps/s on
-    // MI355X); at 4096 x 16 x 32 K2g's two envs per wave win (2.7 vs 2.1), so it is tried after K2g.
+    // K2r (env_replay.hpp): with omega == 0 the walk is a function of the actions; replay it. Fastest
+    // wherever it applies (T = 256, all outputs, G env-steps/s on MI355X: 1024 x 8 x 16 3.07 vs K2g
+    // 1.09; 4096 x 8 x 16 3.60 vs 2.87; 4096 x 16 x 32 2.83 vs 2.77), so it is tried first.
     if (auto_reset && T >= kReplayMinSteps && env->prm[UAVHIP_PRM_OMEGA] == 0.0 && env->M <= envrep::kMaxM &&
         !(env->flags & UAVHIP_ENV_NO_REPLAY)) {
         const size_t l64 = (size_t)envrep::kWavesPerBlock * envrep::wave_doubles<64>(env->N, env->M) * sizeof(double);
@@ -330,6 +321,15 @@ extern "C" int uavhip_env_step(const uavhip_env* env, const int8_t* actions, int
                                done, info);
             return check_launch("k_env_replay");
         }
+    }
+    // two envs per wave pays once there are >= 2 such waves per SIMD (E >= 4096 on 1024 SIMDs);
+    // below that the launch is latency-bound and one env per wave keeps more waves in flight
+    if (lt && env->N <= envgrp::L && env->M <= envgrp::L && env->E % 2 == 0 && env->E >= kGroupMinEnvs &&
+        !(env->flags & UAVHIP_ENV_ONE_PER_WAVE)) {
+        const int per_block = kWavesPerBlock * 2;
+        hipLaunchKernelGGL(k_env_step_g, dim3((env->E + per_block - 1) / per_block), block, 2 * tab, st, *env, actions,
+                           (int)T, (int)auto_reset, obs_out, reward, done, info);
+        return check_launch("k_env_step_g");
     }
     // (the single-step load order with prefetched next-pair candidates, load_regs<TPL, true>, runs
     // inside the fused rollout launch; instantiating it here as well slowed the multi-step kernels
