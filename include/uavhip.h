@@ -344,7 +344,9 @@ enum uavhip_ppo_phase {
 int64_t uavhip_ppo_workspace_floats(int32_t minibatch);
 
 /* Minibatch rows idx[minibatch] (int32, into the trajectory buffers) of states[n][5][14],
- * actions[n] (int8), old_logp / old_values / returns / advantages [n] (f32); `phases` a mask of
+ * actions[n] (int8), old_logp / old_values / returns / advantages [n] (f32); idx[i] < 0 marks a
+ * padding row that adds nothing to loss_sums or grads (a rank's share of a global minibatch drawn
+ * over the ranks' own trajectory shards varies from step to step); `phases` a mask of
  * uavhip_ppo_phase (UAVHIP_PPO_FULL on one GPU; FORWARD | BACKWARD leaves the raw gradients in
  * ppo->grads). BACKWARD needs the workspace FORWARD filled for the same rows. */
 int uavhip_ppo_step(const uavhip_ppo* ppo, const float* states, const int8_t* actions, const float* old_logp,

@@ -857,17 +857,18 @@ __device__ void loss_partials(Smem& sm, const TrainIO& io, int b0) {
         o[6] = l1;
         o[7] = v;
         const CatVals c = categorical(l0, l1);
-        const float logp = o[0] != 0.f ? c.lc1 : c.lc0;
+        const float logp = o[0] > 0.f ? c.lc1 : c.lc0;
         const float ratio = expf(logp - o[1]);
         const float A = o[4];
         const float s1 = ratio * A;
         const float s2 = fminf(fmaxf(ratio, 1.f - io.eps_clip), 1.f + io.eps_clip) * A;
         const float R = o[3], ov = o[2];
         const float vc = ov + fminf(fmaxf(v - ov, -io.eps_clip), io.eps_clip);
-        red[4 * p + 0] = fminf(s1, s2);
-        red[4 * p + 1] = (v - R) * (v - R);
-        red[4 * p + 2] = (vc - R) * (vc - R);
-        red[4 * p + 3] = -(c.lc0 * c.p0 + c.lc1 * c.p1);
+        const bool pad = o[0] < 0.f;  // padding row (idx < 0): no loss terms
+        red[4 * p + 0] = pad ? 0.f : fminf(s1, s2);
+        red[4 * p + 1] = pad ? 0.f : (v - R) * (v - R);
+        red[4 * p + 2] = pad ? 0.f : (vc - R) * (vc - R);
+        red[4 * p + 3] = pad ? 0.f : -(c.lc0 * c.p0 + c.lc1 * c.p1);
     }
     __syncthreads();
     if (threadIdx.x < 4) {
@@ -914,7 +915,8 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         pkv_a = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(threadIdx.x >> 6, 0), 0);
     }
     // windows -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch tail zero-filled);
-    // training mode gathers minibatch row idx[b] of the trajectory buffer
+    // training mode gathers minibatch row idx[b] of the trajectory buffer (idx < 0: a padding row,
+    // computed on row 0 and flagged by action -1 in smp, so it adds nothing to the loss or gradients)
     {   // <= 3 elements per thread, every load of a round issued before any is used: the
         // training gather is two dependent rounds (row index, then window / loss inputs)
         constexpr int kEl = (TOK * LDX + NTHR - 1) / NTHR;
@@ -923,10 +925,15 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         for (int u = 0; u < kEl; ++u) {
             const int i = threadIdx.x + u * NTHR, p = (i / LDX) % SPW;
             src[u] = (size_t)(b0 + p);
-            if (TR && i < TOK * LDX) src[u] = (size_t)io.idx[b0 + p];
+            if (TR && i < TOK * LDX) src[u] = (size_t)max(io.idx[b0 + p], 0);
         }
         size_t ssrc = 0;
-        if (TR && threadIdx.x < SPW) ssrc = (size_t)io.idx[b0 + threadIdx.x];
+        [[maybe_unused]] bool pad = false;
+        if (TR && threadIdx.x < SPW) {
+            const int r = io.idx[b0 + threadIdx.x];
+            pad = r < 0;
+            ssrc = (size_t)max(r, 0);
+        }
         float v[kEl];
 #pragma unroll
         for (int u = 0; u < kEl; ++u) {
@@ -936,7 +943,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         }
         float ld[5];
         if (TR && threadIdx.x < SPW) {  // per-sample loss inputs
-            ld[0] = (float)(io.act_in[ssrc] != 0);
+            ld[0] = pad ? -1.f : (float)(io.act_in[ssrc] != 0);
             ld[1] = io.oldlp_in[ssrc];
             ld[2] = io.oldv_in[ssrc];
             ld[3] = io.ret_in[ssrc];
@@ -1668,7 +1675,8 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         const int p = threadIdx.x;
         const f32x4 oa = ld4(io.smp + (size_t)(b0 + p) * 8), ob = ld4(io.smp + (size_t)(b0 + p) * 8 + 4);
         const float o[8] = {oa.x, oa.y, oa.z, oa.w, ob.x, ob.y, ob.z, ob.w};
-        const int act = o[0] != 0.f;
+        const int act = o[0] > 0.f;
+        const bool pad = o[0] < 0.f;  // padding row (idx < 0): zero output gradients
         const CatVals c = categorical(o[5], o[6]);
         const float logp = act ? c.lc1 : c.lc0;
         const float ratio = expf(logp - o[1]);
@@ -1697,9 +1705,9 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         const float vc = ov + fminf(fmaxf(dv, -io.eps_clip), io.eps_clip);
         const float w1 = L1 > L2 ? 1.f : (L1 == L2 ? 0.5f : 0.f);
         const float w2 = L2 > L1 ? 1.f : (L1 == L2 ? 0.5f : 0.f);
-        gs[4 * p + 0] = c.y0 * (gy0 - dot);
-        gs[4 * p + 1] = c.y1 * (gy1 - dot);
-        gs[4 * p + 2] = io.value_coef * (w1 * 2.f * (v - R) * inv +
+        gs[4 * p + 0] = pad ? 0.f : c.y0 * (gy0 - dot);
+        gs[4 * p + 1] = pad ? 0.f : c.y1 * (gy1 - dot);
+        gs[4 * p + 2] = pad ? 0.f : io.value_coef * (w1 * 2.f * (v - R) * inv +
                                          ((dv >= -io.eps_clip && dv <= io.eps_clip) ? w2 * 2.f * (vc - R) * inv : 0.f));
         if (p == 0 && blockIdx.x == 0 && io.stats) {
             io.stats[0] += (double)(-tot0 * inv);

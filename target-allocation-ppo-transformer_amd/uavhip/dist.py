@@ -84,10 +84,12 @@ def global_moments(partials, count, group=None):
     return t
 
 
-def normalize_global(adv, moments):
-    """adv <- (adv - mean) / (std + 1e-7) with the global moments, on the GPU kernel."""
+def normalize_global(adv, moments, count=None):
+    """adv <- (adv - mean) / (std + 1e-7) with the global moments, on the GPU kernel. count: the
+    global element count when the caller knows it (else read back from moments: a host sync)."""
     from ._lib import LIB, check, ptr, stream_handle
     m = moments[:2].contiguous()
-    check(LIB.uavhip_adv_normalize(ptr(adv), adv.numel(), ptr(m), 1, int(moments[2].item()), None,
-                                   stream_handle()), "uavhip_adv_normalize")
+    n = int(moments[2].item()) if count is None else int(count)
+    check(LIB.uavhip_adv_normalize(ptr(adv), adv.numel(), ptr(m), 1, n, None, stream_handle()),
+          "uavhip_adv_normalize")
     return adv

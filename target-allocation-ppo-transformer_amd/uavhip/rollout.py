@@ -45,7 +45,8 @@ class RolloutEngine:
     def __init__(self, env, policy, horizon, want_info=True, bootstrap=True, seed=None, normalize=True, row_cache=True,
                  fused_step=None, total_envs=None):
         """normalize=False leaves the advantages raw after GAE: a data-parallel caller normalises
-        them with the moments of the whole gathered batch in gather() (ppo.py:94).
+        them with the moments of the whole data-parallel batch in normalize_global() (called by
+        gather()) (ppo.py:94).
         row_cache=False runs every step on the full-window forward (uavhip_policy_forward).
         fused_step: one launch per step (uavhip_rollout_step: forward + sample + env step); default
         on when the row cache is on and N, M <= 64.
@@ -58,6 +59,7 @@ class RolloutEngine:
         self.normalize = normalize
         self.iteration = 0
         self._gathered = (-1, None)  # (iteration, batch) of the last gather()
+        self._normalized = -1        # iteration whose advantages normalize_global() normalised
         self.policy = policy
         self.T = int(horizon)
         self.bootstrap = bootstrap
@@ -183,6 +185,19 @@ class RolloutEngine:
         self.policy_events, self.env_events = events
         return g
 
+    def normalize_global(self, group=None):
+        """The data-parallel exchange the update on set_shard() batches needs: a
+        3-double all-reduce of the advantage moments and normalisation of this rank's advantages
+        with them (ppo.py:94 normalises over the whole batch). Once per iteration; a no-op when the
+        engine normalised locally (one rank)."""
+        from .dist import global_moments, normalize_global
+        if self.normalize or self._normalized == self.iteration:
+            return self.traj
+        tr = self.traj
+        normalize_global(tr.adv, global_moments(tr.partials, tr.adv.numel(), group), count=self.T * self.total)
+        self._normalized = self.iteration
+        return tr
+
     def gather(self, group=None):
         """The data-parallel exchange of one iteration: a 3-double all-reduce of the
         advantage moments and normalisation with them (when the engine left the advantages raw),
@@ -190,12 +205,10 @@ class RolloutEngine:
         20 floats per transition) and the GPU rebuild of the windows. Returns the gathered batch
         as a dict of [world * T * E, ...] tensors (obs, actions, logp, values, returns, advantages,
         dones) in (rank, step, env) order."""
-        from .dist import all_gather_rows, global_moments, normalize_global, pack_compact, unpack_compact
+        from .dist import all_gather_rows, pack_compact, unpack_compact
         if self._gathered[0] == self.iteration:  # once per iteration (normalises in place)
             return self._gathered[1]
-        tr = self.traj
-        if not self.normalize:
-            normalize_global(tr.adv, global_moments(tr.partials, tr.adv.numel(), group))
+        tr = self.normalize_global(group)
         payload = pack_compact(tr.obs, tr.actions, tr.logp, tr.values, tr.ret, tr.adv, tr.dones)
         gathered = all_gather_rows(payload.view(1, -1), group)
         batch = unpack_compact(gathered, tr.T, tr.E)

@@ -9,11 +9,17 @@ one hipGraph (minibatch b reads its rows at a fixed offset of a device permutati
 epoch copies in the permutation and replays it, drawing minibatches like SubsetRandomSampler
 (torch.randperm of the given CPU generator, ppo.py:97-99).
 
-Data parallel (world > 1, every rank holding the same all-gathered buffers and generator seed):
-each rank takes its 1/world slice of every global minibatch; FORWARD, an all-reduce of the four
-loss sums (the clipped value loss picks max(...) over the GLOBAL minibatch), BACKWARD (gradients
-scaled by 1/global minibatch), an all-reduce of the flat gradient (1.68 MB over RCCL/xGMI), then
-the same clip + Adam on every rank: the result is the single-GPU step on the global minibatch.
+Data parallel (world > 1, the same generator seed on every rank), two ways to hold the batch:
+  * set_shard (the default data path, no trajectory exchange): every rank keeps its own rollout
+    shard; minibatches are drawn over the world * n_local global rows exactly as on one GPU, and
+    each rank computes the rows of every global minibatch that it owns (a varying count, padded with
+    idx -1 rows to a multiple of 64);
+  * set_buffers on all-gathered buffers (RolloutEngine.gather): each rank takes its 1/world slice of
+    every global minibatch.
+Either way one step is FORWARD, an all-reduce of the four loss sums (the clipped value loss picks
+max(...) over the GLOBAL minibatch), BACKWARD (gradients scaled by 1/global minibatch), an
+all-reduce of the flat gradient (1.68 MB over RCCL/xGMI), then the same clip + Adam on every rank:
+the result is the single-GPU step on the global minibatch (fp32 sums in another order).
 """
 import ctypes
 
@@ -80,6 +86,7 @@ class FusedPPOTrainer:
         self.graphs = {}    # steps per epoch -> captured epoch hipGraph over the current buffers
         self._store = None  # stage(): the trainer's own trajectory buffers
         self._cap = 0
+        self.n_local = None  # set_shard(): rows of this rank's shard
 
     def set_buffers(self, states, actions, old_logprobs, old_values, returns, advantages):
         """Trajectory buffers the minibatches are drawn from (kept by reference: a captured graph
@@ -96,6 +103,38 @@ class FusedPPOTrainer:
         self.perm = torch.zeros(n, dtype=torch.int32, device=dev)  # the epoch's minibatch order
         self.graphs = {}
         self._store = None
+        self.n_local = None
+
+    def set_shard(self, states, actions, old_logprobs, old_values, returns, advantages):
+        """Data parallel without a trajectory exchange: this rank's own rollout shard of n_local
+        rows (the same count on every rank; global row g = rank * n_local + local row, the
+        (rank, step, env) order RolloutEngine.gather() would produce). run() draws minibatches over
+        the world * n_local global rows and each rank computes the ones it owns."""
+        self.set_buffers(states, actions, old_logprobs, old_values, returns, advantages)
+        self.n_local = self.n
+        self.n = self.n_local * self.world
+
+    def _resize(self, rows):
+        """Rows per rank and step (a multiple of 64): workspace and row-index buffers for them."""
+        ws = LIB.uavhip_ppo_workspace_floats(rows)
+        self.workspace = torch.zeros(int(ws), dtype=torch.float32, device=self.device)
+        self.idx = torch.zeros(rows, dtype=torch.int32, device=self.device)
+        self.minibatch = rows
+        self.desc.minibatch = rows
+        self.desc.workspace = self.workspace.data_ptr()
+
+    def _owned(self, order, steps):
+        """[steps, rows] this rank's rows of each global minibatch of `order` (global row indices,
+        on the device), in minibatch order, padded with -1 to a common multiple of 64."""
+        Bg = self.global_minibatch
+        o = order[:steps * Bg].view(steps, Bg).long()
+        mine = torch.div(o, self.n_local, rounding_mode="floor") == self.rank
+        cnt = mine.sum(1)
+        rows = max(64, -(-int(cnt.max().item()) // 64) * 64)  # one host sync per epoch
+        first = torch.sort((~mine).to(torch.int8), dim=1, stable=True).indices[:, :rows]
+        local = torch.gather(o, 1, first) - self.rank * self.n_local
+        valid = torch.arange(rows, device=o.device)[None, :] < cnt[:, None]
+        return torch.where(valid, local, torch.full_like(local, -1)).to(torch.int32), rows
 
     def stage(self, states, actions, old_logprobs, old_values, returns, advantages):
         """Copy a trajectory into the trainer's own device buffers (capacity grows in powers of two),
@@ -118,6 +157,7 @@ class FusedPPOTrainer:
             dst[:n].copy_(x)
         self.bufs = self._store
         self.n = n
+        self.n_local = None
 
     def step(self, phases=_lib.PPO_FULL, idx=None):
         """uavhip_ppo_step phases (bit mask) on this rank's rows idx (default self.idx)."""
@@ -176,6 +216,8 @@ class FusedPPOTrainer:
                 raise ValueError(f"perms: every epoch's order must list the {self.n} rows")
         use_graph = use_graph and self.world == 1
         steps = self.n // self.global_minibatch
+        if self.n_local is not None and self.world > 1:
+            return self._run_shard(epochs, generator, perms, steps)
         graph = self.graph if use_graph else None
         if use_graph and graph is None and steps > 0:
             graph = self.capture()
@@ -195,6 +237,25 @@ class FusedPPOTrainer:
                     self.ddp_step(self._rows(self.perm, b))
                 cnt += 1
         self.policy._packed_key = None  # parameters changed under torch's version counters: repack
+        if cnt == 0:
+            return 0.0, 0.0, 0.0, 0
+        st = self.stats.tolist()
+        return st[0] / st[3], st[1] / st[3], st[2] / st[3], cnt
+
+    def _run_shard(self, epochs, generator, perms, steps):
+        """run() over a set_shard() batch: per epoch the global order (the same on every rank), this
+        rank's owned rows of each global minibatch, then the data-parallel steps."""
+        self.stats.zero_()
+        cnt = 0
+        for ep in range(epochs):
+            order = perms[ep] if perms is not None else torch.randperm(self.n, generator=generator)
+            rows, r = self._owned(order.to(self.device), steps)
+            if r != self.minibatch:
+                self._resize(r)
+            for b in range(steps):
+                self.ddp_step(rows[b])
+                cnt += 1
+        self.policy._packed_key = None
         if cnt == 0:
             return 0.0, 0.0, 0.0, 0
         st = self.stats.tolist()

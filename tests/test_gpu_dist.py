@@ -13,7 +13,10 @@ to refreshed scenes and windows carried across the iteration boundary -- the gat
 the union's trajectory in (rank, step, env) order bit for bit, the normalised advantages agree to
 1e-6 (the moments are folded in another order), and after 2 epochs of 18 minibatch steps the ranks'
 parameters are identical and equal the single-process update on the global minibatches within the
-Adam tolerance of tests/test_gpu_train.py."""
+Adam tolerance of tests/test_gpu_train.py -- both for the update on the gathered batch and for the
+exchange-free one on each rank's own shard (FusedPPOTrainer.set_shard: a rank computes the rows of
+every global minibatch it owns, padded with idx -1 rows)."""
+import copy
 import os
 import socket
 import sys
@@ -61,6 +64,7 @@ def _rank(rank, port, q):
         torch.cuda.set_device(0)
         from uavhip.train import FusedPPOTrainer
         pol, eng = _engine(E, rank * E, normalize=False)
+        pol_shard = copy.deepcopy(pol)
         eng.start()
         batches = []
         for _ in range(ITERS):
@@ -71,8 +75,14 @@ def _rank(rank, port, q):
         assert tr.world == WORLD and tr.minibatch == BG // WORLD
         tr.set_buffers(b["obs"], b["actions"], b["logp"], b["values"], b["returns"], b["advantages"])
         st = tr.run(epochs=EPOCHS, generator=torch.Generator().manual_seed(3))
+        # the same update from this rank's own shard (advantages already normalised globally)
+        t, n = eng.traj, T * E
+        ts = FusedPPOTrainer(pol_shard, BG)
+        ts.set_shard(t.obs[:T].reshape(n, 5, 14), t.actions.reshape(n), t.logp.reshape(n), t.values.reshape(n),
+                     t.ret.reshape(n), t.adv.reshape(n))
+        st_shard = ts.run(epochs=EPOCHS, generator=torch.Generator().manual_seed(3))
         torch.cuda.synchronize()
-        q.put((rank, batches, tr.params.cpu().numpy(), st))
+        q.put((rank, batches, (tr.params.cpu().numpy(), ts.params.cpu().numpy(), ts.minibatch), (st, st_shard)))
     except BaseException as exc:  # report instead of hanging the parent on q.get
         q.put((rank, repr(exc), None, None))
         raise
@@ -127,20 +137,22 @@ def test_world2_sharded_iteration_matches_one_process():
                                                                    "advantages")))
     s1 = single.run(epochs=EPOCHS, generator=torch.Generator().manual_seed(3), use_graph=False)
     steps = EPOCHS * (WORLD * T * E // BG)
-    assert s1[3] == res[0][2][3] == res[1][2][3] == steps
-    np.testing.assert_allclose(res[0][2][:3], s1[:3], rtol=1e-4)
-    p0, p1 = res[0][1], res[1][1]
-    assert np.array_equal(p0, p1)  # the replicas stay bit-identical
     ps = single.params.cpu().numpy()
     offs, n = layout()
-    ends = offs[1:] + [n]
-    worst = 0.0
-    for (k, v), o, e_ in zip(pol.state_dict().items(), offs, ends):
-        d = np.abs(p0[o:o + v.numel()] - ps[o:o + v.numel()])
-        reach = steps * (2e-4 if k.startswith("actor") else 1e-3)  # lr x steps: Adam's reach
-        if k.endswith("in_proj_bias"):  # the key bias: gradient is rounding noise in both
-            assert d[128:256].max() <= 2 * reach, k
-            d = np.concatenate([d[:128], d[256:]])
-        worst = max(worst, float(d.max()) / reach)
-        assert d.max() <= 0.01 * reach and d.mean() <= 1e-5 * reach, (k, float(d.max()), reach)
-    print(f"data-parallel vs single-process parameters: max |d| = {worst:.3e} x lr x steps")
+    for mode in (0, 1):  # 0: gathered batch, 1: own shards
+        name = ("gathered", "sharded")[mode]
+        assert s1[3] == res[0][2][mode][3] == res[1][2][mode][3] == steps
+        np.testing.assert_allclose(res[0][2][mode][:3], s1[:3], rtol=1e-4)
+        p0, p1 = res[0][1][mode], res[1][1][mode]
+        assert np.array_equal(p0, p1), name  # the replicas stay bit-identical
+        worst = 0.0
+        for (k, v), o in zip(pol.state_dict().items(), offs):
+            d = np.abs(p0[o:o + v.numel()] - ps[o:o + v.numel()])
+            reach = steps * (2e-4 if k.startswith("actor") else 1e-3)  # lr x steps: Adam's reach
+            if k.endswith("in_proj_bias"):  # the key bias: gradient is rounding noise in both
+                assert d[128:256].max() <= 2 * reach, k
+                d = np.concatenate([d[:128], d[256:]])
+            worst = max(worst, float(d.max()) / reach)
+            assert d.max() <= 0.01 * reach and d.mean() <= 1e-5 * reach, (name, k, float(d.max()), reach)
+        print(f"data-parallel ({name}) vs single-process parameters: max |d| = {worst:.3e} x lr x steps")
+    print(f"sharded rows per rank and step: {res[0][1][2]}, {res[1][1][2]} (global minibatch {BG})")

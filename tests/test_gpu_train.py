@@ -165,6 +165,42 @@ def test_data_parallel_phases_match_single_gpu_step():
     np.testing.assert_allclose(ranks[0].stats.cpu().numpy(), single.stats.cpu().numpy(), rtol=1e-5)
 
 
+def test_padding_rows_add_nothing():
+    """Rows idx < 0 (FusedPPOTrainer.set_shard's padding): two simulated ranks owning 50 and 78 rows
+    of a 128-row global minibatch, each padded to 128 rows, sum to the single-GPU step's loss
+    sums and gradients (the same bars as the data-parallel phases above)."""
+    from uavhip import _lib
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.train import FusedPPOTrainer
+    torch.manual_seed(9)
+    base = TransformerActorCritic().cuda()
+    nets = [copy.deepcopy(base) for _ in range(3)]
+    bufs = _buffers(512, seed=13)
+    single = FusedPPOTrainer(nets[0], 128)
+    ranks = [FusedPPOTrainer(nets[1 + r], 128, world=2, rank=r, allreduce=lambda t: None) for r in range(2)]
+    for t in [single] + ranks:
+        t.set_buffers(*bufs)
+    rows = torch.randperm(512, generator=torch.Generator().manual_seed(4))[:128].to(torch.int32).cuda()
+    single.idx.copy_(rows)
+    single.step(_lib.PPO_FORWARD)
+    own = (rows[:50], rows[50:])
+    for t, r in zip(ranks, own):
+        t._resize(128)
+        t.idx.fill_(-1)
+        t.idx[:r.numel()].copy_(r)
+        t.step(_lib.PPO_FORWARD)
+    tot = ranks[0].loss_sums + ranks[1].loss_sums
+    torch.testing.assert_close(tot, single.loss_sums, rtol=2e-6, atol=1e-6)
+    single.step(_lib.PPO_BACKWARD)
+    for t in ranks:
+        t.loss_sums.copy_(single.loss_sums)
+        t.step(_lib.PPO_BACKWARD)
+    g = ranks[0].grads + ranks[1].grads
+    err = float((g - single.grads).abs().max() / single.grads.abs().max())
+    print(f"padded ranks vs single step: max |dg| / max |g| = {err:.2e}")
+    torch.testing.assert_close(g, single.grads, rtol=1e-4, atol=2e-7)
+
+
 def test_device_pack_matches_host_pack():
     """uavhip_policy_pack (device) == policy.pack_weights (host) bit for bit."""
     from uavhip import _lib
