@@ -292,6 +292,14 @@ extern "C" int uavhip_env_reset(const uavhip_env* env, const uint8_t* mask, int3
     return check_launch("k_env_reset");
 }
 
+#ifdef UAVHIP_POLICY_TRACE
+extern "C" int uavhip_env_trace(unsigned long long* out, int n) {  // k_env_replay phase sums (TRACE build)
+    const int total = envrep::kTraceEnvs * envrep::kTracePhases;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(envrep::g_etrace), sizeof(unsigned long long) * (n < total ? n : total),
+                               0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int uavhip_env_step(const uavhip_env* env, const int8_t* actions, int32_t T, int32_t auto_reset,
                                float* obs_out, double* reward, uint8_t* done, double* info, uavhip_stream_t stream) {
     int rc = validate(env, true);
