@@ -12,13 +12,14 @@
 //   walk    lane = step, from the chunk's action bits alone (ballots and popcounts): pointer before /
 //           after, assign, done, episode, full-reset scene flips -- a chunk ends right after a flip,
 //           the rest runs on the new scene;
-//   fold    lane = target / UAV, over the assigns in step order: the per-target not-hit products, locker
-//           costs and lock counts and the info running sums -- step_once's operations in its order --
-//           with every target's nh_final | nh_pure | t_cost after each assign written to a row of
-//           three LDS tables (row 0: the chunk's starting state);
-//   replay  lane = step: J(X) after its assign as the list-order sum over its table row (unlocked
-//           targets add +0.0, as in _calc_J_X), r(X), reward, info and the observation row of the
-//           pointer after the step (obs_row); rows -> LDS;
+//   fold    lane = assign: the per-target not-hit products and locker costs, the info running sums
+//           -- step_once's operations -- as ordered chains over lanes (round r settles chain
+//           position r from position r - 1: bitwise the sequential values), lock counts and
+//           coverage by popcounts over per-target ballots;
+//   replay  lane = step: J(X) after its assign as the list-order sum over every target's current
+//           not-hit product (gathered from the assign lanes; unlocked targets add +0.0, as in
+//           _calc_J_X), r(X), reward, info and the observation row of the pointer after the step
+//           (obs_row); rows -> LDS;
 //   store   16 lanes per step, 4 steps at a time: each step's window out of the row table (an episode
 //           start zeroes the older slots; rows before the chunk come from the carried window).
 // A workgroup holds 4 envs: 4 compute waves (walk, fold, replay, rewards / info) and 4 store waves.
@@ -42,18 +43,14 @@ constexpr int kRowStride = 18;   // floats per observation row in LDS (14 used):
 constexpr int kMaxM = 32;        // targets: the packed step record holds 7-bit pointers, ncov < 256
 constexpr int kSeq = UAVHIP_SEQ_LEN;
 
-// LDS per env, in doubles, every region an even count (16-byte aligned): p_dmg table
-// [N][M], three (C + 1) x (M + 1) column tables (an odd row stride: conflict-free b64 reads of one
-// column by 32 lanes), then twice (chunk k and k + 1): C observation rows, the carried window (70
-// floats).
+// LDS per env, in doubles, every region an even count (16-byte aligned): p_dmg table [N][M], then
+// twice (chunk k and k + 1): C observation rows, the carried window (70 floats).
 __host__ __device__ constexpr size_t even(size_t x) { return (x + 1) & ~(size_t)1; }
-template <int C>
-__host__ __device__ constexpr size_t table_doubles(int M) { return even((size_t)(C + 1) * (M + 1)); }
 template <int C>
 __host__ __device__ constexpr size_t buf_doubles() { return (size_t)C * kRowStride / 2 + 36; }
 template <int C>
 __host__ __device__ constexpr size_t wave_doubles(int N, int M) {
-    return even((size_t)N * M) + 3 * table_doubles<C>(M) + 2 * buf_doubles<C>();
+    return even((size_t)N * M) + 2 * buf_doubles<C>();
 }
 
 __device__ __forceinline__ double shfl_d(double v, int src) {
@@ -66,6 +63,14 @@ __device__ __forceinline__ V put_lane(V v, int i, V old) {
     return lane_id() == i ? v : old;
 }
 __device__ __forceinline__ int top_bit(unsigned long long m) { return m ? 63 - __builtin_clzll(m) : -1; }
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+    return (unsigned long long)(unsigned)readlane_i((int)(unsigned)v, l) |
+           ((unsigned long long)(unsigned)readlane_i((int)(unsigned)(v >> 32), l) << 32);
+}
+__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
+    return (unsigned long long)(unsigned)__shfl((int)(unsigned)v, src) |
+           ((unsigned long long)(unsigned)__shfl((int)(unsigned)(v >> 32), src) << 32);
+}
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 // LDS written by some lanes and read by others of the same wave: complete and order them
 __device__ __forceinline__ void wave_lds_sync() {
@@ -169,12 +174,9 @@ __global__ __launch_bounds__(kBlock) void k_env_replay(uavhip_env env, const int
     const int lane = lane_id(), wv = threadIdx.x >> 6, we = wv & (kWavesPerBlock - 1);
     const int e = blockIdx.x * kWavesPerBlock + we;
     const bool live = e < env.E;
-    const int N = env.N, M = env.M, MS = M + 1;
+    const int N = env.N, M = env.M;
     double* base = s_dyn + (size_t)we * wave_doubles<C>(N, M);
-    double* nhT = base + even((size_t)N * M);
-    double* nhpT = nhT + table_doubles<C>(M);
-    double* tcT = nhpT + table_doubles<C>(M);
-    float* const bufs = reinterpret_cast<float*>(tcT + table_doubles<C>(M));  // [2][C rows | carried window]
+    float* const bufs = reinterpret_cast<float*>(base + even((size_t)N * M));  // [2][C rows | carried window]
     constexpr int kBufFloats = 2 * (int)buf_doubles<C>();
     const long long E = env.E;
     const bool h = obs_f16(env);
@@ -278,85 +280,128 @@ __global__ __launch_bounds__(kBlock) void k_env_replay(uavhip_env env, const int
             const double pp_a = shfl_d(R.ppen, ub);
             const double uc_a = shfl_d(R.ucost, ub);
             ETR(0);
-            // ------------------------------------------------------------ fold
+            // ------------------------------------------------------------ fold (lane = assign)
+            // step_once's per-assign updates (uav_env.py:306-325) as ordered chains over lanes: each
+            // assign continues the chain of the previous assign of its episode (the running sums) and
+            // of the previous assign of its episode to the same target (the not-hit products, the
+            // locker costs); chain position r is settled in round r from the value of position r - 1,
+            // with step_once's operations, so every value is bitwise the sequential one. The chains
+            // of the episode the chunk started in begin from the carried state, later ones from the
+            // fresh state of an episode-end reset (uav_env.py:175-182).
             const double c_r = R.r, c_J = R.J, c_spd = R.sum_pd, c_spf = R.sum_pf, c_ac = R.asg_cost, c_cv = R.cov_val;
             const int c_ncov = R.ncov, c_nasg = R.nasg;
-            if (lane < M) {
-                nhT[lane] = R.nhf[0];
-                nhpT[lane] = R.nhp[0];
-                tcT[lane] = R.tc[0];
-            }
+            const double R0nhf = R.nhf[0], R0nhp = R.nhp[0], R0tc = R.tc[0];  // the chunk's starting targets
             carry[lane] = R.w0;
             if (lane < kObs - kWave) carry[kWave + lane] = R.w1;
-            double ev_spd = 0.0, ev_spf = 0.0, ev_ac = 0.0, ev_cv = 0.0;
-            int ev_cnt = 0;  // lane i: (ncov << 8) | nasg after step i's assign
-            for (unsigned long long ev = (amask | dbits) & nmask; ev; ev &= ev - 1) {  // assigns and episode ends
-                const int i = __builtin_ctzll(ev);
-                const int ci = readlane_i(code, i);
-                if ((ci >> 28) & 1) {  // uav_env.py:306-325, as step_once performs it
-                    const int ubi = ci & 127, tbi = (ci >> 7) & 127;
-                    const double pd = readlane_d(pd_a, i), pp = readlane_d(pp_a, i), uc = readlane_d(uc_a, i);
-                    const double pf = pd * pp;
-                    const int nlk_t = readlane_i(R.nlk[0], tbi);
-                    if (lane == tbi) {
-                        R.nhf[0] = R.nhf[0] * (1.0 - pf);
-                        R.nhp[0] = R.nhp[0] * (1.0 - pd);
-                        R.tc[0] = R.tc[0] + uc;
-                        R.nlk[0] += 1;
-                    }
-                    if (lane == ubi) R.asg = tbi;
-                    R.sum_pd = R.sum_pd + pd;
-                    R.sum_pf = R.sum_pf + pf;
-                    R.asg_cost = R.asg_cost + uc;
-                    if (nlk_t == 0) {
-                        R.cov_val = R.cov_val + readlane_d(R.val[0], tbi);
-                        R.ncov += 1;
-                    }
-                    R.nasg += 1;
-                    if (lane < M) {
-                        const int o = (1 + i) * MS + lane;
-                        nhT[o] = R.nhf[0];
-                        nhpT[o] = R.nhp[0];
-                        tcT[o] = R.tc[0];
-                    }
-                    ev_spd = put_lane(R.sum_pd, i, ev_spd);
-                    ev_spf = put_lane(R.sum_pf, i, ev_spf);
-                    ev_ac = put_lane(R.asg_cost, i, ev_ac);
-                    ev_cv = put_lane(R.cov_val, i, ev_cv);
-                    ev_cnt = put_lane((R.ncov << 8) | R.nasg, i, ev_cnt);
+            // lanes assigning the same target: tmask (assign lanes: those of its target), tm (lane t < M:
+            // those of target t), one ballot per target hit in the chunk
+            unsigned long long tmask = 0, tm = 0;
+            for (unsigned long long rem = amask; rem;) {
+                const int tk = readlane_i(tb, __builtin_ctzll(rem));
+                const unsigned long long m = ballot(la && tb == tk);
+                rem &= ~m;
+                tmask = (la && tb == tk) ? m : tmask;
+                tm = lane == tk ? m : tm;
+            }
+            const int dprev = top_bit(dbits & lt);           // latest episode end before this step
+            const bool fresh = dprev >= 0;                   // the step's episode began inside the chunk
+            const unsigned long long epm = fresh ? ~((2ull << dprev) - 1) : ~0ull;  // its steps
+            const double pf_a = pd_a * pp_a;
+            // per target: not-hit products and locker costs after each assign
+            const unsigned long long tprev = tmask & lt & epm;
+            const int tdep = __popcll(tprev), tsrc = top_bit(tprev);
+            const double st_nhf = shfl_d(R.nhf[0], tb), st_nhp = shfl_d(R.nhp[0], tb), st_tc = shfl_d(R.tc[0], tb);
+            const int st_nlk = __shfl(R.nlk[0], tb);
+            double a_nhf = (fresh ? 1.0 : st_nhf) * (1.0 - pf_a);
+            double a_nhp = (fresh ? 1.0 : st_nhp) * (1.0 - pd_a);
+            double a_tc = (fresh ? 0.0 : st_tc) + uc_a;
+            for (int r = 1; ballot(la && tdep >= r); ++r) {
+                const int sl = tsrc < 0 ? lane : tsrc;
+                const double p_nhf = shfl_d(a_nhf, sl), p_nhp = shfl_d(a_nhp, sl), p_tc = shfl_d(a_tc, sl);
+                const bool now = la && tdep == r;
+                a_nhf = now ? p_nhf * (1.0 - pf_a) : a_nhf;
+                a_nhp = now ? p_nhp * (1.0 - pd_a) : a_nhp;
+                a_tc = now ? p_tc + uc_a : a_tc;
+            }
+            // first lock of the target in the episode: covered (uav_env.py:255-259 N0, cov_val)
+            const bool cov_new = la && tdep == 0 && (fresh || st_nlk == 0);
+            const unsigned long long covbits = ballot(cov_new);
+            const double v_tb = shfl_d(R.val[0], tb);  // (shuffles outside selects: the whole wave active)
+            const double x_cv = cov_new ? v_tb : 0.0;  // + 0.0 keeps a sum >= +0 bitwise
+            // the episode's running sums after each assign
+            const unsigned long long aprv = amask & lt & epm;
+            const int adep = __popcll(aprv), asrc = top_bit(aprv);
+            double ev_spd = (fresh ? 0.0 : c_spd) + pd_a, ev_spf = (fresh ? 0.0 : c_spf) + pf_a;
+            double ev_ac = (fresh ? 0.0 : c_ac) + uc_a, ev_cv = (fresh ? 0.0 : c_cv) + x_cv;
+            for (int r = 1; ballot(la && adep >= r); ++r) {
+                const int sl = asrc < 0 ? lane : asrc;
+                const double p_spd = shfl_d(ev_spd, sl), p_spf = shfl_d(ev_spf, sl), p_ac = shfl_d(ev_ac, sl),
+                             p_cv = shfl_d(ev_cv, sl);
+                const bool now = la && adep == r;
+                ev_spd = now ? p_spd + pd_a : ev_spd;
+                ev_spf = now ? p_spf + pf_a : ev_spf;
+                ev_ac = now ? p_ac + uc_a : ev_ac;
+                ev_cv = now ? p_cv + x_cv : ev_cv;
+            }
+            const int ev_ncov = (fresh ? 0 : c_ncov) + __popcll(covbits & le & epm);
+            const int ev_nasg = (fresh ? 0 : c_nasg) + __popcll(amask & le & epm);
+            const int ev_cnt = (ev_ncov << 8) | ev_nasg;  // lane i: (ncov << 8) | nasg after step i's assign
+            // the state the chunk hands on: that after the last assign of its last episode
+            {
+                const int dl = top_bit(dbits);
+                const unsigned long long fm = dl >= 0 ? ~((2ull << dl) - 1) : ~0ull;
+                const int jt = top_bit(tm & fm), ja = top_bit(amask & fm);
+                const double e_nhf = shfl_d(a_nhf, jt < 0 ? 0 : jt), e_nhp = shfl_d(a_nhp, jt < 0 ? 0 : jt),
+                             e_tc = shfl_d(a_tc, jt < 0 ? 0 : jt);
+                const int nlk_f = __popcll(tm & fm);
+                if (lane < M) {
+                    R.nhf[0] = jt >= 0 ? e_nhf : (dl >= 0 ? 1.0 : R.nhf[0]);
+                    R.nhp[0] = jt >= 0 ? e_nhp : (dl >= 0 ? 1.0 : R.nhp[0]);
+                    R.tc[0] = jt >= 0 ? e_tc : (dl >= 0 ? 0.0 : R.tc[0]);
+                    R.nlk[0] = nlk_f + (dl >= 0 ? 0 : R.nlk[0]);
                 }
-                if ((ci >> 29) & 1) {  // episode end: the state part of reset_regs (uav_env.py:175-182)
-                    R.nhf[0] = 1.0;
-                    R.nhp[0] = 1.0;
-                    R.tc[0] = 0.0;
-                    R.nlk[0] = 0;
-                    R.asg = -1;
-                    R.ncov = 0;
-                    R.nasg = 0;
-                    R.sum_pd = 0.0;
-                    R.sum_pf = 0.0;
-                    R.asg_cost = 0.0;
-                    R.cov_val = 0.0;
+                if (ja >= 0) {
+                    R.sum_pd = readlane_d(ev_spd, ja);
+                    R.sum_pf = readlane_d(ev_spf, ja);
+                    R.asg_cost = readlane_d(ev_ac, ja);
+                    R.cov_val = readlane_d(ev_cv, ja);
+                    const int cnt = readlane_i(ev_cnt, ja);
+                    R.ncov = cnt >> 8;
+                    R.nasg = cnt & 255;
+                } else if (dl >= 0) {
+                    R.sum_pd = R.sum_pf = R.asg_cost = R.cov_val = 0.0;
+                    R.ncov = R.nasg = 0;
+                }
+                if (dl >= 0) R.asg = -1;
+                for (unsigned long long q = amask & fm; q; q &= q - 1) {  // the last episode's locks per UAV
+                    const int ci = readlane_i(code, __builtin_ctzll(q));
+                    if (lane == (ci & 127)) R.asg = (ci >> 7) & 127;
                 }
             }
-            wave_lds_sync();
             ETR(1);
             // ------------------------------------------------------------ replay (lane = step)
-            // J(X), r(X) after this step's assign: the list-order revenue sum over its table row
+            // J(X), r(X) after this step's assign: the list-order revenue sum (uav_env.py:244-269) over
+            // every target's not-hit product at this step -- that after the target's latest assign of
+            // the episode up to here, else the episode's starting value (unlocked targets add +0.0)
             double Jv = 0.0, rv = 0.0;
-            if (la) {
-                const double* col = nhT + (1 + lane) * MS;
+            {
                 double rev = 0.0;
-                for (int k = 0; k < M; ++k) rev = rev + (1.0 - col[k]) * readlane_d(R.val[0], k);
-                const int ncov = ev_cnt >> 8;
-                Jv = rev - (env.prm[UAVHIP_PRM_OMEGA] * ev_ac);
-                rv = (ncov == M) ? 2.0 * Jv : Jv * div_by((double)ncov, (double)M, R.rcp_m);
+                for (int k = 0; k < M; ++k) {
+                    const unsigned long long tmk = readlane_u64(tm, k);
+                    const int j = top_bit(tmk & le & epm);
+                    const double hv = shfl_d(a_nhf, j < 0 ? 0 : j);
+                    const double nh = j >= 0 ? hv : (fresh ? 1.0 : readlane_d(R0nhf, k));
+                    rev = rev + (1.0 - nh) * readlane_d(R.val[0], k);
+                }
+                if (la) {
+                    Jv = rev - (env.prm[UAVHIP_PRM_OMEGA] * ev_ac);
+                    rv = (ev_ncov == M) ? 2.0 * Jv : Jv * div_by((double)ev_ncov, (double)M, R.rcp_m);
+                }
             }
             // the state after this step (before an episode-end reset): that of the latest assign of its
             // episode, else the episode's fresh state (it began inside the chunk), else the chunk's start
-            const int dprev = top_bit(dbits & lt);
             const int alast = top_bit(amask & le), aprev = top_bit(amask & lt);
-            const bool fresh = dprev >= 0, has = alast > dprev, hasp = aprev > dprev;
+            const bool has = alast > dprev, hasp = aprev > dprev;
             const int src = has ? alast : 0;
             const double s_r = shfl_d(rv, src), s_J = shfl_d(Jv, src), s_spd = shfl_d(ev_spd, src),
                          s_spf = shfl_d(ev_spf, src), s_ac = shfl_d(ev_ac, src), s_cv = shfl_d(ev_cv, src);
@@ -383,11 +428,16 @@ __global__ __launch_bounds__(kBlock) void k_env_replay(uavhip_env env, const int
             // episode's first row at (0, 0) on a fresh state (a flip's row is rebuilt on the new scene)
             {
                 const int pu = ld ? 0 : ua, pt = ld ? 0 : ta;
-                const int trow = ld ? -1 : (has ? 1 + alast : (fresh ? -1 : 0));
-                const int o = (trow < 0 ? 0 : trow) * MS + pt;
-                const double nhf = trow < 0 ? 1.0 : nhT[o];
-                const double nhp = trow < 0 ? 1.0 : nhpT[o];
-                const double tc = trow < 0 ? 0.0 : tcT[o];
+                // target pt after the latest assign to it of this step's episode, else the episode's
+                // starting value (fresh, or the chunk's carried state)
+                const int j = top_bit(shfl_u64(tm, pt) & le & epm);
+                const int jl = j < 0 ? 0 : j;
+                const double g_nhf = shfl_d(a_nhf, jl), g_nhp = shfl_d(a_nhp, jl), g_tc = shfl_d(a_tc, jl);
+                const double s_nhf = shfl_d(R0nhf, pt), s_nhp = shfl_d(R0nhp, pt), s_tc = shfl_d(R0tc, pt);
+                const bool zero = ld || (j < 0 && fresh);
+                const double nhf = zero ? 1.0 : (j >= 0 ? g_nhf : s_nhf);
+                const double nhp = zero ? 1.0 : (j >= 0 ? g_nhp : s_nhp);
+                const double tc = zero ? 0.0 : (j >= 0 ? g_tc : s_tc);
                 const ObsRow row = obs_row(shfl_d(R.ucost, pu), shfl_d(R.val[0], pt), tc, nhf, nhp, ld ? 0.0 : ac,
                                            ld ? 0.0 : cv, R.tab[pu * M + pt], shfl_d(R.ppen, pu), R.den_c, R.rcp_c,
                                            R.den_v, R.rcp_v);
