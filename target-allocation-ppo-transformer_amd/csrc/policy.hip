@@ -847,6 +847,32 @@ __device__ __forceinline__ void store_hidden(const Smem& sm, float* __restrict__
 // Training mode: per-sample PPO loss terms of ppo.py:148-160 (Categorical as torch evaluates it,
 // transformer_net.py:124-144) and their workgroup sums in sample order -> fpart[blk][4];
 // logits / value -> smp[b][5..7] for the backward.
+// One sample's four terms from its smp row o[0..4] (action, old logp, old value, return, advantage)
+// and its logits / value -> t[4].
+__device__ __forceinline__ void loss_terms(const float (&o)[5], float l0, float l1, float v, float eps_clip,
+                                           float* t) {
+    const CatVals c = categorical(l0, l1);
+    const float logp = o[0] > 0.f ? c.lc1 : c.lc0;
+    const float ratio = expf(logp - o[1]);
+    const float A = o[4];
+    const float s1 = ratio * A;
+    const float s2 = fminf(fmaxf(ratio, 1.f - eps_clip), 1.f + eps_clip) * A;
+    const float R = o[3], ov = o[2];
+    const float vc = ov + fminf(fmaxf(v - ov, -eps_clip), eps_clip);
+    const bool pad = o[0] < 0.f;  // padding row (idx < 0): no loss terms
+    t[0] = pad ? 0.f : fminf(s1, s2);
+    t[1] = pad ? 0.f : (v - R) * (v - R);
+    t[2] = pad ? 0.f : (vc - R) * (vc - R);
+    t[3] = pad ? 0.f : -(c.lc0 * c.p0 + c.lc1 * c.p1);
+}
+// the block's sums in sample order (threads 0-3, one term each) -> fpart[blk][4]
+__device__ __forceinline__ void loss_block_sums(const float* red, float* fpart, int blk) {
+    if (threadIdx.x < 4) {
+        float acc = 0.f;
+        for (int i = 0; i < SPW; ++i) acc += red[4 * i + threadIdx.x];
+        fpart[blk * 4 + threadIdx.x] = acc;
+    }
+}
 __device__ void loss_partials(Smem& sm, const TrainIO& io, int b0) {
     float* red = sm.x;  // free after the embeddings
     if (threadIdx.x < SPW) {
@@ -856,26 +882,23 @@ __device__ void loss_partials(Smem& sm, const TrainIO& io, int b0) {
         o[5] = l0;
         o[6] = l1;
         o[7] = v;
-        const CatVals c = categorical(l0, l1);
-        const float logp = o[0] > 0.f ? c.lc1 : c.lc0;
-        const float ratio = expf(logp - o[1]);
-        const float A = o[4];
-        const float s1 = ratio * A;
-        const float s2 = fminf(fmaxf(ratio, 1.f - io.eps_clip), 1.f + io.eps_clip) * A;
-        const float R = o[3], ov = o[2];
-        const float vc = ov + fminf(fmaxf(v - ov, -io.eps_clip), io.eps_clip);
-        const bool pad = o[0] < 0.f;  // padding row (idx < 0): no loss terms
-        red[4 * p + 0] = pad ? 0.f : fminf(s1, s2);
-        red[4 * p + 1] = pad ? 0.f : (v - R) * (v - R);
-        red[4 * p + 2] = pad ? 0.f : (vc - R) * (vc - R);
-        red[4 * p + 3] = pad ? 0.f : -(c.lc0 * c.p0 + c.lc1 * c.p1);
+        const float oi[5] = {o[0], o[1], o[2], o[3], o[4]};
+        loss_terms(oi, l0, l1, v, io.eps_clip, red + 4 * p);
     }
     __syncthreads();
-    if (threadIdx.x < 4) {
-        float acc = 0.f;
-        for (int i = 0; i < SPW; ++i) acc += red[4 * i + threadIdx.x];
-        io.fpart[blockIdx.x * 4 + threadIdx.x] = acc;
+    loss_block_sums(red, io.fpart, b0 / SPW);
+}
+// Trunk split: the same partials once both trunks' workgroups have written smp[5..7].
+__global__ __launch_bounds__(64) void k_loss_partials(const TrainIO io) {
+    __shared__ float red[4 * SPW];
+    const int b0 = blockIdx.x * SPW;
+    if (threadIdx.x < SPW) {
+        const float* o = io.smp + (size_t)(b0 + threadIdx.x) * 8;
+        const float oi[5] = {o[0], o[1], o[2], o[3], o[4]};
+        loss_terms(oi, o[5], o[6], o[7], io.eps_clip, red + 4 * threadIdx.x);
     }
+    __syncthreads();
+    loss_block_sums(red, io.fpart, blockIdx.x);
 }
 
 // Fused rollout step (uavhip_rollout_step): the env step of the sampled actions (uav_env.py:295-435)
@@ -904,15 +927,30 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     __shared__ __attribute__((aligned(16))) Smem sm;
     // the younger half (waves 4-7, the arbitration loser of every phase) at priority 1
     if (threadIdx.x >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
-    const int b0 = blockIdx.x * SPW;
-    PTR(0);
-    // training mode: the actor embedding's operands and first K/V weight blocks are loaded before
-    // the minibatch gather stores its rows (a load behind a store burst waits for the burst)
-    [[maybe_unused]] EmbPre ep_a;
-    [[maybe_unused]] APre<2> pkv_a;
+    // training trunk split (TrainIO::split): role 1 = actor trunk + head, 2 = critic trunk + head
+    // of sample block blk; role 0 = both (the rollout always)
+    int blk = blockIdx.x, role = 0;
     if constexpr (TR) {
-        ep_a = embed_load<kActorTrunk>(P);
-        pkv_a = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(threadIdx.x >> 6, 0), 0);
+        if (io.split) {
+            role = blk < io.split ? 1 : 2;
+            if (role == 2) blk -= io.split;
+        }
+    }
+    const bool do_actor = role != 2, do_critic = role != 1;
+    const int b0 = blk * SPW;
+    PTR(0);
+    // training mode: the first trunk's embedding operands and first K/V weight blocks are loaded
+    // before the minibatch gather stores its rows (a load behind a store burst waits for the burst)
+    [[maybe_unused]] EmbPre ep_a, ep_c;
+    [[maybe_unused]] APre<2> pkv_a, pkv_c;
+    if constexpr (TR) {
+        if (do_actor) {
+            ep_a = embed_load<kActorTrunk>(P);
+            pkv_a = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(threadIdx.x >> 6, 0), 0);
+        } else {
+            ep_c = embed_load<kCriticTrunk>(P);
+            pkv_c = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(threadIdx.x >> 6, 0), 0);
+        }
     }
     // windows -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch tail zero-filled);
     // training mode gathers minibatch row idx[b] of the trajectory buffer (idx < 0: a padding row,
@@ -960,14 +998,14 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
                     const int t = i / LDX, s = t / SPW, p = t - s * SPW;
                     const bool m = (s < S - 1) && ((nz >> (lane_id() & 48)) & 0xFFFFull) == 0;
                     sm.mask[p * S + s] = m;
-                    if (TR) io.mask[(size_t)(b0 + p) * S + s] = m ? 1.f : 0.f;
+                    if (TR && do_actor) io.mask[(size_t)(b0 + p) * S + s] = m ? 1.f : 0.f;
                 }
             }
             if (i >= TOK * LDX) continue;
             sm.x[i] = v[u];
-            if (TR) io.xg[(size_t)trow(i / LDX, b0) * 16 + (i % LDX)] = v[u];
+            if (TR && do_actor) io.xg[(size_t)trow(i / LDX, b0) * 16 + (i % LDX)] = v[u];
         }
-        if (TR && threadIdx.x < SPW) {
+        if (TR && do_actor && threadIdx.x < SPW) {
             float* o = io.smp + (size_t)(b0 + threadIdx.x) * 8;
             for (int c = 0; c < 5; ++c) o[c] = ld[c];
         }
@@ -989,84 +1027,98 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     // training mode: the actor head's and the critic embedding's / first GEMM's operands are loaded
     // ahead of the actor's LN2 activation stores (layer_tail hook)
     APre<4> ph;
-    [[maybe_unused]] EmbPre ep_c;
-    [[maybe_unused]] APre<2> pkv_c;
-    if constexpr (!ROWS) {
-        APre<2> pkv;
-        if constexpr (TR) {
-            pkv = pkv_a;
-            embed_apply<kActorTrunk, TR>(sm, ep_a, io.e[0], io.h0[0], b0);
-        } else {
-            pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-            embed<kActorTrunk, TR>(sm, P, io.e[0], io.h0[0], b0);
+    if (do_actor) {
+        if constexpr (!ROWS) {
+            APre<2> pkv;
+            if constexpr (TR) {
+                pkv = pkv_a;
+                embed_apply<kActorTrunk, TR>(sm, ep_a, io.e[0], io.h0[0], b0);
+            } else {
+                pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+                embed<kActorTrunk, TR>(sm, P, io.e[0], io.h0[0], b0);
+            }
+            PTR(2);
+            __syncthreads();
+            if constexpr (TR) {
+                encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0, [&] {
+                    if (wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
+                    if (do_critic) {
+                        ep_c = embed_load<kCriticTrunk>(P);
+                        pkv_c = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+                    }
+                });
+            } else {
+                encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0);
+            }
         }
-        PTR(2);
+        if (!TR && wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
         __syncthreads();
-        if constexpr (TR) {
-            encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0, [&] {
-                if (wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
-                ep_c = embed_load<kCriticTrunk>(P);
-                pkv_c = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-            });
-        } else {
-            encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0);
-        }
-    }
-    if (!TR && wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
-    __syncthreads();
-    PTR(3);
-    head_mlp<kActorHead, 2>(sm, P, ph, sm.logits);
-    if (TR) store_hidden(sm, io.z[0], b0);  // before the critic's LayerNorm partials reuse sm.z
+        PTR(3);
+        head_mlp<kActorHead, 2>(sm, P, ph, sm.logits);
+        if (TR) store_hidden(sm, io.z[0], b0);  // before the critic's LayerNorm partials reuse sm.z
+    }  // do_actor
     PTR(4);
-    // critic trunk (2 layers) + head
-    if constexpr (ROWS) {
-        APre<kPwD> pw[3];
-        RowPre<3> rp;
-        rows_prologue<kCriticTrunk>(sm, P, pw, rp, rio, b0);
-        __syncthreads();
-        encoder_layer_rows<kCriticTrunk>(sm, P, pw, rp, rio, b0);
-    }
-    APre<2> pkv;
-    if constexpr (!ROWS) {
-        if constexpr (TR) {
-            embed_apply<kCriticTrunk, TR>(sm, ep_c, io.e[1], io.h0[1], b0);
-            __syncthreads();
-            encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv_c, io.L[1], b0, [&] {
-                pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
-            });
-        } else {
-            APre<2> pkv0 = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-            embed<kCriticTrunk, TR>(sm, P, io.e[1], io.h0[1], b0);
-            __syncthreads();
-            encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv0, io.L[1], b0);
-        }
-    }
-    if (!TR) pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
-    __syncthreads();
-    if constexpr (TR) {
-        encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0, [&] {
-            if (wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
-        });
-    } else {
-        encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0);
-    }
-    // fused env step, two envs per wave side by side: its state loads are issued here and land
-    // while the critic head runs
+    // fused env step (ENV): two envs per wave side by side, state loads issued before the critic head
     [[maybe_unused]] const bool env_grp =
         ENV && env.N <= envgrp::L && env.M <= envgrp::L && b0 + 2 * wv + 1 < B;
     [[maybe_unused]] envgrp::GRegs gR;
     [[maybe_unused]] envgrp::GPending gq;
-    if constexpr (ENV) {
-        if (env_grp) envgrp::gload_issue(gR, gq, env, b0 + 2 * wv + (lane_id() >> 5), lane_id() & 31);
-    }
-    if (!TR && wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
-    __syncthreads();
-    PTR(5);
-    head_mlp<kCriticHead, 1>(sm, P, ph, sm.value);
-    PTR(6);
+    if (do_critic) {
+        // critic trunk (2 layers) + head
+        if constexpr (ROWS) {
+            APre<kPwD> pw[3];
+            RowPre<3> rp;
+            rows_prologue<kCriticTrunk>(sm, P, pw, rp, rio, b0);
+            __syncthreads();
+            encoder_layer_rows<kCriticTrunk>(sm, P, pw, rp, rio, b0);
+        }
+        APre<2> pkv;
+        if constexpr (!ROWS) {
+            if constexpr (TR) {
+                embed_apply<kCriticTrunk, TR>(sm, ep_c, io.e[1], io.h0[1], b0);
+                __syncthreads();
+                encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv_c, io.L[1], b0, [&] {
+                    pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
+                });
+            } else {
+                APre<2> pkv0 = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+                embed<kCriticTrunk, TR>(sm, P, io.e[1], io.h0[1], b0);
+                __syncthreads();
+                encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv0, io.L[1], b0);
+            }
+        }
+        if (!TR) pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
+        __syncthreads();
+        if constexpr (TR) {
+            encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0, [&] {
+                if (wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
+            });
+        } else {
+            encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0);
+        }
+        // the env step's state loads land while the critic head runs
+        if constexpr (ENV) {
+            if (env_grp) envgrp::gload_issue(gR, gq, env, b0 + 2 * wv + (lane_id() >> 5), lane_id() & 31);
+        }
+        if (!TR && wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
+        __syncthreads();
+        PTR(5);
+        head_mlp<kCriticHead, 1>(sm, P, ph, sm.value);
+        PTR(6);
+        if (TR) store_hidden(sm, io.z[1], b0);
+    }  // do_critic
     if (TR) {
-        store_hidden(sm, io.z[1], b0);
-        loss_partials(sm, io, b0);
+        if (role == 0) {
+            loss_partials(sm, io, b0);
+        } else if (threadIdx.x < SPW) {  // trunk split: this trunk's head outputs -> smp[5..7]
+            float* o = io.smp + (size_t)(b0 + threadIdx.x) * 8;
+            if (do_actor) {
+                o[5] = sm.logits[2 * threadIdx.x];
+                o[6] = sm.logits[2 * threadIdx.x + 1];
+            } else {
+                o[7] = sm.value[threadIdx.x];
+            }
+        }
         return;
     }
     // Categorical(softmax(logits)): sample / log_prob / entropy (transformer_net.py:118-122)
@@ -1449,14 +1501,15 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
     const float* W2T = PT + kTW2;
     const int wv = threadIdx.x >> 6, l = lane_id(), i16 = l & 15, g = l >> 4;
     const int fo = 16 * wv + 4 * g;  // this lane's 4 output features of a 16-row tile of wave wv
-    float* bias = io.bpart + (size_t)blockIdx.x * kBiasPart;  // this workgroup's bias partials
+    const int blk = b0 / SPW;  // the sample block (its partial rows)
+    float* bias = io.bpart + (size_t)blk * kBiasPart;  // this workgroup's bias partials
 
     // LN2 backward: sm.h -> sm.ctx (= df)
     APre<DQ> pa = prefetch<DQ>(W2T, D, 16 * wv, 0);
     LnBwdPre lnp;
     if (ln2_pre) lnp = *ln2_pre;
     else ln_bwd_load(lnp, io.xhat2, io.rstd2, P + kOffs.o[layer_param(trunk, layer, N2W)], qtok0, b0, last);
-    ln_bwd_lds(sm.h, sm.ctx, lnp, io.df, io.ln2_part + (size_t)blockIdx.x * 2 * D, bias + kBiasL2, qtok0, b0, last,
+    ln_bwd_lds(sm.h, sm.ctx, lnp, io.df, io.ln2_part + (size_t)blk * 2 * D, bias + kBiasL2, qtok0, b0, last,
                sm.big);
     BTR(TB + 1);
     __syncthreads();
@@ -1524,7 +1577,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
     __syncthreads();
     BTR(TB + 6);
     // LN1 backward: sm.ctx -> sm.h (= dz1)
-    ln_bwd_lds(sm.ctx, sm.h, lnp, io.dz1, io.ln1_part + (size_t)blockIdx.x * 2 * D, bias + kBiasOut, qtok0, b0, last,
+    ln_bwd_lds(sm.ctx, sm.h, lnp, io.dz1, io.ln1_part + (size_t)blk * 2 * D, bias + kBiasOut, qtok0, b0, last,
                sm.big);
     BTR(TB + 7);
     __syncthreads();
@@ -1639,7 +1692,9 @@ __device__ void embed_bwd(Smem& sm, const EmbBwdPre& ep, float* __restrict__ par
 // ties send half the gradient to each side, clamp passes it on the closed interval), then the
 // heads' backward: dz = relu'(z) (W2^T g) for both heads -> io.dz, LDS (actor: sm.z, critic:
 // sm.ctx + 64, both [16][LDZ]), and the head.2 weight / bias partials of the 16 samples.
-__device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io, int b0) {
+// role (trunk split): 0 both heads, 1 the actor head only, 2 the critic head only.
+__device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io, int b0, int role) {
+    const int blk = b0 / SPW;
     float* gs = sm.ctx;                  // [16][4]: dlogit0, dlogit1, dvalue
     float* dzc = sm.ctx + 64;            // critic dz rows
     float* zs = sm.big;                  // relu(head.0) rows of both heads [2][16][64]
@@ -1656,7 +1711,7 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 s4[c] = add_xor32(add_xor16(add_ror8(add_ror4(add_xor2(add_xor1(s4[c]))))));
-            if (blockIdx.x == 0 && threadIdx.x == 0 && io.tot_out)
+            if (blk == 0 && role != 2 && threadIdx.x == 0 && io.tot_out)
                 for (int c = 0; c < 4; ++c) io.tot_out[c] = s4[c];
         }
         tot0 = s4[0]; tot1 = s4[1]; tot2 = s4[2]; tot3 = s4[3];
@@ -1709,7 +1764,7 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         gs[4 * p + 1] = pad ? 0.f : c.y1 * (gy1 - dot);
         gs[4 * p + 2] = pad ? 0.f : io.value_coef * (w1 * 2.f * (v - R) * inv +
                                          ((dv >= -io.eps_clip && dv <= io.eps_clip) ? w2 * 2.f * (vc - R) * inv : 0.f));
-        if (p == 0 && blockIdx.x == 0 && io.stats) {
+        if (p == 0 && blk == 0 && role != 2 && io.stats) {
             io.stats[0] += (double)(-tot0 * inv);
             io.stats[1] += (double)fmaxf(L1, L2);
             io.stats[2] += (double)(tot3 * inv);
@@ -1720,6 +1775,7 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     static_assert(NTHR % HID == 0, "dz loop: j = tid % 64 for every i");
     for (int i = threadIdx.x; i < 2 * SPW * HID; i += NTHR) {
         const int trunk = i / (SPW * HID), p = (i / HID) % SPW, j = i % HID;
+        if (role == 1 + (trunk ^ 1)) continue;  // the other role's head
         const float z = zs[(trunk * SPW + p) * HID + j];
         const float g = trunk ? w2c * gs[4 * p + 2] : w2a0 * gs[4 * p] + w2a1 * gs[4 * p + 1];
         const float dz = z > 0.f ? g : 0.f;
@@ -1728,15 +1784,16 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     }
     __syncthreads();
     // head.0 bias partials (sum over the 16 samples of dz, from LDS)
-    if (threadIdx.x < 2 * HID) {
+    if (threadIdx.x < 2 * HID && role != 1 + (threadIdx.x / HID ^ 1)) {
         const int trunk = threadIdx.x / HID, j = threadIdx.x % HID;
         const float* d = trunk ? dzc : sm.z;
         float acc = 0.f;
         for (int p = 0; p < SPW; ++p) acc += d[p * LDZ + j];
-        io.hpart[(size_t)blockIdx.x * kHeadPart + kHeadB0 + threadIdx.x] = acc;
+        io.hpart[(size_t)blk * kHeadPart + kHeadB0 + threadIdx.x] = acc;
     }
     // head.2 partials, summed over the 16 samples in order: dW2[o][j] = sum g_o z_j, db2[o] = sum g_o
-    if (threadIdx.x < kHeadB0) {
+    // [0, 2 HID + 2): actor head.2, [2 HID + 2, 3 HID + 3): critic head.2, then padding (actor role)
+    if (threadIdx.x < kHeadB0 && role != ((threadIdx.x >= 2 * HID + 2 && threadIdx.x < 3 * HID + 3) ? 1 : 2)) {
         const int i = threadIdx.x;
         float acc = 0.f;
         if (i < 2 * HID) {
@@ -1750,7 +1807,7 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         } else if (i < 3 * HID + 3) {
             for (int p = 0; p < SPW; ++p) acc += gs[4 * p + 2];
         }
-        io.hpart[(size_t)blockIdx.x * kHeadPart + i] = acc;
+        io.hpart[(size_t)blk * kHeadPart + i] = acc;
     }
 }
 
@@ -1769,17 +1826,22 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
     __shared__ __attribute__((aligned(16))) Smem sm;
     // the younger half (waves 4-7, the arbitration loser of every phase) at priority 1
     if (threadIdx.x >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
-    const int b0 = blockIdx.x * SPW;
+    // trunk split (BwdIO::split): workgroups [0, split) the actor head + trunk, then the critic's
+    int blk = blockIdx.x, role = 0;
+    if (io.split) {
+        role = blk < io.split ? 1 : 2;
+        if (role == 2) blk -= io.split;
+    }
+    const int b0 = blk * SPW;
     if (threadIdx.x < SPW * S) sm.mask[threadIdx.x] = io.mask[(size_t)b0 * S + threadIdx.x] != 0.f;
     BTR(0);
-    heads_bwd(sm, P, io, b0);
+    heads_bwd(sm, P, io, b0, role);
     __syncthreads();
     BTR(1);
-    // critic: head.0, layer 1 (pruned), layer 0, embedding
-    head_input_grad(sm, PT + kHeadT + D * HID, sm.ctx + 64);
-    __syncthreads();
-    BTR(2);
-    {
+    if (role != 1) {  // critic: head.0, layer 1 (pruned), layer 0, embedding
+        head_input_grad(sm, PT + kHeadT + D * HID, sm.ctx + 64);
+        __syncthreads();
+        BTR(2);
         // layer 0's LN2-backward operands are loaded at the end of layer 1's backward
         LnBwdPre l2;
         bwd_layer<kCriticTrunk, 1, true, 4>(sm, P, PT + 2 * kLayerT, io.L[2], b0, nullptr, nullptr, nullptr, nullptr,
@@ -1790,18 +1852,19 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
                                             });
         EmbBwdPre ep;
         bwd_layer<kCriticTrunk, 0, false, 20>(sm, P, PT + 1 * kLayerT, io.L[1], b0, &ep, io.e[1], io.xg, &l2);
-        embed_bwd(sm, ep, io.epart + ((size_t)blockIdx.x * 2 + 1) * kEmbPart);
+        embed_bwd(sm, ep, io.epart + ((size_t)blk * 2 + 1) * kEmbPart);
+        __syncthreads();
+        BTR(52);
     }
-    __syncthreads();
-    BTR(52);
-    // actor: head.0, layer 0 (pruned), embedding
-    head_input_grad(sm, PT + kHeadT, sm.z);
-    __syncthreads();
-    BTR(53);
-    EmbBwdPre ep;
-    bwd_layer<kActorTrunk, 0, true, 36>(sm, P, PT, io.L[0], b0, &ep, io.e[0], io.xg);
-    embed_bwd(sm, ep, io.epart + (size_t)blockIdx.x * 2 * kEmbPart, 57);
-    BTR(54);
+    if (role != 2) {  // actor: head.0, layer 0 (pruned), embedding
+        head_input_grad(sm, PT + kHeadT, sm.z);
+        __syncthreads();
+        BTR(53);
+        EmbBwdPre ep;
+        bwd_layer<kActorTrunk, 0, true, 36>(sm, P, PT, io.L[0], b0, &ep, io.e[0], io.xg);
+        embed_bwd(sm, ep, io.epart + (size_t)blk * 2 * kEmbPart, 57);
+        BTR(54);
+    }
 }
 
 
@@ -1813,13 +1876,20 @@ using namespace uavhip;
 namespace uavhip {
 namespace pol {
 int policy_forward_train(const float* packed, const float* states, const TrainIO& io, int Bm, hipStream_t st) {
-    hipLaunchKernelGGL(k_policy_forward<true>, dim3(Bm / SPW), dim3(NTHR), 0, st, packed, states, Bm, nullptr, 0ull,
-                       0ull, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, io, RowIO{}, uavhip_env{}, EnvOut{});
+    hipLaunchKernelGGL(k_policy_forward<true>, dim3((io.split ? 2 : 1) * (Bm / SPW)), dim3(NTHR), 0, st, packed,
+                       states, Bm, nullptr, 0ull, 0ull, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, io,
+                       RowIO{}, uavhip_env{}, EnvOut{});
     return check_launch("k_policy_forward<train>");
 }
 
+int policy_loss_partials(const TrainIO& io, int Bm, hipStream_t st) {
+    hipLaunchKernelGGL(k_loss_partials, dim3(Bm / SPW), dim3(64), 0, st, io);
+    return check_launch("k_loss_partials");
+}
+
 int policy_backward_train(const float* packed, const float* packedT, const BwdIO& io, int Bm, hipStream_t st) {
-    hipLaunchKernelGGL(k_policy_backward, dim3(Bm / SPW), dim3(NTHR), 0, st, packed, packedT, io);
+    hipLaunchKernelGGL(k_policy_backward, dim3((io.split ? 2 : 1) * (Bm / SPW)), dim3(NTHR), 0, st, packed, packedT,
+                       io);
     return check_launch("k_policy_backward");
 }
 

@@ -28,6 +28,11 @@ struct TrainIO {
     float* fpart;                // [Bm/16][4] per-workgroup loss partials: sum min(s1, s2),
                                  // sum (v-R)^2, sum (vc-R)^2, sum entropy (smp[5..7] = logits, value)
     float eps_clip;
+    // trunk split (small minibatches, 2 Bm/16 <= the CU count): workgroups [0, split) run the
+    // actor trunk + head, [split, 2 split) the critic trunk + head of the same 16-sample blocks
+    // (the two trunks are independent until the loss); the loss partials then come from
+    // k_loss_partials. 0: both trunks in every workgroup.
+    int split;
 };
 
 // ---- K6: fused backward of the three encoder layers + embeddings (policy.hip), one workgroup per
@@ -69,6 +74,7 @@ struct BwdIO {
     const float* e[2];       // [R][128] embeddings after ReLU
     float* epart;            // [Bm/16][2][kEmbPart] embedding gradient partials
     BwdLayerIO L[3];         // actor L0 (pruned), critic L0 (full), critic L1 (pruned)
+    int split;               // trunk split as in TrainIO (actor workgroups first)
 };
 // Transposed copies of each layer's GEMM weights in fragment order (the dX GEMMs' A operands):
 // in_proj^T [128][384] | out_proj^T [128][128] | linear1^T [128][256] | linear2^T [256][128].
@@ -85,6 +91,12 @@ int policy_backward_train(const float* packed, const float* packedT, const BwdIO
 // Launch the training-mode forward over Bm samples (multiple of 16) with fragment-order packed
 // weights `packed` (uavhip_policy_pack) and trajectory windows `states` [n][5][14].
 int policy_forward_train(const float* packed, const float* states, const TrainIO& io, int Bm, hipStream_t st);
+// Trunk split: the per-workgroup loss partials from smp (k_loss_partials; the same terms and
+// order as the fused forward's).
+int policy_loss_partials(const TrainIO& io, int Bm, hipStream_t st);
+// Whether a minibatch of Bm samples per step runs trunk-split (both trunks side by side on
+// separate CUs): only while 2 Bm/16 workgroups fit one per CU.
+inline bool trunk_split(int Bm) { return 2 * (Bm / 16) <= 256; }
 
 }  // namespace pol
 }  // namespace uavhip

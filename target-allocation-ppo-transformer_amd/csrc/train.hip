@@ -4,7 +4,10 @@
 // Layout: a minibatch of Bm samples is R = 5 Bm token rows, row = b * 5 + s, features contiguous.
 // One step is 7 launches on one stream (graph-capturable: no host sync, no allocation):
 //    forward   k_policy_forward<TR> (policy.hip, the rollout's fused kernel writing activations),
-//              with the heads and per-workgroup loss partials, then k_loss_sums (the four sums)
+//              with the heads and per-workgroup loss partials, then k_loss_sums (the four sums).
+//              Minibatches of <= 2048 samples (2 Bm/16 workgroups fit one per CU) run trunk-split:
+//              the actor's and the critic's workgroups side by side (the trunks are independent
+//              until the loss), then k_loss_partials; the backward splits the same way
 //    backward  k_policy_backward (K6, policy.hip: loss and head gradients, dX of the encoder
 //              layers and embeddings, one workgroup per 16 samples), then every weight
 //              gradient dW[out][in] = sum_row dY[row][out] X[row][in] as one stream-K fp32 MFMA
@@ -16,6 +19,7 @@
 // all rows, everything else for Bm rows (compact [Bm][...] tensors), so its gradients are exactly
 // the dense model's.
 #include <cmath>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "policy_layout.hpp"
@@ -298,6 +302,12 @@ inline Plan make_plan(int Bm, float* base) {
 
 inline const float* prm(const uavhip_ppo* c, int i) { return c->params + kOffs.o[i]; }
 
+// Trunk split for this minibatch size (UAVHIP_TRUNK_SPLIT=0 turns it off: tests compare both ways).
+inline int split_blocks(int Bm) {
+    const char* e = std::getenv("UAVHIP_TRUNK_SPLIT");
+    return (pol::trunk_split(Bm) && !(e && e[0] == '0')) ? Bm / kHeadSamples : 0;
+}
+
 }  // namespace tr
 }  // namespace uavhip
 
@@ -372,7 +382,9 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
         io.z[1] = p.z_c;
         io.fpart = p.fpart;
         io.eps_clip = c->eps_clip;
+        io.split = split_blocks(Bm);
         TR_CHECK(pol::policy_forward_train(p.packed, states, io, Bm, st));
+        if (io.split) TR_CHECK(pol::policy_loss_partials(io, Bm, st));
         if (!bwd) {  // with BACKWARD in the same call, K6 sums the partials itself (one launch fewer)
             hipLaunchKernelGGL(k_loss_sums, dim3(1), dim3(64), 0, st, p.fpart, nblk, c->loss_sums);
             TR_CHECK(check_launch("k_loss_sums"));
@@ -427,6 +439,7 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         io.e[0] = p.e_a;
         io.e[1] = p.e_c;
         io.epart = p.epart;
+        io.split = split_blocks(Bm);
         const LayerBufs* lb[3] = {&A, &C0, &C1};
         for (int i = 0; i < 3; ++i)
             io.L[i] = pol::BwdLayerIO{lb[i]->qkv, lb[i]->xhat1, lb[i]->rstd1, lb[i]->u, lb[i]->xhat2, lb[i]->rstd2,

@@ -126,6 +126,31 @@ def test_fused_graph_replay_matches_direct_steps():
     torch.testing.assert_close(lp_fused, lp_torch.detach(), rtol=1e-5, atol=2e-6)
 
 
+@pytest.mark.parametrize("Bm", [64, 1024])
+def test_trunk_split_matches_fused_trunks(Bm, monkeypatch):
+    """Minibatches of <= 2048 samples run the actor's and the critic's trunks in separate workgroups
+    (train.hip split_blocks). Same arithmetic per trunk as the both-trunks workgroup: whole optimizer
+    steps (forward, k_loss_partials, backward, weight gradients, Adam) give bitwise the same
+    parameters, loss statistics and Adam state as UAVHIP_TRUNK_SPLIT=0."""
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.train import FusedPPOTrainer
+    torch.manual_seed(8)
+    nets = [TransformerActorCritic().cuda()]
+    nets.append(copy.deepcopy(nets[0]))
+    bufs = _buffers(3 * Bm, seed=14)
+    out = []
+    for net, flag in zip(nets, ("1", "0")):
+        monkeypatch.setenv("UAVHIP_TRUNK_SPLIT", flag)
+        tr = FusedPPOTrainer(net, Bm)
+        tr.set_buffers(*bufs)
+        out.append((tr.run(epochs=2, generator=torch.Generator().manual_seed(3), use_graph=False), tr))
+    (s1, t1), (s0, t0) = out
+    assert s1 == s0
+    for a, b in ((t1.params, t0.params), (t1.adam_m, t0.adam_m), (t1.adam_v, t0.adam_v)):
+        d = int((a != b).sum())
+        assert d == 0, f"{d} elements differ"
+
+
 def test_data_parallel_phases_match_single_gpu_step():
     """Two ranks simulated on one GPU (phases + summed loss_sums / grads in place of the RCCL
     all-reduces) reproduce the single-GPU step on the global minibatch."""
