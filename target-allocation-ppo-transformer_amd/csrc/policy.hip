@@ -218,16 +218,19 @@ __device__ __forceinline__ int orow(int tok, int b0, bool compact) {
     return compact ? b0 + (tok & (SPW - 1)) : trow(tok, b0);
 }
 
-// The epilogue's per-feature operands (GEMM bias, LN weight and bias), loaded by the caller right
-// after the GEMM -- ahead of its next prefetches and the barrier, whose latency then covers them.
+// The epilogue's per-feature operands: the GEMM bias, loaded by the caller BEFORE the GEMM (the
+// epilogue's first instruction needs it, so a load issued after the GEMM would expose a whole L2
+// round trip), and the LN weight and bias, loaded right after the GEMM -- ahead of its next
+// prefetches and the barrier, whose latency then covers them.
 struct LnPar {
     f32x4 bb, ww, lb;
 };
-__device__ __forceinline__ LnPar ln_load(const float* __restrict__ bias, const float* __restrict__ w,
-                                         const float* __restrict__ b) {
+__device__ __forceinline__ f32x4 ln_bias(const float* __restrict__ bias) {
+    return *reinterpret_cast<const f32x4*>(bias + 16 * (threadIdx.x >> 6) + 4 * (lane_id() >> 4));
+}
+__device__ __forceinline__ LnPar ln_load(const f32x4 bb, const float* __restrict__ w, const float* __restrict__ b) {
     const int f0 = 16 * (threadIdx.x >> 6) + 4 * (lane_id() >> 4);
-    return LnPar{*reinterpret_cast<const f32x4*>(bias + f0), *reinterpret_cast<const f32x4*>(w + f0),
-                 *reinterpret_cast<const f32x4*>(b + f0)};
+    return LnPar{bb, *reinterpret_cast<const f32x4*>(w + f0), *reinterpret_cast<const f32x4*>(b + f0)};
 }
 template <int CT, bool TR = false>
 __device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[CT], const LnPar& lp, int ytok0,
@@ -544,11 +547,12 @@ __device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P
     // out projection, h = LN1(h + attn) in its epilogue
     APre<DQ> pf1a, pf1b;
     {
+        const f32x4 bo4 = ln_bias(bo);
         f32x4 acc[CTQ];
         zero(acc);
         gemm_tile<CTQ, DQ>(acc, po, Wo, D, 16 * wv, 0, sm.ctx, LDH, qtok0);
         PTR(tb + 7);
-        const LnPar lp = ln_load(bo, P + kOffs.o[layer_param(trunk, layer, N1W)], P + kOffs.o[layer_param(trunk, layer, N1B)]);
+        const LnPar lp = ln_load(bo4, P + kOffs.o[layer_param(trunk, layer, N1W)], P + kOffs.o[layer_param(trunk, layer, N1B)]);
         pf1a = prefetch<DQ>(W1, D, 16 * wv, 0);
         pf1b = prefetch<DQ>(W1, D, 128 + 16 * wv, 0);
         residual_layernorm<CTQ, TR>(sm, acc, lp, qtok0, LnOut{io.xhat1, io.h1, io.rstd1, b0, last});
@@ -568,12 +572,13 @@ __device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P
         store_rows(sm.big, LDF, io.u, FF, 0, D, qtok0, b0, last);
         store_rows(sm.ctx, LDF, io.u, FF, D, D, qtok0, b0, last);
     }
+    const f32x4 b24 = ln_bias(b2);
     f32x4 acc2[CTQ];
     zero(acc2);
     gemm_tile<CTQ, DQ>(acc2, pf2a, W2, FF, 16 * wv, 0, sm.big, LDF, qtok0);
     gemm_tile<CTQ, DQ>(acc2, pf2b, W2, FF, 16 * wv, 128, sm.ctx, LDF, qtok0);
     PTR(tb + 12);
-    const LnPar lp2 = ln_load(b2, P + kOffs.o[layer_param(trunk, layer, N2W)], P + kOffs.o[layer_param(trunk, layer, N2B)]);
+    const LnPar lp2 = ln_load(b24, P + kOffs.o[layer_param(trunk, layer, N2W)], P + kOffs.o[layer_param(trunk, layer, N2B)]);
     pre_ln2();
     residual_layernorm<CTQ, TR>(sm, acc2, lp2, qtok0, LnOut{io.xhat2, io.h2, io.rstd2, b0, last});
     PTR(tb + 14);
