@@ -109,6 +109,8 @@ def parse():
     ap.add_argument("--eager", action="store_true", help="launch kernels eagerly instead of replaying a hipGraph")
     ap.add_argument("--unfused", action="store_true",
                     help="separate policy and env launches per step instead of uavhip_rollout_step")
+    ap.add_argument("--per-step-launch", action="store_true",
+                    help="one fused launch per rollout step instead of one launch per iteration")
     ap.add_argument("--full-window", action="store_true",
                     help="policy forward over the full window every step (no window-row ring)")
     return ap.parse_args()
@@ -359,7 +361,7 @@ def main():
     env = VecUAVEnv(E, args.uavs, args.targets, 1, 1, seed=1, full_reset_period=200, env_base=rank * E)
     eng = RolloutEngine(env, policy, T, want_info=True, bootstrap=True, seed=1000, normalize=(world == 1),
                         row_cache=not args.full_window, fused_step=False if args.unfused else None,
-                        total_envs=world * E)
+                        total_envs=world * E, persistent=False if args.per_step_launch else None)
     eng.start()
 
     # The iteration is captured once into a hipGraph and replayed. HIP events (recorded on the
@@ -451,8 +453,9 @@ def main():
         except Exception as exc:  # the headline line must still print
             cpu_env = {"value": None, "error": repr(exc)}
 
-    pol_kernel = ("k_policy_forward<false, true, true>" if eng.fused_step else "k_policy_forward<false, true, false>"
-                  if eng.rowproj is not None else "k_policy_forward<false, false, false>")
+    pol_kernel = ("k_rollout_steps" if eng.persistent else "k_policy_forward<false, true, true>" if eng.fused_step
+                  else "k_policy_forward<false, true, false>" if eng.rowproj is not None
+                  else "k_policy_forward<false, false, false>")
     pol_traffic, pol_src = profiled_traffic(pol_kernel)
     env_traffic = None if eng.fused_step else profiled_traffic("k_env_step<1, false>")[0]
     if rank == 0:
@@ -474,10 +477,15 @@ def main():
                          "flop_per_launch_source": "SURVEY.md 8(d): 2,446,208 FLOP/sample x E",
                          "executed_flop_per_launch": flop_exec * E, "executed_achieved": exec_tf,
                          "executed_frac": exec_tf / MFMA_F32_PEAK_TFLOPS,
-                         "path": ("fused rollout step (window-row forward + sample + env step, one launch)"
+                         "steps_per_launch": T if eng.persistent else 1,
+                         "path": ("fused rollout steps (window-row forward + sample + env step), all T steps of the "
+                                  "iteration in one launch (per-step figures = launch / T)" if eng.persistent else
+                                  "fused rollout step (window-row forward + sample + env step, one launch)"
                                   if eng.fused_step else "window-row ring (layer-0 in_proj of the new row only)"
                                   if eng.rowproj is not None else "full window"),
-                         "timing": ("HIP events around each of the T fused launches of the last timed iteration "
+                         "timing": ("HIP events around the T-step launch of the last timed iteration, divided by T "
+                                    "(env step included)" if eng.persistent else
+                                    "HIP events around each of the T fused launches of the last timed iteration "
                                     "(env step included)" if eng.fused_step else
                                     "HIP events around each of the T+1 launches of the last timed iteration")},
             "env_roofline": {"kernel": "env step inside the fused rollout launch" if eng.fused_step else "k_env_step",

@@ -303,6 +303,20 @@ int uavhip_rollout_step(const uavhip_policy* policy, const uavhip_env* env, cons
                         int8_t* action_out, float* logp, float* value, int32_t auto_reset, float* obs_out,
                         double* reward, uint8_t* done, double* info, uavhip_stream_t stream);
 
+/* n consecutive rollout steps in ONE launch (main_train.py:109-117 repeated n times): step t runs
+ * uavhip_rollout_step on windows obs[t] with ring step `step` + t and sampling counters
+ * offset + t * offset_stride + b, writing actions / logp / value / reward / done [t][E], info
+ * [t][E][UAVHIP_INFO_COUNT] (nullable) and the next windows obs[t + 1]. obs is the time-major
+ * [n + 1][E][5][14] f32 trajectory buffer (obs[0] = the current windows). Bitwise equal to n
+ * uavhip_rollout_step calls. Every workgroup loops over the steps of its own 16 envs, so no
+ * grid-wide synchronisation is involved; saves the per-launch tail and start-up of n - 1
+ * launches. N, M <= 64; f32 observations (no UAVHIP_ENV_OBS_F16). */
+int uavhip_rollout_steps(const uavhip_policy* policy, const uavhip_env* env, float* obs, float* rowproj,
+                         int32_t step, int32_t n, int32_t fill, uint64_t seed, uint64_t offset,
+                         uint64_t offset_stride, const uint64_t* offset_dev, int8_t* actions, float* logp,
+                         float* value, int32_t auto_reset, double* reward, uint8_t* done, double* info,
+                         uavhip_stream_t stream);
+
 /* ---------------------------------------------------------------- PPO update (K5) */
 
 /* One clipped-PPO minibatch step of agents/ppo.py:96-169 (evaluate -> surrogate / clipped value

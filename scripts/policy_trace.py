@@ -72,5 +72,9 @@ for k in slots:
     prev = m0
 start = t[:, 0, 0]
 end = t[:, 0, 63 if ENV else 7]
+dur = (t[:, 0, 63 if ENV else 7] - t[:, 0, 0]).astype(np.float64)
+q = np.percentile(dur, [0, 10, 50, 90, 99, 100])
+print("per-block duration (wave 0, cycles): min %d p10 %d median %d p90 %d p99 %d max %d; max/median %.3f"
+      % (*q, q[5] / q[2]))
 print(f"block start spread {int(start.max() - start.min())} cycles; end spread {int(end.max() - end.min())};"
       f" kernel span {int(end.max() - start.min())} cycles")

@@ -24,7 +24,21 @@ int validate_env(const uavhip_env* env, bool need_state);  // env.hip: descripto
 // ------------------------------------------------------------------ wave helpers
 constexpr int kWave = 64;
 
-__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+// threadIdx.x. In the multi-step rollout TU (rollout_steps.hip, UAVHIP_TID_LAUNDER) every use goes
+// through an empty volatile asm: the step loop there would otherwise hoist every lane-index
+// expression of its body (loop invariant) out of the loop and spill them. (Measured against a
+// ballot-based laundering that keeps CSE inside basic blocks: the same to 0.4 %.)
+#ifdef UAVHIP_TID_LAUNDER
+__device__ __forceinline__ unsigned tid_x() {
+    unsigned t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+#else
+__device__ __forceinline__ unsigned tid_x() { return threadIdx.x; }
+#endif
+__device__ __forceinline__ unsigned tid_env() { return tid_x(); }
+__device__ __forceinline__ int lane_id() { return tid_x() & (kWave - 1); }
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
     const unsigned long long b = __double_as_longlong(v);

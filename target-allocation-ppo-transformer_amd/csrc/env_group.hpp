@@ -39,7 +39,7 @@ struct GRegs {
     float* win;    // LDS scratch [kWin] of this env
 };
 
-__device__ __forceinline__ int gbase() { return threadIdx.x & 32; }
+__device__ __forceinline__ int gbase() { return tid_env() & 32; }
 __device__ __forceinline__ int gsh_i(int v, int j) { return __shfl(v, gbase() + j); }
 __device__ __forceinline__ float gsh_f(float v, int j) { return __shfl(v, gbase() + j); }
 __device__ __forceinline__ double gsh_d(double v, int j) {

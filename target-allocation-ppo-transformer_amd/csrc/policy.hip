@@ -49,19 +49,19 @@ constexpr bool kExpNoStore = false;
 
 // Phase tracing (make TRACE=1 only): waves 0 and 4 of the first 256 workgroups stamp s_memtime at
 // the phase boundaries below; uavhip_policy_trace copies the stamps out. Off in the product build.
-#ifdef UAVHIP_POLICY_TRACE
+#if defined(UAVHIP_POLICY_TRACE) && !defined(UAVHIP_STEPS_TU)
 constexpr int kTraceSlots = 64;
 __device__ unsigned long long g_ptrace[256 * 2 * kTraceSlots];
 #define PTR(id)                                                                                  \
     do {                                                                                         \
-        if ((threadIdx.x & 255) == 0 && blockIdx.x < 256)                                        \
-            g_ptrace[(blockIdx.x * 2 + (threadIdx.x >> 8)) * kTraceSlots + (id)] = __builtin_amdgcn_s_memtime(); \
+        if ((tid_x() & 255) == 0 && blockIdx.x < 256)                                        \
+            g_ptrace[(blockIdx.x * 2 + (tid_x() >> 8)) * kTraceSlots + (id)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 __device__ unsigned long long g_btrace[256 * 2 * kTraceSlots];
 #define BTR(id)                                                                                  \
     do {                                                                                         \
-        if ((threadIdx.x & 255) == 0 && blockIdx.x < 256)                                        \
-            g_btrace[(blockIdx.x * 2 + (threadIdx.x >> 8)) * kTraceSlots + (id)] = __builtin_amdgcn_s_memtime(); \
+        if ((tid_x() & 255) == 0 && blockIdx.x < 256)                                        \
+            g_btrace[(blockIdx.x * 2 + (tid_x() >> 8)) * kTraceSlots + (id)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #else
 #define PTR(id) do {} while (0)
@@ -226,16 +226,16 @@ struct LnPar {
     f32x4 bb, ww, lb;
 };
 __device__ __forceinline__ f32x4 ln_bias(const float* __restrict__ bias) {
-    return *reinterpret_cast<const f32x4*>(bias + 16 * (threadIdx.x >> 6) + 4 * (lane_id() >> 4));
+    return *reinterpret_cast<const f32x4*>(bias + 16 * (tid_x() >> 6) + 4 * (lane_id() >> 4));
 }
 __device__ __forceinline__ LnPar ln_load(const f32x4 bb, const float* __restrict__ w, const float* __restrict__ b) {
-    const int f0 = 16 * (threadIdx.x >> 6) + 4 * (lane_id() >> 4);
+    const int f0 = 16 * (tid_x() >> 6) + 4 * (lane_id() >> 4);
     return LnPar{bb, *reinterpret_cast<const f32x4*>(w + f0), *reinterpret_cast<const f32x4*>(b + f0)};
 }
 template <int CT, bool TR = false>
 __device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[CT], const LnPar& lp, int ytok0,
                                                    const LnOut& lo = LnOut{}) {
-    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
     const int f0 = 16 * wv + 4 * g;
     const f32x4 bb = lp.bb;
     f32x4 v[CT];
@@ -312,7 +312,7 @@ __device__ __forceinline__ void store_rows(const float* src, int lds, float* dst
     return;
 #endif
     const int n4 = ncols / 4, items = (TOK - t0) * n4;
-    for (int i = threadIdx.x; i < items; i += NTHR) {
+    for (int i = tid_x(); i < items; i += NTHR) {
         const int tok = t0 + i / n4, q = i % n4;
         *reinterpret_cast<f32x4*>(dst + (size_t)orow(tok, b0, compact) * ldo + c0 + 4 * q) =
             *reinterpret_cast<const f32x4*>(src + tok * lds + 4 * q);
@@ -323,7 +323,7 @@ __device__ __forceinline__ void store_rows(const float* src, int lds, float* dst
 // each lane owning 4 of the 16 head dims; the task loads the 5 keys / values once for all its
 // queries (group 0: positions 0-2 on waves 0-3, group 1: positions 3-4 on waves 4-7).
 __device__ void attention_full(Smem& sm, int c) {
-    const int q4 = threadIdx.x & 3, task = threadIdx.x >> 2;
+    const int q4 = tid_x() & 3, task = tid_x() >> 2;
     const int hh = task & 3, p = (task >> 2) & 15, grp = task >> 6;
     const int d0 = hh * HD + 4 * q4;
     f32x4 k[S], v[S];
@@ -370,8 +370,8 @@ __device__ void attention_full(Smem& sm, int c) {
 // (dot products reduced over the quad with two xor-shuffles).
 __device__ void attention_chunk(Smem& sm, int c, int qs0, int nqs) {
     const int ntask = nqs * SPW * 4;
-    const int q4 = threadIdx.x & 3;
-    for (int task = threadIdx.x >> 2; task < ntask; task += NTHR / 4) {
+    const int q4 = tid_x() & 3;
+    for (int task = tid_x() >> 2; task < ntask; task += NTHR / 4) {
         const int hh = task & 3, rest = task >> 2, p = rest & 15, si = qs0 + (rest >> 4);
         const int ti = si * SPW + p;
         const int d0 = hh * HD + 4 * q4;
@@ -415,7 +415,7 @@ __device__ __forceinline__ EmbPre embed_load(const float* __restrict__ P) {
     const float* We = P + kOffs.o[trunk + EMB_W];
     const float* be = P + kOffs.o[trunk + EMB_B];
     const float* pos = P + kOffs.o[trunk + POS];
-    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
     const int f = 16 * wv + i16;
     EmbPre r;
     r.a.x = 4 * g + 0 < IN ? We[f * IN + 4 * g + 0] : 0.f;
@@ -433,7 +433,7 @@ __device__ __forceinline__ EmbPre embed_load(const float* __restrict__ P) {
 enum { kEmbH = 0, kEmbSplit = 1, kEmbRows = 2 };
 template <int trunk, bool TR = false, int MODE = kEmbH>
 __device__ void embed_apply(Smem& sm, const EmbPre& ep, float* e_out = nullptr, float* h_out = nullptr, int b0 = 0) {
-    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
     constexpr int NT = MODE == kEmbRows ? S - 1 : S;
     f32x4 acc[NT];
 #pragma unroll
@@ -490,7 +490,7 @@ __device__ __forceinline__ void encoder_layer(Smem& sm, const float* __restrict_
     const float* Win = P + kOffs.o[layer_param(trunk, layer, INW)];
     const float* bin = P + kOffs.o[layer_param(trunk, layer, INB)];
     const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
-    const int wv = threadIdx.x >> 6;
+    const int wv = tid_x() >> 6;
     constexpr int CTQ = last ? 1 : S;              // column tiles that need Q / out / LN / FFN
     constexpr int DQ = depth<CTQ>();
     constexpr int qtok0 = last ? (S - 1) * SPW : 0;
@@ -511,7 +511,7 @@ __device__ __forceinline__ void encoder_layer(Smem& sm, const float* __restrict_
         PTR(tb + 2 + 3 * c);
         if (TR && !kExpNoStore) {  // this chunk's Q (query tokens) / K / V -> qkv[row][part * 128 + 64 c + d]
             // by waves 4-7 (V tiles: less MFMA work than the K + Q waves sharing their SIMDs)
-            for (int i = (int)threadIdx.x - NTHR / 2; i < TOK * 48; i += NTHR / 2) {
+            for (int i = (int)tid_x() - NTHR / 2; i < TOK * 48; i += NTHR / 2) {
                 if (i < 0) break;
                 const int tok = i / 48, r = i - tok * 48, part = r >> 4, q = r & 15;
                 if (part == 0 && tok < qtok0) continue;
@@ -539,7 +539,7 @@ __device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P
     const float* b1 = P + kOffs.o[layer_param(trunk, layer, L1B)];
     const float* W2 = P + kOffs.o[layer_param(trunk, layer, L2W)];
     const float* b2 = P + kOffs.o[layer_param(trunk, layer, L2B)];
-    const int wv = threadIdx.x >> 6;
+    const int wv = tid_x() >> 6;
     constexpr int CTQ = last ? 1 : S;
     constexpr int DQ = depth<CTQ>();
     constexpr int qtok0 = last ? (S - 1) * SPW : 0;
@@ -620,7 +620,7 @@ __device__ __forceinline__ void ppos_load(RowPre<NP>& r, const RowIO& rio) {
     for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int i = (threadIdx.x + NTHR * u) % (S * 192);  // (threads past 960 reload, unused)
+            const int i = (tid_x() + NTHR * u) % (S * 192);  // (threads past 960 reload, unused)
             const int s = i / 192, rr = i - 192 * s, part = rr >> 6, cc = rr & 63;
             r.pp[c][u] = pp[s * 3 * D + part * D + 64 * c + cc];
         }
@@ -630,7 +630,7 @@ __device__ __forceinline__ void ppos_stage(Smem& sm, const RowPre<NP>& r, int c)
     float* pl = reinterpret_cast<float*>(sm.red);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        const int i = threadIdx.x + NTHR * u;
+        const int i = tid_x() + NTHR * u;
         if (i < S * 192) pl[i] = r.pp[c][u];
     }
 }
@@ -638,7 +638,7 @@ __device__ __forceinline__ void ppos_stage(Smem& sm, const RowPre<NP>& r, int c)
 // (position tok >> 4 < 4, sample tok & 15); 16 consecutive lanes read one 256-byte row segment.
 template <int NP>
 __device__ __forceinline__ void ring_item(int u, int& part, int& tok) {
-    const int t2 = (threadIdx.x >> 4) + 32 * u;
+    const int t2 = (tid_x() >> 4) + 32 * u;
     part = t2 % NP;
     tok = t2 / NP;
 }
@@ -647,7 +647,7 @@ template <int trunk, int NP>
 __device__ __forceinline__ void ring_load(RowPre<NP>& r, const Smem& sm, const RowIO& rio, int b0, int c) {
     constexpr int ROFF = trunk == kActorTrunk ? 0 : 2 * D;
     const float* slots = rio.rp + kPposFloats;
-    const int q = threadIdx.x & 15;
+    const int q = tid_x() & 15;
     // predicates and offsets first (LDS reads of the mask), then the loads back to back: no LDS
     // read lands in a register of an outstanding load (that forces a vmcnt(0) drain)
     int off[2 * NP];
@@ -718,7 +718,7 @@ __device__ __forceinline__ void encoder_layer_rows(Smem& sm, const float* __rest
     PTR(tb);
     const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
     const float* Wo = P + kOffs.o[layer_param(trunk, 0, OUTW)];
-    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
     const int rows[3] = {16 * wv, D + 16 * wv, 2 * D + 16 * wv};
     f32x4 acc[3] = {};
     gemm_rows<3, kPwD>(acc, pw, Win, D, rows, sm.ctx, LDH, (S - 1) * SPW, [&] {
@@ -735,7 +735,7 @@ __device__ __forceinline__ void encoder_layer_rows(Smem& sm, const float* __rest
     if (trunk != kActorTrunk) ring_load<trunk>(rp, sm, rio, b0, 1);
     PTR(tb + 13);
     const float* pl = reinterpret_cast<const float*>(sm.red);
-    const int q = threadIdx.x & 15;
+    const int q = tid_x() & 15;
     APre<DQ> po;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -776,7 +776,7 @@ __device__ __forceinline__ void encoder_layer_rows(Smem& sm, const float* __rest
 template <int trunk, int NP>
 __device__ __forceinline__ void rows_prologue(Smem& sm, const float* __restrict__ P, APre<kPwD> (&pw)[3],
                                               RowPre<NP>& rp, const RowIO& rio, int b0) {
-    const int wv = threadIdx.x >> 6;
+    const int wv = tid_x() >> 6;
     const EmbPre ep = embed_load<trunk>(P);
     ppos_load<trunk>(rp, rio);
     const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
@@ -796,11 +796,11 @@ __device__ void head_mlp(Smem& sm, const float* __restrict__ P, const APre<4>& p
     const float* b0 = P + kOffs.o[head + 1];
     const float* W2 = P + kOffs.o[head + 2];
     const float* b2 = P + kOffs.o[head + 3];
-    const int wv = threadIdx.x >> 6;
+    const int wv = tid_x() >> 6;
     // second layer: 16 lanes per (sample p, output a) = item p * nout + a, 4 hidden features per
     // lane; its weights and bias are loaded before the first layer's GEMM
     constexpr int kItems = SPW * nout;
-    const int item = threadIdx.x >> 4, k4 = threadIdx.x & 15;
+    const int item = tid_x() >> 4, k4 = tid_x() & 15;
     const int p = item / nout, a = (item - p * nout) % nout;  // in range for every thread
     const f32x4 w2 = *reinterpret_cast<const f32x4*>(W2 + a * HID + 4 * k4);
     const float bb2 = b2[a];
@@ -842,8 +842,8 @@ __device__ __forceinline__ CatVals categorical(float l0, float l1) {
 
 // Training mode: relu(head.0) rows of the 16 samples (sm.z) -> z [Bm][64].
 __device__ __forceinline__ void store_hidden(const Smem& sm, float* __restrict__ z, int b0) {
-    if (threadIdx.x < SPW * HID / 4) {
-        const int p = threadIdx.x / (HID / 4), q = threadIdx.x % (HID / 4);
+    if (tid_x() < SPW * HID / 4) {
+        const int p = tid_x() / (HID / 4), q = tid_x() % (HID / 4);
         *reinterpret_cast<f32x4*>(z + (size_t)(b0 + p) * HID + 4 * q) =
             *reinterpret_cast<const f32x4*>(sm.z + p * LDZ + 4 * q);
     }
@@ -872,16 +872,16 @@ __device__ __forceinline__ void loss_terms(const float (&o)[5], float l0, float 
 }
 // the block's sums in sample order (threads 0-3, one term each) -> fpart[blk][4]
 __device__ __forceinline__ void loss_block_sums(const float* red, float* fpart, int blk) {
-    if (threadIdx.x < 4) {
+    if (tid_x() < 4) {
         float acc = 0.f;
-        for (int i = 0; i < SPW; ++i) acc += red[4 * i + threadIdx.x];
-        fpart[blk * 4 + threadIdx.x] = acc;
+        for (int i = 0; i < SPW; ++i) acc += red[4 * i + tid_x()];
+        fpart[blk * 4 + tid_x()] = acc;
     }
 }
 __device__ void loss_partials(Smem& sm, const TrainIO& io, int b0) {
     float* red = sm.x;  // free after the embeddings
-    if (threadIdx.x < SPW) {
-        const int p = threadIdx.x;
+    if (tid_x() < SPW) {
+        const int p = tid_x();
         float* o = io.smp + (size_t)(b0 + p) * 8;  // o[0..4] written by this thread at kernel start
         const float l0 = sm.logits[2 * p], l1 = sm.logits[2 * p + 1], v = sm.value[p];
         o[5] = l0;
@@ -893,18 +893,20 @@ __device__ void loss_partials(Smem& sm, const TrainIO& io, int b0) {
     __syncthreads();
     loss_block_sums(red, io.fpart, b0 / SPW);
 }
+#ifndef UAVHIP_STEPS_TU
 // Trunk split: the same partials once both trunks' workgroups have written smp[5..7].
 __global__ __launch_bounds__(64) void k_loss_partials(const TrainIO io) {
     __shared__ float red[4 * SPW];
     const int b0 = blockIdx.x * SPW;
-    if (threadIdx.x < SPW) {
-        const float* o = io.smp + (size_t)(b0 + threadIdx.x) * 8;
+    if (tid_x() < SPW) {
+        const float* o = io.smp + (size_t)(b0 + tid_x()) * 8;
         const float oi[5] = {o[0], o[1], o[2], o[3], o[4]};
-        loss_terms(oi, o[5], o[6], o[7], io.eps_clip, red + 4 * threadIdx.x);
+        loss_terms(oi, o[5], o[6], o[7], io.eps_clip, red + 4 * tid_x());
     }
     __syncthreads();
     loss_block_sums(red, io.fpart, blockIdx.x);
 }
+#endif
 
 // Fused rollout step (uavhip_rollout_step): the env step of the sampled actions (uav_env.py:295-435)
 // after the forward, on the same workgroup's 16 envs.
@@ -918,23 +920,20 @@ struct EnvOut {
 
 // ROWS: layer 0 of both trunks on the window-row projection ring (inference only).
 // ENV: the env step of the sampled actions follows (needs ROWS; envs b0 .. b0 + 15).
-template <bool TR, bool ROWS = false, bool ENV = false>
-__global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict__ P, const float* __restrict__ states,
-                                                         int B, const int8_t* __restrict__ actions_in, uint64_t seed,
-                                                         uint64_t offset, const uint64_t* __restrict__ offset_dev,
-                                                         int8_t* __restrict__ action_out,
-                                                         float* __restrict__ logp_out, float* __restrict__ value_out,
-                                                         float* __restrict__ ent_out, float* __restrict__ logits_out,
-                                                         const TrainIO io, const RowIO rio, const uavhip_env env,
-                                                         const EnvOut eo) {
+// One workgroup's whole forward (+ env step) of its 16 samples; the kernels below wrap it.
+template <bool TR, bool ROWS, bool ENV>
+__device__ __forceinline__ void policy_block(Smem& sm, const float* __restrict__ P, const float* __restrict__ states,
+                                             int B, const int8_t* __restrict__ actions_in, uint64_t seed,
+                                             uint64_t offset, const uint64_t* __restrict__ offset_dev,
+                                             int8_t* __restrict__ action_out, float* __restrict__ logp_out,
+                                             float* __restrict__ value_out, float* __restrict__ ent_out,
+                                             float* __restrict__ logits_out, const TrainIO& io, const RowIO& rio,
+                                             const uavhip_env& env, const EnvOut& eo, int bx) {
     static_assert(!(TR && ROWS), "the training forward recomputes every row");
     static_assert(!ENV || ROWS, "the fused env step follows the rollout forward");
-    __shared__ __attribute__((aligned(16))) Smem sm;
-    // the younger half (waves 4-7, the arbitration loser of every phase) at priority 1
-    if (threadIdx.x >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
     // training trunk split (TrainIO::split): role 1 = actor trunk + head, 2 = critic trunk + head
     // of sample block blk; role 0 = both (the rollout always)
-    int blk = blockIdx.x, role = 0;
+    int blk = bx, role = 0;
     if constexpr (TR) {
         if (io.split) {
             role = blk < io.split ? 1 : 2;
@@ -951,10 +950,10 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     if constexpr (TR) {
         if (do_actor) {
             ep_a = embed_load<kActorTrunk>(P);
-            pkv_a = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(threadIdx.x >> 6, 0), 0);
+            pkv_a = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(tid_x() >> 6, 0), 0);
         } else {
             ep_c = embed_load<kCriticTrunk>(P);
-            pkv_c = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(threadIdx.x >> 6, 0), 0);
+            pkv_c = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(tid_x() >> 6, 0), 0);
         }
     }
     // windows -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch tail zero-filled);
@@ -966,26 +965,26 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         size_t src[kEl];
 #pragma unroll
         for (int u = 0; u < kEl; ++u) {
-            const int i = threadIdx.x + u * NTHR, p = (i / LDX) % SPW;
+            const int i = tid_x() + u * NTHR, p = (i / LDX) % SPW;
             src[u] = (size_t)(b0 + p);
             if (TR && i < TOK * LDX) src[u] = (size_t)max(io.idx[b0 + p], 0);
         }
         size_t ssrc = 0;
         [[maybe_unused]] bool pad = false;
-        if (TR && threadIdx.x < SPW) {
-            const int r = io.idx[b0 + threadIdx.x];
+        if (TR && tid_x() < SPW) {
+            const int r = io.idx[b0 + tid_x()];
             pad = r < 0;
             ssrc = (size_t)max(r, 0);
         }
         float v[kEl];
 #pragma unroll
         for (int u = 0; u < kEl; ++u) {
-            const int i = threadIdx.x + u * NTHR;
+            const int i = tid_x() + u * NTHR;
             const int t = i / LDX, k = i - t * LDX, s = t / SPW, p = t - s * SPW;
             v[u] = (i < TOK * LDX && k < IN && b0 + p < B) ? states[(src[u] * S + s) * IN + k] : 0.f;
         }
         float ld[5];
-        if (TR && threadIdx.x < SPW) {  // per-sample loss inputs
+        if (TR && tid_x() < SPW) {  // per-sample loss inputs
             ld[0] = pad ? -1.f : (float)(io.act_in[ssrc] != 0);
             ld[1] = io.oldlp_in[ssrc];
             ld[2] = io.oldv_in[ssrc];
@@ -994,7 +993,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         }
 #pragma unroll
         for (int u = 0; u < kEl; ++u) {
-            const int i = threadIdx.x + u * NTHR;
+            const int i = tid_x() + u * NTHR;
             {  // key padding mask (all-zero rows, the last never masked) from the registers: the 16
                // lanes of a token row vote
                 static_assert(LDX == 16 && NTHR % LDX == 0, "one token row = 16 lanes");
@@ -1010,14 +1009,14 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
             sm.x[i] = v[u];
             if (TR && do_actor) io.xg[(size_t)trow(i / LDX, b0) * 16 + (i % LDX)] = v[u];
         }
-        if (TR && do_actor && threadIdx.x < SPW) {
-            float* o = io.smp + (size_t)(b0 + threadIdx.x) * 8;
+        if (TR && do_actor && tid_x() < SPW) {
+            float* o = io.smp + (size_t)(b0 + tid_x()) * 8;
             for (int c = 0; c < 5; ++c) o[c] = ld[c];
         }
     }
     __syncthreads();
     PTR(1);
-    const int wv = threadIdx.x >> 6;
+    const int wv = tid_x() >> 6;
     const float* headw_a = P + kOffs.o[kActorHead];
     const float* headw_c = P + kOffs.o[kCriticHead];
     // actor trunk (1 layer) + head
@@ -1103,7 +1102,10 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         }
         // the env step's state loads land while the critic head runs
         if constexpr (ENV) {
-            if (env_grp) envgrp::gload_issue(gR, gq, env, b0 + 2 * wv + (lane_id() >> 5), lane_id() & 31);
+            if (env_grp) {
+                const int le = tid_env() & 63;
+                envgrp::gload_issue(gR, gq, env, b0 + 2 * (int)(tid_env() >> 6) + (le >> 5), le & 31);
+            }
         }
         if (!TR && wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
         __syncthreads();
@@ -1115,20 +1117,20 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     if (TR) {
         if (role == 0) {
             loss_partials(sm, io, b0);
-        } else if (threadIdx.x < SPW) {  // trunk split: this trunk's head outputs -> smp[5..7]
-            float* o = io.smp + (size_t)(b0 + threadIdx.x) * 8;
+        } else if (tid_x() < SPW) {  // trunk split: this trunk's head outputs -> smp[5..7]
+            float* o = io.smp + (size_t)(b0 + tid_x()) * 8;
             if (do_actor) {
-                o[5] = sm.logits[2 * threadIdx.x];
-                o[6] = sm.logits[2 * threadIdx.x + 1];
+                o[5] = sm.logits[2 * tid_x()];
+                o[6] = sm.logits[2 * tid_x() + 1];
             } else {
-                o[7] = sm.value[threadIdx.x];
+                o[7] = sm.value[tid_x()];
             }
         }
         return;
     }
     // Categorical(softmax(logits)): sample / log_prob / entropy (transformer_net.py:118-122)
-    if (threadIdx.x < SPW) {
-        const int p = threadIdx.x, b = b0 + p;
+    if (tid_x() < SPW) {
+        const int p = tid_x(), b = b0 + p;
         if (b < B) {
             const float l0 = sm.logits[2 * p], l1 = sm.logits[2 * p + 1];
             const float m = fmaxf(l0, l1);
@@ -1160,16 +1162,16 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         __syncthreads();
         PTR(60);
         using namespace envdev;
-        const int lane = lane_id(), e0 = b0 + 2 * wv;
+        const int lane = tid_env() & 63, wve = tid_env() >> 6, e0 = b0 + 2 * wve;
         if (env_grp) {
             // both envs side by side, 32 lanes each (env_group.hpp); window scratch in the dead sm.h
             const int j = lane & 31, g = lane >> 5, e = e0 + g;
             envgrp::GRegs& R = gR;
             R.tab = nullptr;
-            R.win = sm.h + (2 * wv + g) * envgrp::kWin;
+            R.win = sm.h + (2 * wve + g) * envgrp::kWin;
             envgrp::gload_finish(R, gq, env, e, j);
             PTR(61);
-            envgrp::gstep<false>(R, env, e, j, sm.mask[2 * wv + g], eo.auto_reset, obs_at(eo.obs, e, obs_f16(env)),
+            envgrp::gstep<false>(R, env, e, j, sm.mask[2 * wve + g], eo.auto_reset, obs_at(eo.obs, e, obs_f16(env)),
                           eo.rew + e, eo.done + e, eo.info ? eo.info + (size_t)e * UAVHIP_INFO_COUNT : nullptr);
             PTR(62);
             envgrp::gstore_regs(R, env, e, j);
@@ -1177,7 +1179,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
         } else if (e0 < B) {
             const bool two = e0 + 1 < B;
             EnvRegs<1> R0, R1;
-            R0.row = R1.row = sm.x + 16 * wv;
+            R0.row = R1.row = sm.x + 16 * wve;
             load_regs<1, true>(R0, env, e0, lane);
             if (two) load_regs<1, true>(R1, env, e0 + 1, lane);
 #pragma unroll
@@ -1185,7 +1187,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
                 if (k == 1 && !two) break;
                 EnvRegs<1>& R = k ? R1 : R0;
                 const int e = e0 + k;
-                step_once<1, false>(R, env, e, lane, sm.mask[2 * wv + k], eo.auto_reset,
+                step_once<1, false>(R, env, e, lane, sm.mask[2 * wve + k], eo.auto_reset,
                                     obs_at(eo.obs, e, obs_f16(env)), eo.rew + e, eo.done + e,
                                     eo.info ? eo.info + (size_t)e * UAVHIP_INFO_COUNT : nullptr);
                 store_regs(R, env, e, lane);
@@ -1194,6 +1196,80 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     }
 }
 
+template <bool TR, bool ROWS = false, bool ENV = false>
+__global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict__ P, const float* __restrict__ states,
+                                                         int B, const int8_t* __restrict__ actions_in, uint64_t seed,
+                                                         uint64_t offset, const uint64_t* __restrict__ offset_dev,
+                                                         int8_t* __restrict__ action_out,
+                                                         float* __restrict__ logp_out, float* __restrict__ value_out,
+                                                         float* __restrict__ ent_out, float* __restrict__ logits_out,
+                                                         const TrainIO io, const RowIO rio, const uavhip_env env,
+                                                         const EnvOut eo) {
+    __shared__ __attribute__((aligned(16))) Smem sm;
+    // the younger half (waves 4-7, the arbitration loser of every phase) at priority 1
+    if (tid_x() >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
+    policy_block<TR, ROWS, ENV>(sm, P, states, B, actions_in, seed, offset, offset_dev, action_out, logp_out, value_out,
+                                ent_out, logits_out, io, rio, env, eo, blockIdx.x);
+}
+
+// Multi-step fused rollout (uavhip_rollout_steps). A workgroup's 16 envs and their windows, ring
+// rows and env state are touched by no other workgroup, so one launch runs n consecutive steps of
+// them with only a workgroup barrier in between (the step's global stores -- next windows, ring
+// row, env state -- are read by the next step's waves of the same workgroup: __syncthreads orders
+// them, workgroup scope). Step t: windows obs[t] -> actions / logp / value [t], obs[t + 1],
+// reward / done / info [t]; ring step g + t; sampling counters offset + t * off_stride + b. Saves
+// the per-launch tail (the slowest of 256 workgroups, +2.6 % over the median) and start-up.
+struct StepSeq {
+    int n;                 // steps in this launch
+    long long obs_stride;  // floats from obs[t] to obs[t + 1] (E * 5 * 14)
+    uint64_t off_stride;   // sampling counter advance per step
+};
+// k_rollout_steps is compiled in its own translation unit (rollout_steps.hip: this file with
+// UAVHIP_STEPS_TU + UAVHIP_TID_LAUNDER); uavhip_rollout_steps launches it through this.
+int launch_rollout_steps(const float* P, float* obs, int B, uint64_t seed, uint64_t offset,
+                         const uint64_t* offset_dev, int8_t* actions, float* logp, float* value, const RowIO& rio,
+                         const uavhip_env& env, const EnvOut& eo, const StepSeq& seq, hipStream_t stream);
+#ifdef UAVHIP_STEPS_TU
+__global__ __launch_bounds__(NTHR) void k_rollout_steps(const float* __restrict__ P, const float* __restrict__ states,
+                                                        int B, uint64_t seed, uint64_t offset,
+                                                        const uint64_t* __restrict__ offset_dev,
+                                                        int8_t* __restrict__ action_out, float* __restrict__ logp_out,
+                                                        float* __restrict__ value_out, const RowIO rio,
+                                                        const uavhip_env env, const EnvOut eo, const StepSeq seq) {
+    __shared__ __attribute__((aligned(16))) Smem sm;
+    if (tid_x() >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
+    for (int t = 0; t < seq.n; ++t) {
+        if (t) __syncthreads();  // the previous step's LDS scratch and global stores
+        // the weight pointer, the ring pointer and the block index laundered per step: otherwise the
+        // compiler hoists every loop-invariant address and load of the body out of the loop and
+        // spills them (the body needs all 256 VGPRs of its 2-waves-per-SIMD budget)
+        typedef const __attribute__((address_space(1))) float* gcf;  // keep the global address space
+        typedef __attribute__((address_space(1))) float* gf;
+        gcf Pg = (gcf)P;
+        gf rg = (gf)rio.rp;
+        int bx = blockIdx.x;
+        uint64_t sd = seed;  // (the Philox key schedule would be hoisted too: 20 SGPRs)
+        asm volatile("" : "+s"(Pg), "+s"(rg), "+s"(bx), "+s"(sd));
+        const float* Pt = (const float*)Pg;
+        float* rp = (float*)rg;
+        const size_t o = (size_t)t * B;
+        const RowIO r{rp, rio.B, rio.g + t};
+        const EnvOut e{eo.auto_reset, eo.obs + t * seq.obs_stride, eo.rew + o, eo.done + o,
+                       eo.info ? eo.info + o * UAVHIP_INFO_COUNT : nullptr};
+        policy_block<false, true, true>(sm, Pt, states + t * seq.obs_stride, B, nullptr, sd, offset + t * seq.off_stride,
+                                        offset_dev, action_out + o, logp_out + o, value_out + o, nullptr, nullptr,
+                                        TrainIO{}, r, env, e, bx);
+    }
+}
+int launch_rollout_steps(const float* P, float* obs, int B, uint64_t seed, uint64_t offset,
+                         const uint64_t* offset_dev, int8_t* actions, float* logp, float* value, const RowIO& rio,
+                         const uavhip_env& env, const EnvOut& eo, const StepSeq& seq, hipStream_t stream) {
+    hipLaunchKernelGGL(k_rollout_steps, dim3((B + SPW - 1) / SPW), dim3(NTHR), 0, stream, P, obs, B, seed, offset,
+                       offset_dev, actions, logp, value, rio, env, eo, seq);
+    return check_launch("k_rollout_steps");
+}
+#endif  // UAVHIP_STEPS_TU
+
 // Ring fill of one trunk: u rows of positions 0-3 of the workgroup's 16 windows -> slots
 // (g + 1 + s) mod 5, the same GEMM (k order, bias add) as the forward's new-row u.
 template <int trunk>
@@ -1201,7 +1277,7 @@ __device__ void rows_fill_trunk(Smem& sm, const float* __restrict__ P, const Row
     constexpr int NP = row_parts<trunk>(), P0 = 3 - NP, ROFF = trunk == kActorTrunk ? 0 : 2 * D;
     const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
     const float* bin = P + kOffs.o[layer_param(trunk, 0, INB)];
-    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
     embed_apply<trunk, false, kEmbRows>(sm, embed_load<trunk>(P));
     __syncthreads();
     float* slots = rio.rp + kPposFloats;
@@ -1228,8 +1304,8 @@ template <int trunk>
 __device__ void rows_ppos_trunk(Smem& sm, const float* __restrict__ P, float* out) {
     const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
     const float* pos = P + kOffs.o[trunk + POS];
-    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < SPW * D; i += NTHR) {
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
+    for (int i = tid_x(); i < SPW * D; i += NTHR) {
         const int t = i / D, k = i - t * D;
         sm.h[t * LDH + k] = t < S ? pos[t * D + k] : 0.f;
     }
@@ -1245,6 +1321,7 @@ __device__ void rows_ppos_trunk(Smem& sm, const float* __restrict__ P, float* ou
     __syncthreads();
 }
 
+#ifndef UAVHIP_STEPS_TU
 // uavhip_policy_forward_rows with fill: rebuilds the ring rows of positions 0-3 of every window
 // (blocks < nb) and the Win pos_s table (block nb) from the current weights.
 __global__ __launch_bounds__(NTHR) void k_policy_rows_fill(const float* __restrict__ P,
@@ -1257,7 +1334,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_rows_fill(const float* __restri
         return;
     }
     const int b0 = blockIdx.x * SPW;
-    for (int i = threadIdx.x; i < (S - 1) * SPW * LDX; i += NTHR) {  // positions 0-3 only
+    for (int i = tid_x(); i < (S - 1) * SPW * LDX; i += NTHR) {  // positions 0-3 only
         const int t = i / LDX, k = i - t * LDX, s = t / SPW, p = t - s * SPW;
         sm.x[i] = (k < IN && b0 + p < rio.B) ? states[((size_t)(b0 + p) * S + s) * IN + k] : 0.f;
     }
@@ -1298,7 +1375,7 @@ struct LnBwdPre {
 };
 __device__ __forceinline__ void ln_bwd_load(LnBwdPre& a, const float* __restrict__ xhat, const float* __restrict__ rstd,
                                             const float* __restrict__ w, int t0, int b0, bool compact) {
-    const int f0 = 8 * (threadIdx.x & 15), grp = threadIdx.x >> 4;
+    const int f0 = 8 * (tid_x() & 15), grp = tid_x() >> 4;
     a.w0 = ld4(w + f0);
     a.w1 = ld4(w + f0 + 4);
 #pragma unroll
@@ -1315,7 +1392,7 @@ __device__ __forceinline__ void ln_bwd_load(LnBwdPre& a, const float* __restrict
 __device__ void ln_bwd_lds(const float* src, float* dst, const LnBwdPre& a, float* __restrict__ gout,
                            float* __restrict__ part, float* __restrict__ bias, int t0, int b0, bool compact,
                            float* scratch) {
-    const int j = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int j = tid_x() & 15, grp = tid_x() >> 4;
     const int f0 = 8 * j;
     const f32x4 w0 = a.w0, w1 = a.w1;
     const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
@@ -1346,13 +1423,13 @@ __device__ void ln_bwd_lds(const float* src, float* dst, const LnBwdPre& a, floa
     st4(sc + D + f0, pb0); st4(sc + D + f0 + 4, pb1);
     st4(sc + 2 * D + f0, pd0); st4(sc + 2 * D + f0 + 4, pd1);
     __syncthreads();
-    if (threadIdx.x < 3 * D) {
+    if (tid_x() < 3 * D) {
         float s4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < NTHR / 16; ++q) s4[q & 3] += scratch[q * 3 * D + threadIdx.x];
+        for (int q = 0; q < NTHR / 16; ++q) s4[q & 3] += scratch[q * 3 * D + tid_x()];
         const float tot = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-        if (threadIdx.x < 2 * D) part[threadIdx.x] = tot;
-        else bias[threadIdx.x - 2 * D] = tot;
+        if (tid_x() < 2 * D) part[tid_x()] = tot;
+        else bias[tid_x() - 2 * D] = tot;
     }
 }
 
@@ -1380,7 +1457,7 @@ struct AttnPre {
 };
 template <bool last>
 __device__ __forceinline__ void attn_bwd_load(AttnPre& a, const float* __restrict__ qkv, int c, int b0) {
-    const int o8 = threadIdx.x & 7, hh = (threadIdx.x >> 3) & 3, p = threadIdx.x >> 5;
+    const int o8 = tid_x() & 7, hh = (tid_x() >> 3) & 3, p = tid_x() >> 5;
     const int col = 64 * c + hh * HD + 2 * o8;
     const size_t rb = (size_t)(b0 + p) * S;
 #pragma unroll
@@ -1394,7 +1471,7 @@ __device__ __forceinline__ void attn_bwd_load(AttnPre& a, const float* __restric
 }
 template <bool last>
 __device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch) {
-    const int o8 = threadIdx.x & 7, hh = (threadIdx.x >> 3) & 3, p = threadIdx.x >> 5;
+    const int o8 = tid_x() & 7, hh = (tid_x() >> 3) & 3, p = tid_x() >> 5;
     const int d0 = hh * HD + 2 * o8;
     const int col = 64 * c + d0;
     f32x2 k[S], v[S], dk[S], dv[S];
@@ -1462,8 +1539,8 @@ __device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch
         sk[e] = add_xor32(sk[e]);
         sv[e] = add_xor32(sv[e]);
     }
-    if ((threadIdx.x & 63) < 32) {
-        float* row = scratch + (threadIdx.x >> 6) * 3 * 64;
+    if ((tid_x() & 63) < 32) {
+        float* row = scratch + (tid_x() >> 6) * 3 * 64;
         st2(row + d0, sdq);
         st2(row + 64 + d0, sk);
         st2(row + 128 + d0, sv);
@@ -1482,10 +1559,10 @@ struct EmbBwdPre {
 };
 __device__ __forceinline__ void embed_bwd_load(EmbBwdPre& ep, const float* __restrict__ e, const float* __restrict__ xg,
                                                int b0) {
-    const int f = threadIdx.x & (D - 1), grp = threadIdx.x >> 7;
+    const int f = tid_x() & (D - 1), grp = tid_x() >> 7;
 #pragma unroll
     for (int i = 0; i < TOK / 4; ++i) ep.ev[i] = e[(size_t)trow(grp + 4 * i, b0) * D + f];
-    const int i = threadIdx.x;
+    const int i = tid_x();
     ep.xv = i < TOK * LDX / 4 ? ld4(xg + (size_t)trow(i / (LDX / 4), b0) * 16 + 4 * (i % (LDX / 4)))
                               : f32x4{0.f, 0.f, 0.f, 0.f};
 }
@@ -1504,7 +1581,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
     const float* WoT = PT + kTWo;
     const float* W1T = PT + kTW1;
     const float* W2T = PT + kTW2;
-    const int wv = threadIdx.x >> 6, l = lane_id(), i16 = l & 15, g = l >> 4;
+    const int wv = tid_x() >> 6, l = lane_id(), i16 = l & 15, g = l >> 4;
     const int fo = 16 * wv + 4 * g;  // this lane's 4 output features of a 16-row tile of wave wv
     const int blk = b0 / SPW;  // the sample block (its partial rows)
     float* bias = io.bpart + (size_t)blk * kBiasPart;  // this workgroup's bias partials
@@ -1607,8 +1684,8 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         attn_bwd_chunk<last>(sm, ap, c, sm.scr);
         __syncthreads();
         BTR(TB + 11 + 2 * c);
-        if (threadIdx.x < 3 * 64) {  // in_proj bias partial of the chunk: the 8 wave rows of sm.scr
-            const int i = threadIdx.x;
+        if (tid_x() < 3 * 64) {  // in_proj bias partial of the chunk: the 8 wave rows of sm.scr
+            const int i = tid_x();
             float v = 0.f;
 #pragma unroll
             for (int w = 0; w < NW; ++w) v += sm.scr[w * 192 + i];
@@ -1619,7 +1696,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         APre<2> pw1 = prefetch<2>(WinT, 3 * D, 16 * wv, D + 64 * c);
         APre<2> pw2 = prefetch<2>(WinT, 3 * D, 16 * wv, 2 * D + 64 * c);
         // dq | dk | dv of the chunk -> dqkv rows: 256-byte row segments, float4 per thread
-        for (int i = threadIdx.x; i < TOK * 48; i += NTHR) {
+        for (int i = tid_x(); i < TOK * 48; i += NTHR) {
             const int tok = i / 48, r = i - tok * 48, part = r >> 4, q = r & 15;
             if (part == 0 && tok < qtok0) continue;  // pruned: dq only on the query rows
             st4(io.dqkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q,
@@ -1655,8 +1732,8 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
 // (feature, token group of 20); partials reduced over the 4 groups through sm.big -> part [2560]
 // in the parameters' order (pos | We | be).
 __device__ void embed_bwd(Smem& sm, const EmbBwdPre& ep, float* __restrict__ part, int tb = 55) {
-    const int f = threadIdx.x & (D - 1), grp = threadIdx.x >> 7;
-    if (threadIdx.x < TOK * LDX / 4) st4(sm.x + 4 * threadIdx.x, ep.xv);  // input windows (sm.x was scratch)
+    const int f = tid_x() & (D - 1), grp = tid_x() >> 7;
+    if (tid_x() < TOK * LDX / 4) st4(sm.x + 4 * tid_x(), ep.xv);  // input windows (sm.x was scratch)
     __syncthreads();
     BTR(tb);
     float acc[IN + 1 + S];
@@ -1683,7 +1760,7 @@ __device__ void embed_bwd(Smem& sm, const EmbBwdPre& ep, float* __restrict__ par
     for (int v = 0; v < NV; ++v) sm.big[(grp * NV + v) * D + f] = acc[v];
     __syncthreads();
     BTR(tb + 1);
-    for (int o = threadIdx.x; o < NV * D; o += NTHR) {
+    for (int o = tid_x(); o < NV * D; o += NTHR) {
         const int v = o >> 7, ff = o & (D - 1);
         const float s = (sm.big[v * D + ff] + sm.big[(NV + v) * D + ff]) +
                         (sm.big[(2 * NV + v) * D + ff] + sm.big[(3 * NV + v) * D + ff]);
@@ -1709,14 +1786,14 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     float tot0, tot1, tot2, tot3;
     if (io.fpart) {
         float s4[4] = {0.f, 0.f, 0.f, 0.f};
-        if (threadIdx.x < 64) {
-            for (int i = threadIdx.x; i < io.nfpart; i += 64)
+        if (tid_x() < 64) {
+            for (int i = tid_x(); i < io.nfpart; i += 64)
 #pragma unroll
                 for (int c = 0; c < 4; ++c) s4[c] += io.fpart[i * 4 + c];
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 s4[c] = add_xor32(add_xor16(add_ror8(add_ror4(add_xor2(add_xor1(s4[c]))))));
-            if (blk == 0 && role != 2 && threadIdx.x == 0 && io.tot_out)
+            if (blk == 0 && role != 2 && tid_x() == 0 && io.tot_out)
                 for (int c = 0; c < 4; ++c) io.tot_out[c] = s4[c];
         }
         tot0 = s4[0]; tot1 = s4[1]; tot2 = s4[2]; tot3 = s4[3];
@@ -1725,14 +1802,14 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     }
     {   // every global input in one round trip: z rows (one float4 per thread), per-sample rows,
         // the head.2 weights of this thread's hidden unit j = tid % 64 (the dz loop below)
-        const int trunk = threadIdx.x >> 8, p = (threadIdx.x >> 4) & 15, q = threadIdx.x & 15;
+        const int trunk = tid_x() >> 8, p = (tid_x() >> 4) & 15, q = tid_x() & 15;
         st4(zs + (trunk * SPW + p) * HID + 4 * q, ld4(io.z[trunk] + (size_t)(b0 + p) * HID + 4 * q));
     }
-    const int jj = threadIdx.x % HID;
+    const int jj = tid_x() % HID;
     const float* W2a = P + kOffs.o[kActorHead + 2];
     const float w2a0 = W2a[jj], w2a1 = W2a[HID + jj], w2c = P[kOffs.o[kCriticHead + 2] + jj];
-    if (threadIdx.x < SPW) {
-        const int p = threadIdx.x;
+    if (tid_x() < SPW) {
+        const int p = tid_x();
         const f32x4 oa = ld4(io.smp + (size_t)(b0 + p) * 8), ob = ld4(io.smp + (size_t)(b0 + p) * 8 + 4);
         const float o[8] = {oa.x, oa.y, oa.z, oa.w, ob.x, ob.y, ob.z, ob.w};
         const int act = o[0] > 0.f;
@@ -1778,7 +1855,7 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     }
     __syncthreads();
     static_assert(NTHR % HID == 0, "dz loop: j = tid % 64 for every i");
-    for (int i = threadIdx.x; i < 2 * SPW * HID; i += NTHR) {
+    for (int i = tid_x(); i < 2 * SPW * HID; i += NTHR) {
         const int trunk = i / (SPW * HID), p = (i / HID) % SPW, j = i % HID;
         if (role == 1 + (trunk ^ 1)) continue;  // the other role's head
         const float z = zs[(trunk * SPW + p) * HID + j];
@@ -1789,17 +1866,17 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     }
     __syncthreads();
     // head.0 bias partials (sum over the 16 samples of dz, from LDS)
-    if (threadIdx.x < 2 * HID && role != 1 + (threadIdx.x / HID ^ 1)) {
-        const int trunk = threadIdx.x / HID, j = threadIdx.x % HID;
+    if (tid_x() < 2 * HID && role != 1 + (tid_x() / HID ^ 1)) {
+        const int trunk = tid_x() / HID, j = tid_x() % HID;
         const float* d = trunk ? dzc : sm.z;
         float acc = 0.f;
         for (int p = 0; p < SPW; ++p) acc += d[p * LDZ + j];
-        io.hpart[(size_t)blk * kHeadPart + kHeadB0 + threadIdx.x] = acc;
+        io.hpart[(size_t)blk * kHeadPart + kHeadB0 + tid_x()] = acc;
     }
     // head.2 partials, summed over the 16 samples in order: dW2[o][j] = sum g_o z_j, db2[o] = sum g_o
     // [0, 2 HID + 2): actor head.2, [2 HID + 2, 3 HID + 3): critic head.2, then padding (actor role)
-    if (threadIdx.x < kHeadB0 && role != ((threadIdx.x >= 2 * HID + 2 && threadIdx.x < 3 * HID + 3) ? 1 : 2)) {
-        const int i = threadIdx.x;
+    if (tid_x() < kHeadB0 && role != ((tid_x() >= 2 * HID + 2 && tid_x() < 3 * HID + 3) ? 1 : 2)) {
+        const int i = tid_x();
         float acc = 0.f;
         if (i < 2 * HID) {
             const int o = i / HID, j = i % HID;
@@ -1819,7 +1896,7 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
 // dL/d(trunk output) of the 16 samples = head.0^T dz (MFMA, K = 64; one 16-feature tile per
 // wave) -> sm.h rows of column tile 4, the top gradient of the trunk's last layer.
 __device__ __forceinline__ void head_input_grad(Smem& sm, const float* __restrict__ W0T, const float* dz) {
-    const int wv = threadIdx.x >> 6, l = lane_id(), i16 = l & 15, g = l >> 4;
+    const int wv = tid_x() >> 6, l = lane_id(), i16 = l & 15, g = l >> 4;
     f32x4 acc[1];
     zero(acc);
     gemm_tile<1, 4, 4>(acc, prefetch<4>(W0T, HID, 16 * wv, 0), W0T, HID, 16 * wv, 0, dz, LDZ, 0);
@@ -1830,7 +1907,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
                                                           const BwdIO io) {
     __shared__ __attribute__((aligned(16))) Smem sm;
     // the younger half (waves 4-7, the arbitration loser of every phase) at priority 1
-    if (threadIdx.x >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
+    if (tid_x() >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
     // trunk split (BwdIO::split): workgroups [0, split) the actor head + trunk, then the critic's
     int blk = blockIdx.x, role = 0;
     if (io.split) {
@@ -1838,7 +1915,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
         if (role == 2) blk -= io.split;
     }
     const int b0 = blk * SPW;
-    if (threadIdx.x < SPW * S) sm.mask[threadIdx.x] = io.mask[(size_t)b0 * S + threadIdx.x] != 0.f;
+    if (tid_x() < SPW * S) sm.mask[tid_x()] = io.mask[(size_t)b0 * S + tid_x()] != 0.f;
     BTR(0);
     heads_bwd(sm, P, io, b0, role);
     __syncthreads();
@@ -1906,7 +1983,7 @@ int policy_backward_train(const float* packed, const float* packedT, const BwdIO
 __global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ flat, float* __restrict__ packed,
                                                      float* __restrict__ packedT) {
     constexpr int nq = kOffs.o[kNumParams] / 4;
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = blockIdx.x * 256 + tid_x();
     if (i < nq) {
         const int f = 4 * i;
         int lo = 0, hi = kNumParams;  // parameter q: kOffs.o[q] <= f < kOffs.o[q + 1]
@@ -2082,3 +2159,38 @@ extern "C" int uavhip_rollout_step(const uavhip_policy* policy, const uavhip_env
                        pol::EnvOut{(int)auto_reset, obs_out, reward, done, info});
     return check_launch("k_rollout_step");
 }
+
+extern "C" int uavhip_rollout_steps(const uavhip_policy* policy, const uavhip_env* env, float* obs, float* rowproj,
+                                    int32_t step, int32_t n, int32_t fill, uint64_t seed, uint64_t offset,
+                                    uint64_t offset_stride, const uint64_t* offset_dev, int8_t* actions, float* logp,
+                                    float* value, int32_t auto_reset, double* reward, uint8_t* done, double* info,
+                                    uavhip_stream_t stream) {
+    if (const int rc = validate_env(env, true)) return rc;
+    const int32_t B = env->E;
+    if (const int rc = check_policy("uavhip_rollout_steps", policy, obs, B)) return rc;
+    if (env->N > 64 || env->M > 64 || (env->flags & UAVHIP_ENV_OBS_F16) || !actions || !logp || !value || !reward ||
+        !done || n <= 0) {
+        set_error("uavhip_rollout_steps: N=%d, M=%d must be <= 64, observations f32, n=%d > 0 and "
+                  "actions/logp/value/reward/done non-NULL", env->N, env->M, n);
+        return UAVHIP_EINVAL;
+    }
+    if (!rowproj || step < 0 || (int64_t)B * pol::S * pol::kRowFloats >= (int64_t)1 << 31) {
+        set_error("uavhip_rollout_steps: NULL rowproj, step=%d < 0 or E=%d above the ring's 32-bit offsets", step, B);
+        return UAVHIP_EINVAL;
+    }
+    const int grid = (B + pol::SPW - 1) / pol::SPW;
+    const pol::RowIO rio{rowproj, (int)B, (int)step};
+    if (fill) {
+        hipLaunchKernelGGL(pol::k_policy_rows_fill, dim3(grid + 1), dim3(pol::NTHR), 0, (hipStream_t)stream,
+                           policy->weights, obs, rio);
+        if (const int rc = check_launch("k_policy_rows_fill")) return rc;
+    }
+    const long long stride = (long long)B * pol::S * pol::IN;
+    return pol::launch_rollout_steps(policy->weights, obs, (int)B, seed, offset, offset_dev, actions, logp, value, rio,
+                                     *env, pol::EnvOut{(int)auto_reset, obs + stride, reward, done, info},
+                                     pol::StepSeq{(int)n, stride, offset_stride}, (hipStream_t)stream);
+}
+#else   // the steps TU ends after k_rollout_steps
+}  // namespace pol
+}  // namespace uavhip
+#endif  // !UAVHIP_STEPS_TU

@@ -97,6 +97,9 @@ _SIGS = {
     "uavhip_rollout_step": (ctypes.c_int, [ctypes.POINTER(PolicyDesc), ctypes.POINTER(EnvDesc), _vp, _vp, _i32,
                                            _i32, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp, _vp, _i32, _vp,
                                            _vp, _vp, _vp, _vp]),
+    "uavhip_rollout_steps": (ctypes.c_int, [ctypes.POINTER(PolicyDesc), ctypes.POINTER(EnvDesc), _vp, _vp, _i32,
+                                            _i32, _i32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp,
+                                            _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     "uavhip_ppo_workspace_floats": (ctypes.c_int64, [_i32]),
     "uavhip_ppo_step": (ctypes.c_int, [ctypes.POINTER(PPODesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
     "uavhip_episode_stats": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _i32, _vp, _vp]),

@@ -191,6 +191,34 @@ class TransformerActorCritic(nn.Module):
                                       ptr(reward_out), ptr(done_out), ptr(info_out), stream_handle()),
               "uavhip_rollout_step")
 
+    def rollout_steps(self, env, obs, rowproj, step, fill, actions, logp, value, rewards, dones, info=None,
+                      auto_reset=True, seed=None, offset=0, offset_stride=0, offset_dev=None):
+        """uavhip_rollout_steps: n = actions.shape[0] consecutive rollout_step()s in one launch.
+        obs [n + 1][E][5][14] f32 (obs[0] = the current windows; obs[t + 1] receives step t's next
+        windows), actions / logp / value / rewards / dones [n][E], info [n][E][INFO_COUNT] or None;
+        step t samples with counters offset + t * offset_stride + b (+ *offset_dev)."""
+        if self._packed is None:
+            self.packed_weights()
+        E, dev = env.E, env.device
+        n = actions.shape[0] if actions.dim() == 2 else -1
+        if n <= 0:
+            raise ValueError("actions: need an int8 [n][E] buffer with n > 0")
+        check_out(obs, "obs", torch.float32, (n + 1, E), dev, (cfg.SEQ_LEN, cfg.STATE_DIM))
+        if rowproj.numel() < LIB.uavhip_policy_rowproj_floats(E) or rowproj.dtype != torch.float32 or \
+                not rowproj.is_contiguous():
+            raise ValueError("rowproj: need a contiguous float32 rowproj_buffer(E)")
+        for t, name, dt, tail in ((actions, "actions", torch.int8, ()), (logp, "logp", torch.float32, ()),
+                                  (value, "value", torch.float32, ()), (rewards, "rewards", torch.float64, ()),
+                                  (dones, "dones", torch.uint8, ()),
+                                  (info, "info", torch.float64, (_lib.INFO_COUNT,))):
+            check_out(t, name, dt, (n, E), dev, tail)
+        seed = self.sample_seed if seed is None else seed
+        check(LIB.uavhip_rollout_steps(self._desc, env.desc, ptr(obs), ptr(rowproj), int(step), int(n),
+                                       int(bool(fill)), ctypes.c_uint64(seed), ctypes.c_uint64(offset),
+                                       ctypes.c_uint64(offset_stride), ptr(offset_dev), ptr(actions), ptr(logp),
+                                       ptr(value), int(bool(auto_reset)), ptr(rewards), ptr(dones), ptr(info),
+                                       stream_handle()), "uavhip_rollout_steps")
+
     @torch.no_grad()
     def get_action(self, state):
         """transformer_net.py:96-122 -> (action [B] int64, log_prob [B], value [B, 1], entropy [B])."""

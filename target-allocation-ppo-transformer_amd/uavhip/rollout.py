@@ -43,13 +43,16 @@ class Trajectory:
 
 class RolloutEngine:
     def __init__(self, env, policy, horizon, want_info=True, bootstrap=True, seed=None, normalize=True, row_cache=True,
-                 fused_step=None, total_envs=None):
+                 fused_step=None, total_envs=None, persistent=None):
         """normalize=False leaves the advantages raw after GAE: a data-parallel caller normalises
         them with the moments of the whole data-parallel batch in normalize_global() (called by
         gather()) (ppo.py:94).
         row_cache=False runs every step on the full-window forward (uavhip_policy_forward).
         fused_step: one launch per step (uavhip_rollout_step: forward + sample + env step); default
         on when the row cache is on and N, M <= 64.
+        persistent: the T fused steps of an iteration as ONE launch (uavhip_rollout_steps: every
+        workgroup loops over the steps of its own envs); default on with fused_step and f32
+        observations. Bitwise the same trajectory as T uavhip_rollout_step launches.
         seed: Philox key of the action sampling (default: the policy's sample_seed, drawn from
         torch's RNG). Sampling counters are global env indices: step t of env e draws counter
         t * total_envs + env.env_base + e, so a rank's shard (VecUAVEnv(env_base=shard start),
@@ -77,6 +80,10 @@ class RolloutEngine:
         if fused_step and not can_fuse:
             raise ValueError("fused_step needs row_cache=True and N, M <= 64")
         self.fused_step = can_fuse if fused_step is None else bool(fused_step)
+        can_persist = self.fused_step and env.obs_dtype == torch.float32
+        if persistent and not can_persist:
+            raise ValueError("persistent needs fused_step and float32 observations")
+        self.persistent = can_persist if persistent is None else bool(persistent)
         self.graph = None
         self.policy_events = None   # [(start, end)] HIP events around each policy launch (optional)
         self.env_events = None
@@ -106,7 +113,16 @@ class RolloutEngine:
         tr, env = self.traj, self.env
         tr.obs[0].copy_(tr.obs[self.T])  # carry the previous iteration's last window
         eev = self.env_events
-        for t in range(self.T):
+        if self.persistent:  # the whole horizon in one launch; step t is the same as in the loop below
+            ev = self.policy_events
+            if ev is not None:
+                ev[0][0].record()
+            self.policy.rollout_steps(env, tr.obs, self.rowproj, 0, True, tr.actions, tr.logp, tr.values,
+                                      tr.rewards, tr.dones, tr.info, seed=self.seed, offset=self._offset(0),
+                                      offset_stride=self.total, offset_dev=self.counter)
+            if ev is not None:
+                ev[0][1].record()
+        for t in range(0 if self.persistent else self.T):
             if self.fused_step:
                 ev = self.policy_events
                 if ev is not None:
@@ -161,6 +177,10 @@ class RolloutEngine:
     def event_ms(self):
         """(policy launch ms list, env launch ms list) of the most recent iteration (fused steps:
         the policy list holds the T fused launches + the bootstrap forward, the env list is empty)."""
+        if self.persistent:  # one launch of T steps: its per-step average T times, then the bootstrap
+            one = self.policy_events[0][0].elapsed_time(self.policy_events[0][1]) / self.T
+            a, b = self.policy_events[self.T]
+            return [one] * self.T + ([a.elapsed_time(b)] if self.bootstrap else []), []
         pol = [a.elapsed_time(b) for a, b in self.policy_events]
         env = [] if self.fused_step else [a.elapsed_time(b) for a, b in self.env_events]
         return pol, env

@@ -396,9 +396,10 @@ def test_graph_ppo_update_matches_eager():
 @pytest.mark.parametrize("E,N,M,period", [(4096, 16, 32, 3), (1000, 8, 16, 2), (96, 64, 64, 0), (33, 4, 4, 5)])
 def test_fused_rollout_step_matches_two_launches(E, N, M, period):
     """uavhip_rollout_step (window-row forward + sampling + env step in one launch) against the
-    separate policy and env launches it replaces (each checked against the reference above), on
-    twin envs from the same seed: every trajectory output, the row cache and the whole env state
-    bitwise over two iterations with auto-reset and full resets flipping to refreshed scenes."""
+    separate policy and env launches it replaces (each checked against the reference above), and
+    uavhip_rollout_steps (all T steps of an iteration in one launch) against both, on triplet envs
+    from the same seed: every trajectory output, the row cache and the whole env state bitwise
+    over two iterations with auto-reset and full resets flipping to refreshed scenes."""
     from uavhip.policy import TransformerActorCritic
     from uavhip.rollout import RolloutEngine
     from uavhip.vec_env import VecUAVEnv
@@ -406,10 +407,10 @@ def test_fused_rollout_step_matches_two_launches(E, N, M, period):
     pol = TransformerActorCritic().cuda()
     T = 20
     res = []
-    for fused in (False, True):
+    for fused, persistent in ((False, False), (True, False), (True, True)):
         env = VecUAVEnv(E, N, M, 1, 1, seed=6, full_reset_period=period)
-        eng = RolloutEngine(env, pol, T, seed=5, fused_step=fused)
-        assert eng.fused_step == fused
+        eng = RolloutEngine(env, pol, T, seed=5, fused_step=fused, persistent=persistent)
+        assert eng.fused_step == fused and eng.persistent == persistent
         eng.start()
         out = []
         for _ in range(2):
@@ -423,8 +424,9 @@ def test_fused_rollout_step_matches_two_launches(E, N, M, period):
     torch.cuda.synchronize()
     if N * M <= 512:
         assert res[1][5].any()  # episodes ended inside the rollout
-    for i, (a, b) in enumerate(zip(*res)):
+    for i, (a, b, c) in enumerate(zip(*res)):
         assert torch.equal(a, b), i
+        assert torch.equal(a, c), i
 
 
 def test_fused_rollout_step_vs_oracle(traj_npz):
