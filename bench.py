@@ -457,6 +457,8 @@ def main():
                   else "k_policy_forward<false, true, false>" if eng.rowproj is not None
                   else "k_policy_forward<false, false, false>")
     pol_traffic, pol_src = profiled_traffic(pol_kernel)
+    if pol_traffic is not None and eng.persistent:  # one launch = T steps: per-step bytes
+        pol_traffic /= T
     env_traffic = None if eng.fused_step else profiled_traffic("k_env_step<1, false>")[0]
     if rank == 0:
         line = {
@@ -472,7 +474,9 @@ def main():
                        "full_reset_period": 200, "launch": mode},
             "roofline": {"kernel": pol_kernel, "bound": "mfma", "achieved": achieved_tf,
                          "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / MFMA_F32_PEAK_TFLOPS,
-                         "traffic": pol_traffic, "traffic_unit": "bytes/launch (PMC)", "traffic_source": pol_src,
+                         "traffic": pol_traffic,
+                         "traffic_unit": "bytes per step (PMC bytes per launch / T)" if eng.persistent else
+                         "bytes/launch (PMC)", "traffic_source": pol_src,
                          "avg_launch_ms": pol_ms, "flop_per_launch": POLICY_FLOP_PER_SAMPLE * E,
                          "flop_per_launch_source": "SURVEY.md 8(d): 2,446,208 FLOP/sample x E",
                          "executed_flop_per_launch": flop_exec * E, "executed_achieved": exec_tf,
