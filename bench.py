@@ -407,9 +407,23 @@ def main():
     # the last timed iteration's launches: T+1 policy and T env launches, or (fused steps) T fused
     # forward + env-step launches and the bootstrap forward (the same kernel without the env step)
     pol_list, env_list = eng.event_ms()
+    env_src = "fused launch minus the bootstrap forward launch"
     if eng.fused_step:
         pol_ms = float(np.mean(pol_list[:T]))
-        env_ms = max(pol_ms - float(pol_list[T]), 1e-6)  # the env step's share of a fused launch
+        per_step = pol_list
+        if eng.persistent:
+            # the env step's share of a step, as in the per-step mode: one extra eager iteration
+            # (after the timed region) of per-step fused launches, each against the bootstrap forward
+            # (the same kernel without the env step)
+            eng.persistent = False
+            try:
+                eng.collect(eager=True)
+                per_step, _ = eng.event_ms()
+            finally:
+                eng.persistent = True
+            env_src = ("per-step fused launch minus the bootstrap forward launch (one extra eager "
+                       "iteration of per-step launches after the timed region)")
+        env_ms = max(float(np.mean(per_step[:T])) - float(per_step[T]), 1e-6)  # the env step's share
     else:
         pol_ms = float(np.mean(pol_list))
         env_ms = float(np.mean(env_list))
@@ -493,7 +507,7 @@ def main():
                                     "(env step included)" if eng.fused_step else
                                     "HIP events around each of the T+1 launches of the last timed iteration")},
             "env_roofline": {"kernel": "env step inside the fused rollout launch" if eng.fused_step else "k_env_step",
-                             "timing": ("fused launch minus the bootstrap forward launch" if eng.fused_step else
+                             "timing": (env_src if eng.fused_step else
                                         "HIP events around each of the T env launches"),
                              "bound": "hbm", "achieved": env_gbs, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS, "avg_launch_ms": env_ms,
