@@ -418,6 +418,7 @@ def main():
             eng.persistent = False
             try:
                 eng.collect(eager=True)
+                torch.cuda.synchronize()
                 per_step, _ = eng.event_ms()
             finally:
                 eng.persistent = True

@@ -32,11 +32,12 @@ x[: B // 4, :2] = 0
 a = torch.empty(B, dtype=torch.int8, device="cuda")
 lp = torch.empty(B, device="cuda")
 v = torch.empty(B, device="cuda")
-fn = _lib.LIB.uavhip_policy_trace
+STEPS = os.environ.get("STEPS", "0") == "1"  # k_rollout_steps (one launch of 8 steps; last step's stamps)
+fn = _lib.LIB.uavhip_steps_trace if STEPS else _lib.LIB.uavhip_policy_trace
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
 ROWS = os.environ.get("ROWS", "0") == "1"  # window-row ring path (uavhip_policy_forward_rows)
-ENV = os.environ.get("ENV", "0") == "1"    # fused rollout step (uavhip_rollout_step), 16 x 32 envs
+ENV = os.environ.get("ENV", "0") == "1" or STEPS  # fused rollout step (uavhip_rollout_step), 16 x 32 envs
 kw = {}
 if ENV:  # the stamps of the last of 8 fused steps
     from uavhip import VecUAVEnv
@@ -46,7 +47,11 @@ if ENV:  # the stamps of the last of 8 fused steps
     eng.start()
     tr = eng.traj
     tr.obs[0].copy_(tr.obs[8])
-    for t in range(8):
+    if STEPS:
+        net.rollout_steps(env, tr.obs[:9].contiguous(), eng.rowproj, 0, True, tr.actions[:8], tr.logp[:8],
+                          tr.values[:8], tr.rewards[:8], tr.dones[:8], tr.info[:8], seed=0, offset=0,
+                          offset_stride=B, offset_dev=eng.counter)
+    for t in range(0 if STEPS else 8):
         net.rollout_step(env, tr.obs[t], eng.rowproj, t, t == 0, tr.actions[t], tr.logp[t], tr.values[t],
                          tr.obs[t + 1], tr.rewards[t], tr.dones[t], seed=0, offset=t * B, offset_dev=eng.counter)
 elif ROWS:

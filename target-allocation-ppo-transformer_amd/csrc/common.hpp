@@ -24,16 +24,13 @@ int validate_env(const uavhip_env* env, bool need_state);  // env.hip: descripto
 // ------------------------------------------------------------------ wave helpers
 constexpr int kWave = 64;
 
-// threadIdx.x. In the multi-step rollout TU (rollout_steps.hip, UAVHIP_TID_LAUNDER) every use goes
-// through an empty volatile asm: the step loop there would otherwise hoist every lane-index
-// expression of its body (loop invariant) out of the loop and spill them. (Measured against a
-// ballot-based laundering that keeps CSE inside basic blocks: the same to 0.4 %.)
+// threadIdx.x. In the multi-step rollout TU (rollout_steps.hip, UAVHIP_TID_LAUNDER) it is
+// threadIdx.x + an LDS word that holds 0: every __syncthreads (a fence) makes that load opaque, so
+// LICM cannot hoist the lane-index expressions of the step loop's body out of the loop (where they
+// would be spilled), while GVN still shares them between the barriers of one phase.
 #ifdef UAVHIP_TID_LAUNDER
-__device__ __forceinline__ unsigned tid_x() {
-    unsigned t = threadIdx.x;
-    asm volatile("" : "+v"(t));
-    return t;
-}
+__shared__ unsigned g_tid_zero;
+__device__ __forceinline__ unsigned tid_x() { return threadIdx.x + g_tid_zero; }
 #else
 __device__ __forceinline__ unsigned tid_x() { return threadIdx.x; }
 #endif

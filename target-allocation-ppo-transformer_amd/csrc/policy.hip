@@ -49,7 +49,11 @@ constexpr bool kExpNoStore = false;
 
 // Phase tracing (make TRACE=1 only): waves 0 and 4 of the first 256 workgroups stamp s_memtime at
 // the phase boundaries below; uavhip_policy_trace copies the stamps out. Off in the product build.
-#if defined(UAVHIP_POLICY_TRACE) && !defined(UAVHIP_STEPS_TU)
+#if defined(UAVHIP_POLICY_TRACE)
+#ifdef UAVHIP_STEPS_TU  // k_rollout_steps: its own buffer (the last step's stamps), uavhip_steps_trace
+#define g_ptrace g_strace
+#define g_btrace g_sbtrace
+#endif
 constexpr int kTraceSlots = 64;
 __device__ unsigned long long g_ptrace[256 * 2 * kTraceSlots];
 #define PTR(id)                                                                                  \
@@ -1230,42 +1234,56 @@ int launch_rollout_steps(const float* P, float* obs, int B, uint64_t seed, uint6
                          const uint64_t* offset_dev, int8_t* actions, float* logp, float* value, const RowIO& rio,
                          const uavhip_env& env, const EnvOut& eo, const StepSeq& seq, hipStream_t stream);
 #ifdef UAVHIP_STEPS_TU
-__global__ __launch_bounds__(NTHR) void k_rollout_steps(const float* __restrict__ P, const float* __restrict__ states,
-                                                        int B, uint64_t seed, uint64_t offset,
-                                                        const uint64_t* __restrict__ offset_dev,
-                                                        int8_t* __restrict__ action_out, float* __restrict__ logp_out,
-                                                        float* __restrict__ value_out, const RowIO rio,
-                                                        const uavhip_env env, const EnvOut eo, const StepSeq seq) {
+// All of the launch's arguments in one struct: the kernel's only parameter, so the kernarg
+// segment holds exactly this struct at offset 0.
+struct StepsArgs {
+    const float* P;
+    const float* states;
+    int B;
+    uint64_t seed, offset;
+    const uint64_t* offset_dev;
+    int8_t* action_out;
+    float *logp_out, *value_out;
+    RowIO rio;
+    uavhip_env env;
+    EnvOut eo;
+    StepSeq seq;
+};
+__global__ __launch_bounds__(NTHR) void k_rollout_steps(const StepsArgs args) {
     __shared__ __attribute__((aligned(16))) Smem sm;
-    if (tid_x() >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
-    for (int t = 0; t < seq.n; ++t) {
-        if (t) __syncthreads();  // the previous step's LDS scratch and global stores
-        // the weight pointer, the ring pointer and the block index laundered per step: otherwise the
-        // compiler hoists every loop-invariant address and load of the body out of the loop and
-        // spills them (the body needs all 256 VGPRs of its 2-waves-per-SIMD budget)
-        typedef const __attribute__((address_space(1))) float* gcf;  // keep the global address space
-        typedef __attribute__((address_space(1))) float* gf;
-        gcf Pg = (gcf)P;
-        gf rg = (gf)rio.rp;
+    if (threadIdx.x >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
+    if (threadIdx.x == 0) g_tid_zero = 0;
+    for (int t = 0; t < args.seq.n; ++t) {
+        __syncthreads();  // g_tid_zero; the previous step's LDS scratch and global stores
+        // Every argument is read through a kernarg pointer laundered per step, so the loads sit where
+        // the body uses them instead of being hoisted out of the loop and kept live (spilled) across
+        // the whole body; pointers loaded from the constant address space are still known global.
+        typedef const __attribute__((address_space(4))) StepsArgs* kargs;
+        kargs ka = (kargs)__builtin_amdgcn_kernarg_segment_ptr();
         int bx = blockIdx.x;
-        uint64_t sd = seed;  // (the Philox key schedule would be hoisted too: 20 SGPRs)
-        asm volatile("" : "+s"(Pg), "+s"(rg), "+s"(bx), "+s"(sd));
-        const float* Pt = (const float*)Pg;
-        float* rp = (float*)rg;
-        const size_t o = (size_t)t * B;
-        const RowIO r{rp, rio.B, rio.g + t};
-        const EnvOut e{eo.auto_reset, eo.obs + t * seq.obs_stride, eo.rew + o, eo.done + o,
-                       eo.info ? eo.info + o * UAVHIP_INFO_COUNT : nullptr};
-        policy_block<false, true, true>(sm, Pt, states + t * seq.obs_stride, B, nullptr, sd, offset + t * seq.off_stride,
-                                        offset_dev, action_out + o, logp_out + o, value_out + o, nullptr, nullptr,
-                                        TrainIO{}, r, env, e, bx);
+        asm volatile("" : "+s"(ka), "+s"(bx));
+        const StepsArgs& a = *(const StepsArgs*)ka;
+        const size_t o = (size_t)t * a.B;
+        const RowIO r{a.rio.rp, a.rio.B, a.rio.g + t};
+        const EnvOut e{a.eo.auto_reset, a.eo.obs + t * a.seq.obs_stride, a.eo.rew + o, a.eo.done + o,
+                       a.eo.info ? a.eo.info + o * UAVHIP_INFO_COUNT : nullptr};
+        policy_block<false, true, true>(sm, a.P, a.states + t * a.seq.obs_stride, a.B, nullptr, a.seed,
+                                        a.offset + t * a.seq.off_stride, a.offset_dev, a.action_out + o, a.logp_out + o,
+                                        a.value_out + o, nullptr, nullptr, TrainIO{}, r, a.env, e, bx);
     }
 }
+#ifdef UAVHIP_POLICY_TRACE
+extern "C" int uavhip_steps_trace(unsigned long long* out, int n) {  // the last step's k_rollout_steps stamps
+    const int total = 256 * 2 * kTraceSlots;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptrace), sizeof(unsigned long long) * (n < total ? n : total), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 int launch_rollout_steps(const float* P, float* obs, int B, uint64_t seed, uint64_t offset,
                          const uint64_t* offset_dev, int8_t* actions, float* logp, float* value, const RowIO& rio,
                          const uavhip_env& env, const EnvOut& eo, const StepSeq& seq, hipStream_t stream) {
-    hipLaunchKernelGGL(k_rollout_steps, dim3((B + SPW - 1) / SPW), dim3(NTHR), 0, stream, P, obs, B, seed, offset,
-                       offset_dev, actions, logp, value, rio, env, eo, seq);
+    hipLaunchKernelGGL(k_rollout_steps, dim3((B + SPW - 1) / SPW), dim3(NTHR), 0, stream,
+                       StepsArgs{P, obs, B, seed, offset, offset_dev, actions, logp, value, rio, env, eo, seq});
     return check_launch("k_rollout_steps");
 }
 #endif  // UAVHIP_STEPS_TU
