@@ -90,6 +90,24 @@ struct Smem {
     int mask[SPW * S];          // key padding mask (transformer_net.py:52-54)
 };
 
+// Lane index plumbing. In the multi-step rollout TU (rollout_steps.hip) every forward helper takes
+// the thread index as a leading parameter, laundered once per step by k_rollout_steps: the
+// compiler then cannot hoist the body's lane-index arithmetic out of the step loop (where it would
+// be spilled) and still shares it across the whole step. Elsewhere the macros are empty and the
+// helpers read threadIdx.x as before.
+#ifdef UAVHIP_STEPS_TU
+#define TID_F unsigned tid_,
+#define TID_C tid_,
+#define TID_K (unsigned)threadIdx.x,
+#define TIDX() tid_
+#else
+#define TID_F
+#define TID_C
+#define TID_K
+#define TIDX() tid_x()
+#endif
+#define LANE() ((int)(TIDX() & (kWave - 1)))
+
 // ------------------------------------------------------------------ GEMM building blocks
 constexpr int KB = 128 / 16;
 
@@ -104,12 +122,12 @@ struct APre {
 // `row / 16`, k-block kb is 1 KiB contiguous, lane l's float4 at 4 l. One wave instruction then
 // reads 1 KiB of consecutive lines instead of 16 half-lines of 16 rows (3.3x the per-CU L2 rate
 // measured on MI355X: scripts/micro/l2bw.hip).
-__device__ __forceinline__ const float* frag_ptr(const float* W, int ldw, int row, int kw0) {
-    return W + ((size_t)(row >> 4) * (ldw >> 4) + (kw0 >> 4)) * 256 + 4 * lane_id();
+__device__ __forceinline__ const float* frag_ptr(TID_F const float* W, int ldw, int row, int kw0) {
+    return W + ((size_t)(row >> 4) * (ldw >> 4) + (kw0 >> 4)) * 256 + 4 * LANE();
 }
 template <int D>
-__device__ __forceinline__ APre<D> prefetch(const float* __restrict__ W, int ldw, int row, int kw0) {
-    const float* wp = frag_ptr(W, ldw, row, kw0);
+__device__ __forceinline__ APre<D> prefetch(TID_F const float* __restrict__ W, int ldw, int row, int kw0) {
+    const float* wp = frag_ptr(TID_C W, ldw, row, kw0);
     APre<D> r;
 #pragma unroll
     for (int p = 0; p < D; ++p) r.a[p] = *reinterpret_cast<const f32x4*>(wp + 256 * p);
@@ -121,10 +139,10 @@ __device__ __forceinline__ APre<D> prefetch(const float* __restrict__ W, int ldw
 // activations from LDS as float4) are issued before the MFMAs of block i; blocks < D come from
 // `pre`. Both operands use the same k permutation (k = 16 i + 4 (lane >> 4) + j for MFMA j).
 template <int CT, int D, int NKB = KB>
-__device__ __forceinline__ void gemm_tile(f32x4 (&acc)[CT], const APre<D>& pre, const float* __restrict__ W, int ldw,
+__device__ __forceinline__ void gemm_tile(TID_F f32x4 (&acc)[CT], const APre<D>& pre, const float* __restrict__ W, int ldw,
                                           int row, int kw0, const float* X, int ldx, int xtok0) {
-    const int l = lane_id(), i16 = l & 15, g = l >> 4;
-    const float* wp = frag_ptr(W, ldw, row, kw0);
+    const int l = LANE(), i16 = l & 15, g = l >> 4;
+    const float* wp = frag_ptr(TID_C W, ldw, row, kw0);
     const float* xp[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) xp[ct] = X + (xtok0 + 16 * ct + i16) * ldx + 4 * g;
@@ -162,9 +180,9 @@ __device__ __forceinline__ void zero(f32x4 (&acc)[CT]) {
 
 // Y[ytok0 + 16 ct + j][ycol + i] = epi(acc + bias[brow + i]); lane (j, g) holds rows 4g..4g+3
 template <int CT, bool RELU>
-__device__ __forceinline__ void store_tile(const f32x4 (&acc)[CT], const f32x4 bb, float* Y, int ldy, int ycol,
+__device__ __forceinline__ void store_tile(TID_F const f32x4 (&acc)[CT], const f32x4 bb, float* Y, int ldy, int ycol,
                                            int ytok0) {
-    const int l = lane_id(), i16 = l & 15, g = l >> 4;
+    const int l = LANE(), i16 = l & 15, g = l >> 4;
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
         f32x4 v = acc[ct] + bb;
@@ -178,13 +196,13 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[CT], const f32x4 b
 // One 16-row output tile per wave: Y[tok][ycol + i] = epi(W[row + i] . X[tok]^T + b[row + i]).
 // The bias is loaded ahead of the k-loop, so the epilogue does not wait one more L2 round trip.
 template <int CT, bool RELU, int D>
-__device__ __forceinline__ void linear1(const APre<D>& pre, const float* W, int ldw, const float* bias, int row,
+__device__ __forceinline__ void linear1(TID_F const APre<D>& pre, const float* W, int ldw, const float* bias, int row,
                                         const float* X, int ldx, int xtok0, float* Y, int ldy, int ycol, int ytok0) {
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + row + 4 * (lane_id() >> 4));
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + row + 4 * (LANE() >> 4));
     f32x4 acc[CT];
     zero(acc);
-    gemm_tile<CT, D>(acc, pre, W, ldw, row, 0, X, ldx, xtok0);
-    store_tile<CT, RELU>(acc, bb, Y, ldy, ycol, ytok0);
+    gemm_tile<CT, D>(TID_C acc, pre, W, ldw, row, 0, X, ldx, xtok0);
+    store_tile<CT, RELU>(TID_C acc, bb, Y, ldy, ycol, ytok0);
 }
 
 // ------------------------------------------------------------------ VALU pieces
@@ -229,17 +247,17 @@ __device__ __forceinline__ int orow(int tok, int b0, bool compact) {
 struct LnPar {
     f32x4 bb, ww, lb;
 };
-__device__ __forceinline__ f32x4 ln_bias(const float* __restrict__ bias) {
-    return *reinterpret_cast<const f32x4*>(bias + 16 * (tid_x() >> 6) + 4 * (lane_id() >> 4));
+__device__ __forceinline__ f32x4 ln_bias(TID_F const float* __restrict__ bias) {
+    return *reinterpret_cast<const f32x4*>(bias + 16 * (TIDX() >> 6) + 4 * (LANE() >> 4));
 }
-__device__ __forceinline__ LnPar ln_load(const f32x4 bb, const float* __restrict__ w, const float* __restrict__ b) {
-    const int f0 = 16 * (tid_x() >> 6) + 4 * (lane_id() >> 4);
+__device__ __forceinline__ LnPar ln_load(TID_F const f32x4 bb, const float* __restrict__ w, const float* __restrict__ b) {
+    const int f0 = 16 * (TIDX() >> 6) + 4 * (LANE() >> 4);
     return LnPar{bb, *reinterpret_cast<const f32x4*>(w + f0), *reinterpret_cast<const f32x4*>(b + f0)};
 }
 template <int CT, bool TR = false>
-__device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[CT], const LnPar& lp, int ytok0,
+__device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (&acc)[CT], const LnPar& lp, int ytok0,
                                                    const LnOut& lo = LnOut{}) {
-    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
+    const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
     const int f0 = 16 * wv + 4 * g;
     const f32x4 bb = lp.bb;
     f32x4 v[CT];
@@ -310,13 +328,13 @@ __device__ __forceinline__ void residual_layernorm(Smem& sm, const f32x4 (&acc)[
 
 // Training mode: copy [tok][cols] rows from LDS (stride lds) to workspace rows (stride ldo, column
 // offset c0) for tokens [t0, TOK), all 512 threads, float4 granules.
-__device__ __forceinline__ void store_rows(const float* src, int lds, float* dst, int ldo, int c0, int ncols, int t0,
+__device__ __forceinline__ void store_rows(TID_F const float* src, int lds, float* dst, int ldo, int c0, int ncols, int t0,
                                            int b0, bool compact) {
 #ifdef UAVHIP_EXP_NOSTORE  // timing experiment only (make NOSTORE=1): activations not written
     return;
 #endif
     const int n4 = ncols / 4, items = (TOK - t0) * n4;
-    for (int i = tid_x(); i < items; i += NTHR) {
+    for (int i = TIDX(); i < items; i += NTHR) {
         const int tok = t0 + i / n4, q = i % n4;
         *reinterpret_cast<f32x4*>(dst + (size_t)orow(tok, b0, compact) * ldo + c0 + 4 * q) =
             *reinterpret_cast<const f32x4*>(src + tok * lds + 4 * q);
@@ -326,8 +344,8 @@ __device__ __forceinline__ void store_rows(const float* src, int lds, float* dst
 // Full-layer attention for heads [4c, 4c+4): one (sample, head, query group) task per 4 lanes,
 // each lane owning 4 of the 16 head dims; the task loads the 5 keys / values once for all its
 // queries (group 0: positions 0-2 on waves 0-3, group 1: positions 3-4 on waves 4-7).
-__device__ void attention_full(Smem& sm, int c) {
-    const int q4 = tid_x() & 3, task = tid_x() >> 2;
+__device__ void attention_full(TID_F Smem& sm, int c) {
+    const int q4 = TIDX() & 3, task = TIDX() >> 2;
     const int hh = task & 3, p = (task >> 2) & 15, grp = task >> 6;
     const int d0 = hh * HD + 4 * q4;
     f32x4 k[S], v[S];
@@ -372,10 +390,10 @@ __device__ void attention_full(Smem& sm, int c) {
 // the keys/values of all 5 positions; reads sm.big (Q|K|V of the chunk), writes sm.ctx.
 // One (query, head) task per 4 consecutive lanes, each lane owning 4 of the 16 head dims
 // (dot products reduced over the quad with two xor-shuffles).
-__device__ void attention_chunk(Smem& sm, int c, int qs0, int nqs) {
+__device__ void attention_chunk(TID_F Smem& sm, int c, int qs0, int nqs) {
     const int ntask = nqs * SPW * 4;
-    const int q4 = tid_x() & 3;
-    for (int task = tid_x() >> 2; task < ntask; task += NTHR / 4) {
+    const int q4 = TIDX() & 3;
+    for (int task = TIDX() >> 2; task < ntask; task += NTHR / 4) {
         const int hh = task & 3, rest = task >> 2, p = rest & 15, si = qs0 + (rest >> 4);
         const int ti = si * SPW + p;
         const int d0 = hh * HD + 4 * q4;
@@ -415,11 +433,11 @@ struct EmbPre {
     f32x4 a, bb, pp[S];
 };
 template <int trunk>
-__device__ __forceinline__ EmbPre embed_load(const float* __restrict__ P) {
+__device__ __forceinline__ EmbPre embed_load(TID_F const float* __restrict__ P) {
     const float* We = P + kOffs.o[trunk + EMB_W];
     const float* be = P + kOffs.o[trunk + EMB_B];
     const float* pos = P + kOffs.o[trunk + POS];
-    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
+    const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
     const int f = 16 * wv + i16;
     EmbPre r;
     r.a.x = 4 * g + 0 < IN ? We[f * IN + 4 * g + 0] : 0.f;
@@ -436,8 +454,8 @@ __device__ __forceinline__ EmbPre embed_load(const float* __restrict__ P) {
 // positions 0-3 -> sm.ctx (row projection fill).
 enum { kEmbH = 0, kEmbSplit = 1, kEmbRows = 2 };
 template <int trunk, bool TR = false, int MODE = kEmbH>
-__device__ void embed_apply(Smem& sm, const EmbPre& ep, float* e_out = nullptr, float* h_out = nullptr, int b0 = 0) {
-    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
+__device__ void embed_apply(TID_F Smem& sm, const EmbPre& ep, float* e_out = nullptr, float* h_out = nullptr, int b0 = 0) {
+    const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
     constexpr int NT = MODE == kEmbRows ? S - 1 : S;
     f32x4 acc[NT];
 #pragma unroll
@@ -464,9 +482,9 @@ __device__ void embed_apply(Smem& sm, const EmbPre& ep, float* e_out = nullptr, 
     }
 }
 template <int trunk, bool TR = false>
-__device__ void embed(Smem& sm, const float* __restrict__ P, float* e_out = nullptr, float* h_out = nullptr,
+__device__ void embed(TID_F Smem& sm, const float* __restrict__ P, float* e_out = nullptr, float* h_out = nullptr,
                       int b0 = 0) {
-    embed_apply<trunk, TR>(sm, embed_load<trunk>(P), e_out, h_out, b0);
+    embed_apply<trunk, TR>(TID_C sm, embed_load<trunk>(TID_C P), e_out, h_out, b0);
 }
 
 // K/V weight row of wave wv for chunk c: waves 0-3 K tiles, waves 4-7 V tiles
@@ -479,7 +497,7 @@ struct NoHook {
     __device__ void operator()() const {}
 };
 template <int trunk, int layer, bool last, bool TR, class F = NoHook>
-__device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P, const APre<depth<last ? 1 : S>()>& po,
+__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const APre<depth<last ? 1 : S>()>& po,
                            const TrainLayerIO& io, int b0, F pre_ln2 = F{});
 
 // One post-LN nn.TransformerEncoderLayer (relu FFN 256, 8 heads). last: prune to column tile 4.
@@ -487,14 +505,14 @@ __device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P
 // SIMD the same number of 16-row output tiles. `pkv` = the caller's prefetch of this layer's first
 // K/V weight blocks. Ends WITHOUT a final barrier: the caller prefetches its next weights, then syncs.
 template <int trunk, int layer, bool last, bool TR = false, class F = NoHook>
-__device__ __forceinline__ void encoder_layer(Smem& sm, const float* __restrict__ P, APre<2> pkv,
+__device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __restrict__ P, APre<2> pkv,
                               const TrainLayerIO& io = TrainLayerIO{}, int b0 = 0, F pre_ln2 = F{}) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
     PTR(tb);
     const float* Win = P + kOffs.o[layer_param(trunk, layer, INW)];
     const float* bin = P + kOffs.o[layer_param(trunk, layer, INB)];
     const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
-    const int wv = tid_x() >> 6;
+    const int wv = TIDX() >> 6;
     constexpr int CTQ = last ? 1 : S;              // column tiles that need Q / out / LN / FFN
     constexpr int DQ = depth<CTQ>();
     constexpr int qtok0 = last ? (S - 1) * SPW : 0;
@@ -503,19 +521,19 @@ __device__ __forceinline__ void encoder_layer(Smem& sm, const float* __restrict_
 #pragma unroll
     for (int c = 0; c < 2; ++c) {  // two chunks of 4 heads (LDS budget)
         APre<DQ> pq;
-        if (wv < 4) pq = prefetch<DQ>(Win, D, 64 * c + 16 * wv, 0);
+        if (wv < 4) pq = prefetch<DQ>(TID_C Win, D, 64 * c + 16 * wv, 0);
         // K (waves 0-3) / V (waves 4-7) of the chunk for all 80 tokens, one 16-row tile each
-        linear1<S, false, 2>(pkv, Win, D, bin, kv_row(wv, c), sm.h, LDH, 0, sm.big, LDB, (1 + (wv >> 2)) * 64 + 16 * (wv & 3), 0);
+        linear1<S, false, 2>(TID_C pkv, Win, D, bin, kv_row(wv, c), sm.h, LDH, 0, sm.big, LDB, (1 + (wv >> 2)) * 64 + 16 * (wv & 3), 0);
         // Q of the chunk for the query tokens, waves 0-3 (their SIMD partners did V)
-        if (wv < 4) linear1<CTQ, false, DQ>(pq, Win, D, bin, 64 * c + 16 * wv, sm.h, LDH, qtok0, sm.big, LDB, 16 * wv, qtok0);
-        if (c == 0) pkv = prefetch<2>(Win, D, kv_row(wv, 1), 0);
-        else po = prefetch<DQ>(Wo, D, 16 * wv, 0);
+        if (wv < 4) linear1<CTQ, false, DQ>(TID_C pq, Win, D, bin, 64 * c + 16 * wv, sm.h, LDH, qtok0, sm.big, LDB, 16 * wv, qtok0);
+        if (c == 0) pkv = prefetch<2>(TID_C Win, D, kv_row(wv, 1), 0);
+        else po = prefetch<DQ>(TID_C Wo, D, 16 * wv, 0);
         PTR(tb + 1 + 3 * c);
         __syncthreads();
         PTR(tb + 2 + 3 * c);
         if (TR && !kExpNoStore) {  // this chunk's Q (query tokens) / K / V -> qkv[row][part * 128 + 64 c + d]
             // by waves 4-7 (V tiles: less MFMA work than the K + Q waves sharing their SIMDs)
-            for (int i = (int)tid_x() - NTHR / 2; i < TOK * 48; i += NTHR / 2) {
+            for (int i = (int)TIDX() - NTHR / 2; i < TOK * 48; i += NTHR / 2) {
                 if (i < 0) break;
                 const int tok = i / 48, r = i - tok * 48, part = r >> 4, q = r & 15;
                 if (part == 0 && tok < qtok0) continue;
@@ -523,18 +541,18 @@ __device__ __forceinline__ void encoder_layer(Smem& sm, const float* __restrict_
                     *reinterpret_cast<const f32x4*>(sm.big + tok * LDB + part * 64 + 4 * q);
             }
         }
-        if (last) attention_chunk(sm, c, S - 1, 1);
-        else attention_full(sm, c);
+        if (last) attention_chunk(TID_C sm, c, S - 1, 1);
+        else attention_full(TID_C sm, c);
         __syncthreads();
         PTR(tb + 3 + 3 * c);
     }
-    layer_tail<trunk, layer, last, TR>(sm, P, po, io, b0, pre_ln2);
+    layer_tail<trunk, layer, last, TR>(TID_C sm, P, po, io, b0, pre_ln2);
 }
 
 // Out-projection + LN1 + FFN + LN2 of an encoder layer, after the attention output is in sm.ctx.
 // `po` = the caller's prefetch of the first out_proj weight blocks.
 template <int trunk, int layer, bool last, bool TR, class F>
-__device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P, const APre<depth<last ? 1 : S>()>& po,
+__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const APre<depth<last ? 1 : S>()>& po,
                            const TrainLayerIO& io, int b0, F pre_ln2) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
     const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
@@ -543,48 +561,48 @@ __device__ __forceinline__ void layer_tail(Smem& sm, const float* __restrict__ P
     const float* b1 = P + kOffs.o[layer_param(trunk, layer, L1B)];
     const float* W2 = P + kOffs.o[layer_param(trunk, layer, L2W)];
     const float* b2 = P + kOffs.o[layer_param(trunk, layer, L2B)];
-    const int wv = tid_x() >> 6;
+    const int wv = TIDX() >> 6;
     constexpr int CTQ = last ? 1 : S;
     constexpr int DQ = depth<CTQ>();
     constexpr int qtok0 = last ? (S - 1) * SPW : 0;
-    if (TR) store_rows(sm.ctx, LDH, io.o, D, 0, D, qtok0, b0, last);  // attention output
+    if (TR) store_rows(TID_C sm.ctx, LDH, io.o, D, 0, D, qtok0, b0, last);  // attention output
     // out projection, h = LN1(h + attn) in its epilogue
     APre<DQ> pf1a, pf1b;
     {
-        const f32x4 bo4 = ln_bias(bo);
+        const f32x4 bo4 = ln_bias(TID_C bo);
         f32x4 acc[CTQ];
         zero(acc);
-        gemm_tile<CTQ, DQ>(acc, po, Wo, D, 16 * wv, 0, sm.ctx, LDH, qtok0);
+        gemm_tile<CTQ, DQ>(TID_C acc, po, Wo, D, 16 * wv, 0, sm.ctx, LDH, qtok0);
         PTR(tb + 7);
-        const LnPar lp = ln_load(bo4, P + kOffs.o[layer_param(trunk, layer, N1W)], P + kOffs.o[layer_param(trunk, layer, N1B)]);
-        pf1a = prefetch<DQ>(W1, D, 16 * wv, 0);
-        pf1b = prefetch<DQ>(W1, D, 128 + 16 * wv, 0);
-        residual_layernorm<CTQ, TR>(sm, acc, lp, qtok0, LnOut{io.xhat1, io.h1, io.rstd1, b0, last});
+        const LnPar lp = ln_load(TID_C bo4, P + kOffs.o[layer_param(trunk, layer, N1W)], P + kOffs.o[layer_param(trunk, layer, N1B)]);
+        pf1a = prefetch<DQ>(TID_C W1, D, 16 * wv, 0);
+        pf1b = prefetch<DQ>(TID_C W1, D, 128 + 16 * wv, 0);
+        residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, io.h1, io.rstd1, b0, last});
     }
     PTR(tb + 8);
     __syncthreads();
     PTR(tb + 9);
     // FFN: hidden features 0-127 -> big, 128-255 -> ctx (both free now), then one K=256 GEMM
-    linear1<CTQ, true, DQ>(pf1a, W1, D, b1, 16 * wv, sm.h, LDH, qtok0, sm.big, LDF, 16 * wv, qtok0);
-    linear1<CTQ, true, DQ>(pf1b, W1, D, b1, 128 + 16 * wv, sm.h, LDH, qtok0, sm.ctx, LDF, 16 * wv, qtok0);
-    const APre<DQ> pf2a = prefetch<DQ>(W2, FF, 16 * wv, 0);
+    linear1<CTQ, true, DQ>(TID_C pf1a, W1, D, b1, 16 * wv, sm.h, LDH, qtok0, sm.big, LDF, 16 * wv, qtok0);
+    linear1<CTQ, true, DQ>(TID_C pf1b, W1, D, b1, 128 + 16 * wv, sm.h, LDH, qtok0, sm.ctx, LDF, 16 * wv, qtok0);
+    const APre<DQ> pf2a = prefetch<DQ>(TID_C W2, FF, 16 * wv, 0);
     PTR(tb + 10);
     __syncthreads();
     PTR(tb + 11);
-    const APre<DQ> pf2b = prefetch<DQ>(W2, FF, 16 * wv, 128);
+    const APre<DQ> pf2b = prefetch<DQ>(TID_C W2, FF, 16 * wv, 128);
     if (TR) {  // FFN hidden (post-ReLU): features 0-127 in big, 128-255 in ctx
-        store_rows(sm.big, LDF, io.u, FF, 0, D, qtok0, b0, last);
-        store_rows(sm.ctx, LDF, io.u, FF, D, D, qtok0, b0, last);
+        store_rows(TID_C sm.big, LDF, io.u, FF, 0, D, qtok0, b0, last);
+        store_rows(TID_C sm.ctx, LDF, io.u, FF, D, D, qtok0, b0, last);
     }
-    const f32x4 b24 = ln_bias(b2);
+    const f32x4 b24 = ln_bias(TID_C b2);
     f32x4 acc2[CTQ];
     zero(acc2);
-    gemm_tile<CTQ, DQ>(acc2, pf2a, W2, FF, 16 * wv, 0, sm.big, LDF, qtok0);
-    gemm_tile<CTQ, DQ>(acc2, pf2b, W2, FF, 16 * wv, 128, sm.ctx, LDF, qtok0);
+    gemm_tile<CTQ, DQ>(TID_C acc2, pf2a, W2, FF, 16 * wv, 0, sm.big, LDF, qtok0);
+    gemm_tile<CTQ, DQ>(TID_C acc2, pf2b, W2, FF, 16 * wv, 128, sm.ctx, LDF, qtok0);
     PTR(tb + 12);
-    const LnPar lp2 = ln_load(b24, P + kOffs.o[layer_param(trunk, layer, N2W)], P + kOffs.o[layer_param(trunk, layer, N2B)]);
+    const LnPar lp2 = ln_load(TID_C b24, P + kOffs.o[layer_param(trunk, layer, N2W)], P + kOffs.o[layer_param(trunk, layer, N2B)]);
     pre_ln2();
-    residual_layernorm<CTQ, TR>(sm, acc2, lp2, qtok0, LnOut{io.xhat2, io.h2, io.rstd2, b0, last});
+    residual_layernorm<CTQ, TR>(TID_C sm, acc2, lp2, qtok0, LnOut{io.xhat2, io.h2, io.rstd2, b0, last});
     PTR(tb + 14);
 }
 
@@ -618,47 +636,47 @@ struct RowPre {
 // Win pos_s of chunk c ([s][part * 64 + d], d < 64) -> registers; staged into sm.red (free during
 // the chunk loop) by ppos_stage.
 template <int trunk, int NP>
-__device__ __forceinline__ void ppos_load(RowPre<NP>& r, const RowIO& rio) {
+__device__ __forceinline__ void ppos_load(TID_F RowPre<NP>& r, const RowIO& rio) {
     const float* pp = rio.rp + (trunk == kActorTrunk ? 0 : S * 3 * D);
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int i = (tid_x() + NTHR * u) % (S * 192);  // (threads past 960 reload, unused)
+            const int i = (TIDX() + NTHR * u) % (S * 192);  // (threads past 960 reload, unused)
             const int s = i / 192, rr = i - 192 * s, part = rr >> 6, cc = rr & 63;
             r.pp[c][u] = pp[s * 3 * D + part * D + 64 * c + cc];
         }
 }
 template <int NP>
-__device__ __forceinline__ void ppos_stage(Smem& sm, const RowPre<NP>& r, int c) {
+__device__ __forceinline__ void ppos_stage(TID_F Smem& sm, const RowPre<NP>& r, int c) {
     float* pl = reinterpret_cast<float*>(sm.red);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        const int i = tid_x() + NTHR * u;
+        const int i = TIDX() + NTHR * u;
         if (i < S * 192) pl[i] = r.pp[c][u];
     }
 }
 // Item u of chunk c for this thread: float4 q of part `part` (of the NP cached parts) of token tok
 // (position tok >> 4 < 4, sample tok & 15); 16 consecutive lanes read one 256-byte row segment.
 template <int NP>
-__device__ __forceinline__ void ring_item(int u, int& part, int& tok) {
-    const int t2 = (tid_x() >> 4) + 32 * u;
+__device__ __forceinline__ void ring_item(TID_F int u, int& part, int& tok) {
+    const int t2 = (TIDX() >> 4) + 32 * u;
     part = t2 % NP;
     tok = t2 / NP;
 }
 // Chunk c of the ring rows (the critic loads chunk 1 only after its new-row GEMM: registers).
 template <int trunk, int NP>
-__device__ __forceinline__ void ring_load(RowPre<NP>& r, const Smem& sm, const RowIO& rio, int b0, int c) {
+__device__ __forceinline__ void ring_load(TID_F RowPre<NP>& r, const Smem& sm, const RowIO& rio, int b0, int c) {
     constexpr int ROFF = trunk == kActorTrunk ? 0 : 2 * D;
     const float* slots = rio.rp + kPposFloats;
-    const int q = tid_x() & 15;
+    const int q = TIDX() & 15;
     // predicates and offsets first (LDS reads of the mask), then the loads back to back: no LDS
     // read lands in a register of an outstanding load (that forces a vmcnt(0) drain)
     int off[2 * NP];
 #pragma unroll
     for (int u = 0; u < 2 * NP; ++u) {
         int part, tok;
-        ring_item<NP>(u, part, tok);
+        ring_item<NP>(TID_C u, part, tok);
         const int s = tok >> 4, p = tok & 15, b = b0 + p;
         const bool ok = b < rio.B && !sm.mask[p * S + s];
         const int slot = (rio.g + 1 + s) % 5;
@@ -679,10 +697,10 @@ __device__ __forceinline__ void ring_load(RowPre<NP>& r, const Smem& sm, const R
 // `issued()` runs right after the last weight load is issued: loads it issues queue behind the
 // GEMM's own (vmcnt retires in order), so none of the GEMM's waits cover them.
 template <int R, int D, class F>
-__device__ __forceinline__ void gemm_rows(f32x4 (&acc)[R], const APre<D> (&pre)[R], const float* __restrict__ W,
+__device__ __forceinline__ void gemm_rows(TID_F f32x4 (&acc)[R], const APre<D> (&pre)[R], const float* __restrict__ W,
                                           int ldw, const int (&row)[R], const float* X, int ldx, int xtok0,
                                           F&& issued) {
-    const int l = lane_id(), i16 = l & 15, g = l >> 4;
+    const int l = LANE(), i16 = l & 15, g = l >> 4;
     const float* xp = X + (xtok0 + i16) * ldx + 4 * g;
     f32x4 a[KB][R], b[KB];
 #pragma unroll
@@ -696,7 +714,7 @@ __device__ __forceinline__ void gemm_rows(f32x4 (&acc)[R], const APre<D> (&pre)[
         if (i + D < KB) {
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                a[i + D][r] = *reinterpret_cast<const f32x4*>(frag_ptr(W, ldw, row[r], 0) + 256 * (i + D));
+                a[i + D][r] = *reinterpret_cast<const f32x4*>(frag_ptr(TID_C W, ldw, row[r], 0) + 256 * (i + D));
             b[i + D] = *reinterpret_cast<const f32x4*>(xp + 16 * (i + D));
         }
         if (i == (D < KB ? KB - D - 1 : 0)) issued();
@@ -713,7 +731,7 @@ __device__ __forceinline__ void gemm_rows(f32x4 (&acc)[R], const APre<D> (&pre)[
 // 0-3 from `rp`; then attention and layer_tail as in encoder_layer. Expects sm.ctx rows 64-79 =
 // e of position 4 (embed_apply kEmbSplit), sm.red = Win pos_s of chunk 0 (ppos_stage).
 template <int trunk, int NP>
-__device__ __forceinline__ void encoder_layer_rows(Smem& sm, const float* __restrict__ P, const APre<kPwD> (&pw)[3], RowPre<NP>& rp,
+__device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* __restrict__ P, const APre<kPwD> (&pw)[3], RowPre<NP>& rp,
                                    const RowIO& rio, int b0) {
     constexpr bool last = trunk == kActorTrunk;  // the actor's layer 0 is its last (pruned) layer
     constexpr int P0 = 3 - NP, ROFF = trunk == kActorTrunk ? 0 : 2 * D;
@@ -722,12 +740,12 @@ __device__ __forceinline__ void encoder_layer_rows(Smem& sm, const float* __rest
     PTR(tb);
     const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
     const float* Wo = P + kOffs.o[layer_param(trunk, 0, OUTW)];
-    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
+    const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
     const int rows[3] = {16 * wv, D + 16 * wv, 2 * D + 16 * wv};
     f32x4 acc[3] = {};
-    gemm_rows<3, kPwD>(acc, pw, Win, D, rows, sm.ctx, LDH, (S - 1) * SPW, [&] {
-        ring_load<trunk>(rp, sm, rio, b0, 0);
-        if (trunk == kActorTrunk) ring_load<trunk>(rp, sm, rio, b0, 1);
+    gemm_rows<3, kPwD>(TID_C acc, pw, Win, D, rows, sm.ctx, LDH, (S - 1) * SPW, [&] {
+        ring_load<trunk>(TID_C rp, sm, rio, b0, 0);
+        if (trunk == kActorTrunk) ring_load<trunk>(TID_C rp, sm, rio, b0, 1);
     });
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[j] += rp.bias[j];  // u = Win e + b
@@ -736,10 +754,10 @@ __device__ __forceinline__ void encoder_layer_rows(Smem& sm, const float* __rest
 #pragma unroll
         for (int j = P0; j < 3; ++j) *reinterpret_cast<f32x4*>(dst + (j - P0) * D) = acc[j];
     }
-    if (trunk != kActorTrunk) ring_load<trunk>(rp, sm, rio, b0, 1);
+    if (trunk != kActorTrunk) ring_load<trunk>(TID_C rp, sm, rio, b0, 1);
     PTR(tb + 13);
     const float* pl = reinterpret_cast<const float*>(sm.red);
-    const int q = tid_x() & 15;
+    const int q = TIDX() & 15;
     APre<DQ> po;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -747,7 +765,7 @@ __device__ __forceinline__ void encoder_layer_rows(Smem& sm, const float* __rest
 #pragma unroll
         for (int u = 0; u < 2 * NP; ++u) {
             int part, tok;
-            ring_item<NP>(u, part, tok);
+            ring_item<NP>(TID_C u, part, tok);
             const int bp = part + P0, s = tok >> 4;
             *reinterpret_cast<f32x4*>(sm.big + tok * LDB + bp * 64 + 4 * q) =
                 rp.v[c][u] + *reinterpret_cast<const f32x4*>(pl + s * 192 + bp * 64 + 4 * q);
@@ -760,17 +778,17 @@ __device__ __forceinline__ void encoder_layer_rows(Smem& sm, const float* __rest
                     acc[j] + *reinterpret_cast<const f32x4*>(pl + (S - 1) * 192 + col);
             }
         }
-        if (c == 1) po = prefetch<DQ>(Wo, D, 16 * wv, 0);
+        if (c == 1) po = prefetch<DQ>(TID_C Wo, D, 16 * wv, 0);
         PTR(tb + 1 + 3 * c);
         __syncthreads();
         PTR(tb + 2 + 3 * c);
-        if (c == 0) ppos_stage(sm, rp, 1);  // sm.red is read again only by the chunk-1 assembly
-        if (last) attention_chunk(sm, c, S - 1, 1);
-        else attention_full(sm, c);
+        if (c == 0) ppos_stage(TID_C sm, rp, 1);  // sm.red is read again only by the chunk-1 assembly
+        if (last) attention_chunk(TID_C sm, c, S - 1, 1);
+        else attention_full(TID_C sm, c);
         __syncthreads();
         PTR(tb + 3 + 3 * c);
     }
-    layer_tail<trunk, 0, last, false>(sm, P, po, TrainLayerIO{}, b0);
+    layer_tail<trunk, 0, last, false>(TID_C sm, P, po, TrainLayerIO{}, b0);
 }
 
 // Everything layer 0 of a trunk needs before its new-row GEMM (which then issues the ring loads
@@ -778,37 +796,37 @@ __device__ __forceinline__ void encoder_layer_rows(Smem& sm, const float* __rest
 // and bias. Ends with the embedding in sm.h / sm.ctx and Win pos_s of
 // chunk 0 in sm.red, without a barrier.
 template <int trunk, int NP>
-__device__ __forceinline__ void rows_prologue(Smem& sm, const float* __restrict__ P, APre<kPwD> (&pw)[3],
+__device__ __forceinline__ void rows_prologue(TID_F Smem& sm, const float* __restrict__ P, APre<kPwD> (&pw)[3],
                                               RowPre<NP>& rp, const RowIO& rio, int b0) {
-    const int wv = tid_x() >> 6;
-    const EmbPre ep = embed_load<trunk>(P);
-    ppos_load<trunk>(rp, rio);
+    const int wv = TIDX() >> 6;
+    const EmbPre ep = embed_load<trunk>(TID_C P);
+    ppos_load<trunk>(TID_C rp, rio);
     const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) pw[j] = prefetch<kPwD>(Win, D, j * D + 16 * wv, 0);
+    for (int j = 0; j < 3; ++j) pw[j] = prefetch<kPwD>(TID_C Win, D, j * D + 16 * wv, 0);
     const float* bin = P + kOffs.o[layer_param(trunk, 0, INB)];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) rp.bias[j] = *reinterpret_cast<const f32x4*>(bin + j * D + 16 * wv + 4 * (lane_id() >> 4));
-    embed_apply<trunk, false, kEmbSplit>(sm, ep);
-    ppos_stage(sm, rp, 0);
+    for (int j = 0; j < 3; ++j) rp.bias[j] = *reinterpret_cast<const f32x4*>(bin + j * D + 16 * wv + 4 * (LANE() >> 4));
+    embed_apply<trunk, false, kEmbSplit>(TID_C sm, ep);
+    ppos_stage(TID_C sm, rp, 0);
 }
 
 // 128 -> 64 (MFMA, waves 0-3) -> relu -> nout (VALU) on the last-position rows (transformer_net.py:77-91)
 template <int head, int nout>
-__device__ void head_mlp(Smem& sm, const float* __restrict__ P, const APre<4>& pw, float* out) {
+__device__ void head_mlp(TID_F Smem& sm, const float* __restrict__ P, const APre<4>& pw, float* out) {
     const float* W0 = P + kOffs.o[head + 0];
     const float* b0 = P + kOffs.o[head + 1];
     const float* W2 = P + kOffs.o[head + 2];
     const float* b2 = P + kOffs.o[head + 3];
-    const int wv = tid_x() >> 6;
+    const int wv = TIDX() >> 6;
     // second layer: 16 lanes per (sample p, output a) = item p * nout + a, 4 hidden features per
     // lane; its weights and bias are loaded before the first layer's GEMM
     constexpr int kItems = SPW * nout;
-    const int item = tid_x() >> 4, k4 = tid_x() & 15;
+    const int item = TIDX() >> 4, k4 = TIDX() & 15;
     const int p = item / nout, a = (item - p * nout) % nout;  // in range for every thread
     const f32x4 w2 = *reinterpret_cast<const f32x4*>(W2 + a * HID + 4 * k4);
     const float bb2 = b2[a];
-    if (wv < HID / 16) linear1<1, true, 4>(pw, W0, D, b0, 16 * wv, sm.h, LDH, (S - 1) * SPW, sm.z, LDZ, 16 * wv, 0);
+    if (wv < HID / 16) linear1<1, true, 4>(TID_C pw, W0, D, b0, 16 * wv, sm.h, LDH, (S - 1) * SPW, sm.z, LDZ, 16 * wv, 0);
     __syncthreads();
     if (item < kItems) {  // wave-uniform: kItems * 16 is a multiple of 64
         const f32x4 z = *reinterpret_cast<const f32x4*>(sm.z + p * LDZ + 4 * k4);
@@ -845,9 +863,9 @@ __device__ __forceinline__ CatVals categorical(float l0, float l1) {
 }
 
 // Training mode: relu(head.0) rows of the 16 samples (sm.z) -> z [Bm][64].
-__device__ __forceinline__ void store_hidden(const Smem& sm, float* __restrict__ z, int b0) {
-    if (tid_x() < SPW * HID / 4) {
-        const int p = tid_x() / (HID / 4), q = tid_x() % (HID / 4);
+__device__ __forceinline__ void store_hidden(TID_F const Smem& sm, float* __restrict__ z, int b0) {
+    if (TIDX() < SPW * HID / 4) {
+        const int p = TIDX() / (HID / 4), q = TIDX() % (HID / 4);
         *reinterpret_cast<f32x4*>(z + (size_t)(b0 + p) * HID + 4 * q) =
             *reinterpret_cast<const f32x4*>(sm.z + p * LDZ + 4 * q);
     }
@@ -875,17 +893,17 @@ __device__ __forceinline__ void loss_terms(const float (&o)[5], float l0, float 
     t[3] = pad ? 0.f : -(c.lc0 * c.p0 + c.lc1 * c.p1);
 }
 // the block's sums in sample order (threads 0-3, one term each) -> fpart[blk][4]
-__device__ __forceinline__ void loss_block_sums(const float* red, float* fpart, int blk) {
-    if (tid_x() < 4) {
+__device__ __forceinline__ void loss_block_sums(TID_F const float* red, float* fpart, int blk) {
+    if (TIDX() < 4) {
         float acc = 0.f;
-        for (int i = 0; i < SPW; ++i) acc += red[4 * i + tid_x()];
-        fpart[blk * 4 + tid_x()] = acc;
+        for (int i = 0; i < SPW; ++i) acc += red[4 * i + TIDX()];
+        fpart[blk * 4 + TIDX()] = acc;
     }
 }
-__device__ void loss_partials(Smem& sm, const TrainIO& io, int b0) {
+__device__ void loss_partials(TID_F Smem& sm, const TrainIO& io, int b0) {
     float* red = sm.x;  // free after the embeddings
-    if (tid_x() < SPW) {
-        const int p = tid_x();
+    if (TIDX() < SPW) {
+        const int p = TIDX();
         float* o = io.smp + (size_t)(b0 + p) * 8;  // o[0..4] written by this thread at kernel start
         const float l0 = sm.logits[2 * p], l1 = sm.logits[2 * p + 1], v = sm.value[p];
         o[5] = l0;
@@ -895,20 +913,20 @@ __device__ void loss_partials(Smem& sm, const TrainIO& io, int b0) {
         loss_terms(oi, l0, l1, v, io.eps_clip, red + 4 * p);
     }
     __syncthreads();
-    loss_block_sums(red, io.fpart, b0 / SPW);
+    loss_block_sums(TID_C red, io.fpart, b0 / SPW);
 }
 #ifndef UAVHIP_STEPS_TU
 // Trunk split: the same partials once both trunks' workgroups have written smp[5..7].
 __global__ __launch_bounds__(64) void k_loss_partials(const TrainIO io) {
     __shared__ float red[4 * SPW];
     const int b0 = blockIdx.x * SPW;
-    if (tid_x() < SPW) {
-        const float* o = io.smp + (size_t)(b0 + tid_x()) * 8;
+    if (TIDX() < SPW) {
+        const float* o = io.smp + (size_t)(b0 + TIDX()) * 8;
         const float oi[5] = {o[0], o[1], o[2], o[3], o[4]};
-        loss_terms(oi, o[5], o[6], o[7], io.eps_clip, red + 4 * tid_x());
+        loss_terms(oi, o[5], o[6], o[7], io.eps_clip, red + 4 * TIDX());
     }
     __syncthreads();
-    loss_block_sums(red, io.fpart, blockIdx.x);
+    loss_block_sums(TID_C red, io.fpart, blockIdx.x);
 }
 #endif
 
@@ -926,7 +944,7 @@ struct EnvOut {
 // ENV: the env step of the sampled actions follows (needs ROWS; envs b0 .. b0 + 15).
 // One workgroup's whole forward (+ env step) of its 16 samples; the kernels below wrap it.
 template <bool TR, bool ROWS, bool ENV>
-__device__ __forceinline__ void policy_block(Smem& sm, const float* __restrict__ P, const float* __restrict__ states,
+__device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __restrict__ P, const float* __restrict__ states,
                                              int B, const int8_t* __restrict__ actions_in, uint64_t seed,
                                              uint64_t offset, const uint64_t* __restrict__ offset_dev,
                                              int8_t* __restrict__ action_out, float* __restrict__ logp_out,
@@ -953,11 +971,11 @@ __device__ __forceinline__ void policy_block(Smem& sm, const float* __restrict__
     [[maybe_unused]] APre<2> pkv_a, pkv_c;
     if constexpr (TR) {
         if (do_actor) {
-            ep_a = embed_load<kActorTrunk>(P);
-            pkv_a = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(tid_x() >> 6, 0), 0);
+            ep_a = embed_load<kActorTrunk>(TID_C P);
+            pkv_a = prefetch<2>(TID_C P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(TIDX() >> 6, 0), 0);
         } else {
-            ep_c = embed_load<kCriticTrunk>(P);
-            pkv_c = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(tid_x() >> 6, 0), 0);
+            ep_c = embed_load<kCriticTrunk>(TID_C P);
+            pkv_c = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(TIDX() >> 6, 0), 0);
         }
     }
     // windows -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch tail zero-filled);
@@ -969,26 +987,26 @@ __device__ __forceinline__ void policy_block(Smem& sm, const float* __restrict__
         size_t src[kEl];
 #pragma unroll
         for (int u = 0; u < kEl; ++u) {
-            const int i = tid_x() + u * NTHR, p = (i / LDX) % SPW;
+            const int i = TIDX() + u * NTHR, p = (i / LDX) % SPW;
             src[u] = (size_t)(b0 + p);
             if (TR && i < TOK * LDX) src[u] = (size_t)max(io.idx[b0 + p], 0);
         }
         size_t ssrc = 0;
         [[maybe_unused]] bool pad = false;
-        if (TR && tid_x() < SPW) {
-            const int r = io.idx[b0 + tid_x()];
+        if (TR && TIDX() < SPW) {
+            const int r = io.idx[b0 + TIDX()];
             pad = r < 0;
             ssrc = (size_t)max(r, 0);
         }
         float v[kEl];
 #pragma unroll
         for (int u = 0; u < kEl; ++u) {
-            const int i = tid_x() + u * NTHR;
+            const int i = TIDX() + u * NTHR;
             const int t = i / LDX, k = i - t * LDX, s = t / SPW, p = t - s * SPW;
             v[u] = (i < TOK * LDX && k < IN && b0 + p < B) ? states[(src[u] * S + s) * IN + k] : 0.f;
         }
         float ld[5];
-        if (TR && tid_x() < SPW) {  // per-sample loss inputs
+        if (TR && TIDX() < SPW) {  // per-sample loss inputs
             ld[0] = pad ? -1.f : (float)(io.act_in[ssrc] != 0);
             ld[1] = io.oldlp_in[ssrc];
             ld[2] = io.oldv_in[ssrc];
@@ -997,14 +1015,14 @@ __device__ __forceinline__ void policy_block(Smem& sm, const float* __restrict__
         }
 #pragma unroll
         for (int u = 0; u < kEl; ++u) {
-            const int i = tid_x() + u * NTHR;
+            const int i = TIDX() + u * NTHR;
             {  // key padding mask (all-zero rows, the last never masked) from the registers: the 16
                // lanes of a token row vote
                 static_assert(LDX == 16 && NTHR % LDX == 0, "one token row = 16 lanes");
                 const unsigned long long nz = __ballot(v[u] != 0.f);
                 if (i < TOK * LDX && (i % LDX) == 0) {
                     const int t = i / LDX, s = t / SPW, p = t - s * SPW;
-                    const bool m = (s < S - 1) && ((nz >> (lane_id() & 48)) & 0xFFFFull) == 0;
+                    const bool m = (s < S - 1) && ((nz >> (LANE() & 48)) & 0xFFFFull) == 0;
                     sm.mask[p * S + s] = m;
                     if (TR && do_actor) io.mask[(size_t)(b0 + p) * S + s] = m ? 1.f : 0.f;
                 }
@@ -1013,24 +1031,24 @@ __device__ __forceinline__ void policy_block(Smem& sm, const float* __restrict__
             sm.x[i] = v[u];
             if (TR && do_actor) io.xg[(size_t)trow(i / LDX, b0) * 16 + (i % LDX)] = v[u];
         }
-        if (TR && do_actor && tid_x() < SPW) {
-            float* o = io.smp + (size_t)(b0 + tid_x()) * 8;
+        if (TR && do_actor && TIDX() < SPW) {
+            float* o = io.smp + (size_t)(b0 + TIDX()) * 8;
             for (int c = 0; c < 5; ++c) o[c] = ld[c];
         }
     }
     __syncthreads();
     PTR(1);
-    const int wv = tid_x() >> 6;
+    const int wv = TIDX() >> 6;
     const float* headw_a = P + kOffs.o[kActorHead];
     const float* headw_c = P + kOffs.o[kCriticHead];
     // actor trunk (1 layer) + head
     if constexpr (ROWS) {
         APre<kPwD> pw[3];
         RowPre<2> rp;
-        rows_prologue<kActorTrunk>(sm, P, pw, rp, rio, b0);
+        rows_prologue<kActorTrunk>(TID_C sm, P, pw, rp, rio, b0);
         PTR(2);
         __syncthreads();
-        encoder_layer_rows<kActorTrunk>(sm, P, pw, rp, rio, b0);
+        encoder_layer_rows<kActorTrunk>(TID_C sm, P, pw, rp, rio, b0);
     }
     // training mode: the actor head's and the critic embedding's / first GEMM's operands are loaded
     // ahead of the actor's LN2 activation stores (layer_tail hook)
@@ -1040,30 +1058,30 @@ __device__ __forceinline__ void policy_block(Smem& sm, const float* __restrict__
             APre<2> pkv;
             if constexpr (TR) {
                 pkv = pkv_a;
-                embed_apply<kActorTrunk, TR>(sm, ep_a, io.e[0], io.h0[0], b0);
+                embed_apply<kActorTrunk, TR>(TID_C sm, ep_a, io.e[0], io.h0[0], b0);
             } else {
-                pkv = prefetch<2>(P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-                embed<kActorTrunk, TR>(sm, P, io.e[0], io.h0[0], b0);
+                pkv = prefetch<2>(TID_C P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+                embed<kActorTrunk, TR>(TID_C sm, P, io.e[0], io.h0[0], b0);
             }
             PTR(2);
             __syncthreads();
             if constexpr (TR) {
-                encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0, [&] {
-                    if (wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
+                encoder_layer<kActorTrunk, 0, true, TR>(TID_C sm, P, pkv, io.L[0], b0, [&] {
+                    if (wv < 4) ph = prefetch<4>(TID_C headw_a, D, 16 * wv, 0);
                     if (do_critic) {
-                        ep_c = embed_load<kCriticTrunk>(P);
-                        pkv_c = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+                        ep_c = embed_load<kCriticTrunk>(TID_C P);
+                        pkv_c = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
                     }
                 });
             } else {
-                encoder_layer<kActorTrunk, 0, true, TR>(sm, P, pkv, io.L[0], b0);
+                encoder_layer<kActorTrunk, 0, true, TR>(TID_C sm, P, pkv, io.L[0], b0);
             }
         }
-        if (!TR && wv < 4) ph = prefetch<4>(headw_a, D, 16 * wv, 0);
+        if (!TR && wv < 4) ph = prefetch<4>(TID_C headw_a, D, 16 * wv, 0);
         __syncthreads();
         PTR(3);
-        head_mlp<kActorHead, 2>(sm, P, ph, sm.logits);
-        if (TR) store_hidden(sm, io.z[0], b0);  // before the critic's LayerNorm partials reuse sm.z
+        head_mlp<kActorHead, 2>(TID_C sm, P, ph, sm.logits);
+        if (TR) store_hidden(TID_C sm, io.z[0], b0);  // before the critic's LayerNorm partials reuse sm.z
     }  // do_actor
     PTR(4);
     // fused env step (ENV): two envs per wave side by side, state loads issued before the critic head
@@ -1076,33 +1094,33 @@ __device__ __forceinline__ void policy_block(Smem& sm, const float* __restrict__
         if constexpr (ROWS) {
             APre<kPwD> pw[3];
             RowPre<3> rp;
-            rows_prologue<kCriticTrunk>(sm, P, pw, rp, rio, b0);
+            rows_prologue<kCriticTrunk>(TID_C sm, P, pw, rp, rio, b0);
             __syncthreads();
-            encoder_layer_rows<kCriticTrunk>(sm, P, pw, rp, rio, b0);
+            encoder_layer_rows<kCriticTrunk>(TID_C sm, P, pw, rp, rio, b0);
         }
         APre<2> pkv;
         if constexpr (!ROWS) {
             if constexpr (TR) {
-                embed_apply<kCriticTrunk, TR>(sm, ep_c, io.e[1], io.h0[1], b0);
+                embed_apply<kCriticTrunk, TR>(TID_C sm, ep_c, io.e[1], io.h0[1], b0);
                 __syncthreads();
-                encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv_c, io.L[1], b0, [&] {
-                    pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
+                encoder_layer<kCriticTrunk, 0, false, TR>(TID_C sm, P, pkv_c, io.L[1], b0, [&] {
+                    pkv = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
                 });
             } else {
-                APre<2> pkv0 = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-                embed<kCriticTrunk, TR>(sm, P, io.e[1], io.h0[1], b0);
+                APre<2> pkv0 = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+                embed<kCriticTrunk, TR>(TID_C sm, P, io.e[1], io.h0[1], b0);
                 __syncthreads();
-                encoder_layer<kCriticTrunk, 0, false, TR>(sm, P, pkv0, io.L[1], b0);
+                encoder_layer<kCriticTrunk, 0, false, TR>(TID_C sm, P, pkv0, io.L[1], b0);
             }
         }
-        if (!TR) pkv = prefetch<2>(P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
+        if (!TR) pkv = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
         __syncthreads();
         if constexpr (TR) {
-            encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0, [&] {
-                if (wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
+            encoder_layer<kCriticTrunk, 1, true, TR>(TID_C sm, P, pkv, io.L[2], b0, [&] {
+                if (wv < 4) ph = prefetch<4>(TID_C headw_c, D, 16 * wv, 0);
             });
         } else {
-            encoder_layer<kCriticTrunk, 1, true, TR>(sm, P, pkv, io.L[2], b0);
+            encoder_layer<kCriticTrunk, 1, true, TR>(TID_C sm, P, pkv, io.L[2], b0);
         }
         // the env step's state loads land while the critic head runs
         if constexpr (ENV) {
@@ -1111,30 +1129,30 @@ __device__ __forceinline__ void policy_block(Smem& sm, const float* __restrict__
                 envgrp::gload_issue(gR, gq, env, b0 + 2 * (int)(tid_env() >> 6) + (le >> 5), le & 31);
             }
         }
-        if (!TR && wv < 4) ph = prefetch<4>(headw_c, D, 16 * wv, 0);
+        if (!TR && wv < 4) ph = prefetch<4>(TID_C headw_c, D, 16 * wv, 0);
         __syncthreads();
         PTR(5);
-        head_mlp<kCriticHead, 1>(sm, P, ph, sm.value);
+        head_mlp<kCriticHead, 1>(TID_C sm, P, ph, sm.value);
         PTR(6);
-        if (TR) store_hidden(sm, io.z[1], b0);
+        if (TR) store_hidden(TID_C sm, io.z[1], b0);
     }  // do_critic
     if (TR) {
         if (role == 0) {
-            loss_partials(sm, io, b0);
-        } else if (tid_x() < SPW) {  // trunk split: this trunk's head outputs -> smp[5..7]
-            float* o = io.smp + (size_t)(b0 + tid_x()) * 8;
+            loss_partials(TID_C sm, io, b0);
+        } else if (TIDX() < SPW) {  // trunk split: this trunk's head outputs -> smp[5..7]
+            float* o = io.smp + (size_t)(b0 + TIDX()) * 8;
             if (do_actor) {
-                o[5] = sm.logits[2 * tid_x()];
-                o[6] = sm.logits[2 * tid_x() + 1];
+                o[5] = sm.logits[2 * TIDX()];
+                o[6] = sm.logits[2 * TIDX() + 1];
             } else {
-                o[7] = sm.value[tid_x()];
+                o[7] = sm.value[TIDX()];
             }
         }
         return;
     }
     // Categorical(softmax(logits)): sample / log_prob / entropy (transformer_net.py:118-122)
-    if (tid_x() < SPW) {
-        const int p = tid_x(), b = b0 + p;
+    if (TIDX() < SPW) {
+        const int p = TIDX(), b = b0 + p;
         if (b < B) {
             const float l0 = sm.logits[2 * p], l1 = sm.logits[2 * p + 1];
             const float m = fmaxf(l0, l1);
@@ -1212,7 +1230,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     __shared__ __attribute__((aligned(16))) Smem sm;
     // the younger half (waves 4-7, the arbitration loser of every phase) at priority 1
     if (tid_x() >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
-    policy_block<TR, ROWS, ENV>(sm, P, states, B, actions_in, seed, offset, offset_dev, action_out, logp_out, value_out,
+    policy_block<TR, ROWS, ENV>(TID_K sm, P, states, B, actions_in, seed, offset, offset_dev, action_out, logp_out, value_out,
                                 ent_out, logits_out, io, rio, env, eo, blockIdx.x);
 }
 
@@ -1261,13 +1279,14 @@ __global__ __launch_bounds__(NTHR) void k_rollout_steps(const StepsArgs args) {
         typedef const __attribute__((address_space(4))) StepsArgs* kargs;
         kargs ka = (kargs)__builtin_amdgcn_kernarg_segment_ptr();
         int bx = blockIdx.x;
-        asm volatile("" : "+s"(ka), "+s"(bx));
+        unsigned tid = threadIdx.x;  // the forward helpers' lane index, opaque per step (TID_F)
+        asm volatile("" : "+s"(ka), "+s"(bx), "+v"(tid));
         const StepsArgs& a = *(const StepsArgs*)ka;
         const size_t o = (size_t)t * a.B;
         const RowIO r{a.rio.rp, a.rio.B, a.rio.g + t};
         const EnvOut e{a.eo.auto_reset, a.eo.obs + t * a.seq.obs_stride, a.eo.rew + o, a.eo.done + o,
                        a.eo.info ? a.eo.info + o * UAVHIP_INFO_COUNT : nullptr};
-        policy_block<false, true, true>(sm, a.P, a.states + t * a.seq.obs_stride, a.B, nullptr, a.seed,
+        policy_block<false, true, true>(tid, sm, a.P, a.states + t * a.seq.obs_stride, a.B, nullptr, a.seed,
                                         a.offset + t * a.seq.off_stride, a.offset_dev, a.action_out + o, a.logp_out + o,
                                         a.value_out + o, nullptr, nullptr, TrainIO{}, r, a.env, e, bx);
     }
@@ -1288,6 +1307,7 @@ int launch_rollout_steps(const float* P, float* obs, int B, uint64_t seed, uint6
 }
 #endif  // UAVHIP_STEPS_TU
 
+#ifndef UAVHIP_STEPS_TU
 // Ring fill of one trunk: u rows of positions 0-3 of the workgroup's 16 windows -> slots
 // (g + 1 + s) mod 5, the same GEMM (k order, bias add) as the forward's new-row u.
 template <int trunk>
@@ -1339,7 +1359,6 @@ __device__ void rows_ppos_trunk(Smem& sm, const float* __restrict__ P, float* ou
     __syncthreads();
 }
 
-#ifndef UAVHIP_STEPS_TU
 // uavhip_policy_forward_rows with fill: rebuilds the ring rows of positions 0-3 of every window
 // (blocks < nb) and the Win pos_s table (block nb) from the current weights.
 __global__ __launch_bounds__(NTHR) void k_policy_rows_fill(const float* __restrict__ P,
