@@ -1281,6 +1281,7 @@ __global__ __launch_bounds__(NTHR) void k_rollout_steps(const StepsArgs args) {
         int bx = blockIdx.x;
         unsigned tid = threadIdx.x;  // the forward helpers' lane index, opaque per step (TID_F)
         asm volatile("" : "+s"(ka), "+s"(bx), "+v"(tid));
+        tid &= NTHR - 1;  // threadIdx.x's range, which the launder hides from the compiler
         const StepsArgs& a = *(const StepsArgs*)ka;
         const size_t o = (size_t)t * a.B;
         const RowIO r{a.rio.rp, a.rio.B, a.rio.g + t};
