@@ -351,7 +351,10 @@ enum uavhip_ppo_phase {
     UAVHIP_PPO_FORWARD = 1,
     UAVHIP_PPO_BACKWARD = 2,
     UAVHIP_PPO_UPDATE = 4,   /* clip_grad_norm_ on grads + Adam */
-    UAVHIP_PPO_FULL = 7
+    UAVHIP_PPO_FULL = 7,
+    UAVHIP_PPO_PACKED = 8    /* with FORWARD: the workspace's packed weight copies are current (an
+                                UPDATE on this workspace refreshes them with the new parameters,
+                                and nothing changed the parameters since): skip the repack */
 };
 
 /* Floats of workspace one step needs at `minibatch` samples. */

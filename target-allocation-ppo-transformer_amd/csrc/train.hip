@@ -177,6 +177,49 @@ constexpr int kSqBlocks = 256;
 
 // clip_grad_norm_(max_norm) + torch.optim.Adam (ppo.py:17-22 groups: actor params < critic trunk
 // offset use lr_actor, the rest lr_critic), elementwise over the flat buffers.
+// The updated float4 of flat params at f -> the forward's fragment-order copy (packed) and the
+// backward's transposed copies (packedT): k_policy_pack's mapping inverted, so an UPDATE leaves
+// both current and the next FORWARD may skip the pack launch (UAVHIP_PPO_PACKED).
+__device__ __forceinline__ void pack_scatter(float* __restrict__ packed, float* __restrict__ packedT, int f, f32x4 p) {
+    // parameter lo: kOffs.o[lo] <= f < kOffs.o[lo + 1]; searched once per wave (scalar), then
+    // advanced per lane (a wave's 256 floats cross at most a few small parameters)
+    const int f0 = __builtin_amdgcn_readfirstlane(f);
+    int lo = 0, hi = kNumParams;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (f0 >= kOffs.o[mid]) lo = mid;
+        else hi = mid;
+    }
+    while (lo + 1 < kNumParams && f >= kOffs.o[lo + 1]) ++lo;
+    const int local = f - kOffs.o[lo], K = kTileK[lo];
+    const bool tiled = K != 0 && local < kSizes[lo];
+    int dst = f;
+    if (tiled) {  // [R][K] weight: fragment index ((r/16 * K/16 + k/16) * 64 + r%16 + 16 (k%16)/4) * 4
+        const int r = local / K, k = local - r * K;
+        dst = kOffs.o[lo] + (((r >> 4) * (K >> 4) + (k >> 4)) * 64 + (r & 15) + 16 * ((k & 15) >> 2)) * 4;
+    }
+    *reinterpret_cast<f32x4*>(packed + dst) = p;
+    if (!tiled) return;
+    int base = -1, Rt = D, Kt = D;  // W stored [Kt][Rt]; packedT holds W^T in fragment order
+#pragma unroll
+    for (int li = 0; li < 3; ++li) {
+        const int trunk = li == 0 ? kActorTrunk : kCriticTrunk, layer = li == 2 ? 1 : 0;
+        if (lo == layer_param(trunk, layer, INW)) { base = li * kLayerT + kTWin; Rt = D; Kt = 3 * D; }
+        if (lo == layer_param(trunk, layer, OUTW)) { base = li * kLayerT + kTWo; Rt = D; Kt = D; }
+        if (lo == layer_param(trunk, layer, L1W)) { base = li * kLayerT + kTW1; Rt = D; Kt = FF; }
+        if (lo == layer_param(trunk, layer, L2W)) { base = li * kLayerT + kTW2; Rt = FF; Kt = D; }
+    }
+    if (lo == kActorHead) { base = kHeadT; Rt = D; Kt = HID; }
+    if (lo == kCriticHead) { base = kHeadT + D * HID; Rt = D; Kt = HID; }
+    if (base < 0) return;
+    const int k = local / Rt, r0 = local - k * Rt;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int r = r0 + j;
+        packedT[base + (((r >> 4) * (Kt >> 4) + (k >> 4)) * 64 + (r & 15) + 16 * ((k & 15) >> 2)) * 4 + (k & 3)] = p[j];
+    }
+}
+
 struct AdamArgs {
     float* params;
     float* grads;
@@ -186,6 +229,7 @@ struct AdamArgs {
     const float* sq_part;
     int n_sq, n, critic_begin;
     float lr_actor, lr_critic, beta1, beta2, eps, max_norm;
+    float *packed, *packedT;  // nullable: refreshed with the updated params (pack_scatter)
 };
 __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     __shared__ float red[4];
@@ -215,6 +259,7 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
         *reinterpret_cast<f32x4*>(a.m + i) = m;
         *reinterpret_cast<f32x4*>(a.v + i) = v;
         *reinterpret_cast<f32x4*>(a.params + i) = p;
+        if (a.packed) pack_scatter(a.packed, a.packedT, i, p);
     }
 }
 
@@ -347,7 +392,8 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
     }
     const int Bg = c->global_minibatch > 0 ? c->global_minibatch : c->minibatch;
     if (c->minibatch <= 0 || c->minibatch % 64 || Bg < c->minibatch || c->n_floats != kOffs.o[kNumParams] ||
-        phases <= 0 || phases > UAVHIP_PPO_FULL || (upd && (!c->adam_m || !c->adam_v || !c->adam_step))) {
+        (phases & UAVHIP_PPO_FULL) == 0 || (phases & ~(UAVHIP_PPO_FULL | UAVHIP_PPO_PACKED)) ||
+        (upd && (!c->adam_m || !c->adam_v || !c->adam_step))) {
         set_error("uavhip_ppo_step: minibatch %d (multiple of 64), global %d, n_floats %d (expected %d), phases %d",
                   c->minibatch, Bg, c->n_floats, kOffs.o[kNumParams], phases);
         return UAVHIP_EINVAL;
@@ -361,7 +407,7 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
     // The rollout's fused forward kernel (policy.hip) in training mode: one workgroup per 16
     // samples, every activation the backward needs written to the workspace.
     if (fwd) {
-        TR_CHECK(pol::policy_pack_train(c->params, p.packed, p.packedT, st));
+        if (!(phases & UAVHIP_PPO_PACKED)) TR_CHECK(pol::policy_pack_train(c->params, p.packed, p.packedT, st));
         pol::TrainIO io{};
         io.idx = idx;
         io.act_in = actions;
@@ -402,7 +448,7 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
         }
         AdamArgs aa{c->params, c->grads, c->adam_m, c->adam_v, c->adam_step, p.sq_part, n_sq, c->n_floats,
                     kOffs.o[kCriticTrunk], c->lr_actor, c->lr_critic, c->beta1, c->beta2, c->adam_eps,
-                    c->max_grad_norm};
+                    c->max_grad_norm, p.packed, p.packedT};
         hipLaunchKernelGGL(k_adam, dim3((c->n_floats / 4 + 255) / 256), dim3(256), 0, st, aa);
         TR_CHECK(check_launch("k_adam"));
     }

@@ -36,7 +36,7 @@ IST = dict(UAV_IDX=0, TARGET_IDX=1, N_COVERED=2, N_ASSIGNED=3, EPISODE=4, ERROR=
 IST_COUNT = 12
 DST = dict(R=0, J=1, ASG_COST=2, COV_VALUE=3, TOTAL_COST=4, TOTAL_VALUE=5, PD_CUR=6, SUM_PDMG=7, SUM_PFIN=8)
 DST_COUNT = 12
-PPO_FORWARD, PPO_BACKWARD, PPO_UPDATE, PPO_FULL = 1, 2, 4, 7
+PPO_FORWARD, PPO_BACKWARD, PPO_UPDATE, PPO_FULL, PPO_PACKED = 1, 2, 4, 7, 8
 EP = dict(ENV=0, EPISODE=1, STEPS=2, REWARD=3, Q0=4, J_SUM=5, MAX_COV=6, ACTION1=7, VALID=8, PDMG_SUM=9,
           PFINAL_SUM=10, ASSIGN_STEPS=11)
 EP_COUNT = 12

@@ -171,9 +171,16 @@ class FusedPPOTrainer:
         Bg, Bl = self.global_minibatch, self.minibatch
         return perm[b * Bg + self.rank * Bl:b * Bg + (self.rank + 1) * Bl]
 
-    def ddp_step(self, idx=None):
+    @staticmethod
+    def _packed(b):
+        """Phase bit of minibatch step b of an epoch: every step after the first skips the repack
+        of the weights (the previous step's UPDATE refreshed the packed copies, PPO_PACKED); the
+        first repacks, so parameters changed between epochs (load_state_dict, ...) are picked up."""
+        return _lib.PPO_PACKED if b > 0 else 0
+
+    def ddp_step(self, idx=None, packed=0):
         """One data-parallel optimizer step (see the module docstring)."""
-        self.step(_lib.PPO_FORWARD, idx)
+        self.step(_lib.PPO_FORWARD | packed, idx)
         self.allreduce(self.loss_sums)
         self.step(_lib.PPO_BACKWARD, idx)
         self.allreduce(self.grads)
@@ -195,7 +202,7 @@ class FusedPPOTrainer:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):  # one epoch: every minibatch step
             for b in range(steps):
-                self.step(_lib.PPO_FULL, self._rows(self.perm, b))
+                self.step(_lib.PPO_FULL | self._packed(b), self._rows(self.perm, b))
         torch.cuda.current_stream().wait_stream(s)
         self.graphs[steps] = g
         return g
@@ -232,9 +239,9 @@ class FusedPPOTrainer:
                 continue
             for b in range(steps):
                 if self.world == 1:
-                    self.step(_lib.PPO_FULL, self._rows(self.perm, b))
+                    self.step(_lib.PPO_FULL | self._packed(b), self._rows(self.perm, b))
                 else:
-                    self.ddp_step(self._rows(self.perm, b))
+                    self.ddp_step(self._rows(self.perm, b), self._packed(b))
                 cnt += 1
         self.policy._packed_key = None  # parameters changed under torch's version counters: repack
         if cnt == 0:
@@ -253,7 +260,7 @@ class FusedPPOTrainer:
             if r != self.minibatch:
                 self._resize(r)
             for b in range(steps):
-                self.ddp_step(rows[b])
+                self.ddp_step(rows[b], self._packed(b))
                 cnt += 1
         self.policy._packed_key = None
         if cnt == 0:

@@ -126,6 +126,38 @@ def test_fused_graph_replay_matches_direct_steps():
     torch.testing.assert_close(lp_fused, lp_torch.detach(), rtol=1e-5, atol=2e-6)
 
 
+@pytest.mark.parametrize("Bm", [64, 4096])
+def test_update_repack_skip_matches_repacking_every_step(Bm):
+    """UPDATE refreshes the packed weight copies (k_adam's pack_scatter: the forward's fragment
+    order and the backward's transposed copies), so steps 1.. of an epoch skip k_policy_pack
+    (PPO_PACKED); FusedPPOTrainer.run does that. Against steps that repack every time: bitwise the
+    same parameters, Adam state and loss statistics (a wrong packed or transposed copy would change
+    the forward or the gradients of the next step). Minibatch 64 runs trunk-split."""
+    from uavhip import _lib
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.train import FusedPPOTrainer
+    torch.manual_seed(9)
+    nets = [TransformerActorCritic().cuda()]
+    nets.append(copy.deepcopy(nets[0]))
+    bufs = _buffers(3 * Bm, seed=15)
+    t1, t0 = FusedPPOTrainer(nets[0], Bm), FusedPPOTrainer(nets[1], Bm)
+    for t in (t1, t0):
+        t.set_buffers(*bufs)
+    s1 = t1.run(epochs=2, generator=torch.Generator().manual_seed(4), use_graph=False)
+    perm = torch.cat([torch.randperm(3 * Bm, generator=g) for g in [torch.Generator().manual_seed(4)] for _ in range(2)])
+    t0.stats.zero_()
+    for ep in range(2):
+        t0.perm[:3 * Bm].copy_(perm[ep * 3 * Bm:(ep + 1) * 3 * Bm])
+        for b in range(3):
+            t0.step(_lib.PPO_FULL, t0._rows(t0.perm, b))
+    st = t0.stats.tolist()
+    s0 = (st[0] / st[3], st[1] / st[3], st[2] / st[3], 6)
+    assert s1 == s0
+    for a, b in ((t1.params, t0.params), (t1.adam_m, t0.adam_m), (t1.adam_v, t0.adam_v)):
+        d = int((a != b).sum())
+        assert d == 0, f"{d} elements differ"
+
+
 @pytest.mark.parametrize("Bm", [64, 1024])
 def test_trunk_split_matches_fused_trunks(Bm, monkeypatch):
     """Minibatches of <= 2048 samples run the actor's and the critic's trunks in separate workgroups

@@ -65,6 +65,10 @@ def test_ctypes_mirrors_header_enums():
     assert scalars[-2:] == ["seed", "env_base"] == [f[0] for f in _lib.EnvDesc._fields_[8:10]]
     assert _header_enum("uavhip_ist")["UAVHIP_IST_COUNT"] == _lib.IST_COUNT
     assert _header_enum("uavhip_dst")["UAVHIP_DST_COUNT"] == _lib.DST_COUNT
+    ph = _header_enum("uavhip_ppo_phase")
+    assert (ph["UAVHIP_PPO_FORWARD"], ph["UAVHIP_PPO_BACKWARD"], ph["UAVHIP_PPO_UPDATE"], ph["UAVHIP_PPO_FULL"],
+            ph["UAVHIP_PPO_PACKED"]) == (_lib.PPO_FORWARD, _lib.PPO_BACKWARD, _lib.PPO_UPDATE, _lib.PPO_FULL,
+                                         _lib.PPO_PACKED)
 
 
 def _struct_fields(name):
