@@ -172,6 +172,50 @@ __device__ __forceinline__ void gemm_tile(TID_F f32x4 (&acc)[CT], const APre<D>&
 }
 template <int CT> constexpr int depth() { return CT == 1 ? 4 : 2; }
 
+// The same GEMM over the 7 k-blocks kb0, kb0 + 1, ... (mod 8) -- every block but kb0 - 1, which
+// the caller accumulated from registers (the wave's own LayerNorm output features, layer_tail).
+template <int D>
+__device__ __forceinline__ APre<D> prefetch_rot(TID_F const float* __restrict__ W, int ldw, int row, int kb0) {
+    const float* wp = frag_ptr(TID_C W, ldw, row, 0);
+    APre<D> r;
+#pragma unroll
+    for (int p = 0; p < D; ++p) r.a[p] = *reinterpret_cast<const f32x4*>(wp + 256 * ((kb0 + p) & (KB - 1)));
+    return r;
+}
+template <int CT, int D>
+__device__ __forceinline__ void gemm_tile_rot(TID_F f32x4 (&acc)[CT], const APre<D>& pre, const float* __restrict__ W,
+                                              int ldw, int row, const float* X, int ldx, int xtok0, int kb0) {
+    constexpr int NKB = KB - 1;
+    const int l = LANE(), i16 = l & 15, g = l >> 4;
+    const float* wp = frag_ptr(TID_C W, ldw, row, 0);
+    const float* xp[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) xp[ct] = X + (xtok0 + 16 * ct + i16) * ldx + 4 * g;
+    f32x4 a[NKB], b[NKB][CT];
+#pragma unroll
+    for (int p = 0; p < D; ++p) {
+        const int kb = (kb0 + p) & (KB - 1);
+        a[p] = pre.a[p];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) b[p][ct] = *reinterpret_cast<const f32x4*>(xp[ct] + 16 * kb);
+    }
+#pragma unroll
+    for (int i = 0; i < NKB; ++i) {
+        if (i + D < NKB) {
+            const int kb = (kb0 + i + D) & (KB - 1);
+            a[i + D] = *reinterpret_cast<const f32x4*>(wp + 256 * kb);
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) b[i + D][ct] = *reinterpret_cast<const f32x4*>(xp[ct] + 16 * kb);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], b[i][ct][j], acc[ct], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 template <int CT>
 __device__ __forceinline__ void zero(f32x4 (&acc)[CT]) {
 #pragma unroll
@@ -256,7 +300,7 @@ __device__ __forceinline__ LnPar ln_load(TID_F const f32x4 bb, const float* __re
 }
 template <int CT, bool TR = false>
 __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (&acc)[CT], const LnPar& lp, int ytok0,
-                                                   const LnOut& lo = LnOut{}) {
+                                                   const LnOut& lo = LnOut{}, f32x4* outv = nullptr) {
     const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
     const int f0 = 16 * wv + 4 * g;
     const f32x4 bb = lp.bb;
@@ -317,6 +361,7 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
         const f32x4 xh = (v[ct] - mean) * rs;
         const f32x4 out = xh * ww + lb;
         *reinterpret_cast<f32x4*>(sm.h + tok * LDH + f0) = out;
+        if (outv) outv[ct] = out;
         if (TR && !kExpNoStore) {
             const size_t r = (size_t)orow(tok, lo.b0, lo.compact);
             *reinterpret_cast<f32x4*>(lo.x + r * D + f0) = xh;
@@ -568,6 +613,12 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
     if (TR) store_rows(TID_C sm.ctx, LDH, io.o, D, 0, D, qtok0, b0, last);  // attention output
     // out projection, h = LN1(h + attn) in its epilogue
     APre<DQ> pf1a, pf1b;
+    // inference, full layer: the wave's own 16 LayerNorm output features are FFN1's k-block wv, so
+    // its MFMAs over that block run from registers before the barrier (beside the other waves'
+    // LayerNorm work) and the GEMM after it covers the other 7 blocks (k-block order rotated)
+    constexpr bool kRot = !TR && CTQ == S;
+    [[maybe_unused]] APre<1> own_a, own_b;
+    [[maybe_unused]] f32x4 fa[CTQ], fb[CTQ];
     {
         const f32x4 bo4 = ln_bias(TID_C bo);
         f32x4 acc[CTQ];
@@ -575,16 +626,44 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
         gemm_tile<CTQ, DQ>(TID_C acc, po, Wo, D, 16 * wv, 0, sm.ctx, LDH, qtok0);
         PTR(tb + 7);
         const LnPar lp = ln_load(TID_C bo4, P + kOffs.o[layer_param(trunk, layer, N1W)], P + kOffs.o[layer_param(trunk, layer, N1B)]);
-        pf1a = prefetch<DQ>(TID_C W1, D, 16 * wv, 0);
-        pf1b = prefetch<DQ>(TID_C W1, D, 128 + 16 * wv, 0);
-        residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, io.h1, io.rstd1, b0, last});
+        if constexpr (kRot) {
+            own_a = prefetch_rot<1>(TID_C W1, D, 16 * wv, wv);
+            own_b = prefetch_rot<1>(TID_C W1, D, 128 + 16 * wv, wv);
+            pf1a = prefetch_rot<DQ>(TID_C W1, D, 16 * wv, wv + 1);
+            pf1b = prefetch_rot<DQ>(TID_C W1, D, 128 + 16 * wv, wv + 1);
+            f32x4 outv[CTQ];
+            residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, io.h1, io.rstd1, b0, last}, outv);
+            zero(fa);
+            zero(fb);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int ct = 0; ct < CTQ; ++ct) {
+                    fa[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(own_a.a[0][j], outv[ct][j], fa[ct], 0, 0, 0);
+                    fb[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(own_b.a[0][j], outv[ct][j], fb[ct], 0, 0, 0);
+                }
+        } else {
+            pf1a = prefetch<DQ>(TID_C W1, D, 16 * wv, 0);
+            pf1b = prefetch<DQ>(TID_C W1, D, 128 + 16 * wv, 0);
+            residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, io.h1, io.rstd1, b0, last});
+        }
     }
     PTR(tb + 8);
     __syncthreads();
     PTR(tb + 9);
     // FFN: hidden features 0-127 -> big, 128-255 -> ctx (both free now), then one K=256 GEMM
-    linear1<CTQ, true, DQ>(TID_C pf1a, W1, D, b1, 16 * wv, sm.h, LDH, qtok0, sm.big, LDF, 16 * wv, qtok0);
-    linear1<CTQ, true, DQ>(TID_C pf1b, W1, D, b1, 128 + 16 * wv, sm.h, LDH, qtok0, sm.ctx, LDF, 16 * wv, qtok0);
+    if constexpr (kRot) {
+        const int grow = 4 * (LANE() >> 4);
+        const f32x4 ba = *reinterpret_cast<const f32x4*>(b1 + 16 * wv + grow);
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(b1 + 128 + 16 * wv + grow);
+        gemm_tile_rot<CTQ, DQ>(TID_C fa, pf1a, W1, D, 16 * wv, sm.h, LDH, qtok0, wv + 1);
+        store_tile<CTQ, true>(TID_C fa, ba, sm.big, LDF, 16 * wv, qtok0);
+        gemm_tile_rot<CTQ, DQ>(TID_C fb, pf1b, W1, D, 128 + 16 * wv, sm.h, LDH, qtok0, wv + 1);
+        store_tile<CTQ, true>(TID_C fb, bb, sm.ctx, LDF, 16 * wv, qtok0);
+    } else {
+        linear1<CTQ, true, DQ>(TID_C pf1a, W1, D, b1, 16 * wv, sm.h, LDH, qtok0, sm.big, LDF, 16 * wv, qtok0);
+        linear1<CTQ, true, DQ>(TID_C pf1b, W1, D, b1, 128 + 16 * wv, sm.h, LDH, qtok0, sm.ctx, LDF, 16 * wv, qtok0);
+    }
     const APre<DQ> pf2a = prefetch<DQ>(TID_C W2, FF, 16 * wv, 0);
     PTR(tb + 10);
     __syncthreads();
