@@ -3,17 +3,20 @@
 4096 envs x 16 UAVs x 32 targets, transformer policy + env step on each MI355X).
 
 One timed "step" = one rollout iteration per rank: T (=64) x {fused policy forward (fp32 MFMA) ->
-on-device sample -> fused env step (fp64)} over E envs, a bootstrap value pass, GAE + advantage
-normalisation, and with N > 1 GPUs the RCCL all-gather of the trajectories.
+on-device sample -> fused env step (fp64)} over E envs -- all T steps in ONE k_rollout_steps launch
+(--per-step-launch: one launch per step) -- a bootstrap value pass, GAE + advantage normalisation,
+and with N > 1 GPUs the RCCL all-gather of the trajectories.
 value = E * T * K * N / max-over-ranks wall time. Inputs (scenes, windows) are resident in HBM.
 
 Also reported (same JSON line):
-  roofline      dominant kernel = k_policy_forward, MFMA fp32 peak; achieved = ALGORITHMIC FLOP per
-                launch (2,446,208 FLOP/sample, the last-token-pruned forward of one
-                window) x E / its average HIP-event duration over the timed region. The rollout's
+  roofline      dominant kernel = k_rollout_steps (per-step figures: its launch / T), MFMA fp32 peak;
+                achieved = ALGORITHMIC FLOP per step (2,446,208 FLOP/sample, the
+                last-token-pruned forward of one window) x E / its HIP-event duration per step in the
+                last timed iteration; traffic = PMC bytes per step (profiles/rNN_pmc.json). The rollout's
                 window-row ring reuses layer-0 Q/K/V of rows 0-3 from earlier steps, so it EXECUTES
                 1,790,848 FLOP/sample; that rate is reported beside it (executed_*)
-  env_roofline  k_env_step against HBM, algorithmic 24*M + 490 B per env-step
+  env_roofline  the env step's share of a fused step (per-step fused launch minus the same forward
+                without it) against HBM, algorithmic 24*M + 490 B per env-step
   env_fused     env-only multi-step launches, T = 256 (K2r omega = 0 replay / K2): BASELINE configs[1]
                 (1024 envs x 8 x 16) and the headline shape, env-steps/s and algorithmic GB/s; and
                 BASELINE configs[4]'s per-GPU shard (8192 envs x 64 x 128, fp16 obs, T = 64)
