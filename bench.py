@@ -15,8 +15,11 @@ Also reported (same JSON line):
                 last timed iteration; traffic = PMC bytes per step (profiles/rNN_pmc.json). The rollout's
                 window-row ring reuses layer-0 Q/K/V of rows 0-3 from earlier steps, so it EXECUTES
                 1,790,848 FLOP/sample; that rate is reported beside it (executed_*)
-  env_roofline  the env step's share of a fused step (per-step fused launch minus the same forward
-                without it) against HBM, algorithmic 24*M + 490 B per env-step
+  env_roofline  the env step inside k_rollout_steps against HBM, algorithmic 24*M + 490 B per
+                env-step: its time = the per-step time above x its share of the step's
+                cycles (s_memtime phase stamps of the TRACE build, scripts/env_phase.py, run as a
+                child process); traffic = PMC bytes per step it adds (product build minus a build
+                with the env step compiled out, profiles/rNN_env_share.json)
   env_fused     env-only multi-step launches, T = 256 (K2r omega = 0 replay / K2): BASELINE configs[1]
                 (1024 envs x 8 x 16) and the headline shape, env-steps/s and algorithmic GB/s; and
                 BASELINE configs[4]'s per-GPU shard (8192 envs x 64 x 128, fp16 obs, T = 64)
@@ -70,6 +73,38 @@ def profiled_traffic(kernel):
         if k.replace("uavhip::pol::", "").replace("uavhip::", "") == kernel and "hbm_bytes_per_launch" in v:
             return v["hbm_bytes_per_launch"], os.path.basename(files[-1])
     return None, None
+
+
+def env_phase_share(args):
+    """The env step's share of a k_rollout_steps step from the TRACE build's phase stamps
+    (scripts/env_phase.py in a child process: its own GPU context, the product library stays
+    loaded here). None (with the reason) when the TRACE build is absent or the probe fails."""
+    import subprocess
+    lib = os.path.join(ROOT, "target-allocation-ppo-transformer_amd", "uavhip", "libuavhip_trace.so")
+    if not os.path.exists(lib):
+        return None, "no TRACE build (libuavhip_trace.so)"
+    env = dict(os.environ, UAVHIP_LIB=lib, E=str(args.envs), N=str(args.uavs), M=str(args.targets),
+               T=str(args.horizon))
+    try:
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "env_phase.py")], env=env,
+                             capture_output=True, text=True, timeout=300)
+        if out.returncode != 0:
+            return None, "env_phase.py failed: " + out.stderr[-300:]
+        return json.loads(out.stdout.strip().splitlines()[-1]), None
+    except Exception as exc:
+        return None, repr(exc)
+
+
+def env_share_traffic():
+    """HBM bytes per env step inside k_rollout_steps (per step of the launch, all E envs) from the
+    newest profiles/rNN_env_share.json (scripts/profile_env_share.sh: PMC FETCH/WRITE passes of the
+    product build and of a build with the env step compiled out; the difference)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_env_share.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d.get("env_bytes_per_step"), os.path.basename(files[-1])
 
 
 def env_counters(kernel):
@@ -410,31 +445,24 @@ def main():
     # the last timed iteration's launches: T+1 policy and T env launches, or (fused steps) T fused
     # forward + env-step launches and the bootstrap forward (the same kernel without the env step)
     pol_list, env_list = eng.event_ms()
-    env_src = "fused launch minus the bootstrap forward launch"
+    env_phase = env_err = None
     if eng.fused_step:
         pol_ms = float(np.mean(pol_list[:T]))
-        per_step = pol_list
-        if eng.persistent:
-            # the env step's share of a step, as in the per-step mode: one extra eager iteration
-            # (after the timed region) of per-step fused launches, each against the bootstrap forward
-            # (the same kernel without the env step)
-            eng.persistent = False
-            try:
-                eng.collect(eager=True)
-                torch.cuda.synchronize()
-                per_step, _ = eng.event_ms()
-            finally:
-                eng.persistent = True
-            env_src = ("per-step fused launch minus the bootstrap forward launch (one extra eager "
-                       "iteration of per-step launches after the timed region)")
-        env_ms = max(float(np.mean(per_step[:T])) - float(per_step[T]), 1e-6)  # the env step's share
+        env_ms = None
+        if eng.persistent and rank == 0 and world == 1:
+            # the env step's share of the step's cycles (TRACE build phase stamps, child process)
+            env_phase, env_err = env_phase_share(args)
+            if env_phase is not None:
+                env_ms = env_phase["share"] * pol_ms
+        elif not eng.persistent:  # per-step launches: the fused launch minus the bootstrap forward
+            env_ms = max(float(np.mean(pol_list[:T])) - float(pol_list[T]), 1e-6)
     else:
         pol_ms = float(np.mean(pol_list))
         env_ms = float(np.mean(env_list))
     flop_exec = ROWS_FLOP_PER_SAMPLE if eng.rowproj is not None else POLICY_FLOP_PER_SAMPLE
     achieved_tf = POLICY_FLOP_PER_SAMPLE * E / (pol_ms * 1e-3) / 1e12
     exec_tf = flop_exec * E / (pol_ms * 1e-3) / 1e12
-    env_gbs = env_bytes_per_step(args.targets) * E / (env_ms * 1e-3) / 1e9
+    env_gbs = None if env_ms is None else env_bytes_per_step(args.targets) * E / (env_ms * 1e-3) / 1e9
 
     env_fused = stress = None
     if rank == 0 and world == 1 and not args.no_env_fused:
@@ -477,7 +505,12 @@ def main():
     pol_traffic, pol_src = profiled_traffic(pol_kernel)
     if pol_traffic is not None and eng.persistent:  # one launch = T steps: per-step bytes
         pol_traffic /= T
-    env_traffic = None if eng.fused_step else profiled_traffic("k_env_step<1, false>")[0]
+    if eng.persistent:
+        env_traffic, env_traffic_src = env_share_traffic()
+    elif eng.fused_step:
+        env_traffic, env_traffic_src = None, None
+    else:
+        env_traffic, env_traffic_src = profiled_traffic("k_env_step<1, false>")
     if rank == 0:
         line = {
             "metric": "env-steps/sec (whole node), full PPO rollout, 4096 envs x 16 UAV x 32 tgt per GPU",
@@ -510,13 +543,23 @@ def main():
                                     "HIP events around each of the T fused launches of the last timed iteration "
                                     "(env step included)" if eng.fused_step else
                                     "HIP events around each of the T+1 launches of the last timed iteration")},
-            "env_roofline": {"kernel": "env step inside the fused rollout launch" if eng.fused_step else "k_env_step",
-                             "timing": (env_src if eng.fused_step else
-                                        "HIP events around each of the T env launches"),
-                             "bound": "hbm", "achieved": env_gbs, "peak": HBM_PEAK_GBS,
-                             "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS, "avg_launch_ms": env_ms,
-                             "traffic": env_traffic,
-                             "bytes_per_env_step": env_bytes_per_step(args.targets)},
+            "env_roofline": None if env_ms is None else {
+                "kernel": "env step inside k_rollout_steps" if eng.persistent else
+                "env step inside the fused rollout launch" if eng.fused_step else "k_env_step",
+                "timing": ("k_rollout_steps per-step time above (HIP events) x the env step's share of the "
+                           "step's cycles: s_memtime phase stamps of the TRACE build, sample -> env.store over "
+                           "start -> env.store, median of 256 workgroups, last step of a 64-step launch "
+                           "(scripts/env_phase.py, child process)" if eng.persistent else
+                           "per-step fused launch minus the bootstrap forward launch" if eng.fused_step else
+                           "HIP events around each of the T env launches"),
+                "share": None if env_phase is None else env_phase["share"],
+                "share_p10_p90": None if env_phase is None else [env_phase["share_p10"], env_phase["share_p90"]],
+                "phase_cycles": None if env_phase is None else env_phase["phases"],
+                "bound": "hbm", "achieved": env_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": env_gbs / HBM_PEAK_GBS, "avg_launch_ms": env_ms,
+                "traffic": env_traffic, "traffic_unit": "HBM bytes per step of all E envs (PMC)",
+                "traffic_source": env_traffic_src, "bytes_per_env_step": env_bytes_per_step(args.targets)},
+            "env_roofline_error": env_err,
             "env_fused": env_fused,
             "score_pairs": stress,
             "ppo_samples_per_s": ppo,

@@ -42,7 +42,14 @@ typedef void* uavhip_stream_t; /* hipStream_t */
                                       (round-to-nearest-even of the f32 window; BASELINE config 4)
                                       instead of f32; the env's own window stays f32          */
 #define UAVHIP_ENV_NO_REPLAY 4     /* multi-step launches: never use the omega = 0 replay kernel
-                                      (K2r, env_replay.hpp), always the step-by-step K2 / K2g  */
+                                      (K2r, env_replay.hpp), always the step-by-step K2 / K2g.
+                                      K2r assumes every tentative assign is accepted, which
+                                      omega = 0 guarantees only when every target value is >= 0
+                                      (J can then never drop, uav_env.py:317-338; pair
+                                      probabilities are clipped to [0, 1] by construction). The
+                                      generators never make a negative value; a caller loading
+                                      host scenes that may must set this flag (VecUAVEnv.
+                                      load_scenes does it).                                      */
 
 enum uavhip_status {
     UAVHIP_OK = 0,

@@ -1,0 +1,37 @@
+"""A bare rollout for profiling: ITERS eager iterations of RolloutEngine at the bench's shape (one
+k_rollout_steps launch of T steps each, + bootstrap forward + GAE + scene refresh), nothing else.
+UAVHIP_LIB selects the library build (product / TRACE / NOENV). Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "target-allocation-ppo-transformer_amd"))
+import torch  # noqa: E402
+
+
+def main():
+    E, N, M, T = (int(os.environ.get(k, d)) for k, d in (("E", 4096), ("N", 16), ("M", 32), ("T", 64)))
+    iters = int(os.environ.get("ITERS", "8"))
+    from uavhip import _lib
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.rollout import RolloutEngine
+    from uavhip.vec_env import VecUAVEnv
+    torch.manual_seed(0)
+    net = TransformerActorCritic().cuda()
+    env = VecUAVEnv(E, N, M, 1, 1, seed=1, full_reset_period=200)
+    eng = RolloutEngine(env, net, horizon=T, persistent=True)
+    eng.start()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        eng.collect(eager=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), "iters": iters, "ms_per_iter": dt / iters * 1e3,
+                      "shape": [E, N, M, T]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

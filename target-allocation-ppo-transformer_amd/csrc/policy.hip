@@ -46,6 +46,13 @@ constexpr bool kExpNoStore = true;
 #else
 constexpr bool kExpNoStore = false;
 #endif
+// make NOENV=1 (profiling builds only, wrong results): the fused rollout kernels skip the env step
+// (scripts/profile_env_share.sh prices the env step as the time / PMC bytes it adds)
+#ifdef UAVHIP_EXP_NOENV
+constexpr bool kExpNoEnv = true;
+#else
+constexpr bool kExpNoEnv = false;
+#endif
 
 // Phase tracing (make TRACE=1 only): waves 0 and 4 of the first 256 workgroups stamp s_memtime at
 // the phase boundaries below; uavhip_policy_trace copies the stamps out. Off in the product build.
@@ -1202,7 +1209,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             encoder_layer<kCriticTrunk, 1, true, TR>(TID_C sm, P, pkv, io.L[2], b0);
         }
         // the env step's state loads land while the critic head runs
-        if constexpr (ENV) {
+        if constexpr (ENV && !kExpNoEnv) {
             if (env_grp) {
                 const int le = tid_env() & 63;
                 envgrp::gload_issue(gR, gq, env, b0 + 2 * (int)(tid_env() >> 6) + (le >> 5), le & 31);
@@ -1256,7 +1263,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
         }
     }
     PTR(7);
-    if constexpr (ENV) {
+    if constexpr (ENV && !kExpNoEnv) {
         // UAVEnv.step of this workgroup's 16 envs, two per wave (one env per wave at a time,
         // envdev::step_once on register state; the wave's row scratch in the dead sm.x). Both envs'
         // registers are loaded in one round before either steps.

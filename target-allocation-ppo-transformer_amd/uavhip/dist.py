@@ -23,6 +23,38 @@ def shard(total, world, rank):
     return start, base + (1 if rank < extra else 0)
 
 
+def resolve_shards(E, env_base, total_envs=None, group=None):
+    """Total env count of a data-parallel rollout, checked across the ranks (once, at engine setup).
+
+    Every rank's env block [env_base, env_base + E) must be disjoint from the others' and inside
+    [0, total): the sampling counters t * total + env_base + e (RolloutEngine) are then unique over
+    the ranks, and T * total is the element count of the global advantage moments (ppo.py:94). With
+    torch.distributed initialised (world > 1) the blocks are all-gathered and total defaults to the
+    sum of every rank's E; a mismatch (e.g. every rank left at env_base 0) raises instead of sampling
+    duplicate actions or normalising with a wrong count. One process: total_envs or E."""
+    E, env_base = int(E), int(env_base)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        total = E if total_envs is None else int(total_envs)
+        if env_base < 0 or env_base + E > total:
+            raise ValueError(f"env block [{env_base}, {env_base + E}) outside total_envs {total}")
+        return total
+    world = dist.get_world_size(group)
+    dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
+    mine = torch.tensor([[E, env_base]], dtype=torch.int64, device=dev)
+    blocks = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(blocks, mine, group=group)
+    blocks = sorted(tuple(int(v) for v in b.view(-1).tolist()) for b in blocks)  # (E, base) per rank
+    total_sum = sum(b[0] for b in blocks)
+    total = total_sum if total_envs is None else int(total_envs)
+    spans = sorted((base, base + e) for e, base in blocks)
+    overlap = any(spans[i][1] > spans[i + 1][0] for i in range(len(spans) - 1))
+    if overlap or spans[0][0] < 0 or spans[-1][1] > total or total != total_sum:
+        raise ValueError(f"data-parallel env blocks {spans} (E, env_base per rank) must be disjoint and tile "
+                         f"total_envs {total} = sum of E {total_sum}: build each rank's VecUAVEnv with "
+                         f"env_base = its shard start (uavhip.dist.shard)")
+    return total
+
+
 def compact_floats(T, E):
     """Floats of one rank's payload."""
     return T * E * (ROW_FLOATS + len(SCALARS)) + E * 70

@@ -10,6 +10,7 @@ Two execution paths:
     "next" row); also the torch fp32 reference the fused kernel is tested against.
 """
 import ctypes
+import itertools
 
 import numpy as np
 import torch
@@ -50,6 +51,17 @@ class _Trunk(nn.Module):
         return self.transformer(h, src_key_padding_mask=pad)
 
 
+_INSTANCES = itertools.count()
+
+
+def _instance_seed():
+    """splitmix64 of (torch.initial_seed(), instance number) -> 62-bit Philox key."""
+    z = (torch.initial_seed() + 0x9E3779B97F4A7C15 * (1 + next(_INSTANCES))) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return (z ^ (z >> 31)) & (2 ** 62 - 1)
+
+
 class TransformerActorCritic(nn.Module):
     def __init__(self):
         super().__init__()
@@ -63,11 +75,12 @@ class TransformerActorCritic(nn.Module):
         self._packed = None
         self._packed_key = None
         self._desc = None
-        # Philox key of the on-device action sampling, drawn from torch's RNG after the parameters (the
-        # initialisation stays the reference's): torch.manual_seed controls it, as it controls the
-        # reference's Categorical sampling (transformer_net.py:120), and separate instances / runs
-        # sample independently. The counter starts at 0 per instance.
-        self.sample_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        # Philox key of the on-device action sampling: torch.initial_seed() (so torch.manual_seed
+        # controls it, as it controls the reference's Categorical sampling, transformer_net.py:120)
+        # mixed with a per-process instance count (separate instances sample independently). Nothing
+        # is drawn from the CPU generator: the sampler permutations after construction (ppo.py:115)
+        # stay the reference's. The counter starts at 0 per instance.
+        self.sample_seed = _instance_seed()
         self._sample_offset = 0
 
     def forward(self, state):

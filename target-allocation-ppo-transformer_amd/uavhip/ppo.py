@@ -58,10 +58,11 @@ def gae_workspace(T, E, device):
 
 
 def ppo_epochs(policy, optimizer, states, actions, old_logprobs, old_values, returns, advantages, epochs=None,
-               batch_size=None, eps_clip=None, grad_clip=None, generator=None, perms=None):
+               batch_size=None, eps_clip=None, grad_clip=None, generator=None, perms=None, on_step=None):
     """Clipped-PPO minibatch epochs (ppo.py:96-169). Returns (mean actor loss, critic loss, entropy, n).
     Minibatches: BatchSampler(SubsetRandomSampler(range(n), generator), batch_size, drop_last=True)
-    per epoch as ppo.py:115, or over the given per-epoch row orders `perms` (recorded sampler draws)."""
+    per epoch as ppo.py:115, or over the given per-epoch row orders `perms` (recorded sampler draws).
+    on_step(): called after every optimizer step (tests record the optimizer state)."""
     epochs = cfg.K_EPOCHS if epochs is None else epochs
     batch_size = cfg.BATCH_SIZE if batch_size is None else batch_size
     eps = cfg.EPS_CLIP if eps_clip is None else eps_clip
@@ -97,6 +98,8 @@ def ppo_epochs(policy, optimizer, states, actions, old_logprobs, old_values, ret
             acc += torch.stack([loss_actor.detach(), loss_critic.detach(), ent_mean.detach()]).double()
             cnt += 1
             optimizer.step()
+            if on_step is not None:
+                on_step()
     if cnt:
         sa, sc, se = (acc / cnt).tolist()
     return sa, sc, se, cnt

@@ -68,9 +68,10 @@ class RolloutEngine:
         self.bootstrap = bootstrap
         self.seed = int(policy.sample_seed if seed is None else seed)
         self.env_base = int(getattr(env, "env_base", 0))
-        self.total = int(env.E if total_envs is None else total_envs)
-        if self.env_base + env.E > self.total:
-            raise ValueError(f"env_base {self.env_base} + E {env.E} exceeds total_envs {self.total}")
+        # world > 1: the ranks' env blocks are all-gathered and checked (disjoint, tiling total), and
+        # total defaults to their sum -- the sampling counters and the global advantage count use it
+        from .dist import resolve_shards
+        self.total = resolve_shards(env.E, self.env_base, total_envs)
         self.traj = Trajectory(self.T, env.E, env.device, want_info)
         self.counter = torch.zeros(1, dtype=torch.int64, device=env.device)  # sampling counter base
         # window-row projections of the obs windows (policy.rowproj_buffer): the windows of one

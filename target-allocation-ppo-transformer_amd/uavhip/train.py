@@ -88,11 +88,18 @@ class FusedPPOTrainer:
         self._cap = 0
         self.n_local = None  # set_shard(): rows of this rank's shard
 
+    def _restore_rows(self):
+        """Back to minibatch / world rows per step after a set_shard() run resized the workspace to
+        its padded owned-row count (gathered or single-GPU buffers slice minibatches by it)."""
+        if self.minibatch != self.global_minibatch // self.world:
+            self._resize(self.global_minibatch // self.world)
+
     def set_buffers(self, states, actions, old_logprobs, old_values, returns, advantages):
         """Trajectory buffers the minibatches are drawn from (kept by reference: a captured graph
         reads them at their current addresses)."""
         n = states.shape[0]
         dev = self.device
+        self._restore_rows()
         self.bufs = (states.to(device=dev, dtype=torch.float32).contiguous().reshape(n, cfg.SEQ_LEN, cfg.STATE_DIM),
                      actions.to(device=dev, dtype=torch.int8).contiguous().reshape(n),
                      old_logprobs.to(device=dev, dtype=torch.float32).contiguous().reshape(n),
@@ -122,6 +129,7 @@ class FusedPPOTrainer:
         self.minibatch = rows
         self.desc.minibatch = rows
         self.desc.workspace = self.workspace.data_ptr()
+        self.graphs = {}  # captured against the old workspace / row count
 
     def _owned(self, order, steps):
         """[steps, rows] this rank's rows of each global minibatch of `order` (global row indices,
@@ -142,6 +150,7 @@ class FusedPPOTrainer:
         cover (PPOAgent.update: every update has a different buffer length)."""
         n = states.shape[0]
         dev = self.device
+        self._restore_rows()
         if self._store is None or self._cap < n:
             cap = 1 << max(10, (n - 1).bit_length())
             f32 = dict(dtype=torch.float32, device=dev)

@@ -132,9 +132,13 @@ class VecUAVEnv:
     def load_scenes(self, scenes, env_ids=None):
         """Copy host scenes (dicts in the tests/golden / scene.generate_scene layout) into buffer 0
         of envs `env_ids` (default 0..len-1), make it their active scene, rescore it. With two
-        buffers the spare is marked stale (uavhip_scene_refresh fills it on device)."""
+        buffers the spare is marked stale (uavhip_scene_refresh fills it on device).
+        A scene with a negative target value turns the omega = 0 replay kernel off for this env set
+        (UAVHIP_ENV_NO_REPLAY: K2r needs every assign accepted, i.e. values >= 0)."""
         if isinstance(scenes, dict):
             scenes = [scenes]
+        if any(np.size(s["tgt_value"]) and float(np.min(s["tgt_value"])) < 0 for s in scenes):
+            self.desc.flags |= _lib.ENV_NO_REPLAY
         ids = list(range(len(scenes))) if env_ids is None else list(env_ids)
         mask = torch.zeros(self.E, dtype=torch.uint8)
         for e, s in zip(ids, scenes):

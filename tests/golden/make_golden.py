@@ -20,8 +20,10 @@ Outputs (all numpy .npz, loaded with allow_pickle=False):
   main_train.npz main_train.train() itself for 30 episodes: every env.step (action, reward, done,
                  info), the per-episode statistic accumulators of main_train.py:98-136 read from
                  train()'s own frame, its CSV rows (:161-195) and the update losses behind them
+  init_rng.npz   the sampler's first torch.randperm after PPOAgent() / two networks under
+                 torch.manual_seed (the CPU generator's position after construction)
 
-Usage:  python tests/golden/make_golden.py   (takes ~1 min on CPU)
+Usage:  python tests/golden/make_golden.py   (takes ~1 min on CPU; `... init_rng` writes only init_rng.npz)
 """
 import json
 import os
@@ -447,6 +449,24 @@ def gen_update(policy):
     return out
 
 
+# ----------------------------------------------------------------------------- CPU RNG after init
+def gen_init_rng():
+    """The sampler's first permutation (SubsetRandomSampler -> torch.randperm, ppo.py:115) drawn right
+    after building the networks under torch.manual_seed(s): PPOAgent() builds policy and policy_old
+    (ppo.py:13-43). A build whose construction draws anything extra from the CPU generator shifts it."""
+    out = {}
+    for s in (0, 7):
+        torch.manual_seed(s)
+        TransformerActorCritic()
+        TransformerActorCritic()
+        out[f"two_nets/{s}"] = torch.randperm(192).numpy()
+        torch.manual_seed(s)
+        PPOAgent()
+        out[f"agent/{s}"] = torch.randperm(192).numpy()
+    out["meta"] = np.array(json.dumps(meta()))
+    return out
+
+
 # ----------------------------------------------------------------------------- main_train statistics
 EP_LOCALS = ("current_ep_reward", "current_q0", "ep_total_J", "ep_steps", "ep_max_cov", "ep_action1_cnt",
              "ep_valid_cnt", "ep_total_p_dmg", "ep_total_p_final", "ep_steps_with_assign")
@@ -522,6 +542,9 @@ def gen_main_train(episodes=30):
 def main():
     outdir = HERE
     torch.set_num_threads(min(8, os.cpu_count() or 1))
+    if sys.argv[1:] == ["init_rng"]:  # the one fixture added in round 3
+        np.savez_compressed(os.path.join(outdir, "init_rng.npz"), **gen_init_rng())
+        return
     np.savez_compressed(os.path.join(outdir, "mechanics.npz"), **gen_mechanics(np.random.default_rng(3)))
     np.savez_compressed(os.path.join(outdir, "scenes.npz"), **gen_scenes())
     traj = gen_traj()

@@ -1,0 +1,80 @@
+"""CPU build-time guard on the code objects of the hot kernels (hipcc cross-compiles gfx950 here).
+
+The one-launch rollout (k_rollout_steps, rollout_steps.hip) keeps the register allocation of the
+single-step kernel only because its body launders the thread index and the kernel arguments per step
+(left alone, LLVM hoists the loop-invariant lane arithmetic and arguments out of
+the step loop and spills 1,412 VGPRs). A compiler change that undoes that would otherwise show up
+only as a silent ~10 % loss in a GPU bench. This test compiles the device code to assembly (a few
+seconds) and checks, from the amdhsa metadata and the kernel body:
+  * spills: VGPR and SGPR spill counts at most 8 (today 6 / 6),
+  * LDS: the fixed group segment fits gfx950's 160 KiB,
+  * VGPRs: at most 256 (two waves per SIMD at 512 threads),
+  * MFMA issue: the count of v_mfma_f32_16x16x4_f32 in the body (the GEMM structure; a change
+    here is a structural change of the kernel and must come with DESIGN.md).
+The training and single-step policy kernels get the spill / LDS / VGPR part of the same check."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "target-allocation-ppo-transformer_amd", "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=gfx950", "-I" + os.path.join(ROOT, "include"),
+         "-Wno-unused-function", "--offload-device-only", "-S"]
+
+pytestmark = pytest.mark.skipif(not (os.path.exists(HIPCC) or shutil.which("hipcc")), reason="needs hipcc")
+
+
+def compile_asm(src, tmp_path):
+    out = tmp_path / (os.path.basename(src) + ".s")
+    subprocess.run([HIPCC] + FLAGS + [os.path.join(CSRC, src), "-o", str(out)], check=True, cwd=CSRC,
+                   capture_output=True, timeout=600)
+    return out.read_text()
+
+
+def kernels(asm):
+    """{mangled name: metadata dict (ints)} from the amdhsa.kernels YAML."""
+    meta = asm[asm.index("amdhsa.kernels:"):]
+    out = {}
+    for blk in meta.split("  - .agpr_count")[1:]:
+        name = re.search(r"\.name:\s+(\S+)", blk).group(1)
+        out[name] = {k: int(re.search(r"\.%s:\s+(\d+)" % k, blk).group(1))
+                     for k in ("vgpr_count", "vgpr_spill_count", "sgpr_spill_count", "group_segment_fixed_size")}
+    return out
+
+
+def body(asm, name):
+    i = asm.index("\n" + name + ":")
+    return asm[i:asm.index(".Lfunc_end", i)]
+
+
+def check_limits(name, m, vgpr_spills=8, sgpr_spills=8):
+    print(f"{name}: {m}")
+    assert m["vgpr_spill_count"] <= vgpr_spills, (name, m)
+    assert m["sgpr_spill_count"] <= sgpr_spills, (name, m)
+    assert m["group_segment_fixed_size"] <= 160 * 1024, (name, m)
+    assert m["vgpr_count"] <= 256, (name, m)
+
+
+def test_rollout_steps_code_object(tmp_path):
+    asm = compile_asm("rollout_steps.hip", tmp_path)
+    ks = kernels(asm)
+    name = next(k for k in ks if "k_rollout_steps" in k)
+    check_limits(name, ks[name])
+    n_mfma = len(re.findall(r"\bv_mfma_f32_16x16x4_f32\b", body(asm, name)))
+    print(f"{name}: {n_mfma} v_mfma_f32_16x16x4_f32")
+    assert n_mfma == 1800
+
+
+def test_policy_kernels_code_objects(tmp_path):
+    ks = kernels(compile_asm("policy.hip", tmp_path))
+    wanted = {"k_policy_backward": 0, "k_policy_forwardILb1ELb0ELb0E": 0, "k_policy_forwardILb0ELb1ELb1E": 0,
+              "k_policy_forwardILb0ELb0ELb0E": 0}
+    for frag in wanted:
+        names = [k for k in ks if frag in k]
+        assert names, frag
+        for n in names:
+            check_limits(n, ks[n], sgpr_spills=40)  # the training forward spills 34 SGPRs to VGPR lanes today

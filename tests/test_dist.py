@@ -117,3 +117,63 @@ def test_shard_covers_all():
                 s, c = shard(total, world, r)
                 seen.extend(range(s, s + c))
             assert seen == list(range(total))
+
+
+def _shard_worker(rank, world, port, q, bases):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "target-allocation-ppo-transformer_amd"))
+    import torch.distributed as dist
+    from uavhip.dist import resolve_shards, shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = {}
+        start, cnt = shard(10, world, rank)
+        out["default"] = resolve_shards(cnt, start)                   # total = sum of the ranks' E
+        out["explicit"] = resolve_shards(cnt, start, total_envs=10)
+        for key, base, total in (("same_base", 0, None), ("bad_total", start, 12), ("custom", bases[rank], None)):
+            try:
+                out[key] = resolve_shards(cnt, base, total_envs=total)
+            except ValueError as exc:
+                out[key] = "ValueError: " + str(exc)
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_resolve_shards_checks_the_rank_blocks():
+    """RolloutEngine's total_envs (the sampling counters t * total + env_base + e and the global
+    advantage count T * total, ppo.py:94) comes from all-gathering the ranks' (E, env_base): the
+    sum by default; overlapping blocks (every rank left at env_base 0) or a total that is not the sum
+    raise on every rank instead of sampling duplicate actions / normalising with a wrong count."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    bases = [6, 0, 3]  # disjoint blocks in another rank order: rank 0 [6, 10), rank 1 [0, 3), rank 2 [3, 6)
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q, bases)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        out = res[r]
+        assert out["default"] == out["explicit"] == 10
+        assert str(out["same_base"]).startswith("ValueError") and "disjoint" in out["same_base"]
+        assert str(out["bad_total"]).startswith("ValueError")
+        assert out["custom"] == 10  # disjoint blocks in any rank order are fine
+
+
+def test_resolve_shards_single_process():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "target-allocation-ppo-transformer_amd"))
+    from uavhip.dist import resolve_shards
+    assert resolve_shards(7, 0) == 7
+    assert resolve_shards(7, 3, total_envs=10) == 10
+    with pytest.raises(ValueError):
+        resolve_shards(7, 4, total_envs=10)

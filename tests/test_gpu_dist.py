@@ -4,16 +4,17 @@ the GPU), advantages normalised with the all-reduced global moments (ppo.py:94),
 data-parallel PPO update (FORWARD / all-reduce loss sums / BACKWARD / all-reduce gradients / clip +
 Adam per global minibatch). gloo carries the collectives (RCCL will not put two ranks on one
 device); the data path and every kernel are the ones the RCCL run uses (uavhip/dist.py,
-uavhip/rollout.py, uavhip/train.py).
+uavhip/rollout.py, uavhip/train.py). Two sizes: a small one, and configs[3]'s own per-GPU shard
+(4096 envs x 16 x 32, T = 64, global minibatch 8192).
 
 Checked against ONE process stepping the union of the envs with the same seeds (SURVEY.md section
-4): shards draw their scenes and action samples by global env index (VecUAVEnv(env_base=...),
-RolloutEngine(total_envs=...)), so over two iterations -- with episode ends, full resets flipping
-to refreshed scenes and windows carried across the iteration boundary -- the gathered batch equals
-the union's trajectory in (rank, step, env) order bit for bit, the normalised advantages agree to
-1e-6 (the moments are folded in another order), and after 2 epochs of 18 minibatch steps the ranks'
-parameters are identical and equal the single-process update on the global minibatches within the
-Adam tolerance of tests/test_gpu_train.py -- both for the update on the gathered batch and for the
+4): shards draw their scenes and action samples by global env index (VecUAVEnv(env_base=...); the
+engines resolve total_envs themselves by all-gathering the ranks' env blocks), so over two
+iterations -- with episode ends, full resets flipping to refreshed scenes and windows carried across
+the iteration boundary -- the gathered batch equals the union's trajectory in (rank, step, env)
+order bit for bit, the normalised advantages agree to 1e-6 (the moments are folded in another
+order), and after the update the ranks' parameters are identical and close to the single-process
+update on the global minibatches -- both for the update on the gathered batch and for the
 exchange-free one on each rank's own shard (FusedPPOTrainer.set_shard: a rank computes the rows of
 every global minibatch it owns, padded with idx -1 rows)."""
 import copy
@@ -29,9 +30,15 @@ from conftest import has_gpu
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs an MI355X")]
 
-WORLD, E, N, M, T = 2, 96, 8, 16, 24
-BG, EPOCHS, PERIOD, ITERS = 256, 2, 3, 2
+WORLD = 2
 KEYS = ("obs", "actions", "logp", "values", "returns", "dones")
+# small: the whole iteration incl. the update checked against the union; configs3: BASELINE
+# configs[3]'s per-GPU shard (4096 envs x 16 UAVs x 32 targets, T = 64) with the bench's global
+# minibatch (4096 per rank), one epoch
+CONFIGS = {
+    "small": dict(E=96, N=8, M=16, T=24, BG=256, EPOCHS=2, PERIOD=3, ITERS=2, full_update_check=True),
+    "configs3": dict(E=4096, N=16, M=32, T=64, BG=8192, EPOCHS=1, PERIOD=3, ITERS=2, full_update_check=False),
+}
 
 
 def _free_port():
@@ -42,18 +49,20 @@ def _free_port():
     return p
 
 
-def _engine(n_envs, env_base, normalize):
+def _engine(c, n_envs, env_base, normalize):
+    """total_envs is left to RolloutEngine: with torch.distributed up it all-gathers the ranks' env
+    blocks (uavhip.dist.resolve_shards) -> WORLD * E, the union's count."""
     from uavhip.policy import TransformerActorCritic
     from uavhip.rollout import RolloutEngine
     from uavhip.vec_env import VecUAVEnv
     torch.manual_seed(0)
     pol = TransformerActorCritic().cuda()
-    env = VecUAVEnv(n_envs, N, M, 1, 1, seed=17, full_reset_period=PERIOD, env_base=env_base)
-    eng = RolloutEngine(env, pol, T, seed=29, normalize=normalize, total_envs=WORLD * E)
+    env = VecUAVEnv(n_envs, c["N"], c["M"], 1, 1, seed=17, full_reset_period=c["PERIOD"], env_base=env_base)
+    eng = RolloutEngine(env, pol, c["T"], seed=29, normalize=normalize)
     return pol, eng
 
 
-def _rank(rank, port, q):
+def _rank(rank, port, q, c):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "target-allocation-ppo-transformer_amd")]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -63,11 +72,13 @@ def _rank(rank, port, q):
     try:
         torch.cuda.set_device(0)
         from uavhip.train import FusedPPOTrainer
-        pol, eng = _engine(E, rank * E, normalize=False)
+        E, T, BG, EPOCHS = c["E"], c["T"], c["BG"], c["EPOCHS"]
+        pol, eng = _engine(c, E, rank * E, normalize=False)
+        assert eng.total == WORLD * E
         pol_shard = copy.deepcopy(pol)
         eng.start()
         batches = []
-        for _ in range(ITERS):
+        for _ in range(c["ITERS"]):
             eng.collect(eager=True)
             b = eng.gather()
             batches.append({k: v.cpu().numpy().copy() for k, v in b.items()})
@@ -90,20 +101,23 @@ def _rank(rank, port, q):
         dist.destroy_process_group()
 
 
-def _union_order(x):
+def _union_order(x, T, E):
     """[T, WORLD * E, ...] -> [(rank, step, env), ...] flattened: the gathered batch's order."""
     x = np.swapaxes(x[:T].reshape(T, WORLD, E, *x.shape[2:]), 0, 1)
     return x.reshape(WORLD * T * E, *x.shape[3:])
 
 
-def test_world2_sharded_iteration_matches_one_process():
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_world2_sharded_iteration_matches_one_process(name):
     import torch.multiprocessing as mp
     from uavhip.policy import layout
     from uavhip.train import FusedPPOTrainer
+    c = CONFIGS[name]
+    E, T, BG, EPOCHS, ITERS = c["E"], c["T"], c["BG"], c["EPOCHS"], c["ITERS"]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, port, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_rank, args=(r, port, q, c)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = {}
@@ -116,13 +130,13 @@ def test_world2_sharded_iteration_matches_one_process():
         assert p.exitcode == 0
 
     # one process over the union of the envs, same seeds
-    pol, eng = _engine(WORLD * E, 0, normalize=True)
+    pol, eng = _engine(c, WORLD * E, 0, normalize=True)
     eng.start()
     for it in range(ITERS):
         tr = eng.collect(eager=True)
         ref = {"obs": tr.obs, "actions": tr.actions, "logp": tr.logp, "values": tr.values, "returns": tr.ret,
                "dones": tr.dones.float(), "advantages": tr.adv}
-        ref = {k: _union_order(v.cpu().numpy()) for k, v in ref.items()}
+        ref = {k: _union_order(v.cpu().numpy(), T, E) for k, v in ref.items()}
         for r in range(WORLD):
             got = res[r][0][it]
             for k in KEYS:
@@ -140,11 +154,11 @@ def test_world2_sharded_iteration_matches_one_process():
     ps = single.params.cpu().numpy()
     offs, n = layout()
     for mode in (0, 1):  # 0: gathered batch, 1: own shards
-        name = ("gathered", "sharded")[mode]
+        mname = ("gathered", "sharded")[mode]
         assert s1[3] == res[0][2][mode][3] == res[1][2][mode][3] == steps
-        np.testing.assert_allclose(res[0][2][mode][:3], s1[:3], rtol=1e-4)
+        np.testing.assert_allclose(res[0][2][mode][:3], s1[:3], rtol=1e-4 if c["full_update_check"] else 1e-3)
         p0, p1 = res[0][1][mode], res[1][1][mode]
-        assert np.array_equal(p0, p1), name  # the replicas stay bit-identical
+        assert np.array_equal(p0, p1), mname  # the replicas stay bit-identical
         worst = 0.0
         for (k, v), o in zip(pol.state_dict().items(), offs):
             d = np.abs(p0[o:o + v.numel()] - ps[o:o + v.numel()])
@@ -153,6 +167,11 @@ def test_world2_sharded_iteration_matches_one_process():
                 assert d[128:256].max() <= 2 * reach, k
                 d = np.concatenate([d[:128], d[256:]])
             worst = max(worst, float(d.max()) / reach)
-            assert d.max() <= 0.01 * reach and d.mean() <= 1e-5 * reach, (name, k, float(d.max()), reach)
-        print(f"data-parallel ({name}) vs single-process parameters: max |d| = {worst:.3e} x lr x steps")
-    print(f"sharded rows per rank and step: {res[0][1][2]}, {res[1][1][2]} (global minibatch {BG})")
+            # both sides are the deterministic HIP step (gradients summed over the ranks in another
+            # order): measured + margin; at configs[3]'s 64 steps only a sanity bar
+            if c["full_update_check"]:
+                assert d.max() <= 0.01 * reach and d.mean() <= 1e-5 * reach, (mname, k, float(d.max()), reach)
+            else:
+                assert d.max() <= reach and d.mean() <= 1e-3 * reach, (mname, k, float(d.max()), reach)
+        print(f"[{name}] data-parallel ({mname}) vs single-process parameters: max |d| = {worst:.3e} x lr x steps")
+    print(f"[{name}] sharded rows per rank and step: {res[0][1][2]}, {res[1][1][2]} (global minibatch {BG})")

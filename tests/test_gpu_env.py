@@ -547,3 +547,106 @@ def test_env_replay_matches_oracle(traj_npz):
                 o_c = refs[e].reset()
             np.testing.assert_allclose(obs[t, e], o_c, rtol=2e-6, atol=1e-6)
     assert done.any()
+
+
+def test_negative_values_disable_the_replay_kernel(traj_npz):
+    """K2r needs every assign accepted (omega = 0 AND target values >= 0). A host scene with a
+    negative target value makes VecUAVEnv.load_scenes set UAVHIP_ENV_NO_REPLAY, so a 120-step launch
+    takes the step-by-step kernel and matches the CPU oracle (whose reject branch, uav_env.py:317-338,
+    fires on the negative-value target) -- decisions bit-exact, rewards to 1e-12."""
+    import oracle
+    from uavhip import _lib
+    from uavhip.vec_env import VecUAVEnv
+    s = None
+    for c in cases(traj_npz):
+        cand = sub(traj_npz, c["key"])
+        if cand["params"][6] == 0.0 and c["M"] <= 32 and len(cand["nfz_pos"]) == 1:
+            s = cand
+            break
+    s = dict(s)
+    s["tgt_value"] = np.asarray(s["tgt_value"], np.float64).copy()
+    s["tgt_value"][::2] *= -1.0  # every other target a liability
+    E, T = 16, 120
+    v = VecUAVEnv(E, int(len(s["uav_load"])), int(len(s["tgt_value"])), 1, 1, full_reset_period=0)
+    v.set_params(s["params"])
+    assert not v.desc.flags & _lib.ENV_NO_REPLAY
+    v.load_scenes([s] * E)
+    assert v.desc.flags & _lib.ENV_NO_REPLAY
+    v.reset(episode=1)
+    acts = (np.random.default_rng(2).random((T, E)) < 0.6).astype(np.int8)
+    obs, rew, done, info = (x.cpu().numpy() for x in v.step(torch.from_numpy(acts).cuda()))
+    refs = [oracle.OracleEnv(s, s["params"]) for _ in range(E)]
+    for r in refs:
+        r.reset()
+    rejects = 0
+    for t in range(T):
+        for e in range(E):
+            o_c, r_c, d_c, inf_c = refs[e].step(int(acts[t, e]))
+            rejects += int(acts[t, e] == 1 and inf_c[2] == 0)
+            assert bool(done[t, e]) == d_c, (t, e)
+            assert abs(rew[t, e] - r_c) <= 1e-12 * max(1.0, abs(r_c)), (t, e)
+            np.testing.assert_array_equal(info[t, e, 5:7], inf_c[5:7])
+            if d_c:
+                refs[e].reset()
+    print(f"rejected assigns: {rejects}")
+    assert rejects > 0
+
+
+def test_configs4_shard_at_size():
+    """BASELINE configs[4]'s per-GPU shard at its own size: 8192 envs x 64 UAVs x 128 targets, fp16
+    observations, auto-reset with full_reset_period 200 (main_train.py:79), 200 steps.
+    (1) One 200-step launch (K2 one env per wave: M > 32 rules out the grouped and replay kernels)
+        against 200 single-step launches of twin envs: every output and the carried state bitwise.
+    (2) Every env: rewards / info finite, no stepping errors, episodes ended, and the fp16 windows
+        are exactly the fp32 run's windows rounded to binary16 (twin envs, f32 observations).
+    (3) 8 sampled envs replayed through the CPU oracle on their device-generated scenes: done /
+        pointer / num_assigned / is_valid bit-exact, rewards and J to 1e-12 (uav_env.py:295-435)."""
+    import oracle
+    from uavhip import _lib
+    from uavhip.vec_env import VecUAVEnv
+    E, N, M, T = 8192, 64, 128, 200
+    g = torch.Generator(device="cuda").manual_seed(12)
+    acts = (torch.rand(T, E, device="cuda", generator=g) < 0.4).to(torch.int8)
+
+    def make(dt):
+        v = VecUAVEnv(E, N, M, 1, 1, full_reset_period=200, seed=13, obs_dtype=dt)
+        v.istate[:, _lib.IST["EPISODE"]] = 1
+        v.generate_scenes()
+        return v, v.reset(episode=1).clone()
+
+    v16, obs0_16 = make(torch.float16)
+    obs16, r16, d16, i16 = (x.clone() for x in v16.step(acts))
+    state16 = [x.clone() for x in (v16.istate, v16.dstate, v16.window, v16.nh_final, v16.assigned)]
+    # (1) the same 200 steps as single-step launches
+    w16, _ = make(torch.float16)
+    singles = [[x.clone() for x in w16.step(acts[t])] for t in range(T)]
+    for k, name in enumerate(("obs", "reward", "done", "info")):
+        assert torch.equal(torch.stack([s[k] for s in singles]), (obs16, r16, d16, i16)[k]), name
+    for a, b in zip(state16, (w16.istate, w16.dstate, w16.window, w16.nh_final, w16.assigned)):
+        assert torch.equal(a, b)
+    del singles, w16
+    # (2) properties of every env + the fp16 windows against the fp32 twin's
+    assert torch.isfinite(r16).all() and torch.isfinite(i16).all() and (r16 >= 0).all()
+    assert int(v16.errors().max()) == 0
+    ends = d16.sum(0)
+    assert int((ends > 0).sum()) == E  # every env ended at least one episode
+    v32, obs0_32 = make(torch.float32)
+    obs32, r32, d32, i32 = (x.clone() for x in v32.step(acts))
+    assert torch.equal(obs0_16, obs0_32.half()) and torch.equal(obs16, obs32.half())
+    assert torch.equal(r16, r32) and torch.equal(d16, d32) and torch.equal(i16, i32)
+    # (3) 8 envs through the CPU oracle
+    rew, done, info, a_np = r32.cpu().numpy(), d32.cpu().numpy(), i32.cpu().numpy(), acts.cpu().numpy()
+    prm = np.array([v32.desc.prm[i] for i in range(_lib.PRM_COUNT)])
+    fresh, _ = make(torch.float32)  # the scenes before any reset (no full reset within 200 steps)
+    for e in np.random.default_rng(1).choice(E, 8, replace=False):
+        ref = oracle.OracleEnv(_device_scene(fresh, int(e)), prm)
+        ref.reset()
+        for t in range(T):
+            o_c, r_c, d_c, i_c = ref.step(int(a_np[t, e]))
+            assert bool(done[t, e]) == d_c, (e, t)
+            assert abs(rew[t, e] - r_c) <= 1e-12 * max(1.0, abs(r_c)), (e, t, rew[t, e], r_c)
+            np.testing.assert_array_equal(info[t, e, [1, 2, 5, 6]], i_c[[1, 2, 5, 6]])
+            assert abs(info[t, e, 0] - i_c[0]) <= 1e-12 * max(1.0, abs(i_c[0]))
+            if d_c:
+                ref.reset()
+    print(f"configs[4] shard: {int(ends.sum())} episodes ended over {E} envs x {T} steps")

@@ -133,6 +133,23 @@ def test_policy_init_matches_reference(policy_npz):
         np.testing.assert_array_equal(v.numpy(), policy_npz["a/w/" + k], err_msg=k)
 
 
+def test_construction_leaves_the_cpu_generator_where_the_reference_does():
+    """tests/golden/init_rng.npz: the reference's first sampler permutation (ppo.py:115,
+    torch.randperm) after building two networks (PPOAgent's policy + policy_old, ppo.py:13-43) under
+    torch.manual_seed(s). The build's networks draw nothing beyond the reference's initialisation
+    (the Philox sampling key comes from torch.initial_seed()), so the minibatch orders of every
+    later update() are the reference's. Different instances still get different sampling keys."""
+    from conftest import load_golden
+    from uavhip.policy import TransformerActorCritic
+    f = load_golden("init_rng.npz")
+    for s in (0, 7):
+        torch.manual_seed(s)
+        a, b = TransformerActorCritic(), TransformerActorCritic()
+        np.testing.assert_array_equal(torch.randperm(192).numpy(), f[f"two_nets/{s}"])
+        np.testing.assert_array_equal(f[f"two_nets/{s}"], f[f"agent/{s}"])  # PPOAgent draws nothing else
+        assert a.sample_seed != b.sample_seed and 0 <= a.sample_seed < 2 ** 62
+
+
 def test_policy_torch_path_matches_reference(policy_npz):
     """evaluate() (torch path used by the PPO update) reproduces the reference outputs on CPU."""
     from uavhip.policy import TransformerActorCritic
