@@ -12,6 +12,7 @@ OUT="$R/gpurun_out/envshare_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for b in product noenv; do
+  mkdir -p "$OUT/$b"
   if [ "$b" = product ]; then export UAVHIP_LIB="$R/target-allocation-ppo-transformer_amd/uavhip/libuavhip.so";
   else export UAVHIP_LIB="$R/target-allocation-ppo-transformer_amd/uavhip/libuavhip_noenv.so"; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$b/trace" -o run -- python3 "$R/scripts/rollout_run.py" > "$OUT/$b/trace.log" 2>&1 || exit $?

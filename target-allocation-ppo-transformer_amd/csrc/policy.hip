@@ -379,13 +379,13 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
 }
 
 // Training mode: copy [tok][cols] rows from LDS (stride lds) to workspace rows (stride ldo, column
-// offset c0) for tokens [t0, TOK), all 512 threads, float4 granules.
+// offset c0) for tokens [t0, t1), all 512 threads, float4 granules.
 __device__ __forceinline__ void store_rows(TID_F const float* src, int lds, float* dst, int ldo, int c0, int ncols, int t0,
-                                           int b0, bool compact) {
+                                           int b0, bool compact, int t1 = TOK) {
 #ifdef UAVHIP_EXP_NOSTORE  // timing experiment only (make NOSTORE=1): activations not written
     return;
 #endif
-    const int n4 = ncols / 4, items = (TOK - t0) * n4;
+    const int n4 = ncols / 4, items = (t1 - t0) * n4;
     for (int i = TIDX(); i < items; i += NTHR) {
         const int tok = t0 + i / n4, q = i % n4;
         *reinterpret_cast<f32x4*>(dst + (size_t)orow(tok, b0, compact) * ldo + c0 + 4 * q) =
@@ -548,9 +548,11 @@ __device__ __forceinline__ int kv_row(int wv, int c) { return (1 + (wv >> 2)) * 
 struct NoHook {
     __device__ void operator()() const {}
 };
-template <int trunk, int layer, bool last, bool TR, class F = NoHook>
-__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const APre<depth<last ? 1 : S>()>& po,
-                           const TrainLayerIO& io, int b0, F pre_ln2 = F{});
+// PSX (position split, the small-minibatch training step): a full (unpruned) layer computed for
+// the 16 tokens of ONE window position, column tile qt / 16, in [b * 5 + s] rows.
+template <int trunk, int layer, bool last, bool TR, class F = NoHook, int PSX = 0>
+__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const APre<depth<(last || PSX) ? 1 : S>()>& po,
+                           const TrainLayerIO& io, int b0, F pre_ln2 = F{}, int qt = 0);
 
 // One post-LN nn.TransformerEncoderLayer (relu FFN 256, 8 heads). last: prune to column tile 4.
 // Work split: 8 waves, wave w and w+4 share a SIMD (and its MFMA pipe); every GEMM gives each
@@ -603,9 +605,9 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
 
 // Out-projection + LN1 + FFN + LN2 of an encoder layer, after the attention output is in sm.ctx.
 // `po` = the caller's prefetch of the first out_proj weight blocks.
-template <int trunk, int layer, bool last, bool TR, class F>
-__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const APre<depth<last ? 1 : S>()>& po,
-                           const TrainLayerIO& io, int b0, F pre_ln2) {
+template <int trunk, int layer, bool last, bool TR, class F, int PSX>
+__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const APre<depth<(last || PSX) ? 1 : S>()>& po,
+                           const TrainLayerIO& io, int b0, F pre_ln2, int qt) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
     const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
     const float* bo = P + kOffs.o[layer_param(trunk, layer, OUTB)];
@@ -614,10 +616,11 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
     const float* W2 = P + kOffs.o[layer_param(trunk, layer, L2W)];
     const float* b2 = P + kOffs.o[layer_param(trunk, layer, L2B)];
     const int wv = TIDX() >> 6;
-    constexpr int CTQ = last ? 1 : S;
+    constexpr int CTQ = (last || PSX) ? 1 : S;
     constexpr int DQ = depth<CTQ>();
-    constexpr int qtok0 = last ? (S - 1) * SPW : 0;
-    if (TR) store_rows(TID_C sm.ctx, LDH, io.o, D, 0, D, qtok0, b0, last);  // attention output
+    const int qtok0 = last ? (S - 1) * SPW : (PSX ? qt : 0);
+    const int qtok1 = qtok0 + SPW * CTQ;
+    if (TR) store_rows(TID_C sm.ctx, LDH, io.o, D, 0, D, qtok0, b0, last, qtok1);  // attention output
     // out projection, h = LN1(h + attn) in its epilogue
     APre<DQ> pf1a, pf1b;
     // inference, full layer: the wave's own 16 LayerNorm output features are FFN1's k-block wv, so
@@ -677,8 +680,8 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
     PTR(tb + 11);
     const APre<DQ> pf2b = prefetch<DQ>(TID_C W2, FF, 16 * wv, 128);
     if (TR) {  // FFN hidden (post-ReLU): features 0-127 in big, 128-255 in ctx
-        store_rows(TID_C sm.big, LDF, io.u, FF, 0, D, qtok0, b0, last);
-        store_rows(TID_C sm.ctx, LDF, io.u, FF, D, D, qtok0, b0, last);
+        store_rows(TID_C sm.big, LDF, io.u, FF, 0, D, qtok0, b0, last, qtok1);
+        store_rows(TID_C sm.ctx, LDF, io.u, FF, D, D, qtok0, b0, last, qtok1);
     }
     const f32x4 b24 = ln_bias(TID_C b2);
     f32x4 acc2[CTQ];
@@ -1016,57 +1019,14 @@ __global__ __launch_bounds__(64) void k_loss_partials(const TrainIO io) {
 }
 #endif
 
-// Fused rollout step (uavhip_rollout_step): the env step of the sampled actions (uav_env.py:295-435)
-// after the forward, on the same workgroup's 16 envs.
-struct EnvOut {
-    int auto_reset;
-    float* obs;     // [E][5][14] next windows (f32, or binary16 under UAVHIP_ENV_OBS_F16)
-    double* rew;    // [E]
-    uint8_t* done;  // [E]
-    double* info;   // [E][UAVHIP_INFO_COUNT] (nullable)
-};
-
-// ROWS: layer 0 of both trunks on the window-row projection ring (inference only).
-// ENV: the env step of the sampled actions follows (needs ROWS; envs b0 .. b0 + 15).
-// One workgroup's whole forward (+ env step) of its 16 samples; the kernels below wrap it.
-template <bool TR, bool ROWS, bool ENV>
-__device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __restrict__ P, const float* __restrict__ states,
-                                             int B, const int8_t* __restrict__ actions_in, uint64_t seed,
-                                             uint64_t offset, const uint64_t* __restrict__ offset_dev,
-                                             int8_t* __restrict__ action_out, float* __restrict__ logp_out,
-                                             float* __restrict__ value_out, float* __restrict__ ent_out,
-                                             float* __restrict__ logits_out, const TrainIO& io, const RowIO& rio,
-                                             const uavhip_env& env, const EnvOut& eo, int bx) {
-    static_assert(!(TR && ROWS), "the training forward recomputes every row");
-    static_assert(!ENV || ROWS, "the fused env step follows the rollout forward");
-    // training trunk split (TrainIO::split): role 1 = actor trunk + head, 2 = critic trunk + head
-    // of sample block blk; role 0 = both (the rollout always)
-    int blk = bx, role = 0;
-    if constexpr (TR) {
-        if (io.split) {
-            role = blk < io.split ? 1 : 2;
-            if (role == 2) blk -= io.split;
-        }
-    }
-    const bool do_actor = role != 2, do_critic = role != 1;
-    const int b0 = blk * SPW;
-    PTR(0);
-    // training mode: the first trunk's embedding operands and first K/V weight blocks are loaded
-    // before the minibatch gather stores its rows (a load behind a store burst waits for the burst)
-    [[maybe_unused]] EmbPre ep_a, ep_c;
-    [[maybe_unused]] APre<2> pkv_a, pkv_c;
-    if constexpr (TR) {
-        if (do_actor) {
-            ep_a = embed_load<kActorTrunk>(TID_C P);
-            pkv_a = prefetch<2>(TID_C P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(TIDX() >> 6, 0), 0);
-        } else {
-            ep_c = embed_load<kCriticTrunk>(TID_C P);
-            pkv_c = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(TIDX() >> 6, 0), 0);
-        }
-    }
-    // windows -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch tail zero-filled);
-    // training mode gathers minibatch row idx[b] of the trajectory buffer (idx < 0: a padding row,
-    // computed on row 0 and flagged by action -1 in smp, so it adds nothing to the loss or gradients)
+// The 16 windows of a workgroup -> sm.x[tok = s*16 + p][k], k padded 14 -> 16 with zeros (batch
+// tail zero-filled) and the key padding mask -> sm.mask; training mode gathers minibatch row idx[b]
+// of the trajectory buffer (idx < 0: a padding row, computed on row 0 and flagged by action -1 in
+// smp, so it adds nothing to the loss or gradients) and, if `writer`, stores the windows, the mask
+// and the per-sample loss inputs into the workspace. Ends without a barrier.
+template <bool TR>
+__device__ __forceinline__ void gather_windows(TID_F Smem& sm, const float* __restrict__ states, int B, const TrainIO& io,
+                                               int b0, bool do_actor) {
     {   // <= 3 elements per thread, every load of a round issued before any is used: the
         // training gather is two dependent rounds (row index, then window / loss inputs)
         constexpr int kEl = (TOK * LDX + NTHR - 1) / NTHR;
@@ -1122,6 +1082,57 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             for (int c = 0; c < 5; ++c) o[c] = ld[c];
         }
     }
+}
+
+// Fused rollout step (uavhip_rollout_step): the env step of the sampled actions (uav_env.py:295-435)
+// after the forward, on the same workgroup's 16 envs.
+struct EnvOut {
+    int auto_reset;
+    float* obs;     // [E][5][14] next windows (f32, or binary16 under UAVHIP_ENV_OBS_F16)
+    double* rew;    // [E]
+    uint8_t* done;  // [E]
+    double* info;   // [E][UAVHIP_INFO_COUNT] (nullable)
+};
+
+// ROWS: layer 0 of both trunks on the window-row projection ring (inference only).
+// ENV: the env step of the sampled actions follows (needs ROWS; envs b0 .. b0 + 15).
+// One workgroup's whole forward (+ env step) of its 16 samples; the kernels below wrap it.
+template <bool TR, bool ROWS, bool ENV>
+__device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __restrict__ P, const float* __restrict__ states,
+                                             int B, const int8_t* __restrict__ actions_in, uint64_t seed,
+                                             uint64_t offset, const uint64_t* __restrict__ offset_dev,
+                                             int8_t* __restrict__ action_out, float* __restrict__ logp_out,
+                                             float* __restrict__ value_out, float* __restrict__ ent_out,
+                                             float* __restrict__ logits_out, const TrainIO& io, const RowIO& rio,
+                                             const uavhip_env& env, const EnvOut& eo, int bx) {
+    static_assert(!(TR && ROWS), "the training forward recomputes every row");
+    static_assert(!ENV || ROWS, "the fused env step follows the rollout forward");
+    // training trunk split (TrainIO::split): role 1 = actor trunk + head, 2 = critic trunk + head
+    // of sample block blk; role 0 = both (the rollout always)
+    int blk = bx, role = 0;
+    if constexpr (TR) {
+        if (io.split) {
+            role = blk < io.split ? 1 : 2;
+            if (role == 2) blk -= io.split;
+        }
+    }
+    const bool do_actor = role != 2, do_critic = role != 1;
+    const int b0 = blk * SPW;
+    PTR(0);
+    // training mode: the first trunk's embedding operands and first K/V weight blocks are loaded
+    // before the minibatch gather stores its rows (a load behind a store burst waits for the burst)
+    [[maybe_unused]] EmbPre ep_a, ep_c;
+    [[maybe_unused]] APre<2> pkv_a, pkv_c;
+    if constexpr (TR) {
+        if (do_actor) {
+            ep_a = embed_load<kActorTrunk>(TID_C P);
+            pkv_a = prefetch<2>(TID_C P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(TIDX() >> 6, 0), 0);
+        } else {
+            ep_c = embed_load<kCriticTrunk>(TID_C P);
+            pkv_c = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(TIDX() >> 6, 0), 0);
+        }
+    }
+    gather_windows<TR>(TID_C sm, states, B, io, b0, do_actor);
     __syncthreads();
     PTR(1);
     const int wv = TIDX() >> 6;
@@ -1498,14 +1509,14 @@ struct LnBwdPre {
     float RS[kLnIt];
 };
 __device__ __forceinline__ void ln_bwd_load(LnBwdPre& a, const float* __restrict__ xhat, const float* __restrict__ rstd,
-                                            const float* __restrict__ w, int t0, int b0, bool compact) {
+                                            const float* __restrict__ w, int t0, int b0, bool compact, int t1 = TOK) {
     const int f0 = 8 * (tid_x() & 15), grp = tid_x() >> 4;
     a.w0 = ld4(w + f0);
     a.w1 = ld4(w + f0 + 4);
 #pragma unroll
     for (int it = 0; it < kLnIt; ++it) {
         const int tok = t0 + grp + it * (NTHR / 16);
-        if (tok < TOK) {  // wave-uniform
+        if (tok < t1) {  // wave-uniform
             const size_t r = (size_t)orow(tok, b0, compact);
             a.X0[it] = ld4(xhat + r * D + f0);
             a.X1[it] = ld4(xhat + r * D + f0 + 4);
@@ -1515,7 +1526,7 @@ __device__ __forceinline__ void ln_bwd_load(LnBwdPre& a, const float* __restrict
 }
 __device__ void ln_bwd_lds(const float* src, float* dst, const LnBwdPre& a, float* __restrict__ gout,
                            float* __restrict__ part, float* __restrict__ bias, int t0, int b0, bool compact,
-                           float* scratch) {
+                           float* scratch, int t1 = TOK) {
     const int j = tid_x() & 15, grp = tid_x() >> 4;
     const int f0 = 8 * j;
     const f32x4 w0 = a.w0, w1 = a.w1;
@@ -1525,7 +1536,7 @@ __device__ void ln_bwd_lds(const float* src, float* dst, const LnBwdPre& a, floa
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
         const int tok = t0 + grp + it * (NTHR / 16);
-        if (tok >= TOK) continue;
+        if (tok >= t1) continue;
         const size_t r = (size_t)orow(tok, b0, compact);
         const f32x4 g0 = ld4(src + tok * LDH + f0), g1 = ld4(src + tok * LDH + f0 + 4);
         const f32x4 x0 = a.X0[it], x1 = a.X1[it];
@@ -1579,8 +1590,10 @@ __device__ __forceinline__ void st2(float* p, f32x2 v) { *reinterpret_cast<f32x2
 struct AttnPre {
     f32x2 k[S], v[S], q[S];
 };
+// qsel >= 0 (position split): the one query position qsel; else every position (full layer) or
+// position 4 (pruned layer)
 template <bool last>
-__device__ __forceinline__ void attn_bwd_load(AttnPre& a, const float* __restrict__ qkv, int c, int b0) {
+__device__ __forceinline__ void attn_bwd_load(AttnPre& a, const float* __restrict__ qkv, int c, int b0, int qsel = -1) {
     const int o8 = tid_x() & 7, hh = (tid_x() >> 3) & 3, p = tid_x() >> 5;
     const int col = 64 * c + hh * HD + 2 * o8;
     const size_t rb = (size_t)(b0 + p) * S;
@@ -1591,10 +1604,10 @@ __device__ __forceinline__ void attn_bwd_load(AttnPre& a, const float* __restric
     }
 #pragma unroll
     for (int i = 0; i < S; ++i)
-        if (!last || i == S - 1) a.q[i] = ld2(qkv + (rb + i) * 3 * D + col);
+        if (qsel >= 0 ? i == qsel : (!last || i == S - 1)) a.q[i] = ld2(qkv + (rb + i) * 3 * D + col);
 }
 template <bool last>
-__device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch) {
+__device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch, int qsel = -1) {
     const int o8 = tid_x() & 7, hh = (tid_x() >> 3) & 3, p = tid_x() >> 5;
     const int d0 = hh * HD + 2 * o8;
     const int col = 64 * c + d0;
@@ -1612,7 +1625,7 @@ __device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch
 #pragma unroll
     for (int i = 0; i < S; ++i) {
         f32x2 dq = {0.f, 0.f};
-        if (!last || i == S - 1) {
+        if (qsel >= 0 ? i == qsel : (!last || i == S - 1)) {
             const f32x2 q = a.q[i];
             const f32x2 g = ld2(sm.ctx + (i * SPW + p) * LDH + col);
             float pr[S], dp[S];
@@ -1693,30 +1706,40 @@ __device__ __forceinline__ void embed_bwd_load(EmbBwdPre& ep, const float* __res
 
 // ln2_pre: this layer's LN2-backward operands, already loaded by the caller (nullptr: load here);
 // next_load: issues the next phase's global loads behind this layer's last weight loads.
-template <int trunk, int layer, bool last, int TB, class F = NoHook>
+// MODE (the position-split training step, K7 below): kBwdFull = the whole layer; kBwdNoDx = stop after
+// the attention backward (dqkv rows and bias partials written; no W_in^T GEMM, no residual -- the
+// per-position kernels form dL/d(layer input)); kBwdPos = a full layer for the 16 query tokens of
+// ONE window position (tokens [qt, qt + 16), [b * 5 + s] rows, partial row prow): its dq rows go to
+// dqkv, its contributions to every position's dk / dv to kvc ([prow][80 tokens][dk 128 | dv 128]).
+enum { kBwdFull = 0, kBwdNoDx = 1, kBwdPos = 2 };
+template <int trunk, int layer, bool last, int TB, class F = NoHook, int MODE = kBwdFull>
 __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __restrict__ PT, const BwdLayerIO& io,
                           int b0, EmbBwdPre* ep = nullptr, const float* e_emb = nullptr, const float* xg = nullptr,
-                          const LnBwdPre* ln2_pre = nullptr, F next_load = F{}) {
+                          const LnBwdPre* ln2_pre = nullptr, F next_load = F{}, int qt = 0, int prow = -1,
+                          float* __restrict__ kvc = nullptr) {
     BTR(TB);
-    constexpr int CTQ = last ? 1 : S;
+    static_assert(MODE != kBwdPos || !last, "position split: full layers only");
+    constexpr int CTQ = (last || MODE == kBwdPos) ? 1 : S;
     constexpr int DQ = depth<CTQ>();
-    constexpr int qtok0 = last ? (S - 1) * SPW : 0;
+    const int qtok0 = last ? (S - 1) * SPW : (MODE == kBwdPos ? qt : 0);
+    const int qtok1 = qtok0 + SPW * CTQ;
+    const int qsel = MODE == kBwdPos ? qt / SPW : -1;
     const float* WinT = PT + kTWin;
     const float* WoT = PT + kTWo;
     const float* W1T = PT + kTW1;
     const float* W2T = PT + kTW2;
     const int wv = tid_x() >> 6, l = lane_id(), i16 = l & 15, g = l >> 4;
     const int fo = 16 * wv + 4 * g;  // this lane's 4 output features of a 16-row tile of wave wv
-    const int blk = b0 / SPW;  // the sample block (its partial rows)
+    const int blk = prow >= 0 ? prow : b0 / SPW;  // this workgroup's partial rows
     float* bias = io.bpart + (size_t)blk * kBiasPart;  // this workgroup's bias partials
 
     // LN2 backward: sm.h -> sm.ctx (= df)
     APre<DQ> pa = prefetch<DQ>(W2T, D, 16 * wv, 0);
     LnBwdPre lnp;
     if (ln2_pre) lnp = *ln2_pre;
-    else ln_bwd_load(lnp, io.xhat2, io.rstd2, P + kOffs.o[layer_param(trunk, layer, N2W)], qtok0, b0, last);
+    else ln_bwd_load(lnp, io.xhat2, io.rstd2, P + kOffs.o[layer_param(trunk, layer, N2W)], qtok0, b0, last, qtok1);
     ln_bwd_lds(sm.h, sm.ctx, lnp, io.df, io.ln2_part + (size_t)blk * 2 * D, bias + kBiasL2, qtok0, b0, last,
-               sm.big);
+               sm.big, qtok1);
     BTR(TB + 1);
     __syncthreads();
     BTR(TB + 2);
@@ -1776,15 +1799,15 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
     pa = prefetch<DQ>(WoT, D, 16 * wv, 0);
     // LN1 backward's operands, then chunk 0's Q / K / V for the attention backward: their HBM
     // latency hides under the residual pass / barrier and LN1 backward
-    ln_bwd_load(lnp, io.xhat1, io.rstd1, P + kOffs.o[layer_param(trunk, layer, N1W)], qtok0, b0, last);
+    ln_bwd_load(lnp, io.xhat1, io.rstd1, P + kOffs.o[layer_param(trunk, layer, N1W)], qtok0, b0, last, qtok1);
     AttnPre ap;
-    attn_bwd_load<last>(ap, io.qkv, 0, b0);
+    attn_bwd_load<last>(ap, io.qkv, 0, b0, qsel);
     BTR(TB + 5);
     __syncthreads();
     BTR(TB + 6);
     // LN1 backward: sm.ctx -> sm.h (= dz1)
     ln_bwd_lds(sm.ctx, sm.h, lnp, io.dz1, io.ln1_part + (size_t)blk * 2 * D, bias + kBiasOut, qtok0, b0, last,
-               sm.big);
+               sm.big, qtok1);
     BTR(TB + 7);
     __syncthreads();
     BTR(TB + 8);
@@ -1800,12 +1823,14 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
     __syncthreads();
     BTR(TB + 10);
     // attention backward per chunk of 4 heads, dh_in += Win^T [dq | dk | dv] of the chunk (K = 3 x 64)
+    constexpr bool kDx = MODE == kBwdFull;
     f32x4 acc[S];
     zero(acc);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-        APre<2> pw = prefetch<2>(WinT, 3 * D, 16 * wv, 64 * c);
-        attn_bwd_chunk<last>(sm, ap, c, sm.scr);
+        [[maybe_unused]] APre<2> pw;
+        if constexpr (kDx) pw = prefetch<2>(WinT, 3 * D, 16 * wv, 64 * c);
+        attn_bwd_chunk<last>(sm, ap, c, sm.scr, qsel);
         __syncthreads();
         BTR(TB + 11 + 2 * c);
         if (tid_x() < 3 * 64) {  // in_proj bias partial of the chunk: the 8 wave rows of sm.scr
@@ -1817,28 +1842,37 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
         }
         // first weight blocks of the chunk's K and V parts, loaded ahead of the stores below (the
         // vector memory counter retires in order: loads behind a store burst wait for it)
-        APre<2> pw1 = prefetch<2>(WinT, 3 * D, 16 * wv, D + 64 * c);
-        APre<2> pw2 = prefetch<2>(WinT, 3 * D, 16 * wv, 2 * D + 64 * c);
+        [[maybe_unused]] APre<2> pw1, pw2;
+        if constexpr (kDx) {
+            pw1 = prefetch<2>(WinT, 3 * D, 16 * wv, D + 64 * c);
+            pw2 = prefetch<2>(WinT, 3 * D, 16 * wv, 2 * D + 64 * c);
+        }
         // dq | dk | dv of the chunk -> dqkv rows: 256-byte row segments, float4 per thread
         for (int i = tid_x(); i < TOK * 48; i += NTHR) {
             const int tok = i / 48, r = i - tok * 48, part = r >> 4, q = r & 15;
-            if (part == 0 && tok < qtok0) continue;  // pruned: dq only on the query rows
-            st4(io.dqkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q,
-                ld4(sm.big + tok * LDB + part * 64 + 4 * q));
+            if (part == 0 && (tok < qtok0 || tok >= qtok1)) continue;  // dq only on the query rows
+            const f32x4 v = ld4(sm.big + tok * LDB + part * 64 + 4 * q);
+            if (MODE == kBwdPos && part > 0)  // this query position's share of every position's dk / dv
+                st4(kvc + ((size_t)blk * TOK + tok) * 2 * D + (part - 1) * D + 64 * c + 4 * q, v);
+            else
+                st4(io.dqkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q, v);
         }
-        if (last) {  // dq is zero outside the query tile: Win_q^T dq only for column tile 4
-            f32x4 a1[1] = {acc[S - 1]};
-            gemm_tile<1, 2, 4>(a1, pw, WinT, 3 * D, 16 * wv, 64 * c, sm.big, LDB, (S - 1) * SPW);
-            acc[S - 1] = a1[0];
-        } else {
-            gemm_tile<S, 2, 4>(acc, pw, WinT, 3 * D, 16 * wv, 64 * c, sm.big, LDB, 0);
+        if constexpr (kDx) {
+            if (last) {  // dq is zero outside the query tile: Win_q^T dq only for column tile 4
+                f32x4 a1[1] = {acc[S - 1]};
+                gemm_tile<1, 2, 4>(a1, pw, WinT, 3 * D, 16 * wv, 64 * c, sm.big, LDB, (S - 1) * SPW);
+                acc[S - 1] = a1[0];
+            } else {
+                gemm_tile<S, 2, 4>(acc, pw, WinT, 3 * D, 16 * wv, 64 * c, sm.big, LDB, 0);
+            }
+            gemm_tile<S, 2, 4>(acc, pw1, WinT, 3 * D, 16 * wv, D + 64 * c, sm.big + 64, LDB, 0);
+            gemm_tile<S, 2, 4>(acc, pw2, WinT, 3 * D, 16 * wv, 2 * D + 64 * c, sm.big + 128, LDB, 0);
         }
-        gemm_tile<S, 2, 4>(acc, pw1, WinT, 3 * D, 16 * wv, D + 64 * c, sm.big + 64, LDB, 0);
-        gemm_tile<S, 2, 4>(acc, pw2, WinT, 3 * D, 16 * wv, 2 * D + 64 * c, sm.big + 128, LDB, 0);
-        if (c == 0) attn_bwd_load<last>(ap, io.qkv, 1, b0);  // behind every weight load of the chunk
+        if (c == 0) attn_bwd_load<last>(ap, io.qkv, 1, b0, qsel);  // behind every weight load of the chunk
         if (c == 0) __syncthreads();  // big is rewritten by chunk 1
         BTR(TB + 12 + 2 * c);
     }
+    if constexpr (!kDx) return;
     if (layer == 0 && ep) embed_bwd_load(*ep, e_emb, xg, b0);
     next_load();
     // + dz1 on the rows that carried the residual -> sm.h
@@ -2073,6 +2107,326 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
     }
 }
 
+// ================================================================== K7: position-split training step
+// Small minibatches leave most CUs idle in the 16-samples-per-workgroup kernels above (minibatch 64:
+// 8 workgroups, each with ~30 MFLOP of its critic trunk = ~48 us at one CU's MFMA peak). Here every
+// full (unpruned) encoder layer runs as 5 workgroups per 16-sample block, one per window position
+// (16 tokens = one MFMA column tile): token-local work (embedding, Q|K|V projection, out-projection,
+// LayerNorms, FFN) splits exactly; attention needs every position's K / V, so the launches are cut
+// there and the K / V rows go through the workspace (L2-resident at these sizes):
+//   F1  block x trunk x position: gather, embedding, layer-0 Q|K|V of the position
+//   F2  block x (critic x 5 positions | actor x position 4): layer-0 attention for the position's
+//       queries, out-proj + LN1 + FFN + LN2; critic: layer-1 K|V of the position (Q at position 4);
+//       actor: the head
+//   F3  block (critic): layer 1 (pruned: position 4) attention + tail + head, the loss partials
+//   B1  block x trunk: loss / head backward, the pruned top layer's backward down to its dqkv rows
+//   B2  block x trunk x position: dL/d(top layer input) at the position = W_in^T dqkv + residual;
+//       actor: embedding backward; critic: layer-0 backward for the position's queries -- its dq rows
+//       and its share of every position's dk / dv (kvc)
+//   B3  block x position (critic): dk / dv of the position = the 5 shares in position order (fixed:
+//       deterministic), W_in^T, residual, embedding backward
+// Partial rows (bias / LayerNorm / embedding gradients) are per (block, position): row b * 5 + s
+// (per-block layers use row b * 5). The same weight-gradient GEMM, reduction and Adam follow.
+constexpr int LDQ = 3 * D + 8;  // a [dq | dk | dv] row in LDS (392 floats: 2 mod 16 slots of 16 B)
+
+__device__ __forceinline__ void ps_mask(Smem& sm, const float* __restrict__ mask, int b0) {
+    if (tid_x() < SPW * S) sm.mask[tid_x()] = mask[(size_t)b0 * S + tid_x()] != 0.f;
+}
+
+// Workspace rows [(b0 + p) * 5 + s][c0 .. c0 + cols) -> LDS rows s * 16 + p (stride lds)
+__device__ __forceinline__ void ps_rows_in(float* dst, int lds, const float* __restrict__ src, int ld, int c0, int cols,
+                                           int s, int b0) {
+    const int n4 = cols / 4;
+    for (int i = tid_x(); i < SPW * n4; i += NTHR) {
+        const int p = i / n4, q = i - p * n4;
+        st4(dst + (s * SPW + p) * lds + 4 * q, ld4(src + (size_t)trow(s * SPW + p, b0) * ld + c0 + 4 * q));
+    }
+}
+
+// Embedding of window position s (transformer_net.py:57-59): h = relu(W_e x + b_e) + pos[s] -> sm.h
+// rows 16 s + p and the e / h0 workspace rows; wave w computes features [16 w, 16 w + 16).
+template <int trunk>
+__device__ void ps_embed(Smem& sm, const float* __restrict__ P, float* __restrict__ e_out, float* __restrict__ h_out,
+                         int b0, int s) {
+    const float* We = P + kOffs.o[trunk + EMB_W];
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
+    const int f = 16 * wv + i16;
+    f32x4 a;
+    a.x = 4 * g + 0 < IN ? We[f * IN + 4 * g + 0] : 0.f;
+    a.y = 4 * g + 1 < IN ? We[f * IN + 4 * g + 1] : 0.f;
+    a.z = 4 * g + 2 < IN ? We[f * IN + 4 * g + 2] : 0.f;
+    a.w = 4 * g + 3 < IN ? We[f * IN + 4 * g + 3] : 0.f;
+    const f32x4 bb = ld4(P + kOffs.o[trunk + EMB_B] + 16 * wv + 4 * g);
+    const f32x4 pp = ld4(P + kOffs.o[trunk + POS] + s * D + 16 * wv + 4 * g);
+    const f32x4 x = ld4(sm.x + (s * SPW + i16) * LDX + 4 * g);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], x[j], acc, 0, 0, 0);
+    f32x4 e = acc + bb;
+    e.x = fmaxf(e.x, 0.f); e.y = fmaxf(e.y, 0.f); e.z = fmaxf(e.z, 0.f); e.w = fmaxf(e.w, 0.f);
+    const f32x4 v = e + pp;
+    st4(sm.h + (s * SPW + i16) * LDH + 16 * wv + 4 * g, v);
+    const size_t r = (size_t)trow(s * SPW + i16, b0);
+    st4(e_out + r * D + 16 * wv + 4 * g, e);
+    st4(h_out + r * D + 16 * wv + 4 * g, v);
+}
+
+// in_proj rows [16 tile0, 384) of the 16 tokens of position s (sm.h rows 16 s + p) -> qkv rows
+// (Q = rows 0-127, K = 128-255, V = 256-383 of a [b * 5 + s][384] row), bias added.
+__device__ void ps_inproj(Smem& sm, const float* __restrict__ W, const float* __restrict__ bias,
+                          float* __restrict__ qkv, int tile0, int s, int b0) {
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
+    const size_t r = (size_t)trow(s * SPW + i16, b0);
+    for (int t = tile0 + wv; t < 3 * D / 16; t += NW) {  // wave-uniform
+        const int row = 16 * t;
+        const f32x4 bb = ld4(bias + row + 4 * g);
+        f32x4 acc[1];
+        zero(acc);
+        gemm_tile<1, 4>(acc, prefetch<4>(W, D, row, 0), W, D, row, 0, sm.h, LDH, s * SPW);
+        st4(qkv + r * 3 * D + row + 4 * g, acc[0] + bb);
+    }
+}
+
+// Q of position s and K | V of all five positions for the heads of chunk c -> sm.big [tok][Q|K|V]
+__device__ void ps_qkv_chunk(Smem& sm, const float* __restrict__ qkv, int c, int s, int b0) {
+    for (int i = tid_x(); i < SPW * 16 + TOK * 32; i += NTHR) {
+        int tok, part, q;
+        if (i < SPW * 16) {
+            tok = s * SPW + i / 16; part = 0; q = i % 16;
+        } else {
+            const int k = i - SPW * 16;
+            tok = k / 32; part = 1 + (k % 32) / 16; q = k % 16;
+        }
+        st4(sm.big + tok * LDB + part * 64 + 4 * q, ld4(qkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q));
+    }
+}
+
+__global__ __launch_bounds__(NTHR) void k_ps_f1(const float* __restrict__ P, const float* __restrict__ states, int B,
+                                                const TrainIO io) {
+    __shared__ __attribute__((aligned(16))) Smem sm;
+    const int blk = blockIdx.x / 10, r = blockIdx.x % 10, s = r % S, b0 = blk * SPW;
+    const bool critic = r >= S;
+    gather_windows<true>(sm, states, B, io, b0, r == 0);  // one workgroup per block writes the rows
+    __syncthreads();
+    const int trunk = critic ? kCriticTrunk : kActorTrunk;
+    if (critic) ps_embed<kCriticTrunk>(sm, P, io.e[1], io.h0[1], b0, s);
+    else ps_embed<kActorTrunk>(sm, P, io.e[0], io.h0[0], b0, s);
+    __syncthreads();
+    // the actor's only layer is pruned: Q at position 4 only
+    ps_inproj(sm, P + kOffs.o[layer_param(trunk, 0, INW)], P + kOffs.o[layer_param(trunk, 0, INB)],
+              io.L[critic ? 1 : 0].qkv, critic || s == S - 1 ? 0 : D / 16, s, b0);
+}
+
+__global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, const TrainIO io) {
+    __shared__ __attribute__((aligned(16))) Smem sm;
+    const int blk = blockIdx.x / 6, r = blockIdx.x % 6, b0 = blk * SPW, wv = tid_x() >> 6;
+    const bool critic = r < S;
+    const int s = critic ? r : S - 1, ti = critic ? 1 : 0;
+    ps_mask(sm, io.mask, b0);
+    ps_rows_in(sm.h, LDH, io.h0[ti], D, 0, D, s, b0);  // the layer input (residual) of the position
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        ps_qkv_chunk(sm, io.L[ti].qkv, c, s, b0);
+        __syncthreads();
+        attention_chunk(sm, c, s, 1);
+        __syncthreads();
+    }
+    if (critic) {
+        const APre<4> po = prefetch<4>(P + kOffs.o[layer_param(kCriticTrunk, 0, OUTW)], D, 16 * wv, 0);
+        layer_tail<kCriticTrunk, 0, false, true, NoHook, 1>(sm, P, po, io.L[1], b0, NoHook{}, s * SPW);
+        __syncthreads();
+        // layer 1 (pruned) of this position: K | V, and Q at position 4
+        ps_inproj(sm, P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], P + kOffs.o[layer_param(kCriticTrunk, 1, INB)],
+                  io.L[2].qkv, s == S - 1 ? 0 : D / 16, s, b0);
+        return;
+    }
+    const APre<4> po = prefetch<4>(P + kOffs.o[layer_param(kActorTrunk, 0, OUTW)], D, 16 * wv, 0);
+    layer_tail<kActorTrunk, 0, true, true>(sm, P, po, io.L[0], b0);
+    APre<4> ph;
+    if (wv < 4) ph = prefetch<4>(P + kOffs.o[kActorHead], D, 16 * wv, 0);
+    __syncthreads();
+    head_mlp<kActorHead, 2>(sm, P, ph, sm.logits);
+    store_hidden(sm, io.z[0], b0);
+    if (tid_x() < SPW) {
+        float* o = io.smp + (size_t)(b0 + tid_x()) * 8;
+        o[5] = sm.logits[2 * tid_x()];
+        o[6] = sm.logits[2 * tid_x() + 1];
+    }
+}
+
+__global__ __launch_bounds__(NTHR) void k_ps_f3(const float* __restrict__ P, const TrainIO io) {
+    __shared__ __attribute__((aligned(16))) Smem sm;
+    const int b0 = blockIdx.x * SPW, wv = tid_x() >> 6;
+    ps_mask(sm, io.mask, b0);
+    ps_rows_in(sm.h, LDH, io.L[1].h2, D, 0, D, S - 1, b0);  // layer 1's input (residual) at position 4
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        ps_qkv_chunk(sm, io.L[2].qkv, c, S - 1, b0);
+        __syncthreads();
+        attention_chunk(sm, c, S - 1, 1);
+        __syncthreads();
+    }
+    const APre<4> po = prefetch<4>(P + kOffs.o[layer_param(kCriticTrunk, 1, OUTW)], D, 16 * wv, 0);
+    layer_tail<kCriticTrunk, 1, true, true>(sm, P, po, io.L[2], b0);
+    APre<4> ph;
+    if (wv < 4) ph = prefetch<4>(P + kOffs.o[kCriticHead], D, 16 * wv, 0);
+    __syncthreads();
+    head_mlp<kCriticHead, 1>(sm, P, ph, sm.value);
+    store_hidden(sm, io.z[1], b0);
+    if (tid_x() < SPW) {  // the actor's logits (F2) beside the value: the block's loss partials
+        const float* o = io.smp + (size_t)(b0 + tid_x()) * 8;
+        sm.logits[2 * tid_x()] = o[5];
+        sm.logits[2 * tid_x() + 1] = o[6];
+    }
+    __syncthreads();
+    loss_partials(sm, io, b0);
+}
+
+__global__ __launch_bounds__(NTHR) void k_ps_b1(const float* __restrict__ P, const float* __restrict__ PT,
+                                                const BwdIO io) {
+    __shared__ __attribute__((aligned(16))) Smem sm;
+    if (tid_x() >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
+    const int blk = blockIdx.x >> 1, role = 1 + (blockIdx.x & 1), b0 = blk * SPW;
+    ps_mask(sm, io.mask, b0);
+    heads_bwd(sm, P, io, b0, role);
+    __syncthreads();
+    if (role == 2) {  // critic: head.0, layer 1 (pruned) down to its dqkv rows
+        head_input_grad(sm, PT + kHeadT + D * HID, sm.ctx + 64);
+        __syncthreads();
+        bwd_layer<kCriticTrunk, 1, true, 4, NoHook, kBwdNoDx>(sm, P, PT + 2 * kLayerT, io.L[2], b0, nullptr, nullptr,
+                                                                 nullptr, nullptr, NoHook{}, 0, blk * S);
+    } else {  // actor: head.0, layer 0 (pruned) down to its dqkv rows
+        head_input_grad(sm, PT + kHeadT, sm.z);
+        __syncthreads();
+        bwd_layer<kActorTrunk, 0, true, 36, NoHook, kBwdNoDx>(sm, P, PT, io.L[0], b0, nullptr, nullptr, nullptr,
+                                                                nullptr, NoHook{}, 0, blk * S);
+    }
+}
+
+// The 16 [dq | dk | dv] rows of position s -> sm.big rows p (stride LDQ); with_q = false: a pruned
+// layer off its query position (dq never written there: zero)
+__device__ __forceinline__ void ps_dqkv_in(Smem& sm, const float* __restrict__ dqkv, bool with_q, int s, int b0) {
+    for (int i = tid_x(); i < SPW * 96; i += NTHR) {
+        const int p = i / 96, q = i - 96 * p;
+        f32x4 v = ld4(dqkv + (size_t)trow(s * SPW + p, b0) * 3 * D + 4 * q);
+        if (!with_q && q < 32) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        st4(sm.big + p * LDQ + 4 * q, v);
+    }
+}
+// dL/d(layer input) of position s = W_in^T [dq | dk | dv] (sm.big, ps_dqkv_in) + the residual rows
+// res + p * res_ld (nullptr: none) -> sm.h rows 16 s + p
+__device__ void ps_dx(Smem& sm, const float* __restrict__ WinT, bool with_q, const float* __restrict__ res, int res_ld,
+                      int s) {
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
+    const int fo = 16 * wv + 4 * g;
+    f32x4 acc[1];
+    zero(acc);
+#pragma unroll
+    for (int part = 0; part < 3; ++part) {
+        if (part == 0 && !with_q) continue;
+        gemm_tile<1, 4>(acc, prefetch<4>(WinT, 3 * D, 16 * wv, part * D), WinT, 3 * D, 16 * wv, part * D,
+                        sm.big + part * D, LDQ, 0);
+    }
+    f32x4 v = acc[0];
+    if (res) v += ld4(res + (size_t)i16 * res_ld + fo);
+    st4(sm.h + (s * SPW + i16) * LDH + fo, v);
+}
+
+// Embedding backward of position s from sm.h rows 16 s + p = dL/d(h0): thread = (feature, token
+// group of 4); the [pos | We | be] partial row of (block, position) -> part (only pos row s nonzero).
+__device__ void ps_embed_bwd(Smem& sm, const float* __restrict__ e, const float* __restrict__ xg,
+                             float* __restrict__ part, int s, int b0) {
+    const int f = tid_x() & (D - 1), grp = tid_x() >> 7;
+    if (tid_x() < SPW * LDX / 4) {
+        const int p = tid_x() / (LDX / 4), q = tid_x() % (LDX / 4);
+        st4(sm.x + p * LDX + 4 * q, ld4(xg + (size_t)trow(s * SPW + p, b0) * 16 + 4 * q));
+    }
+    float ev[SPW / 4];
+#pragma unroll
+    for (int i = 0; i < SPW / 4; ++i) ev[i] = e[(size_t)trow(s * SPW + grp + 4 * i, b0) * D + f];
+    __syncthreads();
+    float acc[IN + 1], accp = 0.f;
+#pragma unroll
+    for (int v = 0; v < IN + 1; ++v) acc[v] = 0.f;
+#pragma unroll
+    for (int i = 0; i < SPW / 4; ++i) {
+        const int p = grp + 4 * i;
+        const float gv = sm.h[(s * SPW + p) * LDH + f];
+        accp += gv;
+        const float gp = ev[i] > 0.f ? gv : 0.f;
+        acc[IN] += gp;
+#pragma unroll
+        for (int q = 0; q < LDX / 4; ++q) {
+            const f32x4 x4 = ld4(sm.x + p * LDX + 4 * q);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (4 * q + k < IN) acc[4 * q + k] += gp * x4[k];
+        }
+    }
+    constexpr int NV = IN + 1 + S;  // 20
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+        sm.big[(grp * NV + v) * D + f] = v <= IN ? acc[v] : (v == IN + 1 + s ? accp : 0.f);
+    __syncthreads();
+    for (int o = tid_x(); o < NV * D; o += NTHR) {
+        const int v = o >> 7, ff = o & (D - 1);
+        const float sum = (sm.big[v * D + ff] + sm.big[(NV + v) * D + ff]) +
+                          (sm.big[(2 * NV + v) * D + ff] + sm.big[(3 * NV + v) * D + ff]);
+        const int dst = v < IN ? S * D + ff * IN + v : (v == IN ? S * D + D * IN + ff : (v - IN - 1) * D + ff);
+        part[dst] = sum;
+    }
+}
+
+__global__ __launch_bounds__(NTHR) void k_ps_b2(const float* __restrict__ P, const float* __restrict__ PT,
+                                                const BwdIO io, float* __restrict__ kvc) {
+    __shared__ __attribute__((aligned(16))) Smem sm;
+    if (tid_x() >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
+    const int blk = blockIdx.x / 10, r = blockIdx.x % 10, s = r % S, b0 = blk * SPW, prow = blk * S + s;
+    const bool critic = r >= S, q4 = s == S - 1;
+    ps_mask(sm, io.mask, b0);
+    // dL/d(input of the trunk's top, pruned layer) at position s; its residual path (LN1's input
+    // gradient, compact [b] rows) exists at the query position 4 only
+    const BwdLayerIO& top = io.L[critic ? 2 : 0];
+    ps_dqkv_in(sm, top.dqkv, q4, s, b0);
+    __syncthreads();
+    ps_dx(sm, PT + (critic ? 2 : 0) * kLayerT + kTWin, q4, q4 ? top.dz1 + (size_t)b0 * D : nullptr, D, s);
+    __syncthreads();
+    if (!critic) {
+        ps_embed_bwd(sm, io.e[0], io.xg, io.epart + (size_t)prow * 2 * kEmbPart, s, b0);
+        return;
+    }
+    bwd_layer<kCriticTrunk, 0, false, 20, NoHook, kBwdPos>(sm, P, PT + kLayerT, io.L[1], b0, nullptr, nullptr, nullptr,
+                                                              nullptr, NoHook{}, s * SPW, prow, kvc);
+}
+
+__global__ __launch_bounds__(NTHR) void k_ps_b3(const float* __restrict__ PT, const BwdIO io,
+                                                const float* __restrict__ kvc) {
+    __shared__ __attribute__((aligned(16))) Smem sm;
+    const int blk = blockIdx.x / S, j = blockIdx.x % S, b0 = blk * SPW, prow = blk * S + j;
+    // [dq | dk | dv] rows of position j: dq from B2 (position j), dk / dv = the five query
+    // positions' shares summed in position order (deterministic); dk / dv -> the dqkv rows
+    float* dqkv = io.L[1].dqkv;
+    for (int i = tid_x(); i < SPW * 96; i += NTHR) {
+        const int p = i / 96, q = i - 96 * p, tok = j * SPW + p;
+        const size_t row = (size_t)trow(tok, b0);
+        f32x4 v;
+        if (q < 32) {
+            v = ld4(dqkv + row * 3 * D + 4 * q);
+        } else {
+            v = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < S; ++s) v += ld4(kvc + ((size_t)(blk * S + s) * TOK + tok) * 2 * D + 4 * (q - 32));
+            st4(dqkv + row * 3 * D + 4 * q, v);
+        }
+        st4(sm.big + p * LDQ + 4 * q, v);
+    }
+    __syncthreads();
+    // + LN1's input gradient of layer 0 at position j (the residual path)
+    ps_dx(sm, PT + kLayerT + kTWin, true, io.L[1].dz1 + (size_t)trow(j * SPW, b0) * D, S * D, j);
+    __syncthreads();
+    ps_embed_bwd(sm, io.e[1], io.xg, io.epart + ((size_t)prow * 2 + 1) * kEmbPart, j, b0);
+}
+
 
 }  // namespace pol
 }  // namespace uavhip
@@ -2091,6 +2445,26 @@ int policy_forward_train(const float* packed, const float* states, const TrainIO
 int policy_loss_partials(const TrainIO& io, int Bm, hipStream_t st) {
     hipLaunchKernelGGL(k_loss_partials, dim3(Bm / SPW), dim3(64), 0, st, io);
     return check_launch("k_loss_partials");
+}
+
+int policy_forward_ps(const float* packed, const float* states, const TrainIO& io, int Bm, hipStream_t st) {
+    const int nblk = Bm / SPW;
+    hipLaunchKernelGGL(k_ps_f1, dim3(nblk * 10), dim3(NTHR), 0, st, packed, states, Bm, io);
+    if (const int rc = check_launch("k_ps_f1")) return rc;
+    hipLaunchKernelGGL(k_ps_f2, dim3(nblk * 6), dim3(NTHR), 0, st, packed, io);
+    if (const int rc = check_launch("k_ps_f2")) return rc;
+    hipLaunchKernelGGL(k_ps_f3, dim3(nblk), dim3(NTHR), 0, st, packed, io);
+    return check_launch("k_ps_f3");
+}
+
+int policy_backward_ps(const float* packed, const float* packedT, const BwdIO& io, float* kvc, int Bm, hipStream_t st) {
+    const int nblk = Bm / SPW;
+    hipLaunchKernelGGL(k_ps_b1, dim3(nblk * 2), dim3(NTHR), 0, st, packed, packedT, io);
+    if (const int rc = check_launch("k_ps_b1")) return rc;
+    hipLaunchKernelGGL(k_ps_b2, dim3(nblk * 10), dim3(NTHR), 0, st, packed, packedT, io, kvc);
+    if (const int rc = check_launch("k_ps_b2")) return rc;
+    hipLaunchKernelGGL(k_ps_b3, dim3(nblk * S), dim3(NTHR), 0, st, packedT, io, static_cast<const float*>(kvc));
+    return check_launch("k_ps_b3");
 }
 
 int policy_backward_train(const float* packed, const float* packedT, const BwdIO& io, int Bm, hipStream_t st) {

@@ -94,6 +94,13 @@ int policy_forward_train(const float* packed, const float* states, const TrainIO
 // Trunk split: the per-workgroup loss partials from smp (k_loss_partials; the same terms and
 // order as the fused forward's).
 int policy_loss_partials(const TrainIO& io, int Bm, hipStream_t st);
+// Position split (K7, policy.hip): small minibatches run every full encoder layer as one workgroup per
+// (16-sample block, window position); partial rows per (block, position) = b * 5 + s, and kvc
+// [Bm / 16 * 5][80][256] carries each query position's share of every position's dk / dv.
+constexpr int kPsMaxBm = 256;
+inline bool ps_capable(int Bm) { return Bm <= kPsMaxBm; }
+int policy_forward_ps(const float* packed, const float* states, const TrainIO& io, int Bm, hipStream_t st);
+int policy_backward_ps(const float* packed, const float* packedT, const BwdIO& io, float* kvc, int Bm, hipStream_t st);
 // Whether a minibatch of Bm samples per step runs trunk-split (both trunks side by side on
 // separate CUs): only while 2 Bm/16 workgroups fit one per CU.
 inline bool trunk_split(int Bm) { return 2 * (Bm / 16) <= 256; }

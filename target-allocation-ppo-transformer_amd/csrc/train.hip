@@ -286,13 +286,15 @@ struct Plan {
     LayerBufs la, lc0, lc1;
     float *z_a, *z_c, *dz_a, *dz_c, *fpart, *hpart, *epart, *sq_part;
     float* wg_part;  // weight-gradient partial tiles [kWgGrid * kWgRuns][kWgSlot]
-    float* bpart;    // [Bm/16][kBiasPart] bias partials of K6
+    float* bpart;    // [prows][kBiasPart] bias partials of K6 / K7
+    float* kvc;      // K7: [prows][80][256] each query position's share of every position's dk | dv
+    int prows;       // partial rows: Bm/16, or 5 Bm/16 (position split: row b * 5 + s)
     float* packed;  // fragment-order copy of the parameters for the fused forward
     float* packedT; // transposed GEMM weights for the fused backward
     size_t total;   // workspace floats
 };
 
-inline void carve_layer(WS& w, LayerBufs& L, int R, int rows) {
+inline void carve_layer(WS& w, LayerBufs& L, int R, int rows, int parts) {
     L.qkv = w.take((size_t)R * 3 * D);
     L.o = w.take((size_t)rows * D);
     L.xhat1 = w.take((size_t)rows * D);
@@ -306,9 +308,8 @@ inline void carve_layer(WS& w, LayerBufs& L, int R, int rows) {
     L.dz1 = w.take((size_t)rows * D);
     L.du = w.take((size_t)rows * FF);
     L.df = w.take((size_t)rows * D);
-    const size_t parts = (size_t)R / (S * 16);  // one partial per 16-sample workgroup of K6
-    L.ln1_part = w.take(parts * 2 * D);
-    L.ln2_part = w.take(parts * 2 * D);
+    L.ln1_part = w.take((size_t)parts * 2 * D);  // one partial row per workgroup of K6 / K7
+    L.ln2_part = w.take((size_t)parts * 2 * D);
 }
 
 inline Plan make_plan(int Bm, float* base) {
@@ -318,6 +319,9 @@ inline Plan make_plan(int Bm, float* base) {
     p.Bm = Bm;
     p.R = Bm * S;
     const int R = p.R;
+    // partial rows: sized for the position split whenever this minibatch may run it (independent
+    // of UAVHIP_POS_SPLIT, so the workspace size never depends on the environment)
+    p.prows = (pol::ps_capable(Bm) ? S : 1) * (Bm / kHeadSamples);
     p.xg = w.take((size_t)R * 16);
     p.mask = w.take(R);
     p.smp = w.take((size_t)Bm * 8);
@@ -325,19 +329,20 @@ inline Plan make_plan(int Bm, float* base) {
     p.h0_a = w.take((size_t)R * D);
     p.e_c = w.take((size_t)R * D);
     p.h0_c = w.take((size_t)R * D);
-    carve_layer(w, p.la, R, Bm);
-    carve_layer(w, p.lc0, R, R);
-    carve_layer(w, p.lc1, R, Bm);
+    carve_layer(w, p.la, R, Bm, p.prows);
+    carve_layer(w, p.lc0, R, R, p.prows);
+    carve_layer(w, p.lc1, R, Bm, p.prows);
     p.z_a = w.take((size_t)Bm * HID);
     p.z_c = w.take((size_t)Bm * HID);
     p.dz_a = w.take((size_t)Bm * HID);
     p.dz_c = w.take((size_t)Bm * HID);
     p.fpart = w.take((size_t)(Bm / kHeadSamples) * 4);
     p.hpart = w.take((size_t)(Bm / kHeadSamples) * kHeadPart);
-    p.epart = w.take((size_t)(Bm / kHeadSamples) * 2 * kEmbPart);
+    p.epart = w.take((size_t)p.prows * 2 * kEmbPart);
     p.sq_part = w.take(1 << 16);
     p.wg_part = w.take((size_t)kWgGrid * kWgRuns * kWgSlot);
-    p.bpart = w.take((size_t)(Bm / kHeadSamples) * pol::kBiasPart);
+    p.bpart = w.take((size_t)p.prows * pol::kBiasPart);
+    p.kvc = pol::ps_capable(Bm) ? w.take((size_t)p.prows * S * kHeadSamples * 2 * D) : nullptr;  // [prows][80][256]
     p.packed = w.take(kOffs.o[kNumParams]);
     p.packedT = w.take(pol::kPackedTFloats);
     p.total = w.off;
@@ -346,6 +351,12 @@ inline Plan make_plan(int Bm, float* base) {
 
 
 inline const float* prm(const uavhip_ppo* c, int i) { return c->params + kOffs.o[i]; }
+
+// Position split (K7) for this minibatch size (UAVHIP_POS_SPLIT=0 turns it off: tests compare both ways).
+inline bool pos_split(int Bm) {
+    const char* e = std::getenv("UAVHIP_POS_SPLIT");
+    return pol::ps_capable(Bm) && !(e && e[0] == '0');
+}
 
 // Trunk split for this minibatch size (UAVHIP_TRUNK_SPLIT=0 turns it off: tests compare both ways).
 inline int split_blocks(int Bm) {
@@ -428,9 +439,13 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
         io.z[1] = p.z_c;
         io.fpart = p.fpart;
         io.eps_clip = c->eps_clip;
-        io.split = split_blocks(Bm);
-        TR_CHECK(pol::policy_forward_train(p.packed, states, io, Bm, st));
-        if (io.split) TR_CHECK(pol::policy_loss_partials(io, Bm, st));
+        if (pos_split(Bm)) {  // K7: F1 / F2 / F3 (F3 writes the loss partials)
+            TR_CHECK(pol::policy_forward_ps(p.packed, states, io, Bm, st));
+        } else {
+            io.split = split_blocks(Bm);
+            TR_CHECK(pol::policy_forward_train(p.packed, states, io, Bm, st));
+            if (io.split) TR_CHECK(pol::policy_loss_partials(io, Bm, st));
+        }
         if (!bwd) {  // with BACKWARD in the same call, K6 sums the partials itself (one launch fewer)
             hipLaunchKernelGGL(k_loss_sums, dim3(1), dim3(64), 0, st, p.fpart, nblk, c->loss_sums);
             TR_CHECK(check_launch("k_loss_sums"));
@@ -461,6 +476,11 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
     const int Bm = p.Bm, R = p.R, nblk = Bm / kHeadSamples;
     const LayerBufs &A = p.la, &C0 = p.lc0, &C1 = p.lc1;
     const int ta = kActorTrunk, tc = kCriticTrunk;
+    // partial rows: K6 one per 16-sample workgroup; K7 one per (block, position), row b * 5 + s, the
+    // per-block layers (actor L0, critic L1: their pruned tails) at row b * 5
+    const bool ps = pos_split(Bm);
+    const int rstep = ps ? S : 1;                 // rows from one block's per-block partial row to the next
+    const int full_parts = ps ? p.prows : nblk;    // critic L0 and the embeddings (K7: every row)
     {
         pol::BwdIO io{};
         io.smp = p.smp;
@@ -485,13 +505,14 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         io.e[0] = p.e_a;
         io.e[1] = p.e_c;
         io.epart = p.epart;
-        io.split = split_blocks(Bm);
+        io.split = ps ? 0 : split_blocks(Bm);
         const LayerBufs* lb[3] = {&A, &C0, &C1};
         for (int i = 0; i < 3; ++i)
             io.L[i] = pol::BwdLayerIO{lb[i]->qkv, lb[i]->xhat1, lb[i]->rstd1, lb[i]->u, lb[i]->xhat2, lb[i]->rstd2,
                                       lb[i]->dqkv, lb[i]->dz1, lb[i]->du, lb[i]->df, lb[i]->ln1_part,
                                       lb[i]->ln2_part, p.bpart + (size_t)i * pol::kBiasLayer};
-        TR_CHECK(pol::policy_backward_train(p.packed, p.packedT, io, Bm, st));
+        if (ps) TR_CHECK(pol::policy_backward_ps(p.packed, p.packedT, io, p.kvc, Bm, st));
+        else TR_CHECK(pol::policy_backward_train(p.packed, p.packedT, io, Bm, st));
     }
 
     // ---------------------------------------------------------------- weight gradients
@@ -552,23 +573,27 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         for (int i = 0; i < 3; ++i) {
             const float* bp = p.bpart + (size_t)i * pol::kBiasLayer;
             const int tr_ = lt[i][0], ly = lt[i][1];
-            seg(bp + pol::kBiasL1, kOffs.o[layer_param(tr_, ly, L1B)], FF, nblk, pol::kBiasPart);
-            seg(bp + pol::kBiasL2, kOffs.o[layer_param(tr_, ly, L2B)], D, nblk, pol::kBiasPart);
-            seg(bp + pol::kBiasOut, kOffs.o[layer_param(tr_, ly, OUTB)], D, nblk, pol::kBiasPart);
-            seg(bp + pol::kBiasIn, kOffs.o[layer_param(tr_, ly, INB)], 3 * D, nblk, pol::kBiasPart);
+            const int np = i == 1 ? full_parts : nblk;
+            const int ps_ = (i == 1 && ps ? 1 : rstep) * pol::kBiasPart;
+            seg(bp + pol::kBiasL1, kOffs.o[layer_param(tr_, ly, L1B)], FF, np, ps_);
+            seg(bp + pol::kBiasL2, kOffs.o[layer_param(tr_, ly, L2B)], D, np, ps_);
+            seg(bp + pol::kBiasOut, kOffs.o[layer_param(tr_, ly, OUTB)], D, np, ps_);
+            seg(bp + pol::kBiasIn, kOffs.o[layer_param(tr_, ly, INB)], 3 * D, np, ps_);
         }
     }
     // LayerNorm weight | bias (adjacent parameters, as in the partial rows)
     const LayerBufs* lbs[3] = {&A, &C0, &C1};
     const int lts[3][2] = {{ta, 0}, {tc, 0}, {tc, 1}};
     for (int i = 0; i < 3; ++i) {
-        seg(lbs[i]->ln1_part, kOffs.o[layer_param(lts[i][0], lts[i][1], N1W)], 2 * D, nblk, 2 * D);
-        seg(lbs[i]->ln2_part, kOffs.o[layer_param(lts[i][0], lts[i][1], N2W)], 2 * D, nblk, 2 * D);
+        const int np = i == 1 ? full_parts : nblk;
+        const int ps_ = (i == 1 && ps ? 1 : rstep) * 2 * D;
+        seg(lbs[i]->ln1_part, kOffs.o[layer_param(lts[i][0], lts[i][1], N1W)], 2 * D, np, ps_);
+        seg(lbs[i]->ln2_part, kOffs.o[layer_param(lts[i][0], lts[i][1], N2W)], 2 * D, np, ps_);
     }
-    // embeddings (pos | We | be per trunk, adjacent parameters)
+    // embeddings (pos | We | be per trunk, adjacent parameters; K7: one row per (block, position))
     for (int trunk = 0; trunk < 2; ++trunk)
-        seg(p.epart + (size_t)trunk * kEmbPart, kOffs.o[(trunk ? kCriticTrunk : kActorTrunk) + POS], kEmbPart, nblk,
-            2 * kEmbPart);
+        seg(p.epart + (size_t)trunk * kEmbPart, kOffs.o[(trunk ? kCriticTrunk : kActorTrunk) + POS], kEmbPart,
+            full_parts, 2 * kEmbPart);
     // heads: head.2 weight | bias (adjacent), head.0 bias
     seg(p.hpart, kOffs.o[kActorHead + 2], 2 * HID + 2, nblk, kHeadPart);
     seg(p.hpart + 2 * HID + 2, kOffs.o[kCriticHead + 2], HID + 1, nblk, kHeadPart);

@@ -17,6 +17,11 @@ that, plus the fp32 rounding of the update itself -- large where an element's gr
 against e (Adam normalises rounding noise up to a full lr-sized step: the in_proj key bias, whose
 gradient softmax cancels exactly, is the extreme case), tiny where the gradient is large.
 
+The GPU tests give the bound the actual elementwise difference of the two sides' clipped gradients
+of the step (and check that difference against the kernels' gradient bar separately), so the step
+check is the update arithmetic against the gradients it was given; without a g_other, e is the
+a-priori grad_error() below.
+
 Without teacher forcing no such bound exists: an element Adam moved by a rounding-sized gradient
 changes every later gradient (the feedback is first order through the Hessian, not negligible), so
 multi-step comparisons are only meaningful between deterministic runs (measured + margin).
@@ -46,10 +51,10 @@ class AdamStepBound:
     def __init__(self, segments, lr, betas=(0.9, 0.999), eps=1e-8, rel=1e-4, abs_=1e-7):
         self.segs, self.lr = list(segments), lr.double()
         self.b1, self.b2, self.eps, self.rel, self.abs = betas[0], betas[1], eps, rel, abs_
-        self.worst = {}
+        self.worst, self.worst_grad = {}, {}
 
     def grad_error(self, g):
-        g = g.double()
+        g = g.double().cpu()
         e = torch.zeros_like(g)
         err2 = 0.0
         for _, o, n in self.segs:
@@ -59,38 +64,61 @@ class AdamStepBound:
         gn = float(g.norm())
         return e + g.abs() * (math.sqrt(err2) / gn if gn > 0 else 0.0)  # clip_grad_norm_ coefficient
 
-    def bound(self, t, g, m, v):
+    def bound(self, t, g, m, v, e=None):
         """The reference's state after its step t (1-based): clipped gradient g, exp_avg m,
-        exp_avg_sq v -> per-element bound on |d parameter| of this step."""
-        m, v = m.double(), v.double()
-        e = self.grad_error(g)
+        exp_avg_sq v; e: elementwise bound on how far the other side's g_t is off (default: the
+        a-priori grad_error(g)) -> per-element bound on |d parameter| of this step."""
+        g, m, v = g.double().cpu(), m.double().cpu(), v.double().cpu()
+        e = self.grad_error(g) if e is None else e.double().cpu()
         w1 = (1 - self.b1) / (1 - self.b1 ** t)
         w2 = math.sqrt((1 - self.b2) / (1 - self.b2 ** t))
         s = (v / (1 - self.b2 ** t)).sqrt()
         u = (m / (1 - self.b1 ** t)) / (s + self.eps)
         du = e * (w1 + w2 * u.abs()) / ((s - w2 * e).clamp(min=0) + self.eps)
         du = torch.minimum(du, u.abs() + umax(t, self.b1, self.b2))
-        return self.lr * du
+        return self.lr.cpu() * du
 
-    def check(self, t, g, m, v, got, want, p_before, label=""):
+    def check(self, t, g, m, v, got, want, p_before, label="", g_other=None, grad_rel=5e-5):
         """|got - want| <= bound + fp32 rounding of both updates (2 ulp of the parameter before and
-        after, 1e-6 lr), element by element; records the worst |d| / bound per tensor."""
-        got, want, p0 = got.double(), want.double(), p_before.double()
-        tol = self.bound(t, g, m, v) + 2.0 ** -22 * (want.abs() + p0.abs()) + 1e-6 * self.lr
+        after, 1e-6 lr), element by element; records the worst |d| / bound per tensor.
+        g_other: the other side's clipped gradient of this step. Then (a) it must agree with g to
+        grad_rel of each tensor's max |g| (the kernels' gradient bar) and (b) the bound is taken
+        from the actual elementwise gradient difference (+ 1e-6 relative slack for the clip
+        coefficient) -- the update arithmetic checked against the gradients it was given."""
+        got, want, p0 = got.double().cpu(), want.double().cpu(), p_before.double().cpu()
+        gd = g.double().cpu()
+        e = None
+        if g_other is not None:
+            go = g_other.double().cpu()
+            diff = (go - gd).abs()
+            for name, o, n in self.segs:
+                scale = float(gd[o:o + n].abs().max())
+                err = float(diff[o:o + n].max())
+                self.worst_grad[name] = max(self.worst_grad.get(name, 0.0), err / max(scale, 1e-30))
+                assert err <= grad_rel * scale + 1e-7, f"{label} step {t} {name}: gradient |d| {err:.3e} vs max {scale:.3e}"
+            e = diff + 1e-6 * gd.abs() + 1e-12
+        b = self.bound(t, gd, m, v, e)
+        tol = b + 2.0 ** -22 * (want.abs() + p0.abs()) + 1e-6 * self.lr.cpu()
         d = (got - want).abs()
         for name, o, n in self.segs:
             r = float((d[o:o + n] / tol[o:o + n]).max())
             self.worst[name] = max(self.worst.get(name, 0.0), r)
             bad = d[o:o + n] > tol[o:o + n]
             if bool(bad.any()):
-                i = int(bad.nonzero()[0])
-                raise AssertionError(f"{label} step {t} {name}[{i}]: |d| {float(d[o + i]):.3e} > bound "
-                                     f"{float(tol[o + i]):.3e} ({int(bad.sum())} elements over)")
+                i = o + int(bad.nonzero()[0])
+                vs = float((v.double().cpu()[i] / (1 - self.b2 ** t)) ** 0.5)
+                raise AssertionError(f"{label} step {t} {name}[{i - o}]: |d| {float(d[i]):.3e} > bound {float(tol[i]):.3e} "
+                                     f"({int(bad.sum())} elements over; g {float(gd[i]):.3e}, s {vs:.3e}, "
+                                     f"m {float(m[i]):.3e}, e {float(e[i]) if e is not None else float('nan'):.3e})")
         return tol
 
     def report(self):
         k = max(self.worst, key=self.worst.get)
-        print(f"Adam step: max |d| / bound = {self.worst[k]:.3e} ({k})")
+        msg = f"Adam step: max |d| / bound = {self.worst[k]:.3e} ({k})"
+        if self.worst_grad:
+            kg = max(self.worst_grad, key=self.worst_grad.get)
+            msg += f"; max gradient |d| / max |g| = {self.worst_grad[kg]:.3e} ({kg})"
+        print(msg)
         return self.worst[k]
 
 
@@ -124,8 +152,7 @@ def torch_step_bound(policy, optimizer, **kw):
         for p in gr["params"]:
             lr_of[p] = gr["lr"]
     _, segs = flatten_named(named)
-    lr = torch.cat([torch.full((p.numel(),), float(lr_of[p]), dtype=torch.float64, device=p.device)
-                    for _, p in named])
+    lr = torch.cat([torch.full((p.numel(),), float(lr_of[p]), dtype=torch.float64) for _, p in named])
     gr = optimizer.param_groups[0]
     return AdamStepBound(segs, lr, betas=gr["betas"], eps=gr["eps"], **kw)
 
@@ -138,7 +165,7 @@ def trainer_step_bound(trainer, **kw):
     named = list(trainer.policy.state_dict().items())
     segs = [(k, o, v.numel()) for (k, v), o in zip(named, offs)]
     d = trainer.desc
-    lr = torch.full((n,), float(d.lr_critic), dtype=torch.float64, device=trainer.params.device)
+    lr = torch.full((n,), float(d.lr_critic), dtype=torch.float64)
     critic0 = min(o for k, o, _ in segs if k.startswith("critic"))
     lr[:critic0] = float(d.lr_actor)
     return AdamStepBound(segs, lr, betas=(d.beta1, d.beta2), eps=d.adam_eps, **kw)

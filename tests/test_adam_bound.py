@@ -64,9 +64,16 @@ def test_step_bound_covers_perturbed_gradients(k, scale, holds):
     frac = float((sb.bound(t, gr, m, v) / sb.lr).median())
     print(f"t={t}: median bound / lr = {frac:.3e}")
     assert frac < 0.05  # not vacuous
+    g_other = torch.cat([p.grad.reshape(-1) for p in other.parameters()])
     if holds:
-        sb.check(t, gr, m, v, got, want, p0)
+        sb.check(t, gr, m, v, got, want, p0)  # the a-priori bound (rel = 1e-4 of max |g|)
+        sb.check(t, gr, m, v, got, want, p0, g_other=g_other)  # the bound from the actual gradient difference
         sb.report()
     else:
         with pytest.raises(AssertionError):
             sb.check(t, gr, m, v, got, want, p0)
+    # the actual-difference bound holds even for the large perturbation (the gradient bar is then
+    # what catches it)
+    with pytest.raises(AssertionError, match="gradient"):
+        sb.check(t, gr, m, v, got, want, p0, g_other=g_other, grad_rel=scale / 10)
+    sb.check(t, gr, m, v, got, want, p0, g_other=g_other, grad_rel=2 * scale)

