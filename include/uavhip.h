@@ -347,7 +347,10 @@ typedef struct uavhip_ppo {
     int32_t n_floats;
     int32_t minibatch;   /* samples per step on this rank, multiple of 64 */
     int32_t global_minibatch; /* samples per step over all ranks (0: = minibatch) */
-    float lr_actor, lr_critic, beta1, beta2, adam_eps; /* 2e-4, 1e-3, 0.9, 0.999, 1e-8 */
+    /* torch.optim.Adam's hyper-parameters as torch holds them (Python floats = doubles): the bias
+       corrections and step size are formed in double and the per-element coefficients rounded to
+       float once, exactly as torch's single-tensor Adam does (agents/ppo.py:17-22) */
+    double lr_actor, lr_critic, beta1, beta2, adam_eps; /* 2e-4, 1e-3, 0.9, 0.999, 1e-8 */
     float eps_clip, max_grad_norm, value_coef, entropy_coef; /* 0.2, 1.0, 0.5, 0.01 */
 } uavhip_ppo;
 
@@ -407,6 +410,8 @@ int uavhip_episode_stats(const double* reward, const uint8_t* done, const int8_t
 
 /* ---------------------------------------------------------------- misc */
 const char* uavhip_last_error(void);
+/* 3 since round 3 (struct uavhip_ppo: the Adam hyper-parameters are doubles); the ctypes binding
+   refuses a library of another version */
 int32_t uavhip_abi_version(void);
 
 #ifdef __cplusplus

@@ -176,7 +176,14 @@ __global__ __launch_bounds__(256) void k_grad_norm(const float* __restrict__ gra
 constexpr int kSqBlocks = 256;
 
 // clip_grad_norm_(max_norm) + torch.optim.Adam (ppo.py:17-22 groups: actor params < critic trunk
-// offset use lr_actor, the rest lr_critic), elementwise over the flat buffers.
+// offset use lr_actor, the rest lr_critic), elementwise over the flat buffers, in the operation order
+// and roundings of torch's single-tensor Adam (torch/optim/adam.py, the CPU path the reference runs):
+//   m = lerp(m, g, 1 - b1)            = fma(w1, g - m, m)       (the vectorised lerp, weight < 0.5)
+//   v = v * b2;  v = addcmul(v, g, g, 1 - b2) = v + ((1 - b2) g) g
+//   denom = sqrt(v) / sqrt(1 - b2^t) + eps
+//   p = addcdiv(p, m, denom, -lr / (1 - b1^t)) = p + ((-step) m) / denom
+// with the bias corrections and step size in double from the double hyper-parameters and each
+// coefficient rounded to float once; no other contraction (explicit _rn operations).
 // The updated float4 of flat params at f -> the forward's fragment-order copy (packed) and the
 // backward's transposed copies (packedT): k_policy_pack's mapping inverted, so an UPDATE leaves
 // both current and the next FORWARD may skip the pack launch (UAVHIP_PPO_PACKED).
@@ -228,33 +235,44 @@ struct AdamArgs {
     const double* step;
     const float* sq_part;
     int n_sq, n, critic_begin;
-    float lr_actor, lr_critic, beta1, beta2, eps, max_norm;
+    double lr_actor, lr_critic, beta1, beta2, eps;
+    float max_norm;
     float *packed, *packedT;  // nullable: refreshed with the updated params (pack_scatter)
 };
 __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     __shared__ float red[4];
-    float s = 0.f;
-    for (int i = threadIdx.x; i < a.n_sq; i += 256) s += a.sq_part[i];
+    // the g^2 block partials (~2k): 8 independent loads in flight per thread, not a dependent chain
+    float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = threadIdx.x; i < a.n_sq; i += 8 * 256) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i + 256 * u < a.n_sq) s8[u] += a.sq_part[i + 256 * u];
+    }
+    float s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     s = wave_sum(s);
     if (lane_id() == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
     const float norm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
     const float coef = fminf(a.max_norm / (norm + 1e-6f), 1.0f);
     const double t = a.step[0];
-    const double bc1 = 1.0 - pow((double)a.beta1, t);
-    const float bs = (float)sqrt(1.0 - pow((double)a.beta2, t));
-    const float ss_a = (float)((double)a.lr_actor / bc1), ss_c = (float)((double)a.lr_critic / bc1);
+    const double bc1 = 1.0 - pow(a.beta1, t), bc2 = 1.0 - pow(a.beta2, t);
+    const float nss_a = (float)(-(a.lr_actor / bc1)), nss_c = (float)(-(a.lr_critic / bc1));
+    const float bc2s = (float)sqrt(bc2), w1 = (float)(1.0 - a.beta1), b2 = (float)a.beta2;
+    const float w2 = (float)(1.0 - a.beta2), epsf = (float)a.eps;
     for (int i4 = blockIdx.x * 256 + threadIdx.x; 4 * i4 < a.n; i4 += gridDim.x * 256) {
         const int i = 4 * i4;  // n and critic_begin are multiples of 4 (padded layout)
-        const float ss = i < a.critic_begin ? ss_a : ss_c;
+        const float nss = i < a.critic_begin ? nss_a : nss_c;
         f32x4 g = *reinterpret_cast<const f32x4*>(a.grads + i) * coef;
         f32x4 m = *reinterpret_cast<const f32x4*>(a.m + i);
         f32x4 v = *reinterpret_cast<const f32x4*>(a.v + i);
         f32x4 p = *reinterpret_cast<const f32x4*>(a.params + i);
-        m = m + (1.f - a.beta1) * (g - m);
-        v = v * a.beta2 + (1.f - a.beta2) * (g * g);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) p[j] = p[j] + (-ss) * (m[j] / (sqrtf(v[j]) / bs + a.eps));
+        for (int j = 0; j < 4; ++j) {
+            m[j] = __fmaf_rn(w1, __fsub_rn(g[j], m[j]), m[j]);  // torch's vectorised lerp: one fma
+            v[j] = __fadd_rn(__fmul_rn(v[j], b2), __fmul_rn(__fmul_rn(w2, g[j]), g[j]));
+            const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v[j]), bc2s), epsf);
+            p[j] = __fadd_rn(p[j], __fdiv_rn(__fmul_rn(nss, m[j]), denom));
+        }
         *reinterpret_cast<f32x4*>(a.grads + i) = g;
         *reinterpret_cast<f32x4*>(a.m + i) = m;
         *reinterpret_cast<f32x4*>(a.v + i) = v;

@@ -68,8 +68,8 @@ class PPODesc(ctypes.Structure):
     _fields_ = [("params", _vp), ("grads", _vp), ("adam_m", _vp), ("adam_v", _vp), ("adam_step", _vp),
                 ("workspace", _vp), ("loss_sums", _vp), ("stats", _vp), ("n_floats", _i32), ("minibatch", _i32),
                 ("global_minibatch", _i32)] + \
-              [(n, ctypes.c_float) for n in ("lr_actor", "lr_critic", "beta1", "beta2", "adam_eps", "eps_clip",
-                                             "max_grad_norm", "value_coef", "entropy_coef")]
+              [(n, ctypes.c_double) for n in ("lr_actor", "lr_critic", "beta1", "beta2", "adam_eps")] + \
+              [(n, ctypes.c_float) for n in ("eps_clip", "max_grad_norm", "value_coef", "entropy_coef")]
 
 
 # name -> (restype, argtypes)
@@ -113,6 +113,9 @@ class UavHipError(RuntimeError):
     pass
 
 
+ABI_VERSION = 3  # include/uavhip.h uavhip_abi_version
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libuavhip.so not built at {LIB_PATH}: run `make -C "
@@ -124,6 +127,9 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.uavhip_abi_version() != ABI_VERSION:  # a stale build would misread the descriptors
+        raise ImportError(f"{LIB_PATH}: ABI version {lib.uavhip_abi_version()}, this binding needs {ABI_VERSION}: "
+                          f"rebuild (make -C target-allocation-ppo-transformer_amd/csrc)")
     return lib
 
 

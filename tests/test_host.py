@@ -43,7 +43,7 @@ def test_library_exports_every_header_symbol():
     for f in fns:
         assert hasattr(_lib.LIB, f), f
     assert set(fns) == set(_lib.EXPORTS)
-    assert _lib.LIB.uavhip_abi_version() == 2
+    assert _lib.LIB.uavhip_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_ctypes_mirrors_header_enums():
@@ -83,9 +83,30 @@ def _struct_fields(name):
     return out
 
 
+def _struct_types(name):
+    """[(field, C type)] of a header struct (pointers as 'ptr')."""
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), txt, re.S).group(1)
+    out = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        base = decl.split()[0] if not decl.startswith("const") else decl.split()[1]
+        for part in decl.split(","):
+            nm = re.findall(r"\w+", part.replace("*", " "))[-1]
+            out.append((nm, "ptr" if "*" in part or ("*" in decl and part is decl.split(",")[0]) else base))
+    return out
+
+
 def test_ctypes_mirrors_header_structs():
+    import ctypes
     from uavhip import _lib
     assert _struct_fields("uavhip_ppo") == [f[0] for f in _lib.PPODesc._fields_]
+    # and the field types: the Adam hyper-parameters are doubles (torch's Python floats)
+    kinds = {"float": ctypes.c_float, "double": ctypes.c_double, "int32_t": ctypes.c_int32, "ptr": ctypes.c_void_p}
+    for (nm, ty), (fn, ft) in zip(_struct_types("uavhip_ppo"), _lib.PPODesc._fields_):
+        assert nm == fn and ft is kinds[ty], (nm, ty, ft)
     assert _struct_fields("uavhip_policy") == [f[0] for f in _lib.PolicyDesc._fields_]
     assert _lib.LIB.uavhip_ppo_workspace_floats(64) > 0
     assert _lib.LIB.uavhip_ppo_workspace_floats(4096) > _lib.LIB.uavhip_ppo_workspace_floats(64)
