@@ -243,6 +243,10 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     __shared__ float red[4];
     // the g^2 block partials (~2k): 8 independent loads in flight per thread, not a dependent chain
     float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#if defined(UAVHIP_EXP) && (UAVHIP_EXP == 101 || UAVHIP_EXP == 104)
+    if (threadIdx.x == 0) s8[0] = a.sq_part[0];
+    if (0)
+#endif
     for (int i = threadIdx.x; i < a.n_sq; i += 8 * 256) {
 #pragma unroll
         for (int u = 0; u < 8; ++u)
@@ -255,7 +259,11 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     const float norm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
     const float coef = fminf(a.max_norm / (norm + 1e-6f), 1.0f);
     const double t = a.step[0];
+#if defined(UAVHIP_EXP) && (UAVHIP_EXP == 103 || UAVHIP_EXP == 104)
+    const double bc1 = 1.0 - a.beta1 * t, bc2 = 1.0 - a.beta2 * t;
+#else
     const double bc1 = 1.0 - pow(a.beta1, t), bc2 = 1.0 - pow(a.beta2, t);
+#endif
     const float nss_a = (float)(-(a.lr_actor / bc1)), nss_c = (float)(-(a.lr_critic / bc1));
     const float bc2s = (float)sqrt(bc2), w1 = (float)(1.0 - a.beta1), b2 = (float)a.beta2;
     const float w2 = (float)(1.0 - a.beta2), epsf = (float)a.eps;
@@ -277,7 +285,11 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
         *reinterpret_cast<f32x4*>(a.m + i) = m;
         *reinterpret_cast<f32x4*>(a.v + i) = v;
         *reinterpret_cast<f32x4*>(a.params + i) = p;
+#if defined(UAVHIP_EXP) && (UAVHIP_EXP == 102 || UAVHIP_EXP == 104)
+        if (a.packed) *reinterpret_cast<f32x4*>(a.packed + i) = p;
+#else
         if (a.packed) pack_scatter(a.packed, a.packedT, i, p);
+#endif
     }
 }
 
