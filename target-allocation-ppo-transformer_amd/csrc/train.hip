@@ -80,6 +80,22 @@ __global__ __launch_bounds__(64) void k_loss_sums(const float* __restrict__ part
 using pol::kEmbPart;
 
 // ================================================================== gradient reduction + Adam
+// Adam's per-step scalars, computed once by the block that advances the step counter (block 0 of
+// k_reduce_grads or k_grad_norm): the bias corrections in double from the double hyper-parameters
+// (torch's non-capturable single-tensor Adam), each coefficient rounded to float once.
+struct AdamHyper {
+    double lr_actor, lr_critic, beta1, beta2;
+};
+struct AdamScalars {
+    float nss_a, nss_c, bc2s, pad;  // -lr / (1 - b1^t) per group, sqrt(1 - b2^t)
+};
+__device__ __forceinline__ void adam_advance(double* __restrict__ step, const AdamHyper& h, AdamScalars* __restrict__ sc) {
+    const double t = step[0] + 1.0;
+    step[0] = t;
+    const double bc1 = 1.0 - pow(h.beta1, t), bc2 = 1.0 - pow(h.beta2, t);
+    *sc = AdamScalars{(float)(-(h.lr_actor / bc1)), (float)(-(h.lr_critic / bc1)), (float)sqrt(bc2), 0.f};
+}
+
 // grads[dst + i] = sum_p src[p * part_stride + i] for each segment; block partial sums of g^2.
 // Few parts (split-K slabs): one thread per element. Many parts (per-workgroup partials of K6 /
 // the heads): a block takes 64 consecutive elements, each wave every 4th part, so every load is a
@@ -97,7 +113,8 @@ struct SegBatch {
     int n;
 };
 __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* __restrict__ grads,
-                                                      float* __restrict__ sq_part, double* __restrict__ step) {
+                                                      float* __restrict__ sq_part, double* __restrict__ step,
+                                                      const AdamHyper h, AdamScalars* __restrict__ sc) {
     __shared__ float red[4];
     __shared__ float wsum[4][64];
     int si = 0, hi = sb.n;  // segment of this block: binary search (each probe is a kernarg load)
@@ -154,14 +171,15 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
     __syncthreads();
     if (threadIdx.x == 0) {
         sq_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
-        if (step && blockIdx.x == 0) step[0] += 1.0;  // single-GPU step: these are the final grads
+        if (step && blockIdx.x == 0) adam_advance(step, h, sc);  // single-GPU step: these are the final grads
     }
 }
 
 // Block partial sums of g^2 over the flat gradient after a cross-rank all-reduce (data-parallel
 // UPDATE phase; a single-GPU step takes them from k_reduce_grads); advances Adam's step counter.
 __global__ __launch_bounds__(256) void k_grad_norm(const float* __restrict__ grads, int n, float* __restrict__ sq_part,
-                                                   double* __restrict__ step) {
+                                                   double* __restrict__ step, const AdamHyper h,
+                                                   AdamScalars* __restrict__ sc) {
     __shared__ float red[4];
     float s = 0.f;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) s += grads[i] * grads[i];
@@ -170,7 +188,7 @@ __global__ __launch_bounds__(256) void k_grad_norm(const float* __restrict__ gra
     __syncthreads();
     if (threadIdx.x == 0) {
         sq_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
-        if (blockIdx.x == 0) step[0] += 1.0;
+        if (blockIdx.x == 0) adam_advance(step, h, sc);
     }
 }
 constexpr int kSqBlocks = 256;
@@ -182,114 +200,143 @@ constexpr int kSqBlocks = 256;
 //   v = v * b2;  v = addcmul(v, g, g, 1 - b2) = v + ((1 - b2) g) g
 //   denom = sqrt(v) / sqrt(1 - b2^t) + eps
 //   p = addcdiv(p, m, denom, -lr / (1 - b1^t)) = p + ((-step) m) / denom
-// with the bias corrections and step size in double from the double hyper-parameters and each
-// coefficient rounded to float once; no other contraction (explicit _rn operations).
-// The updated float4 of flat params at f -> the forward's fragment-order copy (packed) and the
-// backward's transposed copies (packedT): k_policy_pack's mapping inverted, so an UPDATE leaves
-// both current and the next FORWARD may skip the pack launch (UAVHIP_PPO_PACKED).
-__device__ __forceinline__ void pack_scatter(float* __restrict__ packed, float* __restrict__ packedT, int f, f32x4 p) {
-    // parameter lo: kOffs.o[lo] <= f < kOffs.o[lo + 1]; searched once per wave (scalar), then
-    // advanced per lane (a wave's 256 floats cross at most a few small parameters)
-    const int f0 = __builtin_amdgcn_readfirstlane(f);
-    int lo = 0, hi = kNumParams;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (f0 >= kOffs.o[mid]) lo = mid;
-        else hi = mid;
-    }
-    while (lo + 1 < kNumParams && f >= kOffs.o[lo + 1]) ++lo;
-    const int local = f - kOffs.o[lo], K = kTileK[lo];
-    const bool tiled = K != 0 && local < kSizes[lo];
-    int dst = f;
-    if (tiled) {  // [R][K] weight: fragment index ((r/16 * K/16 + k/16) * 64 + r%16 + 16 (k%16)/4) * 4
-        const int r = local / K, k = local - r * K;
-        dst = kOffs.o[lo] + (((r >> 4) * (K >> 4) + (k >> 4)) * 64 + (r & 15) + 16 * ((k & 15) >> 2)) * 4;
-    }
-    *reinterpret_cast<f32x4*>(packed + dst) = p;
-    if (!tiled) return;
-    int base = -1, Rt = D, Kt = D;  // W stored [Kt][Rt]; packedT holds W^T in fragment order
-#pragma unroll
+// with the step-dependent scalars from AdamScalars; no other contraction (explicit _rn operations).
+//
+// Work items: a GEMM weight (kTileK != 0, flat [NR][NC]) in 4 x 4 blocks (rows i0..i0+3, columns
+// j0..j0+3), every other parameter in float4s. Each parameter's items start a new 256-item block,
+// so a block's parameter is a table lookup. A 4 x 4 block refreshes the forward's fragment-order copy
+// (packed: four float4, one per row) and the backward's transposed copy (packedT: four float4, one
+// per column) -- k_policy_pack's mapping inverted, each thread's four stores one contiguous 64 B --
+// so an UPDATE leaves both current and the next FORWARD may skip the pack launch (UAVHIP_PPO_PACKED).
+constexpr int kAdamMaxBlocks = 192;
+struct AdamBlocks {
+    int n;
+    int param[kAdamMaxBlocks];  // parameter of the block
+    int first[kAdamMaxBlocks];  // its first item within the parameter
+    int tbase[kAdamMaxBlocks];  // packedT offset of the parameter's transposed copy, -1: none
+};
+constexpr int adam_items(int q) { return kTileK[q] ? kSizes[q] / 16 : pad4(kSizes[q]) / 4; }
+constexpr int packedT_base(int q) {
     for (int li = 0; li < 3; ++li) {
         const int trunk = li == 0 ? kActorTrunk : kCriticTrunk, layer = li == 2 ? 1 : 0;
-        if (lo == layer_param(trunk, layer, INW)) { base = li * kLayerT + kTWin; Rt = D; Kt = 3 * D; }
-        if (lo == layer_param(trunk, layer, OUTW)) { base = li * kLayerT + kTWo; Rt = D; Kt = D; }
-        if (lo == layer_param(trunk, layer, L1W)) { base = li * kLayerT + kTW1; Rt = D; Kt = FF; }
-        if (lo == layer_param(trunk, layer, L2W)) { base = li * kLayerT + kTW2; Rt = FF; Kt = D; }
+        if (q == layer_param(trunk, layer, INW)) return li * kLayerT + kTWin;
+        if (q == layer_param(trunk, layer, OUTW)) return li * kLayerT + kTWo;
+        if (q == layer_param(trunk, layer, L1W)) return li * kLayerT + kTW1;
+        if (q == layer_param(trunk, layer, L2W)) return li * kLayerT + kTW2;
     }
-    if (lo == kActorHead) { base = kHeadT; Rt = D; Kt = HID; }
-    if (lo == kCriticHead) { base = kHeadT + D * HID; Rt = D; Kt = HID; }
-    if (base < 0) return;
-    const int k = local / Rt, r0 = local - k * Rt;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int r = r0 + j;
-        packedT[base + (((r >> 4) * (Kt >> 4) + (k >> 4)) * 64 + (r & 15) + 16 * ((k & 15) >> 2)) * 4 + (k & 3)] = p[j];
-    }
+    if (q == kActorHead) return kHeadT;
+    if (q == kCriticHead) return kHeadT + D * HID;
+    return -1;
 }
+constexpr AdamBlocks make_adam_blocks() {
+    AdamBlocks b{};
+    for (int q = 0; q < kNumParams; ++q)
+        for (int f = 0; f < adam_items(q); f += 256) {
+            b.param[b.n] = q;
+            b.first[b.n] = f;
+            b.tbase[b.n] = packedT_base(q);
+            ++b.n;
+        }
+    return b;
+}
+constexpr AdamBlocks kAdamBlocks = make_adam_blocks();
+static_assert(kAdamBlocks.n <= kAdamMaxBlocks, "Adam block table");
+static_assert(kTileK[kActorHead] == D && packedT_base(kActorHead) >= 0, "every tiled weight has a transposed copy");
 
 struct AdamArgs {
     float* params;
     float* grads;
     float* m;
     float* v;
-    const double* step;
+    const AdamScalars* sc;
     const float* sq_part;
-    int n_sq, n, critic_begin;
-    double lr_actor, lr_critic, beta1, beta2, eps;
+    int n_sq;
+    double beta1, beta2, eps;
     float max_norm;
-    float *packed, *packedT;  // nullable: refreshed with the updated params (pack_scatter)
+    float *packed, *packedT;  // nullable: refreshed with the updated params
 };
+
+__device__ __forceinline__ void adam4(f32x4& p, f32x4& m, f32x4& v, const f32x4 g, float nss, float bc2s, float w1,
+                                      float b2, float w2, float epsf) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        m[j] = __fmaf_rn(w1, __fsub_rn(g[j], m[j]), m[j]);  // torch's vectorised lerp: one fma
+        v[j] = __fadd_rn(__fmul_rn(v[j], b2), __fmul_rn(__fmul_rn(w2, g[j]), g[j]));
+        const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v[j]), bc2s), epsf);
+        p[j] = __fadd_rn(p[j], __fdiv_rn(__fmul_rn(nss, m[j]), denom));
+    }
+}
+
 __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     __shared__ float red[4];
+    const int q = kAdamBlocks.param[blockIdx.x];
+    const int item = kAdamBlocks.first[blockIdx.x] + threadIdx.x;
+    const int NC = kTileK[q], off = kOffs.o[q];
+    const bool tiled = NC != 0;
+    const bool live = item < adam_items(q);
+    // this thread's elements: rows i0..i0+3 x columns j0..j0+3 (tiled) or one float4 (nrow = 1);
+    // loaded before the g^2 partials so both latencies overlap
+    const int i0 = tiled ? 4 * (item / (NC / 4)) : 0, j0 = tiled ? 4 * (item % (NC / 4)) : 0;
+    const int nrow = tiled ? 4 : 1;
+    f32x4 g[4], m[4], v[4], p[4];
+    auto at = [&](int r) { return tiled ? off + (i0 + r) * NC + j0 : off + 4 * item; };
+    if (live) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (r < nrow) {
+                g[r] = *reinterpret_cast<const f32x4*>(a.grads + at(r));
+                m[r] = *reinterpret_cast<const f32x4*>(a.m + at(r));
+                v[r] = *reinterpret_cast<const f32x4*>(a.v + at(r));
+                p[r] = *reinterpret_cast<const f32x4*>(a.params + at(r));
+            }
+    }
     // the g^2 block partials (~2k): 8 independent loads in flight per thread, not a dependent chain
     float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#if defined(UAVHIP_EXP) && (UAVHIP_EXP == 101 || UAVHIP_EXP == 104)
-    if (threadIdx.x == 0) s8[0] = a.sq_part[0];
-    if (0)
-#endif
     for (int i = threadIdx.x; i < a.n_sq; i += 8 * 256) {
 #pragma unroll
         for (int u = 0; u < 8; ++u)
             if (i + 256 * u < a.n_sq) s8[u] += a.sq_part[i + 256 * u];
     }
+    const AdamScalars sc = *a.sc;
     float s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     s = wave_sum(s);
     if (lane_id() == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
+    if (!live) return;
     const float norm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
     const float coef = fminf(a.max_norm / (norm + 1e-6f), 1.0f);
-    const double t = a.step[0];
-#if defined(UAVHIP_EXP) && (UAVHIP_EXP == 103 || UAVHIP_EXP == 104)
-    const double bc1 = 1.0 - a.beta1 * t, bc2 = 1.0 - a.beta2 * t;
-#else
-    const double bc1 = 1.0 - pow(a.beta1, t), bc2 = 1.0 - pow(a.beta2, t);
-#endif
-    const float nss_a = (float)(-(a.lr_actor / bc1)), nss_c = (float)(-(a.lr_critic / bc1));
-    const float bc2s = (float)sqrt(bc2), w1 = (float)(1.0 - a.beta1), b2 = (float)a.beta2;
-    const float w2 = (float)(1.0 - a.beta2), epsf = (float)a.eps;
-    for (int i4 = blockIdx.x * 256 + threadIdx.x; 4 * i4 < a.n; i4 += gridDim.x * 256) {
-        const int i = 4 * i4;  // n and critic_begin are multiples of 4 (padded layout)
-        const float nss = i < a.critic_begin ? nss_a : nss_c;
-        f32x4 g = *reinterpret_cast<const f32x4*>(a.grads + i) * coef;
-        f32x4 m = *reinterpret_cast<const f32x4*>(a.m + i);
-        f32x4 v = *reinterpret_cast<const f32x4*>(a.v + i);
-        f32x4 p = *reinterpret_cast<const f32x4*>(a.params + i);
+    const float nss = q < kCriticTrunk ? sc.nss_a : sc.nss_c;
+    const float w1 = (float)(1.0 - a.beta1), b2 = (float)a.beta2, w2 = (float)(1.0 - a.beta2), epsf = (float)a.eps;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            m[j] = __fmaf_rn(w1, __fsub_rn(g[j], m[j]), m[j]);  // torch's vectorised lerp: one fma
-            v[j] = __fadd_rn(__fmul_rn(v[j], b2), __fmul_rn(__fmul_rn(w2, g[j]), g[j]));
-            const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v[j]), bc2s), epsf);
-            p[j] = __fadd_rn(p[j], __fdiv_rn(__fmul_rn(nss, m[j]), denom));
+    for (int r = 0; r < 4; ++r)
+        if (r < nrow) {
+            g[r] = g[r] * coef;
+            adam4(p[r], m[r], v[r], g[r], nss, sc.bc2s, w1, b2, w2, epsf);
+            *reinterpret_cast<f32x4*>(a.grads + at(r)) = g[r];
+            *reinterpret_cast<f32x4*>(a.m + at(r)) = m[r];
+            *reinterpret_cast<f32x4*>(a.v + at(r)) = v[r];
+            *reinterpret_cast<f32x4*>(a.params + at(r)) = p[r];
         }
-        *reinterpret_cast<f32x4*>(a.grads + i) = g;
-        *reinterpret_cast<f32x4*>(a.m + i) = m;
-        *reinterpret_cast<f32x4*>(a.v + i) = v;
-        *reinterpret_cast<f32x4*>(a.params + i) = p;
-#if defined(UAVHIP_EXP) && (UAVHIP_EXP == 102 || UAVHIP_EXP == 104)
-        if (a.packed) *reinterpret_cast<f32x4*>(a.packed + i) = p;
-#else
-        if (a.packed) pack_scatter(a.packed, a.packedT, i, p);
-#endif
+    if (!a.packed) return;
+    if (!tiled) {  // plain parameters are copied as they are
+        *reinterpret_cast<f32x4*>(a.packed + at(0)) = p[0];
+        return;
+    }
+    // packed: row i of [NR][NC] in fragment order, float4 = columns j0..j0+3
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = i0 + r;
+        *reinterpret_cast<f32x4*>(a.packed + off + (((i >> 4) * (NC >> 4) + (j0 >> 4)) * 64 + (i & 15) +
+                                                      16 * ((j0 & 15) >> 2)) * 4) = p[r];
+    }
+    // packedT: W^T ([NC][NR]) in fragment order, float4 = rows i0..i0+3 of column j
+    const int NR = kSizes[q] / NC, tb = kAdamBlocks.tbase[blockIdx.x];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int j = j0 + c;
+        *reinterpret_cast<f32x4*>(a.packedT + tb + (((j >> 4) * (NR >> 4) + (i0 >> 4)) * 64 + (j & 15) +
+                                                     16 * ((i0 & 15) >> 2)) * 4) =
+            f32x4{p[0][c], p[1][c], p[2][c], p[3][c]};
     }
 }
 
@@ -315,6 +362,7 @@ struct Plan {
     float *xg, *mask, *smp, *e_a, *h0_a, *e_c, *h0_c;
     LayerBufs la, lc0, lc1;
     float *z_a, *z_c, *dz_a, *dz_c, *fpart, *hpart, *epart, *sq_part;
+    AdamScalars* adam_sc;  // Adam's step-dependent scalars (k_reduce_grads / k_grad_norm -> k_adam)
     float* wg_part;  // weight-gradient partial tiles [kWgGrid * kWgRuns][kWgSlot]
     float* bpart;    // [prows][kBiasPart] bias partials of K6 / K7
     float* kvc;      // K7: [prows][80][256] each query position's share of every position's dk | dv
@@ -370,6 +418,7 @@ inline Plan make_plan(int Bm, float* base) {
     p.hpart = w.take((size_t)(Bm / kHeadSamples) * kHeadPart);
     p.epart = w.take((size_t)p.prows * 2 * kEmbPart);
     p.sq_part = w.take(1 << 16);
+    p.adam_sc = reinterpret_cast<AdamScalars*>(w.take(4));
     p.wg_part = w.take((size_t)kWgGrid * kWgRuns * kWgSlot);
     p.bpart = w.take((size_t)p.prows * pol::kBiasPart);
     p.kvc = pol::ps_capable(Bm) ? w.take((size_t)p.prows * S * kHeadSamples * 2 * D) : nullptr;  // [prows][80][256]
@@ -381,6 +430,7 @@ inline Plan make_plan(int Bm, float* base) {
 
 
 inline const float* prm(const uavhip_ppo* c, int i) { return c->params + kOffs.o[i]; }
+inline AdamHyper adam_hyper(const uavhip_ppo* c) { return AdamHyper{c->lr_actor, c->lr_critic, c->beta1, c->beta2}; }
 
 // Position split (K7) for this minibatch size (UAVHIP_POS_SPLIT=0 turns it off: tests compare both ways).
 inline bool pos_split(int Bm) {
@@ -488,13 +538,12 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
     if (upd) {
         if (!bwd) {
             hipLaunchKernelGGL(k_grad_norm, dim3(kSqBlocks), dim3(256), 0, st, c->grads, c->n_floats, p.sq_part,
-                               c->adam_step);
+                               c->adam_step, adam_hyper(c), p.adam_sc);
             TR_CHECK(check_launch("k_grad_norm"));
         }
-        AdamArgs aa{c->params, c->grads, c->adam_m, c->adam_v, c->adam_step, p.sq_part, n_sq, c->n_floats,
-                    kOffs.o[kCriticTrunk], c->lr_actor, c->lr_critic, c->beta1, c->beta2, c->adam_eps,
-                    c->max_grad_norm, p.packed, p.packedT};
-        hipLaunchKernelGGL(k_adam, dim3((c->n_floats / 4 + 255) / 256), dim3(256), 0, st, aa);
+        AdamArgs aa{c->params, c->grads, c->adam_m, c->adam_v, p.adam_sc, p.sq_part, n_sq, c->beta1, c->beta2,
+                    c->adam_eps, c->max_grad_norm, p.packed, p.packedT};
+        hipLaunchKernelGGL(k_adam, dim3(kAdamBlocks.n), dim3(256), 0, st, aa);
         TR_CHECK(check_launch("k_adam"));
     }
     return UAVHIP_OK;
@@ -634,7 +683,8 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         return UAVHIP_EINVAL;
     }
     // padding floats between parameters stay zero
-    hipLaunchKernelGGL(k_reduce_grads, dim3(seg_blocks), dim3(256), 0, st, sb, c->grads, p.sq_part, step);
+    hipLaunchKernelGGL(k_reduce_grads, dim3(seg_blocks), dim3(256), 0, st, sb, c->grads, p.sq_part, step, adam_hyper(c),
+                       p.adam_sc);
     *n_sq = seg_blocks;
     return check_launch("k_reduce_grads");
 }
