@@ -202,20 +202,21 @@ constexpr int kSqBlocks = 256;
 //   p = addcdiv(p, m, denom, -lr / (1 - b1^t)) = p + ((-step) m) / denom
 // with the step-dependent scalars from AdamScalars; no other contraction (explicit _rn operations).
 //
-// Work items: a GEMM weight (kTileK != 0, flat [NR][NC]) in 4 x 4 blocks (rows i0..i0+3, columns
-// j0..j0+3), every other parameter in float4s. Each parameter's items start a new 256-item block,
-// so a block's parameter is a table lookup. A 4 x 4 block refreshes the forward's fragment-order copy
-// (packed: four float4, one per row) and the backward's transposed copy (packedT: four float4, one
-// per column) -- k_policy_pack's mapping inverted, each thread's four stores one contiguous 64 B --
-// so an UPDATE leaves both current and the next FORWARD may skip the pack launch (UAVHIP_PPO_PACKED).
-constexpr int kAdamMaxBlocks = 192;
+// Work items: one float4 per thread, 256 per block; each parameter's items start a new block, so
+// a block's parameter is a table lookup. A GEMM weight's block (kTileK != 0, flat [NR][NC]) covers
+// 1024 / NC whole rows: after the update every thread writes its float4 into the forward's
+// fragment-order copy (packed), and the block's tile goes through LDS so that every thread writes
+// one float4 of the backward's transposed copy (packedT: four consecutive rows of one column) --
+// k_policy_pack's mapping inverted, so an UPDATE leaves both current and the next FORWARD may
+// skip the pack launch (UAVHIP_PPO_PACKED).
+constexpr int kAdamMaxBlocks = 512;
 struct AdamBlocks {
     int n;
     int param[kAdamMaxBlocks];  // parameter of the block
-    int first[kAdamMaxBlocks];  // its first item within the parameter
+    int first[kAdamMaxBlocks];  // its first float4 within the parameter
     int tbase[kAdamMaxBlocks];  // packedT offset of the parameter's transposed copy, -1: none
 };
-constexpr int adam_items(int q) { return kTileK[q] ? kSizes[q] / 16 : pad4(kSizes[q]) / 4; }
+constexpr int adam_items(int q) { return pad4(kSizes[q]) / 4; }
 constexpr int packedT_base(int q) {
     for (int li = 0; li < 3; ++li) {
         const int trunk = li == 0 ? kActorTrunk : kCriticTrunk, layer = li == 2 ? 1 : 0;
@@ -240,8 +241,13 @@ constexpr AdamBlocks make_adam_blocks() {
     return b;
 }
 constexpr AdamBlocks kAdamBlocks = make_adam_blocks();
-static_assert(kAdamBlocks.n <= kAdamMaxBlocks, "Adam block table");
-static_assert(kTileK[kActorHead] == D && packedT_base(kActorHead) >= 0, "every tiled weight has a transposed copy");
+constexpr bool adam_tiles_ok() {  // every tiled weight: whole blocks of whole rows, a transposed copy
+    for (int q = 0; q < kNumParams; ++q)
+        if (kTileK[q] && (kSizes[q] % 1024 || 1024 % kTileK[q] || (1024 / kTileK[q]) % 4 || packedT_base(q) < 0))
+            return false;
+    return true;
+}
+static_assert(kAdamBlocks.n <= kAdamMaxBlocks && adam_tiles_ok(), "Adam block table");
 
 struct AdamArgs {
     float* params;
@@ -256,39 +262,21 @@ struct AdamArgs {
     float *packed, *packedT;  // nullable: refreshed with the updated params
 };
 
-__device__ __forceinline__ void adam4(f32x4& p, f32x4& m, f32x4& v, const f32x4 g, float nss, float bc2s, float w1,
-                                      float b2, float w2, float epsf) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        m[j] = __fmaf_rn(w1, __fsub_rn(g[j], m[j]), m[j]);  // torch's vectorised lerp: one fma
-        v[j] = __fadd_rn(__fmul_rn(v[j], b2), __fmul_rn(__fmul_rn(w2, g[j]), g[j]));
-        const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v[j]), bc2s), epsf);
-        p[j] = __fadd_rn(p[j], __fdiv_rn(__fmul_rn(nss, m[j]), denom));
-    }
-}
-
 __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     __shared__ float red[4];
+    __shared__ __attribute__((aligned(16))) float tile[1024];
     const int q = kAdamBlocks.param[blockIdx.x];
     const int item = kAdamBlocks.first[blockIdx.x] + threadIdx.x;
     const int NC = kTileK[q], off = kOffs.o[q];
-    const bool tiled = NC != 0;
     const bool live = item < adam_items(q);
-    // this thread's elements: rows i0..i0+3 x columns j0..j0+3 (tiled) or one float4 (nrow = 1);
-    // loaded before the g^2 partials so both latencies overlap
-    const int i0 = tiled ? 4 * (item / (NC / 4)) : 0, j0 = tiled ? 4 * (item % (NC / 4)) : 0;
-    const int nrow = tiled ? 4 : 1;
-    f32x4 g[4], m[4], v[4], p[4];
-    auto at = [&](int r) { return tiled ? off + (i0 + r) * NC + j0 : off + 4 * item; };
+    const int f = off + 4 * item;
+    // the update operands first, then the g^2 partials: both latencies overlap
+    f32x4 g, m, v, p;
     if (live) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (r < nrow) {
-                g[r] = *reinterpret_cast<const f32x4*>(a.grads + at(r));
-                m[r] = *reinterpret_cast<const f32x4*>(a.m + at(r));
-                v[r] = *reinterpret_cast<const f32x4*>(a.v + at(r));
-                p[r] = *reinterpret_cast<const f32x4*>(a.params + at(r));
-            }
+        g = *reinterpret_cast<const f32x4*>(a.grads + f);
+        m = *reinterpret_cast<const f32x4*>(a.m + f);
+        v = *reinterpret_cast<const f32x4*>(a.v + f);
+        p = *reinterpret_cast<const f32x4*>(a.params + f);
     }
     // the g^2 block partials (~2k): 8 independent loads in flight per thread, not a dependent chain
     float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -302,42 +290,42 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     s = wave_sum(s);
     if (lane_id() == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (!live) return;
     const float norm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
     const float coef = fminf(a.max_norm / (norm + 1e-6f), 1.0f);
     const float nss = q < kCriticTrunk ? sc.nss_a : sc.nss_c;
     const float w1 = (float)(1.0 - a.beta1), b2 = (float)a.beta2, w2 = (float)(1.0 - a.beta2), epsf = (float)a.eps;
+    if (live) {
+        g = g * coef;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-        if (r < nrow) {
-            g[r] = g[r] * coef;
-            adam4(p[r], m[r], v[r], g[r], nss, sc.bc2s, w1, b2, w2, epsf);
-            *reinterpret_cast<f32x4*>(a.grads + at(r)) = g[r];
-            *reinterpret_cast<f32x4*>(a.m + at(r)) = m[r];
-            *reinterpret_cast<f32x4*>(a.v + at(r)) = v[r];
-            *reinterpret_cast<f32x4*>(a.params + at(r)) = p[r];
+        for (int j = 0; j < 4; ++j) {
+            m[j] = __fmaf_rn(w1, __fsub_rn(g[j], m[j]), m[j]);  // torch's vectorised lerp: one fma
+            v[j] = __fadd_rn(__fmul_rn(v[j], b2), __fmul_rn(__fmul_rn(w2, g[j]), g[j]));
+            const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v[j]), sc.bc2s), epsf);
+            p[j] = __fadd_rn(p[j], __fdiv_rn(__fmul_rn(nss, m[j]), denom));
         }
+        *reinterpret_cast<f32x4*>(a.grads + f) = g;
+        *reinterpret_cast<f32x4*>(a.m + f) = m;
+        *reinterpret_cast<f32x4*>(a.v + f) = v;
+        *reinterpret_cast<f32x4*>(a.params + f) = p;
+    }
     if (!a.packed) return;
-    if (!tiled) {  // plain parameters are copied as they are
-        *reinterpret_cast<f32x4*>(a.packed + at(0)) = p[0];
+    if (!NC) {  // plain parameters are copied as they are
+        if (live) *reinterpret_cast<f32x4*>(a.packed + f) = p;
         return;
     }
-    // packed: row i of [NR][NC] in fragment order, float4 = columns j0..j0+3
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int i = i0 + r;
-        *reinterpret_cast<f32x4*>(a.packed + off + (((i >> 4) * (NC >> 4) + (j0 >> 4)) * 64 + (i & 15) +
-                                                      16 * ((j0 & 15) >> 2)) * 4) = p[r];
-    }
-    // packedT: W^T ([NC][NR]) in fragment order, float4 = rows i0..i0+3 of column j
-    const int NR = kSizes[q] / NC, tb = kAdamBlocks.tbase[blockIdx.x];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const int j = j0 + c;
-        *reinterpret_cast<f32x4*>(a.packedT + tb + (((j >> 4) * (NR >> 4) + (i0 >> 4)) * 64 + (j & 15) +
-                                                     16 * ((i0 & 15) >> 2)) * 4) =
-            f32x4{p[0][c], p[1][c], p[2][c], p[3][c]};
-    }
+    // packed: row i of [NR][NC] in fragment order, float4 = columns j..j+3
+    const int loc = 4 * item, i = loc / NC, j = loc - i * NC;
+    *reinterpret_cast<f32x4*>(a.packed + off + (((i >> 4) * (NC >> 4) + (j >> 4)) * 64 + (i & 15) +
+                                                  16 * ((j & 15) >> 2)) * 4) = p;
+    // packedT: W^T ([NC][NR]) in fragment order, float4 = rows it..it+3 of column jt
+    *reinterpret_cast<f32x4*>(tile + 4 * threadIdx.x) = p;
+    __syncthreads();
+    const int NR = kSizes[q] / NC, i0 = 4 * kAdamBlocks.first[blockIdx.x] / NC;
+    const int jt = threadIdx.x % NC, rq = threadIdx.x / NC, it = i0 + 4 * rq;
+    const f32x4 col = {tile[(4 * rq) * NC + jt], tile[(4 * rq + 1) * NC + jt], tile[(4 * rq + 2) * NC + jt],
+                       tile[(4 * rq + 3) * NC + jt]};
+    *reinterpret_cast<f32x4*>(a.packedT + kAdamBlocks.tbase[blockIdx.x] +
+                              (((jt >> 4) * (NR >> 4) + (it >> 4)) * 64 + (jt & 15) + 16 * ((it & 15) >> 2)) * 4) = col;
 }
 
 // ================================================================== host orchestration
