@@ -251,7 +251,8 @@ int uavhip_windows_from_rows(const float* first, const float* rows, const float*
  * uavhip/policy.py pack_weights() from the 50-key state_dict: each parameter at its
  * uavhip_policy_layout() offset, flat or in MFMA fragment order (uavhip_policy_tiling()). */
 typedef struct uavhip_policy {
-    const float* weights; /* packed buffer, layout = uavhip_policy_layout() offsets */
+    const float* weights; /* packed buffer, layout = uavhip_policy_layout() offsets + split copies */
+                          /* (n_floats = uavhip_policy_split_layout()) */
     int32_t n_floats;
     int32_t d_model, n_heads, d_ff, d_head_hidden; /* 128, 8, 256, 64 */
     int32_t actor_layers, critic_layers;           /* 1, 2 */
@@ -260,6 +261,14 @@ typedef struct uavhip_policy {
 /* Offsets (in floats) of every parameter in the packed buffer, in state_dict key order
  * (see policy.py). Returns the total number of floats; offsets may be NULL. */
 int32_t uavhip_policy_layout(int32_t* offsets, int32_t max_offsets);
+
+/* The inference forward's packed buffer (uavhip_policy.weights / n_floats) holds, after the
+ * uavhip_policy_layout() parameters, split copies of the GEMM weights that run on the f16 matrix
+ * cores as fp32-accurate split products: weight `params[i]` (state_dict index, [R][K]) at float
+ * offset `offsets[i]`, as two fp16 planes w1 = f16(w), w2 = f16((w - w1) * 2^11) in split fragment
+ * order (blocks of 16 rows x 32 k: 1 KiB of w1 then 1 KiB of w2, lane = r%16 + 16 ((k%32)/8)
+ * holding k%8 = 0..7). Returns the packed buffer's total floats; params / offsets may be NULL. */
+int32_t uavhip_policy_split_layout(int32_t* params, int32_t* offsets, int32_t max_entries);
 
 /* flat (state_dict order, uavhip_policy_layout offsets, every parameter row-major) -> packed
  * (the same with the uavhip_policy_tiling weights in MFMA fragment order), on the device. */
@@ -410,8 +419,9 @@ int uavhip_episode_stats(const double* reward, const uint8_t* done, const int8_t
 
 /* ---------------------------------------------------------------- misc */
 const char* uavhip_last_error(void);
-/* 3 since round 3 (struct uavhip_ppo: the Adam hyper-parameters are doubles); the ctypes binding
-   refuses a library of another version */
+/* 4 since round 3 (struct uavhip_ppo: the Adam hyper-parameters are doubles; the inference packed
+   buffer carries split weight copies, uavhip_policy_split_layout); the ctypes binding refuses a
+   library of another version */
 int32_t uavhip_abi_version(void);
 
 #ifdef __cplusplus

@@ -25,4 +25,4 @@ int check_launch(const char* what) {
 }  // namespace uavhip
 
 extern "C" const char* uavhip_last_error(void) { return uavhip::g_err; }
-extern "C" int32_t uavhip_abi_version(void) { return 3; }
+extern "C" int32_t uavhip_abi_version(void) { return 4; }

@@ -229,6 +229,114 @@ __device__ __forceinline__ void zero(f32x4 (&acc)[CT]) {
     for (int ct = 0; ct < CT; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
+// ------------------------------------------------------------------ split products on the f16 cores
+// fp32-accurate GEMMs on v_mfma_f32_16x16x32_f16 (16 cycles per 16 x 16 x 32 block against 8 x 32
+// for the f32 MFMA): both operands carried as two fp16 planes, x1 = f16(x), x2 = f16((x - x1) 2^11)
+// (x1 + 2^-11 x2 = x to 2^-22 relative, the 2^11 keeps x2 out of the fp16 subnormals), and
+//   W X^T = hi + 2^-11 lo,   hi += W1 X1,   lo += W1 X2 + W2 X1       (3 MFMAs per block)
+// -- the dropped W2 X2 is 2^-22 of a product; the fp32 accumulation dominates the error
+// (scripts/micro/split_gemm.hip: max error 0.42x the f32 MFMA's on the FFN1 shape, 3.6x faster).
+// Weights: the packed buffer's split copies (policy_layout.hpp kSplitParam / kSplitOffs), blocks of
+// 16 rows x 32 k = 1 KiB of w1 then 1 KiB of w2, lane l = r%16 + 16 ((k%32)/8) holding k%8.
+// Activations: two planes of [tok][LDP halves] in LDS, plane 2 at +TOK * LDP; lane (i16, g) reads
+// 8 halves of token i16 per plane with one ds_read_b128 (272-B rows: conflict-free).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+constexpr int LDP = D + 8;           // halves per plane row
+constexpr int kPlane = TOK * LDP;    // halves per plane: two planes fill a [TOK][LDH] fp32 buffer
+static_assert(2 * kPlane * 2 == TOK * LDH * 4, "the two planes of an activation replace its fp32 copy");
+constexpr float kLoScale = 1.0f / 2048.0f;
+
+template <int D_>
+struct HPre {
+    f16x8 a1[D_], a2[D_];
+};
+__device__ __forceinline__ const f16x8* hfrag_ptr(TID_F const float* P, int soff, int K, int row, int kw0) {
+    return reinterpret_cast<const f16x8*>(P + soff) + ((size_t)(row >> 4) * (K >> 5) + (kw0 >> 5)) * 128 + LANE();
+}
+template <int D_>
+__device__ __forceinline__ HPre<D_> hprefetch(TID_F const float* __restrict__ P, int soff, int K, int row, int kw0) {
+    const f16x8* wp = hfrag_ptr(TID_C P, soff, K, row, kw0);
+    HPre<D_> r;
+#pragma unroll
+    for (int p = 0; p < D_; ++p) {
+        r.a1[p] = wp[128 * p];
+        r.a2[p] = wp[128 * p + 64];
+    }
+    return r;
+}
+// hi / lo[ct] += W[row + i][kw0 + k] * X[xtok0 + 16 ct + j][k] over k in [0, 128) (4 blocks of 32):
+// A blocks >= D_ loaded one block ahead of their use, B (LDS) one block ahead.
+template <int CT, int D_>
+__device__ __forceinline__ void hgemm_tile(TID_F f32x4 (&hi)[CT], f32x4 (&lo)[CT], const HPre<D_>& pre,
+                                           const float* __restrict__ P, int soff, int K, int row, int kw0,
+                                           const _Float16* X, int xtok0) {
+    constexpr int NKB = D / 32;
+    const int l = LANE(), i16 = l & 15, g = l >> 4;
+    const f16x8* wp = hfrag_ptr(TID_C P, soff, K, row, kw0);
+    const _Float16* xp[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) xp[ct] = X + (xtok0 + 16 * ct + i16) * LDP + 8 * g;
+    f16x8 a1[NKB], a2[NKB], b1[2][CT], b2[2][CT];
+#pragma unroll
+    for (int p = 0; p < D_; ++p) {
+        a1[p] = pre.a1[p];
+        a2[p] = pre.a2[p];
+    }
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+        b1[0][ct] = *reinterpret_cast<const f16x8*>(xp[ct]);
+        b2[0][ct] = *reinterpret_cast<const f16x8*>(xp[ct] + kPlane);
+    }
+#pragma unroll
+    for (int i = 0; i < NKB; ++i) {
+        const int cur = i & 1;
+        if (i + D_ < NKB) {
+            a1[i + D_] = wp[128 * (i + D_)];
+            a2[i + D_] = wp[128 * (i + D_) + 64];
+        }
+        if (i + 1 < NKB) {
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                b1[cur ^ 1][ct] = *reinterpret_cast<const f16x8*>(xp[ct] + 32 * (i + 1));
+                b2[cur ^ 1][ct] = *reinterpret_cast<const f16x8*>(xp[ct] + 32 * (i + 1) + kPlane);
+            }
+        }
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            hi[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], b1[cur][ct], hi[ct], 0, 0, 0);
+            lo[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], b2[cur][ct], lo[ct], 0, 0, 0);
+            lo[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[i], b1[cur][ct], lo[ct], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+// v -> its two planes at Y + tok * LDP + c (plane 2 at + kPlane): one 8-byte store per plane
+__device__ __forceinline__ void hsplit_store(_Float16* Y, int o, const f32x4 v) {
+    f16x4 v1, v2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v1[j] = (_Float16)v[j];
+        v2[j] = (_Float16)((v[j] - (float)v1[j]) * 2048.f);
+    }
+    *reinterpret_cast<f16x4*>(Y + o) = v1;
+    *reinterpret_cast<f16x4*>(Y + o + kPlane) = v2;
+}
+// Y planes [ytok0 + 16 ct + j][ycol + i] = epi(hi + 2^-11 lo + bias[row + i])
+template <int CT, bool RELU>
+__device__ __forceinline__ void hstore_tile(TID_F const f32x4 (&hi)[CT], const f32x4 (&lo)[CT], const f32x4 bb,
+                                            _Float16* Y, int ycol, int ytok0) {
+    const int l = LANE(), i16 = l & 15, g = l >> 4;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+        f32x4 v = hi[ct] + lo[ct] * kLoScale + bb;
+        if (RELU) {
+            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        hsplit_store(Y, (ytok0 + 16 * ct + i16) * LDP + ycol + 4 * g, v);
+    }
+}
+
 // Y[ytok0 + 16 ct + j][ycol + i] = epi(acc + bias[brow + i]); lane (j, g) holds rows 4g..4g+3
 template <int CT, bool RELU>
 __device__ __forceinline__ void store_tile(TID_F const f32x4 (&acc)[CT], const f32x4 bb, float* Y, int ldy, int ycol,
@@ -305,9 +413,13 @@ __device__ __forceinline__ LnPar ln_load(TID_F const f32x4 bb, const float* __re
     const int f0 = 16 * (TIDX() >> 6) + 4 * (LANE() >> 4);
     return LnPar{bb, *reinterpret_cast<const f32x4*>(w + f0), *reinterpret_cast<const f32x4*>(b + f0)};
 }
-template <int CT, bool TR = false>
+// PLANES: the output goes to sm.h as the two fp16 planes of the split products (the next GEMM's
+// operand; the caller keeps the fp32 output from `outv`); resid: the residual from registers (the
+// lane's own elements, as `outv` returned them) instead of sm.h.
+template <int CT, bool TR = false, bool PLANES = false>
 __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (&acc)[CT], const LnPar& lp, int ytok0,
-                                                   const LnOut& lo = LnOut{}, f32x4* outv = nullptr) {
+                                                   const LnOut& lo = LnOut{}, f32x4* outv = nullptr,
+                                                   const f32x4* resid = nullptr) {
     const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
     const int f0 = 16 * wv + 4 * g;
     const f32x4 bb = lp.bb;
@@ -315,7 +427,7 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
         const int tok = ytok0 + 16 * ct + i16;
-        v[ct] = acc[ct] + bb + *reinterpret_cast<const f32x4*>(sm.h + tok * LDH + f0);
+        v[ct] = acc[ct] + bb + (resid ? resid[ct] : *reinterpret_cast<const f32x4*>(sm.h + tok * LDH + f0));
         float s = (v[ct].x + v[ct].y) + (v[ct].z + v[ct].w);
         s = add_xor32(add_xor16(s));
         const float m = s * (1.0f / 16);
@@ -367,7 +479,8 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
         }
         const f32x4 xh = (v[ct] - mean) * rs;
         const f32x4 out = xh * ww + lb;
-        *reinterpret_cast<f32x4*>(sm.h + tok * LDH + f0) = out;
+        if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.h), tok * LDP + f0, out);
+        else *reinterpret_cast<f32x4*>(sm.h + tok * LDH + f0) = out;
         if (outv) outv[ct] = out;
         if (TR && !kExpNoStore) {
             const size_t r = (size_t)orow(tok, lo.b0, lo.compact);
@@ -603,6 +716,71 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
     layer_tail<trunk, layer, last, TR>(TID_C sm, P, po, io, b0, pre_ln2);
 }
 
+// Out-projection + LN1 + FFN + LN2 of a full (80-token) inference layer with the FFN as split
+// products (layer_tail's kSplit path); the out-projection stays on the f32 MFMA.
+template <int trunk, int layer>
+__device__ __forceinline__ void layer_ffn_split(TID_F Smem& sm, const float* __restrict__ P, const APre<depth<S>()>& po) {
+    [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
+    constexpr int DQ = depth<S>();
+    const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
+    const float* bo = P + kOffs.o[layer_param(trunk, layer, OUTB)];
+    const float* b1 = P + kOffs.o[layer_param(trunk, layer, L1B)];
+    const float* b2 = P + kOffs.o[layer_param(trunk, layer, L2B)];
+    constexpr int s1 = split_slot(layer_param(trunk, layer, L1W)), s2 = split_slot(layer_param(trunk, layer, L2W));
+    const int wv = TIDX() >> 6;
+    _Float16* const hp = reinterpret_cast<_Float16*>(sm.h);
+    _Float16* const bp = reinterpret_cast<_Float16*>(sm.big);
+    _Float16* const cp = reinterpret_cast<_Float16*>(sm.ctx);
+    f32x4 h1[S];  // LN1's output: LN2's residual
+    HPre<2> w1a;
+    {
+        const f32x4 bo4 = ln_bias(TID_C bo);
+        f32x4 acc[S];
+        zero(acc);
+        gemm_tile<S, DQ>(TID_C acc, po, Wo, D, 16 * wv, 0, sm.ctx, LDH, 0);
+        PTR(tb + 7);
+        const LnPar lp = ln_load(TID_C bo4, P + kOffs.o[layer_param(trunk, layer, N1W)], P + kOffs.o[layer_param(trunk, layer, N1B)]);
+        w1a = hprefetch<2>(TID_C P, s1, D, 16 * wv, 0);
+        residual_layernorm<S, false, true>(TID_C sm, acc, lp, 0, LnOut{}, h1);
+    }
+    PTR(tb + 8);
+    __syncthreads();
+    PTR(tb + 9);
+    {  // FFN1: hidden features 0-127 -> big planes, 128-255 -> ctx planes (both free now)
+        const int grow = 4 * (LANE() >> 4);
+        const f32x4 ba = *reinterpret_cast<const f32x4*>(b1 + 16 * wv + grow);
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(b1 + 128 + 16 * wv + grow);
+        f32x4 hi[S], lo[S];
+        zero(hi);
+        zero(lo);
+        hgemm_tile<S, 2>(TID_C hi, lo, w1a, P, s1, D, 16 * wv, 0, hp, 0);
+        const HPre<2> w1b = hprefetch<2>(TID_C P, s1, D, 128 + 16 * wv, 0);
+        hstore_tile<S, true>(TID_C hi, lo, ba, bp, 16 * wv, 0);
+        zero(hi);
+        zero(lo);
+        hgemm_tile<S, 2>(TID_C hi, lo, w1b, P, s1, D, 128 + 16 * wv, 0, hp, 0);
+        hstore_tile<S, true>(TID_C hi, lo, bb, cp, 16 * wv, 0);
+    }
+    const HPre<2> w2a = hprefetch<2>(TID_C P, s2, FF, 16 * wv, 0);
+    PTR(tb + 10);
+    __syncthreads();
+    PTR(tb + 11);
+    const HPre<2> w2b = hprefetch<2>(TID_C P, s2, FF, 16 * wv, 128);
+    const f32x4 b24 = ln_bias(TID_C b2);
+    f32x4 hi[S], lo[S];
+    zero(hi);
+    zero(lo);
+    hgemm_tile<S, 2>(TID_C hi, lo, w2a, P, s2, FF, 16 * wv, 0, bp, 0);
+    hgemm_tile<S, 2>(TID_C hi, lo, w2b, P, s2, FF, 16 * wv, 128, cp, 0);
+    PTR(tb + 12);
+    const LnPar lp2 = ln_load(TID_C b24, P + kOffs.o[layer_param(trunk, layer, N2W)], P + kOffs.o[layer_param(trunk, layer, N2B)]);
+    f32x4 acc2[S];
+#pragma unroll
+    for (int ct = 0; ct < S; ++ct) acc2[ct] = hi[ct] + lo[ct] * kLoScale;
+    residual_layernorm<S>(TID_C sm, acc2, lp2, 0, LnOut{}, nullptr, h1);
+    PTR(tb + 14);
+}
+
 // Out-projection + LN1 + FFN + LN2 of an encoder layer, after the attention output is in sm.ctx.
 // `po` = the caller's prefetch of the first out_proj weight blocks.
 template <int trunk, int layer, bool last, bool TR, class F, int PSX>
@@ -623,6 +801,16 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
     if (TR) store_rows(TID_C sm.ctx, LDH, io.o, D, 0, D, qtok0, b0, last, qtok1);  // attention output
     // out projection, h = LN1(h + attn) in its epilogue
     APre<DQ> pf1a, pf1b;
+    // inference, full layer (the critic's layer 0): the FFN runs as split products on the f16
+    // matrix cores (hgemm_tile): LN1 writes its output as the two fp16 planes into sm.h and keeps
+    // the fp32 values in registers (LN2's residual), FFN1 writes the hidden planes into big
+    // (features 0-127) and ctx (128-255), FFN2 reads them
+    constexpr bool kSplit = !TR && CTQ == S && split_slot(layer_param(trunk, layer, L1W)) >= 0 &&
+                            split_slot(layer_param(trunk, layer, L2W)) >= 0;
+    if constexpr (kSplit) {
+        layer_ffn_split<trunk, layer>(TID_C sm, P, po);
+        return;
+    }
     // inference, full layer: the wave's own 16 LayerNorm output features are FFN1's k-block wv, so
     // its MFMAs over that block run from registers before the barrier (beside the other waves'
     // LayerNorm work) and the GEMM after it covers the other 7 blocks (k-block order rotated)
@@ -2527,6 +2715,35 @@ __global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ f
     *reinterpret_cast<f32x4*>(packedT + idx) = f32x4{w[k * Rt], w[(k + 1) * Rt], w[(k + 2) * Rt], w[(k + 3) * Rt]};
 }
 
+// flat -> the split copies of the kSplitParam weights (policy_layout.hpp): one thread per lane of a
+// (16-row tile, 32-k block), two f16x8 stores (w1 = f16(w), w2 = f16((w - w1) 2^11), round to nearest).
+__global__ __launch_bounds__(256) void k_policy_split(const float* __restrict__ flat, float* __restrict__ packed) {
+    const int i = blockIdx.x * 256 + tid_x();
+    int si = 0, base = 0;
+    while (si < kNumSplit && i >= base + kSizes[kSplitParam[si]] / 8) base += kSizes[kSplitParam[si++]] / 8;
+    if (si >= kNumSplit) return;
+    const int q = kSplitParam[si], K = kTileK[q], u = i - base;  // u = (t * K/32 + kb) * 64 + lane
+    const int l = u & 63, blk = u >> 6, kb = blk % (K / 32), t = blk / (K / 32);
+    const float* src = flat + kOffs.o[q] + (size_t)(16 * t + (l & 15)) * K + 32 * kb + 8 * (l >> 4);
+    const f32x4 a = *reinterpret_cast<const f32x4*>(src), b = *reinterpret_cast<const f32x4*>(src + 4);
+    f16x8 w1, w2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float w = j < 4 ? a[j] : b[j - 4];
+        w1[j] = (_Float16)w;
+        w2[j] = (_Float16)((w - (float)w1[j]) * 2048.f);
+    }
+    f16x8* dst = reinterpret_cast<f16x8*>(packed + kSplitOffs.o[si]) + (size_t)blk * 128 + l;
+    dst[0] = w1;
+    dst[64] = w2;
+}
+
+int policy_split(const float* flat, float* packed, hipStream_t st) {
+    constexpr int n = (kPackedFloats - kOffs.o[kNumParams]) / 8;
+    hipLaunchKernelGGL(k_policy_split, dim3((n + 255) / 256), dim3(256), 0, st, flat, packed);
+    return check_launch("k_policy_split");
+}
+
 int policy_pack_train(const float* flat, float* packed, float* packedT, hipStream_t st) {
     const int items = kOffs.o[kNumParams] / 4 + kPackedTFloats / 4;
     hipLaunchKernelGGL(k_policy_pack, dim3((items + 255) / 256), dim3(256), 0, st, flat, packed, packedT);
@@ -2543,13 +2760,22 @@ extern "C" int uavhip_policy_pack(const float* flat, float* packed, uavhip_strea
     const int n = pol::kOffs.o[pol::kNumParams] / 4;
     hipLaunchKernelGGL(pol::k_policy_pack, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, flat, packed,
                        nullptr);
-    return check_launch("k_policy_pack");
+    if (const int rc = check_launch("k_policy_pack")) return rc;
+    return pol::policy_split(flat, packed, (hipStream_t)stream);
 }
 
 extern "C" int32_t uavhip_policy_layout(int32_t* offsets, int32_t max_offsets) {
     if (offsets)
         for (int i = 0; i < pol::kNumParams && i < max_offsets; ++i) offsets[i] = pol::kOffs.o[i];
     return pol::kOffs.o[pol::kNumParams];
+}
+
+extern "C" int32_t uavhip_policy_split_layout(int32_t* params, int32_t* offsets, int32_t max_entries) {
+    for (int i = 0; i < pol::kNumSplit && i < max_entries; ++i) {
+        if (params) params[i] = pol::kSplitParam[i];
+        if (offsets) offsets[i] = pol::kSplitOffs.o[i];
+    }
+    return pol::kPackedFloats;
 }
 
 extern "C" int32_t uavhip_policy_tiling(int32_t* kcols, int32_t max_params) {
@@ -2576,11 +2802,11 @@ static int check_policy(const char* fn, const uavhip_policy* policy, const float
         set_error("%s: NULL policy/weights/states or B=%d", fn, B);
         return UAVHIP_EINVAL;
     }
-    if (policy->n_floats != pol::kOffs.o[pol::kNumParams] || policy->d_model != pol::D || policy->n_heads != pol::NH ||
+    if (policy->n_floats != pol::kPackedFloats || policy->d_model != pol::D || policy->n_heads != pol::NH ||
         policy->d_ff != pol::FF || policy->d_head_hidden != pol::HID || policy->actor_layers != 1 ||
         policy->critic_layers != 2) {
         set_error("%s: unsupported architecture / packed size %d (expected %d)", fn, policy->n_floats,
-                  pol::kOffs.o[pol::kNumParams]);
+                  pol::kPackedFloats);
         return UAVHIP_EINVAL;
     }
     return UAVHIP_OK;

@@ -46,5 +46,29 @@ enum { POS = 0, EMB_W = 1, EMB_B = 2 };
 enum { INW = 0, INB, OUTW, OUTB, L1W, L1B, L2W, L2B, N1W, N1B, N2W, N2B };
 __host__ __device__ constexpr int layer_param(int trunk, int l, int which) { return trunk + 3 + kLayerParams * l + which; }
 
+// ---- split copies (inference forward only): the GEMM weights of the full 80-token layer that run
+// on the f16 matrix cores as fp32-accurate split products (policy.hip, hgemm_tile). Each weight
+// W [R][K] is appended to the packed buffer as two fp16 planes, w1 = f16(w), w2 = f16((w - w1) 2^11),
+// in split fragment order: per 16-row tile t and 32-k block kb, 1 KiB of plane 1 then 1 KiB of
+// plane 2, lane l = r%16 + 16 ((k%32)/8) holding k%8 = 0..7 -- one float per weight, like the fp32
+// copy. The split copies follow the 50 parameters.
+constexpr int kNumSplit = 2;
+constexpr int kSplitParam[kNumSplit] = {layer_param(kCriticTrunk, 0, L1W), layer_param(kCriticTrunk, 0, L2W)};
+struct SplitOffs { int o[kNumSplit + 1]; };
+constexpr SplitOffs make_split_offs() {
+    SplitOffs r{};
+    int acc = kOffs.o[kNumParams];
+    for (int i = 0; i < kNumSplit; ++i) { r.o[i] = acc; acc += kSizes[kSplitParam[i]]; }
+    r.o[kNumSplit] = acc;
+    return r;
+}
+constexpr SplitOffs kSplitOffs = make_split_offs();
+constexpr int kPackedFloats = kSplitOffs.o[kNumSplit];  // the inference forward's packed buffer
+constexpr int split_slot(int q) {
+    for (int i = 0; i < kNumSplit; ++i)
+        if (kSplitParam[i] == q) return kSplitOffs.o[i];
+    return -1;
+}
+
 }  // namespace pol
 }  // namespace uavhip

@@ -86,6 +86,7 @@ _SIGS = {
     "uavhip_adv_normalize": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, _i32, ctypes.c_int64, _vp, _vp]),
     "uavhip_windows_from_rows": (ctypes.c_int, [_vp, _vp, _vp, _i32, ctypes.c_int64, _i32, _i32, _i32, _vp, _vp]),
     "uavhip_policy_layout": (_i32, [ctypes.POINTER(_i32), _i32]),
+    "uavhip_policy_split_layout": (_i32, [_vp, _vp, _i32]),
     "uavhip_policy_tiling": (_i32, [ctypes.POINTER(_i32), _i32]),
     "uavhip_policy_pack": (ctypes.c_int, [_vp, _vp, _vp]),
     "uavhip_policy_forward": (ctypes.c_int, [ctypes.POINTER(PolicyDesc), _vp, _i32, _vp, ctypes.c_uint64,
@@ -113,7 +114,7 @@ class UavHipError(RuntimeError):
     pass
 
 
-ABI_VERSION = 3  # include/uavhip.h uavhip_abi_version
+ABI_VERSION = 4  # include/uavhip.h uavhip_abi_version
 
 
 def _load():

@@ -262,6 +262,29 @@ def tiling():
     return [kc[i] for i in range(np_)]
 
 
+def split_layout():
+    """[(state_dict index, float offset)] of the split weight copies and the packed buffer's total
+    floats (include/uavhip.h uavhip_policy_split_layout)."""
+    params, offs = (ctypes.c_int32 * 16)(*([-1] * 16)), (ctypes.c_int32 * 16)()
+    total = LIB.uavhip_policy_split_layout(params, offs, 16)
+    return [(params[i], offs[i]) for i in range(16) if params[i] >= 0], int(total)
+
+
+def to_split_fragment_order(w):
+    """[R][K] fp32 -> the split copy as float32 words: two fp16 planes w1 = f16(w),
+    w2 = f16((w - w1) * 2^11) in blocks of 16 rows x 32 k (1 KiB of w1, then 1 KiB of w2), lane
+    l = r%16 + 16 ((k%32)//8) holding k%8 = 0..7 (the f16 MFMA operand layout, policy.hip hgemm_tile)."""
+    R, K = w.shape
+    w = w.to(torch.float32)
+    w1 = w.to(torch.float16)
+    w2 = ((w - w1.to(torch.float32)) * 2048.0).to(torch.float16)
+
+    def frag(p):
+        return p.reshape(R // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(R // 16, K // 32, 512)
+
+    return torch.stack([frag(w1), frag(w2)], dim=2).reshape(-1).view(torch.float32)
+
+
 def to_fragment_order(w, K):
     """[R][K] -> MFMA fragment order (include/uavhip.h uavhip_policy_tiling): blocks of 16 rows x
     16 k, inside a block lane = r%16 + 16 * ((k%16)//4) holds k%4 = 0..3."""
@@ -275,14 +298,15 @@ def from_fragment_order(flat, R, K):
 
 def pack_weights(state_dict, device=None):
     """Lay the 50-key state_dict out as the kernel's packed buffer (state_dict key order; GEMM
-    weights in MFMA fragment order)."""
+    weights in MFMA fragment order), followed by the split copies (split_layout())."""
     offs, n = layout()
     kcols = tiling()
     items = list(state_dict.items())
     if len(items) != len(offs) or len(kcols) != len(offs):
         raise ValueError(f"expected {len(offs)} state_dict entries, got {len(items)}")
     dev = device if device is not None else items[0][1].device
-    buf = torch.zeros(n, dtype=torch.float32, device=dev)
+    splits, total = split_layout()
+    buf = torch.zeros(total, dtype=torch.float32, device=dev)
     ends = offs[1:] + [n]
     for (k, v), o, e, K in zip(items, offs, ends, kcols):
         v = v.detach().to(device=dev, dtype=torch.float32)
@@ -294,5 +318,8 @@ def pack_weights(state_dict, device=None):
             flat = v.reshape(-1)
         if flat.numel() > e - o:
             raise ValueError(f"{k}: {flat.numel()} floats do not fit the packed slot {e - o}")
+        buf[o:o + flat.numel()] = flat
+    for q, o in splits:  # the split copies of the f16-matrix-core GEMM weights
+        flat = to_split_fragment_order(items[q][1].detach().to(device=dev, dtype=torch.float32))
         buf[o:o + flat.numel()] = flat
     return buf

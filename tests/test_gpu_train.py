@@ -388,16 +388,16 @@ def test_padding_rows_add_nothing():
 
 
 def test_device_pack_matches_host_pack():
-    """uavhip_policy_pack (device) == policy.pack_weights (host) bit for bit."""
+    """uavhip_policy_pack (device) == policy.pack_weights (host) bit for bit, split copies included."""
     from uavhip import _lib
-    from uavhip.policy import TransformerActorCritic, layout, pack_weights
+    from uavhip.policy import TransformerActorCritic, layout, pack_weights, split_layout
     torch.manual_seed(1)
     net = TransformerActorCritic().cuda()
     offs, n = layout()
     flat = torch.zeros(n, device="cuda")
     for p, o in zip(net.state_dict().values(), offs):
         flat[o:o + p.numel()] = p.reshape(-1)
-    packed = torch.full((n,), float("nan"), device="cuda")
+    packed = torch.full((split_layout()[1],), float("nan"), device="cuda")  # + the split copies
     _lib.check(_lib.LIB.uavhip_policy_pack(_lib.ptr(flat), _lib.ptr(packed), _lib.stream_handle()), "pack")
     assert torch.equal(packed, pack_weights(net.state_dict(), device="cuda"))
 

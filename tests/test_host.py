@@ -43,7 +43,7 @@ def test_library_exports_every_header_symbol():
     for f in fns:
         assert hasattr(_lib.LIB, f), f
     assert set(fns) == set(_lib.EXPORTS)
-    assert _lib.LIB.uavhip_abi_version() == _lib.ABI_VERSION == 3
+    assert _lib.LIB.uavhip_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_ctypes_mirrors_header_enums():
@@ -210,6 +210,35 @@ def test_packed_layout_covers_state_dict():
         else:
             assert torch.equal(got, v.reshape(-1)), k
     assert n == sum((s + 3) // 4 * 4 for s in sizes)
+
+
+def test_split_copies_encode_the_weights():
+    """The split copies after the 50 parameters (include/uavhip.h uavhip_policy_split_layout): two
+    fp16 planes per weight, w1 = f16(w), w2 = f16((w - w1) * 2^11), in 16 x 32 blocks (1 KiB of w1,
+    then 1 KiB of w2; lane = r%16 + 16 ((k%32)//8) holding k%8). w1 + 2^-11 w2 = w to 2^-22 relative."""
+    from uavhip.policy import TransformerActorCritic, layout, pack_weights, split_layout
+    _, n = layout()
+    splits, total = split_layout()
+    assert splits and total == n + sum(list(TransformerActorCritic().state_dict().values())[q].numel() for q, _ in splits)
+    torch.manual_seed(3)
+    sd = TransformerActorCritic().state_dict()
+    buf = pack_weights(sd)
+    assert buf.numel() == total
+    items = list(sd.items())
+    for q, o in splits:
+        k, w = items[q]
+        R, K = w.shape
+        planes = buf[o:o + R * K].view(torch.float16).reshape(R // 16, K // 32, 2, 64, 8).float()
+        for r, c in ((0, 0), (R - 3, K - 6), (17, 45)):
+            lane, j = r % 16 + 16 * ((c % 32) // 8), c % 8
+            w1, w2 = planes[r // 16, c // 32, 0, lane, j], planes[r // 16, c // 32, 1, lane, j]
+            assert w1 == torch.tensor(float(w[r, c])).half().float(), k
+            assert abs(float(w1 + w2 / 2048) - float(w[r, c])) <= 2 ** -22 * abs(float(w[r, c])) + 2 ** -35, k
+        dec = planes[:, :, 0] + planes[:, :, 1] / 2048  # [R/16][K/32][64][8] -> [R][K]
+        dec = dec.reshape(R // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(R, K)
+        # 2^-22 relative; below fp16's normal range (|w| < 2^-14) w1 is subnormal and the bound is
+        # 2^-24 * 2^-11 absolute
+        assert bool(((dec - w).abs() <= 2 ** -22 * w.abs() + 2 ** -35).all()), k
 
 
 def test_config_matches_reference_constants(traj_npz):
