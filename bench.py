@@ -2,14 +2,16 @@
 """Headline benchmark: env-steps/s of the full PPO rollout (BASELINE.json configs[2]:
 4096 envs x 16 UAVs x 32 targets, transformer policy + env step on each MI355X).
 
-One timed "step" = one rollout iteration per rank: T (=64) x {fused policy forward (fp32 MFMA) ->
+One timed "step" = one rollout iteration per rank: T (=64) x {fused policy forward (fp32-accurate MFMA) ->
 on-device sample -> fused env step (fp64)} over E envs -- all T steps in ONE k_rollout_steps launch
 (--per-step-launch: one launch per step) -- a bootstrap value pass, GAE + advantage normalisation,
 and with N > 1 GPUs the RCCL all-gather of the trajectories.
 value = E * T * K * N / max-over-ranks wall time. Inputs (scenes, windows) are resident in HBM.
 
 Also reported (same JSON line):
-  roofline      dominant kernel = k_rollout_steps (per-step figures: its launch / T), MFMA fp32 peak;
+  roofline      dominant kernel = k_rollout_steps (per-step figures: its launch / T); peak = the MFMA
+                peak of its FLOP mix (the critic's 80-token GEMMs as fp32-accurate split products on
+                the f16 cores at 16/3 x the f32 MFMA rate, the rest on the f32 MFMA);
                 achieved = ALGORITHMIC FLOP per step (2,446,208 FLOP/sample, the
                 last-token-pruned forward of one window) x E / its HIP-event duration per step in the
                 last timed iteration; traffic = PMC bytes per step (profiles/rNN_pmc.json). The rollout's
@@ -54,6 +56,12 @@ POLICY_FLOP_PER_SAMPLE = 2_446_208  # full-window forward (last-
 # the rollout's window-row path (uavhip_policy_forward_rows) forms layer-0 Q|K|V of the new row
 # only: minus 4 rows x (actor K,V 256 + critic Q,K,V 384) x 128 x 2 FLOP
 ROWS_FLOP_PER_SAMPLE = POLICY_FLOP_PER_SAMPLE - 4 * (256 + 384) * 128 * 2  # 1,790,848
+# of these, the GEMMs over all 80 tokens of the critic (layer-0 out-projection + FFN, layer-1 K / V, and
+# its position-4 Q) run as split products on the f16 matrix cores (3 x v_mfma_f32_16x16x32_f16 per
+# fp32-accurate 16 x 16 x 32 block): (128 + 2 * 256 + 256) x 128 x 2 x 80 + 128 x 128 x 2 x 16
+# FLOP per 16-sample workgroup
+SPLIT_FLOP_PER_SAMPLE = ((128 + 2 * 256 + 256) * 128 * 2 * 80 + 128 * 128 * 2 * 16) // 16  # 1,179,648
+MFMA_SPLIT_PEAK_TFLOPS = 157.3 * 16 / 3  # fp32-equivalent: f16 MFMA (16x the f32 rate) / 3 products
 TRAIN_FLOP_PER_SAMPLE_EPOCH = 3 * 4_040_000  # training ~ 3 x dense forward
 TRAIN_EXEC_FLOP_PER_SAMPLE_EPOCH = 7_460_000  # pruned forward + dX + dW
 MFMA_F32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: fp32 MFMA = vector peak
@@ -462,6 +470,10 @@ def main():
     flop_exec = ROWS_FLOP_PER_SAMPLE if eng.rowproj is not None else POLICY_FLOP_PER_SAMPLE
     achieved_tf = POLICY_FLOP_PER_SAMPLE * E / (pol_ms * 1e-3) / 1e12
     exec_tf = flop_exec * E / (pol_ms * 1e-3) / 1e12
+    # the MFMA peak of the FLOP mix: f32 MFMA for the rest, split products at 16/3 x the f32 rate
+    mix_peak = lambda flop: flop / ((flop - SPLIT_FLOP_PER_SAMPLE) / MFMA_F32_PEAK_TFLOPS  # noqa: E731
+                                   + SPLIT_FLOP_PER_SAMPLE / MFMA_SPLIT_PEAK_TFLOPS)
+    peak_alg, peak_exec = mix_peak(POLICY_FLOP_PER_SAMPLE), mix_peak(flop_exec)
     env_gbs = None if env_ms is None else env_bytes_per_step(args.targets) * E / (env_ms * 1e-3) / 1e9
 
     env_fused = stress = None
@@ -516,7 +528,8 @@ def main():
             "metric": "env-steps/sec (whole node), full PPO rollout, 4096 envs x 16 UAV x 32 tgt per GPU",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32 policy (MFMA) + f64 env", "data": "synthetic (on-device Philox scenes, "
+            "vs_baseline": None, "dtype": "f32 policy (f32 MFMA + fp32-accurate split products on the f16 MFMA) + f64 env",
+            "data": "synthetic (on-device Philox scenes, "
             "random-init policy, actions sampled from the policy)",
             "config": {"workload": "BASELINE configs[2]: full rollout (policy fwd -> sample -> env.step) + GAE"
                        + (" + RCCL trajectory all-gather" if world > 1 else ""),
@@ -524,14 +537,19 @@ def main():
                        "env_steps_per_step": E * T * world, "parallelism": f"env-sharded x{world}",
                        "full_reset_period": 200, "launch": mode},
             "roofline": {"kernel": pol_kernel, "bound": "mfma", "achieved": achieved_tf,
-                         "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / MFMA_F32_PEAK_TFLOPS,
+                         "peak": peak_alg, "unit": "TFLOP/s (fp32-accurate)", "frac": achieved_tf / peak_alg,
+                         "peak_source": (f"MFMA peak of the FLOP mix: {SPLIT_FLOP_PER_SAMPLE:,} FLOP/sample as split "
+                                         f"products on the f16 cores ({MFMA_SPLIT_PEAK_TFLOPS:.1f} TFLOP/s fp32-"
+                                         f"equivalent = 2.5 PF f16 / 3), the rest on the f32 MFMA "
+                                         f"({MFMA_F32_PEAK_TFLOPS} TFLOP/s); MI355X_MICROARCH.md"),
                          "traffic": pol_traffic,
                          "traffic_unit": "bytes per step (PMC bytes per launch / T)" if eng.persistent else
                          "bytes/launch (PMC)", "traffic_source": pol_src,
                          "avg_launch_ms": pol_ms, "flop_per_launch": POLICY_FLOP_PER_SAMPLE * E,
                          "flop_per_launch_source": "SURVEY.md 8(d): 2,446,208 FLOP/sample x E",
                          "executed_flop_per_launch": flop_exec * E, "executed_achieved": exec_tf,
-                         "executed_frac": exec_tf / MFMA_F32_PEAK_TFLOPS,
+                         "executed_peak": peak_exec, "executed_frac": exec_tf / peak_exec,
+                         "split_flop_per_launch": SPLIT_FLOP_PER_SAMPLE * E,
                          "steps_per_launch": T if eng.persistent else 1,
                          "path": ("fused rollout steps (window-row forward + sample + env step), all T steps of the "
                                   "iteration in one launch (per-step figures = launch / T)" if eng.persistent else

@@ -416,7 +416,9 @@ __device__ __forceinline__ LnPar ln_load(TID_F const f32x4 bb, const float* __re
 // PLANES: the output goes to sm.h as the two fp16 planes of the split products (the next GEMM's
 // operand; the caller keeps the fp32 output from `outv`); resid: the residual from registers (the
 // lane's own elements, as `outv` returned them) instead of sm.h.
-template <int CT, bool TR = false, bool PLANES = false>
+// ROW4 (with PLANES): the fp32 output of position 4 (tokens 64-79) also goes to sm.ctx rows 0-15 (the
+// next, pruned layer's residual and query rows).
+template <int CT, bool TR = false, bool PLANES = false, bool ROW4 = false>
 __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (&acc)[CT], const LnPar& lp, int ytok0,
                                                    const LnOut& lo = LnOut{}, f32x4* outv = nullptr,
                                                    const f32x4* resid = nullptr) {
@@ -481,6 +483,9 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
         const f32x4 out = xh * ww + lb;
         if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.h), tok * LDP + f0, out);
         else *reinterpret_cast<f32x4*>(sm.h + tok * LDH + f0) = out;
+        if constexpr (ROW4) {
+            if (ct == CT - 1) *reinterpret_cast<f32x4*>(sm.ctx + (tok - (S - 1) * SPW) * LDH + f0) = out;
+        }
         if (outv) outv[ct] = out;
         if (TR && !kExpNoStore) {
             const size_t r = (size_t)orow(tok, lo.b0, lo.compact);
@@ -509,6 +514,8 @@ __device__ __forceinline__ void store_rows(TID_F const float* src, int lds, floa
 // Full-layer attention for heads [4c, 4c+4): one (sample, head, query group) task per 4 lanes,
 // each lane owning 4 of the 16 head dims; the task loads the 5 keys / values once for all its
 // queries (group 0: positions 0-2 on waves 0-3, group 1: positions 3-4 on waves 4-7).
+// PLANES: the output goes to sm.ctx as the two fp16 planes of the split products (the out-projection's operand).
+template <bool PLANES = false>
 __device__ void attention_full(TID_F Smem& sm, int c) {
     const int q4 = TIDX() & 3, task = TIDX() >> 2;
     const int hh = task & 3, p = (task >> 2) & 15, grp = task >> 6;
@@ -546,7 +553,8 @@ __device__ void attention_full(TID_F Smem& sm, int c) {
             f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int j = 0; j < S; ++j) o += (sc[j] * inv) * v[j];
-            *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o;
+            if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), ti * LDP + 4 * c * HD + d0, o);
+            else *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o;
         }
     }
 }
@@ -661,30 +669,118 @@ __device__ __forceinline__ int kv_row(int wv, int c) { return (1 + (wv >> 2)) * 
 struct NoHook {
     __device__ void operator()() const {}
 };
+// Split-product paths of the inference forward (policy_layout.hpp kSplitParam): a full layer whose
+// out-projection and FFN run on the f16 cores, and a layer whose in_proj does (K / V / Q from the
+// fp16 planes of its input, which the previous layer's LN2 then writes).
+template <int trunk, int layer>
+constexpr bool split_tail() {
+    return layer < 2 && split_slot(layer_param(trunk, layer, OUTW)) >= 0 && split_slot(layer_param(trunk, layer, L1W)) >= 0 &&
+           split_slot(layer_param(trunk, layer, L2W)) >= 0;
+}
+template <int trunk, int layer>
+constexpr bool split_inproj() {
+    return layer < 2 && split_slot(layer_param(trunk, layer, INW)) >= 0;
+}
+// The caller's prefetch of a layer tail's first out-projection weights / of a layer's first K/V
+// weights: the split copy's blocks on the split paths, the fp32 fragments otherwise.
+template <int trunk, int layer, bool last, bool TR, int PSX = 0>
+using TailPre = std::conditional_t<!TR && !last && !PSX && split_tail<trunk, layer>(), HPre<2>,
+                                   APre<depth<(last || PSX) ? 1 : S>()>>;
+template <int trunk, int layer, bool last, bool TR>
+__device__ __forceinline__ TailPre<trunk, layer, last, TR> tail_prefetch(TID_F const float* __restrict__ P) {
+    const int wv = TIDX() >> 6;
+    if constexpr (!TR && !last && split_tail<trunk, layer>())
+        return hprefetch<2>(TID_C P, split_slot(layer_param(trunk, layer, OUTW)), D, 16 * wv, 0);
+    else
+        return prefetch<depth<last ? 1 : S>()>(TID_C P + kOffs.o[layer_param(trunk, layer, OUTW)], D, 16 * wv, 0);
+}
+template <int trunk, int layer, bool TR>
+using KvPre = std::conditional_t<!TR && split_inproj<trunk, layer>(), HPre<2>, APre<2>>;
+template <int trunk, int layer, bool TR>
+__device__ __forceinline__ KvPre<trunk, layer, TR> kv_prefetch(TID_F const float* __restrict__ P) {
+    const int wv = TIDX() >> 6;
+    if constexpr (!TR && split_inproj<trunk, layer>())
+        return hprefetch<2>(TID_C P, split_slot(layer_param(trunk, layer, INW)), D, kv_row(wv, 0), 0);
+    else
+        return prefetch<2>(TID_C P + kOffs.o[layer_param(trunk, layer, INW)], D, kv_row(wv, 0), 0);
+}
+
 // PSX (position split, the small-minibatch training step): a full (unpruned) layer computed for
 // the 16 tokens of ONE window position, column tile qt / 16, in [b * 5 + s] rows.
 template <int trunk, int layer, bool last, bool TR, class F = NoHook, int PSX = 0>
-__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const APre<depth<(last || PSX) ? 1 : S>()>& po,
+__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const TailPre<trunk, layer, last, TR, PSX>& po,
                            const TrainLayerIO& io, int b0, F pre_ln2 = F{}, int qt = 0);
+
+// A pruned inference layer whose in_proj runs as split products: K / V of all 80 tokens and Q of
+// position 4 from the fp16 planes of the layer input in sm.h (the previous layer's LN2 wrote them,
+// and its position-4 rows in fp32 to sm.ctx rows 0-15), fp32 Q | K | V into sm.big.
+template <int trunk, int layer>
+__device__ __forceinline__ void encoder_layer_split_inproj(TID_F Smem& sm, const float* __restrict__ P, HPre<2> pkv, int b0) {
+    [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
+    PTR(tb);
+    constexpr int si = split_slot(layer_param(trunk, layer, INW));
+    const float* bin = P + kOffs.o[layer_param(trunk, layer, INB)];
+    const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
+    const _Float16* hp = reinterpret_cast<const _Float16*>(sm.h);
+    APre<4> po;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {  // two chunks of 4 heads (LDS budget)
+        HPre<2> pq;
+        if (wv < 4) pq = hprefetch<2>(TID_C P, si, D, 64 * c + 16 * wv, 0);
+        {  // K (waves 0-3) / V (waves 4-7) of the chunk for all 80 tokens
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(bin + kv_row(wv, c) + 4 * g);
+            f32x4 hi[S], lo[S];
+            zero(hi);
+            zero(lo);
+            hgemm_tile<S, 2>(TID_C hi, lo, pkv, P, si, D, kv_row(wv, c), 0, hp, 0);
+            const int col = (1 + (wv >> 2)) * 64 + 16 * (wv & 3) + 4 * g;
+#pragma unroll
+            for (int ct = 0; ct < S; ++ct)
+                *reinterpret_cast<f32x4*>(sm.big + (16 * ct + i16) * LDB + col) = hi[ct] + lo[ct] * kLoScale + bb;
+        }
+        if (wv < 4) {  // Q of the chunk for position 4 (their SIMD partners did V)
+            const f32x4 bq = *reinterpret_cast<const f32x4*>(bin + 64 * c + 16 * wv + 4 * g);
+            f32x4 hi[1], lo[1];
+            zero(hi);
+            zero(lo);
+            hgemm_tile<1, 2>(TID_C hi, lo, pq, P, si, D, 64 * c + 16 * wv, 0, hp, (S - 1) * SPW);
+            *reinterpret_cast<f32x4*>(sm.big + ((S - 1) * SPW + i16) * LDB + 16 * wv + 4 * g) = hi[0] + lo[0] * kLoScale + bq;
+        }
+        if (c == 0) pkv = hprefetch<2>(TID_C P, si, D, kv_row(wv, 1), 0);
+        else po = prefetch<4>(TID_C P + kOffs.o[layer_param(trunk, layer, OUTW)], D, 16 * wv, 0);
+        PTR(tb + 1 + 3 * c);
+        __syncthreads();
+        PTR(tb + 2 + 3 * c);
+        attention_chunk(TID_C sm, c, S - 1, 1);
+        __syncthreads();
+        PTR(tb + 3 + 3 * c);
+    }
+    layer_tail<trunk, layer, true, false>(TID_C sm, P, po, TrainLayerIO{}, b0);
+}
 
 // One post-LN nn.TransformerEncoderLayer (relu FFN 256, 8 heads). last: prune to column tile 4.
 // Work split: 8 waves, wave w and w+4 share a SIMD (and its MFMA pipe); every GEMM gives each
 // SIMD the same number of 16-row output tiles. `pkv` = the caller's prefetch of this layer's first
 // K/V weight blocks. Ends WITHOUT a final barrier: the caller prefetches its next weights, then syncs.
 template <int trunk, int layer, bool last, bool TR = false, class F = NoHook>
-__device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __restrict__ P, APre<2> pkv,
+__device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __restrict__ P, KvPre<trunk, layer, TR> pkv,
                               const TrainLayerIO& io = TrainLayerIO{}, int b0 = 0, F pre_ln2 = F{}) {
+    if constexpr (!TR && split_inproj<trunk, layer>()) {
+        static_assert(last, "split in_proj: a pruned layer after a split full layer");
+        encoder_layer_split_inproj<trunk, layer>(TID_C sm, P, pkv, b0);
+        return;
+    } else {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
     PTR(tb);
     const float* Win = P + kOffs.o[layer_param(trunk, layer, INW)];
     const float* bin = P + kOffs.o[layer_param(trunk, layer, INB)];
-    const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
     const int wv = TIDX() >> 6;
     constexpr int CTQ = last ? 1 : S;              // column tiles that need Q / out / LN / FFN
     constexpr int DQ = depth<CTQ>();
     constexpr int qtok0 = last ? (S - 1) * SPW : 0;
+    constexpr bool planes = !TR && !last && split_tail<trunk, layer>();
 
-    APre<DQ> po;
+    TailPre<trunk, layer, last, TR> po;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {  // two chunks of 4 heads (LDS budget)
         APre<DQ> pq;
@@ -694,7 +790,7 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
         // Q of the chunk for the query tokens, waves 0-3 (their SIMD partners did V)
         if (wv < 4) linear1<CTQ, false, DQ>(TID_C pq, Win, D, bin, 64 * c + 16 * wv, sm.h, LDH, qtok0, sm.big, LDB, 16 * wv, qtok0);
         if (c == 0) pkv = prefetch<2>(TID_C Win, D, kv_row(wv, 1), 0);
-        else po = prefetch<DQ>(TID_C Wo, D, 16 * wv, 0);
+        else po = tail_prefetch<trunk, layer, last, TR>(TID_C P);
         PTR(tb + 1 + 3 * c);
         __syncthreads();
         PTR(tb + 2 + 3 * c);
@@ -709,24 +805,25 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
             }
         }
         if (last) attention_chunk(TID_C sm, c, S - 1, 1);
-        else attention_full(TID_C sm, c);
+        else attention_full<planes>(TID_C sm, c);
         __syncthreads();
         PTR(tb + 3 + 3 * c);
     }
     layer_tail<trunk, layer, last, TR>(TID_C sm, P, po, io, b0, pre_ln2);
+    }
 }
 
 // Out-projection + LN1 + FFN + LN2 of a full (80-token) inference layer with the FFN as split
 // products (layer_tail's kSplit path); the out-projection stays on the f32 MFMA.
 template <int trunk, int layer>
-__device__ __forceinline__ void layer_ffn_split(TID_F Smem& sm, const float* __restrict__ P, const APre<depth<S>()>& po) {
+__device__ __forceinline__ void layer_ffn_split(TID_F Smem& sm, const float* __restrict__ P, const HPre<2>& po) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
-    constexpr int DQ = depth<S>();
-    const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
     const float* bo = P + kOffs.o[layer_param(trunk, layer, OUTB)];
     const float* b1 = P + kOffs.o[layer_param(trunk, layer, L1B)];
     const float* b2 = P + kOffs.o[layer_param(trunk, layer, L2B)];
     constexpr int s1 = split_slot(layer_param(trunk, layer, L1W)), s2 = split_slot(layer_param(trunk, layer, L2W));
+    constexpr int so = split_slot(layer_param(trunk, layer, OUTW));
+    constexpr bool next_planes = split_inproj<trunk, layer + 1>();  // LN2 writes the next layer's operand planes
     const int wv = TIDX() >> 6;
     _Float16* const hp = reinterpret_cast<_Float16*>(sm.h);
     _Float16* const bp = reinterpret_cast<_Float16*>(sm.big);
@@ -736,8 +833,14 @@ __device__ __forceinline__ void layer_ffn_split(TID_F Smem& sm, const float* __r
     {
         const f32x4 bo4 = ln_bias(TID_C bo);
         f32x4 acc[S];
-        zero(acc);
-        gemm_tile<S, DQ>(TID_C acc, po, Wo, D, 16 * wv, 0, sm.ctx, LDH, 0);
+        {  // out-projection from the attention output's planes (attention_full<true>)
+            f32x4 hi[S], lo[S];
+            zero(hi);
+            zero(lo);
+            hgemm_tile<S, 2>(TID_C hi, lo, po, P, so, D, 16 * wv, 0, cp, 0);
+#pragma unroll
+            for (int ct = 0; ct < S; ++ct) acc[ct] = hi[ct] + lo[ct] * kLoScale;
+        }
         PTR(tb + 7);
         const LnPar lp = ln_load(TID_C bo4, P + kOffs.o[layer_param(trunk, layer, N1W)], P + kOffs.o[layer_param(trunk, layer, N1B)]);
         w1a = hprefetch<2>(TID_C P, s1, D, 16 * wv, 0);
@@ -777,14 +880,14 @@ __device__ __forceinline__ void layer_ffn_split(TID_F Smem& sm, const float* __r
     f32x4 acc2[S];
 #pragma unroll
     for (int ct = 0; ct < S; ++ct) acc2[ct] = hi[ct] + lo[ct] * kLoScale;
-    residual_layernorm<S>(TID_C sm, acc2, lp2, 0, LnOut{}, nullptr, h1);
+    residual_layernorm<S, false, next_planes, next_planes>(TID_C sm, acc2, lp2, 0, LnOut{}, nullptr, h1);
     PTR(tb + 14);
 }
 
 // Out-projection + LN1 + FFN + LN2 of an encoder layer, after the attention output is in sm.ctx.
 // `po` = the caller's prefetch of the first out_proj weight blocks.
 template <int trunk, int layer, bool last, bool TR, class F, int PSX>
-__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const APre<depth<(last || PSX) ? 1 : S>()>& po,
+__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const TailPre<trunk, layer, last, TR, PSX>& po,
                            const TrainLayerIO& io, int b0, F pre_ln2, int qt) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
     const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
@@ -805,12 +908,13 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
     // matrix cores (hgemm_tile): LN1 writes its output as the two fp16 planes into sm.h and keeps
     // the fp32 values in registers (LN2's residual), FFN1 writes the hidden planes into big
     // (features 0-127) and ctx (128-255), FFN2 reads them
-    constexpr bool kSplit = !TR && CTQ == S && split_slot(layer_param(trunk, layer, L1W)) >= 0 &&
-                            split_slot(layer_param(trunk, layer, L2W)) >= 0;
-    if constexpr (kSplit) {
+    if constexpr (!TR && !last && !PSX && split_tail<trunk, layer>()) {
         layer_ffn_split<trunk, layer>(TID_C sm, P, po);
         return;
-    }
+    } else {
+    // a pruned layer after a split full layer: the residual (its input at position 4) is in sm.ctx
+    // rows 0-15 (sm.h holds the input's fp16 planes)
+    constexpr bool kResCtx = !TR && last && !PSX && split_inproj<trunk, layer>();
     // inference, full layer: the wave's own 16 LayerNorm output features are FFN1's k-block wv, so
     // its MFMAs over that block run from registers before the barrier (beside the other waves'
     // LayerNorm work) and the GEMM after it covers the other 7 blocks (k-block order rotated)
@@ -843,7 +947,12 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
         } else {
             pf1a = prefetch<DQ>(TID_C W1, D, 16 * wv, 0);
             pf1b = prefetch<DQ>(TID_C W1, D, 128 + 16 * wv, 0);
-            residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, io.h1, io.rstd1, b0, last});
+            if constexpr (kResCtx) {
+                const f32x4 r4[1] = {*reinterpret_cast<const f32x4*>(sm.ctx + (LANE() & 15) * LDH + 16 * wv + 4 * (LANE() >> 4))};
+                residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{}, nullptr, r4);
+            } else {
+                residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, io.h1, io.rstd1, b0, last});
+            }
         }
     }
     PTR(tb + 8);
@@ -881,6 +990,7 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
     pre_ln2();
     residual_layernorm<CTQ, TR>(TID_C sm, acc2, lp2, qtok0, LnOut{io.xhat2, io.h2, io.rstd2, b0, last});
     PTR(tb + 14);
+    }
 }
 
 // ------------------------------------------------------------------ window-row projections
@@ -1012,11 +1122,10 @@ __device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* 
                                    const RowIO& rio, int b0) {
     constexpr bool last = trunk == kActorTrunk;  // the actor's layer 0 is its last (pruned) layer
     constexpr int P0 = 3 - NP, ROFF = trunk == kActorTrunk ? 0 : 2 * D;
-    constexpr int CTQ = last ? 1 : S, DQ = depth<CTQ>();
+    constexpr bool planes = !last && split_tail<trunk, 0>();  // attention output as split-product planes
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1);
     PTR(tb);
     const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
-    const float* Wo = P + kOffs.o[layer_param(trunk, 0, OUTW)];
     const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
     const int rows[3] = {16 * wv, D + 16 * wv, 2 * D + 16 * wv};
     f32x4 acc[3] = {};
@@ -1035,7 +1144,7 @@ __device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* 
     PTR(tb + 13);
     const float* pl = reinterpret_cast<const float*>(sm.red);
     const int q = TIDX() & 15;
-    APre<DQ> po;
+    TailPre<trunk, 0, last, false> po;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         // Q | K | V of the chunk -> sm.big: positions 0-3 from the ring, position 4 from acc
@@ -1055,13 +1164,13 @@ __device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* 
                     acc[j] + *reinterpret_cast<const f32x4*>(pl + (S - 1) * 192 + col);
             }
         }
-        if (c == 1) po = prefetch<DQ>(TID_C Wo, D, 16 * wv, 0);
+        if (c == 1) po = tail_prefetch<trunk, 0, last, false>(TID_C P);
         PTR(tb + 1 + 3 * c);
         __syncthreads();
         PTR(tb + 2 + 3 * c);
         if (c == 0) ppos_stage(TID_C sm, rp, 1);  // sm.red is read again only by the chunk-1 assembly
         if (last) attention_chunk(TID_C sm, c, S - 1, 1);
-        else attention_full(TID_C sm, c);
+        else attention_full<planes>(TID_C sm, c);
         __syncthreads();
         PTR(tb + 3 + 3 * c);
     }
@@ -1383,7 +1492,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             __syncthreads();
             encoder_layer_rows<kCriticTrunk>(TID_C sm, P, pw, rp, rio, b0);
         }
-        APre<2> pkv;
+        KvPre<kCriticTrunk, 1, TR> pkv;
         if constexpr (!ROWS) {
             if constexpr (TR) {
                 embed_apply<kCriticTrunk, TR>(TID_C sm, ep_c, io.e[1], io.h0[1], b0);
@@ -1398,7 +1507,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
                 encoder_layer<kCriticTrunk, 0, false, TR>(TID_C sm, P, pkv0, io.L[1], b0);
             }
         }
-        if (!TR) pkv = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
+        if (!TR) pkv = kv_prefetch<kCriticTrunk, 1, TR>(TID_C P);
         __syncthreads();
         if constexpr (TR) {
             encoder_layer<kCriticTrunk, 1, true, TR>(TID_C sm, P, pkv, io.L[2], b0, [&] {

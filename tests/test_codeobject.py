@@ -54,7 +54,7 @@ def body(asm, name):
 
 # (f32, f16) MFMA instructions in k_rollout_steps: the f32 GEMMs, and the split-product GEMMs of the
 # critic's full layer
-ROLLOUT_MFMA = (1160, 240)
+ROLLOUT_MFMA = (616, 444)
 
 
 def check_limits(name, m, vgpr_spills=16, sgpr_spills=8):
