@@ -643,7 +643,10 @@ __device__ void embed_apply(TID_F Smem& sm, const EmbPre& ep, float* e_out = nul
         f32x4 e = acc[ct] + ep.bb;
         e.x = fmaxf(e.x, 0.f); e.y = fmaxf(e.y, 0.f); e.z = fmaxf(e.z, 0.f); e.w = fmaxf(e.w, 0.f);
         const int o = (ct * SPW + i16) * LDH + 16 * wv + 4 * g;
-        if (MODE == kEmbRows || (MODE == kEmbSplit && ct == S - 1)) *reinterpret_cast<f32x4*>(sm.ctx + o) = e;
+        constexpr bool ring_planes = split_slot(layer_param(trunk, 0, INW)) >= 0;  // the ring GEMM's operand
+        if ((MODE == kEmbRows || (MODE == kEmbSplit && ct == S - 1)) && ring_planes)
+            hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), (ct * SPW + i16) * LDP + 16 * wv + 4 * g, e);
+        else if (MODE == kEmbRows || (MODE == kEmbSplit && ct == S - 1)) *reinterpret_cast<f32x4*>(sm.ctx + o) = e;
         if (MODE == kEmbRows) continue;
         const f32x4 v = e + ep.pp[ct];
         *reinterpret_cast<f32x4*>(sm.h + o) = v;
@@ -678,8 +681,9 @@ constexpr bool split_tail() {
            split_slot(layer_param(trunk, layer, L2W)) >= 0;
 }
 template <int trunk, int layer>
-constexpr bool split_inproj() {
-    return layer < 2 && split_slot(layer_param(trunk, layer, INW)) >= 0;
+constexpr bool split_inproj() {  // layer >= 1: its input comes from a split full layer's LN2 (layer 0's
+                                 // in_proj split copy serves the window-row ring only: split_ring)
+    return layer >= 1 && layer < 2 && split_slot(layer_param(trunk, layer, INW)) >= 0;
 }
 // The caller's prefetch of a layer tail's first out-projection weights / of a layer's first K/V
 // weights: the split copy's blocks on the split paths, the fp32 fragments otherwise.
@@ -1113,12 +1117,61 @@ __device__ __forceinline__ void gemm_rows(TID_F f32x4 (&acc)[R], const APre<D> (
     }
 }
 
+// gemm_rows as split products: R weight tiles of a split copy against one activation tile's planes
+template <int R, int D_, class F>
+__device__ __forceinline__ void hgemm_rows(TID_F f32x4 (&hi)[R], f32x4 (&lo)[R], const HPre<D_> (&pre)[R],
+                                           const float* __restrict__ P, int soff, int K, const int (&row)[R],
+                                           const _Float16* X, int xtok0, F&& issued) {
+    constexpr int NKB = D / 32;
+    const int l = LANE(), i16 = l & 15, g = l >> 4;
+    const _Float16* xp = X + (xtok0 + i16) * LDP + 8 * g;
+    f16x8 a1[NKB][R], a2[NKB][R], b1[NKB], b2[NKB];
+#pragma unroll
+    for (int p = 0; p < D_; ++p)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            a1[p][r] = pre[r].a1[p];
+            a2[p][r] = pre[r].a2[p];
+        }
+    b1[0] = *reinterpret_cast<const f16x8*>(xp);
+    b2[0] = *reinterpret_cast<const f16x8*>(xp + kPlane);
+#pragma unroll
+    for (int i = 0; i < NKB; ++i) {
+        if (i + 1 < NKB) {  // B one block ahead
+            b1[i + 1] = *reinterpret_cast<const f16x8*>(xp + 32 * (i + 1));
+            b2[i + 1] = *reinterpret_cast<const f16x8*>(xp + 32 * (i + 1) + kPlane);
+        }
+        if (i + D_ < NKB) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const f16x8* wp = hfrag_ptr(TID_C P, soff, K, row[r], 0) + 128 * (i + D_);
+                a1[i + D_][r] = wp[0];
+                a2[i + D_][r] = wp[64];
+            }
+        }
+        if (i == (D_ < NKB ? NKB - D_ - 1 : 0)) issued();
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            hi[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i][r], b1[i], hi[r], 0, 0, 0);
+            lo[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i][r], b2[i], lo[r], 0, 0, 0);
+            lo[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[i][r], b1[i], lo[r], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+// The new-row GEMM's weight prefetch (rows_prologue): the split copy's first blocks when layer 0's
+// in_proj has one, the fp32 fragments otherwise.
+template <int trunk>
+constexpr bool split_ring() { return split_slot(layer_param(trunk, 0, INW)) >= 0; }
+template <int trunk>
+using RingPre = std::conditional_t<split_ring<trunk>(), HPre<2>, APre<kPwD>>;
+
 // Layer 0 of a trunk on the ring: u of the new row (position 4) from `pw` (in_proj rows 128 j +
 // 16 wv: this wave's Q, K and V features, all in chunk wv >> 2) and the ring rows of positions
 // 0-3 from `rp`; then attention and layer_tail as in encoder_layer. Expects sm.ctx rows 64-79 =
 // e of position 4 (embed_apply kEmbSplit), sm.red = Win pos_s of chunk 0 (ppos_stage).
 template <int trunk, int NP>
-__device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* __restrict__ P, const APre<kPwD> (&pw)[3], RowPre<NP>& rp,
+__device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* __restrict__ P, const RingPre<trunk> (&pw)[3], RowPre<NP>& rp,
                                    const RowIO& rio, int b0) {
     constexpr bool last = trunk == kActorTrunk;  // the actor's layer 0 is its last (pruned) layer
     constexpr int P0 = 3 - NP, ROFF = trunk == kActorTrunk ? 0 : 2 * D;
@@ -1129,10 +1182,19 @@ __device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* 
     const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
     const int rows[3] = {16 * wv, D + 16 * wv, 2 * D + 16 * wv};
     f32x4 acc[3] = {};
-    gemm_rows<3, kPwD>(TID_C acc, pw, Win, D, rows, sm.ctx, LDH, (S - 1) * SPW, [&] {
+    auto ring_issue = [&] {
         ring_load<trunk>(TID_C rp, sm, rio, b0, 0);
         if (trunk == kActorTrunk) ring_load<trunk>(TID_C rp, sm, rio, b0, 1);
-    });
+    };
+    if constexpr (split_ring<trunk>()) {  // e of position 4 as planes in sm.ctx (embed_apply kEmbSplit)
+        f32x4 lo[3] = {};
+        hgemm_rows<3, 2>(TID_C acc, lo, pw, P, split_slot(layer_param(trunk, 0, INW)), D, rows,
+                         reinterpret_cast<const _Float16*>(sm.ctx), (S - 1) * SPW, ring_issue);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[j] += lo[j] * kLoScale;
+    } else {
+        gemm_rows<3, kPwD>(TID_C acc, pw, Win, D, rows, sm.ctx, LDH, (S - 1) * SPW, ring_issue);
+    }
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[j] += rp.bias[j];  // u = Win e + b
     if (b0 + i16 < rio.B) {  // the new row -> ring slot g mod 5
@@ -1182,14 +1244,17 @@ __device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* 
 // and bias. Ends with the embedding in sm.h / sm.ctx and Win pos_s of
 // chunk 0 in sm.red, without a barrier.
 template <int trunk, int NP>
-__device__ __forceinline__ void rows_prologue(TID_F Smem& sm, const float* __restrict__ P, APre<kPwD> (&pw)[3],
+__device__ __forceinline__ void rows_prologue(TID_F Smem& sm, const float* __restrict__ P, RingPre<trunk> (&pw)[3],
                                               RowPre<NP>& rp, const RowIO& rio, int b0) {
     const int wv = TIDX() >> 6;
     const EmbPre ep = embed_load<trunk>(TID_C P);
     ppos_load<trunk>(TID_C rp, rio);
     const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) pw[j] = prefetch<kPwD>(TID_C Win, D, j * D + 16 * wv, 0);
+    for (int j = 0; j < 3; ++j) {
+        if constexpr (split_ring<trunk>()) pw[j] = hprefetch<2>(TID_C P, split_slot(layer_param(trunk, 0, INW)), D, j * D + 16 * wv, 0);
+        else pw[j] = prefetch<kPwD>(TID_C Win, D, j * D + 16 * wv, 0);
+    }
     const float* bin = P + kOffs.o[layer_param(trunk, 0, INB)];
 #pragma unroll
     for (int j = 0; j < 3; ++j) rp.bias[j] = *reinterpret_cast<const f32x4*>(bin + j * D + 16 * wv + 4 * (LANE() >> 4));
@@ -1437,7 +1502,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     const float* headw_c = P + kOffs.o[kCriticHead];
     // actor trunk (1 layer) + head
     if constexpr (ROWS) {
-        APre<kPwD> pw[3];
+        RingPre<kActorTrunk> pw[3];
         RowPre<2> rp;
         rows_prologue<kActorTrunk>(TID_C sm, P, pw, rp, rio, b0);
         PTR(2);
@@ -1486,7 +1551,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     if (do_critic) {
         // critic trunk (2 layers) + head
         if constexpr (ROWS) {
-            APre<kPwD> pw[3];
+            RingPre<kCriticTrunk> pw[3];
             RowPre<3> rp;
             rows_prologue<kCriticTrunk>(TID_C sm, P, pw, rp, rio, b0);
             __syncthreads();
@@ -1719,7 +1784,17 @@ __device__ void rows_fill_trunk(Smem& sm, const float* __restrict__ P, const Row
         const int row = j * D + 16 * wv;
         f32x4 acc[S - 1];
         zero(acc);
-        gemm_tile<S - 1, 2>(acc, prefetch<2>(Win, D, row, 0), Win, D, row, 0, sm.ctx, LDH, 0);
+        if constexpr (split_ring<trunk>()) {  // the forward's new-row GEMM as split products: the same sums
+            constexpr int si = split_slot(layer_param(trunk, 0, INW));
+            f32x4 lo[S - 1];
+            zero(lo);
+            hgemm_tile<S - 1, 2>(acc, lo, hprefetch<2>(P, si, D, row, 0), P, si, D, row, 0,
+                                 reinterpret_cast<const _Float16*>(sm.ctx), 0);
+#pragma unroll
+            for (int s = 0; s < S - 1; ++s) acc[s] += lo[s] * kLoScale;
+        } else {
+            gemm_tile<S - 1, 2>(acc, prefetch<2>(Win, D, row, 0), Win, D, row, 0, sm.ctx, LDH, 0);
+        }
         const f32x4 bb = *reinterpret_cast<const f32x4*>(bin + row + 4 * g);
         const int b = b0 + i16;
         if (b < rio.B) {
