@@ -10,8 +10,8 @@ value = E * T * K * N / max-over-ranks wall time. Inputs (scenes, windows) are r
 
 Also reported (same JSON line):
   roofline      dominant kernel = k_rollout_steps (per-step figures: its launch / T); peak = the MFMA
-                peak of its FLOP mix (the critic's 80-token GEMMs as fp32-accurate split products on
-                the f16 cores at 16/3 x the f32 MFMA rate, the rest on the f32 MFMA);
+                peak of its FLOP mix (the encoder GEMMs as fp32-accurate split products on the f16
+                cores at 16/3 x the f32 MFMA rate, embeddings and heads on the f32 MFMA);
                 achieved = ALGORITHMIC FLOP per step (2,446,208 FLOP/sample, the
                 last-token-pruned forward of one window) x E / its HIP-event duration per step in the
                 last timed iteration; traffic = PMC bytes per step (profiles/rNN_pmc.json). The rollout's
@@ -56,11 +56,16 @@ POLICY_FLOP_PER_SAMPLE = 2_446_208  # full-window forward (last-
 # the rollout's window-row path (uavhip_policy_forward_rows) forms layer-0 Q|K|V of the new row
 # only: minus 4 rows x (actor K,V 256 + critic Q,K,V 384) x 128 x 2 FLOP
 ROWS_FLOP_PER_SAMPLE = POLICY_FLOP_PER_SAMPLE - 4 * (256 + 384) * 128 * 2  # 1,790,848
-# of these, the GEMMs over all 80 tokens of the critic (layer-0 out-projection + FFN, layer-1 K / V, and
-# its position-4 Q) run as split products on the f16 matrix cores (3 x v_mfma_f32_16x16x32_f16 per
-# fp32-accurate 16 x 16 x 32 block): (128 + 2 * 256 + 256) x 128 x 2 x 80 + 128 x 128 x 2 x 16
-# FLOP per 16-sample workgroup
-SPLIT_FLOP_PER_SAMPLE = ((128 + 2 * 256 + 256) * 128 * 2 * 80 + 128 * 128 * 2 * 16) // 16  # 1,179,648
+# of these, every encoder GEMM runs as split products on the f16 matrix cores (3 x
+# v_mfma_f32_16x16x32_f16 per fp32-accurate 16 x 16 x 32 block), per 16-sample workgroup:
+# the critic's layer 0 out-projection + FFN over 80 tokens, its layer-1 K / V over 80 tokens and Q over
+# 16, the out-projection + FFN of both pruned top layers over 16 tokens, and -- on the window-row
+# ring -- the new row's layer-0 Q | K | V of both trunks (16 tokens). The embeddings and heads stay on
+# the f32 MFMA.
+_SPLIT_WG = ((128 + 2 * 256) * 128 * 2 * 80 + 256 * 128 * 2 * 80 + 128 * 128 * 2 * 16
+             + 2 * (128 + 2 * 256) * 128 * 2 * 16)
+SPLIT_FLOP_PER_SAMPLE = _SPLIT_WG // 16                                         # full window: 1,507,328
+SPLIT_FLOP_PER_SAMPLE_ROWS = (_SPLIT_WG + 2 * 384 * 128 * 2 * 16) // 16         # ring: 1,703,936
 MFMA_SPLIT_PEAK_TFLOPS = 157.3 * 16 / 3  # fp32-equivalent: f16 MFMA (16x the f32 rate) / 3 products
 TRAIN_FLOP_PER_SAMPLE_EPOCH = 3 * 4_040_000  # training ~ 3 x dense forward
 TRAIN_EXEC_FLOP_PER_SAMPLE_EPOCH = 7_460_000  # pruned forward + dX + dW
@@ -470,10 +475,13 @@ def main():
     flop_exec = ROWS_FLOP_PER_SAMPLE if eng.rowproj is not None else POLICY_FLOP_PER_SAMPLE
     achieved_tf = POLICY_FLOP_PER_SAMPLE * E / (pol_ms * 1e-3) / 1e12
     exec_tf = flop_exec * E / (pol_ms * 1e-3) / 1e12
-    # the MFMA peak of the FLOP mix: f32 MFMA for the rest, split products at 16/3 x the f32 rate
-    mix_peak = lambda flop: flop / ((flop - SPLIT_FLOP_PER_SAMPLE) / MFMA_F32_PEAK_TFLOPS  # noqa: E731
-                                   + SPLIT_FLOP_PER_SAMPLE / MFMA_SPLIT_PEAK_TFLOPS)
-    peak_alg, peak_exec = mix_peak(POLICY_FLOP_PER_SAMPLE), mix_peak(flop_exec)
+    # the MFMA peak of the FLOP mix: split products at 16/3 x the f32 rate, the rest on the f32 MFMA.
+    # The algorithmic count prices the ring's skipped layer-0 rows as the same split products.
+    split = SPLIT_FLOP_PER_SAMPLE_ROWS if eng.rowproj is not None else SPLIT_FLOP_PER_SAMPLE
+    mix_peak = lambda flop, sp: flop / ((flop - sp) / MFMA_F32_PEAK_TFLOPS  # noqa: E731
+                                        + sp / MFMA_SPLIT_PEAK_TFLOPS)
+    split_alg = split + (POLICY_FLOP_PER_SAMPLE - flop_exec)
+    peak_alg, peak_exec = mix_peak(POLICY_FLOP_PER_SAMPLE, split_alg), mix_peak(flop_exec, split)
     env_gbs = None if env_ms is None else env_bytes_per_step(args.targets) * E / (env_ms * 1e-3) / 1e9
 
     env_fused = stress = None
@@ -538,8 +546,8 @@ def main():
                        "full_reset_period": 200, "launch": mode},
             "roofline": {"kernel": pol_kernel, "bound": "mfma", "achieved": achieved_tf,
                          "peak": peak_alg, "unit": "TFLOP/s (fp32-accurate)", "frac": achieved_tf / peak_alg,
-                         "peak_source": (f"MFMA peak of the FLOP mix: {SPLIT_FLOP_PER_SAMPLE:,} FLOP/sample as split "
-                                         f"products on the f16 cores ({MFMA_SPLIT_PEAK_TFLOPS:.1f} TFLOP/s fp32-"
+                         "peak_source": (f"MFMA peak of the FLOP mix: {split_alg:,} of the {POLICY_FLOP_PER_SAMPLE:,} "
+                                         f"FLOP/sample as split products on the f16 cores ({MFMA_SPLIT_PEAK_TFLOPS:.1f} TFLOP/s fp32-"
                                          f"equivalent = 2.5 PF f16 / 3), the rest on the f32 MFMA "
                                          f"({MFMA_F32_PEAK_TFLOPS} TFLOP/s); MI355X_MICROARCH.md"),
                          "traffic": pol_traffic,
@@ -549,7 +557,7 @@ def main():
                          "flop_per_launch_source": "SURVEY.md 8(d): 2,446,208 FLOP/sample x E",
                          "executed_flop_per_launch": flop_exec * E, "executed_achieved": exec_tf,
                          "executed_peak": peak_exec, "executed_frac": exec_tf / peak_exec,
-                         "split_flop_per_launch": SPLIT_FLOP_PER_SAMPLE * E,
+                         "split_flop_per_launch": split * E,
                          "steps_per_launch": T if eng.persistent else 1,
                          "path": ("fused rollout steps (window-row forward + sample + env step), all T steps of the "
                                   "iteration in one launch (per-step figures = launch / T)" if eng.persistent else

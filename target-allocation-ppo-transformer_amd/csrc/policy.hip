@@ -563,6 +563,7 @@ __device__ void attention_full(TID_F Smem& sm, int c) {
 // the keys/values of all 5 positions; reads sm.big (Q|K|V of the chunk), writes sm.ctx.
 // One (query, head) task per 4 consecutive lanes, each lane owning 4 of the 16 head dims
 // (dot products reduced over the quad with two xor-shuffles).
+template <bool PLANES = false>
 __device__ void attention_chunk(TID_F Smem& sm, int c, int qs0, int nqs) {
     const int ntask = nqs * SPW * 4;
     const int q4 = TIDX() & 3;
@@ -594,7 +595,8 @@ __device__ void attention_chunk(TID_F Smem& sm, int c, int qs0, int nqs) {
             const f32x4 v = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 128 + d0);
             o += (sc[j] * inv) * v;
         }
-        *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o;
+        if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), ti * LDP + 4 * c * HD + d0, o);
+        else *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o;
     }
 }
 
@@ -688,12 +690,12 @@ constexpr bool split_inproj() {  // layer >= 1: its input comes from a split ful
 // The caller's prefetch of a layer tail's first out-projection weights / of a layer's first K/V
 // weights: the split copy's blocks on the split paths, the fp32 fragments otherwise.
 template <int trunk, int layer, bool last, bool TR, int PSX = 0>
-using TailPre = std::conditional_t<!TR && !last && !PSX && split_tail<trunk, layer>(), HPre<2>,
+using TailPre = std::conditional_t<!TR && !PSX && split_tail<trunk, layer>(), HPre<2>,
                                    APre<depth<(last || PSX) ? 1 : S>()>>;
 template <int trunk, int layer, bool last, bool TR>
 __device__ __forceinline__ TailPre<trunk, layer, last, TR> tail_prefetch(TID_F const float* __restrict__ P) {
     const int wv = TIDX() >> 6;
-    if constexpr (!TR && !last && split_tail<trunk, layer>())
+    if constexpr (!TR && split_tail<trunk, layer>())
         return hprefetch<2>(TID_C P, split_slot(layer_param(trunk, layer, OUTW)), D, 16 * wv, 0);
     else
         return prefetch<depth<last ? 1 : S>()>(TID_C P + kOffs.o[layer_param(trunk, layer, OUTW)], D, 16 * wv, 0);
@@ -726,7 +728,8 @@ __device__ __forceinline__ void encoder_layer_split_inproj(TID_F Smem& sm, const
     const float* bin = P + kOffs.o[layer_param(trunk, layer, INB)];
     const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
     const _Float16* hp = reinterpret_cast<const _Float16*>(sm.h);
-    APre<4> po;
+    TailPre<trunk, layer, true, false> po;
+    constexpr bool planes = split_tail<trunk, layer>();
 #pragma unroll
     for (int c = 0; c < 2; ++c) {  // two chunks of 4 heads (LDS budget)
         HPre<2> pq;
@@ -751,11 +754,11 @@ __device__ __forceinline__ void encoder_layer_split_inproj(TID_F Smem& sm, const
             *reinterpret_cast<f32x4*>(sm.big + ((S - 1) * SPW + i16) * LDB + 16 * wv + 4 * g) = hi[0] + lo[0] * kLoScale + bq;
         }
         if (c == 0) pkv = hprefetch<2>(TID_C P, si, D, kv_row(wv, 1), 0);
-        else po = prefetch<4>(TID_C P + kOffs.o[layer_param(trunk, layer, OUTW)], D, 16 * wv, 0);
+        else po = tail_prefetch<trunk, layer, true, false>(TID_C P);
         PTR(tb + 1 + 3 * c);
         __syncthreads();
         PTR(tb + 2 + 3 * c);
-        attention_chunk(TID_C sm, c, S - 1, 1);
+        attention_chunk<planes>(TID_C sm, c, S - 1, 1);
         __syncthreads();
         PTR(tb + 3 + 3 * c);
     }
@@ -782,7 +785,7 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
     constexpr int CTQ = last ? 1 : S;              // column tiles that need Q / out / LN / FFN
     constexpr int DQ = depth<CTQ>();
     constexpr int qtok0 = last ? (S - 1) * SPW : 0;
-    constexpr bool planes = !TR && !last && split_tail<trunk, layer>();
+    constexpr bool planes = !TR && split_tail<trunk, layer>();
 
     TailPre<trunk, layer, last, TR> po;
 #pragma unroll
@@ -808,7 +811,7 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
                     *reinterpret_cast<const f32x4*>(sm.big + tok * LDB + part * 64 + 4 * q);
             }
         }
-        if (last) attention_chunk(TID_C sm, c, S - 1, 1);
+        if (last) attention_chunk<planes>(TID_C sm, c, S - 1, 1);
         else attention_full<planes>(TID_C sm, c);
         __syncthreads();
         PTR(tb + 3 + 3 * c);
@@ -817,38 +820,51 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
     }
 }
 
-// Out-projection + LN1 + FFN + LN2 of a full (80-token) inference layer with the FFN as split
-// products (layer_tail's kSplit path); the out-projection stays on the f32 MFMA.
-template <int trunk, int layer>
-__device__ __forceinline__ void layer_ffn_split(TID_F Smem& sm, const float* __restrict__ P, const HPre<2>& po) {
+// Out-projection + LN1 + FFN + LN2 of an inference layer as split products (layer_tail's split
+// path): a full layer (80 tokens) or a pruned one (the 16 tokens of position 4). The attention
+// output's planes are in sm.ctx (attention_full / attention_chunk <true>); LN1 writes its output's
+// planes into sm.h and keeps the fp32 values in registers (LN2's residual); FFN1 writes the hidden
+// planes into big (features 0-127) and ctx (128-255); LN2 writes fp32 into sm.h -- or, when the next
+// layer's in_proj runs as split products, that layer's operand planes (and position 4 in fp32 to
+// sm.ctx rows 0-15). A pruned layer after such a layer takes its residual from sm.ctx rows 0-15.
+template <int trunk, int layer, bool last>
+__device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __restrict__ P, const HPre<2>& po) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
+    constexpr int CT = last ? 1 : S, t0 = last ? (S - 1) * SPW : 0;
     const float* bo = P + kOffs.o[layer_param(trunk, layer, OUTB)];
     const float* b1 = P + kOffs.o[layer_param(trunk, layer, L1B)];
     const float* b2 = P + kOffs.o[layer_param(trunk, layer, L2B)];
     constexpr int s1 = split_slot(layer_param(trunk, layer, L1W)), s2 = split_slot(layer_param(trunk, layer, L2W));
     constexpr int so = split_slot(layer_param(trunk, layer, OUTW));
-    constexpr bool next_planes = split_inproj<trunk, layer + 1>();  // LN2 writes the next layer's operand planes
+    constexpr bool next_planes = !last && split_inproj<trunk, layer + 1>();  // LN2 writes the next layer's operand
+    constexpr bool res_ctx = split_inproj<trunk, layer>();  // the residual is in sm.ctx rows 0-15
+    static_assert(!res_ctx || last, "a split in_proj feeds a pruned layer");
     const int wv = TIDX() >> 6;
     _Float16* const hp = reinterpret_cast<_Float16*>(sm.h);
     _Float16* const bp = reinterpret_cast<_Float16*>(sm.big);
     _Float16* const cp = reinterpret_cast<_Float16*>(sm.ctx);
-    f32x4 h1[S];  // LN1's output: LN2's residual
+    f32x4 h1[CT];  // LN1's output: LN2's residual
     HPre<2> w1a;
     {
         const f32x4 bo4 = ln_bias(TID_C bo);
-        f32x4 acc[S];
-        {  // out-projection from the attention output's planes (attention_full<true>)
-            f32x4 hi[S], lo[S];
+        f32x4 acc[CT];
+        {  // out-projection from the attention output's planes
+            f32x4 hi[CT], lo[CT];
             zero(hi);
             zero(lo);
-            hgemm_tile<S, 2>(TID_C hi, lo, po, P, so, D, 16 * wv, 0, cp, 0);
+            hgemm_tile<CT, 2>(TID_C hi, lo, po, P, so, D, 16 * wv, 0, cp, t0);
 #pragma unroll
-            for (int ct = 0; ct < S; ++ct) acc[ct] = hi[ct] + lo[ct] * kLoScale;
+            for (int ct = 0; ct < CT; ++ct) acc[ct] = hi[ct] + lo[ct] * kLoScale;
         }
         PTR(tb + 7);
         const LnPar lp = ln_load(TID_C bo4, P + kOffs.o[layer_param(trunk, layer, N1W)], P + kOffs.o[layer_param(trunk, layer, N1B)]);
         w1a = hprefetch<2>(TID_C P, s1, D, 16 * wv, 0);
-        residual_layernorm<S, false, true>(TID_C sm, acc, lp, 0, LnOut{}, h1);
+        if constexpr (res_ctx) {
+            const f32x4 r4[1] = {*reinterpret_cast<const f32x4*>(sm.ctx + (LANE() & 15) * LDH + 16 * wv + 4 * (LANE() >> 4))};
+            residual_layernorm<CT, false, true>(TID_C sm, acc, lp, t0, LnOut{}, h1, r4);
+        } else {
+            residual_layernorm<CT, false, true>(TID_C sm, acc, lp, t0, LnOut{}, h1);
+        }
     }
     PTR(tb + 8);
     __syncthreads();
@@ -857,16 +873,16 @@ __device__ __forceinline__ void layer_ffn_split(TID_F Smem& sm, const float* __r
         const int grow = 4 * (LANE() >> 4);
         const f32x4 ba = *reinterpret_cast<const f32x4*>(b1 + 16 * wv + grow);
         const f32x4 bb = *reinterpret_cast<const f32x4*>(b1 + 128 + 16 * wv + grow);
-        f32x4 hi[S], lo[S];
+        f32x4 hi[CT], lo[CT];
         zero(hi);
         zero(lo);
-        hgemm_tile<S, 2>(TID_C hi, lo, w1a, P, s1, D, 16 * wv, 0, hp, 0);
+        hgemm_tile<CT, 2>(TID_C hi, lo, w1a, P, s1, D, 16 * wv, 0, hp, t0);
         const HPre<2> w1b = hprefetch<2>(TID_C P, s1, D, 128 + 16 * wv, 0);
-        hstore_tile<S, true>(TID_C hi, lo, ba, bp, 16 * wv, 0);
+        hstore_tile<CT, true>(TID_C hi, lo, ba, bp, 16 * wv, t0);
         zero(hi);
         zero(lo);
-        hgemm_tile<S, 2>(TID_C hi, lo, w1b, P, s1, D, 128 + 16 * wv, 0, hp, 0);
-        hstore_tile<S, true>(TID_C hi, lo, bb, cp, 16 * wv, 0);
+        hgemm_tile<CT, 2>(TID_C hi, lo, w1b, P, s1, D, 128 + 16 * wv, 0, hp, t0);
+        hstore_tile<CT, true>(TID_C hi, lo, bb, cp, 16 * wv, t0);
     }
     const HPre<2> w2a = hprefetch<2>(TID_C P, s2, FF, 16 * wv, 0);
     PTR(tb + 10);
@@ -874,17 +890,17 @@ __device__ __forceinline__ void layer_ffn_split(TID_F Smem& sm, const float* __r
     PTR(tb + 11);
     const HPre<2> w2b = hprefetch<2>(TID_C P, s2, FF, 16 * wv, 128);
     const f32x4 b24 = ln_bias(TID_C b2);
-    f32x4 hi[S], lo[S];
+    f32x4 hi[CT], lo[CT];
     zero(hi);
     zero(lo);
-    hgemm_tile<S, 2>(TID_C hi, lo, w2a, P, s2, FF, 16 * wv, 0, bp, 0);
-    hgemm_tile<S, 2>(TID_C hi, lo, w2b, P, s2, FF, 16 * wv, 128, cp, 0);
+    hgemm_tile<CT, 2>(TID_C hi, lo, w2a, P, s2, FF, 16 * wv, 0, bp, t0);
+    hgemm_tile<CT, 2>(TID_C hi, lo, w2b, P, s2, FF, 16 * wv, 128, cp, t0);
     PTR(tb + 12);
     const LnPar lp2 = ln_load(TID_C b24, P + kOffs.o[layer_param(trunk, layer, N2W)], P + kOffs.o[layer_param(trunk, layer, N2B)]);
-    f32x4 acc2[S];
+    f32x4 acc2[CT];
 #pragma unroll
-    for (int ct = 0; ct < S; ++ct) acc2[ct] = hi[ct] + lo[ct] * kLoScale;
-    residual_layernorm<S, false, next_planes, next_planes>(TID_C sm, acc2, lp2, 0, LnOut{}, nullptr, h1);
+    for (int ct = 0; ct < CT; ++ct) acc2[ct] = hi[ct] + lo[ct] * kLoScale;
+    residual_layernorm<CT, false, next_planes, next_planes>(TID_C sm, acc2, lp2, t0, LnOut{}, nullptr, h1);
     PTR(tb + 14);
 }
 
@@ -912,8 +928,8 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
     // matrix cores (hgemm_tile): LN1 writes its output as the two fp16 planes into sm.h and keeps
     // the fp32 values in registers (LN2's residual), FFN1 writes the hidden planes into big
     // (features 0-127) and ctx (128-255), FFN2 reads them
-    if constexpr (!TR && !last && !PSX && split_tail<trunk, layer>()) {
-        layer_ffn_split<trunk, layer>(TID_C sm, P, po);
+    if constexpr (!TR && !PSX && split_tail<trunk, layer>()) {
+        layer_tail_split<trunk, layer, last>(TID_C sm, P, po);
         return;
     } else {
     // a pruned layer after a split full layer: the residual (its input at position 4) is in sm.ctx
@@ -1175,7 +1191,7 @@ __device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* 
                                    const RowIO& rio, int b0) {
     constexpr bool last = trunk == kActorTrunk;  // the actor's layer 0 is its last (pruned) layer
     constexpr int P0 = 3 - NP, ROFF = trunk == kActorTrunk ? 0 : 2 * D;
-    constexpr bool planes = !last && split_tail<trunk, 0>();  // attention output as split-product planes
+    constexpr bool planes = split_tail<trunk, 0>();  // attention output as split-product planes
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1);
     PTR(tb);
     const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
@@ -1231,7 +1247,7 @@ __device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* 
         __syncthreads();
         PTR(tb + 2 + 3 * c);
         if (c == 0) ppos_stage(TID_C sm, rp, 1);  // sm.red is read again only by the chunk-1 assembly
-        if (last) attention_chunk(TID_C sm, c, S - 1, 1);
+        if (last) attention_chunk<planes>(TID_C sm, c, S - 1, 1);
         else attention_full<planes>(TID_C sm, c);
         __syncthreads();
         PTR(tb + 3 + 3 * c);

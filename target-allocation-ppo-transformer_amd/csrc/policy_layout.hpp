@@ -48,16 +48,19 @@ __host__ __device__ constexpr int layer_param(int trunk, int l, int which) { ret
 
 // ---- split copies (inference forward only): the GEMM weights over all 80 tokens that run on the
 // f16 matrix cores as fp32-accurate split products (policy.hip, hgemm_tile): the critic's layer-0
-// out-projection and FFN, and its layer-1 in_proj (K / V of every token, Q of position 4); and the
-// layer-0 in_proj of both trunks for the rollout's window-row ring (the new row's Q | K | V). Each weight
+// out-projection and FFN, and its layer-1 in_proj (K / V of every token, Q of position 4); the
+// layer-0 in_proj of both trunks for the rollout's window-row ring (the new row's Q | K | V); and the
+// out-projection and FFN of both trunks' pruned top layers (the 16 tokens of position 4). Each weight
 // W [R][K] is appended to the packed buffer as two fp16 planes, w1 = f16(w), w2 = f16((w - w1) 2^11),
 // in split fragment order: per 16-row tile t and 32-k block kb, 1 KiB of plane 1 then 1 KiB of
 // plane 2, lane l = r%16 + 16 ((k%32)/8) holding k%8 = 0..7 -- one float per weight, like the fp32
 // copy. The split copies follow the 50 parameters.
-constexpr int kNumSplit = 6;
-constexpr int kSplitParam[kNumSplit] = {layer_param(kCriticTrunk, 0, L1W), layer_param(kCriticTrunk, 0, L2W),
-                                        layer_param(kCriticTrunk, 0, OUTW), layer_param(kCriticTrunk, 1, INW),
-                                        layer_param(kActorTrunk, 0, INW), layer_param(kCriticTrunk, 0, INW)};
+constexpr int kNumSplit = 12;
+constexpr int kSplitParam[kNumSplit] = {
+    layer_param(kCriticTrunk, 0, L1W),  layer_param(kCriticTrunk, 0, L2W), layer_param(kCriticTrunk, 0, OUTW),
+    layer_param(kCriticTrunk, 1, INW),  layer_param(kActorTrunk, 0, INW),  layer_param(kCriticTrunk, 0, INW),
+    layer_param(kActorTrunk, 0, OUTW),  layer_param(kActorTrunk, 0, L1W),  layer_param(kActorTrunk, 0, L2W),
+    layer_param(kCriticTrunk, 1, OUTW), layer_param(kCriticTrunk, 1, L1W), layer_param(kCriticTrunk, 1, L2W)};
 struct SplitOffs { int o[kNumSplit + 1]; };
 constexpr SplitOffs make_split_offs() {
     SplitOffs r{};

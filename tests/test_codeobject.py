@@ -6,7 +6,7 @@ single-step kernel only because its body launders the thread index and the kerne
 the step loop and spills 1,412 VGPRs). A compiler change that undoes that would otherwise show up
 only as a silent ~10 % loss in a GPU bench. This test compiles the device code to assembly (a few
 seconds) and checks, from the amdhsa metadata and the kernel body:
-  * spills: VGPR spill count at most 16, SGPR at most 8 (today 12 / 8),
+  * spills: VGPR spill count at most 32, SGPR at most 8 (today 28 / 8; the LICM failure mode spills 1,412),
   * LDS: the fixed group segment fits gfx950's 160 KiB,
   * VGPRs: at most 256 (two waves per SIMD at 512 threads),
   * MFMA issue: the counts of v_mfma_f32_16x16x4_f32 and of the split products'
@@ -52,12 +52,12 @@ def body(asm, name):
     return asm[i:asm.index(".Lfunc_end", i)]
 
 
-# (f32, f16) MFMA instructions in k_rollout_steps: the f32 GEMMs, and the split-product GEMMs of the
-# critic's full layer
-ROLLOUT_MFMA = (616, 444)
+# (f32, f16) MFMA instructions in k_rollout_steps: the f32 GEMMs (embeddings, heads) and the
+# split-product GEMMs of every encoder layer
+ROLLOUT_MFMA = (104, 636)
 
 
-def check_limits(name, m, vgpr_spills=16, sgpr_spills=8):
+def check_limits(name, m, vgpr_spills=32, sgpr_spills=8):
     print(f"{name}: {m}")
     assert m["vgpr_spill_count"] <= vgpr_spills, (name, m)
     assert m["sgpr_spill_count"] <= sgpr_spills, (name, m)
