@@ -1,21 +1,9 @@
 // wgrad.hpp -- weight gradients of the PPO training step (train.hip): for a list of problems,
-// dW[m][n] = sum_k dY[k][m] X[k][n] over the minibatch rows k, fp32 on the f32-input MFMA
-// (v_mfma_f32_16x16x4_f32). Bias gradients (sums of dY over k) come from k_policy_backward's
-// per-workgroup partials, not from here.
+// dW[m][n] = sum_k dY[k][m] X[k][n] over the minibatch rows k, fp32-accurate split products on the
+// f16 MFMA (v_mfma_f32_16x16x32_f16, see k_wgrad). Bias gradients (sums of dY over k) come from
+// k_policy_backward's per-workgroup partials, not from here.
 //
-// Operands. dY and X are the workspace's [row][feature] activations, so both are k-major: the LDS
-// images are copies of the global rows ([64 k][128] per operand and slab), filled by
-// global_load_lds_dwordx4 with no transposition and no register staging. MFMA fragments are read
-// along m / n with ds_read_b128: lane (i, g) reads columns 4i..4i+3 of row k = 4 kk + g, which is
-// row i of four 16 x 16 tiles at once (tile a holds the columns 4i + a). A quarter wave reads 256
-// contiguous bytes: conflict-free. The epilogue undoes the column permutation with float4 stores.
-//
-// Workgroup: 512 threads = 8 waves, one 128 x 128 output tile; wave w computes the 64 x 64
-// quadrant w & 3 over the k-steps of parity w >> 2 (4 x 4 MFMA tiles, 64 accumulator VGPRs), the
-// two parities are added through LDS at the end. LDS: 2 stages x (A + B) x 64 x 128 floats = 128
-// KiB, one workgroup per CU.
-//
-// Work split (stream-K over 64-deep k-slabs): the problems' 128 x 128 output tiles x K / 64 slabs
+// Work split (stream-K over 32-deep k-slabs): the problems' 128 x 128 output tiles x K / 32 slabs
 // form one list (problem-major, then tile, then k); workgroup w takes the contiguous range
 // [w U / G, (w + 1) U / G) and accumulates each tile's slabs in registers, writing one partial
 // tile per (workgroup, tile) run into slot kWgRuns w + j (j = the run's index within the
@@ -32,7 +20,7 @@ namespace tr {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWgT = 128;                 // output tile edge
-constexpr int kWgBK = 64;                 // k rows per slab
+constexpr int kWgBK = 32;                 // k rows per slab (one 32-k MFMA block)
 constexpr int kWgThreads = 512;
 constexpr int kWgRuns = 3;                // partial slots per workgroup
 constexpr int kWgSlot = kWgT * kWgT;      // floats per partial slot
@@ -53,8 +41,6 @@ struct WgBatch {
     float* part;  // [grid * kWgRuns][kWgSlot]
 };
 
-typedef __attribute__((address_space(3))) void wg_lds_void;
-typedef __attribute__((address_space(1))) void wg_glob_void;
 
 // Stamps (make TRACE=1 only): per workgroup, s_memtime at kernel start and, per run, after the
 // first slab landed / after the k-loop / after the epilogue (uavhip_wgrad_trace copies them out).
@@ -78,28 +64,90 @@ __device__ __forceinline__ int wg_find(const WgBatch& b, int u) {
     return lo;
 }
 
-// Issue the global_load_lds of one 64 x 128 slab of an operand (rows k0.., columns c0..) into
-// `lds` ([64][128] floats): 32 row pairs (1 KiB each), 4 per wave. Columns >= ncols (a 64-wide
-// problem) load column c0 instead; those products land in output rows that are never stored.
-__device__ __forceinline__ void wg_load_slab(const float* X, int ld, int k0, int c0, int ncols, float* lds) {
-    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-    int col = 4 * (l & 31);
-    if (c0 + col >= ncols) col = 0;
+// Split products with THREE fp16 planes: every operand element is staged as
+// x = x1 + 2^-11 x2 + 2^-22 x3 (x1 = f16(x), x2 = f16((x - x1) 2^11), x3 = f16((x - x1 - 2^-11 x2) 2^22),
+// exact to 2^-33) and dW = hi + 2^-11 mid + 2^-22 lo with hi += A1 B1, mid += A1 B2 + A2 B1,
+// lo += A1 B3 + A3 B1 + A2 B2 on v_mfma_f32_16x16x32_f16 (6 x 16 cycles per 16 x 16 x 32 block
+// against 8 x 32 for the f32 MFMA). The weight gradients sum thousands of rows whose terms
+// largely cancel (the in_proj key rows: softmax removes the key bias), so the two-plane form's
+// 2^-22 per product is not enough here; this one is more accurate than the f32 MFMA's fp32 sums.
+//
+// Operands. dY and X are the workspace's [row][feature] activations: k-major. Each thread loads its
+// share of a 32 x 128 slab from global as float4 (registers, one slab ahead), splits it and writes
+// the planes into the LDS stage as [k][128] fp16 images with 256-B rows whose 16-B chunks are
+// XOR-swizzled (cdna_hip_programming.md T10 image (b)); the MFMA fragments -- 8 consecutive k of one
+// m (A) or n (B) column per lane -- come out of ds_read_b64_tr_b16 (two per plane: rows 8g..8g+3
+// and 8g+4..8g+7 of the slab), conflict-free with a 32-lane half's two row blocks 8 rows apart.
+//
+// Workgroup: 512 threads = 8 waves, one 128 x 128 output tile; wave w owns rows 64 (w & 1) .. + 63
+// (4 m-tiles) x columns 32 (w >> 1) .. + 31 (2 n-tiles) over the whole k range (hi, mid, lo: 96
+// accumulator VGPRs). LDS: 2 stages x 6 planes x 8 KiB = 96 KiB, one workgroup per CU.
+typedef _Float16 wg_f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 wg_f16x8 __attribute__((ext_vector_type(8)));
+typedef short wg_i16x4 __attribute__((vector_size(8)));
+typedef __attribute__((address_space(3))) wg_i16x4 wg_lds_i16x4;
+constexpr int kWgRowB = 2 * kWgT;              // bytes per plane row: 128 fp16
+constexpr int kWgPlaneB = kWgBK * kWgRowB;     // 8 KiB: one plane of a 32 x 128 slab
+constexpr int kWgStageB = 6 * kWgPlaneB;       // A x1 x2 x3 | B x1 x2 x3
+static_assert(kWgBK == 32, "one 32-k MFMA block per slab");
+
+__device__ __forceinline__ int wg_swz(int row, int ch) {
+    return kWgRowB * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+// this thread's share of a slab: rows (t >> 5) + 16 i, columns 4 (t & 31) .. + 3 of each operand.
+// Columns >= M (a 64-wide problem) read column m0 instead; their products land in output rows
+// that are never stored.
+struct WgSlab {
+    f32x4 a[2], b[2];
+};
+__device__ __forceinline__ void wg_gload(WgSlab& r, const WgProb& P, int k0, int m0, int n0) {
+    const int t = threadIdx.x, c = 4 * (t & 31);
+    const int ca = m0 + c < P.M ? m0 + c : m0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int rp = 4 * wv + q;
-        const float* src = X + (size_t)(k0 + 2 * rp + (l >> 5)) * ld + c0 + col;
-        __builtin_amdgcn_global_load_lds((wg_glob_void*)src, (wg_lds_void*)(lds + rp * 256), 16, 0, 0);
+    for (int i = 0; i < 2; ++i) {
+        const int row = k0 + (t >> 5) + 16 * i;
+        r.a[i] = *reinterpret_cast<const f32x4*>(P.A + (size_t)row * P.lda + ca);
+        r.b[i] = *reinterpret_cast<const f32x4*>(P.B + (size_t)row * P.ldb + n0 + c);
     }
+}
+__device__ __forceinline__ void wg_split_store(const f32x4 v, char* plane, int off) {
+    wg_f16x4 x1, x2, x3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        x1[j] = (_Float16)v[j];
+        const float r1 = v[j] - (float)x1[j];                 // exact
+        x2[j] = (_Float16)(r1 * 2048.f);
+        x3[j] = (_Float16)((r1 - (float)x2[j] * (1.0f / 2048.0f)) * 4194304.f);  // r1 - x2 2^-11: exact
+    }
+    *reinterpret_cast<wg_f16x4*>(plane + off) = x1;
+    *reinterpret_cast<wg_f16x4*>(plane + kWgPlaneB + off) = x2;
+    *reinterpret_cast<wg_f16x4*>(plane + 2 * kWgPlaneB + off) = x3;
+}
+__device__ __forceinline__ void wg_stage_store(const WgSlab& r, char* stage) {
+    const int t = threadIdx.x, c4 = t & 31;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int off = wg_swz((t >> 5) + 16 * i, c4 >> 1) + 8 * (c4 & 1);
+        wg_split_store(r.a[i], stage, off);
+        wg_split_store(r.b[i], stage + 3 * kWgPlaneB, off);
+    }
+}
+// 16 columns (c16 .. c16 + 15) x 8 consecutive k (8 g ..) of a plane: lane (i16, g) gets column
+// c16 + i16 -- the f16 MFMA operand -- from two transposed reads of 4 rows each
+__device__ __forceinline__ wg_f16x8 wg_frag(const char* plane, int c16) {
+    const int l = threadIdx.x & 63, g = l >> 4, q = (l & 15) >> 2, p = l & 3;
+    const int r0 = 8 * g + q, ch = (c16 >> 3) + (p >> 1), sub = 8 * (p & 1);
+    const wg_i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((wg_lds_i16x4*)(plane + wg_swz(r0, ch) + sub));
+    const wg_i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((wg_lds_i16x4*)(plane + wg_swz(r0 + 4, ch) + sub));
+    const wg_f16x4 a = __builtin_bit_cast(wg_f16x4, lo), b = __builtin_bit_cast(wg_f16x4, hi);
+    return wg_f16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
 __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
-    // stage s: A at wg_smem + 2 s * kWgBK * kWgT, B right after it
-    __shared__ __attribute__((aligned(16))) float wg_smem[4 * kWgBK * kWgT];
-    constexpr int kStage = 2 * kWgBK * kWgT;
+    __shared__ __attribute__((aligned(16))) char wg_smem[2 * kWgStageB];
     const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, i16 = l & 15, g = l >> 4;
-    const int quad = wv & 3, kp = wv >> 2;
-    const int qm = 64 * (quad & 1), qn = 64 * (quad >> 1);
+    const int mt0 = 4 * (wv & 1), nt0 = 2 * (wv >> 1);  // this wave's first m-tile / n-tile
     const long long U = wb.units, G = gridDim.x;
     int u = (int)(blockIdx.x * U / G);
     const int u_end = (int)((blockIdx.x + 1) * U / G);
@@ -112,63 +160,60 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
         const int tile = local / P.slabs, s0 = local - tile * P.slabs;
         const int n_slabs = min(u_end - u, P.slabs - s0);
         const int m0 = (tile / P.tiles_n) * kWgT, n0 = (tile % P.tiles_n) * kWgT;
-        f32x4 acc[4][4];
+        f32x4 hi[4][2], mid[4][2], lo[4][2];
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
-            for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-        wg_load_slab(P.A, P.lda, s0 * kWgBK, m0, P.M, wg_smem);
-        wg_load_slab(P.B, P.ldb, s0 * kWgBK, n0, P.N, wg_smem + kWgBK * kWgT);
-        __syncthreads();  // waits vmcnt(0): the first slab has landed
+            for (int b = 0; b < 2; ++b) hi[a][b] = mid[a][b] = lo[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        WgSlab nx;
+        wg_gload(nx, P, s0 * kWgBK, m0, n0);
+        wg_stage_store(nx, wg_smem);
+        if (n_slabs > 1) wg_gload(nx, P, (s0 + 1) * kWgBK, m0, n0);
+        __syncthreads();
         WTR(1 + 4 * run);
         for (int s = 0; s < n_slabs; ++s) {
-            const int cur = s & 1;
-            if (s + 1 < n_slabs) {
-                float* nxt = wg_smem + (cur ^ 1) * kStage;
-                wg_load_slab(P.A, P.lda, (s0 + s + 1) * kWgBK, m0, P.M, nxt);
-                wg_load_slab(P.B, P.ldb, (s0 + s + 1) * kWgBK, n0, P.N, nxt + kWgBK * kWgT);
+            const char* st = wg_smem + (s & 1) * kWgStageB;
+            wg_f16x8 a1[4], a2[4], a3[4], b1[2], b2[2], b3[2];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                a1[a] = wg_frag(st, 16 * (mt0 + a));
+                a2[a] = wg_frag(st + kWgPlaneB, 16 * (mt0 + a));
+                a3[a] = wg_frag(st + 2 * kWgPlaneB, 16 * (mt0 + a));
             }
-            const float* as = wg_smem + cur * kStage + qm + 4 * i16;
-            const float* bs = wg_smem + cur * kStage + kWgBK * kWgT + qn + 4 * i16;
 #pragma unroll
-            for (int h = 0; h < kWgBK / 8; ++h) {
-                const int k = 4 * (2 * h + kp) + g;
-                const f32x4 fa = *reinterpret_cast<const f32x4*>(as + k * kWgT);
-                const f32x4 fb = *reinterpret_cast<const f32x4*>(bs + k * kWgT);
-#pragma unroll
-                for (int a = 0; a < 4; ++a)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a], fb[b], acc[a][b], 0, 0, 0);
+            for (int b = 0; b < 2; ++b) {
+                b1[b] = wg_frag(st + 3 * kWgPlaneB, 16 * (nt0 + b));
+                b2[b] = wg_frag(st + 4 * kWgPlaneB, 16 * (nt0 + b));
+                b3[b] = wg_frag(st + 5 * kWgPlaneB, 16 * (nt0 + b));
             }
-            __syncthreads();  // next slab landed (vmcnt(0)); everyone is done reading this one
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    hi[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[a], b1[b], hi[a][b], 0, 0, 0);
+                    mid[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[a], b2[b], mid[a][b], 0, 0, 0);
+                    mid[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[a], b1[b], mid[a][b], 0, 0, 0);
+                    lo[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[a], b3[b], lo[a][b], 0, 0, 0);
+                    lo[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a3[a], b1[b], lo[a][b], 0, 0, 0);
+                    lo[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[a], b2[b], lo[a][b], 0, 0, 0);
+                }
+            if (s + 1 < n_slabs) {  // slab s + 1 (landed in registers meanwhile) -> the other stage
+                wg_stage_store(nx, wg_smem + ((s + 1) & 1) * kWgStageB);
+                if (s + 2 < n_slabs) wg_gload(nx, P, (s0 + s + 2) * kWgBK, m0, n0);
+            }
+            __syncthreads();  // the next stage is written; everyone is done reading this one
         }
         WTR(2 + 4 * run);
-        // k-parity 1 -> LDS, parity 0 adds and stores. Lane (i16, g) of tile (a, b) holds
-        // dW[m0 + qm + 16 g + 4 r + a][n0 + qn + 4 i16 + b], r = 0..3.
-        float* red = wg_smem + quad * 64 * 64;
-        if (kp == 1) {
+        // lane (i16, g) of tile (a, b) holds dW[m0 + 16 (mt0 + a) + 4 g + r][n0 + 16 (nt0 + b) + i16]
+        float* out = wb.part + (size_t)(blockIdx.x * kWgRuns + run) * kWgSlot;
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    *reinterpret_cast<f32x4*>(red + (16 * g + 4 * r + a) * 64 + 4 * i16) =
-                        f32x4{acc[a][0][r], acc[a][1][r], acc[a][2][r], acc[a][3][r]};
-        }
-        __syncthreads();
-        if (kp == 0) {
-            float* out = wb.part + (size_t)(blockIdx.x * kWgRuns + run) * kWgSlot;
+            for (int b = 0; b < 2; ++b) {
+                const f32x4 v = hi[a][b] + (mid[a][b] + lo[a][b] * (1.0f / 2048.0f)) * (1.0f / 2048.0f);
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int ml = qm + 16 * g + 4 * r + a;
-                    const f32x4 o = *reinterpret_cast<const f32x4*>(red + (16 * g + 4 * r + a) * 64 + 4 * i16);
-                    *reinterpret_cast<f32x4*>(out + ml * kWgT + qn + 4 * i16) =
-                        o + f32x4{acc[a][0][r], acc[a][1][r], acc[a][2][r], acc[a][3][r]};
-                }
-        }
-        __syncthreads();  // LDS is reloaded by the next run
+                for (int r = 0; r < 4; ++r) out[(16 * (mt0 + a) + 4 * g + r) * kWgT + 16 * (nt0 + b) + i16] = v[r];
+            }
         WTR(3 + 4 * run);
         u += n_slabs;
         ++run;
