@@ -514,9 +514,9 @@ __device__ __forceinline__ void store_rows(TID_F const float* src, int lds, floa
 // Full-layer attention for heads [4c, 4c+4): one (sample, head, query group) task per 4 lanes,
 // each lane owning 4 of the 16 head dims; the task loads the 5 keys / values once for all its
 // queries (group 0: positions 0-2 on waves 0-3, group 1: positions 3-4 on waves 4-7).
-// PLANES: the output goes to sm.ctx as the two fp16 planes of the split products (the out-projection's operand).
-template <bool PLANES = false>
-__device__ void attention_full(TID_F Smem& sm, int c) {
+// attention_full_core leaves the outputs in registers (o[qi] for query position qs0 + qi, qi < nq);
+// attention_full_store writes them to sm.ctx (PLANES: as the split products' fp16 planes).
+__device__ __forceinline__ void attention_full_core(TID_F Smem& sm, int c, f32x4 (&o)[3]) {
     const int q4 = TIDX() & 3, task = TIDX() >> 2;
     const int hh = task & 3, p = (task >> 2) & 15, grp = task >> 6;
     const int d0 = hh * HD + 4 * q4;
@@ -531,6 +531,7 @@ __device__ void attention_full(TID_F Smem& sm, int c) {
     const int qs0 = grp ? 3 : 0, nq = grp ? 2 : 3;
 #pragma unroll
     for (int qi = 0; qi < 3; ++qi) {
+        o[qi] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (qi < nq) {
             const int ti = (qs0 + qi) * SPW + p;
             const f32x4 q = *reinterpret_cast<const f32x4*>(sm.big + ti * LDB + d0);
@@ -550,53 +551,81 @@ __device__ void attention_full(TID_F Smem& sm, int c) {
                 den += sc[j];
             }
             const float inv = 1.0f / den;
-            f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int j = 0; j < S; ++j) o += (sc[j] * inv) * v[j];
-            if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), ti * LDP + 4 * c * HD + d0, o);
-            else *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o;
+            for (int j = 0; j < S; ++j) o[qi] += (sc[j] * inv) * v[j];
         }
     }
+}
+template <bool PLANES>
+__device__ __forceinline__ void attention_full_store(TID_F Smem& sm, int c, const f32x4 (&o)[3]) {
+    const int q4 = TIDX() & 3, task = TIDX() >> 2;
+    const int hh = task & 3, p = (task >> 2) & 15, grp = task >> 6;
+    const int d0 = hh * HD + 4 * q4, qs0 = grp ? 3 : 0, nq = grp ? 2 : 3;
+#pragma unroll
+    for (int qi = 0; qi < 3; ++qi) {
+        if (qi < nq) {
+            const int ti = (qs0 + qi) * SPW + p;
+            if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), ti * LDP + 4 * c * HD + d0, o[qi]);
+            else *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o[qi];
+        }
+    }
+}
+// PLANES: the output goes to sm.ctx as the two fp16 planes of the split products (the out-projection's operand).
+template <bool PLANES = false>
+__device__ void attention_full(TID_F Smem& sm, int c) {
+    f32x4 o[3];
+    attention_full_core(TID_C sm, c, o);
+    attention_full_store<PLANES>(TID_C sm, c, o);
 }
 
 // Scaled-dot-product attention for heads [4c, 4c+4) of the query positions [qs0, qs0 + nqs) over
 // the keys/values of all 5 positions; reads sm.big (Q|K|V of the chunk), writes sm.ctx.
 // One (query, head) task per 4 consecutive lanes, each lane owning 4 of the 16 head dims
-// (dot products reduced over the quad with two xor-shuffles).
+// (dot products reduced over the quad with two xor-shuffles). _core: one query position (nqs = 1):
+// threads < 256 own one task each, its output in `o`.
+__device__ __forceinline__ void attention_task(TID_F Smem& sm, int task, int qs0, f32x4& o, int& ti, int& d0) {
+    const int q4 = TIDX() & 3;
+    const int hh = task & 3, rest = task >> 2, p = rest & 15, si = qs0 + (rest >> 4);
+    ti = si * SPW + p;
+    d0 = hh * HD + 4 * q4;
+    const f32x4 q = *reinterpret_cast<const f32x4*>(sm.big + ti * LDB + d0);
+    float sc[S];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        const f32x4 k = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 64 + d0);
+        float part = q.x * k.x + q.y * k.y + q.z * k.z + q.w * k.w;
+        part = add_xor2(add_xor1(part));
+        sc[j] = sm.mask[p * S + j] ? -INFINITY : part * 0.25f;  // 1/sqrt(16)
+        mx = fmaxf(mx, sc[j]);
+    }
+    float den = 0.f;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        sc[j] = __expf(sc[j] - mx);
+        den += sc[j];
+    }
+    const float inv = 1.0f / den;
+    o = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 128 + d0);
+        o += (sc[j] * inv) * v;
+    }
+}
+template <bool PLANES>
+__device__ __forceinline__ void attention_out(TID_F Smem& sm, int c, int ti, int d0, const f32x4 o) {
+    if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), ti * LDP + 4 * c * HD + d0, o);
+    else *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o;
+}
 template <bool PLANES = false>
 __device__ void attention_chunk(TID_F Smem& sm, int c, int qs0, int nqs) {
     const int ntask = nqs * SPW * 4;
-    const int q4 = TIDX() & 3;
     for (int task = TIDX() >> 2; task < ntask; task += NTHR / 4) {
-        const int hh = task & 3, rest = task >> 2, p = rest & 15, si = qs0 + (rest >> 4);
-        const int ti = si * SPW + p;
-        const int d0 = hh * HD + 4 * q4;
-        const f32x4 q = *reinterpret_cast<const f32x4*>(sm.big + ti * LDB + d0);
-        float sc[S];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            const f32x4 k = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 64 + d0);
-            float part = q.x * k.x + q.y * k.y + q.z * k.z + q.w * k.w;
-            part = add_xor2(add_xor1(part));
-            sc[j] = sm.mask[p * S + j] ? -INFINITY : part * 0.25f;  // 1/sqrt(16)
-            mx = fmaxf(mx, sc[j]);
-        }
-        float den = 0.f;
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            sc[j] = __expf(sc[j] - mx);
-            den += sc[j];
-        }
-        const float inv = 1.0f / den;
-        f32x4 o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 128 + d0);
-            o += (sc[j] * inv) * v;
-        }
-        if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), ti * LDP + 4 * c * HD + d0, o);
-        else *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o;
+        f32x4 o;
+        int ti, d0;
+        attention_task(TID_C sm, task, qs0, o, ti, d0);
+        attention_out<PLANES>(TID_C sm, c, ti, d0, o);
     }
 }
 
@@ -628,7 +657,9 @@ __device__ __forceinline__ EmbPre embed_load(TID_F const float* __restrict__ P) 
 // -> sm.ctx rows 64-79 (the window-row projection path's in_proj input). kEmbRows: only e of
 // positions 0-3 -> sm.ctx (row projection fill).
 enum { kEmbH = 0, kEmbSplit = 1, kEmbRows = 2 };
-template <int trunk, bool TR = false, int MODE = kEmbH>
+// PL (kEmbH): also the two fp16 planes of h into sm.ctx (the split layer-0 in_proj's operand,
+// encoder_layer_split).
+template <int trunk, bool TR = false, int MODE = kEmbH, bool PL = false>
 __device__ void embed_apply(TID_F Smem& sm, const EmbPre& ep, float* e_out = nullptr, float* h_out = nullptr, int b0 = 0) {
     const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
     constexpr int NT = MODE == kEmbRows ? S - 1 : S;
@@ -652,6 +683,7 @@ __device__ void embed_apply(TID_F Smem& sm, const EmbPre& ep, float* e_out = nul
         if (MODE == kEmbRows) continue;
         const f32x4 v = e + ep.pp[ct];
         *reinterpret_cast<f32x4*>(sm.h + o) = v;
+        if constexpr (PL) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), (ct * SPW + i16) * LDP + 16 * wv + 4 * g, v);
         if (TR && !kExpNoStore) {
             const size_t r = (size_t)trow(ct * SPW + i16, b0);
             *reinterpret_cast<f32x4*>(e_out + r * D + 16 * wv + 4 * g) = e;
@@ -688,48 +720,100 @@ constexpr bool split_inproj() {  // layer >= 1: its input comes from a split ful
     return layer >= 1 && layer < 2 && split_slot(layer_param(trunk, layer, INW)) >= 0;
 }
 // The caller's prefetch of a layer tail's first out-projection weights / of a layer's first K/V
-// weights: the split copy's blocks on the split paths, the fp32 fragments otherwise.
-template <int trunk, int layer, bool last, bool TR, int PSX = 0>
-using TailPre = std::conditional_t<!TR && !PSX && split_tail<trunk, layer>(), HPre<2>,
+// weights: the split copy's blocks on the split paths, the fp32 fragments otherwise. SP selects the
+// split paths: the inference forward always (SP = !TR), the training forward (TR) when its caller
+// asks (kTrainSplit); the position-split kernels (PSX) never.
+template <int trunk, int layer>
+constexpr bool split_l0() {  // layer 0's in_proj from the embedding's planes (the training forward)
+    return layer == 0 && split_slot(layer_param(trunk, 0, INW)) >= 0;
+}
+template <int trunk, int layer, bool last, bool TR, int PSX = 0, bool SP = !TR>
+using TailPre = std::conditional_t<SP && !PSX && split_tail<trunk, layer>(), HPre<2>,
                                    APre<depth<(last || PSX) ? 1 : S>()>>;
-template <int trunk, int layer, bool last, bool TR>
-__device__ __forceinline__ TailPre<trunk, layer, last, TR> tail_prefetch(TID_F const float* __restrict__ P) {
+template <int trunk, int layer, bool last, bool TR, bool SP = !TR>
+__device__ __forceinline__ TailPre<trunk, layer, last, TR, 0, SP> tail_prefetch(TID_F const float* __restrict__ P) {
     const int wv = TIDX() >> 6;
-    if constexpr (!TR && split_tail<trunk, layer>())
+    if constexpr (SP && split_tail<trunk, layer>())
         return hprefetch<2>(TID_C P, split_slot(layer_param(trunk, layer, OUTW)), D, 16 * wv, 0);
     else
         return prefetch<depth<last ? 1 : S>()>(TID_C P + kOffs.o[layer_param(trunk, layer, OUTW)], D, 16 * wv, 0);
 }
-template <int trunk, int layer, bool TR>
-using KvPre = std::conditional_t<!TR && split_inproj<trunk, layer>(), HPre<2>, APre<2>>;
-template <int trunk, int layer, bool TR>
-__device__ __forceinline__ KvPre<trunk, layer, TR> kv_prefetch(TID_F const float* __restrict__ P) {
+template <int trunk, int layer, bool TR, bool SP = !TR>
+constexpr bool split_kv() {
+    return SP && (split_inproj<trunk, layer>() || (TR && split_l0<trunk, layer>()));
+}
+template <int trunk, int layer, bool TR, bool SP = !TR>
+using KvPre = std::conditional_t<split_kv<trunk, layer, TR, SP>(), HPre<2>, APre<2>>;
+template <int trunk, int layer, bool TR, bool SP = !TR>
+__device__ __forceinline__ KvPre<trunk, layer, TR, SP> kv_prefetch(TID_F const float* __restrict__ P) {
     const int wv = TIDX() >> 6;
-    if constexpr (!TR && split_inproj<trunk, layer>())
+    if constexpr (split_kv<trunk, layer, TR, SP>())
         return hprefetch<2>(TID_C P, split_slot(layer_param(trunk, layer, INW)), D, kv_row(wv, 0), 0);
     else
         return prefetch<2>(TID_C P + kOffs.o[layer_param(trunk, layer, INW)], D, kv_row(wv, 0), 0);
 }
+// The training forward's split switch (k_policy_forward<true>; the K7 position-split kernels stay f32).
+constexpr bool kTrainSplit = true;
 
 // PSX (position split, the small-minibatch training step): a full (unpruned) layer computed for
 // the 16 tokens of ONE window position, column tile qt / 16, in [b * 5 + s] rows.
-template <int trunk, int layer, bool last, bool TR, class F = NoHook, int PSX = 0>
-__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const TailPre<trunk, layer, last, TR, PSX>& po,
+template <int trunk, int layer, bool last, bool TR, class F = NoHook, int PSX = 0, bool SP = !TR>
+__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const TailPre<trunk, layer, last, TR, PSX, SP>& po,
                            const TrainLayerIO& io, int b0, F pre_ln2 = F{}, int qt = 0);
 
-// A pruned inference layer whose in_proj runs as split products: K / V of all 80 tokens and Q of
-// position 4 from the fp16 planes of the layer input in sm.h (the previous layer's LN2 wrote them,
-// and its position-4 rows in fp32 to sm.ctx rows 0-15), fp32 Q | K | V into sm.big.
-template <int trunk, int layer>
-__device__ __forceinline__ void encoder_layer_split_inproj(TID_F Smem& sm, const float* __restrict__ P, HPre<2> pkv, int b0) {
+// Training mode: the Q|K|V of chunk c of the tokens [qtok0, 80) (Q) / all (K, V) from sm.big to qkv
+// rows, by waves 4-7 (less MFMA work than the K + Q waves sharing their SIMDs).
+__device__ __forceinline__ void store_qkv_chunk(TID_F const Smem& sm, float* __restrict__ qkv, int c, int qtok0, int b0) {
+    if (kExpNoStore) return;
+    for (int i = (int)TIDX() - NTHR / 2; i < TOK * 48; i += NTHR / 2) {
+        if (i < 0) break;
+        const int tok = i / 48, r = i - tok * 48, part = r >> 4, q = r & 15;
+        if (part == 0 && tok < qtok0) continue;
+        *reinterpret_cast<f32x4*>(qkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q) =
+            *reinterpret_cast<const f32x4*>(sm.big + tok * LDB + part * 64 + 4 * q);
+    }
+}
+// Training mode: fp32 rows from the two planes of a split-product operand in LDS (the values the
+// GEMM consumed: x1 + 2^-11 x2) -> workspace rows (stride ldo, column offset c0), tokens [t0, t1).
+__device__ __forceinline__ void store_rows_planes(TID_F const _Float16* src, float* dst, int ldo, int c0, int ncols,
+                                                  int t0, int b0, bool compact, int t1) {
+    if (kExpNoStore) return;
+    const int n4 = ncols / 4, items = (t1 - t0) * n4;
+    for (int i = TIDX(); i < items; i += NTHR) {
+        const int tok = t0 + i / n4, q = i % n4;
+        const f16x4 x1 = *reinterpret_cast<const f16x4*>(src + tok * LDP + 4 * q);
+        const f16x4 x2 = *reinterpret_cast<const f16x4*>(src + kPlane + tok * LDP + 4 * q);
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (float)x1[j] + (float)x2[j] * kLoScale;
+        *reinterpret_cast<f32x4*>(dst + (size_t)orow(tok, b0, compact) * ldo + c0 + 4 * q) = v;
+    }
+}
+
+// An encoder layer whose in_proj runs as split products: K / V of all 80 tokens and Q of the query
+// tokens from the fp16 planes of the layer input, fp32 Q | K | V into sm.big, then attention and
+// the layer tail. The input planes are
+//   layer >= 1: in sm.h (the previous layer's LN2 wrote them, and its position-4 rows in fp32 to
+//               sm.ctx rows 0-15: the residual of this pruned layer);
+//   layer 0 (training forward): in sm.ctx (the embedding wrote them beside its fp32 rows in sm.h) --
+//               so chunk 0's attention output waits in registers until chunk 1's GEMMs have read
+//               sm.ctx, then both chunks are written.
+template <int trunk, int layer, bool last, bool TR, class F = NoHook>
+__device__ __forceinline__ void encoder_layer_split(TID_F Smem& sm, const float* __restrict__ P, HPre<2> pkv,
+                                                    const TrainLayerIO& io, int b0, F pre_ln2) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
     PTR(tb);
     constexpr int si = split_slot(layer_param(trunk, layer, INW));
+    constexpr int CTQ = last ? 1 : S, qtok0 = last ? (S - 1) * SPW : 0;
+    constexpr bool in_ctx = layer == 0;                 // the input planes: sm.ctx (layer 0) or sm.h
+    constexpr bool planes = split_tail<trunk, layer>();  // the attention output as planes
+    static_assert(in_ctx || last, "a split in_proj after a split full layer: a pruned layer");
     const float* bin = P + kOffs.o[layer_param(trunk, layer, INB)];
     const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
-    const _Float16* hp = reinterpret_cast<const _Float16*>(sm.h);
-    TailPre<trunk, layer, true, false> po;
-    constexpr bool planes = split_tail<trunk, layer>();
+    const _Float16* hp = reinterpret_cast<const _Float16*>(in_ctx ? sm.ctx : sm.h);
+    TailPre<trunk, layer, last, TR, 0, true> po;
+    [[maybe_unused]] f32x4 att0[last ? 1 : 3];  // chunk 0's attention output (in_ctx)
+    [[maybe_unused]] int ti0 = 0, d00 = 0;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {  // two chunks of 4 heads (LDS budget)
         HPre<2> pq;
@@ -745,36 +829,62 @@ __device__ __forceinline__ void encoder_layer_split_inproj(TID_F Smem& sm, const
             for (int ct = 0; ct < S; ++ct)
                 *reinterpret_cast<f32x4*>(sm.big + (16 * ct + i16) * LDB + col) = hi[ct] + lo[ct] * kLoScale + bb;
         }
-        if (wv < 4) {  // Q of the chunk for position 4 (their SIMD partners did V)
+        if (wv < 4) {  // Q of the chunk for the query tokens (their SIMD partners did V)
             const f32x4 bq = *reinterpret_cast<const f32x4*>(bin + 64 * c + 16 * wv + 4 * g);
-            f32x4 hi[1], lo[1];
+            f32x4 hi[CTQ], lo[CTQ];
             zero(hi);
             zero(lo);
-            hgemm_tile<1, 2>(TID_C hi, lo, pq, P, si, D, 64 * c + 16 * wv, 0, hp, (S - 1) * SPW);
-            *reinterpret_cast<f32x4*>(sm.big + ((S - 1) * SPW + i16) * LDB + 16 * wv + 4 * g) = hi[0] + lo[0] * kLoScale + bq;
+            hgemm_tile<CTQ, 2>(TID_C hi, lo, pq, P, si, D, 64 * c + 16 * wv, 0, hp, qtok0);
+#pragma unroll
+            for (int ct = 0; ct < CTQ; ++ct)
+                *reinterpret_cast<f32x4*>(sm.big + (qtok0 + 16 * ct + i16) * LDB + 16 * wv + 4 * g) =
+                    hi[ct] + lo[ct] * kLoScale + bq;
         }
         if (c == 0) pkv = hprefetch<2>(TID_C P, si, D, kv_row(wv, 1), 0);
-        else po = tail_prefetch<trunk, layer, true, false>(TID_C P);
+        else po = tail_prefetch<trunk, layer, last, TR, true>(TID_C P);
         PTR(tb + 1 + 3 * c);
         __syncthreads();
         PTR(tb + 2 + 3 * c);
-        attention_chunk<planes>(TID_C sm, c, S - 1, 1);
+        if constexpr (TR) store_qkv_chunk(TID_C sm, io.qkv, c, qtok0, b0);
+        if constexpr (!in_ctx) {
+            attention_chunk<planes>(TID_C sm, c, S - 1, 1);
+        } else if constexpr (last) {  // one query position: threads < 256 own one task each
+            f32x4 o;
+            int ti = 0, d0 = 0;
+            if (TIDX() < 4 * SPW * 4) attention_task(TID_C sm, TIDX() >> 2, S - 1, o, ti, d0);
+            if (c == 0) {
+                att0[0] = o;
+                ti0 = ti;
+                d00 = d0;
+            } else if (TIDX() < 4 * SPW * 4) {
+                attention_out<planes>(TID_C sm, 0, ti0, d00, att0[0]);
+                attention_out<planes>(TID_C sm, 1, ti, d0, o);
+            }
+        } else {
+            if (c == 0) {
+                attention_full_core(TID_C sm, 0, att0);
+            } else {
+                f32x4 o[3];
+                attention_full_core(TID_C sm, 1, o);
+                attention_full_store<planes>(TID_C sm, 0, att0);
+                attention_full_store<planes>(TID_C sm, 1, o);
+            }
+        }
         __syncthreads();
         PTR(tb + 3 + 3 * c);
     }
-    layer_tail<trunk, layer, true, false>(TID_C sm, P, po, TrainLayerIO{}, b0);
+    layer_tail<trunk, layer, last, TR, F, 0, true>(TID_C sm, P, po, io, b0, pre_ln2);
 }
 
 // One post-LN nn.TransformerEncoderLayer (relu FFN 256, 8 heads). last: prune to column tile 4.
 // Work split: 8 waves, wave w and w+4 share a SIMD (and its MFMA pipe); every GEMM gives each
 // SIMD the same number of 16-row output tiles. `pkv` = the caller's prefetch of this layer's first
 // K/V weight blocks. Ends WITHOUT a final barrier: the caller prefetches its next weights, then syncs.
-template <int trunk, int layer, bool last, bool TR = false, class F = NoHook>
-__device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __restrict__ P, KvPre<trunk, layer, TR> pkv,
+template <int trunk, int layer, bool last, bool TR = false, class F = NoHook, bool SP = !TR>
+__device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __restrict__ P, KvPre<trunk, layer, TR, SP> pkv,
                               const TrainLayerIO& io = TrainLayerIO{}, int b0 = 0, F pre_ln2 = F{}) {
-    if constexpr (!TR && split_inproj<trunk, layer>()) {
-        static_assert(last, "split in_proj: a pruned layer after a split full layer");
-        encoder_layer_split_inproj<trunk, layer>(TID_C sm, P, pkv, b0);
+    if constexpr (split_kv<trunk, layer, TR, SP>()) {
+        encoder_layer_split<trunk, layer, last, TR, F>(TID_C sm, P, pkv, io, b0, pre_ln2);
         return;
     } else {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
@@ -785,9 +895,9 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
     constexpr int CTQ = last ? 1 : S;              // column tiles that need Q / out / LN / FFN
     constexpr int DQ = depth<CTQ>();
     constexpr int qtok0 = last ? (S - 1) * SPW : 0;
-    constexpr bool planes = !TR && split_tail<trunk, layer>();
+    constexpr bool planes = SP && split_tail<trunk, layer>();
 
-    TailPre<trunk, layer, last, TR> po;
+    TailPre<trunk, layer, last, TR, 0, SP> po;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {  // two chunks of 4 heads (LDS budget)
         APre<DQ> pq;
@@ -797,7 +907,7 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
         // Q of the chunk for the query tokens, waves 0-3 (their SIMD partners did V)
         if (wv < 4) linear1<CTQ, false, DQ>(TID_C pq, Win, D, bin, 64 * c + 16 * wv, sm.h, LDH, qtok0, sm.big, LDB, 16 * wv, qtok0);
         if (c == 0) pkv = prefetch<2>(TID_C Win, D, kv_row(wv, 1), 0);
-        else po = tail_prefetch<trunk, layer, last, TR>(TID_C P);
+        else po = tail_prefetch<trunk, layer, last, TR, SP>(TID_C P);
         PTR(tb + 1 + 3 * c);
         __syncthreads();
         PTR(tb + 2 + 3 * c);
@@ -816,7 +926,7 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
         __syncthreads();
         PTR(tb + 3 + 3 * c);
     }
-    layer_tail<trunk, layer, last, TR>(TID_C sm, P, po, io, b0, pre_ln2);
+    layer_tail<trunk, layer, last, TR, F, 0, SP>(TID_C sm, P, po, io, b0, pre_ln2);
     }
 }
 
@@ -827,10 +937,14 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
 // planes into big (features 0-127) and ctx (128-255); LN2 writes fp32 into sm.h -- or, when the next
 // layer's in_proj runs as split products, that layer's operand planes (and position 4 in fp32 to
 // sm.ctx rows 0-15). A pruned layer after such a layer takes its residual from sm.ctx rows 0-15.
-template <int trunk, int layer, bool last>
-__device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __restrict__ P, const HPre<2>& po) {
+// Training mode (TR): the activations the backward reads are written as in layer_tail -- the
+// attention output and the FFN hidden from their planes (the values the GEMMs consumed), the
+// LayerNorm outputs from registers.
+template <int trunk, int layer, bool last, bool TR = false, class F = NoHook>
+__device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __restrict__ P, const HPre<2>& po,
+                                                 const TrainLayerIO& io = TrainLayerIO{}, int b0 = 0, F pre_ln2 = F{}) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
-    constexpr int CT = last ? 1 : S, t0 = last ? (S - 1) * SPW : 0;
+    constexpr int CT = last ? 1 : S, t0 = last ? (S - 1) * SPW : 0, t1 = t0 + SPW * CT;
     const float* bo = P + kOffs.o[layer_param(trunk, layer, OUTB)];
     const float* b1 = P + kOffs.o[layer_param(trunk, layer, L1B)];
     const float* b2 = P + kOffs.o[layer_param(trunk, layer, L2B)];
@@ -845,6 +959,7 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     _Float16* const cp = reinterpret_cast<_Float16*>(sm.ctx);
     f32x4 h1[CT];  // LN1's output: LN2's residual
     HPre<2> w1a;
+    if constexpr (TR) store_rows_planes(TID_C cp, io.o, D, 0, D, t0, b0, last, t1);  // attention output
     {
         const f32x4 bo4 = ln_bias(TID_C bo);
         f32x4 acc[CT];
@@ -859,11 +974,12 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
         PTR(tb + 7);
         const LnPar lp = ln_load(TID_C bo4, P + kOffs.o[layer_param(trunk, layer, N1W)], P + kOffs.o[layer_param(trunk, layer, N1B)]);
         w1a = hprefetch<2>(TID_C P, s1, D, 16 * wv, 0);
+        const LnOut lo1{io.xhat1, io.h1, io.rstd1, b0, last};
         if constexpr (res_ctx) {
             const f32x4 r4[1] = {*reinterpret_cast<const f32x4*>(sm.ctx + (LANE() & 15) * LDH + 16 * wv + 4 * (LANE() >> 4))};
-            residual_layernorm<CT, false, true>(TID_C sm, acc, lp, t0, LnOut{}, h1, r4);
+            residual_layernorm<CT, TR, true>(TID_C sm, acc, lp, t0, lo1, h1, r4);
         } else {
-            residual_layernorm<CT, false, true>(TID_C sm, acc, lp, t0, LnOut{}, h1);
+            residual_layernorm<CT, TR, true>(TID_C sm, acc, lp, t0, lo1, h1);
         }
     }
     PTR(tb + 8);
@@ -889,6 +1005,10 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     __syncthreads();
     PTR(tb + 11);
     const HPre<2> w2b = hprefetch<2>(TID_C P, s2, FF, 16 * wv, 128);
+    if constexpr (TR) {  // FFN hidden (post-ReLU): features 0-127 from big, 128-255 from ctx
+        store_rows_planes(TID_C bp, io.u, FF, 0, D, t0, b0, last, t1);
+        store_rows_planes(TID_C cp, io.u, FF, D, D, t0, b0, last, t1);
+    }
     const f32x4 b24 = ln_bias(TID_C b2);
     f32x4 hi[CT], lo[CT];
     zero(hi);
@@ -900,14 +1020,16 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     f32x4 acc2[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc2[ct] = hi[ct] + lo[ct] * kLoScale;
-    residual_layernorm<CT, false, next_planes, next_planes>(TID_C sm, acc2, lp2, t0, LnOut{}, nullptr, h1);
+    pre_ln2();
+    residual_layernorm<CT, TR, next_planes, next_planes>(TID_C sm, acc2, lp2, t0, LnOut{io.xhat2, io.h2, io.rstd2, b0, last},
+                                                       nullptr, h1);
     PTR(tb + 14);
 }
 
 // Out-projection + LN1 + FFN + LN2 of an encoder layer, after the attention output is in sm.ctx.
 // `po` = the caller's prefetch of the first out_proj weight blocks.
-template <int trunk, int layer, bool last, bool TR, class F, int PSX>
-__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const TailPre<trunk, layer, last, TR, PSX>& po,
+template <int trunk, int layer, bool last, bool TR, class F, int PSX, bool SP>
+__device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restrict__ P, const TailPre<trunk, layer, last, TR, PSX, SP>& po,
                            const TrainLayerIO& io, int b0, F pre_ln2, int qt) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
     const float* Wo = P + kOffs.o[layer_param(trunk, layer, OUTW)];
@@ -928,13 +1050,13 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
     // matrix cores (hgemm_tile): LN1 writes its output as the two fp16 planes into sm.h and keeps
     // the fp32 values in registers (LN2's residual), FFN1 writes the hidden planes into big
     // (features 0-127) and ctx (128-255), FFN2 reads them
-    if constexpr (!TR && !PSX && split_tail<trunk, layer>()) {
-        layer_tail_split<trunk, layer, last>(TID_C sm, P, po);
+    if constexpr (SP && !PSX && split_tail<trunk, layer>()) {
+        layer_tail_split<trunk, layer, last, TR, F>(TID_C sm, P, po, io, b0, pre_ln2);
         return;
     } else {
     // a pruned layer after a split full layer: the residual (its input at position 4) is in sm.ctx
     // rows 0-15 (sm.h holds the input's fp16 planes)
-    constexpr bool kResCtx = !TR && last && !PSX && split_inproj<trunk, layer>();
+    constexpr bool kResCtx = SP && last && !PSX && split_inproj<trunk, layer>();
     // inference, full layer: the wave's own 16 LayerNorm output features are FFN1's k-block wv, so
     // its MFMAs over that block run from registers before the barrier (beside the other waves'
     // LayerNorm work) and the GEMM after it covers the other 7 blocks (k-block order rotated)
@@ -1500,14 +1622,15 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     // training mode: the first trunk's embedding operands and first K/V weight blocks are loaded
     // before the minibatch gather stores its rows (a load behind a store burst waits for the burst)
     [[maybe_unused]] EmbPre ep_a, ep_c;
-    [[maybe_unused]] APre<2> pkv_a, pkv_c;
+    [[maybe_unused]] KvPre<kActorTrunk, 0, TR, kTrainSplit> pkv_a;
+    [[maybe_unused]] KvPre<kCriticTrunk, 0, TR, kTrainSplit> pkv_c;
     if constexpr (TR) {
         if (do_actor) {
             ep_a = embed_load<kActorTrunk>(TID_C P);
-            pkv_a = prefetch<2>(TID_C P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(TIDX() >> 6, 0), 0);
+            pkv_a = kv_prefetch<kActorTrunk, 0, TR, kTrainSplit>(TID_C P);
         } else {
             ep_c = embed_load<kCriticTrunk>(TID_C P);
-            pkv_c = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(TIDX() >> 6, 0), 0);
+            pkv_c = kv_prefetch<kCriticTrunk, 0, TR, kTrainSplit>(TID_C P);
         }
     }
     gather_windows<TR>(TID_C sm, states, B, io, b0, do_actor);
@@ -1530,25 +1653,25 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     APre<4> ph;
     if (do_actor) {
         if constexpr (!ROWS) {
-            APre<2> pkv;
             if constexpr (TR) {
-                pkv = pkv_a;
-                embed_apply<kActorTrunk, TR>(TID_C sm, ep_a, io.e[0], io.h0[0], b0);
-            } else {
-                pkv = prefetch<2>(TID_C P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-                embed<kActorTrunk, TR>(TID_C sm, P, io.e[0], io.h0[0], b0);
-            }
-            PTR(2);
-            __syncthreads();
-            if constexpr (TR) {
-                encoder_layer<kActorTrunk, 0, true, TR>(TID_C sm, P, pkv, io.L[0], b0, [&] {
+                // the split layer-0 in_proj reads the embedding's planes in sm.ctx
+                embed_apply<kActorTrunk, TR, kEmbH, split_kv<kActorTrunk, 0, TR, kTrainSplit>()>(TID_C sm, ep_a, io.e[0],
+                                                                                               io.h0[0], b0);
+                PTR(2);
+                __syncthreads();
+                auto hook = [&] {
                     if (wv < 4) ph = prefetch<4>(TID_C headw_a, D, 16 * wv, 0);
                     if (do_critic) {
                         ep_c = embed_load<kCriticTrunk>(TID_C P);
-                        pkv_c = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+                        pkv_c = kv_prefetch<kCriticTrunk, 0, TR, kTrainSplit>(TID_C P);
                     }
-                });
+                };
+                encoder_layer<kActorTrunk, 0, true, TR, decltype(hook), kTrainSplit>(TID_C sm, P, pkv_a, io.L[0], b0, hook);
             } else {
+                APre<2> pkv = prefetch<2>(TID_C P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+                embed<kActorTrunk, TR>(TID_C sm, P, io.e[0], io.h0[0], b0);
+                PTR(2);
+                __syncthreads();
                 encoder_layer<kActorTrunk, 0, true, TR>(TID_C sm, P, pkv, io.L[0], b0);
             }
         }
@@ -1573,14 +1696,14 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             __syncthreads();
             encoder_layer_rows<kCriticTrunk>(TID_C sm, P, pw, rp, rio, b0);
         }
-        KvPre<kCriticTrunk, 1, TR> pkv;
+        KvPre<kCriticTrunk, 1, TR, TR ? kTrainSplit : true> pkv;
         if constexpr (!ROWS) {
             if constexpr (TR) {
-                embed_apply<kCriticTrunk, TR>(TID_C sm, ep_c, io.e[1], io.h0[1], b0);
+                embed_apply<kCriticTrunk, TR, kEmbH, split_kv<kCriticTrunk, 0, TR, kTrainSplit>()>(TID_C sm, ep_c, io.e[1],
+                                                                                                 io.h0[1], b0);
                 __syncthreads();
-                encoder_layer<kCriticTrunk, 0, false, TR>(TID_C sm, P, pkv_c, io.L[1], b0, [&] {
-                    pkv = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], D, kv_row(wv, 0), 0);
-                });
+                auto hook = [&] { pkv = kv_prefetch<kCriticTrunk, 1, TR, kTrainSplit>(TID_C P); };
+                encoder_layer<kCriticTrunk, 0, false, TR, decltype(hook), kTrainSplit>(TID_C sm, P, pkv_c, io.L[1], b0, hook);
             } else {
                 APre<2> pkv0 = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
                 embed<kCriticTrunk, TR>(TID_C sm, P, io.e[1], io.h0[1], b0);
@@ -1588,12 +1711,13 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
                 encoder_layer<kCriticTrunk, 0, false, TR>(TID_C sm, P, pkv0, io.L[1], b0);
             }
         }
-        if (!TR) pkv = kv_prefetch<kCriticTrunk, 1, TR>(TID_C P);
+        if constexpr (!TR) pkv = kv_prefetch<kCriticTrunk, 1, TR>(TID_C P);
         __syncthreads();
         if constexpr (TR) {
-            encoder_layer<kCriticTrunk, 1, true, TR>(TID_C sm, P, pkv, io.L[2], b0, [&] {
+            auto hook = [&] {
                 if (wv < 4) ph = prefetch<4>(TID_C headw_c, D, 16 * wv, 0);
-            });
+            };
+            encoder_layer<kCriticTrunk, 1, true, TR, decltype(hook), kTrainSplit>(TID_C sm, P, pkv, io.L[2], b0, hook);
         } else {
             encoder_layer<kCriticTrunk, 1, true, TR>(TID_C sm, P, pkv, io.L[2], b0);
         }
@@ -2947,7 +3071,8 @@ int policy_split(const float* flat, float* packed, hipStream_t st) {
 int policy_pack_train(const float* flat, float* packed, float* packedT, hipStream_t st) {
     const int items = kOffs.o[kNumParams] / 4 + kPackedTFloats / 4;
     hipLaunchKernelGGL(k_policy_pack, dim3((items + 255) / 256), dim3(256), 0, st, flat, packed, packedT);
-    return check_launch("k_policy_pack");
+    if (const int rc = check_launch("k_policy_pack")) return rc;
+    return policy_split(flat, packed, st);
 }
 }  // namespace pol
 }  // namespace uavhip

@@ -215,6 +215,7 @@ struct AdamBlocks {
     int param[kAdamMaxBlocks];  // parameter of the block
     int first[kAdamMaxBlocks];  // its first float4 within the parameter
     int tbase[kAdamMaxBlocks];  // packedT offset of the parameter's transposed copy, -1: none
+    int sbase[kAdamMaxBlocks];  // packed offset of the parameter's split copy, -1: none
 };
 constexpr int adam_items(int q) { return pad4(kSizes[q]) / 4; }
 constexpr int packedT_base(int q) {
@@ -236,6 +237,7 @@ constexpr AdamBlocks make_adam_blocks() {
             b.param[b.n] = q;
             b.first[b.n] = f;
             b.tbase[b.n] = packedT_base(q);
+            b.sbase[b.n] = split_slot(q);
             ++b.n;
         }
     return b;
@@ -317,6 +319,20 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     const int loc = 4 * item, i = loc / NC, j = loc - i * NC;
     *reinterpret_cast<f32x4*>(a.packed + off + (((i >> 4) * (NC >> 4) + (j >> 4)) * 64 + (i & 15) +
                                                   16 * ((j & 15) >> 2)) * 4) = p;
+    // the split copy (policy_layout.hpp kSplitParam): the fp16 planes of these four weights, lane
+    // (i % 16) + 16 ((j % 32) / 8) of block (i / 16, j / 32), halves j % 8 .. + 3
+    if (const int sb = kAdamBlocks.sbase[blockIdx.x]; sb >= 0) {
+        wg_f16x4 w1, w2;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            w1[e] = (_Float16)p[e];
+            w2[e] = (_Float16)((p[e] - (float)w1[e]) * 2048.f);
+        }
+        _Float16* sp = reinterpret_cast<_Float16*>(a.packed + sb) +
+                       (((i >> 4) * (NC >> 5) + (j >> 5)) * 128 + (i & 15) + 16 * ((j & 31) >> 3)) * 8 + (j & 7);
+        *reinterpret_cast<wg_f16x4*>(sp) = w1;
+        *reinterpret_cast<wg_f16x4*>(sp + 64 * 8) = w2;
+    }
     // packedT: W^T ([NC][NR]) in fragment order, float4 = rows it..it+3 of column jt
     *reinterpret_cast<f32x4*>(tile + 4 * threadIdx.x) = p;
     __syncthreads();
@@ -410,7 +426,7 @@ inline Plan make_plan(int Bm, float* base) {
     p.wg_part = w.take((size_t)kWgGrid * kWgRuns * kWgSlot);
     p.bpart = w.take((size_t)p.prows * pol::kBiasPart);
     p.kvc = pol::ps_capable(Bm) ? w.take((size_t)p.prows * S * kHeadSamples * 2 * D) : nullptr;  // [prows][80][256]
-    p.packed = w.take(kOffs.o[kNumParams]);
+    p.packed = w.take(kPackedFloats);  // + the split copies (the training forward's split products)
     p.packedT = w.take(pol::kPackedTFloats);
     p.total = w.off;
     return p;
