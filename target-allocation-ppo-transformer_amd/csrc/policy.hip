@@ -267,16 +267,17 @@ __device__ __forceinline__ HPre<D_> hprefetch(TID_F const float* __restrict__ P,
 }
 // hi / lo[ct] += W[row + i][kw0 + k] * X[xtok0 + 16 ct + j][k] over k in [0, 128) (4 blocks of 32):
 // A blocks >= D_ loaded one block ahead of their use, B (LDS) one block ahead.
-template <int CT, int D_>
+// NKB blocks of 32 k; the activation planes have rows of LDX_ halves, plane 2 at + PLX halves.
+template <int CT, int D_, int NKB = D / 32, int LDX_ = LDP, int PLX = kPlane>
 __device__ __forceinline__ void hgemm_tile(TID_F f32x4 (&hi)[CT], f32x4 (&lo)[CT], const HPre<D_>& pre,
                                            const float* __restrict__ P, int soff, int K, int row, int kw0,
                                            const _Float16* X, int xtok0) {
-    constexpr int NKB = D / 32;
+    constexpr int kPlane = PLX;
     const int l = LANE(), i16 = l & 15, g = l >> 4;
     const f16x8* wp = hfrag_ptr(TID_C P, soff, K, row, kw0);
     const _Float16* xp[CT];
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) xp[ct] = X + (xtok0 + 16 * ct + i16) * LDP + 8 * g;
+    for (int ct = 0; ct < CT; ++ct) xp[ct] = X + (xtok0 + 16 * ct + i16) * LDX_ + 8 * g;
     f16x8 a1[NKB], a2[NKB], b1[2][CT], b2[2][CT];
 #pragma unroll
     for (int p = 0; p < D_; ++p) {
@@ -2036,6 +2037,8 @@ __device__ __forceinline__ void ln_bwd_load(LnBwdPre& a, const float* __restrict
         }
     }
 }
+// PL: dst receives the two fp16 planes of the split products (the next GEMM's operand) instead of fp32.
+template <bool PL = false>
 __device__ void ln_bwd_lds(const float* src, float* dst, const LnBwdPre& a, float* __restrict__ gout,
                            float* __restrict__ part, float* __restrict__ bias, int t0, int b0, bool compact,
                            float* scratch, int t1 = TOK) {
@@ -2057,8 +2060,13 @@ __device__ void ln_bwd_lds(const float* src, float* dst, const LnBwdPre& a, floa
         const float m1 = row16_sum(hsum(gw0) + hsum(gw1)) * (1.0f / D);
         const float m2 = row16_sum(hsum(gw0 * x0) + hsum(gw1 * x1)) * (1.0f / D);
         const f32x4 d0 = rs * (gw0 - m1 - x0 * m2), d1 = rs * (gw1 - m1 - x1 * m2);
-        st4(dst + tok * LDH + f0, d0);
-        st4(dst + tok * LDH + f0 + 4, d1);
+        if constexpr (PL) {
+            hsplit_store(reinterpret_cast<_Float16*>(dst), tok * LDP + f0, d0);
+            hsplit_store(reinterpret_cast<_Float16*>(dst), tok * LDP + f0 + 4, d1);
+        } else {
+            st4(dst + tok * LDH + f0, d0);
+            st4(dst + tok * LDH + f0 + 4, d1);
+        }
         st4(gout + r * D + f0, d0);
         st4(gout + r * D + f0 + 4, d1);
         pw0 += g0 * x0; pw1 += g1 * x1;
@@ -2118,8 +2126,25 @@ __device__ __forceinline__ void attn_bwd_load(AttnPre& a, const float* __restric
     for (int i = 0; i < S; ++i)
         if (qsel >= 0 ? i == qsel : (!last || i == S - 1)) a.q[i] = ld2(qkv + (rb + i) * 3 * D + col);
 }
-template <bool last>
-__device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch, int qsel = -1) {
+// SP (split-product backward): dq | dk | dv go to sm.big as the two fp16 planes of the W_in^T GEMM's
+// operand ([tok][LDB halves], plane 2 at + TOK LDB) and, exact, straight to the dqkv rows (dqkv != nullptr).
+__device__ __forceinline__ void attn_out2(Smem& sm, float* __restrict__ dqkv, int b0, int tok, int col, int part,
+                                          int c, f32x2 v, bool sp) {
+    if (sp) {
+        _Float16* bp = reinterpret_cast<_Float16*>(sm.big) + tok * LDB + part * 64 + col;
+        const _Float16 a0 = (_Float16)v.x, a1 = (_Float16)v.y;
+        typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<f16x2*>(bp) = f16x2{a0, a1};
+        *reinterpret_cast<f16x2*>(bp + TOK * LDB) = f16x2{(_Float16)((v.x - (float)a0) * 2048.f),
+                                                          (_Float16)((v.y - (float)a1) * 2048.f)};
+        st2(dqkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + col, v);
+    } else {
+        st2(sm.big + tok * LDB + part * 64 + col, v);
+    }
+}
+template <bool last, bool SP = false>
+__device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch, int qsel = -1,
+                               float* __restrict__ dqkv = nullptr, int b0 = 0) {
     const int o8 = tid_x() & 7, hh = (tid_x() >> 3) & 3, p = tid_x() >> 5;
     const int d0 = hh * HD + 2 * o8;
     const int col = 64 * c + d0;
@@ -2171,13 +2196,13 @@ __device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch
             }
             sdq += dq;
         }
-        st2(sm.big + (i * SPW + p) * LDB + d0, dq);
+        if (!SP || !last || i == S - 1) attn_out2(sm, dqkv, b0, i * SPW + p, d0, 0, c, dq, SP);
     }
     f32x2 sk = {0.f, 0.f}, sv = {0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-        st2(sm.big + (j * SPW + p) * LDB + 64 + d0, dk[j]);
-        st2(sm.big + (j * SPW + p) * LDB + 128 + d0, dv[j]);
+        attn_out2(sm, dqkv, b0, j * SPW + p, d0, 1, c, dk[j], SP);
+        attn_out2(sm, dqkv, b0, j * SPW + p, d0, 2, c, dv[j], SP);
         sk += dk[j];
         sv += dv[j];
     }
@@ -2216,6 +2241,167 @@ __device__ __forceinline__ void embed_bwd_load(EmbBwdPre& ep, const float* __res
                               : f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
+// The full-layer backward as split products (bwd_layer<..., SP>): the same phases, barriers and
+// outputs as the f32 path below.
+template <int trunk, int layer, bool last, int TB, class F>
+__device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const float* __restrict__ PT, const BwdLayerIO& io,
+                                int b0, EmbBwdPre* ep, const float* e_emb, const float* xg, const LnBwdPre* ln2_pre,
+                                F next_load, int liT) {
+    constexpr int CTQ = last ? 1 : S;
+    const int qtok0 = last ? (S - 1) * SPW : 0, qtok1 = qtok0 + SPW * CTQ;
+    (void)liT;  // PT is this layer's packedT (the caller's offset): its split copy at PT + kTSplit
+    const int sWin = kTSplit + kTWin, sWo = kTSplit + kTWo, sW1 = kTSplit + kTW1, sW2 = kTSplit + kTW2;
+    const int wv = tid_x() >> 6, l = lane_id(), i16 = l & 15, g = l >> 4;
+    const int fo = 16 * wv + 4 * g;
+    const int blk = b0 / SPW;
+    float* bias = io.bpart + (size_t)blk * kBiasPart;
+    _Float16* const hp = reinterpret_cast<_Float16*>(sm.h);
+    _Float16* const bp = reinterpret_cast<_Float16*>(sm.big);
+    _Float16* const cp = reinterpret_cast<_Float16*>(sm.ctx);
+    auto unsplit = [](const _Float16* x, int o) {  // x1 + 2^-11 x2 of 4 halves at o
+        const f16x4 a = *reinterpret_cast<const f16x4*>(x + o), b = *reinterpret_cast<const f16x4*>(x + o + kPlane);
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (float)a[j] + (float)b[j] * kLoScale;
+        return v;
+    };
+    // LN2 backward: sm.h -> df planes in sm.ctx
+    HPre<2> pa = hprefetch<2>(PT, sW2, D, 16 * wv, 0);
+    LnBwdPre lnp;
+    if (ln2_pre) lnp = *ln2_pre;
+    else ln_bwd_load(lnp, io.xhat2, io.rstd2, P + kOffs.o[layer_param(trunk, layer, N2W)], qtok0, b0, last, qtok1);
+    ln_bwd_lds<true>(sm.h, sm.ctx, lnp, io.df, io.ln2_part + (size_t)blk * 2 * D, bias + kBiasL2, qtok0, b0, last,
+                     sm.big, qtok1);
+    BTR(TB + 1);
+    __syncthreads();
+    BTR(TB + 2);
+    // du = relu'(u) (W2^T df): wave wv owns hidden tiles 16 wv (-> big planes) and 128 + 16 wv (-> h planes)
+    HPre<2> pb;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int row = 128 * t + 16 * wv;
+        f32x4 hi[CTQ], lo[CTQ], uu[CTQ];
+#pragma unroll
+        for (int ct = 0; ct < CTQ; ++ct)
+            uu[ct] = ld4(io.u + (size_t)orow(qtok0 + 16 * ct + i16, b0, last) * FF + row + 4 * g);
+        zero(hi);
+        zero(lo);
+        if (t == 0) {
+            hgemm_tile<CTQ, 2>(hi, lo, pa, PT, sW2, D, row, 0, cp, qtok0);
+            pb = hprefetch<2>(PT, sW2, D, 128 + 16 * wv, 0);
+        } else {
+            hgemm_tile<CTQ, 2>(hi, lo, pb, PT, sW2, D, row, 0, cp, qtok0);
+            pa = hprefetch<2>(PT, sW1, FF, 16 * wv, 0);
+        }
+        _Float16* dstp = t ? hp : bp;
+        f32x4 sd = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ct = 0; ct < CTQ; ++ct) {
+            const int tok = qtok0 + 16 * ct + i16;
+            const size_t r = (size_t)orow(tok, b0, last);
+            const f32x4 u = uu[ct];
+            f32x4 d = hi[ct] + lo[ct] * kLoScale;
+            d.x = u.x > 0.f ? d.x : 0.f; d.y = u.y > 0.f ? d.y : 0.f;
+            d.z = u.z > 0.f ? d.z : 0.f; d.w = u.w > 0.f ? d.w : 0.f;
+            st4(io.du + r * FF + row + 4 * g, d);
+            hsplit_store(dstp, tok * LDP + fo, d);
+            sd += d;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sd[e] = row16_sum(sd[e]);
+        if (i16 == 0) st4(bias + kBiasL1 + row + 4 * g, sd);
+    }
+    BTR(TB + 3);
+    __syncthreads();
+    BTR(TB + 4);
+    // dh1 = df + W1^T du (K = 256: hidden 0-127 in big, 128-255 in h) -> sm.ctx in fp32, after every
+    // lane has read its df (the fp32 rows overlap the planes)
+    {
+        f32x4 hi[CTQ], lo[CTQ];
+        zero(hi);
+        zero(lo);
+        hgemm_tile<CTQ, 2>(hi, lo, pa, PT, sW1, FF, 16 * wv, 0, bp, qtok0);
+        hgemm_tile<CTQ, 2>(hi, lo, hprefetch<2>(PT, sW1, FF, 16 * wv, 128), PT, sW1, FF, 16 * wv, 128, hp, qtok0);
+#pragma unroll
+        for (int ct = 0; ct < CTQ; ++ct) hi[ct] = hi[ct] + lo[ct] * kLoScale + unsplit(cp, (qtok0 + 16 * ct + i16) * LDP + fo);
+        __syncthreads();
+#pragma unroll
+        for (int ct = 0; ct < CTQ; ++ct) st4(sm.ctx + (qtok0 + 16 * ct + i16) * LDH + fo, hi[ct]);
+    }
+    pa = hprefetch<2>(PT, sWo, D, 16 * wv, 0);
+    ln_bwd_load(lnp, io.xhat1, io.rstd1, P + kOffs.o[layer_param(trunk, layer, N1W)], qtok0, b0, last, qtok1);
+    AttnPre ap;
+    attn_bwd_load<last>(ap, io.qkv, 0, b0, -1);
+    BTR(TB + 5);
+    __syncthreads();
+    BTR(TB + 6);
+    // LN1 backward: sm.ctx -> dz1 planes in sm.h
+    ln_bwd_lds<true>(sm.ctx, sm.h, lnp, io.dz1, io.ln1_part + (size_t)blk * 2 * D, bias + kBiasOut, qtok0, b0, last,
+                     sm.big, qtok1);
+    BTR(TB + 7);
+    __syncthreads();
+    BTR(TB + 8);
+    // d(attention output) = Wo^T dz1 -> sm.ctx (fp32: the attention backward's operand)
+    {
+        f32x4 hi[CTQ], lo[CTQ];
+        zero(hi);
+        zero(lo);
+        hgemm_tile<CTQ, 2>(hi, lo, pa, PT, sWo, D, 16 * wv, 0, hp, qtok0);
+#pragma unroll
+        for (int ct = 0; ct < CTQ; ++ct) st4(sm.ctx + (qtok0 + 16 * ct + i16) * LDH + fo, hi[ct] + lo[ct] * kLoScale);
+    }
+    BTR(TB + 9);
+    __syncthreads();
+    BTR(TB + 10);
+    // attention backward per chunk of 4 heads, dh_in += W_in^T [dq | dk | dv] of the chunk (K = 3 x 64)
+    f32x4 hi[S], lo[S];
+    zero(hi);
+    zero(lo);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        HPre<2> pw = hprefetch<2>(PT, sWin, 3 * D, 16 * wv, 64 * c);
+        attn_bwd_chunk<last, true>(sm, ap, c, sm.scr, -1, io.dqkv, b0);
+        __syncthreads();
+        BTR(TB + 11 + 2 * c);
+        if (tid_x() < 3 * 64) {  // in_proj bias partial of the chunk: the 8 wave rows of sm.scr
+            const int i = tid_x();
+            float v = 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) v += sm.scr[w * 192 + i];
+            bias[kBiasIn + (i >> 6) * D + 64 * c + (i & 63)] = v;
+        }
+        const HPre<2> pw1 = hprefetch<2>(PT, sWin, 3 * D, 16 * wv, D + 64 * c);
+        const HPre<2> pw2 = hprefetch<2>(PT, sWin, 3 * D, 16 * wv, 2 * D + 64 * c);
+        if (last) {  // dq is zero outside the query tile: W_in,q^T dq only for column tile 4
+            f32x4 h1[1] = {hi[S - 1]}, l1[1] = {lo[S - 1]};
+            hgemm_tile<1, 2, 2, LDB, TOK * LDB>(h1, l1, pw, PT, sWin, 3 * D, 16 * wv, 64 * c, bp, (S - 1) * SPW);
+            hi[S - 1] = h1[0];
+            lo[S - 1] = l1[0];
+        } else {
+            hgemm_tile<S, 2, 2, LDB, TOK * LDB>(hi, lo, pw, PT, sWin, 3 * D, 16 * wv, 64 * c, bp, 0);
+        }
+        hgemm_tile<S, 2, 2, LDB, TOK * LDB>(hi, lo, pw1, PT, sWin, 3 * D, 16 * wv, D + 64 * c, bp + 64, 0);
+        hgemm_tile<S, 2, 2, LDB, TOK * LDB>(hi, lo, pw2, PT, sWin, 3 * D, 16 * wv, 2 * D + 64 * c, bp + 128, 0);
+        if (c == 0) attn_bwd_load<last>(ap, io.qkv, 1, b0, -1);  // behind every weight load of the chunk
+        if (c == 0) __syncthreads();  // big is rewritten by chunk 1
+        BTR(TB + 12 + 2 * c);
+    }
+    if (layer == 0 && ep) embed_bwd_load(*ep, e_emb, xg, b0);
+    next_load();
+    // + dz1 on the rows that carried the residual -> sm.h (fp32, after every lane has read its dz1)
+    f32x4 res[S];
+#pragma unroll
+    for (int ct = 0; ct < S; ++ct) {
+        const int tok = 16 * ct + i16;
+        res[ct] = tok >= qtok0 ? unsplit(hp, tok * LDP + fo) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ct = 0; ct < S; ++ct) st4(sm.h + (16 * ct + i16) * LDH + fo, hi[ct] + lo[ct] * kLoScale + res[ct]);
+    __syncthreads();
+    BTR(TB + 15);
+}
+
 // ln2_pre: this layer's LN2-backward operands, already loaded by the caller (nullptr: load here);
 // next_load: issues the next phase's global loads behind this layer's last weight loads.
 // MODE (the position-split training step, K7 below): kBwdFull = the whole layer; kBwdNoDx = stop after
@@ -2224,11 +2410,18 @@ __device__ __forceinline__ void embed_bwd_load(EmbBwdPre& ep, const float* __res
 // ONE window position (tokens [qt, qt + 16), [b * 5 + s] rows, partial row prow): its dq rows go to
 // dqkv, its contributions to every position's dk / dv to kvc ([prow][80 tokens][dk 128 | dv 128]).
 enum { kBwdFull = 0, kBwdNoDx = 1, kBwdPos = 2 };
-template <int trunk, int layer, bool last, int TB, class F = NoHook, int MODE = kBwdFull>
+constexpr bool kBwdSplit = true;  // K6 (k_policy_backward) on split products; the K7 kernels stay f32
+// SP (kBwdFull only): every dX GEMM as split products on the f16 MFMA -- A = the transposed split
+// copies (PT + kTSplit), B = planes the producing epilogue writes: df (LN2 backward -> sm.ctx), du
+// (-> sm.big / sm.h), dz1 (LN1 backward -> sm.h), dq | dk | dv (attention backward -> sm.big, rows of
+// LDB halves); the residual terms read back from planes are x1 + 2^-11 x2.
+template <int trunk, int layer, bool last, int TB, class F = NoHook, int MODE = kBwdFull, bool SP = false>
 __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __restrict__ PT, const BwdLayerIO& io,
                           int b0, EmbBwdPre* ep = nullptr, const float* e_emb = nullptr, const float* xg = nullptr,
                           const LnBwdPre* ln2_pre = nullptr, F next_load = F{}, int qt = 0, int prow = -1,
                           float* __restrict__ kvc = nullptr) {
+    static_assert(!SP || MODE == kBwdFull, "split products: the full-layer backward");
+    constexpr int liT = (trunk == kActorTrunk ? 0 : 1 + layer) * kLayerT;  // this layer's packedT offset
     BTR(TB);
     static_assert(MODE != kBwdPos || !last, "position split: full layers only");
     constexpr int CTQ = (last || MODE == kBwdPos) ? 1 : S;
@@ -2245,6 +2438,10 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
     const int blk = prow >= 0 ? prow : b0 / SPW;  // this workgroup's partial rows
     float* bias = io.bpart + (size_t)blk * kBiasPart;  // this workgroup's bias partials
 
+    if constexpr (SP) {
+        bwd_layer_split<trunk, layer, last, TB, F>(sm, P, PT, io, b0, ep, e_emb, xg, ln2_pre, next_load, liT);
+        return;
+    } else {
     // LN2 backward: sm.h -> sm.ctx (= df)
     APre<DQ> pa = prefetch<DQ>(W2T, D, 16 * wv, 0);
     LnBwdPre lnp;
@@ -2396,6 +2593,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
     }
     __syncthreads();
     BTR(TB + 15);
+    }
 }
 
 // Embedding backward from sm.h = dL/d(h0) (80 tokens): h0 = relu(We x + be) + pos. Thread =
@@ -2596,14 +2794,14 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
         BTR(2);
         // layer 0's LN2-backward operands are loaded at the end of layer 1's backward
         LnBwdPre l2;
-        bwd_layer<kCriticTrunk, 1, true, 4>(sm, P, PT + 2 * kLayerT, io.L[2], b0, nullptr, nullptr, nullptr, nullptr,
-                                            [&] {
-                                                ln_bwd_load(l2, io.L[1].xhat2, io.L[1].rstd2,
-                                                            P + kOffs.o[layer_param(kCriticTrunk, 0, N2W)], 0, b0,
-                                                            false);
-                                            });
+        auto hook = [&] {
+            ln_bwd_load(l2, io.L[1].xhat2, io.L[1].rstd2, P + kOffs.o[layer_param(kCriticTrunk, 0, N2W)], 0, b0, false);
+        };
+        bwd_layer<kCriticTrunk, 1, true, 4, decltype(hook), kBwdFull, kBwdSplit>(sm, P, PT + 2 * kLayerT, io.L[2], b0,
+                                                                              nullptr, nullptr, nullptr, nullptr, hook);
         EmbBwdPre ep;
-        bwd_layer<kCriticTrunk, 0, false, 20>(sm, P, PT + 1 * kLayerT, io.L[1], b0, &ep, io.e[1], io.xg, &l2);
+        bwd_layer<kCriticTrunk, 0, false, 20, NoHook, kBwdFull, kBwdSplit>(sm, P, PT + 1 * kLayerT, io.L[1], b0, &ep,
+                                                                         io.e[1], io.xg, &l2);
         embed_bwd(sm, ep, io.epart + ((size_t)blk * 2 + 1) * kEmbPart);
         __syncthreads();
         BTR(52);
@@ -2613,7 +2811,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
         __syncthreads();
         BTR(53);
         EmbBwdPre ep;
-        bwd_layer<kActorTrunk, 0, true, 36>(sm, P, PT, io.L[0], b0, &ep, io.e[0], io.xg);
+        bwd_layer<kActorTrunk, 0, true, 36, NoHook, kBwdFull, kBwdSplit>(sm, P, PT, io.L[0], b0, &ep, io.e[0], io.xg);
         embed_bwd(sm, ep, io.epart + (size_t)blk * 2 * kEmbPart, 57);
         BTR(54);
     }
@@ -3068,10 +3266,39 @@ int policy_split(const float* flat, float* packed, hipStream_t st) {
     return check_launch("k_policy_split");
 }
 
+// flat -> the split copies of the three layers' transposed weights (packedT + kTSplit): one thread
+// per lane of a (16-row tile, 32-k block) of W^T, W^T[r][k] = W[k][r] gathered from the flat rows.
+__global__ __launch_bounds__(256) void k_policyT_split(const float* __restrict__ flat, float* __restrict__ packedT) {
+    const int i = blockIdx.x * 256 + tid_x();  // lane index over all 3 x kLayerT / 8 (tile, block, lane)
+    if (i >= kHeadT / 8) return;
+    const int li = i / (kLayerT / 8), loc = i - li * (kLayerT / 8);
+    const int trunk = li == 0 ? kActorTrunk : kCriticTrunk, layer = li == 2 ? 1 : 0;
+    int which, base, Rt, Kt;  // W^T is [Rt][Kt]; W flat [Kt][Rt]
+    if (loc < kTWo / 8) { which = INW; base = kTWin; Rt = D; Kt = 3 * D; }
+    else if (loc < kTW1 / 8) { which = OUTW; base = kTWo; Rt = D; Kt = D; }
+    else if (loc < kTW2 / 8) { which = L1W; base = kTW1; Rt = D; Kt = FF; }
+    else { which = L2W; base = kTW2; Rt = FF; Kt = D; }
+    const int u = loc - base / 8, l = u & 63, blk = u >> 6, kb = blk % (Kt / 32), rt = blk / (Kt / 32);
+    const int r = 16 * rt + (l & 15), k0 = 32 * kb + 8 * (l >> 4);
+    const float* w = flat + kOffs.o[layer_param(trunk, layer, which)] + r;
+    f16x8 w1, w2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float v = w[(size_t)(k0 + j) * Rt];
+        w1[j] = (_Float16)v;
+        w2[j] = (_Float16)((v - (float)w1[j]) * 2048.f);
+    }
+    f16x8* dst = reinterpret_cast<f16x8*>(packedT + kTSplit + li * kLayerT + base) + (size_t)blk * 128 + l;
+    dst[0] = w1;
+    dst[64] = w2;
+}
+
 int policy_pack_train(const float* flat, float* packed, float* packedT, hipStream_t st) {
     const int items = kOffs.o[kNumParams] / 4 + kPackedTFloats / 4;
     hipLaunchKernelGGL(k_policy_pack, dim3((items + 255) / 256), dim3(256), 0, st, flat, packed, packedT);
     if (const int rc = check_launch("k_policy_pack")) return rc;
+    hipLaunchKernelGGL(k_policyT_split, dim3((kHeadT / 8 + 255) / 256), dim3(256), 0, st, flat, packedT);
+    if (const int rc = check_launch("k_policyT_split")) return rc;
     return policy_split(flat, packed, st);
 }
 }  // namespace pol

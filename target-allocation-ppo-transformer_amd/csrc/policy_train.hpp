@@ -83,6 +83,11 @@ constexpr int kLayerT = kTW2 + D * FF;  // 131072 floats per layer
 // then head.0^T [128][64] of the actor and the critic head
 constexpr int kHeadT = 3 * kLayerT;
 constexpr int kPackedTFloats = kHeadT + 2 * D * HID;
+// then the split copies of the three layers' transposed weights (the backward's dX GEMMs as split
+// products): two fp16 planes per weight in split fragment order (policy_layout.hpp), at kTSplit +
+// the weight's packedT offset
+constexpr int kTSplit = kPackedTFloats;
+constexpr int kPackedTAllFloats = kTSplit + kHeadT;
 
 // flat parameters -> packed (forward) and packedT (backward) in one launch
 int policy_pack_train(const float* flat, float* packed, float* packedT, hipStream_t st);

@@ -340,8 +340,21 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     const int jt = threadIdx.x % NC, rq = threadIdx.x / NC, it = i0 + 4 * rq;
     const f32x4 col = {tile[(4 * rq) * NC + jt], tile[(4 * rq + 1) * NC + jt], tile[(4 * rq + 2) * NC + jt],
                        tile[(4 * rq + 3) * NC + jt]};
-    *reinterpret_cast<f32x4*>(a.packedT + kAdamBlocks.tbase[blockIdx.x] +
-                              (((jt >> 4) * (NR >> 4) + (it >> 4)) * 64 + (jt & 15) + 16 * ((it & 15) >> 2)) * 4) = col;
+    const int tb = kAdamBlocks.tbase[blockIdx.x];
+    *reinterpret_cast<f32x4*>(a.packedT + tb + (((jt >> 4) * (NR >> 4) + (it >> 4)) * 64 + (jt & 15) + 16 * ((it & 15) >> 2)) * 4) =
+        col;
+    if (tb < kHeadT) {  // a layer weight: its transposed split copy (W^T[jt][it .. it + 3], halves it % 8 ..)
+        wg_f16x4 w1, w2;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            w1[e] = (_Float16)col[e];
+            w2[e] = (_Float16)((col[e] - (float)w1[e]) * 2048.f);
+        }
+        _Float16* sp = reinterpret_cast<_Float16*>(a.packedT + kTSplit + tb) +
+                       (((jt >> 4) * (NR >> 5) + (it >> 5)) * 128 + (jt & 15) + 16 * ((it & 31) >> 3)) * 8 + (it & 7);
+        *reinterpret_cast<wg_f16x4*>(sp) = w1;
+        *reinterpret_cast<wg_f16x4*>(sp + 64 * 8) = w2;
+    }
 }
 
 // ================================================================== host orchestration
@@ -427,7 +440,7 @@ inline Plan make_plan(int Bm, float* base) {
     p.bpart = w.take((size_t)p.prows * pol::kBiasPart);
     p.kvc = pol::ps_capable(Bm) ? w.take((size_t)p.prows * S * kHeadSamples * 2 * D) : nullptr;  // [prows][80][256]
     p.packed = w.take(kPackedFloats);  // + the split copies (the training forward's split products)
-    p.packedT = w.take(pol::kPackedTFloats);
+    p.packedT = w.take(pol::kPackedTAllFloats);  // + the transposed split copies (K6's split products)
     p.total = w.off;
     return p;
 }
