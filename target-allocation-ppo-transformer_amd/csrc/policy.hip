@@ -941,18 +941,26 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
 // Training mode (TR): the activations the backward reads are written as in layer_tail -- the
 // attention output and the FFN hidden from their planes (the values the GEMMs consumed), the
 // LayerNorm outputs from registers.
-template <int trunk, int layer, bool last, bool TR = false, class F = NoHook>
+// PSX (the K7 position-split forward): a full layer for the 16 tokens of one position, [qt, qt + 16),
+// its residual in sm.h, LN2's output as planes for the kernel's next in_proj (ps_inproj_split); and
+// K7's pruned layers take their residual from sm.h (PSX = 2).
+template <int trunk, int layer, bool last, bool TR = false, class F = NoHook, int PSX = 0>
 __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __restrict__ P, const HPre<2>& po,
-                                                 const TrainLayerIO& io = TrainLayerIO{}, int b0 = 0, F pre_ln2 = F{}) {
+                                                 const TrainLayerIO& io = TrainLayerIO{}, int b0 = 0, F pre_ln2 = F{},
+                                                 int qt = 0) {
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
-    constexpr int CT = last ? 1 : S, t0 = last ? (S - 1) * SPW : 0, t1 = t0 + SPW * CT;
+    constexpr int CT = (last || PSX) ? 1 : S;
+    const int t0 = last ? (S - 1) * SPW : (PSX ? qt : 0), t1 = t0 + SPW * CT;
     const float* bo = P + kOffs.o[layer_param(trunk, layer, OUTB)];
     const float* b1 = P + kOffs.o[layer_param(trunk, layer, L1B)];
     const float* b2 = P + kOffs.o[layer_param(trunk, layer, L2B)];
     constexpr int s1 = split_slot(layer_param(trunk, layer, L1W)), s2 = split_slot(layer_param(trunk, layer, L2W));
     constexpr int so = split_slot(layer_param(trunk, layer, OUTW));
-    constexpr bool next_planes = !last && split_inproj<trunk, layer + 1>();  // LN2 writes the next layer's operand
-    constexpr bool res_ctx = split_inproj<trunk, layer>();  // the residual is in sm.ctx rows 0-15
+    // LN2 writes the next layer's operand planes (+ position 4 in fp32 to sm.ctx rows 0-15 for the
+    // full forward's pruned next layer)
+    constexpr bool next_planes = !last && split_inproj<trunk, layer + 1>();
+    constexpr bool row4 = next_planes && !PSX;
+    constexpr bool res_ctx = split_inproj<trunk, layer>() && !PSX;  // the residual is in sm.ctx rows 0-15
     static_assert(!res_ctx || last, "a split in_proj feeds a pruned layer");
     const int wv = TIDX() >> 6;
     _Float16* const hp = reinterpret_cast<_Float16*>(sm.h);
@@ -1022,8 +1030,8 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc2[ct] = hi[ct] + lo[ct] * kLoScale;
     pre_ln2();
-    residual_layernorm<CT, TR, next_planes, next_planes>(TID_C sm, acc2, lp2, t0, LnOut{io.xhat2, io.h2, io.rstd2, b0, last},
-                                                       nullptr, h1);
+    residual_layernorm<CT, TR, next_planes, row4>(TID_C sm, acc2, lp2, t0, LnOut{io.xhat2, io.h2, io.rstd2, b0, last},
+                                                nullptr, h1);
     PTR(tb + 14);
 }
 
@@ -2129,7 +2137,7 @@ __device__ __forceinline__ void attn_bwd_load(AttnPre& a, const float* __restric
 // SP (split-product backward): dq | dk | dv go to sm.big as the two fp16 planes of the W_in^T GEMM's
 // operand ([tok][LDB halves], plane 2 at + TOK LDB) and, exact, straight to the dqkv rows (dqkv != nullptr).
 __device__ __forceinline__ void attn_out2(Smem& sm, float* __restrict__ dqkv, int b0, int tok, int col, int part,
-                                          int c, f32x2 v, bool sp) {
+                                          int c, f32x2 v, bool sp, float* __restrict__ kvc = nullptr, int kblk = 0) {
     if (sp) {
         _Float16* bp = reinterpret_cast<_Float16*>(sm.big) + tok * LDB + part * 64 + col;
         const _Float16 a0 = (_Float16)v.x, a1 = (_Float16)v.y;
@@ -2137,14 +2145,18 @@ __device__ __forceinline__ void attn_out2(Smem& sm, float* __restrict__ dqkv, in
         *reinterpret_cast<f16x2*>(bp) = f16x2{a0, a1};
         *reinterpret_cast<f16x2*>(bp + TOK * LDB) = f16x2{(_Float16)((v.x - (float)a0) * 2048.f),
                                                           (_Float16)((v.y - (float)a1) * 2048.f)};
-        st2(dqkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + col, v);
+        if (kvc && part > 0)  // position split: this query position's share of every position's dk / dv
+            st2(kvc + ((size_t)kblk * TOK + tok) * 2 * D + (part - 1) * D + 64 * c + col, v);
+        else
+            st2(dqkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + col, v);
     } else {
         st2(sm.big + tok * LDB + part * 64 + col, v);
     }
 }
 template <bool last, bool SP = false>
 __device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch, int qsel = -1,
-                               float* __restrict__ dqkv = nullptr, int b0 = 0) {
+                               float* __restrict__ dqkv = nullptr, int b0 = 0, float* __restrict__ kvc = nullptr,
+                               int kblk = 0) {
     const int o8 = tid_x() & 7, hh = (tid_x() >> 3) & 3, p = tid_x() >> 5;
     const int d0 = hh * HD + 2 * o8;
     const int col = 64 * c + d0;
@@ -2196,13 +2208,13 @@ __device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch
             }
             sdq += dq;
         }
-        if (!SP || !last || i == S - 1) attn_out2(sm, dqkv, b0, i * SPW + p, d0, 0, c, dq, SP);
+        if (!SP || (qsel >= 0 ? i == qsel : (!last || i == S - 1))) attn_out2(sm, dqkv, b0, i * SPW + p, d0, 0, c, dq, SP);
     }
     f32x2 sk = {0.f, 0.f}, sv = {0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-        attn_out2(sm, dqkv, b0, j * SPW + p, d0, 1, c, dk[j], SP);
-        attn_out2(sm, dqkv, b0, j * SPW + p, d0, 2, c, dv[j], SP);
+        attn_out2(sm, dqkv, b0, j * SPW + p, d0, 1, c, dk[j], SP, kvc, kblk);
+        attn_out2(sm, dqkv, b0, j * SPW + p, d0, 2, c, dv[j], SP, kvc, kblk);
         sk += dk[j];
         sv += dv[j];
     }
@@ -2241,19 +2253,25 @@ __device__ __forceinline__ void embed_bwd_load(EmbBwdPre& ep, const float* __res
                               : f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-// The full-layer backward as split products (bwd_layer<..., SP>): the same phases, barriers and
-// outputs as the f32 path below.
-template <int trunk, int layer, bool last, int TB, class F>
+enum { kBwdFull = 0, kBwdNoDx = 1, kBwdPos = 2 };  // bwd_layer's MODE (see bwd_layer)
+constexpr bool kBwdSplit = true;  // K6 (k_policy_backward) on split products
+constexpr bool kPsSplit = true;   // the K7 position-split kernels (k_ps_f1..f3, k_ps_b1..b3) on split products
+static_assert(kTrainF32LayerCopies || (kTrainSplit && kBwdSplit && kPsSplit),
+              "a training kernel on f32 products reads the fp32 layer copies policy_pack_train leaves NaN");
+// The layer backward as split products (bwd_layer<..., SP>): the same phases, barriers and outputs
+// as the f32 path below, for every MODE.
+template <int trunk, int layer, bool last, int TB, class F, int MODE>
 __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const float* __restrict__ PT, const BwdLayerIO& io,
                                 int b0, EmbBwdPre* ep, const float* e_emb, const float* xg, const LnBwdPre* ln2_pre,
-                                F next_load, int liT) {
-    constexpr int CTQ = last ? 1 : S;
-    const int qtok0 = last ? (S - 1) * SPW : 0, qtok1 = qtok0 + SPW * CTQ;
+                                F next_load, int liT, int qt, int prow, float* __restrict__ kvc) {
+    constexpr int CTQ = (last || MODE == kBwdPos) ? 1 : S;
+    const int qtok0 = last ? (S - 1) * SPW : (MODE == kBwdPos ? qt : 0), qtok1 = qtok0 + SPW * CTQ;
+    const int qsel = MODE == kBwdPos ? qt / SPW : -1;
     (void)liT;  // PT is this layer's packedT (the caller's offset): its split copy at PT + kTSplit
     const int sWin = kTSplit + kTWin, sWo = kTSplit + kTWo, sW1 = kTSplit + kTW1, sW2 = kTSplit + kTW2;
     const int wv = tid_x() >> 6, l = lane_id(), i16 = l & 15, g = l >> 4;
     const int fo = 16 * wv + 4 * g;
-    const int blk = b0 / SPW;
+    const int blk = prow >= 0 ? prow : b0 / SPW;  // this workgroup's partial rows
     float* bias = io.bpart + (size_t)blk * kBiasPart;
     _Float16* const hp = reinterpret_cast<_Float16*>(sm.h);
     _Float16* const bp = reinterpret_cast<_Float16*>(sm.big);
@@ -2331,7 +2349,7 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
     pa = hprefetch<2>(PT, sWo, D, 16 * wv, 0);
     ln_bwd_load(lnp, io.xhat1, io.rstd1, P + kOffs.o[layer_param(trunk, layer, N1W)], qtok0, b0, last, qtok1);
     AttnPre ap;
-    attn_bwd_load<last>(ap, io.qkv, 0, b0, -1);
+    attn_bwd_load<last>(ap, io.qkv, 0, b0, qsel);
     BTR(TB + 5);
     __syncthreads();
     BTR(TB + 6);
@@ -2359,8 +2377,9 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
     zero(lo);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-        HPre<2> pw = hprefetch<2>(PT, sWin, 3 * D, 16 * wv, 64 * c);
-        attn_bwd_chunk<last, true>(sm, ap, c, sm.scr, -1, io.dqkv, b0);
+        [[maybe_unused]] HPre<2> pw;
+        if constexpr (MODE == kBwdFull) pw = hprefetch<2>(PT, sWin, 3 * D, 16 * wv, 64 * c);
+        attn_bwd_chunk<last, true>(sm, ap, c, sm.scr, qsel, io.dqkv, b0, MODE == kBwdPos ? kvc : nullptr, blk);
         __syncthreads();
         BTR(TB + 11 + 2 * c);
         if (tid_x() < 3 * 64) {  // in_proj bias partial of the chunk: the 8 wave rows of sm.scr
@@ -2369,6 +2388,11 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
 #pragma unroll
             for (int w = 0; w < NW; ++w) v += sm.scr[w * 192 + i];
             bias[kBiasIn + (i >> 6) * D + 64 * c + (i & 63)] = v;
+        }
+        if constexpr (MODE != kBwdFull) {  // the per-position kernels form dL/d(layer input)
+            if (c == 0) attn_bwd_load<last>(ap, io.qkv, 1, b0, qsel);
+            if (c == 0) __syncthreads();  // sm.scr is rewritten by chunk 1
+            continue;
         }
         const HPre<2> pw1 = hprefetch<2>(PT, sWin, 3 * D, 16 * wv, D + 64 * c);
         const HPre<2> pw2 = hprefetch<2>(PT, sWin, 3 * D, 16 * wv, 2 * D + 64 * c);
@@ -2382,10 +2406,11 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
         }
         hgemm_tile<S, 2, 2, LDB, TOK * LDB>(hi, lo, pw1, PT, sWin, 3 * D, 16 * wv, D + 64 * c, bp + 64, 0);
         hgemm_tile<S, 2, 2, LDB, TOK * LDB>(hi, lo, pw2, PT, sWin, 3 * D, 16 * wv, 2 * D + 64 * c, bp + 128, 0);
-        if (c == 0) attn_bwd_load<last>(ap, io.qkv, 1, b0, -1);  // behind every weight load of the chunk
+        if (c == 0) attn_bwd_load<last>(ap, io.qkv, 1, b0, qsel);  // behind every weight load of the chunk
         if (c == 0) __syncthreads();  // big is rewritten by chunk 1
         BTR(TB + 12 + 2 * c);
     }
+    if constexpr (MODE != kBwdFull) return;
     if (layer == 0 && ep) embed_bwd_load(*ep, e_emb, xg, b0);
     next_load();
     // + dz1 on the rows that carried the residual -> sm.h (fp32, after every lane has read its dz1)
@@ -2409,8 +2434,6 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
 // per-position kernels form dL/d(layer input)); kBwdPos = a full layer for the 16 query tokens of
 // ONE window position (tokens [qt, qt + 16), [b * 5 + s] rows, partial row prow): its dq rows go to
 // dqkv, its contributions to every position's dk / dv to kvc ([prow][80 tokens][dk 128 | dv 128]).
-enum { kBwdFull = 0, kBwdNoDx = 1, kBwdPos = 2 };
-constexpr bool kBwdSplit = true;  // K6 (k_policy_backward) on split products; the K7 kernels stay f32
 // SP (kBwdFull only): every dX GEMM as split products on the f16 MFMA -- A = the transposed split
 // copies (PT + kTSplit), B = planes the producing epilogue writes: df (LN2 backward -> sm.ctx), du
 // (-> sm.big / sm.h), dz1 (LN1 backward -> sm.h), dq | dk | dv (attention backward -> sm.big, rows of
@@ -2420,7 +2443,6 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
                           int b0, EmbBwdPre* ep = nullptr, const float* e_emb = nullptr, const float* xg = nullptr,
                           const LnBwdPre* ln2_pre = nullptr, F next_load = F{}, int qt = 0, int prow = -1,
                           float* __restrict__ kvc = nullptr) {
-    static_assert(!SP || MODE == kBwdFull, "split products: the full-layer backward");
     constexpr int liT = (trunk == kActorTrunk ? 0 : 1 + layer) * kLayerT;  // this layer's packedT offset
     BTR(TB);
     static_assert(MODE != kBwdPos || !last, "position split: full layers only");
@@ -2439,7 +2461,8 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
     float* bias = io.bpart + (size_t)blk * kBiasPart;  // this workgroup's bias partials
 
     if constexpr (SP) {
-        bwd_layer_split<trunk, layer, last, TB, F>(sm, P, PT, io, b0, ep, e_emb, xg, ln2_pre, next_load, liT);
+        bwd_layer_split<trunk, layer, last, TB, F, MODE>(sm, P, PT, io, b0, ep, e_emb, xg, ln2_pre, next_load, liT, qt,
+                                                         prow, kvc);
         return;
     } else {
     // LN2 backward: sm.h -> sm.ctx (= df)
@@ -2855,7 +2878,7 @@ __device__ __forceinline__ void ps_rows_in(float* dst, int lds, const float* __r
 
 // Embedding of window position s (transformer_net.py:57-59): h = relu(W_e x + b_e) + pos[s] -> sm.h
 // rows 16 s + p and the e / h0 workspace rows; wave w computes features [16 w, 16 w + 16).
-template <int trunk>
+template <int trunk, bool PL = false>  // PL: also the planes of h into sm.ctx (ps_inproj_split's operand)
 __device__ void ps_embed(Smem& sm, const float* __restrict__ P, float* __restrict__ e_out, float* __restrict__ h_out,
                          int b0, int s) {
     const float* We = P + kOffs.o[trunk + EMB_W];
@@ -2876,6 +2899,7 @@ __device__ void ps_embed(Smem& sm, const float* __restrict__ P, float* __restric
     e.x = fmaxf(e.x, 0.f); e.y = fmaxf(e.y, 0.f); e.z = fmaxf(e.z, 0.f); e.w = fmaxf(e.w, 0.f);
     const f32x4 v = e + pp;
     st4(sm.h + (s * SPW + i16) * LDH + 16 * wv + 4 * g, v);
+    if constexpr (PL) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), (s * SPW + i16) * LDP + 16 * wv + 4 * g, v);
     const size_t r = (size_t)trow(s * SPW + i16, b0);
     st4(e_out + r * D + 16 * wv + 4 * g, e);
     st4(h_out + r * D + 16 * wv + 4 * g, v);
@@ -2897,18 +2921,72 @@ __device__ void ps_inproj(Smem& sm, const float* __restrict__ W, const float* __
     }
 }
 
-// Q of position s and K | V of all five positions for the heads of chunk c -> sm.big [tok][Q|K|V]
-__device__ void ps_qkv_chunk(Smem& sm, const float* __restrict__ qkv, int c, int s, int b0) {
-    for (int i = tid_x(); i < SPW * 16 + TOK * 32; i += NTHR) {
-        int tok, part, q;
-        if (i < SPW * 16) {
-            tok = s * SPW + i / 16; part = 0; q = i % 16;
-        } else {
-            const int k = i - SPW * 16;
-            tok = k / 32; part = 1 + (k % 32) / 16; q = k % 16;
-        }
-        st4(sm.big + tok * LDB + part * 64 + 4 * q, ld4(qkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q));
+// ps_inproj as split products: the operand planes of the 16 tokens at X rows 16 s + p, W's split copy at soff
+__device__ void ps_inproj_split(const float* __restrict__ P, int soff, const float* __restrict__ bias,
+                                float* __restrict__ qkv, int tile0, int s, int b0, const _Float16* X) {
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
+    const size_t r = (size_t)trow(s * SPW + i16, b0);
+    for (int t = tile0 + wv; t < 3 * D / 16; t += NW) {  // wave-uniform
+        const int row = 16 * t;
+        const f32x4 bb = ld4(bias + row + 4 * g);
+        f32x4 hi[1], lo[1];
+        zero(hi);
+        zero(lo);
+        hgemm_tile<1, 2>(hi, lo, hprefetch<2>(P, soff, D, row, 0), P, soff, D, row, 0, X, s * SPW);
+        st4(qkv + r * 3 * D + row + 4 * g, hi[0] + lo[0] * kLoScale + bb);
     }
+}
+
+// Q of position s and K | V of all five positions for the heads of chunk c -> sm.big [tok][Q|K|V];
+// in two halves so that chunk 1's loads can be in flight during chunk 0's attention
+constexpr int kQkvItems = SPW * 16 + TOK * 32, kQkvIt = (kQkvItems + NTHR - 1) / NTHR;
+struct QkvPre {
+    f32x4 v[kQkvIt];
+};
+__device__ __forceinline__ void ps_qkv_item(int i, int s, int& tok, int& part, int& q) {
+    if (i < SPW * 16) {
+        tok = s * SPW + i / 16; part = 0; q = i % 16;
+    } else {
+        const int k = i - SPW * 16;
+        tok = k / 32; part = 1 + (k % 32) / 16; q = k % 16;
+    }
+}
+__device__ __forceinline__ void ps_qkv_load(QkvPre& r, const float* __restrict__ qkv, int c, int s, int b0) {
+#pragma unroll
+    for (int k = 0; k < kQkvIt; ++k) {
+        const int i = tid_x() + NTHR * k;
+        if (i < kQkvItems) {
+            int tok, part, q;
+            ps_qkv_item(i, s, tok, part, q);
+            r.v[k] = ld4(qkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q);
+        }
+    }
+}
+__device__ __forceinline__ void ps_qkv_store(Smem& sm, const QkvPre& r, int s) {
+#pragma unroll
+    for (int k = 0; k < kQkvIt; ++k) {
+        const int i = tid_x() + NTHR * k;
+        if (i < kQkvItems) {
+            int tok, part, q;
+            ps_qkv_item(i, s, tok, part, q);
+            st4(sm.big + tok * LDB + part * 64 + 4 * q, r.v[k]);
+        }
+    }
+}
+// the attention of both chunks (K7 F2 / F3): chunk 1's Q | K | V loads overlap chunk 0's attention
+template <bool PLANES>
+__device__ __forceinline__ void ps_attention(Smem& sm, const float* __restrict__ qkv, int s, int b0) {
+    QkvPre r;
+    ps_qkv_load(r, qkv, 0, s, b0);
+    ps_qkv_store(sm, r, s);
+    __syncthreads();
+    ps_qkv_load(r, qkv, 1, s, b0);
+    attention_chunk<PLANES>(sm, 0, s, 1);
+    __syncthreads();
+    ps_qkv_store(sm, r, s);
+    __syncthreads();
+    attention_chunk<PLANES>(sm, 1, s, 1);
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(NTHR) void k_ps_f1(const float* __restrict__ P, const float* __restrict__ states, int B,
@@ -2919,12 +2997,18 @@ __global__ __launch_bounds__(NTHR) void k_ps_f1(const float* __restrict__ P, con
     gather_windows<true>(sm, states, B, io, b0, r == 0);  // one workgroup per block writes the rows
     __syncthreads();
     const int trunk = critic ? kCriticTrunk : kActorTrunk;
-    if (critic) ps_embed<kCriticTrunk>(sm, P, io.e[1], io.h0[1], b0, s);
-    else ps_embed<kActorTrunk>(sm, P, io.e[0], io.h0[0], b0, s);
+    if (critic) ps_embed<kCriticTrunk, kPsSplit>(sm, P, io.e[1], io.h0[1], b0, s);
+    else ps_embed<kActorTrunk, kPsSplit>(sm, P, io.e[0], io.h0[0], b0, s);
     __syncthreads();
     // the actor's only layer is pruned: Q at position 4 only
-    ps_inproj(sm, P + kOffs.o[layer_param(trunk, 0, INW)], P + kOffs.o[layer_param(trunk, 0, INB)],
-              io.L[critic ? 1 : 0].qkv, critic || s == S - 1 ? 0 : D / 16, s, b0);
+    if constexpr (kPsSplit) {
+        ps_inproj_split(P, critic ? split_slot(layer_param(kCriticTrunk, 0, INW)) : split_slot(layer_param(kActorTrunk, 0, INW)),
+                        P + kOffs.o[layer_param(trunk, 0, INB)], io.L[critic ? 1 : 0].qkv, critic || s == S - 1 ? 0 : D / 16,
+                        s, b0, reinterpret_cast<const _Float16*>(sm.ctx));
+    } else {
+        ps_inproj(sm, P + kOffs.o[layer_param(trunk, 0, INW)], P + kOffs.o[layer_param(trunk, 0, INB)],
+                  io.L[critic ? 1 : 0].qkv, critic || s == S - 1 ? 0 : D / 16, s, b0);
+    }
 }
 
 __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, const TrainIO io) {
@@ -2934,24 +3018,32 @@ __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, con
     const int s = critic ? r : S - 1, ti = critic ? 1 : 0;
     ps_mask(sm, io.mask, b0);
     ps_rows_in(sm.h, LDH, io.h0[ti], D, 0, D, s, b0);  // the layer input (residual) of the position
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        ps_qkv_chunk(sm, io.L[ti].qkv, c, s, b0);
-        __syncthreads();
-        attention_chunk(sm, c, s, 1);
-        __syncthreads();
+    ps_attention<kPsSplit>(sm, io.L[ti].qkv, s, b0);
+    if constexpr (kPsSplit) {  // the layer tails and the next in_proj as split products
+        if (critic) {
+            const HPre<2> po = hprefetch<2>(P, split_slot(layer_param(kCriticTrunk, 0, OUTW)), D, 16 * wv, 0);
+            layer_tail_split<kCriticTrunk, 0, false, true, NoHook, 1>(sm, P, po, io.L[1], b0, NoHook{}, s * SPW);
+            __syncthreads();
+            // layer 1 (pruned) of this position: K | V, and Q at position 4, from LN2's planes in sm.h
+            ps_inproj_split(P, split_slot(layer_param(kCriticTrunk, 1, INW)), P + kOffs.o[layer_param(kCriticTrunk, 1, INB)],
+                            io.L[2].qkv, s == S - 1 ? 0 : D / 16, s, b0, reinterpret_cast<const _Float16*>(sm.h));
+            return;
+        }
+        const HPre<2> po = hprefetch<2>(P, split_slot(layer_param(kActorTrunk, 0, OUTW)), D, 16 * wv, 0);
+        layer_tail_split<kActorTrunk, 0, true, true>(sm, P, po, io.L[0], b0);
+    } else {
+        if (critic) {
+            const APre<4> po = prefetch<4>(P + kOffs.o[layer_param(kCriticTrunk, 0, OUTW)], D, 16 * wv, 0);
+            layer_tail<kCriticTrunk, 0, false, true, NoHook, 1>(sm, P, po, io.L[1], b0, NoHook{}, s * SPW);
+            __syncthreads();
+            // layer 1 (pruned) of this position: K | V, and Q at position 4
+            ps_inproj(sm, P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], P + kOffs.o[layer_param(kCriticTrunk, 1, INB)],
+                      io.L[2].qkv, s == S - 1 ? 0 : D / 16, s, b0);
+            return;
+        }
+        const APre<4> po = prefetch<4>(P + kOffs.o[layer_param(kActorTrunk, 0, OUTW)], D, 16 * wv, 0);
+        layer_tail<kActorTrunk, 0, true, true>(sm, P, po, io.L[0], b0);
     }
-    if (critic) {
-        const APre<4> po = prefetch<4>(P + kOffs.o[layer_param(kCriticTrunk, 0, OUTW)], D, 16 * wv, 0);
-        layer_tail<kCriticTrunk, 0, false, true, NoHook, 1>(sm, P, po, io.L[1], b0, NoHook{}, s * SPW);
-        __syncthreads();
-        // layer 1 (pruned) of this position: K | V, and Q at position 4
-        ps_inproj(sm, P + kOffs.o[layer_param(kCriticTrunk, 1, INW)], P + kOffs.o[layer_param(kCriticTrunk, 1, INB)],
-                  io.L[2].qkv, s == S - 1 ? 0 : D / 16, s, b0);
-        return;
-    }
-    const APre<4> po = prefetch<4>(P + kOffs.o[layer_param(kActorTrunk, 0, OUTW)], D, 16 * wv, 0);
-    layer_tail<kActorTrunk, 0, true, true>(sm, P, po, io.L[0], b0);
     APre<4> ph;
     if (wv < 4) ph = prefetch<4>(P + kOffs.o[kActorHead], D, 16 * wv, 0);
     __syncthreads();
@@ -2969,15 +3061,14 @@ __global__ __launch_bounds__(NTHR) void k_ps_f3(const float* __restrict__ P, con
     const int b0 = blockIdx.x * SPW, wv = tid_x() >> 6;
     ps_mask(sm, io.mask, b0);
     ps_rows_in(sm.h, LDH, io.L[1].h2, D, 0, D, S - 1, b0);  // layer 1's input (residual) at position 4
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        ps_qkv_chunk(sm, io.L[2].qkv, c, S - 1, b0);
-        __syncthreads();
-        attention_chunk(sm, c, S - 1, 1);
-        __syncthreads();
+    ps_attention<kPsSplit>(sm, io.L[2].qkv, S - 1, b0);
+    if constexpr (kPsSplit) {  // the residual is in sm.h (ps_rows_in): PSX = 2
+        const HPre<2> po = hprefetch<2>(P, split_slot(layer_param(kCriticTrunk, 1, OUTW)), D, 16 * wv, 0);
+        layer_tail_split<kCriticTrunk, 1, true, true, NoHook, 2>(sm, P, po, io.L[2], b0);
+    } else {
+        const APre<4> po = prefetch<4>(P + kOffs.o[layer_param(kCriticTrunk, 1, OUTW)], D, 16 * wv, 0);
+        layer_tail<kCriticTrunk, 1, true, true>(sm, P, po, io.L[2], b0);
     }
-    const APre<4> po = prefetch<4>(P + kOffs.o[layer_param(kCriticTrunk, 1, OUTW)], D, 16 * wv, 0);
-    layer_tail<kCriticTrunk, 1, true, true>(sm, P, po, io.L[2], b0);
     APre<4> ph;
     if (wv < 4) ph = prefetch<4>(P + kOffs.o[kCriticHead], D, 16 * wv, 0);
     __syncthreads();
@@ -3003,24 +3094,40 @@ __global__ __launch_bounds__(NTHR) void k_ps_b1(const float* __restrict__ P, con
     if (role == 2) {  // critic: head.0, layer 1 (pruned) down to its dqkv rows
         head_input_grad(sm, PT + kHeadT + D * HID, sm.ctx + 64);
         __syncthreads();
-        bwd_layer<kCriticTrunk, 1, true, 4, NoHook, kBwdNoDx>(sm, P, PT + 2 * kLayerT, io.L[2], b0, nullptr, nullptr,
+        bwd_layer<kCriticTrunk, 1, true, 4, NoHook, kBwdNoDx, kPsSplit>(sm, P, PT + 2 * kLayerT, io.L[2], b0, nullptr, nullptr,
                                                                  nullptr, nullptr, NoHook{}, 0, blk * S);
     } else {  // actor: head.0, layer 0 (pruned) down to its dqkv rows
         head_input_grad(sm, PT + kHeadT, sm.z);
         __syncthreads();
-        bwd_layer<kActorTrunk, 0, true, 36, NoHook, kBwdNoDx>(sm, P, PT, io.L[0], b0, nullptr, nullptr, nullptr,
+        bwd_layer<kActorTrunk, 0, true, 36, NoHook, kBwdNoDx, kPsSplit>(sm, P, PT, io.L[0], b0, nullptr, nullptr, nullptr,
                                                                 nullptr, NoHook{}, 0, blk * S);
     }
 }
 
 // The 16 [dq | dk | dv] rows of position s -> sm.big rows p (stride LDQ); with_q = false: a pruned
 // layer off its query position (dq never written there: zero)
+// (kPsSplit: as the two fp16 planes of ps_dx's split products, rows of LDQ halves, plane 2 at + SPW LDQ)
+__device__ __forceinline__ void ps_big_store(Smem& sm, int p, int q, const f32x4 v) {
+    if constexpr (kPsSplit) {
+        _Float16* bp = reinterpret_cast<_Float16*>(sm.big);
+        f16x4 a, b;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            a[j] = (_Float16)v[j];
+            b[j] = (_Float16)((v[j] - (float)a[j]) * 2048.f);
+        }
+        *reinterpret_cast<f16x4*>(bp + p * LDQ + 4 * q) = a;
+        *reinterpret_cast<f16x4*>(bp + SPW * LDQ + p * LDQ + 4 * q) = b;
+    } else {
+        st4(sm.big + p * LDQ + 4 * q, v);
+    }
+}
 __device__ __forceinline__ void ps_dqkv_in(Smem& sm, const float* __restrict__ dqkv, bool with_q, int s, int b0) {
     for (int i = tid_x(); i < SPW * 96; i += NTHR) {
         const int p = i / 96, q = i - 96 * p;
         f32x4 v = ld4(dqkv + (size_t)trow(s * SPW + p, b0) * 3 * D + 4 * q);
         if (!with_q && q < 32) v = f32x4{0.f, 0.f, 0.f, 0.f};
-        st4(sm.big + p * LDQ + 4 * q, v);
+        ps_big_store(sm, p, q, v);
     }
 }
 // dL/d(layer input) of position s = W_in^T [dq | dk | dv] (sm.big, ps_dqkv_in) + the residual rows
@@ -3031,11 +3138,24 @@ __device__ void ps_dx(Smem& sm, const float* __restrict__ WinT, bool with_q, con
     const int fo = 16 * wv + 4 * g;
     f32x4 acc[1];
     zero(acc);
+    if constexpr (kPsSplit) {  // WinT + kTSplit: the split copy of this layer's in_proj^T
+        f32x4 lo[1];
+        zero(lo);
+        const _Float16* bp = reinterpret_cast<const _Float16*>(sm.big);
 #pragma unroll
-    for (int part = 0; part < 3; ++part) {
-        if (part == 0 && !with_q) continue;
-        gemm_tile<1, 4>(acc, prefetch<4>(WinT, 3 * D, 16 * wv, part * D), WinT, 3 * D, 16 * wv, part * D,
-                        sm.big + part * D, LDQ, 0);
+        for (int part = 0; part < 3; ++part) {
+            if (part == 0 && !with_q) continue;
+            hgemm_tile<1, 2, 4, LDQ, SPW * LDQ>(acc, lo, hprefetch<2>(WinT, kTSplit, 3 * D, 16 * wv, part * D), WinT,
+                                                kTSplit, 3 * D, 16 * wv, part * D, bp + part * D, 0);
+        }
+        acc[0] += lo[0] * kLoScale;
+    } else {
+#pragma unroll
+        for (int part = 0; part < 3; ++part) {
+            if (part == 0 && !with_q) continue;
+            gemm_tile<1, 4>(acc, prefetch<4>(WinT, 3 * D, 16 * wv, part * D), WinT, 3 * D, 16 * wv, part * D,
+                            sm.big + part * D, LDQ, 0);
+        }
     }
     f32x4 v = acc[0];
     if (res) v += ld4(res + (size_t)i16 * res_ld + fo);
@@ -3105,7 +3225,7 @@ __global__ __launch_bounds__(NTHR) void k_ps_b2(const float* __restrict__ P, con
         ps_embed_bwd(sm, io.e[0], io.xg, io.epart + (size_t)prow * 2 * kEmbPart, s, b0);
         return;
     }
-    bwd_layer<kCriticTrunk, 0, false, 20, NoHook, kBwdPos>(sm, P, PT + kLayerT, io.L[1], b0, nullptr, nullptr, nullptr,
+    bwd_layer<kCriticTrunk, 0, false, 20, NoHook, kBwdPos, kPsSplit>(sm, P, PT + kLayerT, io.L[1], b0, nullptr, nullptr, nullptr,
                                                               nullptr, NoHook{}, s * SPW, prow, kvc);
 }
 
@@ -3128,7 +3248,7 @@ __global__ __launch_bounds__(NTHR) void k_ps_b3(const float* __restrict__ PT, co
             for (int s = 0; s < S; ++s) v += ld4(kvc + ((size_t)(blk * S + s) * TOK + tok) * 2 * D + 4 * (q - 32));
             st4(dqkv + row * 3 * D + 4 * q, v);
         }
-        st4(sm.big + p * LDQ + 4 * q, v);
+        ps_big_store(sm, p, q, v);
     }
     __syncthreads();
     // + LN1's input gradient of layer 0 at position j (the residual path)
@@ -3207,10 +3327,19 @@ __global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ f
             const int kb = blk % KB, rt = blk / KB;
             src = kOffs.o[lo] + (16 * rt + (lane & 15)) * K + 16 * kb + 4 * (lane >> 4);
         }
-        *reinterpret_cast<f32x4*>(packed + f) = *reinterpret_cast<const f32x4*>(flat + src);
+        // the training pack (packedT given): the split-copy weights' fp32 copies are never read
+        const bool dead = !kTrainF32LayerCopies && packedT && K != 0 && split_slot(lo) >= 0;
+        *reinterpret_cast<f32x4*>(packed + f) =
+            dead ? f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")}
+                 : *reinterpret_cast<const f32x4*>(flat + src);
         return;
     }
     if (!packedT || i >= nq + kPackedTFloats / 4) return;
+    if (!kTrainF32LayerCopies && 4 * (i - nq) < kHeadT) {  // a layer weight's fp32 transposed copy: dead
+        *reinterpret_cast<f32x4*>(packedT + 4 * (i - nq)) =
+            f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+        return;
+    }
     const int idx = 4 * (i - nq);
     int src, m, Rt, Kt;
     if (idx < kHeadT) {

@@ -88,6 +88,11 @@ constexpr int kPackedTFloats = kHeadT + 2 * D * HID;
 // the weight's packedT offset
 constexpr int kTSplit = kPackedTFloats;
 constexpr int kPackedTAllFloats = kTSplit + kHeadT;
+// The training kernels read the encoder GEMM weights only through their split copies (policy.hip
+// kTrainSplit / kBwdSplit / kPsSplit): the trainer's fp32 fragment-order copies of those weights
+// (packed at their kOffs slots, packedT below kHeadT) are dead. policy_pack_train fills them with
+// NaN (a read would poison every output) and k_adam does not refresh them.
+constexpr bool kTrainF32LayerCopies = false;
 
 // flat parameters -> packed (forward) and packedT (backward) in one launch
 int policy_pack_train(const float* flat, float* packed, float* packedT, hipStream_t st);

@@ -105,6 +105,7 @@ struct Segment {
     const float* src_rest;  // part p >= 1 at src_rest + (p - 1) * part_stride
     int dst, count, parts, part_stride, block_begin, tile_mode;
     int dst_ld;             // 0: dst + i; else a 128-wide weight tile, dst + (i / 128) * dst_ld + i % 128
+    int vec4;               // element mode with 16-byte aligned rows: a thread sums 4 consecutive elements
 };
 constexpr int kMaxSegs = 64;
 constexpr int kTileModeParts = 16;  // more parts than this: tile mode
@@ -148,6 +149,28 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
             const float tot = (wsum[0][l] + wsum[1][l]) + (wsum[2][l] + wsum[3][l]);
             grads[dsti(i)] = tot;
             sq = tot * tot;
+        }
+    } else if (S_.vec4) {
+        const int i = 4 * ((blockIdx.x - S_.block_begin) * 256 + threadIdx.x);
+        if (i + 4 <= S_.count) {
+            f32x4 acc[4] = {};
+            int p = 0;
+#pragma unroll 2
+            for (; p + 4 <= S_.parts; p += 4) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[u] += *reinterpret_cast<const f32x4*>(part(p + u) + i);
+            }
+            for (; p < S_.parts; ++p) acc[0] += *reinterpret_cast<const f32x4*>(part(p) + i);
+            const f32x4 tot = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+            *reinterpret_cast<f32x4*>(grads + dsti(i)) = tot;
+            sq = (tot[0] * tot[0] + tot[1] * tot[1]) + (tot[2] * tot[2] + tot[3] * tot[3]);
+        } else {
+            for (int e = i; e < S_.count; ++e) {  // the ragged end of the segment
+                float tot = 0.f;
+                for (int p = 0; p < S_.parts; ++p) tot += part(p)[e];
+                grads[dsti(e)] = tot;
+                sq += tot * tot;
+            }
         }
     } else {
         const int i = (blockIdx.x - S_.block_begin) * 256 + threadIdx.x;
@@ -315,13 +338,16 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
         if (live) *reinterpret_cast<f32x4*>(a.packed + f) = p;
         return;
     }
-    // packed: row i of [NR][NC] in fragment order, float4 = columns j..j+3
+    // packed: row i of [NR][NC] in fragment order, float4 = columns j..j+3 (not for the weights the
+    // training kernels read only through their split copies: policy_train.hpp kTrainF32LayerCopies)
     const int loc = 4 * item, i = loc / NC, j = loc - i * NC;
-    *reinterpret_cast<f32x4*>(a.packed + off + (((i >> 4) * (NC >> 4) + (j >> 4)) * 64 + (i & 15) +
-                                                  16 * ((j & 15) >> 2)) * 4) = p;
+    const int sb = kAdamBlocks.sbase[blockIdx.x];
+    if (kTrainF32LayerCopies || sb < 0)
+        *reinterpret_cast<f32x4*>(a.packed + off + (((i >> 4) * (NC >> 4) + (j >> 4)) * 64 + (i & 15) +
+                                                      16 * ((j & 15) >> 2)) * 4) = p;
     // the split copy (policy_layout.hpp kSplitParam): the fp16 planes of these four weights, lane
     // (i % 16) + 16 ((j % 32) / 8) of block (i / 16, j / 32), halves j % 8 .. + 3
-    if (const int sb = kAdamBlocks.sbase[blockIdx.x]; sb >= 0) {
+    if (sb >= 0) {
         wg_f16x4 w1, w2;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -341,8 +367,9 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     const f32x4 col = {tile[(4 * rq) * NC + jt], tile[(4 * rq + 1) * NC + jt], tile[(4 * rq + 2) * NC + jt],
                        tile[(4 * rq + 3) * NC + jt]};
     const int tb = kAdamBlocks.tbase[blockIdx.x];
-    *reinterpret_cast<f32x4*>(a.packedT + tb + (((jt >> 4) * (NR >> 4) + (it >> 4)) * 64 + (jt & 15) + 16 * ((it & 15) >> 2)) * 4) =
-        col;
+    if (kTrainF32LayerCopies || tb >= kHeadT)
+        *reinterpret_cast<f32x4*>(a.packedT + tb + (((jt >> 4) * (NR >> 4) + (it >> 4)) * 64 + (jt & 15) +
+                                                    16 * ((it & 15) >> 2)) * 4) = col;
     if (tb < kHeadT) {  // a layer weight: its transposed split copy (W^T[jt][it .. it + 3], halves it % 8 ..)
         wg_f16x4 w1, w2;
 #pragma unroll
@@ -623,7 +650,10 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         s.dst_ld = dst_ld;
         s.block_begin = seg_blocks;
         s.tile_mode = parts > kTileModeParts && !src_rest;
-        seg_blocks += s.tile_mode ? (count + 63) / 64 : (count + 255) / 256;
+        auto al16 = [](const float* q) { return ((uintptr_t)q & 15) == 0; };
+        s.vec4 = !s.tile_mode && al16(s.src) && al16(s.src_rest) && part_stride % 4 == 0 && dst % 4 == 0 &&
+                 dst_ld % 4 == 0;
+        seg_blocks += s.tile_mode ? (count + 63) / 64 : s.vec4 ? (count + 1023) / 1024 : (count + 255) / 256;
     };
     {
         // dW[out][in] = sum_rows dY[row][out] X[row][in]; dst = the weight's float offset
