@@ -118,13 +118,13 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
                                                       const AdamHyper h, AdamScalars* __restrict__ sc) {
     __shared__ float red[4];
     __shared__ float wsum[4][64];
-    int si = 0, hi = sb.n;  // segment of this block: binary search (each probe is a kernarg load)
-    while (hi - si > 1) {
-        const int mid = (si + hi) >> 1;
-        if ((int)blockIdx.x >= sb.s[mid].block_begin) si = mid;
-        else hi = mid;
-    }
-    const Segment& S_ = sb.s[si];
+    // segment of this block: lane l tests segment l (one round of kernarg loads, not a dependent
+    // binary search); the segments are in block order, so the count of those begun is its index + 1
+    static_assert(kMaxSegs <= 64, "one segment per lane");
+    const int sl = lane_id();
+    const bool begun = sl < sb.n && (int)blockIdx.x >= sb.s[sl].block_begin;
+    const int si = __popcll(__ballot(begun)) - 1;
+    const Segment S_ = sb.s[si];  // by value: one batch of scalar loads, not one per field use
     const size_t ps = S_.part_stride;
     auto part = [&](int p) { return p == 0 ? S_.src : S_.src_rest + (size_t)(p - 1) * ps; };
     auto dsti = [&](int i) { return S_.dst + (S_.dst_ld ? (i >> 7) * S_.dst_ld + (i & 127) : i); };

