@@ -69,10 +69,15 @@ SPLIT_FLOP_PER_SAMPLE_ROWS = (_SPLIT_WG + 2 * 384 * 128 * 2 * 16) // 16         
 MFMA_SPLIT_PEAK_TFLOPS = 157.3 * 16 / 3  # fp32-equivalent: f16 MFMA (16x the f32 rate) / 3 products
 TRAIN_FLOP_PER_SAMPLE_EPOCH = 3 * 4_040_000  # training ~ 3 x dense forward
 TRAIN_EXEC_FLOP_PER_SAMPLE_EPOCH = 7_460_000  # pruned forward + dX + dW
-# where that work runs: the forward's encoder GEMMs as two-plane split products
-# (3 f16 MFMAs per block), the embeddings and heads and the input gradients (dX) on the f32 MFMA, the
-# weight gradients (k_wgrad) as three-plane split products (6 f16 MFMAs per block)
+# where that work runs: the forward's encoder GEMMs and the encoder layers' input
+# gradients (dX: K6 / K7 on the transposed split copies) as two-plane split products (3 f16 MFMAs per
+# block), the weight gradients (k_wgrad) as three-plane split products (6 f16 MFMAs per block), the
+# embeddings and heads on the f32 MFMA
 TRAIN_FWD_SPLIT_FLOP = 2_446_208 - 2 * 80 * 128 * 16 * 2 // 16 - 2 * 64 * 128 * 2  # 2,389,248
+# dX per sample: the critic's full layer 0 over its 5 tokens (Win^T 384, Wo^T 128, W1^T / W2^T 256
+# each, x 128 x 2) + the two pruned top layers (Wo^T / W1^T / W2^T on token 4, Win^T's dq on token 4
+# and dk | dv on all 5)
+TRAIN_DX_SPLIT_FLOP = 5 * (384 + 128 + 256 + 256) * 128 * 2 + 2 * ((128 + 256 + 256 + 128) + 5 * 256) * 128 * 2
 TRAIN_WGRAD_FLOP = 2_390_000
 MFMA_SPLIT3_PEAK_TFLOPS = 157.3 * 16 / 6
 MFMA_F32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: fp32 MFMA = vector peak
@@ -344,10 +349,11 @@ def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
     # + input gradients 2.62 + weight gradients 2.39 MFLOP), over all GPUs
     alg_tf = se * TRAIN_FLOP_PER_SAMPLE_EPOCH / 1e12
     exe_tf = se * TRAIN_EXEC_FLOP_PER_SAMPLE_EPOCH / 1e12
-    # the MFMA peak of the executed FLOP mix (per GPU, x world): split products at 16/3 (forward) and
-    # 16/6 (weight gradients) x the f32 MFMA rate, the rest on the f32 MFMA
-    f32_flop = TRAIN_EXEC_FLOP_PER_SAMPLE_EPOCH - TRAIN_FWD_SPLIT_FLOP - TRAIN_WGRAD_FLOP
-    mix_s = (TRAIN_FWD_SPLIT_FLOP / MFMA_SPLIT_PEAK_TFLOPS + TRAIN_WGRAD_FLOP / MFMA_SPLIT3_PEAK_TFLOPS
+    # the MFMA peak of the executed FLOP mix (per GPU, x world): split products at 16/3 (forward, dX)
+    # and 16/6 (weight gradients) x the f32 MFMA rate, the rest on the f32 MFMA
+    split2 = TRAIN_FWD_SPLIT_FLOP + TRAIN_DX_SPLIT_FLOP
+    f32_flop = TRAIN_EXEC_FLOP_PER_SAMPLE_EPOCH - split2 - TRAIN_WGRAD_FLOP
+    mix_s = (split2 / MFMA_SPLIT_PEAK_TFLOPS + TRAIN_WGRAD_FLOP / MFMA_SPLIT3_PEAK_TFLOPS
              + f32_flop / MFMA_F32_PEAK_TFLOPS)
     peak = TRAIN_EXEC_FLOP_PER_SAMPLE_EPOCH / mix_s * world
     return {"value": n / pdt, "unit": "PPO samples/s (whole node: transitions in the update batch / update "
@@ -356,8 +362,11 @@ def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
            "sample_epochs_per_s": se, "impl": impl,
            "roofline": {"bound": "mfma", "unit": "TFLOP/s (fp32-accurate)", "peak": peak, "achieved": exe_tf,
                         "frac": exe_tf / peak,
-                        "peak_source": "MFMA peak of the executed FLOP mix (forward GEMMs as two-plane split "
-                                       "products, weight gradients as three-plane, input gradients on the f32 MFMA)",
+                        "peak_source": "MFMA peak of the executed FLOP mix (forward GEMMs and the encoder input "
+                                       "gradients as two-plane split products, weight gradients as three-plane, "
+                                       "embeddings and heads on the f32 MFMA)",
+                        # round 2's measure (every FLOP priced on the f32 MFMA, 157.3 TFLOP/s per GPU)
+                        "f32_mfma_equivalent_frac": exe_tf / (MFMA_F32_PEAK_TFLOPS * world),
                         "algorithmic_achieved": alg_tf,
                         "flop_per_sample_epoch": TRAIN_FLOP_PER_SAMPLE_EPOCH,
                         "flop_source": "SURVEY.md 8(d): 3 x the dense forward (4.04 MFLOP) per sample-epoch",
@@ -572,6 +581,8 @@ def main():
                          "flop_per_launch_source": "SURVEY.md 8(d): 2,446,208 FLOP/sample x E",
                          "executed_flop_per_launch": flop_exec * E, "executed_achieved": exec_tf,
                          "executed_peak": peak_exec, "executed_frac": exec_tf / peak_exec,
+                         # round 2's measure (every executed FLOP priced on the f32 MFMA, 157.3 TFLOP/s)
+                         "f32_mfma_equivalent_frac": exec_tf / MFMA_F32_PEAK_TFLOPS,
                          "split_flop_per_launch": split * E,
                          "steps_per_launch": T if eng.persistent else 1,
                          "path": ("fused rollout steps (window-row forward + sample + env step), all T steps of the "
