@@ -327,7 +327,12 @@ def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
                     "MFMA GEMM, fused clip + Adam), one hipGraph replay per epoch")
         else:
             impl = ("HIP training step, data parallel: forward / all-reduce loss sums / backward / "
-                    "all-reduce grads (RCCL) / clip+Adam per global minibatch")
+                    "all-reduce grads / clip+Adam per global minibatch")
+            if trainer.graph_collectives:  # RCCL: the epoch with its all-reduces as one graph (not timed)
+                trainer.capture()
+                impl += ", one hipGraph replay per epoch with the RCCL all-reduces captured"
+            else:
+                impl += f", eager ({dist.get_backend()} collectives)"
         gen = torch.Generator().manual_seed(1234)  # same minibatch order on every rank
         run = lambda: trainer.run(generator=gen)  # noqa: E731
     torch.cuda.synchronize()
@@ -479,6 +484,25 @@ def main():
     env_steps = E * T * args.steps * world
     value = env_steps / elapsed
 
+    timeline = None
+    if dist is not None:  # one more iteration, untimed, with the phases separated: rollout | exchange
+        torch.cuda.synchronize()
+        dist.barrier()
+        a = time.perf_counter()
+        eng.collect()
+        torch.cuda.synchronize()
+        b = time.perf_counter()
+        eng.gather()
+        torch.cuda.synchronize()
+        c = time.perf_counter()
+        t = torch.tensor([b - a, c - b], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        timeline = {"rollout_ms": t[0].item() * 1e3, "exchange_ms": t[1].item() * 1e3,
+                    "exchange": "global advantage moments all-reduce + compact trajectory all-gather + window rebuild",
+                    "backend": dist.get_backend(),
+                    "timing": "one extra iteration after the timed region, host clock with a device sync between "
+                              "the phases, max over ranks"}
+
     # the last timed iteration's launches: T+1 policy and T env launches, or (fused steps) T fused
     # forward + env-step launches and the bootstrap forward (the same kernel without the env step)
     pol_list, env_list = eng.event_ms()
@@ -615,6 +639,7 @@ def main():
             "env_fused": env_fused,
             "score_pairs": stress,
             "ppo_samples_per_s": ppo,
+            "iteration_timeline": timeline,
             "ppo_samples_per_s_mb64": ppo64,
             "cpu_baseline": cpu,
             "cpu_env_baseline": cpu_env,

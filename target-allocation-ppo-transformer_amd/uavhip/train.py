@@ -19,7 +19,9 @@ Data parallel (world > 1, the same generator seed on every rank), two ways to ho
 Either way one step is FORWARD, an all-reduce of the four loss sums (the clipped value loss picks
 max(...) over the GLOBAL minibatch), BACKWARD (gradients scaled by 1/global minibatch), an
 all-reduce of the flat gradient (1.68 MB over RCCL/xGMI), then the same clip + Adam on every rank:
-the result is the single-GPU step on the global minibatch (fp32 sums in another order).
+the result is the single-GPU step on the global minibatch (fp32 sums in another order). On an RCCL
+group ("nccl") the collectives are captured with the kernels: a data-parallel epoch over gathered
+buffers is one hipGraph replay like a single-GPU one (gloo's collectives run on the host: eager).
 """
 import ctypes
 
@@ -34,17 +36,21 @@ from .policy import layout
 class FusedPPOTrainer:
     def __init__(self, policy, minibatch, lr_actor=None, lr_critic=None, eps_clip=None, max_grad_norm=None,
                  value_coef=0.5, entropy_coef=0.01, betas=(0.9, 0.999), adam_eps=1e-8, world=None, rank=None,
-                 group=None, allreduce=None):
+                 group=None, allreduce=None, data_parallel=None):
         """minibatch: samples per optimizer step over all ranks (each rank runs minibatch / world).
         world / rank default to torch.distributed's (1 / 0 when not initialised); allreduce(t)
-        sums a device tensor over the ranks in place (default: torch.distributed.all_reduce)."""
+        sums a device tensor over the ranks in place (default: torch.distributed.all_reduce).
+        data_parallel: run the phase-split step with its two all-reduces (default: world > 1)."""
         import torch.distributed as tdist
         ddp = tdist.is_available() and tdist.is_initialized()
         self.world = int(world if world is not None else (tdist.get_world_size(group) if ddp else 1))
         self.rank = int(rank if rank is not None else (tdist.get_rank(group) if ddp else 0))
         if minibatch <= 0 or minibatch % (64 * self.world):
             raise ValueError("minibatch must be a positive multiple of 64 x world")
+        self.dp = self.world > 1 if data_parallel is None else bool(data_parallel)
         self.allreduce = allreduce or (lambda t: tdist.all_reduce(t, group=group))
+        # torch.distributed's own all-reduce on an RCCL group can be captured into the epoch graph
+        self.graph_collectives = allreduce is None and ddp and tdist.get_backend(group) == "nccl"
         dev = next(policy.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("FusedPPOTrainer runs on the GPU (HIP) only")
@@ -202,16 +208,28 @@ class FusedPPOTrainer:
         return self.grads
 
     def capture(self):
-        """Capture one epoch (every minibatch step of the current buffer length) into a hipGraph."""
-        if self.world > 1:
-            raise RuntimeError("graph capture is single-GPU; the data-parallel step has collectives between phases")
+        """Capture one epoch (every minibatch step of the current buffer length) into a hipGraph; a
+        data-parallel epoch with its RCCL all-reduces (every rank captures the same sequence, so the
+        replays meet in the same collectives)."""
+        if self.dp and not self.graph_collectives:
+            raise RuntimeError("graph capture of the data-parallel step needs torch.distributed's all-reduce on "
+                               "an RCCL ('nccl') group; gloo collectives run eagerly")
+        if self.dp and self.n_local is not None:
+            raise RuntimeError("set_shard() epochs resize per epoch: they run eagerly")
         steps = self.n // self.global_minibatch
+        if self.dp:  # the communicator is created at its first collective, which must not be in a capture
+            self.allreduce(torch.zeros(1, dtype=torch.float32, device=self.device))
+            torch.cuda.synchronize()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):  # one epoch: every minibatch step
-            for b in range(steps):
-                self.step(_lib.PPO_FULL | self._packed(b), self._rows(self.perm, b))
+        # thread_local: the process group's watchdog thread keeps polling its events during the capture
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local" if self.dp else "global"):
+            for b in range(steps):  # one epoch: every minibatch step
+                if self.dp:
+                    self.ddp_step(self._rows(self.perm, b), self._packed(b))
+                else:
+                    self.step(_lib.PPO_FULL | self._packed(b), self._rows(self.perm, b))
         torch.cuda.current_stream().wait_stream(s)
         self.graphs[steps] = g
         return g
@@ -230,9 +248,9 @@ class FusedPPOTrainer:
             epochs = len(perms)
             if any(p.numel() != self.n for p in perms):
                 raise ValueError(f"perms: every epoch's order must list the {self.n} rows")
-        use_graph = use_graph and self.world == 1
+        use_graph = use_graph and (not self.dp or self.graph_collectives)
         steps = self.n // self.global_minibatch
-        if self.n_local is not None and self.world > 1:
+        if self.n_local is not None and self.dp:
             return self._run_shard(epochs, generator, perms, steps)
         graph = self.graph if use_graph else None
         if use_graph and graph is None and steps > 0:
@@ -247,7 +265,7 @@ class FusedPPOTrainer:
                 cnt += steps
                 continue
             for b in range(steps):
-                if self.world == 1:
+                if not self.dp:
                     self.step(_lib.PPO_FULL | self._packed(b), self._rows(self.perm, b))
                 else:
                     self.ddp_step(self._rows(self.perm, b), self._packed(b))

@@ -180,3 +180,60 @@ def test_world2_sharded_iteration_matches_one_process(name):
                 assert d.max() <= reach, (mname, k, float(d.max()), reach)
         print(f"[{name}] data-parallel ({mname}) vs single-process parameters: max |d| = {worst:.3e} x lr x steps")
     print(f"[{name}] sharded rows per rank and step: {res[0][1][2]}, {res[1][1][2]} (global minibatch {BG})")
+
+
+def _rccl_world1(port, q):
+    """A world-1 RCCL group on the one MI355X: the data-parallel step (FORWARD / all-reduce / BACKWARD
+    / all-reduce / UPDATE) eagerly, then as captured epoch graphs holding the RCCL all-reduces."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "target-allocation-ppo-transformer_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        from uavhip.policy import TransformerActorCritic
+        from uavhip.train import FusedPPOTrainer
+        g = torch.Generator().manual_seed(5)
+        n = 2048
+        states = torch.randn(n, 5, 14, generator=g)
+        states[: n // 8, :3] = 0
+        bufs = (states, torch.randint(0, 2, (n,), generator=g), -0.69 + 0.05 * torch.randn(n, generator=g),
+                torch.randn(n, generator=g), torch.randn(n, generator=g), torch.randn(n, generator=g))
+        out = []
+        for use_graph in (False, True):
+            torch.manual_seed(0)
+            tr = FusedPPOTrainer(TransformerActorCritic().cuda(), 256, data_parallel=True)
+            assert tr.dp and tr.graph_collectives
+            tr.set_buffers(*(b.cuda() for b in bufs))
+            st = tr.run(epochs=2, generator=torch.Generator().manual_seed(1), use_graph=use_graph)
+            torch.cuda.synchronize()
+            out.append((tr.params.cpu().numpy(), tr.adam_m.cpu().numpy(), tr.adam_v.cpu().numpy(), st,
+                        tr.graph is not None))
+        q.put(out)
+    except BaseException as exc:  # report instead of hanging the parent on q.get
+        q.put(repr(exc))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_epoch_graph_matches_eager_data_parallel_steps():
+    """The data-parallel epoch captured with its RCCL all-reduces (what bench.py replays at N > 1)
+    equals the eager phase-split steps bit for bit, on a world-1 RCCL group (RCCL puts one rank per
+    device; the collective count and order per epoch are the N-GPU run's)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_world1, args=(_free_port(), q))
+    p.start()
+    out = q.get(timeout=300)
+    p.join(timeout=60)
+    assert not isinstance(out, str), out
+    assert p.exitcode == 0
+    (pe, me, ve, se, ge), (pg, mg, vg, sg, gg) = out
+    assert not ge and gg  # eager, then a captured epoch graph
+    assert se == sg and se[3] == 2 * 2048 // 256
+    for a, b in ((pe, pg), (me, mg), (ve, vg)):
+        assert np.array_equal(a, b)
