@@ -64,6 +64,15 @@ for i in range(0 if ENV else 5):
 torch.cuda.synchronize()
 buf = np.zeros(256 * 2 * 64, np.uint64)
 assert fn(buf.ctypes.data, buf.size) == 0
+if os.environ.get("WAVES") == "8":  # a TRACE_WAVES=8 build: [64 workgroups][8 waves][slots]
+    t8 = buf.reshape(64, 8, 64).astype(np.int64)
+    slots = sorted((k for k in NAMES if (t8[:, :, k] != 0).all()),
+                   key=lambda k: np.median(t8[:, 0, k] - t8[:, 0, 0]))
+    rel = t8 - t8[:, 0:1, 0:1]  # every wave against wave 0's block start
+    print(f"B={B}; median cycles since block start, waves 0-7 (64 workgroups)")
+    for k in slots:
+        print(f"{k:3d} {NAMES[k]:18s} " + " ".join(f"{int(np.median(rel[:, w, k])):7d}" for w in range(8)))
+    sys.exit(0)
 t = buf.reshape(256, 2, 64).astype(np.int64)
 slots = sorted((k for k in NAMES if (t[:, 0, k] != 0).all()), key=lambda k: np.median(t[:, 0, k] - t[:, 0, 0]))
 base = t[:, :, 0:1]

@@ -63,11 +63,19 @@ constexpr bool kExpNoEnv = false;
 #endif
 constexpr int kTraceSlots = 64;
 __device__ unsigned long long g_ptrace[256 * 2 * kTraceSlots];
+#ifdef UAVHIP_TRACE_ALLWAVES  // make TRACE=1 TRACE_WAVES=8: all 8 waves of the first 64 workgroups
+#define PTR(id)                                                                                  \
+    do {                                                                                         \
+        if ((tid_x() & 63) == 0 && blockIdx.x < 64)                                          \
+            g_ptrace[(blockIdx.x * 8 + (tid_x() >> 6)) * kTraceSlots + (id)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
 #define PTR(id)                                                                                  \
     do {                                                                                         \
         if ((tid_x() & 255) == 0 && blockIdx.x < 256)                                        \
             g_ptrace[(blockIdx.x * 2 + (tid_x() >> 8)) * kTraceSlots + (id)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+#endif
 __device__ unsigned long long g_btrace[256 * 2 * kTraceSlots];
 #define BTR(id)                                                                                  \
     do {                                                                                         \
@@ -664,16 +672,19 @@ template <int trunk, bool TR = false, int MODE = kEmbH, bool PL = false>
 __device__ void embed_apply(TID_F Smem& sm, const EmbPre& ep, float* e_out = nullptr, float* h_out = nullptr, int b0 = 0) {
     const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
     constexpr int NT = MODE == kEmbRows ? S - 1 : S;
+    // the ring forward's actor (its only layer is pruned to position 4): positions 0-3 come from the
+    // ring rows and only position 4 is a residual, so only its embedding is formed
+    constexpr int CT0 = MODE == kEmbSplit && trunk == kActorTrunk ? S - 1 : 0;
     f32x4 acc[NT];
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct) {
+    for (int ct = CT0; ct < NT; ++ct) {
         const f32x4 b = *reinterpret_cast<const f32x4*>(sm.x + (ct * SPW + i16) * LDX + 4 * g);
         acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(ep.a[j], b[j], acc[ct], 0, 0, 0);
     }
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct) {
+    for (int ct = CT0; ct < NT; ++ct) {
         f32x4 e = acc[ct] + ep.bb;
         e.x = fmaxf(e.x, 0.f); e.y = fmaxf(e.y, 0.f); e.z = fmaxf(e.z, 0.f); e.w = fmaxf(e.w, 0.f);
         const int o = (ct * SPW + i16) * LDH + 16 * wv + 4 * g;
@@ -753,7 +764,7 @@ __device__ __forceinline__ KvPre<trunk, layer, TR, SP> kv_prefetch(TID_F const f
     else
         return prefetch<2>(TID_C P + kOffs.o[layer_param(trunk, layer, INW)], D, kv_row(wv, 0), 0);
 }
-// The training forward's split switch (k_policy_forward<true>; the K7 position-split kernels stay f32).
+// The training forward's split switch (k_policy_forward<true>; the K7 kernels: kPsSplit below).
 constexpr bool kTrainSplit = true;
 
 // PSX (position split, the small-minibatch training step): a full (unpruned) layer computed for

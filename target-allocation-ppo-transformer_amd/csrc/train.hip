@@ -1,8 +1,10 @@
 // train.hip -- K5: one clipped-PPO minibatch step (agents/ppo.py:96-169) of TransformerActorCritic
-// (networks/transformer_net.py) on gfx950, fp32 throughout.
+// (networks/transformer_net.py) on gfx950, fp32-accurate throughout: every encoder GEMM (forward,
+// input gradients, weight gradients) as split products on the f16 MFMA.
 //
 // Layout: a minibatch of Bm samples is R = 5 Bm token rows, row = b * 5 + s, features contiguous.
-// One step is 7 launches on one stream (graph-capturable: no host sync, no allocation):
+// One step is 5-7 launches on one stream (graph-capturable: no host sync, no allocation); minibatches
+// of <= 256 samples run the position split instead (K7, policy.hip: 3 forward + 3 backward launches):
 //    forward   k_policy_forward<TR> (policy.hip, the rollout's fused kernel writing activations),
 //              with the heads and per-workgroup loss partials, then k_loss_sums (the four sums).
 //              Minibatches of <= 2048 samples (2 Bm/16 workgroups fit one per CU) run trunk-split:
@@ -10,8 +12,8 @@
 //              until the loss), then k_loss_partials; the backward splits the same way
 //    backward  k_policy_backward (K6, policy.hip: loss and head gradients, dX of the encoder
 //              layers and embeddings, one workgroup per 16 samples), then every weight
-//              gradient dW[out][in] = sum_row dY[row][out] X[row][in] as one stream-K fp32 MFMA
-//              launch (wgrad.hpp: per-workgroup partial tiles), and one k_reduce_grads over all
+//              gradient dW[out][in] = sum_row dY[row][out] X[row][in] as one stream-K launch of
+//              three-plane split products (wgrad.hpp: per-workgroup partial tiles), and one k_reduce_grads over all
 //              partials (weight tiles, K6's bias / LayerNorm / embedding / head partials)
 //    update    k_adam (clip_grad_norm_ + Adam on the g^2 block partials of k_reduce_grads, or of
 //              k_grad_norm after a data-parallel all-reduce)
