@@ -981,7 +981,11 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     HPre<2> w1a;
     if constexpr (TR) store_rows_planes(TID_C cp, io.o, D, 0, D, t0, b0, last, t1);  // attention output
     {
-        const f32x4 bo4 = ln_bias(TID_C bo);
+        // the epilogue's bias and LN1's weight / bias ahead of the GEMM: issued after it, their L2
+        // round trip (~2 k cycles with every CU reading the same lines) outlasted the partials +
+        // barrier + statistics in front of their first use
+        const LnPar lp = ln_load(TID_C ln_bias(TID_C bo), P + kOffs.o[layer_param(trunk, layer, N1W)],
+                                 P + kOffs.o[layer_param(trunk, layer, N1B)]);
         f32x4 acc[CT];
         {  // out-projection from the attention output's planes
             f32x4 hi[CT], lo[CT];
@@ -992,7 +996,6 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
             for (int ct = 0; ct < CT; ++ct) acc[ct] = hi[ct] + lo[ct] * kLoScale;
         }
         PTR(tb + 7);
-        const LnPar lp = ln_load(TID_C bo4, P + kOffs.o[layer_param(trunk, layer, N1W)], P + kOffs.o[layer_param(trunk, layer, N1B)]);
         w1a = hprefetch<2>(TID_C P, s1, D, 16 * wv, 0);
         const LnOut lo1{io.xhat1, io.h1, io.rstd1, b0, last};
         if constexpr (res_ctx) {
@@ -1029,14 +1032,14 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
         store_rows_planes(TID_C bp, io.u, FF, 0, D, t0, b0, last, t1);
         store_rows_planes(TID_C cp, io.u, FF, D, D, t0, b0, last, t1);
     }
-    const f32x4 b24 = ln_bias(TID_C b2);
+    const LnPar lp2 = ln_load(TID_C ln_bias(TID_C b2), P + kOffs.o[layer_param(trunk, layer, N2W)],
+                              P + kOffs.o[layer_param(trunk, layer, N2B)]);  // ahead of the GEMM, as LN1's
     f32x4 hi[CT], lo[CT];
     zero(hi);
     zero(lo);
     hgemm_tile<CT, 2>(TID_C hi, lo, w2a, P, s2, FF, 16 * wv, 0, bp, t0);
     hgemm_tile<CT, 2>(TID_C hi, lo, w2b, P, s2, FF, 16 * wv, 128, cp, t0);
     PTR(tb + 12);
-    const LnPar lp2 = ln_load(TID_C b24, P + kOffs.o[layer_param(trunk, layer, N2W)], P + kOffs.o[layer_param(trunk, layer, N2B)]);
     f32x4 acc2[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc2[ct] = hi[ct] + lo[ct] * kLoScale;
