@@ -246,13 +246,21 @@ __device__ __forceinline__ void zero(f32x4 (&acc)[CT]) {
 // (scripts/micro/split_gemm.hip: max error 0.42x the f32 MFMA's on the FFN1 shape, 3.6x faster).
 // Weights: the packed buffer's split copies (policy_layout.hpp kSplitParam / kSplitOffs), blocks of
 // 16 rows x 32 k = 1 KiB of w1 then 1 KiB of w2, lane l = r%16 + 16 ((k%32)/8) holding k%8.
-// Activations: two planes of [tok][LDP halves] in LDS, plane 2 at +TOK * LDP; lane (i16, g) reads
-// 8 halves of token i16 per plane with one ds_read_b128 (272-B rows: conflict-free).
+// Activations: both planes of a token in one LDS row, [tok][plane 1: 128 halves | plane 2: 128 |
+// pad 16] (plane 2 at + kPlane); lane (i16, g) reads 8 halves of token i16 per plane with one
+// ds_read_b128. The 544-B rows put token i16 at bank offset 8 i16 (mod 64), conflict-free for
+// ds_read_b128's lane groups (MI355X_MICROARCH.md LDS table) like the fp32 [tok][136] rows.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-constexpr int LDP = D + 8;           // halves per plane row
-constexpr int kPlane = TOK * LDP;    // halves per plane: two planes fill a [TOK][LDH] fp32 buffer
-static_assert(2 * kPlane * 2 == TOK * LDH * 4, "the two planes of an activation replace its fp32 copy");
+#if defined(UAVHIP_EXP) && UAVHIP_EXP == 4  // A/B: the round-3 layout, plane 2 after all rows of plane 1
+constexpr int LDP = D + 8;
+constexpr int kPlane = TOK * LDP;
+#else
+constexpr int LDP = 2 * D + 16;      // halves per token row (both planes + pad)
+constexpr int kPlane = D;            // plane 2 within the row
+#endif
+static_assert(TOK * LDP * 2 <= TOK * LDH * 4 && kPlane + D <= LDP + (LDP == D + 8 ? TOK * LDP : 0),
+              "the two planes of an activation replace its fp32 copy");
 constexpr float kLoScale = 1.0f / 2048.0f;
 
 template <int D_>
