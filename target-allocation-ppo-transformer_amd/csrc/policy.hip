@@ -2157,15 +2157,19 @@ __device__ __forceinline__ void attn_bwd_load(AttnPre& a, const float* __restric
         if (qsel >= 0 ? i == qsel : (!last || i == S - 1)) a.q[i] = ld2(qkv + (rb + i) * 3 * D + col);
 }
 // SP (split-product backward): dq | dk | dv go to sm.big as the two fp16 planes of the W_in^T GEMM's
-// operand ([tok][LDB halves], plane 2 at + TOK LDB) and, exact, straight to the dqkv rows (dqkv != nullptr).
+// operand -- both planes of a token in one row, [tok][plane 1: 192 halves | plane 2: 192 | pad 16]
+// (800-B rows: token i16 at bank offset 8 i16, conflict-free ds_read_b128 operand reads) -- and,
+// exact, straight to the dqkv rows (dqkv != nullptr).
+constexpr int kLdbP = 2 * LDB, kPlaneB = 3 * 64;  // halves per row, plane 2 within the row
+static_assert(kPlaneB + 3 * 64 <= kLdbP, "both planes in an LDB row");
 __device__ __forceinline__ void attn_out2(Smem& sm, float* __restrict__ dqkv, int b0, int tok, int col, int part,
                                           int c, f32x2 v, bool sp, float* __restrict__ kvc = nullptr, int kblk = 0) {
     if (sp) {
-        _Float16* bp = reinterpret_cast<_Float16*>(sm.big) + tok * LDB + part * 64 + col;
+        _Float16* bp = reinterpret_cast<_Float16*>(sm.big) + tok * kLdbP + part * 64 + col;
         const _Float16 a0 = (_Float16)v.x, a1 = (_Float16)v.y;
         typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
         *reinterpret_cast<f16x2*>(bp) = f16x2{a0, a1};
-        *reinterpret_cast<f16x2*>(bp + TOK * LDB) = f16x2{(_Float16)((v.x - (float)a0) * 2048.f),
+        *reinterpret_cast<f16x2*>(bp + kPlaneB) = f16x2{(_Float16)((v.x - (float)a0) * 2048.f),
                                                           (_Float16)((v.y - (float)a1) * 2048.f)};
         if (kvc && part > 0)  // position split: this query position's share of every position's dk / dv
             st2(kvc + ((size_t)kblk * TOK + tok) * 2 * D + (part - 1) * D + 64 * c + col, v);
@@ -2420,14 +2424,14 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
         const HPre<2> pw2 = hprefetch<2>(PT, sWin, 3 * D, 16 * wv, 2 * D + 64 * c);
         if (last) {  // dq is zero outside the query tile: W_in,q^T dq only for column tile 4
             f32x4 h1[1] = {hi[S - 1]}, l1[1] = {lo[S - 1]};
-            hgemm_tile<1, 2, 2, LDB, TOK * LDB>(h1, l1, pw, PT, sWin, 3 * D, 16 * wv, 64 * c, bp, (S - 1) * SPW);
+            hgemm_tile<1, 2, 2, kLdbP, kPlaneB>(h1, l1, pw, PT, sWin, 3 * D, 16 * wv, 64 * c, bp, (S - 1) * SPW);
             hi[S - 1] = h1[0];
             lo[S - 1] = l1[0];
         } else {
-            hgemm_tile<S, 2, 2, LDB, TOK * LDB>(hi, lo, pw, PT, sWin, 3 * D, 16 * wv, 64 * c, bp, 0);
+            hgemm_tile<S, 2, 2, kLdbP, kPlaneB>(hi, lo, pw, PT, sWin, 3 * D, 16 * wv, 64 * c, bp, 0);
         }
-        hgemm_tile<S, 2, 2, LDB, TOK * LDB>(hi, lo, pw1, PT, sWin, 3 * D, 16 * wv, D + 64 * c, bp + 64, 0);
-        hgemm_tile<S, 2, 2, LDB, TOK * LDB>(hi, lo, pw2, PT, sWin, 3 * D, 16 * wv, 2 * D + 64 * c, bp + 128, 0);
+        hgemm_tile<S, 2, 2, kLdbP, kPlaneB>(hi, lo, pw1, PT, sWin, 3 * D, 16 * wv, D + 64 * c, bp + 64, 0);
+        hgemm_tile<S, 2, 2, kLdbP, kPlaneB>(hi, lo, pw2, PT, sWin, 3 * D, 16 * wv, 2 * D + 64 * c, bp + 128, 0);
         if (c == 0) attn_bwd_load<last>(ap, io.qkv, 1, b0, qsel);  // behind every weight load of the chunk
         if (c == 0) __syncthreads();  // big is rewritten by chunk 1
         BTR(TB + 12 + 2 * c);
@@ -2459,7 +2463,7 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
 // SP (kBwdFull only): every dX GEMM as split products on the f16 MFMA -- A = the transposed split
 // copies (PT + kTSplit), B = planes the producing epilogue writes: df (LN2 backward -> sm.ctx), du
 // (-> sm.big / sm.h), dz1 (LN1 backward -> sm.h), dq | dk | dv (attention backward -> sm.big, rows of
-// LDB halves); the residual terms read back from planes are x1 + 2^-11 x2.
+// kLdbP halves, attn_out2); the residual terms read back from planes are x1 + 2^-11 x2.
 template <int trunk, int layer, bool last, int TB, class F = NoHook, int MODE = kBwdFull, bool SP = false>
 __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __restrict__ PT, const BwdLayerIO& io,
                           int b0, EmbBwdPre* ep = nullptr, const float* e_emb = nullptr, const float* xg = nullptr,
@@ -3128,7 +3132,8 @@ __global__ __launch_bounds__(NTHR) void k_ps_b1(const float* __restrict__ P, con
 
 // The 16 [dq | dk | dv] rows of position s -> sm.big rows p (stride LDQ); with_q = false: a pruned
 // layer off its query position (dq never written there: zero)
-// (kPsSplit: as the two fp16 planes of ps_dx's split products, rows of LDQ halves, plane 2 at + SPW LDQ)
+// (kPsSplit: as the two fp16 planes of ps_dx's split products, both in one row of 2 LDQ halves,
+// plane 2 at + 3 D: conflict-free ds_read_b128 like the fp32 LDQ rows)
 __device__ __forceinline__ void ps_big_store(Smem& sm, int p, int q, const f32x4 v) {
     if constexpr (kPsSplit) {
         _Float16* bp = reinterpret_cast<_Float16*>(sm.big);
@@ -3138,8 +3143,8 @@ __device__ __forceinline__ void ps_big_store(Smem& sm, int p, int q, const f32x4
             a[j] = (_Float16)v[j];
             b[j] = (_Float16)((v[j] - (float)a[j]) * 2048.f);
         }
-        *reinterpret_cast<f16x4*>(bp + p * LDQ + 4 * q) = a;
-        *reinterpret_cast<f16x4*>(bp + SPW * LDQ + p * LDQ + 4 * q) = b;
+        *reinterpret_cast<f16x4*>(bp + p * 2 * LDQ + 4 * q) = a;  // [p][plane 1 | plane 2 | pad]
+        *reinterpret_cast<f16x4*>(bp + p * 2 * LDQ + 3 * D + 4 * q) = b;
     } else {
         st4(sm.big + p * LDQ + 4 * q, v);
     }
@@ -3167,7 +3172,7 @@ __device__ void ps_dx(Smem& sm, const float* __restrict__ WinT, bool with_q, con
 #pragma unroll
         for (int part = 0; part < 3; ++part) {
             if (part == 0 && !with_q) continue;
-            hgemm_tile<1, 2, 4, LDQ, SPW * LDQ>(acc, lo, hprefetch<2>(WinT, kTSplit, 3 * D, 16 * wv, part * D), WinT,
+            hgemm_tile<1, 2, 4, 2 * LDQ, 3 * D>(acc, lo, hprefetch<2>(WinT, kTSplit, 3 * D, 16 * wv, part * D), WinT,
                                                 kTSplit, 3 * D, 16 * wv, part * D, bp + part * D, 0);
         }
         acc[0] += lo[0] * kLoScale;
