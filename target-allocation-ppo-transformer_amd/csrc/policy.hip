@@ -261,6 +261,10 @@ constexpr int kPlane = D;            // plane 2 within the row
 #endif
 static_assert(TOK * LDP * 2 <= TOK * LDH * 4 && kPlane + D <= LDP + (LDP == D + 8 ? TOK * LDP : 0),
               "the two planes of an activation replace its fp32 copy");
+// Offset of (token, column) in a plane image: the 16-B chunk index XOR-swizzled by bit 2 of the token,
+// so the epilogues' ds_write_b64 (16 consecutive tokens per lane group) are at most 2-way conflicted
+// (4-way without it) while the GEMMs' ds_read_b128 stay conflict-free
+__device__ __forceinline__ int psw(int tok, int col) { return tok * LDP + (col ^ (((tok >> 2) & 1) << 3)); }
 constexpr float kLoScale = 1.0f / 2048.0f;
 
 template <int D_>
@@ -293,7 +297,8 @@ __device__ __forceinline__ void hgemm_tile(TID_F f32x4 (&hi)[CT], f32x4 (&lo)[CT
     const f16x8* wp = hfrag_ptr(TID_C P, soff, K, row, kw0);
     const _Float16* xp[CT];
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) xp[ct] = X + (xtok0 + 16 * ct + i16) * LDX_ + 8 * g;
+    for (int ct = 0; ct < CT; ++ct)  // the LDP images: psw's swizzle (xtok0 is a multiple of 16)
+        xp[ct] = X + (xtok0 + 16 * ct + i16) * LDX_ + (LDX_ == LDP ? 8 * (g ^ ((i16 >> 2) & 1)) : 8 * g);
     f16x8 a1[NKB], a2[NKB], b1[2][CT], b2[2][CT];
 #pragma unroll
     for (int p = 0; p < D_; ++p) {
@@ -328,7 +333,7 @@ __device__ __forceinline__ void hgemm_tile(TID_F f32x4 (&hi)[CT], f32x4 (&lo)[CT
         __builtin_amdgcn_sched_barrier(0);
     }
 }
-// v -> its two planes at Y + tok * LDP + c (plane 2 at + kPlane): one 8-byte store per plane
+// v -> its two planes at Y + psw(tok, c) (plane 2 at + kPlane): one 8-byte store per plane
 __device__ __forceinline__ void hsplit_store(_Float16* Y, int o, const f32x4 v) {
     f16x4 v1, v2;
 #pragma unroll
@@ -350,7 +355,7 @@ __device__ __forceinline__ void hstore_tile(TID_F const f32x4 (&hi)[CT], const f
         if (RELU) {
             v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         }
-        hsplit_store(Y, (ytok0 + 16 * ct + i16) * LDP + ycol + 4 * g, v);
+        hsplit_store(Y, psw((ytok0 + 16 * ct + i16), ycol + 4 * g), v);
     }
 }
 
@@ -498,7 +503,7 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
         }
         const f32x4 xh = (v[ct] - mean) * rs;
         const f32x4 out = xh * ww + lb;
-        if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.h), tok * LDP + f0, out);
+        if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.h), psw(tok, f0), out);
         else *reinterpret_cast<f32x4*>(sm.h + tok * LDH + f0) = out;
         if constexpr (ROW4) {
             if (ct == CT - 1) *reinterpret_cast<f32x4*>(sm.ctx + (tok - (S - 1) * SPW) * LDH + f0) = out;
@@ -582,7 +587,7 @@ __device__ __forceinline__ void attention_full_store(TID_F Smem& sm, int c, cons
     for (int qi = 0; qi < 3; ++qi) {
         if (qi < nq) {
             const int ti = (qs0 + qi) * SPW + p;
-            if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), ti * LDP + 4 * c * HD + d0, o[qi]);
+            if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw(ti, 4 * c * HD + d0), o[qi]);
             else *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o[qi];
         }
     }
@@ -632,7 +637,7 @@ __device__ __forceinline__ void attention_task(TID_F Smem& sm, int task, int qs0
 }
 template <bool PLANES>
 __device__ __forceinline__ void attention_out(TID_F Smem& sm, int c, int ti, int d0, const f32x4 o) {
-    if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), ti * LDP + 4 * c * HD + d0, o);
+    if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw(ti, 4 * c * HD + d0), o);
     else *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o;
 }
 template <bool PLANES = false>
@@ -698,12 +703,12 @@ __device__ void embed_apply(TID_F Smem& sm, const EmbPre& ep, float* e_out = nul
         const int o = (ct * SPW + i16) * LDH + 16 * wv + 4 * g;
         constexpr bool ring_planes = split_slot(layer_param(trunk, 0, INW)) >= 0;  // the ring GEMM's operand
         if ((MODE == kEmbRows || (MODE == kEmbSplit && ct == S - 1)) && ring_planes)
-            hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), (ct * SPW + i16) * LDP + 16 * wv + 4 * g, e);
+            hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((ct * SPW + i16), 16 * wv + 4 * g), e);
         else if (MODE == kEmbRows || (MODE == kEmbSplit && ct == S - 1)) *reinterpret_cast<f32x4*>(sm.ctx + o) = e;
         if (MODE == kEmbRows) continue;
         const f32x4 v = e + ep.pp[ct];
         *reinterpret_cast<f32x4*>(sm.h + o) = v;
-        if constexpr (PL) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), (ct * SPW + i16) * LDP + 16 * wv + 4 * g, v);
+        if constexpr (PL) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((ct * SPW + i16), 16 * wv + 4 * g), v);
         if (TR && !kExpNoStore) {
             const size_t r = (size_t)trow(ct * SPW + i16, b0);
             *reinterpret_cast<f32x4*>(e_out + r * D + 16 * wv + 4 * g) = e;
@@ -801,8 +806,8 @@ __device__ __forceinline__ void store_rows_planes(TID_F const _Float16* src, flo
     const int n4 = ncols / 4, items = (t1 - t0) * n4;
     for (int i = TIDX(); i < items; i += NTHR) {
         const int tok = t0 + i / n4, q = i % n4;
-        const f16x4 x1 = *reinterpret_cast<const f16x4*>(src + tok * LDP + 4 * q);
-        const f16x4 x2 = *reinterpret_cast<const f16x4*>(src + kPlane + tok * LDP + 4 * q);
+        const f16x4 x1 = *reinterpret_cast<const f16x4*>(src + psw(tok, 4 * q));
+        const f16x4 x2 = *reinterpret_cast<const f16x4*>(src + kPlane + psw(tok, 4 * q));
         f32x4 v;
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = (float)x1[j] + (float)x2[j] * kLoScale;
@@ -1293,7 +1298,7 @@ __device__ __forceinline__ void hgemm_rows(TID_F f32x4 (&hi)[R], f32x4 (&lo)[R],
                                            const _Float16* X, int xtok0, F&& issued) {
     constexpr int NKB = D / 32;
     const int l = LANE(), i16 = l & 15, g = l >> 4;
-    const _Float16* xp = X + (xtok0 + i16) * LDP + 8 * g;
+    const _Float16* xp = X + (xtok0 + i16) * LDP + 8 * (g ^ ((i16 >> 2) & 1));  // psw's swizzle
     f16x8 a1[NKB][R], a2[NKB][R], b1[NKB], b2[NKB];
 #pragma unroll
     for (int p = 0; p < D_; ++p)
@@ -2091,8 +2096,8 @@ __device__ void ln_bwd_lds(const float* src, float* dst, const LnBwdPre& a, floa
         const float m2 = row16_sum(hsum(gw0 * x0) + hsum(gw1 * x1)) * (1.0f / D);
         const f32x4 d0 = rs * (gw0 - m1 - x0 * m2), d1 = rs * (gw1 - m1 - x1 * m2);
         if constexpr (PL) {
-            hsplit_store(reinterpret_cast<_Float16*>(dst), tok * LDP + f0, d0);
-            hsplit_store(reinterpret_cast<_Float16*>(dst), tok * LDP + f0 + 4, d1);
+            hsplit_store(reinterpret_cast<_Float16*>(dst), psw(tok, f0), d0);
+            hsplit_store(reinterpret_cast<_Float16*>(dst), psw(tok, f0 + 4), d1);
         } else {
             st4(dst + tok * LDH + f0, d0);
             st4(dst + tok * LDH + f0 + 4, d1);
@@ -2348,7 +2353,7 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
             d.x = u.x > 0.f ? d.x : 0.f; d.y = u.y > 0.f ? d.y : 0.f;
             d.z = u.z > 0.f ? d.z : 0.f; d.w = u.w > 0.f ? d.w : 0.f;
             st4(io.du + r * FF + row + 4 * g, d);
-            hsplit_store(dstp, tok * LDP + fo, d);
+            hsplit_store(dstp, psw(tok, fo), d);
             sd += d;
         }
 #pragma unroll
@@ -2367,7 +2372,7 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
         hgemm_tile<CTQ, 2>(hi, lo, pa, PT, sW1, FF, 16 * wv, 0, bp, qtok0);
         hgemm_tile<CTQ, 2>(hi, lo, hprefetch<2>(PT, sW1, FF, 16 * wv, 128), PT, sW1, FF, 16 * wv, 128, hp, qtok0);
 #pragma unroll
-        for (int ct = 0; ct < CTQ; ++ct) hi[ct] = hi[ct] + lo[ct] * kLoScale + unsplit(cp, (qtok0 + 16 * ct + i16) * LDP + fo);
+        for (int ct = 0; ct < CTQ; ++ct) hi[ct] = hi[ct] + lo[ct] * kLoScale + unsplit(cp, psw((qtok0 + 16 * ct + i16), fo));
         __syncthreads();
 #pragma unroll
         for (int ct = 0; ct < CTQ; ++ct) st4(sm.ctx + (qtok0 + 16 * ct + i16) * LDH + fo, hi[ct]);
@@ -2444,7 +2449,7 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
 #pragma unroll
     for (int ct = 0; ct < S; ++ct) {
         const int tok = 16 * ct + i16;
-        res[ct] = tok >= qtok0 ? unsplit(hp, tok * LDP + fo) : f32x4{0.f, 0.f, 0.f, 0.f};
+        res[ct] = tok >= qtok0 ? unsplit(hp, psw(tok, fo)) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     __syncthreads();
 #pragma unroll
@@ -2925,7 +2930,7 @@ __device__ void ps_embed(Smem& sm, const float* __restrict__ P, float* __restric
     e.x = fmaxf(e.x, 0.f); e.y = fmaxf(e.y, 0.f); e.z = fmaxf(e.z, 0.f); e.w = fmaxf(e.w, 0.f);
     const f32x4 v = e + pp;
     st4(sm.h + (s * SPW + i16) * LDH + 16 * wv + 4 * g, v);
-    if constexpr (PL) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), (s * SPW + i16) * LDP + 16 * wv + 4 * g, v);
+    if constexpr (PL) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((s * SPW + i16), 16 * wv + 4 * g), v);
     const size_t r = (size_t)trow(s * SPW + i16, b0);
     st4(e_out + r * D + 16 * wv + 4 * g, e);
     st4(h_out + r * D + 16 * wv + 4 * g, v);
