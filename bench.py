@@ -328,13 +328,26 @@ def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
         else:
             impl = ("HIP training step, data parallel: forward / all-reduce loss sums / backward / "
                     "all-reduce grads / clip+Adam per global minibatch")
+            graphed = False
             if trainer.graph_collectives:  # RCCL: the epoch with its all-reduces as one graph (not timed)
-                trainer.capture()
+                try:
+                    trainer.capture()
+                    graphed = True
+                except Exception as exc:  # every rank must take the same path: agree below
+                    print(f"[bench] rank {dist.get_rank()}: data-parallel graph capture failed: {exc!r}",
+                          file=sys.stderr)
+                ok = torch.tensor([1 if graphed else 0], device=dev, dtype=torch.int32)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                graphed = bool(ok.item())
+                if not graphed:
+                    trainer.graphs = {}
+            if graphed:
                 impl += ", one hipGraph replay per epoch with the RCCL all-reduces captured"
             else:
                 impl += f", eager ({dist.get_backend()} collectives)"
         gen = torch.Generator().manual_seed(1234)  # same minibatch order on every rank
-        run = lambda: trainer.run(generator=gen)  # noqa: E731
+        use_graph = world == 1 or bool(trainer.graphs)
+        run = lambda: trainer.run(generator=gen, use_graph=use_graph)  # noqa: E731
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
