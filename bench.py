@@ -5,7 +5,8 @@
 One timed "step" = one rollout iteration per rank: T (=64) x {fused policy forward (fp32-accurate MFMA) ->
 on-device sample -> fused env step (fp64)} over E envs -- all T steps in ONE k_rollout_steps launch
 (--per-step-launch: one launch per step) -- a bootstrap value pass, GAE + advantage normalisation,
-and with N > 1 GPUs the RCCL all-gather of the trajectories.
+and with N > 1 GPUs the all-gather of the trajectories: pipelined peer-to-peer copies
+beside the next rollout, or one RCCL all-gather after each rollout (--rccl-gather / fallback).
 value = E * T * K * N / max-over-ranks wall time. Inputs (scenes, windows) are resident in HBM.
 
 Also reported (same JSON line):
@@ -167,6 +168,9 @@ def parse():
     ap.add_argument("--ppo-impl", choices=["fused", "torch-graph", "torch-eager"], default="fused",
                     help="PPO update implementation timed for ppo_samples_per_s")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rccl-gather", action="store_true",
+                    help="N > 1: the exchange as one RCCL all-gather after each rollout instead of the pipelined "
+                         "peer-to-peer copies beside the next rollout (uavhip.dist.IpcAllGather)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--eager", action="store_true", help="launch kernels eagerly instead of replaying a hipGraph")
     ap.add_argument("--unfused", action="store_true",
@@ -472,19 +476,46 @@ def main():
             eng.graph = None
             mode = "eager launches (graph capture failed)"
 
+    # N > 1: the exchange pipelined one iteration behind the rollout (peer-to-peer copies out of
+    # IPC-mapped buffers on a side stream, beside the next rollout; host sync over a gloo group), or
+    # one RCCL all-gather after each rollout (--rccl-gather, or when the IPC mapping fails on any rank)
+    xchg, xchg_err = None, None
+    if dist is not None and not args.rccl_gather:
+        from uavhip.dist import IpcAllGather, compact_floats
+        host_group = dist.new_group(backend="gloo")
+        try:
+            xchg = IpcAllGather(compact_floats(T, E), dev, host_group)
+        except Exception as exc:
+            xchg_err = repr(exc)
+        ok = torch.tensor([0 if xchg is None else 1], device=dev, dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if not ok.item():
+            xchg = None
+            xchg_err = xchg_err or "the IPC mapping failed on another rank"
+
     def iteration(eager=False):
         eng.collect(eager=eager)
         if dist is not None:
-            eng.gather()
+            if xchg is None:
+                eng.gather()
+                return
+            if xchg.pending is not None:
+                eng.gather_finish(xchg)  # the previous iteration's exchange, beside this rollout
+            eng.gather_submit(xchg)
 
     for _ in range(args.warmup):
         iteration()
+    if xchg is not None and xchg.pending is not None:
+        eng.gather_finish(xchg)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         iteration(eager=(i == args.steps - 1))
+    if xchg is not None:  # the last iteration's exchange (exposed: inside the timed region)
+        eng.gather_finish(xchg)
+        eng.gather()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -497,6 +528,21 @@ def main():
     env_steps = E * T * args.steps * world
     value = env_steps / elapsed
 
+    exchange = None
+    if dist is not None:  # the exchange kind, and the pipelined copies checked against RCCL's all-gather
+        exchange = {"kind": "rccl all-gather after each rollout" if xchg is None else
+                    "peer-to-peer copies out of IPC-mapped buffers, pipelined beside the next rollout",
+                    "fallback_reason": xchg_err, "check": None}
+        if xchg is not None:
+            from uavhip.dist import all_gather_rows, pack_compact
+            tr_ = eng.traj
+            ref = all_gather_rows(pack_compact(tr_.obs, tr_.actions, tr_.logp, tr_.values, tr_.ret, tr_.adv,
+                                               tr_.dones).view(1, -1))
+            same = torch.tensor([int(torch.equal(ref, xchg.recv[(xchg.k - 1) & 1]))], device=dev, dtype=torch.int32)
+            dist.all_reduce(same, op=dist.ReduceOp.MIN)
+            exchange["check"] = bool(same.item())
+            exchange["check_what"] = "the last timed iteration's gathered payloads == RCCL all_gather of the same payloads, bitwise, every rank"
+
     timeline = None
     if dist is not None:  # one more iteration, untimed, with the phases separated: rollout | exchange
         torch.cuda.synchronize()
@@ -505,6 +551,9 @@ def main():
         eng.collect()
         torch.cuda.synchronize()
         b = time.perf_counter()
+        if xchg is not None:
+            eng.gather_submit(xchg)
+            eng.gather_finish(xchg)
         eng.gather()
         torch.cuda.synchronize()
         c = time.perf_counter()
@@ -601,7 +650,8 @@ def main():
             "data": "synthetic (on-device Philox scenes, "
             "random-init policy, actions sampled from the policy)",
             "config": {"workload": "BASELINE configs[2]: full rollout (policy fwd -> sample -> env.step) + GAE"
-                       + (" + RCCL trajectory all-gather" if world > 1 else ""),
+                       + (" + trajectory all-gather (" + ("RCCL" if xchg is None else "pipelined peer copies")
+                          + ")" if world > 1 else ""),
                        "envs_per_gpu": E, "uavs": args.uavs, "targets": args.targets, "horizon": T,
                        "env_steps_per_step": E * T * world, "parallelism": f"env-sharded x{world}",
                        "full_reset_period": 200, "launch": mode},
@@ -653,6 +703,7 @@ def main():
             "score_pairs": stress,
             "ppo_samples_per_s": ppo,
             "iteration_timeline": timeline,
+            "exchange": exchange,
             "ppo_samples_per_s_mb64": ppo64,
             "cpu_baseline": cpu,
             "cpu_env_baseline": cpu_env,

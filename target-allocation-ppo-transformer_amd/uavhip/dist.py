@@ -125,3 +125,69 @@ def normalize_global(adv, moments, count=None):
     check(LIB.uavhip_adv_normalize(ptr(adv), adv.numel(), ptr(m), 1, n, None, stream_handle()),
           "uavhip_adv_normalize")
     return adv
+
+
+class IpcAllGather:
+    """The trajectory all-gather as peer-to-peer copies out of IPC-mapped buffers, pipelined one
+    iteration behind the rollout so that iteration k's exchange runs beside iteration k + 1's
+    rollout: RCCL's all-gather kernels cannot become resident beside k_rollout_steps,
+    which holds every CU, while a device-to-device copy between two GPUs is a DMA transfer.
+
+    Every rank owns two send buffers (iteration parity p) that the other ranks map through IPC
+    (hipIpcGetMemHandle; handles exchanged over `group`, a gloo group) and two receive buffers
+    [world, floats]. submit(payload) enqueues the copy of this iteration's payload into send[p] on
+    the current stream. progress() completes the pending exchange: the host waits until its payload
+    is written and its copies of the previous iteration are done, a host barrier (every rank: both),
+    then a side stream copies every peer's send[p] into recv[p] (and its own). Send buffers are
+    rewritten only after every rank passed the barrier that follows the copies reading them, so no
+    interprocess events are needed. Call progress() after enqueueing the next iteration's work: the
+    host wait returns as that work starts, and the copies run beside it."""
+
+    def __init__(self, floats, device, group):
+        from torch.multiprocessing.reductions import rebuild_cuda_tensor, reduce_tensor
+        self.world, self.rank, self.group = dist.get_world_size(group), dist.get_rank(group), group
+        self.floats, self.device = int(floats), device
+        f32 = dict(dtype=torch.float32, device=device)
+        self.send = [torch.zeros(self.floats, **f32) for _ in range(2)]
+        self.recv = [torch.zeros(self.world, self.floats, **f32) for _ in range(2)]
+        torch.cuda.synchronize(device)
+        objs = [None] * self.world
+        dist.all_gather_object(objs, [reduce_tensor(t)[1] for t in self.send], group=group)
+        self.peer_send = {j: [rebuild_cuda_tensor(*a) for a in bufs] for j, bufs in enumerate(objs) if j != self.rank}
+        self.side = torch.cuda.Stream(device)
+        self.packed = [torch.cuda.Event(), torch.cuda.Event()]
+        self.copied = [None, None]
+        self.k = 0
+        self.pending = None
+        dist.barrier(group=group)
+
+    def submit(self, payload):
+        """Enqueue this iteration's flat fp32 payload (current stream); progress() exchanges it."""
+        if self.pending is not None:
+            raise RuntimeError("IpcAllGather.submit: the previous payload was not progressed")
+        p = self.k & 1
+        self.send[p].copy_(payload.view(-1))
+        self.packed[p].record()
+        self.pending = p
+        self.k += 1
+
+    def progress(self):
+        """Exchange the pending payload -> (receive buffer [world, floats], event recorded on the side
+        stream once it is complete; the caller's stream must wait on it before reading)."""
+        p = self.pending
+        if p is None:
+            raise RuntimeError("IpcAllGather.progress: nothing submitted")
+        self.packed[p].synchronize()
+        if self.copied[p ^ 1] is not None:
+            self.copied[p ^ 1].synchronize()  # this rank's reads of the peers' other-parity buffers
+        dist.barrier(group=self.group)
+        self.side.wait_event(self.packed[p])
+        with torch.cuda.stream(self.side):
+            self.recv[p][self.rank].copy_(self.send[p])
+            for j in sorted(self.peer_send):
+                self.recv[p][j].copy_(self.peer_send[j][p])
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        self.copied[p] = ev
+        self.pending = None
+        return self.recv[p], ev

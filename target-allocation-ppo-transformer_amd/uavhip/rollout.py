@@ -61,7 +61,8 @@ class RolloutEngine:
         self.env = env
         self.normalize = normalize
         self.iteration = 0
-        self._gathered = (-1, None)  # (iteration, batch) of the last gather()
+        self._gathered = (-1, None, None)  # (iteration, batch, pending event) of the last gather()
+        self._submitted = -1  # iteration of the payload gather_submit() enqueued
         self._normalized = -1        # iteration whose advantages normalize_global() normalised
         self.policy = policy
         self.T = int(horizon)
@@ -228,10 +229,41 @@ class RolloutEngine:
         dones) in (rank, step, env) order."""
         from .dist import all_gather_rows, pack_compact, unpack_compact
         if self._gathered[0] == self.iteration:  # once per iteration (normalises in place)
-            return self._gathered[1]
+            batch, ev = self._gathered[1], self._gathered[2]
+            if ev is not None:  # from the pipelined exchange: complete on its side stream
+                cur = torch.cuda.current_stream()
+                cur.wait_event(ev)
+                for t in batch.values():
+                    t.record_stream(cur)
+                self._gathered = (self.iteration, batch, None)
+            return batch
         tr = self.normalize_global(group)
         payload = pack_compact(tr.obs, tr.actions, tr.logp, tr.values, tr.ret, tr.adv, tr.dones)
         gathered = all_gather_rows(payload.view(1, -1), group)
         batch = unpack_compact(gathered, tr.T, tr.E)
-        self._gathered = (self.iteration, batch)
+        self._gathered = (self.iteration, batch, None)
         return batch
+
+    def gather_submit(self, exchange, group=None):
+        """The pipelined form of gather() (uavhip.dist.IpcAllGather): normalise with the global moments
+        and enqueue this iteration's compact payload; gather_finish() completes the exchange -- call
+        it after enqueueing the next iteration's rollout, beside which the copies then run."""
+        from .dist import pack_compact
+        tr = self.normalize_global(group)
+        exchange.submit(pack_compact(tr.obs, tr.actions, tr.logp, tr.values, tr.ret, tr.adv, tr.dones))
+        self._submitted = self.iteration
+
+    def gather_finish(self, exchange):
+        """Complete the submitted exchange: the peer copies and the window rebuild on the exchange's
+        side stream. The batch (as gather() returns it) is what gather() returns while no later
+        iteration has been collected; its consumers wait on the returned event."""
+        from .dist import unpack_compact
+        recv, ev = exchange.progress()
+        side = exchange.side
+        with torch.cuda.stream(side):
+            batch = unpack_compact(recv, self.T, self.env.E)
+        done = torch.cuda.Event()
+        done.record(side)
+        if self._submitted == self.iteration:
+            self._gathered = (self.iteration, batch, done)
+        return batch, done

@@ -237,3 +237,76 @@ def test_rccl_epoch_graph_matches_eager_data_parallel_steps():
     assert se == sg and se[3] == 2 * 2048 // 256
     for a, b in ((pe, pg), (me, mg), (ve, vg)):
         assert np.array_equal(a, b)
+
+
+def _ipc_rank(rank, port, q):
+    """World 2 on the one MI355X (gloo): the pipelined IPC exchange (uavhip.dist.IpcAllGather) over
+    raw payloads through both buffer parities, then through RolloutEngine.gather_submit/finish
+    against the synchronous gather() of the same iteration."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "target-allocation-ppo-transformer_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        torch.cuda.set_device(0)
+        from uavhip.dist import IpcAllGather, compact_floats
+        dev = torch.device("cuda", 0)
+        F = 4099
+        x = IpcAllGather(F, dev, None)
+        raw = []
+        for it in range(5):
+            x.submit(torch.arange(F, device=dev, dtype=torch.float32) + 100000 * rank + 10 * it)
+            torch.cuda._sleep(1000)  # the next iteration's work, enqueued before progress()
+            recv, ev = x.progress()
+            torch.cuda.current_stream().wait_event(ev)
+            raw.append(recv.cpu().numpy().copy())
+        c = CONFIGS["small"]
+        E, T = c["E"], c["T"]
+        pol, eng = _engine(c, E, rank * E, normalize=False)
+        ex = IpcAllGather(compact_floats(T, E), dev, None)
+        eng.start()
+        eng.collect(eager=True)
+        ref = {k: v.cpu().numpy().copy() for k, v in eng.gather().items()}
+        eng.gather_submit(ex)
+        eng.collect(eager=True)  # the next rollout, then the pending exchange beside it
+        batch, ev = eng.gather_finish(ex)
+        torch.cuda.current_stream().wait_event(ev)
+        got = {k: v.cpu().numpy().copy() for k, v in batch.items()}
+        q.put((rank, raw, ref, got))
+    except BaseException as exc:
+        q.put((rank, repr(exc), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipelined_ipc_exchange_matches_all_gather():
+    """bench.py's N > 1 exchange: every rank's payload of every iteration lands in every rank's
+    receive buffer through both buffer parities (the ordering that lets a send buffer be rewritten),
+    and the engine's pipelined gather of an iteration equals its synchronous gather() bit for bit."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ipc_rank, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(WORLD):
+        r, raw, ref, got = q.get(timeout=300)
+        assert not isinstance(raw, str), f"rank {r}: {raw}"
+        res[r] = (raw, ref, got)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    F = 4099
+    for r in range(WORLD):
+        raw, ref, got = res[r]
+        for it, recv in enumerate(raw):
+            want = np.stack([np.arange(F, dtype=np.float32) + 100000 * j + 10 * it for j in range(WORLD)])
+            assert np.array_equal(recv, want), (r, it)
+        assert set(ref) == set(got)
+        for k in ref:
+            assert np.array_equal(ref[k], got[k]), (r, k)
