@@ -1631,9 +1631,14 @@ struct EnvOut {
 };
 
 // ROWS: layer 0 of both trunks on the window-row projection ring (inference only).
-// ENV: the env step of the sampled actions follows (needs ROWS; envs b0 .. b0 + 15).
+// ENV: the env step of the sampled actions follows (needs ROWS; envs b0 .. b0 + 15): a bit mask of
+// the env-step code compiled in -- kEnvGrp (two envs per wave, N, M <= 32, both envs of every wave in
+// range), kEnvWave (one env per wave, any N, M <= 64), both (chosen per wave at run time). The
+// one-launch rollout instantiates one path per launch: its loop body then fits the instruction cache
+// (64 KiB shared by two CUs; both paths: 71 KB).
+enum { kEnvGrp = 1, kEnvWave = 2, kEnvBoth = 3 };
 // One workgroup's whole forward (+ env step) of its 16 samples; the kernels below wrap it.
-template <bool TR, bool ROWS, bool ENV>
+template <bool TR, bool ROWS, int ENV>
 __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __restrict__ P, const float* __restrict__ states,
                                              int B, const int8_t* __restrict__ actions_in, uint64_t seed,
                                              uint64_t offset, const uint64_t* __restrict__ offset_dev,
@@ -1720,7 +1725,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     PTR(4);
     // fused env step (ENV): two envs per wave side by side, state loads issued before the critic head
     [[maybe_unused]] const bool env_grp =
-        ENV && env.N <= envgrp::L && env.M <= envgrp::L && b0 + 2 * wv + 1 < B;
+        (ENV & kEnvGrp) && env.N <= envgrp::L && env.M <= envgrp::L && b0 + 2 * wv + 1 < B;
     [[maybe_unused]] envgrp::GRegs gR;
     [[maybe_unused]] envgrp::GPending gq;
     if (do_critic) {
@@ -1758,7 +1763,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             encoder_layer<kCriticTrunk, 1, true, TR>(TID_C sm, P, pkv, io.L[2], b0);
         }
         // the env step's state loads land while the critic head runs
-        if constexpr (ENV && !kExpNoEnv) {
+        if constexpr ((ENV & kEnvGrp) && !kExpNoEnv) {
             if (env_grp) {
                 const int le = tid_env() & 63;
                 envgrp::gload_issue(gR, gq, env, b0 + 2 * (int)(tid_env() >> 6) + (le >> 5), le & 31);
@@ -1820,7 +1825,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
         PTR(60);
         using namespace envdev;
         const int lane = tid_env() & 63, wve = tid_env() >> 6, e0 = b0 + 2 * wve;
-        if (env_grp) {
+        if constexpr ((ENV & kEnvGrp) != 0) if (env_grp) {
             // both envs side by side, 32 lanes each (env_group.hpp); window scratch in the dead sm.h
             const int j = lane & 31, g = lane >> 5, e = e0 + g;
             envgrp::GRegs& R = gR;
@@ -1833,7 +1838,8 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             PTR(62);
             envgrp::gstore_regs(R, env, e, j);
             PTR(63);
-        } else if (e0 < B) {
+        }
+        if constexpr ((ENV & kEnvWave) != 0) if (!env_grp && e0 < B) {
             const bool two = e0 + 1 < B;
             EnvRegs<1> R0, R1;
             R0.row = R1.row = sm.x + 16 * wve;
@@ -1853,7 +1859,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     }
 }
 
-template <bool TR, bool ROWS = false, bool ENV = false>
+template <bool TR, bool ROWS = false, int ENV = 0>
 __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict__ P, const float* __restrict__ states,
                                                          int B, const int8_t* __restrict__ actions_in, uint64_t seed,
                                                          uint64_t offset, const uint64_t* __restrict__ offset_dev,
@@ -1902,6 +1908,7 @@ struct StepsArgs {
     EnvOut eo;
     StepSeq seq;
 };
+template <int ENVP>  // kEnvGrp / kEnvWave (launch_rollout_steps picks)
 __global__ __launch_bounds__(NTHR) void k_rollout_steps(const StepsArgs args) {
     __shared__ __attribute__((aligned(16))) Smem sm;
     if (threadIdx.x >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
@@ -1922,7 +1929,7 @@ __global__ __launch_bounds__(NTHR) void k_rollout_steps(const StepsArgs args) {
         const RowIO r{a.rio.rp, a.rio.B, a.rio.g + t};
         const EnvOut e{a.eo.auto_reset, a.eo.obs + t * a.seq.obs_stride, a.eo.rew + o, a.eo.done + o,
                        a.eo.info ? a.eo.info + o * UAVHIP_INFO_COUNT : nullptr};
-        policy_block<false, true, true>(tid, sm, a.P, a.states + t * a.seq.obs_stride, a.B, nullptr, a.seed,
+        policy_block<false, true, ENVP>(tid, sm, a.P, a.states + t * a.seq.obs_stride, a.B, nullptr, a.seed,
                                         a.offset + t * a.seq.off_stride, a.offset_dev, a.action_out + o, a.logp_out + o,
                                         a.value_out + o, nullptr, nullptr, TrainIO{}, r, a.env, e, bx);
     }
@@ -1937,8 +1944,13 @@ extern "C" int uavhip_steps_trace(unsigned long long* out, int n) {  // the last
 int launch_rollout_steps(const float* P, float* obs, int B, uint64_t seed, uint64_t offset,
                          const uint64_t* offset_dev, int8_t* actions, float* logp, float* value, const RowIO& rio,
                          const uavhip_env& env, const EnvOut& eo, const StepSeq& seq, hipStream_t stream) {
-    hipLaunchKernelGGL(k_rollout_steps, dim3((B + SPW - 1) / SPW), dim3(NTHR), 0, stream,
-                       StepsArgs{P, obs, B, seed, offset, offset_dev, actions, logp, value, rio, env, eo, seq});
+    // two envs per wave wherever every wave's envs come in pairs (policy_block's env_grp for all of
+    // them): the grouped path alone; else the one-env-per-wave path alone (bitwise the same steps)
+    const StepsArgs sa{P, obs, B, seed, offset, offset_dev, actions, logp, value, rio, env, eo, seq};
+    if (env.N <= envgrp::L && env.M <= envgrp::L && B % 2 == 0)
+        hipLaunchKernelGGL(k_rollout_steps<kEnvGrp>, dim3((B + SPW - 1) / SPW), dim3(NTHR), 0, stream, sa);
+    else
+        hipLaunchKernelGGL(k_rollout_steps<kEnvWave>, dim3((B + SPW - 1) / SPW), dim3(NTHR), 0, stream, sa);
     return check_launch("k_rollout_steps");
 }
 #endif  // UAVHIP_STEPS_TU
@@ -3590,7 +3602,7 @@ extern "C" int uavhip_rollout_step(const uavhip_policy* policy, const uavhip_env
                            policy->weights, states, rio);
         if (const int rc = check_launch("k_policy_rows_fill")) return rc;
     }
-    hipLaunchKernelGGL((pol::k_policy_forward<false, true, true>), dim3(grid), dim3(pol::NTHR), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL((pol::k_policy_forward<false, true, pol::kEnvBoth>), dim3(grid), dim3(pol::NTHR), 0, (hipStream_t)stream,
                        policy->weights, states, (int)B, nullptr, seed, offset, offset_dev, action_out, logp, value,
                        nullptr, nullptr, pol::TrainIO{}, rio, *env,
                        pol::EnvOut{(int)auto_reset, obs_out, reward, done, info});
