@@ -252,15 +252,9 @@ __device__ __forceinline__ void zero(f32x4 (&acc)[CT]) {
 // ds_read_b128's lane groups (MI355X_MICROARCH.md LDS table) like the fp32 [tok][136] rows.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-#if defined(UAVHIP_EXP) && UAVHIP_EXP == 4  // A/B: the round-3 layout, plane 2 after all rows of plane 1
-constexpr int LDP = D + 8;
-constexpr int kPlane = TOK * LDP;
-#else
 constexpr int LDP = 2 * D + 16;      // halves per token row (both planes + pad)
 constexpr int kPlane = D;            // plane 2 within the row
-#endif
-static_assert(TOK * LDP * 2 <= TOK * LDH * 4 && kPlane + D <= LDP + (LDP == D + 8 ? TOK * LDP : 0),
-              "the two planes of an activation replace its fp32 copy");
+static_assert(TOK * LDP * 2 == TOK * LDH * 4 && kPlane + D <= LDP, "the two planes of an activation replace its fp32 copy");
 // Offset of (token, column) in a plane image: the 16-B chunk index XOR-swizzled by bit 2 of the token,
 // so the epilogues' ds_write_b64 (16 consecutive tokens per lane group) are at most 2-way conflicted
 // (4-way without it) while the GEMMs' ds_read_b128 stay conflict-free
@@ -2717,13 +2711,26 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     const float inv = 1.0f / (float)io.Bg;
     // the four loss sums (used by wave 0 only): from the all-reduced buffer, or summed here from
     // the forward's workgroup partials with k_loss_sums' exact order (train.hip)
+    // every global input issued before the first use: z rows (one float4 per thread), the head.2
+    // weights of this thread's hidden unit j = tid % 64 (the dz loop below), the per-sample rows,
+    // then the loss-sum partials four rows per thread at a time (a dependent chain of L2 round trips
+    // before: the heads prologue took 10.7 k cycles of K6)
+    const int zt = tid_x() >> 8, zp = (tid_x() >> 4) & 15, zq = tid_x() & 15;
+    const f32x4 zr = ld4(io.z[zt] + (size_t)(b0 + zp) * HID + 4 * zq);
+    const int jj = tid_x() % HID;
+    const float* W2a = P + kOffs.o[kActorHead + 2];
+    const float w2a0 = W2a[jj], w2a1 = W2a[HID + jj], w2c = P[kOffs.o[kCriticHead + 2] + jj];
+    f32x4 oa = {0.f, 0.f, 0.f, 0.f}, ob = oa;
+    if (tid_x() < SPW) {
+        oa = ld4(io.smp + (size_t)(b0 + tid_x()) * 8);
+        ob = ld4(io.smp + (size_t)(b0 + tid_x()) * 8 + 4);
+    }
     float tot0, tot1, tot2, tot3;
     if (io.fpart) {
-        float s4[4] = {0.f, 0.f, 0.f, 0.f};
-        if (tid_x() < 64) {
-            for (int i = tid_x(); i < io.nfpart; i += 64)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) s4[c] += io.fpart[i * 4 + c];
+        f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+        if (tid_x() < 64) {  // row i's four sums, rows in k_loss_sums' order per lane
+#pragma unroll 4
+            for (int i = tid_x(); i < io.nfpart; i += 64) s4 += ld4(io.fpart + (size_t)i * 4);
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 s4[c] = add_xor32(add_xor16(add_ror8(add_ror4(add_xor2(add_xor1(s4[c]))))));
@@ -2734,17 +2741,9 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     } else {
         tot0 = io.tot[0]; tot1 = io.tot[1]; tot2 = io.tot[2]; tot3 = io.tot[3];
     }
-    {   // every global input in one round trip: z rows (one float4 per thread), per-sample rows,
-        // the head.2 weights of this thread's hidden unit j = tid % 64 (the dz loop below)
-        const int trunk = tid_x() >> 8, p = (tid_x() >> 4) & 15, q = tid_x() & 15;
-        st4(zs + (trunk * SPW + p) * HID + 4 * q, ld4(io.z[trunk] + (size_t)(b0 + p) * HID + 4 * q));
-    }
-    const int jj = tid_x() % HID;
-    const float* W2a = P + kOffs.o[kActorHead + 2];
-    const float w2a0 = W2a[jj], w2a1 = W2a[HID + jj], w2c = P[kOffs.o[kCriticHead + 2] + jj];
+    st4(zs + (zt * SPW + zp) * HID + 4 * zq, zr);
     if (tid_x() < SPW) {
         const int p = tid_x();
-        const f32x4 oa = ld4(io.smp + (size_t)(b0 + p) * 8), ob = ld4(io.smp + (size_t)(b0 + p) * 8 + 4);
         const float o[8] = {oa.x, oa.y, oa.z, oa.w, ob.x, ob.y, ob.z, ob.w};
         const int act = o[0] > 0.f;
         const bool pad = o[0] < 0.f;  // padding row (idx < 0): zero output gradients
