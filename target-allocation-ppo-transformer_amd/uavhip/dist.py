@@ -144,16 +144,34 @@ class IpcAllGather:
     host wait returns as that work starts, and the copies run beside it."""
 
     def __init__(self, floats, device, group):
+        """Collective over `group`: every rank takes part in the same calls whether or not its own
+        setup fails, and all of them raise if any rank's did (no rank is left waiting)."""
         from torch.multiprocessing.reductions import rebuild_cuda_tensor, reduce_tensor
         self.world, self.rank, self.group = dist.get_world_size(group), dist.get_rank(group), group
         self.floats, self.device = int(floats), device
-        f32 = dict(dtype=torch.float32, device=device)
-        self.send = [torch.zeros(self.floats, **f32) for _ in range(2)]
-        self.recv = [torch.zeros(self.world, self.floats, **f32) for _ in range(2)]
-        torch.cuda.synchronize(device)
+        err, handles = None, None
+        try:
+            f32 = dict(dtype=torch.float32, device=device)
+            self.send = [torch.zeros(self.floats, **f32) for _ in range(2)]
+            self.recv = [torch.zeros(self.world, self.floats, **f32) for _ in range(2)]
+            torch.cuda.synchronize(device)
+            handles = [reduce_tensor(t)[1] for t in self.send]
+        except Exception as exc:
+            err = exc
         objs = [None] * self.world
-        dist.all_gather_object(objs, [reduce_tensor(t)[1] for t in self.send], group=group)
-        self.peer_send = {j: [rebuild_cuda_tensor(*a) for a in bufs] for j, bufs in enumerate(objs) if j != self.rank}
+        dist.all_gather_object(objs, handles, group=group)
+        if err is None and any(o is None for o in objs):
+            err = RuntimeError("IpcAllGather: another rank could not export its buffers")
+        if err is None:
+            try:
+                self.peer_send = {j: [rebuild_cuda_tensor(*a) for a in bufs] for j, bufs in enumerate(objs)
+                                  if j != self.rank}
+            except Exception as exc:
+                err = exc
+        oks = [None] * self.world
+        dist.all_gather_object(oks, err is None, group=group)
+        if err is not None or not all(oks):
+            raise RuntimeError(f"IpcAllGather setup failed on {'this' if err else 'another'} rank: {err!r}")
         self.side = torch.cuda.Stream(device)
         self.packed = [torch.cuda.Event(), torch.cuda.Event()]
         self.copied = [None, None]

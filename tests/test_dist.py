@@ -177,3 +177,41 @@ def test_resolve_shards_single_process():
     assert resolve_shards(7, 3, total_envs=10) == 10
     with pytest.raises(ValueError):
         resolve_shards(7, 4, total_envs=10)
+
+
+def _ipc_setup_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "target-allocation-ppo-transformer_amd"))
+    import torch.distributed as dist
+    from uavhip.dist import IpcAllGather
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.synchronize = lambda *a, **k: None  # no GPU here: rank 0 exports host buffers
+        try:
+            IpcAllGather(16 if rank == 0 else -1, torch.device("cpu"), None)  # rank 1 fails to allocate
+            q.put((rank, "no error"))
+        except RuntimeError as exc:
+            q.put((rank, str(exc)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ipc_exchange_setup_fails_on_every_rank_together():
+    """bench.py's pipelined exchange falls back to RCCL's all-gather when any rank cannot set it up:
+    IpcAllGather's setup is collective, so a failure on one rank raises on every rank (none is left
+    waiting in a collective the failed rank skipped)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ipc_setup_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert "this rank" in res[1] and "another rank" in res[0], res
