@@ -1628,8 +1628,7 @@ struct EnvOut {
 // ENV: the env step of the sampled actions follows (needs ROWS; envs b0 .. b0 + 15): a bit mask of
 // the env-step code compiled in -- kEnvGrp (two envs per wave, N, M <= 32, both envs of every wave in
 // range), kEnvWave (one env per wave, any N, M <= 64), both (chosen per wave at run time). The
-// one-launch rollout instantiates one path per launch: its loop body then fits the instruction cache
-// (64 KiB shared by two CUs; both paths: 71 KB).
+// one-launch rollout instantiates one path per launch (71 -> 58.5 KB of code, 28 -> 9 VGPR spills).
 enum { kEnvGrp = 1, kEnvWave = 2, kEnvBoth = 3 };
 // One workgroup's whole forward (+ env step) of its 16 samples; the kernels below wrap it.
 template <bool TR, bool ROWS, int ENV>
