@@ -506,7 +506,7 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
         if (TR && !kExpNoStore) {
             const size_t r = (size_t)orow(tok, lo.b0, lo.compact);
             *reinterpret_cast<f32x4*>(lo.x + r * D + f0) = xh;
-            *reinterpret_cast<f32x4*>(lo.h + r * D + f0) = out;
+            if (lo.h) *reinterpret_cast<f32x4*>(lo.h + r * D + f0) = out;  // nullptr: formed by k_wgrad
             if (wv == 0 && g == 0) lo.rs[r] = rs;
         }
     }
@@ -706,7 +706,7 @@ __device__ void embed_apply(TID_F Smem& sm, const EmbPre& ep, float* e_out = nul
         if (TR && !kExpNoStore) {
             const size_t r = (size_t)trow(ct * SPW + i16, b0);
             *reinterpret_cast<f32x4*>(e_out + r * D + 16 * wv + 4 * g) = e;
-            *reinterpret_cast<f32x4*>(h_out + r * D + 16 * wv + 4 * g) = v;
+            if (h_out) *reinterpret_cast<f32x4*>(h_out + r * D + 16 * wv + 4 * g) = v;
         }
     }
 }
@@ -1004,7 +1004,9 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
         }
         PTR(tb + 7);
         w1a = hprefetch<2>(TID_C P, s1, D, 16 * wv, 0);
-        const LnOut lo1{io.xhat1, io.h1, io.rstd1, b0, last};
+        // the LayerNorm outputs go to the workspace only for the position-split kernels (K7 reads
+        // them across launches); the fused training step's weight gradients form them from x-hat
+        const LnOut lo1{io.xhat1, PSX ? io.h1 : nullptr, io.rstd1, b0, last};
         if constexpr (res_ctx) {
             const f32x4 r4[1] = {*reinterpret_cast<const f32x4*>(sm.ctx + (LANE() & 15) * LDH + 16 * wv + 4 * (LANE() >> 4))};
             residual_layernorm<CT, TR, true>(TID_C sm, acc, lp, t0, lo1, h1, r4);
@@ -1051,7 +1053,7 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc2[ct] = hi[ct] + lo[ct] * kLoScale;
     pre_ln2();
-    residual_layernorm<CT, TR, next_planes, row4>(TID_C sm, acc2, lp2, t0, LnOut{io.xhat2, io.h2, io.rstd2, b0, last},
+    residual_layernorm<CT, TR, next_planes, row4>(TID_C sm, acc2, lp2, t0, LnOut{io.xhat2, PSX ? io.h2 : nullptr, io.rstd2, b0, last},
                                                 nullptr, h1);
     PTR(tb + 14);
 }
@@ -1106,7 +1108,7 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
             pf1a = prefetch_rot<DQ>(TID_C W1, D, 16 * wv, wv + 1);
             pf1b = prefetch_rot<DQ>(TID_C W1, D, 128 + 16 * wv, wv + 1);
             f32x4 outv[CTQ];
-            residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, io.h1, io.rstd1, b0, last}, outv);
+            residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, PSX ? io.h1 : nullptr, io.rstd1, b0, last}, outv);
             zero(fa);
             zero(fb);
 #pragma unroll
@@ -1123,7 +1125,7 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
                 const f32x4 r4[1] = {*reinterpret_cast<const f32x4*>(sm.ctx + (LANE() & 15) * LDH + 16 * wv + 4 * (LANE() >> 4))};
                 residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{}, nullptr, r4);
             } else {
-                residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, io.h1, io.rstd1, b0, last});
+                residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, PSX ? io.h1 : nullptr, io.rstd1, b0, last});
             }
         }
     }
@@ -1160,7 +1162,7 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
     PTR(tb + 12);
     const LnPar lp2 = ln_load(TID_C b24, P + kOffs.o[layer_param(trunk, layer, N2W)], P + kOffs.o[layer_param(trunk, layer, N2B)]);
     pre_ln2();
-    residual_layernorm<CTQ, TR>(TID_C sm, acc2, lp2, qtok0, LnOut{io.xhat2, io.h2, io.rstd2, b0, last});
+    residual_layernorm<CTQ, TR>(TID_C sm, acc2, lp2, qtok0, LnOut{io.xhat2, PSX ? io.h2 : nullptr, io.rstd2, b0, last});
     PTR(tb + 14);
     }
 }
@@ -1690,7 +1692,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             if constexpr (TR) {
                 // the split layer-0 in_proj reads the embedding's planes in sm.ctx
                 embed_apply<kActorTrunk, TR, kEmbH, split_kv<kActorTrunk, 0, TR, kTrainSplit>()>(TID_C sm, ep_a, io.e[0],
-                                                                                               io.h0[0], b0);
+                                                                                               nullptr, b0);
                 PTR(2);
                 __syncthreads();
                 auto hook = [&] {
@@ -1703,7 +1705,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
                 encoder_layer<kActorTrunk, 0, true, TR, decltype(hook), kTrainSplit>(TID_C sm, P, pkv_a, io.L[0], b0, hook);
             } else {
                 APre<2> pkv = prefetch<2>(TID_C P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-                embed<kActorTrunk, TR>(TID_C sm, P, io.e[0], io.h0[0], b0);
+                embed<kActorTrunk, TR>(TID_C sm, P, io.e[0], nullptr, b0);
                 PTR(2);
                 __syncthreads();
                 encoder_layer<kActorTrunk, 0, true, TR>(TID_C sm, P, pkv, io.L[0], b0);
@@ -1734,13 +1736,13 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
         if constexpr (!ROWS) {
             if constexpr (TR) {
                 embed_apply<kCriticTrunk, TR, kEmbH, split_kv<kCriticTrunk, 0, TR, kTrainSplit>()>(TID_C sm, ep_c, io.e[1],
-                                                                                                 io.h0[1], b0);
+                                                                                                 nullptr, b0);
                 __syncthreads();
                 auto hook = [&] { pkv = kv_prefetch<kCriticTrunk, 1, TR, kTrainSplit>(TID_C P); };
                 encoder_layer<kCriticTrunk, 0, false, TR, decltype(hook), kTrainSplit>(TID_C sm, P, pkv_c, io.L[1], b0, hook);
             } else {
                 APre<2> pkv0 = prefetch<2>(TID_C P + kOffs.o[layer_param(kCriticTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-                embed<kCriticTrunk, TR>(TID_C sm, P, io.e[1], io.h0[1], b0);
+                embed<kCriticTrunk, TR>(TID_C sm, P, io.e[1], nullptr, b0);
                 __syncthreads();
                 encoder_layer<kCriticTrunk, 0, false, TR>(TID_C sm, P, pkv0, io.L[1], b0);
             }

@@ -661,27 +661,42 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         // dW[out][in] = sum_rows dY[row][out] X[row][in]; dst = the weight's float offset
         WgPlan wp;
         int dst[kWgMaxProbs];
-        auto dw = [&](const float* dY, int ldy, const float* X, int ldx, int M, int N, int K, int dst_w) {
-            dst[wp.b.n] = dst_w;
-            wp.add(dY, ldy, X, ldx, M, N, K);
+        // X operands the fused forward does not store (wgrad.hpp kWgX*): a LayerNorm output from its
+        // x-hat (x-hat * gamma + beta), a layer-0 input from the embedding (e + pos[s])
+        struct XSrc {
+            const float* x;
+            int mode;
+            const float *g, *b;
+            XSrc at_token4() const {  // the token-4 rows (stride S D): one position of the pos table
+                return XSrc{x + (S - 1) * D, mode == kWgXPosRow ? (int)kWgXPosFixed : mode, g,
+                            mode == kWgXPosRow ? b + (S - 1) * D : b};
+            }
         };
-        auto layer_dw = [&](const LayerBufs& B, int tr_, int ly, const float* hin, int rows) {
+        auto ln_out = [&](const float* xhat, int tr_, int ly, int w) {  // w = N1W or N2W (+1: bias)
+            return XSrc{xhat, kWgXAffine, prm(c, layer_param(tr_, ly, w)), prm(c, layer_param(tr_, ly, w + 1))};
+        };
+        auto emb_out = [&](const float* e, int tr_) { return XSrc{e, kWgXPosRow, nullptr, prm(c, tr_ + POS)}; };
+        auto dw = [&](const float* dY, int ldy, const XSrc& X, int ldx, int M, int N, int K, int dst_w) {
+            dst[wp.b.n] = dst_w;
+            wp.add(dY, ldy, X.x, ldx, M, N, K, X.mode, X.g, X.b);
+        };
+        auto layer_dw = [&](const LayerBufs& B, int tr_, int ly, const XSrc& hin, int rows) {
             const int pw = kOffs.o[layer_param(tr_, ly, INW)];
             if (rows == R) {
                 dw(B.dqkv, 3 * D, hin, D, 3 * D, D, R, pw);
             } else {  // pruned: K/V rows over all R rows, Q rows over the Bm token-4 rows
                 dw(B.dqkv + D, 3 * D, hin, D, 2 * D, D, R, pw + D * D);
-                dw(B.dqkv + (S - 1) * 3 * D, S * 3 * D, hin + (S - 1) * D, S * D, D, D, Bm, pw);
+                dw(B.dqkv + (S - 1) * 3 * D, S * 3 * D, hin.at_token4(), S * D, D, D, Bm, pw);
             }
-            dw(B.dz1, D, B.o, D, D, D, rows, kOffs.o[layer_param(tr_, ly, OUTW)]);
-            dw(B.du, FF, B.h1, D, FF, D, rows, kOffs.o[layer_param(tr_, ly, L1W)]);
-            dw(B.df, D, B.u, FF, D, FF, rows, kOffs.o[layer_param(tr_, ly, L2W)]);
+            dw(B.dz1, D, XSrc{B.o, kWgX, nullptr, nullptr}, D, D, D, rows, kOffs.o[layer_param(tr_, ly, OUTW)]);
+            dw(B.du, FF, ln_out(B.xhat1, tr_, ly, N1W), D, FF, D, rows, kOffs.o[layer_param(tr_, ly, L1W)]);
+            dw(B.df, D, XSrc{B.u, kWgX, nullptr, nullptr}, FF, D, FF, rows, kOffs.o[layer_param(tr_, ly, L2W)]);
         };
-        layer_dw(C0, tc, 0, p.h0_c, R);  // the long problems first
-        layer_dw(A, ta, 0, p.h0_a, Bm);
-        layer_dw(C1, tc, 1, C0.h2, Bm);
-        dw(p.dz_a, HID, A.h2, D, HID, D, Bm, kOffs.o[kActorHead]);
-        dw(p.dz_c, HID, C1.h2, D, HID, D, Bm, kOffs.o[kCriticHead]);
+        layer_dw(C0, tc, 0, emb_out(p.e_c, tc), R);  // the long problems first
+        layer_dw(A, ta, 0, emb_out(p.e_a, ta), Bm);
+        layer_dw(C1, tc, 1, ln_out(C0.xhat2, tc, 0, N2W), Bm);
+        dw(p.dz_a, HID, ln_out(A.xhat2, ta, 0, N2W), D, HID, D, Bm, kOffs.o[kActorHead]);
+        dw(p.dz_c, HID, ln_out(C1.xhat2, tc, 1, N2W), D, HID, D, Bm, kOffs.o[kCriticHead]);
         wp.b.part = p.wg_part;
         const bool sched = wp.ok && wp.tiles([&](const WgTileRuns& t) {
             const WgProb& P = wp.b.p[t.prob];

@@ -27,9 +27,16 @@ constexpr int kWgSlot = kWgT * kWgT;      // floats per partial slot
 constexpr int kWgMaxProbs = 16;
 constexpr int kWgGrid = 256;              // one workgroup per CU
 
+// X operands the training forward does not store: a LayerNorm output is formed from
+// its stored x-hat as x-hat * gamma + beta (per column), a layer-0 input from the stored embedding as
+// e + pos[s] (row k = b * 5 + s, or one fixed position s for the token-4 rows)
+enum { kWgX = 0, kWgXAffine = 1, kWgXPosRow = 2, kWgXPosFixed = 3 };
 struct WgProb {
     const float* A;  // dY: row k at A + k * lda, columns m
-    const float* B;  // X:  row k at B + k * ldb, columns n
+    const float* B;  // X:  row k at B + k * ldb, columns n (before the transform xmode)
+    const float* xg;  // kWgXAffine: gamma [N]
+    const float* xb;  // kWgXAffine: beta [N]; kWgXPosRow: pos [5][N]; kWgXPosFixed: pos row [N]
+    int xmode;
     int M, N, K, lda, ldb;
     int tiles_n, tiles, slabs;  // per problem: column tiles, tiles, slabs per tile
     int unit_begin;             // first slab unit of this problem
@@ -100,7 +107,10 @@ __device__ __forceinline__ int wg_swz(int row, int ch) {
 // that are never stored.
 struct WgSlab {
     f32x4 a[2], b[2];
+    f32x4 x[2];  // the X transform's additive term of each row: beta, or the row's pos
 };
+// Every load is unconditional (the host points xg / xb at valid memory for every mode), so the
+// wait counts stay exact across the software pipeline; the mode only selects arithmetic.
 __device__ __forceinline__ void wg_gload(WgSlab& r, const WgProb& P, int k0, int m0, int n0) {
     const int t = threadIdx.x, c = 4 * (t & 31);
     const int ca = m0 + c < P.M ? m0 + c : m0;
@@ -109,7 +119,13 @@ __device__ __forceinline__ void wg_gload(WgSlab& r, const WgProb& P, int k0, int
         const int row = k0 + (t >> 5) + 16 * i;
         r.a[i] = *reinterpret_cast<const f32x4*>(P.A + (size_t)row * P.lda + ca);
         r.b[i] = *reinterpret_cast<const f32x4*>(P.B + (size_t)row * P.ldb + n0 + c);
+        r.x[i] = *reinterpret_cast<const f32x4*>(P.xb + (P.xmode == kWgXPosRow ? (row % 5) * P.N : 0) + n0 + c);
     }
+}
+// gamma of this thread's 4 columns n0 + 4 (t & 31) .. + 3 (1 unless kWgXAffine), once per tile run
+__device__ __forceinline__ f32x4 wg_xgamma(const WgProb& P, int n0) {
+    const f32x4 g = *reinterpret_cast<const f32x4*>(P.xg + n0 + 4 * (threadIdx.x & 31));
+    return P.xmode == kWgXAffine ? g : f32x4{1.f, 1.f, 1.f, 1.f};
 }
 __device__ __forceinline__ void wg_split_store(const f32x4 v, char* plane, int off) {
     wg_f16x4 x1, x2, x3;
@@ -124,13 +140,15 @@ __device__ __forceinline__ void wg_split_store(const f32x4 v, char* plane, int o
     *reinterpret_cast<wg_f16x4*>(plane + kWgPlaneB + off) = x2;
     *reinterpret_cast<wg_f16x4*>(plane + 2 * kWgPlaneB + off) = x3;
 }
-__device__ __forceinline__ void wg_stage_store(const WgSlab& r, char* stage) {
+// the X operand as the forward formed it: x-hat * gamma + beta (its LayerNorm epilogue's expression),
+// e + pos[s] (gamma 1: exact), or x itself (applied at staging: the slab's loads have landed by then)
+__device__ __forceinline__ void wg_stage_store(const WgSlab& r, char* stage, int xmode, const f32x4 xg) {
     const int t = threadIdx.x, c4 = t & 31;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int off = wg_swz((t >> 5) + 16 * i, c4 >> 1) + 8 * (c4 & 1);
         wg_split_store(r.a[i], stage, off);
-        wg_split_store(r.b[i], stage + 3 * kWgPlaneB, off);
+        wg_split_store(xmode != kWgX ? r.b[i] * xg + r.x[i] : r.b[i], stage + 3 * kWgPlaneB, off);
     }
 }
 // 16 columns (c16 .. c16 + 15) x 8 consecutive k (8 g ..) of a plane: lane (i16, g) gets column
@@ -165,9 +183,11 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
         for (int a = 0; a < 4; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) hi[a][b] = mid[a][b] = lo[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int xmode = P.xmode;
+        const f32x4 xg = wg_xgamma(P, n0);
         WgSlab nx;
         wg_gload(nx, P, s0 * kWgBK, m0, n0);
-        wg_stage_store(nx, wg_smem);
+        wg_stage_store(nx, wg_smem, xmode, xg);
         if (n_slabs > 1) wg_gload(nx, P, (s0 + 1) * kWgBK, m0, n0);
         __syncthreads();
         WTR(1 + 4 * run);
@@ -198,7 +218,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
                     lo[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[a], b2[b], lo[a][b], 0, 0, 0);
                 }
             if (s + 1 < n_slabs) {  // slab s + 1 (landed in registers meanwhile) -> the other stage
-                wg_stage_store(nx, wg_smem + ((s + 1) & 1) * kWgStageB);
+                wg_stage_store(nx, wg_smem + ((s + 1) & 1) * kWgStageB, xmode, xg);
                 if (s + 2 < n_slabs) wg_gload(nx, P, (s0 + s + 2) * kWgBK, m0, n0);
             }
             __syncthreads();  // the next stage is written; everyone is done reading this one
@@ -231,13 +251,17 @@ struct WgPlan {
     WgBatch b{};
     int grid = 0;
     bool ok = true;
-    void add(const float* A, int lda, const float* B, int ldb, int M, int N, int K) {
-        if (b.n >= kWgMaxProbs || N % kWgT || K % kWgBK || (M % kWgT && M != 64) || lda % 4 || ldb % 4) {
+    void add(const float* A, int lda, const float* B, int ldb, int M, int N, int K, int xmode = kWgX,
+             const float* xg = nullptr, const float* xb = nullptr) {
+        if (b.n >= kWgMaxProbs || N % kWgT || K % kWgBK || (M % kWgT && M != 64) || lda % 4 || ldb % 4 ||
+            (xmode == kWgXAffine && (!xg || !xb)) || (xmode >= kWgXPosRow && !xb)) {
             ok = false;
             return;
         }
         WgProb& P = b.p[b.n++];
         P.A = A; P.B = B; P.M = M; P.N = N; P.K = K; P.lda = lda; P.ldb = ldb;
+        // xg / xb are read whatever the mode: unused ones point at N valid floats (X's row 0)
+        P.xmode = xmode; P.xb = xb ? xb : B; P.xg = xg ? xg : P.xb;
         P.tiles_n = N / kWgT;
         P.tiles = ((M + kWgT - 1) / kWgT) * P.tiles_n;
         P.slabs = K / kWgBK;
