@@ -16,7 +16,9 @@ from uavhip import _lib  # noqa: E402
 from uavhip.policy import TransformerActorCritic  # noqa: E402
 
 NAMES = {0: "start", 1: "x+mask", 2: "a.embed", 3: "a.layer+sync", 4: "a.head", 5: "c.layers+sync", 6: "c.head",
-         7: "sample", 60: "env.sync", 61: "env.loads", 62: "env.step", 63: "env.store"}
+         7: "sample", 60: "env.sync", 61: "env.loads", 62: "env.step", 63: "env.store",
+         55: "C0.LN1 acc ready", 56: "C0.LN1 partials", 57: "C0.LN1 barrier", 23: "C0.LN2 acc ready",
+         39: "C0.LN2 partials", 58: "C0.LN2 barrier"}
 LAYER = ["start", "c0 gemm", "c0 sync", "c0 attn+sync", "c1 gemm", "c1 sync", "c1 attn+sync", "outproj", "sync",
          "LN1+sync", "FFN1", "sync", "FFN2+sync", "store+sync", "LN2"]
 for li, tag in enumerate(["A", "C0", "C1"]):

@@ -434,7 +434,9 @@ __device__ __forceinline__ LnPar ln_load(TID_F const f32x4 bb, const float* __re
 // lane's own elements, as `outv` returned them) instead of sm.h.
 // ROW4 (with PLANES): the fp32 output of position 4 (tokens 64-79) also goes to sm.ctx rows 0-15 (the
 // next, pruned layer's residual and query rows).
-template <int CT, bool TR = false, bool PLANES = false, bool ROW4 = false>
+// T0 / T1 / T2 (trace builds, >= 0): phase stamps when the GEMM accumulators are consumed, when the
+// partial statistics are written, after the barrier
+template <int CT, bool TR = false, bool PLANES = false, bool ROW4 = false, int T0 = -1, int T1 = -1, int T2 = -1>
 __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (&acc)[CT], const LnPar& lp, int ytok0,
                                                    const LnOut& lo = LnOut{}, f32x4* outv = nullptr,
                                                    const f32x4* resid = nullptr) {
@@ -442,6 +444,16 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
     const int f0 = 16 * wv + 4 * g;
     const f32x4 bb = lp.bb;
     f32x4 v[CT];
+#if defined(UAVHIP_POLICY_TRACE)
+    if constexpr (T0 >= 0) {
+        float dep = 0.f;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) dep += acc[ct].x;
+        asm volatile("" ::"v"(dep));
+        __builtin_amdgcn_sched_barrier(0);
+        PTR(T0);
+    }
+#endif
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
         const int tok = ytok0 + 16 * ct + i16;
@@ -454,7 +466,16 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
         q = add_xor32(add_xor16(q));
         if (g == 0) sm.red[wv * TOK + tok] = make_float2(m, q);
     }
+#if defined(UAVHIP_POLICY_TRACE)
+    if constexpr (T1 >= 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        PTR(T1);
+    }
+#endif
     __syncthreads();
+#if defined(UAVHIP_POLICY_TRACE)
+    if constexpr (T2 >= 0) PTR(T2);
+#endif
     const f32x4 ww = lp.ww, lb = lp.lb;
     // (mean, 1/std) of token tok from the 8 per-wave partials
     auto stats = [&](int tok, float& mean, float& rs) {
@@ -980,6 +1001,7 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     constexpr bool row4 = next_planes && !PSX;
     constexpr bool res_ctx = split_inproj<trunk, layer>() && !PSX;  // the residual is in sm.ctx rows 0-15
     static_assert(!res_ctx || last, "a split in_proj feeds a pruned layer");
+    constexpr bool kC0 = trunk != 0 && layer == 0 && !TR && !PSX;  // trace stamps of the critic's layer-0 LNs
     const int wv = TIDX() >> 6;
     _Float16* const hp = reinterpret_cast<_Float16*>(sm.h);
     _Float16* const bp = reinterpret_cast<_Float16*>(sm.big);
@@ -1011,7 +1033,7 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
             const f32x4 r4[1] = {*reinterpret_cast<const f32x4*>(sm.ctx + (LANE() & 15) * LDH + 16 * wv + 4 * (LANE() >> 4))};
             residual_layernorm<CT, TR, true>(TID_C sm, acc, lp, t0, lo1, h1, r4);
         } else {
-            residual_layernorm<CT, TR, true>(TID_C sm, acc, lp, t0, lo1, h1);
+            residual_layernorm<CT, TR, true, false, kC0 ? 55 : -1, kC0 ? 56 : -1, kC0 ? 57 : -1>(TID_C sm, acc, lp, t0, lo1, h1);
         }
     }
     PTR(tb + 8);
@@ -1053,8 +1075,8 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc2[ct] = hi[ct] + lo[ct] * kLoScale;
     pre_ln2();
-    residual_layernorm<CT, TR, next_planes, row4>(TID_C sm, acc2, lp2, t0, LnOut{io.xhat2, PSX ? io.h2 : nullptr, io.rstd2, b0, last},
-                                                nullptr, h1);
+    residual_layernorm<CT, TR, next_planes, row4, kC0 ? 23 : -1, kC0 ? 39 : -1, kC0 ? 58 : -1>(
+        TID_C sm, acc2, lp2, t0, LnOut{io.xhat2, PSX ? io.h2 : nullptr, io.rstd2, b0, last}, nullptr, h1);
     PTR(tb + 14);
 }
 
