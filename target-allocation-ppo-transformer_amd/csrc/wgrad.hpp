@@ -34,8 +34,8 @@ enum { kWgX = 0, kWgXAffine = 1, kWgXPosRow = 2, kWgXPosFixed = 3 };
 struct WgProb {
     const float* A;  // dY: row k at A + k * lda, columns m
     const float* B;  // X:  row k at B + k * ldb, columns n (before the transform xmode)
-    const float* xg;  // kWgXAffine: gamma [N]
-    const float* xb;  // kWgXAffine: beta [N]; kWgXPosRow: pos [5][N]; kWgXPosFixed: pos row [N]
+    const float* xg;  // kWgXAffine: gamma [N] (other modes: read, unused; WgPlan::add points it at N valid floats)
+    const float* xb;  // kWgXAffine: beta [N]; kWgXPosRow: pos [5][N]; kWgXPosFixed: pos row [N]; kWgX: X row 0
     int xmode;
     int M, N, K, lda, ldb;
     int tiles_n, tiles, slabs;  // per problem: column tiles, tiles, slabs per tile
