@@ -85,19 +85,60 @@ MFMA_F32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: fp32 MFMA = vector 
 HBM_PEAK_GBS = 8000.0
 
 
+def _kernel_base(name):
+    """Kernel name without namespaces and template arguments: 'uavhip::pol::k_rollout_steps<1>' ->
+    'k_rollout_steps' (rocprofv3 reports the demangled template instance)."""
+    import re
+    return re.sub(r"<.*>$", "", name).split("::")[-1].strip()
+
+
 def profiled_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/rNN_pmc.json, written by scripts/summarize_profile.py from separate rocprofv3
-    --pmc FETCH_SIZE / WRITE_SIZE passes of this benchmark; FETCH doubled per the gfx950 note)."""
+    --pmc FETCH_SIZE / WRITE_SIZE passes of this benchmark; FETCH doubled per the gfx950 note).
+    Matched on the exact name first, then on the name without namespaces / template arguments
+    (a template kernel such as k_rollout_steps<1> is reported with its arguments)."""
     import glob
     files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")) if "train" not in f)
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    for k, v in d.get("pmc", {}).items():
-        if k.replace("uavhip::pol::", "").replace("uavhip::", "") == kernel and "hbm_bytes_per_launch" in v:
+    pmc = {k: v for k, v in d.get("pmc", {}).items() if "hbm_bytes_per_launch" in v}
+    for k, v in pmc.items():
+        if k.replace("uavhip::pol::", "").replace("uavhip::", "") == kernel:
             return v["hbm_bytes_per_launch"], os.path.basename(files[-1])
+    hits = [v for k, v in pmc.items() if _kernel_base(k) == _kernel_base(kernel)]
+    if len(hits) == 1:
+        return hits[0]["hbm_bytes_per_launch"], os.path.basename(files[-1])
     return None, None
+
+
+def env_differential(args, pairs=2):
+    """The env step's time inside k_rollout_steps, live on this box: scripts/rollout_run.py as a child
+    process (its own GPU context) on the product library and on the build with the env step
+    compiled out (libuavhip_noenv.so, make NOENV=1; profiling only, wrong results), alternated
+    `pairs` times; each run reports the median HIP-event time per step of its k_rollout_steps
+    launches. Returns ({product_ms, noenv_ms, env_ms (medians per step)}, None) or (None, reason)."""
+    import subprocess
+    libdir = os.path.join(ROOT, "target-allocation-ppo-transformer_amd", "uavhip")
+    libs = {"product": os.path.join(libdir, "libuavhip.so"), "noenv": os.path.join(libdir, "libuavhip_noenv.so")}
+    if not os.path.exists(libs["noenv"]):
+        return None, "no NOENV build (libuavhip_noenv.so)"
+    got = {"product": [], "noenv": []}
+    try:
+        for _ in range(pairs):
+            for b in ("product", "noenv"):
+                env = dict(os.environ, UAVHIP_LIB=libs[b], E=str(args.envs), N=str(args.uavs), M=str(args.targets),
+                           T=str(args.horizon), ITERS="6")
+                out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rollout_run.py")], env=env,
+                                     capture_output=True, text=True, timeout=300)
+                if out.returncode != 0:
+                    return None, f"rollout_run.py ({b}) failed: " + out.stderr[-300:]
+                got[b].append(json.loads(out.stdout.strip().splitlines()[-1])["step_ms"])
+    except Exception as exc:
+        return None, repr(exc)
+    prod, noenv = float(np.median(got["product"])), float(np.median(got["noenv"]))
+    return {"product_ms": prod, "noenv_ms": noenv, "env_ms": prod - noenv, "runs": got}, None
 
 
 def env_phase_share(args):
@@ -123,13 +164,14 @@ def env_phase_share(args):
 def env_share_traffic():
     """HBM bytes per env step inside k_rollout_steps (per step of the launch, all E envs) from the
     newest profiles/rNN_env_share.json (scripts/profile_env_share.sh: PMC FETCH/WRITE passes of the
-    product build and of a build with the env step compiled out; the difference)."""
+    product build and of a build with the env step compiled out; the difference), with the
+    profiled time differential of the same runs."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_env_share.json")))
     if not files:
-        return None, None
+        return None, None, None
     d = json.load(open(files[-1]))
-    return d.get("env_bytes_per_step"), os.path.basename(files[-1])
+    return d.get("env_bytes_per_step"), os.path.basename(files[-1]), d.get("env_ns_per_step")
 
 
 def env_counters(kernel):
@@ -168,6 +210,7 @@ def parse():
     ap.add_argument("--ppo-impl", choices=["fused", "torch-graph", "torch-eager"], default="fused",
                     help="PPO update implementation timed for ppo_samples_per_s")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end rollout + update iteration legs")
     ap.add_argument("--rccl-gather", action="store_true",
                     help="N > 1: the exchange as one RCCL all-gather after each rollout instead of the pipelined "
                          "peer-to-peer copies beside the next rollout (uavhip.dist.IpcAllGather)")
@@ -334,17 +377,8 @@ def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
                     "all-reduce grads / clip+Adam per global minibatch")
             graphed = False
             if trainer.graph_collectives:  # RCCL: the epoch with its all-reduces as one graph (not timed)
-                try:
-                    trainer.capture()
-                    graphed = True
-                except Exception as exc:  # every rank must take the same path: agree below
-                    print(f"[bench] rank {dist.get_rank()}: data-parallel graph capture failed: {exc!r}",
-                          file=sys.stderr)
-                ok = torch.tensor([1 if graphed else 0], device=dev, dtype=torch.int32)
-                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-                graphed = bool(ok.item())
-                if not graphed:
-                    trainer.graphs = {}
+                # collective: the ranks vote inside capture(); None on every rank if any rank failed
+                graphed = trainer.capture() is not None
             if graphed:
                 impl += ", one hipGraph replay per epoch with the RCCL all-reduces captured"
             else:
@@ -423,6 +457,48 @@ def ppo_mb64_rate(policy, eng, E, T, dev, n_sub=16384):
     return {"value": n_sub / dt, "unit": "PPO samples/s (transitions / update wall time, 5 epochs)",
             "minibatch": 64, "batch": n_sub, "optimizer_steps": cnt, "ms_per_optimizer_step": dt / cnt * 1e3,
             "impl": "HIP training step at the reference's minibatch 64, one hipGraph replay per epoch"}
+
+
+def e2e_iteration_rate(eng, policy, E, T, minibatch, iters=2):
+    """The loop the reference runs (main_train.py:109-146): a rollout iteration, then the PPO update
+    (5 epochs) over ALL of its E * T transitions at `minibatch`, then the next rollout on the updated
+    weights -- timed end to end on the host clock (device-synchronised at both ends), with the phase
+    split from HIP events on the launch stream. One process, N = 1. The trainer's buffers are views
+    of the engine's trajectory (every rollout writes them in place); the update's epoch graph (or its
+    256-step chunk graph, FusedPPOTrainer.max_graph_steps) is captured once before the timed loop.
+    Returns env-steps/s including the update and the per-phase times."""
+    from uavhip.train import FusedPPOTrainer
+    tr = eng.traj
+    n = E * T
+    trainer = FusedPPOTrainer(policy, minibatch)
+    trainer.set_buffers(tr.obs[:T].reshape(n, 5, 14), tr.actions.reshape(n), tr.logp.reshape(n),
+                        tr.values.reshape(n), tr.ret.reshape(n), tr.adv.reshape(n))
+    gen = torch.Generator().manual_seed(99)
+    eng.collect()
+    trainer.capture()  # not timed (once per buffer set)
+    trainer.run(generator=gen)  # warm-up iteration's update
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    steps = 0
+    for i in range(iters):
+        ev[i][0].record()
+        eng.collect()  # graph replay; repacks the policy's inference weights after the update
+        ev[i][1].record()
+        steps += trainer.run(generator=gen)[3]
+        ev[i][2].record()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    roll = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+    upd = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+    return {"value": n * iters / dt, "unit": "env-steps/s including the PPO update (rollout + GAE + 5-epoch update "
+            "over every transition, serial, as main_train.py runs them)", "minibatch": minibatch,
+            "iterations": iters, "ms_per_iteration": dt / iters * 1e3, "rollout_ms": roll, "update_ms": upd,
+            "update_share": upd / (roll + upd), "optimizer_steps_per_iteration": steps // iters,
+            "ms_per_optimizer_step": upd / max(1, steps // iters),
+            "ppo_samples_per_s": n / (upd * 1e-3),
+            "timing": "host clock over the loop; phase split from HIP events around the rollout replay and the update"}
 
 
 def main():
@@ -568,15 +644,21 @@ def main():
     # the last timed iteration's launches: T+1 policy and T env launches, or (fused steps) T fused
     # forward + env-step launches and the bootstrap forward (the same kernel without the env step)
     pol_list, env_list = eng.event_ms()
-    env_phase = env_err = None
+    env_phase = env_err = env_diff = None
     if eng.fused_step:
         pol_ms = float(np.mean(pol_list[:T]))
         env_ms = None
         if eng.persistent and rank == 0 and world == 1:
-            # the env step's share of the step's cycles (TRACE build phase stamps, child process)
-            env_phase, env_err = env_phase_share(args)
-            if env_phase is not None:
-                env_ms = env_phase["share"] * pol_ms
+            # the env step's cost = the compiled-out differential (product minus NOENV build, HIP
+            # events, child processes on this box); the TRACE build's phase share is a diagnostic
+            env_diff, env_err = env_differential(args)
+            if env_diff is not None and env_diff["env_ms"] > 0:
+                env_ms = env_diff["env_ms"]
+            elif env_diff is not None:
+                env_err = f"non-positive differential {env_diff['env_ms']:.4f} ms"
+            env_phase, phase_err = env_phase_share(args)
+            if phase_err:
+                env_err = (env_err + "; " if env_err else "") + "phase share: " + phase_err
         elif not eng.persistent:  # per-step launches: the fused launch minus the bootstrap forward
             env_ms = max(float(np.mean(pol_list[:T])) - float(pol_list[T]), 1e-6)
     else:
@@ -621,6 +703,16 @@ def main():
             print(f"[bench] PPO update measurement failed: {exc!r}", file=sys.stderr)
             ppo = {"value": None, "error": repr(exc)}
 
+    e2e = None
+    if not args.no_ppo and not args.no_e2e and world == 1 and args.ppo_impl == "fused":
+        e2e = {}
+        for mb, it in ((args.ppo_minibatch, 3), (64, 1)):
+            try:
+                e2e[f"minibatch_{mb}"] = e2e_iteration_rate(eng, policy, E, T, mb, iters=it)
+            except Exception as exc:  # the headline rollout line must still print
+                print(f"[bench] end-to-end iteration at minibatch {mb} failed: {exc!r}", file=sys.stderr)
+                e2e[f"minibatch_{mb}"] = {"value": None, "error": repr(exc)}
+
     cpu = cpu_env = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, policy.state_dict(), args.cpu_seconds)
@@ -635,12 +727,24 @@ def main():
     pol_traffic, pol_src = profiled_traffic(pol_kernel)
     if pol_traffic is not None and eng.persistent:  # one launch = T steps: per-step bytes
         pol_traffic /= T
+    env_prof_ns = None
     if eng.persistent:
-        env_traffic, env_traffic_src = env_share_traffic()
+        env_traffic, env_traffic_src, env_prof_ns = env_share_traffic()
     elif eng.fused_step:
         env_traffic, env_traffic_src = None, None
     else:
         env_traffic, env_traffic_src = profiled_traffic("k_env_step<1, false>")
+    # consistency: PMC bytes over the env step's time must not exceed the HBM peak (a traffic figure
+    # from another code state, or a time that is not the env step's, would); such traffic is dropped
+    env_traffic_gbs = env_traffic_check = None
+    if env_traffic is not None and env_ms is not None:
+        env_traffic_gbs = env_traffic / (env_ms * 1e-3) / 1e9
+        env_traffic_check = env_traffic_gbs <= HBM_PEAK_GBS
+        if not env_traffic_check:
+            env_err = (env_err + "; " if env_err else "") + (
+                f"traffic {env_traffic / 1e6:.1f} MB per step over {env_ms * 1e3:.2f} us implies "
+                f"{env_traffic_gbs:.0f} GB/s > HBM peak: traffic dropped")
+            env_traffic = None
     if rank == 0:
         line = {
             "metric": "env-steps/sec (whole node), full PPO rollout, 4096 envs x 16 UAV x 32 tgt per GPU",
@@ -685,19 +789,24 @@ def main():
             "env_roofline": None if env_ms is None else {
                 "kernel": "env step inside k_rollout_steps" if eng.persistent else
                 "env step inside the fused rollout launch" if eng.fused_step else "k_env_step",
-                "timing": ("k_rollout_steps per-step time above (HIP events) x the env step's share of the "
-                           "step's cycles: s_memtime phase stamps of the TRACE build, sample -> env.store over "
-                           "start -> env.store, median of 256 workgroups, last step of a 64-step launch "
-                           "(scripts/env_phase.py, child process)" if eng.persistent else
+                "timing": ("the compiled-out differential: k_rollout_steps per step on the product build minus "
+                           "on the NOENV build (env step compiled out), HIP events, median of alternating "
+                           "child-process runs on this box (scripts/rollout_run.py)" if eng.persistent else
                            "per-step fused launch minus the bootstrap forward launch" if eng.fused_step else
                            "HIP events around each of the T env launches"),
-                "share": None if env_phase is None else env_phase["share"],
-                "share_p10_p90": None if env_phase is None else [env_phase["share_p10"], env_phase["share_p90"]],
-                "phase_cycles": None if env_phase is None else env_phase["phases"],
+                "differential": env_diff,
+                "profiled_differential_ms": None if env_prof_ns is None else env_prof_ns * 1e-6,
+                "phase_share_diagnostic": None if env_phase is None else {
+                    "share": env_phase["share"], "share_p10_p90": [env_phase["share_p10"], env_phase["share_p90"]],
+                    "share_x_step_ms": env_phase["share"] * pol_ms, "phase_cycles": env_phase["phases"],
+                    "what": "TRACE build s_memtime stamps: sample -> env.store over the step (diagnostic only: "
+                            "it misses the env step's indirect cost on the policy phases)"},
                 "bound": "hbm", "achieved": env_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": env_gbs / HBM_PEAK_GBS, "avg_launch_ms": env_ms,
-                "traffic": env_traffic, "traffic_unit": "HBM bytes per step of all E envs (PMC)",
-                "traffic_source": env_traffic_src, "bytes_per_env_step": env_bytes_per_step(args.targets)},
+                "traffic": env_traffic, "traffic_unit": "HBM bytes per step of all E envs (PMC: product minus NOENV)",
+                "traffic_source": env_traffic_src, "traffic_gbs_at_this_time": env_traffic_gbs,
+                "traffic_within_hbm_peak": env_traffic_check,
+                "bytes_per_env_step": env_bytes_per_step(args.targets)},
             "env_roofline_error": env_err,
             "env_fused": env_fused,
             "score_pairs": stress,
@@ -705,13 +814,19 @@ def main():
             "iteration_timeline": timeline,
             "exchange": exchange,
             "ppo_samples_per_s_mb64": ppo64,
+            "e2e_iteration": e2e,
             "cpu_baseline": cpu,
             "cpu_env_baseline": cpu_env,
         }
+        if exchange is not None and exchange.get("check") is False:
+            line["invalid"] = ("the pipelined exchange's gathered payloads differ from RCCL's all_gather of the "
+                               "same payloads: the multi-GPU throughput is not valid")
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if exchange is not None and exchange.get("check") is False:
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -417,6 +417,25 @@ int uavhip_episode_stats(const double* reward, const uint8_t* done, const int8_t
                          const float* value, int32_t T, int32_t E, double* acc, double* records,
                          int32_t max_records, uint32_t* n_records, uavhip_stream_t stream);
 
+/* ---------------------------------------------------------------- N > 1 trajectory exchange
+ * The all-gather of trajectories before the update (the reference has no multi-GPU
+ * path, main_train.py:109-146 runs one process) as peer-to-peer copies beside the next rollout
+ * (uavhip.dist.IpcAllGather). Host-side helpers over the HIP runtime:
+ *   uavhip_peer_access  : can the current device read peer_device's memory? enables peer access
+ *                         (an already enabled one is fine); *can_access = 1 for the same device
+ *   uavhip_ipc_export   : IPC handle (UAVHIP_IPC_HANDLE_BYTES) of the allocation holding ptr, and
+ *                         ptr's offset inside it
+ *   uavhip_ipc_open     : map a peer's exported allocation into the CURRENT device's address space
+ *                         (no context on the exporter's device); *ptr = base + offset
+ *   uavhip_ipc_close    : unmap (the base returned by open minus its offset)
+ *   uavhip_copy_async   : device-to-device copy on `stream` (a mapped peer buffer as the source) */
+#define UAVHIP_IPC_HANDLE_BYTES 64
+int uavhip_peer_access(int32_t peer_device, int32_t* can_access);
+int uavhip_ipc_export(const void* ptr, void* handle, uint64_t* offset);
+int uavhip_ipc_open(const void* handle, uint64_t offset, void** ptr);
+int uavhip_ipc_close(void* base);
+int uavhip_copy_async(void* dst, const void* src, uint64_t bytes, uavhip_stream_t stream);
+
 /* ---------------------------------------------------------------- misc */
 const char* uavhip_last_error(void);
 /* 4 since round 3 (struct uavhip_ppo: the Adam hyper-parameters are doubles; the inference packed

@@ -1,6 +1,9 @@
 """A bare rollout for profiling: ITERS eager iterations of RolloutEngine at the bench's shape (one
 k_rollout_steps launch of T steps each, + bootstrap forward + GAE + scene refresh), nothing else.
-UAVHIP_LIB selects the library build (product / TRACE / NOENV). Prints one JSON line."""
+UAVHIP_LIB selects the library build (product / TRACE / NOENV). Prints one JSON line: host wall time
+per iteration and the median over the iterations of the k_rollout_steps launch per step (HIP events
+on the launch stream, bench.py's measure). bench.py runs this as a child process on the product and
+the NOENV builds to price the env step by its compiled-out differential."""
 import json
 import os
 import sys
@@ -23,13 +26,18 @@ def main():
     env = VecUAVEnv(E, N, M, 1, 1, seed=1, full_reset_period=200)
     eng = RolloutEngine(env, net, horizon=T, persistent=True)
     eng.start()
+    eng.enable_events()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    steps = []
     for _ in range(iters):
         eng.collect(eager=True)
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        steps.append(eng.event_ms()[0][0])
     dt = time.perf_counter() - t0
+    warm = steps[1:] if len(steps) > 1 else steps  # the first launch warms up
     print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), "iters": iters, "ms_per_iter": dt / iters * 1e3,
+                      "step_ms": sorted(warm)[len(warm) // 2], "step_ms_all": steps,
                       "shape": [E, N, M, T]}), flush=True)
 
 

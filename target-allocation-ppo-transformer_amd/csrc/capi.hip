@@ -1,6 +1,7 @@
 // capi.hip -- error plumbing and ABI version of libuavhip.so (see include/uavhip.h).
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
 
 #include "common.hpp"
 
@@ -26,3 +27,101 @@ int check_launch(const char* what) {
 
 extern "C" const char* uavhip_last_error(void) { return uavhip::g_err; }
 extern "C" int32_t uavhip_abi_version(void) { return 4; }
+
+// ------------------------------------------------------------------ the N > 1 trajectory exchange
+// Peer-to-peer plumbing for uavhip.dist.IpcAllGather: a rank exports its send buffers
+// as IPC handles, every other rank opens them into ITS OWN device's address space (no context on the
+// exporter's device) after checking and enabling peer access, and copies out of them on a stream of
+// its own device.
+extern "C" int uavhip_peer_access(int32_t peer_device, int32_t* can_access) {
+    int cur = 0, can = 0;
+    if (!can_access) {
+        uavhip::set_error("uavhip_peer_access: NULL pointer");
+        return UAVHIP_EINVAL;
+    }
+    *can_access = 0;
+    if (hipGetDevice(&cur) != hipSuccess) {
+        uavhip::set_error("uavhip_peer_access: hipGetDevice failed");
+        return UAVHIP_EHIP;
+    }
+    if (peer_device == cur) {  // the same device (several ranks on one GPU): no peer mapping needed
+        *can_access = 1;
+        return UAVHIP_OK;
+    }
+    if (hipDeviceCanAccessPeer(&can, cur, peer_device) != hipSuccess) {
+        uavhip::set_error("uavhip_peer_access: hipDeviceCanAccessPeer(%d, %d) failed", cur, peer_device);
+        return UAVHIP_EHIP;
+    }
+    if (!can) return UAVHIP_OK;
+    const hipError_t e = hipDeviceEnablePeerAccess(peer_device, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+        (void)hipGetLastError();
+        uavhip::set_error("uavhip_peer_access: hipDeviceEnablePeerAccess(%d) from %d: %s", peer_device, cur,
+                          hipGetErrorString(e));
+        return UAVHIP_EHIP;
+    }
+    (void)hipGetLastError();  // clear an already-enabled status
+    *can_access = 1;
+    return UAVHIP_OK;
+}
+
+extern "C" int uavhip_ipc_export(const void* ptr, void* handle, uint64_t* offset) {
+    if (!ptr || !handle || !offset) {
+        uavhip::set_error("uavhip_ipc_export: NULL pointer");
+        return UAVHIP_EINVAL;
+    }
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess) {
+        uavhip::set_error("uavhip_ipc_export: hipMemGetAddressRange failed");
+        return UAVHIP_EHIP;
+    }
+    hipIpcMemHandle_t h;
+    const hipError_t e = hipIpcGetMemHandle(&h, (void*)base);
+    if (e != hipSuccess) {
+        uavhip::set_error("uavhip_ipc_export: hipIpcGetMemHandle: %s", hipGetErrorString(e));
+        return UAVHIP_EHIP;
+    }
+    static_assert(sizeof(h) == UAVHIP_IPC_HANDLE_BYTES, "IPC handle size");
+    memcpy(handle, &h, sizeof h);
+    *offset = (uint64_t)((const char*)ptr - (const char*)base);
+    return UAVHIP_OK;
+}
+
+extern "C" int uavhip_ipc_open(const void* handle, uint64_t offset, void** ptr) {
+    if (!handle || !ptr) {
+        uavhip::set_error("uavhip_ipc_open: NULL pointer");
+        return UAVHIP_EINVAL;
+    }
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof h);
+    void* base = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+        uavhip::set_error("uavhip_ipc_open: hipIpcOpenMemHandle: %s", hipGetErrorString(e));
+        return UAVHIP_EHIP;
+    }
+    *ptr = (char*)base + offset;
+    return UAVHIP_OK;
+}
+
+extern "C" int uavhip_ipc_close(void* base) {
+    if (hipIpcCloseMemHandle(base) != hipSuccess) {
+        uavhip::set_error("uavhip_ipc_close: hipIpcCloseMemHandle failed");
+        return UAVHIP_EHIP;
+    }
+    return UAVHIP_OK;
+}
+
+extern "C" int uavhip_copy_async(void* dst, const void* src, uint64_t bytes, uavhip_stream_t stream) {
+    if ((!dst || !src) && bytes) {
+        uavhip::set_error("uavhip_copy_async: NULL pointer");
+        return UAVHIP_EINVAL;
+    }
+    const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+    if (e != hipSuccess) {
+        uavhip::set_error("uavhip_copy_async: %s", hipGetErrorString(e));
+        return UAVHIP_EHIP;
+    }
+    return UAVHIP_OK;
+}

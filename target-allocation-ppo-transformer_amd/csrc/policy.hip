@@ -2732,6 +2732,10 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     float* dzc = sm.ctx + 64;            // critic dz rows
     float* zs = sm.big;                  // relu(head.0) rows of both heads [2][16][64]
     const float inv = 1.0f / (float)io.Bg;
+    // the gradient path's 1/Bg pre-scaled by the power of two io.gscale (BwdIO::gscale): gradients
+    // leave this function gscale x the loss's, bit for bit (power-of-two scaling commutes with every
+    // rounding), and stay that way through the linear backward until k_reduce_grads' 1/gscale
+    const float ginv = inv * io.gscale;
     // the four loss sums (used by wave 0 only): from the all-reduced buffer, or summed here from
     // the forward's workgroup partials with k_loss_sums' exact order (train.hip)
     // every global input issued before the first use: z rows (one float4 per thread), the head.2
@@ -2776,12 +2780,12 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         const float A = o[4], lo = 1.f - io.eps_clip, hi = 1.f + io.eps_clip;
         const float s1 = ratio * A;
         const float s2 = fminf(fmaxf(ratio, lo), hi) * A;
-        const float gmin = -inv;  // d(-mean(min)) / d min_i
+        const float gmin = -ginv;  // d(-mean(min)) / d min_i (x gscale)
         const float g1 = s1 < s2 ? gmin : (s1 == s2 ? 0.5f * gmin : 0.f);
         const float g2 = s2 < s1 ? gmin : (s1 == s2 ? 0.5f * gmin : 0.f);
         const float gr = g1 * A + ((ratio >= lo && ratio <= hi) ? g2 * A : 0.f);
         const float glogp = gr * ratio;
-        const float gent = -io.entropy_coef * inv;
+        const float gent = -io.entropy_coef * ginv;
         // back through lc = log(clamp(p)), ent = -sum(lc * p), p = y / s, s = y0 + y1, y = softmax
         float glc0 = -gent * c.p0, glc1 = -gent * c.p1;
         if (act) glc1 += glogp; else glc0 += glogp;
@@ -2800,8 +2804,8 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         const float w2 = L2 > L1 ? 1.f : (L1 == L2 ? 0.5f : 0.f);
         gs[4 * p + 0] = pad ? 0.f : c.y0 * (gy0 - dot);
         gs[4 * p + 1] = pad ? 0.f : c.y1 * (gy1 - dot);
-        gs[4 * p + 2] = pad ? 0.f : io.value_coef * (w1 * 2.f * (v - R) * inv +
-                                         ((dv >= -io.eps_clip && dv <= io.eps_clip) ? w2 * 2.f * (vc - R) * inv : 0.f));
+        gs[4 * p + 2] = pad ? 0.f : io.value_coef * (w1 * 2.f * (v - R) * ginv +
+                                         ((dv >= -io.eps_clip && dv <= io.eps_clip) ? w2 * 2.f * (vc - R) * ginv : 0.f));
         if (p == 0 && blk == 0 && role != 2 && io.stats) {
             io.stats[0] += (double)(-tot0 * inv);
             io.stats[1] += (double)fmaxf(L1, L2);

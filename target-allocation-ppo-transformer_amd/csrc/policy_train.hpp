@@ -69,6 +69,11 @@ struct BwdIO {
     double* stats;           // += loss_actor, loss_critic, entropy, 1 (workgroup 0)
     float eps_clip, value_coef, entropy_coef;
     int Bg;                  // samples in the global minibatch
+    // every gradient the backward writes is pre-scaled by gscale = the power of two >= Bg (the
+    // loss's 1/Bg folded in as gscale/Bg, exact): per-sample gradients O(1) instead of O(1/Bg), so
+    // the dX GEMMs' fp16 operand planes stay above the fp16 subnormal range (x2 = f16((x - x1) 2^11)
+    // loses relative accuracy below 2^-14); k_reduce_grads multiplies by 1/gscale (exact)
+    float gscale;
     const float* xg;         // [R][16] input windows (TrainIO::xg)
     const float* mask;       // [R] key padding mask
     const float* e[2];       // [R][128] embeddings after ReLU

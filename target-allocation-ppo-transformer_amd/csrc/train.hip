@@ -115,9 +115,12 @@ struct SegBatch {
     Segment s[kMaxSegs];
     int n;
 };
+// unscale = 1 / BwdIO::gscale (a power of two: exact): the backward's partials carry the pre-scaled
+// gradient, the flat buffer the loss's.
 __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* __restrict__ grads,
                                                       float* __restrict__ sq_part, double* __restrict__ step,
-                                                      const AdamHyper h, AdamScalars* __restrict__ sc) {
+                                                      const AdamHyper h, AdamScalars* __restrict__ sc,
+                                                      const float unscale) {
     __shared__ float red[4];
     __shared__ float wsum[4][64];
     // segment of this block: lane l tests segment l (one round of kernarg loads, not a dependent
@@ -148,7 +151,7 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
         wsum[wv][l] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
         __syncthreads();
         if (wv == 0 && i < S_.count) {
-            const float tot = (wsum[0][l] + wsum[1][l]) + (wsum[2][l] + wsum[3][l]);
+            const float tot = ((wsum[0][l] + wsum[1][l]) + (wsum[2][l] + wsum[3][l])) * unscale;
             grads[dsti(i)] = tot;
             sq = tot * tot;
         }
@@ -163,13 +166,14 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
                 for (int u = 0; u < 4; ++u) acc[u] += *reinterpret_cast<const f32x4*>(part(p + u) + i);
             }
             for (; p < S_.parts; ++p) acc[0] += *reinterpret_cast<const f32x4*>(part(p) + i);
-            const f32x4 tot = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+            const f32x4 tot = ((acc[0] + acc[1]) + (acc[2] + acc[3])) * unscale;
             *reinterpret_cast<f32x4*>(grads + dsti(i)) = tot;
             sq = (tot[0] * tot[0] + tot[1] * tot[1]) + (tot[2] * tot[2] + tot[3] * tot[3]);
         } else {
             for (int e = i; e < S_.count; ++e) {  // the ragged end of the segment
                 float tot = 0.f;
                 for (int p = 0; p < S_.parts; ++p) tot += part(p)[e];
+                tot *= unscale;
                 grads[dsti(e)] = tot;
                 sq += tot * tot;
             }
@@ -186,7 +190,7 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
                 for (int u = 0; u < 4; ++u) acc[u] += part(p + u)[i];
             }
             for (; p < S_.parts; ++p) acc[0] += part(p)[i];
-            const float tot = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+            const float tot = ((acc[0] + acc[1]) + (acc[2] + acc[3])) * unscale;
             grads[dsti(i)] = tot;
             sq = tot * tot;
         }
@@ -475,6 +479,16 @@ inline Plan make_plan(int Bm, float* base) {
 }
 
 
+// The backward's gradient pre-scale (BwdIO::gscale): the power of two >= the global minibatch
+// (UAVHIP_GRAD_PRESCALE=0: 1, the unscaled backward, for the per-element precision test's A/B).
+inline float grad_prescale(int Bg) {
+    const char* e = std::getenv("UAVHIP_GRAD_PRESCALE");
+    if (e && e[0] == '0') return 1.0f;
+    int s = 1;
+    while (s < Bg && s < (1 << 30)) s <<= 1;
+    return (float)s;
+}
+
 inline const float* prm(const uavhip_ppo* c, int i) { return c->params + kOffs.o[i]; }
 inline AdamHyper adam_hyper(const uavhip_ppo* c) { return AdamHyper{c->lr_actor, c->lr_critic, c->beta1, c->beta2}; }
 
@@ -625,6 +639,7 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         io.value_coef = c->value_coef;
         io.entropy_coef = c->entropy_coef;
         io.Bg = Bg;
+        io.gscale = grad_prescale(Bg);
         io.xg = p.xg;
         io.mask = p.mask;
         io.e[0] = p.e_a;
@@ -748,7 +763,7 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
     }
     // padding floats between parameters stay zero
     hipLaunchKernelGGL(k_reduce_grads, dim3(seg_blocks), dim3(256), 0, st, sb, c->grads, p.sq_part, step, adam_hyper(c),
-                       p.adam_sc);
+                       p.adam_sc, 1.0f / grad_prescale(Bg));
     *n_sq = seg_blocks;
     return check_launch("k_reduce_grads");
 }

@@ -104,6 +104,11 @@ _SIGS = {
     "uavhip_ppo_workspace_floats": (ctypes.c_int64, [_i32]),
     "uavhip_ppo_step": (ctypes.c_int, [ctypes.POINTER(PPODesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
     "uavhip_episode_stats": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _i32, _vp, _vp]),
+    "uavhip_peer_access": (ctypes.c_int, [_i32, ctypes.POINTER(_i32)]),
+    "uavhip_ipc_export": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
+    "uavhip_ipc_open": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_vp)]),
+    "uavhip_ipc_close": (ctypes.c_int, [_vp]),
+    "uavhip_copy_async": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp]),
     "uavhip_last_error": (ctypes.c_char_p, []),
     "uavhip_abi_version": (_i32, []),
 }

@@ -23,7 +23,7 @@ def shard(total, world, rank):
     return start, base + (1 if rank < extra else 0)
 
 
-def resolve_shards(E, env_base, total_envs=None, group=None):
+def resolve_shards(E, env_base, total_envs=None, group=None, device=None):
     """Total env count of a data-parallel rollout, checked across the ranks (once, at engine setup).
 
     Every rank's env block [env_base, env_base + E) must be disjoint from the others' and inside
@@ -31,7 +31,9 @@ def resolve_shards(E, env_base, total_envs=None, group=None):
     the ranks, and T * total is the element count of the global advantage moments (ppo.py:94). With
     torch.distributed initialised (world > 1) the blocks are all-gathered and total defaults to the
     sum of every rank's E; a mismatch (e.g. every rank left at env_base 0) raises instead of sampling
-    duplicate actions or normalising with a wrong count. One process: total_envs or E."""
+    duplicate actions or normalising with a wrong count. One process: total_envs or E.
+    Collective over `group` (every rank of it must call it); on an RCCL group the exchanged tensor
+    lives on `device` (the env's device; default the current device)."""
     E, env_base = int(E), int(env_base)
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         total = E if total_envs is None else int(total_envs)
@@ -39,7 +41,8 @@ def resolve_shards(E, env_base, total_envs=None, group=None):
             raise ValueError(f"env block [{env_base}, {env_base + E}) outside total_envs {total}")
         return total
     world = dist.get_world_size(group)
-    dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
+    dev = "cpu" if dist.get_backend(group) == "gloo" else (
+        torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device()))
     mine = torch.tensor([[E, env_base]], dtype=torch.int64, device=dev)
     blocks = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(blocks, mine, group=group)
@@ -127,6 +130,71 @@ def normalize_global(adv, moments, count=None):
     return adv
 
 
+class HipPeerMapper:
+    """The device side of IpcAllGather over the C ABI (include/uavhip.h, N > 1 exchange): export a
+    send buffer as an IPC handle, check / enable peer access to another device, map a peer's buffer
+    into THIS device's address space (hipIpcOpenMemHandle from the current device: no HIP context
+    is created on the exporter's device) and copy out of it on a stream of this device."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self._maps = {}  # handle bytes -> [base pointer, references]: two buffers of one allocation map once
+
+    def device_index(self):
+        return self.device.index if self.device.index is not None else torch.cuda.current_device()
+
+    def alloc(self, shape):
+        return torch.zeros(*shape, dtype=torch.float32, device=self.device)
+
+    def sync(self):
+        torch.cuda.synchronize(self.device)
+
+    def export(self, t):
+        import ctypes
+        from ._lib import LIB, check
+        h = (ctypes.c_char * 64)()
+        off = ctypes.c_uint64(0)
+        check(LIB.uavhip_ipc_export(t.data_ptr(), h, ctypes.byref(off)), "uavhip_ipc_export")
+        return bytes(h), int(off.value)
+
+    def can_access(self, peer_device):
+        import ctypes
+        from ._lib import LIB, check
+        ok = ctypes.c_int32(0)
+        with torch.cuda.device(self.device):
+            check(LIB.uavhip_peer_access(int(peer_device), ctypes.byref(ok)), "uavhip_peer_access")
+        return bool(ok.value)
+
+    def open(self, handle):
+        import ctypes
+        from ._lib import LIB, check
+        h, off = handle
+        if h not in self._maps:
+            p = ctypes.c_void_p(0)
+            with torch.cuda.device(self.device):
+                check(LIB.uavhip_ipc_open(h, 0, ctypes.byref(p)), "uavhip_ipc_open")
+            self._maps[h] = [int(p.value), 0]
+        self._maps[h][1] += 1
+        return (self._maps[h][0] + off, h)
+
+    def close(self, mapped):
+        from ._lib import LIB
+        ent = self._maps.get(mapped[1])
+        if ent is None:
+            return
+        ent[1] -= 1
+        if ent[1] == 0:
+            with torch.cuda.device(self.device):
+                LIB.uavhip_ipc_close(ent[0])
+            del self._maps[mapped[1]]
+
+    def copy(self, dst, mapped, stream):
+        """dst (a tensor of this device) <- the mapped peer buffer, on `stream`."""
+        from ._lib import LIB, check
+        check(LIB.uavhip_copy_async(dst.data_ptr(), mapped[0], dst.numel() * dst.element_size(),
+                                    stream.cuda_stream), "uavhip_copy_async")
+
+
 class IpcAllGather:
     """The trajectory all-gather as peer-to-peer copies out of IPC-mapped buffers, pipelined one
     iteration behind the rollout so that iteration k's exchange runs beside iteration k + 1's
@@ -134,50 +202,74 @@ class IpcAllGather:
     which holds every CU, while a device-to-device copy between two GPUs is a DMA transfer.
 
     Every rank owns two send buffers (iteration parity p) that the other ranks map through IPC
-    (hipIpcGetMemHandle; handles exchanged over `group`, a gloo group) and two receive buffers
-    [world, floats]. submit(payload) enqueues the copy of this iteration's payload into send[p] on
-    the current stream. progress() completes the pending exchange: the host waits until its payload
-    is written and its copies of the previous iteration are done, a host barrier (every rank: both),
-    then a side stream copies every peer's send[p] into recv[p] (and its own). Send buffers are
-    rewritten only after every rank passed the barrier that follows the copies reading them, so no
-    interprocess events are needed. Call progress() after enqueueing the next iteration's work: the
-    host wait returns as that work starts, and the copies run beside it."""
+    (handles exchanged over `group`, a gloo group) and two receive buffers [world, floats]. Setup
+    checks peer access from this rank's device to every other rank's device (hipDeviceCanAccessPeer,
+    then hipDeviceEnablePeerAccess) and maps each peer buffer into this device's own address space
+    (no HIP context on any other device). submit(payload) enqueues the copy of this iteration's
+    payload into send[p] on the current stream. progress() completes the pending exchange: the host
+    waits until its payload is written and its copies of the previous iteration are done, a host
+    barrier (every rank: both), then the side stream -- a stream of this rank's device -- copies every
+    peer's send[p] into recv[p] (and its own). Send buffers are rewritten only after every rank passed
+    the barrier that follows the copies reading them, so no interprocess events are needed. Call
+    progress() after enqueueing the next iteration's work: the host wait returns as that work
+    starts, and the copies run beside it.
 
-    def __init__(self, floats, device, group):
+    `mapper` supplies the device operations (default HipPeerMapper; the CPU tests inject fakes)."""
+
+    def __init__(self, floats, device, group, mapper=None):
         """Collective over `group`: every rank takes part in the same calls whether or not its own
-        setup fails, and all of them raise if any rank's did (no rank is left waiting)."""
-        from torch.multiprocessing.reductions import rebuild_cuda_tensor, reduce_tensor
+        setup fails, and all of them raise if any rank's did (allocation, export, a pair of devices
+        without peer access, or a mapping that fails) -- bench.py then falls back to RCCL's
+        all-gather on every rank."""
         self.world, self.rank, self.group = dist.get_world_size(group), dist.get_rank(group), group
         self.floats, self.device = int(floats), device
-        err, handles = None, None
+        self.mapper = mapper if mapper is not None else HipPeerMapper(device)
+        err, mine = None, None
         try:
-            f32 = dict(dtype=torch.float32, device=device)
-            self.send = [torch.zeros(self.floats, **f32) for _ in range(2)]
-            self.recv = [torch.zeros(self.world, self.floats, **f32) for _ in range(2)]
-            torch.cuda.synchronize(device)
-            handles = [reduce_tensor(t)[1] for t in self.send]
-        except Exception as exc:
+            self.send = [self.mapper.alloc((self.floats,)) for _ in range(2)]
+            self.recv = [self.mapper.alloc((self.world, self.floats)) for _ in range(2)]
+            self.mapper.sync()
+            mine = (self.mapper.device_index(), [self.mapper.export(t) for t in self.send])
+        except Exception as exc:  # noqa: BLE001 -- reported collectively below
             err = exc
         objs = [None] * self.world
-        dist.all_gather_object(objs, handles, group=group)
+        dist.all_gather_object(objs, mine, group=group)
         if err is None and any(o is None for o in objs):
-            err = RuntimeError("IpcAllGather: another rank could not export its buffers")
+            err = RuntimeError("another rank could not export its buffers")
+        self.peer_devices = {j: o[0] for j, o in enumerate(objs) if o is not None}
+        self.peer_send = {}
         if err is None:
             try:
-                self.peer_send = {j: [rebuild_cuda_tensor(*a) for a in bufs] for j, bufs in enumerate(objs)
-                                  if j != self.rank}
-            except Exception as exc:
+                no_peer = [j for j, o in enumerate(objs) if j != self.rank and not self.mapper.can_access(o[0])]
+                if no_peer:
+                    raise RuntimeError(f"no peer access from device {mine[0]} to the devices of ranks {no_peer} "
+                                       f"({[objs[j][0] for j in no_peer]})")
+                self.peer_send = {j: [self.mapper.open(h) for h in o[1]] for j, o in enumerate(objs) if j != self.rank}
+            except Exception as exc:  # noqa: BLE001
                 err = exc
         oks = [None] * self.world
-        dist.all_gather_object(oks, err is None, group=group)
-        if err is not None or not all(oks):
-            raise RuntimeError(f"IpcAllGather setup failed on {'this' if err else 'another'} rank: {err!r}")
-        self.side = torch.cuda.Stream(device)
-        self.packed = [torch.cuda.Event(), torch.cuda.Event()]
+        dist.all_gather_object(oks, None if err is None else repr(err), group=group)
+        bad = {j: e for j, e in enumerate(oks) if e is not None}
+        if bad:
+            self.close()
+            raise RuntimeError(f"IpcAllGather setup failed on {'this' if err else 'another'} rank: "
+                               f"{ {j: e for j, e in bad.items()} }")
+        self.side = torch.cuda.Stream(device) if self.device.type == "cuda" else None
+        self.packed = [torch.cuda.Event(), torch.cuda.Event()] if self.side is not None else [None, None]
         self.copied = [None, None]
         self.k = 0
         self.pending = None
         dist.barrier(group=group)
+
+    def close(self):
+        """Unmap the peers' buffers (collective use: after the last progress())."""
+        for bufs in getattr(self, "peer_send", {}).values():
+            for m in bufs:
+                try:
+                    self.mapper.close(m)
+                except Exception:  # noqa: BLE001 -- teardown
+                    pass
+        self.peer_send = {}
 
     def submit(self, payload):
         """Enqueue this iteration's flat fp32 payload (current stream); progress() exchanges it."""
@@ -202,8 +294,8 @@ class IpcAllGather:
         self.side.wait_event(self.packed[p])
         with torch.cuda.stream(self.side):
             self.recv[p][self.rank].copy_(self.send[p])
-            for j in sorted(self.peer_send):
-                self.recv[p][j].copy_(self.peer_send[j][p])
+            for j in sorted(self.peer_send):  # every copy on the side stream of THIS device
+                self.mapper.copy(self.recv[p][j], self.peer_send[j][p], self.side)
         ev = torch.cuda.Event()
         ev.record(self.side)
         self.copied[p] = ev

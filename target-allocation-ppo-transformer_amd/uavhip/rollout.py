@@ -43,7 +43,7 @@ class Trajectory:
 
 class RolloutEngine:
     def __init__(self, env, policy, horizon, want_info=True, bootstrap=True, seed=None, normalize=True, row_cache=True,
-                 fused_step=None, total_envs=None, persistent=None):
+                 fused_step=None, total_envs=None, persistent=None, group=None):
         """normalize=False leaves the advantages raw after GAE: a data-parallel caller normalises
         them with the moments of the whole data-parallel batch in normalize_global() (called by
         gather()) (ppo.py:94).
@@ -57,7 +57,11 @@ class RolloutEngine:
         torch's RNG). Sampling counters are global env indices: step t of env e draws counter
         t * total_envs + env.env_base + e, so a rank's shard (VecUAVEnv(env_base=shard start),
         total_envs = all ranks' envs, the same seed everywhere) samples exactly what the same envs
-        sample in one process over the union, and no two ranks share a counter."""
+        sample in one process over the union, and no two ranks share a counter.
+        group: the torch.distributed process group of the data-parallel rollout (default: WORLD).
+        Construction is COLLECTIVE over it when torch.distributed is initialised (resolve_shards
+        all-gathers every rank's env block): build the engine on every rank of `group` at the same
+        point; normalize_global / gather / gather_submit use the same group by default."""
         self.env = env
         self.normalize = normalize
         self.iteration = 0
@@ -72,7 +76,8 @@ class RolloutEngine:
         # world > 1: the ranks' env blocks are all-gathered and checked (disjoint, tiling total), and
         # total defaults to their sum -- the sampling counters and the global advantage count use it
         from .dist import resolve_shards
-        self.total = resolve_shards(env.E, self.env_base, total_envs)
+        self.group = group
+        self.total = resolve_shards(env.E, self.env_base, total_envs, group=group, device=env.device)
         self.traj = Trajectory(self.T, env.E, env.device, want_info)
         self.counter = torch.zeros(1, dtype=torch.int64, device=env.device)  # sampling counter base
         # window-row projections of the obs windows (policy.rowproj_buffer): the windows of one
@@ -213,6 +218,7 @@ class RolloutEngine:
         with them (ppo.py:94 normalises over the whole batch). Once per iteration; a no-op when the
         engine normalised locally (one rank)."""
         from .dist import global_moments, normalize_global
+        group = self.group if group is None else group
         if self.normalize or self._normalized == self.iteration:
             return self.traj
         tr = self.traj
@@ -228,6 +234,7 @@ class RolloutEngine:
         as a dict of [world * T * E, ...] tensors (obs, actions, logp, values, returns, advantages,
         dones) in (rank, step, env) order."""
         from .dist import all_gather_rows, pack_compact, unpack_compact
+        group = self.group if group is None else group
         if self._gathered[0] == self.iteration:  # once per iteration (normalises in place)
             batch, ev = self._gathered[1], self._gathered[2]
             if ev is not None:  # from the pipelined exchange: complete on its side stream
@@ -249,7 +256,7 @@ class RolloutEngine:
         and enqueue this iteration's compact payload; gather_finish() completes the exchange -- call
         it after enqueueing the next iteration's rollout, beside which the copies then run."""
         from .dist import pack_compact
-        tr = self.normalize_global(group)
+        tr = self.normalize_global(self.group if group is None else group)
         exchange.submit(pack_compact(tr.obs, tr.actions, tr.logp, tr.values, tr.ret, tr.adv, tr.dones))
         self._submitted = self.iteration
 

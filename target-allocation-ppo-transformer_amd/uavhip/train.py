@@ -207,41 +207,65 @@ class FusedPPOTrainer:
         self.step(_lib.PPO_FORWARD | _lib.PPO_BACKWARD)
         return self.grads
 
+    #: an epoch of more minibatch steps than this is replayed as chunks of one captured graph of this
+    #: many steps (each chunk's rows copied into the front of the permutation buffer first), so the
+    #: reference's minibatch 64 over a whole rollout (4,096 steps per epoch at 4096 envs x 64) needs
+    #: no 37 k-node graph
+    max_graph_steps = 256
+
     def capture(self):
-        """Capture one epoch (every minibatch step of the current buffer length) into a hipGraph; a
-        data-parallel epoch with its RCCL all-reduces (every rank captures the same sequence, so the
-        replays meet in the same collectives)."""
+        """Capture one epoch (every minibatch step of the current buffer length, or a chunk of
+        max_graph_steps of them) into a hipGraph; a data-parallel epoch with its RCCL all-reduces
+        (every rank captures the same sequence, so the replays meet in the same collectives).
+        Data parallel: the ranks vote on the capture (an all-reduce of a success flag after it); if
+        any rank failed, every rank drops its graph and returns None, and run() steps eagerly on all
+        of them -- no rank can go on into replays the others never join."""
         if self.dp and not self.graph_collectives:
             raise RuntimeError("graph capture of the data-parallel step needs torch.distributed's all-reduce on "
                                "an RCCL ('nccl') group; gloo collectives run eagerly")
         if self.dp and self.n_local is not None:
             raise RuntimeError("set_shard() epochs resize per epoch: they run eagerly")
-        steps = self.n // self.global_minibatch
+        steps = min(self.n // self.global_minibatch, self.max_graph_steps)
         if self.dp:  # the communicator is created at its first collective, which must not be in a capture
             self.allreduce(torch.zeros(1, dtype=torch.float32, device=self.device))
             torch.cuda.synchronize()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        g = torch.cuda.CUDAGraph()
-        # thread_local: the process group's watchdog thread keeps polling its events during the capture
-        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local" if self.dp else "global"):
-            for b in range(steps):  # one epoch: every minibatch step
-                if self.dp:
-                    self.ddp_step(self._rows(self.perm, b), self._packed(b))
-                else:
-                    self.step(_lib.PPO_FULL | self._packed(b), self._rows(self.perm, b))
-        torch.cuda.current_stream().wait_stream(s)
+        g, err = None, None
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            # thread_local: the process group's watchdog thread keeps polling its events during the capture
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local" if self.dp else "global"):
+                for b in range(steps):  # one epoch (or chunk): every minibatch step
+                    if self.dp:
+                        self.ddp_step(self._rows(self.perm, b), self._packed(b))
+                    else:
+                        self.step(_lib.PPO_FULL | self._packed(b), self._rows(self.perm, b))
+            torch.cuda.current_stream().wait_stream(s)
+        except Exception as exc:  # noqa: BLE001 -- data parallel: voted on below, then re-raised / eager
+            g, err = None, exc
+        if self.dp:
+            ok = torch.tensor([0.0 if g is None else 1.0], dtype=torch.float32, device=self.device)
+            self.allreduce(ok)
+            if int(ok.item()) != self.world:
+                self.graphs.pop(steps, None)
+                return None
+        elif err is not None:
+            raise err
         self.graphs[steps] = g
         return g
 
     @property
     def graph(self):
-        return self.graphs.get(self.n // self.global_minibatch)
+        return self.graphs.get(min(self.n // self.global_minibatch, self.max_graph_steps))
 
     def run(self, epochs=None, generator=None, use_graph=True, perms=None):
         """K epochs of minibatch steps over the buffers -> (mean actor loss, critic loss, entropy, n_steps).
         Minibatch order: torch.randperm(n, generator) per epoch (SubsetRandomSampler's draw,
-        ppo.py:115), or the given `perms` ([epochs][n] row orders, e.g. recorded from the reference)."""
+        ppo.py:115), or the given `perms` ([epochs][n] row orders, e.g. recorded from the reference).
+        Epochs of more than max_graph_steps steps replay the chunk graph once per chunk (its rows
+        copied device-to-device into the front of the permutation buffer before each replay) and step
+        the remainder eagerly: the same steps in the same order as one epoch graph."""
         epochs = cfg.K_EPOCHS if epochs is None else epochs
         if perms is not None:
             perms = [torch.as_tensor(p, dtype=torch.int32) for p in perms]
@@ -255,26 +279,46 @@ class FusedPPOTrainer:
         graph = self.graph if use_graph else None
         if use_graph and graph is None and steps > 0:
             graph = self.capture()
+        chunk = min(steps, self.max_graph_steps)
+        Bg = self.global_minibatch
+        order_dev = None
+        if graph is not None and steps > chunk:
+            order_dev = torch.empty(self.n, dtype=torch.int32, device=self.device)
         self.stats.zero_()
         cnt = 0
         for ep in range(epochs):
             order = perms[ep] if perms is not None else torch.randperm(self.n, generator=generator)
-            self.perm[:self.n].copy_(order)
-            if graph is not None:
-                graph.replay()
-                cnt += steps
+            if order_dev is None:
+                self.perm[:self.n].copy_(order)
+                if graph is not None:
+                    graph.replay()
+                    cnt += steps
+                    continue
+                for b in range(steps):
+                    self._eager_step(self.perm, b)
+                    cnt += 1
                 continue
-            for b in range(steps):
-                if not self.dp:
-                    self.step(_lib.PPO_FULL | self._packed(b), self._rows(self.perm, b))
-                else:
-                    self.ddp_step(self._rows(self.perm, b), self._packed(b))
+            order_dev.copy_(order)
+            for c in range(steps // chunk):  # whole chunks: the chunk graph over perm[:chunk * Bg]
+                self.perm[:chunk * Bg].copy_(order_dev[c * chunk * Bg:(c + 1) * chunk * Bg])
+                graph.replay()
+                cnt += chunk
+            for b in range(steps - steps % chunk, steps):  # the ragged rest, eager
+                self._eager_step(order_dev, b)
                 cnt += 1
         self.policy._packed_key = None  # parameters changed under torch's version counters: repack
         if cnt == 0:
             return 0.0, 0.0, 0.0, 0
         st = self.stats.tolist()
         return st[0] / st[3], st[1] / st[3], st[2] / st[3], cnt
+
+    def _eager_step(self, perm, b):
+        """Minibatch step b of the order in perm, launched directly (the first step of an epoch
+        repacks; later ones reuse the copies the previous UPDATE refreshed)."""
+        if not self.dp:
+            self.step(_lib.PPO_FULL | self._packed(b), self._rows(perm, b))
+        else:
+            self.ddp_step(self._rows(perm, b), self._packed(b))
 
     def _run_shard(self, epochs, generator, perms, steps):
         """run() over a set_shard() batch: per epoch the global order (the same on every rank), this

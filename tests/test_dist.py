@@ -138,6 +138,10 @@ def _shard_worker(rank, world, port, q, bases):
                 out[key] = resolve_shards(cnt, base, total_envs=total)
             except ValueError as exc:
                 out[key] = "ValueError: " + str(exc)
+        # a sub-group (RolloutEngine(group=...)): only its ranks take part, the total is theirs
+        sub = dist.new_group([0, 1])  # collective over the world
+        if rank < 2:
+            out["subgroup"] = resolve_shards(4, 4 * rank, group=sub)
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
@@ -166,6 +170,8 @@ def test_resolve_shards_checks_the_rank_blocks():
         assert str(out["same_base"]).startswith("ValueError") and "disjoint" in out["same_base"]
         assert str(out["bad_total"]).startswith("ValueError")
         assert out["custom"] == 10  # disjoint blocks in any rank order are fine
+        if r < 2:
+            assert out["subgroup"] == 8  # the sub-group's two blocks, not the world's
 
 
 def test_resolve_shards_single_process():
@@ -179,7 +185,40 @@ def test_resolve_shards_single_process():
         resolve_shards(7, 4, total_envs=10)
 
 
-def _ipc_setup_worker(rank, world, port, q):
+class _FakeMapper:
+    """CPU stand-in for uavhip.dist.HipPeerMapper: device `dev`, allocation failing when asked to,
+    peer access from this device to the devices in `no_peer` refused."""
+
+    def __init__(self, dev, fail_alloc=False, no_peer=()):
+        self.dev, self.fail_alloc, self.no_peer = dev, fail_alloc, set(no_peer)
+        self.opened, self.closed = [], []
+
+    def device_index(self):
+        return self.dev
+
+    def alloc(self, shape):
+        if self.fail_alloc:
+            raise RuntimeError("out of memory (simulated)")
+        return torch.zeros(*shape)
+
+    def sync(self):
+        pass
+
+    def export(self, t):
+        return (b"h" * 64, 0)
+
+    def can_access(self, peer):
+        return peer == self.dev or peer not in self.no_peer
+
+    def open(self, handle):
+        self.opened.append(handle)
+        return (len(self.opened), 0)
+
+    def close(self, m):
+        self.closed.append(m)
+
+
+def _ipc_setup_worker(rank, world, port, q, case):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "target-allocation-ppo-transformer_amd"))
@@ -189,29 +228,59 @@ def _ipc_setup_worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        torch.cuda.synchronize = lambda *a, **k: None  # no GPU here: rank 0 exports host buffers
+        if case == "alloc":      # rank 1 cannot allocate its buffers
+            m = _FakeMapper(rank, fail_alloc=rank == 1)
+        elif case == "peer":     # rank 2's device has no peer access to rank 0's
+            m = _FakeMapper(rank, no_peer=(0,) if rank == 2 else ())
+        else:                    # every pair has peer access (one device per rank)
+            m = _FakeMapper(rank)
         try:
-            IpcAllGather(16 if rank == 0 else -1, torch.device("cpu"), None)  # rank 1 fails to allocate
-            q.put((rank, "no error"))
+            x = IpcAllGather(16, torch.device("cpu"), None, mapper=m)
+            q.put((rank, ("ok", sorted(x.peer_send), x.peer_devices, len(m.opened))))
         except RuntimeError as exc:
-            q.put((rank, str(exc)))
+            q.put((rank, ("error", str(exc), len(m.opened), len(m.closed))))
     finally:
         dist.destroy_process_group()
 
 
-def test_ipc_exchange_setup_fails_on_every_rank_together():
-    """bench.py's pipelined exchange falls back to RCCL's all-gather when any rank cannot set it up:
-    IpcAllGather's setup is collective, so a failure on one rank raises on every rank (none is left
-    waiting in a collective the failed rank skipped)."""
-    world = 2
+def _run_ipc_case(world, case):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ipc_setup_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_ipc_setup_worker, args=(r, world, port, q, case)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert "this rank" in res[1] and "another rank" in res[0], res
+    return res
+
+
+def test_ipc_exchange_setup_fails_on_every_rank_together():
+    """bench.py's pipelined exchange falls back to RCCL's all-gather when any rank cannot set it up:
+    IpcAllGather's setup is collective, so a failure on one rank raises on every rank (none is left
+    waiting in a collective the failed rank skipped)."""
+    res = _run_ipc_case(2, "alloc")
+    assert res[1][0] == "error" and "this rank" in res[1][1], res
+    assert res[0][0] == "error" and "another rank" in res[0][1], res
+
+
+def test_ipc_exchange_peer_access_decision():
+    """Peer access is checked for every (this device, peer device) pair before anything is mapped
+    (HipPeerMapper.can_access: hipDeviceCanAccessPeer + hipDeviceEnablePeerAccess). One pair
+    without it (rank 2's device cannot reach rank 0's) makes EVERY rank raise -- so every rank falls
+    back to RCCL together -- and the ranks that had mapped peer buffers unmap them; with every pair
+    reachable each rank maps its world - 1 peers' two send buffers and learns their devices."""
+    world = 3
+    res = _run_ipc_case(world, "peer")
+    for r in range(world):
+        assert res[r][0] == "error", res
+        assert ("this rank" if r == 2 else "another rank") in res[r][1], res
+        assert "no peer access" in res[r][1], res
+        assert res[r][2] == res[r][3]  # whatever was mapped was unmapped
+    res = _run_ipc_case(world, "all")
+    for r in range(world):
+        status, peers, devs, opened = res[r]
+        assert status == "ok" and peers == [j for j in range(world) if j != r], res
+        assert devs == {j: j for j in range(world)} and opened == 2 * (world - 1)

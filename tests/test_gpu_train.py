@@ -499,3 +499,105 @@ def test_set_buffers_after_a_shard_run_restores_the_row_count():
     tr.run(epochs=1, generator=torch.Generator().manual_seed(1))
     tr.stage(*bufs)
     assert tr.minibatch == tr.idx.numel() == 128
+
+
+def _fp64_reference_grads(net, bufs, idx):
+    """fp64 torch autograd on the CPU of the same loss (the reference's backward, ppo.py:153-160, in
+    double): per-parameter gradients, and the gradients reaching the trunk outputs and the
+    embeddings (the dY operands the backward's dX GEMMs start from), captured by hooks."""
+    ref = copy.deepcopy(net).double().cpu()
+    b = [t[idx].cpu() for t in bufs]
+    b = [t.double() if t.is_floating_point() else t for t in b]
+    dys = {}
+
+    def keep(name):
+        def hook(_m, _i, out):
+            out.register_hook(lambda g: dys.__setitem__(name, g.detach().clone()))
+        return hook
+    ref.actor_net.register_forward_hook(keep("actor trunk output"))
+    ref.critic_net.register_forward_hook(keep("critic trunk output"))
+    ref.actor_net.embedding.register_forward_hook(keep("actor embedding"))
+    ref.critic_net.embedding.register_forward_hook(keep("critic embedding"))
+    loss, _ = _torch_loss(ref, *b)
+    loss.backward()
+    return {k: p.grad for k, p in ref.named_parameters()}, dys
+
+
+@pytest.mark.parametrize("Bm", [64, 4096])
+def test_gradients_per_element_vs_fp64(Bm):
+    """Every gradient ELEMENT of the HIP step against fp64 autograd on the CPU.
+    The backward carries its gradients pre-scaled by the power of two >= Bm (BwdIO::gscale), so the
+    dY operands of the split-product dX GEMMs are O(1) instead of O(1/Bm) (at Bm = 4096 the actor
+    trunk's dY is ~1e-6 unscaled: below fp16's normal range, where the two-plane split loses relative
+    accuracy); k_reduce_grads undoes the scale exactly. Bar, per element with |ref| >= 1e-3 of its
+    tensor's max: |hip - ref64| <= 2e-4 |ref64| + 1e-7 max|ref|. For scale, the same bar applied to
+    torch fp32 on the CPU (the reference's own precision) is printed beside it. Prints the |dY|
+    quantiles of the trunk outputs and embeddings (unscaled, as the loss defines them)."""
+    from uavhip.policy import TransformerActorCritic, layout
+    from uavhip.train import FusedPPOTrainer
+    torch.manual_seed(31)
+    net = TransformerActorCritic().cuda()
+    n = 2 * Bm
+    bufs = _buffers(n, seed=32)
+    idx = torch.randperm(n, generator=torch.Generator().manual_seed(33))[:Bm]
+    ref64, dys = _fp64_reference_grads(net, bufs, idx)
+    ref32 = copy.deepcopy(net).cpu()
+    loss, _ = _torch_loss(ref32, *(t[idx].cpu() for t in bufs))
+    loss.backward()
+    tr = FusedPPOTrainer(net, Bm)
+    tr.set_buffers(*bufs)
+    grads = tr.gradients(idx.cuda()).double().cpu()
+    for k, g in dys.items():
+        q = np.quantile(g.abs().numpy().ravel(), [0.1, 0.5, 0.9, 1.0])
+        print(f"Bm {Bm} |dY| {k}: p10 {q[0]:.2e} p50 {q[1]:.2e} p90 {q[2]:.2e} max {q[3]:.2e}")
+    offs, _ = layout()
+    worst_hip, worst_t32, bad = 0.0, 0.0, []
+    for (k, p32), o in zip(ref32.named_parameters(), offs):
+        r = ref64[k].reshape(-1)
+        got = grads[o:o + p32.numel()]
+        scale = float(r.abs().max())
+        sel = r.abs() >= 1e-3 * scale
+        if not bool(sel.any()):
+            continue
+        tol = 2e-4 * r.abs() + 1e-7 * scale
+        rh = float(((got - r).abs() / tol)[sel].max())
+        rt = float(((p32.grad.reshape(-1).double() - r).abs() / tol)[sel].max())
+        rel = ((got - r).abs() / r.abs())[sel]
+        worst_hip, worst_t32 = max(worst_hip, rh), max(worst_t32, rt)
+        print(f"Bm {Bm} {k}: {int(sel.sum())}/{r.numel()} elements, max rel {float(rel.max()):.2e} "
+              f"(p99 {float(rel.quantile(0.99)):.2e}), bar use {rh:.3f} (torch fp32 CPU: {rt:.3f})")
+        if rh > 1.0:
+            bad.append(k)
+    print(f"Bm {Bm}: worst bar use HIP {worst_hip:.3f}, torch fp32 CPU {worst_t32:.3f}")
+    assert not bad, f"elements outside the per-element bar in {bad}"
+
+
+def test_gradient_prescale_ab(monkeypatch):
+    """A/B of the gradient pre-scale at Bm = 4096 (UAVHIP_GRAD_PRESCALE=0: the round-3 backward with
+    1/Bm folded into the per-sample loss gradient): the per-element error against fp64 autograd on
+    the CPU, printed for both; the pre-scaled step must not be worse."""
+    from uavhip.policy import TransformerActorCritic, layout
+    from uavhip.train import FusedPPOTrainer
+    Bm = 4096
+    torch.manual_seed(31)
+    net = TransformerActorCritic().cuda()
+    bufs = _buffers(2 * Bm, seed=32)
+    idx = torch.randperm(2 * Bm, generator=torch.Generator().manual_seed(33))[:Bm]
+    ref64, _ = _fp64_reference_grads(net, bufs, idx)
+    offs, _ = layout()
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("UAVHIP_GRAD_PRESCALE", mode)
+        tr = FusedPPOTrainer(copy.deepcopy(net), Bm)
+        tr.set_buffers(*bufs)
+        grads = tr.gradients(idx.cuda()).double().cpu()
+        rels = []
+        for (k, p), o in zip(net.named_parameters(), offs):
+            r = ref64[k].reshape(-1)
+            sel = r.abs() >= 1e-3 * float(r.abs().max())
+            rels.append(((grads[o:o + p.numel()] - r).abs() / r.abs())[sel])
+        rel = torch.cat(rels)
+        out[mode] = (float(rel.quantile(0.5)), float(rel.quantile(0.99)), float(rel.max()))
+        print(f"UAVHIP_GRAD_PRESCALE={mode}: per-element rel error vs fp64 p50 {out[mode][0]:.2e} "
+              f"p99 {out[mode][1]:.2e} max {out[mode][2]:.2e}")
+    assert out["1"][1] <= out["0"][1] * 1.05
