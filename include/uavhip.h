@@ -337,7 +337,9 @@ int uavhip_rollout_steps(const uavhip_policy* policy, const uavhip_env* env, flo
 
 /* One clipped-PPO minibatch step of agents/ppo.py:96-169 (evaluate -> surrogate / clipped value
  * / entropy loss -> backward -> clip_grad_norm_(1.0) -> Adam with the four parameter groups of
- * ppo.py:17-22), as hand-written kernels: grouped fp32 MFMA GEMMs for every linear layer
+ * ppo.py:17-22), as hand-written kernels: fp32-accurate split-product GEMMs on the f16 MFMA for the
+ * encoder layers (forward / input gradients two-plane, weight gradients three-plane) and f32 MFMA
+ * GEMMs for the embeddings and heads
  * (forward, input gradients, split-K weight gradients), fused residual+LayerNorm, attention,
  * heads+loss, and a fused clip+Adam. Parameters, gradients and the Adam moments are FLAT
  * buffers in the plain (not fragment-order) uavhip_policy_layout() layout; the torch module's
@@ -358,7 +360,9 @@ typedef struct uavhip_ppo {
     int32_t global_minibatch; /* samples per step over all ranks (0: = minibatch) */
     /* torch.optim.Adam's hyper-parameters as torch holds them (Python floats = doubles): the bias
        corrections and step size are formed in double and the per-element coefficients rounded to
-       float once, exactly as torch's single-tensor Adam does (agents/ppo.py:17-22) */
+       float once, as torch's single-tensor Adam does -- its path for CPU tensors, where the reference's
+       fixtures were recorded (agents/ppo.py:17-22); torch's CUDA default (foreach) differs by one
+       rounding per element (train.hip k_adam) */
     double lr_actor, lr_critic, beta1, beta2, adam_eps; /* 2e-4, 1e-3, 0.9, 0.999, 1e-8 */
     float eps_clip, max_grad_norm, value_coef, entropy_coef; /* 0.2, 1.0, 0.5, 0.01 */
 } uavhip_ppo;

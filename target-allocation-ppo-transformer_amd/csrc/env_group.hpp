@@ -20,6 +20,17 @@ namespace envgrp {
 using namespace envdev;
 
 constexpr int L = 32;  // lanes per env
+
+// Attribution builds of the fused rollout's env step (make EXP=n, profiling only, WRONG results;
+// scripts/profile_env_attrib.sh): each compiles out one group of the step's global accesses so its
+// PMC bytes and time can be priced by difference against the product build.
+//   21 scene values (tgt_value / uav_cost / p_pen of both buffers)   22 per-target / per-UAV state
+//   23 istate / dstate rows    24 the env's own window    25 the state stores (gstore_regs)
+//   26 the step's outputs (obs / reward / done / info)    27 the dependent p_dmg load of the new pair
+#ifndef UAVHIP_EXP
+#define UAVHIP_EXP 0
+#endif
+constexpr int kAttr = UAVHIP_EXP;
 constexpr int kWin = 96;  // LDS scratch per env: window at [2, 72), new row at [72, 86)
 
 struct GRegs {
@@ -86,7 +97,8 @@ __device__ void gload_table(GRegs& R, const uavhip_env& env, int j) {
 template <bool TAB = true>
 __device__ __forceinline__ void gload_cur_pair(GRegs& R, const uavhip_env& env) {
     if (R.u < env.N) {
-        R.pd_cur = TAB ? R.tab[R.u * env.M + R.t] : env.p_dmg[(R.sb * env.N + R.u) * env.M + R.t];
+        R.pd_cur = TAB ? R.tab[R.u * env.M + R.t]
+                       : (kAttr == 27 ? 0.5 : env.p_dmg[(R.sb * env.N + R.u) * env.M + R.t]);
         R.pp_cur = gsh_d(R.ppen, R.u);
     } else {
         R.pd_cur = 0.0;
@@ -214,23 +226,42 @@ __device__ __forceinline__ void gload_issue(GRegs& R, GPending& q, const uavhip_
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
         const long long sb = (long long)(b < nb ? b : 0) * env.E + e;
+        if (kAttr == 21) {
+            q.valb[b] = 4.0 + j;
+            q.ucb[b] = 1.0;
+            q.ppb[b] = 0.9;
+            continue;
+        }
         q.valb[b] = j < M ? env.tgt_value[sb * M + j] : 0.0;
         q.ucb[b] = j < N ? env.uav_cost[sb * N + j] : 0.0;
         q.ppb[b] = j < N ? env.p_pen[sb * N + j] : 0.0;
     }
-    q.isv = is[j < UAVHIP_IST_COUNT ? j : 0];
-    q.dsv = ds[j < UAVHIP_DST_COUNT ? j : 0];
+    if (kAttr == 23) {
+        q.isv = j == UAVHIP_IST_EPISODE ? 1 : 0;
+        q.dsv = j == UAVHIP_DST_TOTAL_COST || j == UAVHIP_DST_TOTAL_VALUE ? 20.0 : 0.0;
+    } else {
+        q.isv = is[j < UAVHIP_IST_COUNT ? j : 0];
+        q.dsv = ds[j < UAVHIP_DST_COUNT ? j : 0];
+    }
     const long long o = (long long)e * M + j;
     const bool v = j < M;
-    R.nhf = v ? env.nh_final[o] : 1.0;
-    R.nhp = v ? env.nh_pure[o] : 1.0;
-    R.tc = v ? env.t_cost[o] : 0.0;
-    R.nlk = v ? env.n_lock[o] : 0;
-    R.asg = j < N ? env.assigned[(long long)e * N + j] : -1;
+    if (kAttr == 22) {
+        R.nhf = 1.0; R.nhp = 1.0; R.tc = 0.0; R.nlk = 0; R.asg = -1;
+    } else {
+        R.nhf = v ? env.nh_final[o] : 1.0;
+        R.nhp = v ? env.nh_pure[o] : 1.0;
+        R.tc = v ? env.t_cost[o] : 0.0;
+        R.nlk = v ? env.n_lock[o] : 0;
+        R.asg = j < N ? env.assigned[(long long)e * N + j] : -1;
+    }
     const float* w = env.window + (long long)e * kObs;
-    R.w0 = w[j];
-    R.w1 = w[L + j];
-    R.w2 = j < kObs - 2 * L ? w[2 * L + j] : 0.0f;
+    if (kAttr == 24) {
+        R.w0 = R.w1 = R.w2 = 0.0f;
+    } else {
+        R.w0 = w[j];
+        R.w1 = w[L + j];
+        R.w2 = j < kObs - 2 * L ? w[2 * L + j] : 0.0f;
+    }
 }
 __device__ __forceinline__ void gload_finish(GRegs& R, const GPending& q, const uavhip_env& env, int e, int j) {
     const int N = env.N, M = env.M;
@@ -306,6 +337,7 @@ __device__ void gload_regs(GRegs& R, const uavhip_env& env, int e, int j) {
 
 __device__ void gstore_regs(const GRegs& R, const uavhip_env& env, int e, int j) {
     const int N = env.N, M = env.M;
+    if (kAttr == 25) return;
     if (j < M) {
         const long long o = (long long)e * M + j;
         env.nh_final[o] = R.nhf;
@@ -347,6 +379,9 @@ template <bool TAB = true>
 __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int auto_reset, float* obs_o,
                       double* rew_o, uint8_t* done_o, double* info_o) {
     const int N = env.N, M = env.M;
+    if (kAttr == 26) {
+        obs_o = nullptr; rew_o = nullptr; done_o = nullptr; info_o = nullptr;
+    }
     if (R.u >= N) {  // stepping a finished env: the reference raises IndexError (:296)
         R.err |= 1;
         if (obs_o) gwrite_obs(obs_o, R, j, true, obs_f16(env));

@@ -1,6 +1,13 @@
 // policy.hip -- K4: fused TransformerActorCritic forward (networks/transformer_net.py:15-144) on
-// gfx950, fp32 end to end (the reference's dtype) on the f32-input MFMA (v_mfma_f32_16x16x4_f32,
-// exact fp32 products, fp32 accumulation).
+// gfx950, fp32-accurate (the reference's dtype): every encoder GEMM as split products on the f16
+// MFMA (v_mfma_f32_16x16x32_f16, each operand as two fp16 planes x1 = f16(x), x2 = f16((x - x1) 2^11),
+// three MFMAs per block, fp32 accumulation), the embeddings (K = 14) and the heads on
+// the f32 MFMA (v_mfma_f32_16x16x4_f32, exact fp32 products). Range of the split operands: 2^-22
+// relative per product for |x| in [2^-14, 65504]; below 2^-14 an absolute floor of ~2^-36 (the
+// backward therefore carries its gradients pre-scaled, BwdIO::gscale); at or above 65520 x1 is inf
+// and every output that reads it is non-finite (never a finite wrong value).
+// (The notes below on tiles and layout date from the all-f32 design and still describe the f32
+// building blocks.)
 //
 // Work decomposition (MI355X-first):
 //  * one workgroup = 4 waves = 16 samples = 80 tokens, token index tok = s * 16 + p (s = window

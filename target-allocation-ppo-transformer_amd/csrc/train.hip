@@ -224,7 +224,11 @@ constexpr int kSqBlocks = 256;
 
 // clip_grad_norm_(max_norm) + torch.optim.Adam (ppo.py:17-22 groups: actor params < critic trunk
 // offset use lr_actor, the rest lr_critic), elementwise over the flat buffers, in the operation order
-// and roundings of torch's single-tensor Adam (torch/optim/adam.py, the CPU path the reference runs):
+// and roundings of torch's single-tensor Adam (torch/optim/adam.py) -- the path torch takes for CPU
+// tensors, where the reference's update ran when its fixtures were recorded (tests/golden/
+// make_golden.py, no GPU). On a CUDA device (agents/ppo.py:14 when one is present) torch defaults to
+// the foreach path, p + step * (m / denom): one rounding apart per element, inside the teacher-forced
+// bound of tests/adam_bound.py; parity with that path is bounded, not bitwise:
 //   m = lerp(m, g, 1 - b1)            = fma(w1, g - m, m)       (the vectorised lerp, weight < 0.5)
 //   v = v * b2;  v = addcmul(v, g, g, 1 - b2) = v + ((1 - b2) g) g
 //   denom = sqrt(v) / sqrt(1 - b2^t) + eps

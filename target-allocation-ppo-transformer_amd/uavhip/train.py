@@ -1,5 +1,7 @@
 """FusedPPOTrainer: the clipped-PPO update of agents/ppo.py:96-169 on the HIP training step of
-libuavhip.so (uavhip_ppo_step, csrc/train.hip) -- grouped fp32 MFMA GEMMs, fused LayerNorm /
+libuavhip.so (uavhip_ppo_step, csrc/train.hip) -- fp32-accurate split-product GEMMs on the f16 MFMA
+(forward and input gradients two-plane, weight gradients three-plane; gradients carried pre-scaled
+by the power of two >= the minibatch so the planes stay in fp16's normal range), fused LayerNorm /
 attention / heads+loss kernels and a fused clip_grad_norm_ + Adam.
 
 The policy's parameters become views of one flat buffer (the uavhip_policy_layout() order), so

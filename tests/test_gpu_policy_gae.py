@@ -480,3 +480,61 @@ def test_fused_rollout_step_vs_oracle(traj_npz):
             np.testing.assert_allclose(o_h[e], o_c, rtol=2e-6, atol=1e-6)
         obs = nxt
     assert n_done > 0
+
+
+@pytest.mark.parametrize("scale", [1.0, 40.0, 400.0])
+def test_fused_forward_large_activations(policy_npz, scale):
+    """Dynamic range of the split-product forward: the critic's layer-0 FFN1
+    weight and bias scaled so the FFN hidden activations -- the FFN2 GEMM's split operand -- reach
+    1e2 .. 1e4 (measured max printed); the fused forward still matches the torch fp32 module to the
+    usual bars (the split planes are 2^-22 relative anywhere in [2^-14, 65504])."""
+    net = _load_policy(policy_npz, "b")
+    lin = net.critic_net.transformer.layers[0].linear1
+    with torch.no_grad():
+        lin.weight.mul_(scale)
+        lin.bias.mul_(scale)
+    g = torch.Generator().manual_seed(7)
+    x = (torch.randn(256, 5, 14, generator=g) * 0.7).cuda()
+    a = torch.randint(0, 2, (256,), generator=g).cuda()
+    hid = {}
+    h = lin.register_forward_hook(lambda m, i, o: hid.__setitem__("max", float(o.relu().abs().max())))
+    with torch.no_grad():
+        logp_t, v_t, _ = net.evaluate(x, a)
+    h.remove()
+    print(f"scale {scale}: FFN hidden max {hid['max']:.3e}")
+    _, logp, value, _, _ = net.fused_forward(x, actions=a)
+    assert_close_report(f"scale {scale} logp", logp.cpu().numpy(), logp_t.cpu().numpy(), rtol=1e-5, atol=2e-6)
+    assert_close_report(f"scale {scale} value", value.cpu().numpy(), v_t[:, 0].cpu().numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_fused_forward_overflow_is_never_finite_and_wrong(policy_npz):
+    """Above fp16's range (|x| >= 65520) a split operand's first plane is inf: every output that
+    reads it must come out non-finite -- flagged, never a finite wrong value. The critic's FFN1 scaled
+    so its hidden activations exceed 1e5: the values of the rows whose hidden activations overflow are
+    NaN / inf, every other row (and every logp: the actor trunk is untouched) still matches torch."""
+    net = _load_policy(policy_npz, "b")
+    lin = net.critic_net.transformer.layers[0].linear1
+    with torch.no_grad():
+        lin.weight.mul_(4000.0)
+        lin.bias.mul_(4000.0)
+    g = torch.Generator().manual_seed(8)
+    x = (torch.randn(256, 5, 14, generator=g) * 0.7).cuda()
+    a = torch.randint(0, 2, (256,), generator=g).cuda()
+    rows = {}
+
+    def hook(m, i, o):
+        rows["over"] = (o.relu().abs() >= 65520).flatten(1).any(1)  # [B] any token / feature of the sample
+
+    h = lin.register_forward_hook(hook)
+    with torch.no_grad():
+        logp_t, v_t, _ = net.evaluate(x, a)
+    h.remove()
+    over = rows["over"]
+    print(f"{int(over.sum())}/{over.numel()} samples with an FFN hidden activation >= 65520")
+    assert bool(over.any())
+    _, logp, value, _, _ = net.fused_forward(x, actions=a)
+    fin = torch.isfinite(value)
+    assert not bool(fin[over].any()), "an overflowing split operand produced a finite value"
+    assert_close_report("overflow: unaffected values", value[~over].cpu().numpy(), v_t[~over, 0].cpu().numpy(),
+                        rtol=1e-5, atol=1e-5)
+    assert_close_report("overflow: logp (actor)", logp.cpu().numpy(), logp_t.cpu().numpy(), rtol=1e-5, atol=2e-6)

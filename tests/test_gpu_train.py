@@ -530,9 +530,15 @@ def test_gradients_per_element_vs_fp64(Bm):
     dY operands of the split-product dX GEMMs are O(1) instead of O(1/Bm) (at Bm = 4096 the actor
     trunk's dY is ~1e-6 unscaled: below fp16's normal range, where the two-plane split loses relative
     accuracy); k_reduce_grads undoes the scale exactly. Bar, per element with |ref| >= 1e-3 of its
-    tensor's max: |hip - ref64| <= 2e-4 |ref64| + 1e-7 max|ref|. For scale, the same bar applied to
-    torch fp32 on the CPU (the reference's own precision) is printed beside it. Prints the |dY|
-    quantiles of the trunk outputs and embeddings (unscaled, as the loss defines them)."""
+    tensor's max: |hip - ref64| <= 2e-4 |ref64| + 1e-7 max|ref|, OR no more than twice the error of
+    torch fp32 on the CPU (the reference's own precision) at that element + 2e-6 |ref64|. The second
+    clause exists for the few elements whose fp32 gradient is decided by fp32 rounding upstream (a
+    ReLU / mask decision of an activation within rounding of 0): at Bm = 4096 both fp32
+    implementations miss fp64 there by the same ~1e-2 relative (measured on MI355X, r04a). And over
+    all elements above the floor: p99 of the HIP relative error <= 2 x torch fp32's p99 + 1e-6.
+    Prints, per tensor, the worst relative error, the bar use of both fp32 implementations and how
+    many elements needed the second clause; and the |dY| quantiles of the trunk outputs and embeddings
+    (unscaled, as the loss defines them)."""
     from uavhip.policy import TransformerActorCritic, layout
     from uavhip.train import FusedPPOTrainer
     torch.manual_seed(31)
@@ -551,25 +557,39 @@ def test_gradients_per_element_vs_fp64(Bm):
         q = np.quantile(g.abs().numpy().ravel(), [0.1, 0.5, 0.9, 1.0])
         print(f"Bm {Bm} |dY| {k}: p10 {q[0]:.2e} p50 {q[1]:.2e} p90 {q[2]:.2e} max {q[3]:.2e}")
     offs, _ = layout()
-    worst_hip, worst_t32, bad = 0.0, 0.0, []
+    worst_hip, worst_t32, bad, rels_h, rels_t, n_second = 0.0, 0.0, [], [], [], 0
     for (k, p32), o in zip(ref32.named_parameters(), offs):
         r = ref64[k].reshape(-1)
         got = grads[o:o + p32.numel()]
+        t32 = p32.grad.reshape(-1).double()
         scale = float(r.abs().max())
         sel = r.abs() >= 1e-3 * scale
         if not bool(sel.any()):
             continue
         tol = 2e-4 * r.abs() + 1e-7 * scale
-        rh = float(((got - r).abs() / tol)[sel].max())
-        rt = float(((p32.grad.reshape(-1).double() - r).abs() / tol)[sel].max())
-        rel = ((got - r).abs() / r.abs())[sel]
+        eh, et = (got - r).abs(), (t32 - r).abs()
+        first = eh <= tol
+        second = eh <= 2 * et + 2e-6 * r.abs()
+        rh = float((eh / tol)[sel].max())
+        rt = float((et / tol)[sel].max())
+        rel, relt = (eh / r.abs())[sel], (et / r.abs())[sel]
+        rels_h.append(rel)
+        rels_t.append(relt)
         worst_hip, worst_t32 = max(worst_hip, rh), max(worst_t32, rt)
+        n2 = int((sel & ~first & second).sum())
+        n_second += n2
         print(f"Bm {Bm} {k}: {int(sel.sum())}/{r.numel()} elements, max rel {float(rel.max()):.2e} "
-              f"(p99 {float(rel.quantile(0.99)):.2e}), bar use {rh:.3f} (torch fp32 CPU: {rt:.3f})")
-        if rh > 1.0:
-            bad.append(k)
-    print(f"Bm {Bm}: worst bar use HIP {worst_hip:.3f}, torch fp32 CPU {worst_t32:.3f}")
-    assert not bad, f"elements outside the per-element bar in {bad}"
+              f"(p99 {float(rel.quantile(0.99)):.2e}; torch fp32 {float(relt.max()):.2e} / "
+              f"{float(relt.quantile(0.99)):.2e}), bar use {rh:.3f} (torch fp32 CPU: {rt:.3f}), "
+              f"{n2} element(s) by the fp32-reference clause")
+        if bool((sel & ~first & ~second).any()):
+            bad.append((k, int((sel & ~first & ~second).sum())))
+    ph = float(torch.cat(rels_h).quantile(0.99))
+    pt = float(torch.cat(rels_t).quantile(0.99))
+    print(f"Bm {Bm}: worst bar use HIP {worst_hip:.3f}, torch fp32 CPU {worst_t32:.3f}; p99 rel HIP {ph:.2e}, "
+          f"torch fp32 {pt:.2e}; {n_second} element(s) passed by the fp32-reference clause")
+    assert not bad, f"elements outside both per-element bars: {bad}"
+    assert ph <= 2 * pt + 1e-6, (ph, pt)
 
 
 def test_gradient_prescale_ab(monkeypatch):
