@@ -119,11 +119,17 @@ class TransformerActorCritic(nn.Module):
         key = (dev, tuple(p._version for p in params), tuple(p.data_ptr() for p in params))
         if self._packed is not None and self._packed_key == key:
             return self._packed
-        fresh = pack_weights(self.state_dict(), device=dev)
-        if self._packed is not None and self._packed.device == dev and self._packed.numel() == fresh.numel():
-            self._packed.copy_(fresh)  # in place: a captured hipGraph keeps pointing at this buffer
+        if dev.type == "cuda":
+            # on the device (uavhip_policy_pack: one launch from the flat parameter buffer, bitwise the
+            # host pack_weights, test_device_pack_matches_host_pack), in place when the buffer exists:
+            # a captured hipGraph keeps pointing at it
+            _, total = split_layout()
+            if self._packed is None or self._packed.device != dev or self._packed.numel() != total:
+                self._packed = torch.empty(total, dtype=torch.float32, device=dev)
+            flat = _flat_parameters(params)
+            check(LIB.uavhip_policy_pack(ptr(flat), ptr(self._packed), stream_handle()), "uavhip_policy_pack")
         else:
-            self._packed = fresh
+            self._packed = pack_weights(self.state_dict(), device=dev)
         self._packed_key = key
         d = _lib.PolicyDesc()
         d.weights = self._packed.data_ptr()
@@ -296,6 +302,25 @@ def to_fragment_order(w, K):
 
 def from_fragment_order(flat, R, K):
     return flat.reshape(R // 16, K // 16, 4, 16, 4).permute(0, 3, 1, 2, 4).reshape(R, K)
+
+
+def _flat_parameters(params):
+    """The parameters as one flat fp32 device buffer in the uavhip_policy_layout() order: the storage
+    itself when every parameter is already a view at its layout offset of one buffer
+    (FusedPPOTrainer's), else a copy (padding floats zero)."""
+    offs, n = layout()
+    p0 = params[0]
+    st = p0.untyped_storage()
+    base = st.data_ptr()
+    if all(p.dtype == torch.float32 and p.is_contiguous() and p.untyped_storage().data_ptr() == base for p in params):
+        start = p0.data_ptr() - 4 * offs[0]
+        if (start - base) % 4 == 0 and start >= base and start - base + 4 * n <= st.nbytes() and \
+                all(p.data_ptr() == start + 4 * o for p, o in zip(params, offs)):
+            return torch.empty(0, dtype=torch.float32, device=p0.device).set_(st, (start - base) // 4, (n,))
+    flat = torch.zeros(n, dtype=torch.float32, device=p0.device)
+    for p, o in zip(params, offs):
+        flat[o:o + p.numel()].copy_(p.detach().reshape(-1))
+    return flat
 
 
 def pack_weights(state_dict, device=None):

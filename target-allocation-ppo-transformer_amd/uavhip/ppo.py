@@ -145,7 +145,13 @@ class PPOAgent:
         self.buffer["actions"].append(action)
         self.buffer["logprobs"].append(logp)
         self.buffer["values"].append(value)
-        return int(action.item())
+        a = int(action.item())  # the host sync the reference's loop already has
+        if not bool(torch.isfinite(logp).all() & torch.isfinite(value).all()):
+            # torch's Categorical rejects non-finite probabilities (transformer_net.py:118-120); here
+            # they mean a split-product operand left fp16's range (|x| >= 65520, policy.hip header)
+            raise ValueError("the policy produced a non-finite log-probability / value (an activation beyond "
+                             "the split products' fp16 range)")
+        return a
 
     def store_transition(self, reward, done):
         self.buffer["rewards"].append(reward)

@@ -170,6 +170,18 @@ class RolloutEngine:
             self._body()
         return self.traj
 
+    def check_finite(self):
+        """Raise if the last iteration's log-probabilities or values are not finite (one reduction and
+        a host sync; not called by collect()). Non-finite policy outputs are how the split-product
+        forward flags an activation beyond fp16's range (|x| >= 65520, policy.hip header): never a
+        finite wrong value."""
+        tr = self.traj
+        ok = torch.isfinite(tr.logp).all() & torch.isfinite(tr.values).all()
+        if not bool(ok):
+            raise FloatingPointError("rollout: non-finite log-probabilities / values (an activation beyond the "
+                                     "split products' fp16 range)")
+        return True
+
     def roll(self):
         """Kept for API compatibility: each iteration starts by carrying obs[T] into obs[0]."""
 

@@ -402,6 +402,27 @@ def test_device_pack_matches_host_pack():
     assert torch.equal(packed, pack_weights(net.state_dict(), device="cuda"))
 
 
+def test_packed_weights_repack_on_device():
+    """TransformerActorCritic.packed_weights() repacks on the device (uavhip_policy_pack) from the
+    flat parameter buffer -- zero-copy when the parameters are views of FusedPPOTrainer's buffer,
+    else a gathered copy -- in place, and equals the host pack_weights bit for bit, both before the
+    trainer wraps the module and after optimizer steps changed its weights."""
+    from uavhip import _lib
+    from uavhip.policy import TransformerActorCritic, pack_weights
+    from uavhip.train import FusedPPOTrainer
+    torch.manual_seed(2)
+    net = TransformerActorCritic().cuda()
+    buf = net.packed_weights()
+    assert torch.equal(buf, pack_weights(net.state_dict(), device="cuda"))
+    tr = FusedPPOTrainer(net, 64)
+    bufs = _buffers(256, seed=3)
+    tr.set_buffers(*bufs)
+    tr.run(epochs=1, generator=torch.Generator().manual_seed(5), use_graph=False)
+    buf2 = net.packed_weights()
+    assert buf2.data_ptr() == buf.data_ptr()  # in place: captured rollout graphs stay valid
+    assert torch.equal(buf2, pack_weights(net.state_dict(), device="cuda"))
+
+
 def test_fused_update_replays_reference_update():
     """The HIP training step against the reference's own PPOAgent.update() (tests/golden/ppo_update.npz,
     agents/ppo.py:68-181): from the fixture's weights w0 and buffers, GAE on the GPU, then the 15
