@@ -502,6 +502,15 @@ inline bool pos_split(int Bm) {
     return pol::ps_capable(Bm) && !(e && e[0] == '0');
 }
 
+// Weight gradients in direct mode (WgBatch::direct) when no tile has more than kWgDirectMaxSlabs
+// slabs (UAVHIP_WGRAD_DIRECT=0 / 1 forces stream-K / direct: tests compare both ways).
+inline bool wgrad_direct(int max_slabs) {
+    const char* e = std::getenv("UAVHIP_WGRAD_DIRECT");
+    if (e && e[0] == '0') return false;
+    if (e && e[0] == '1') return true;
+    return max_slabs <= kWgDirectMaxSlabs;
+}
+
 // Trunk split for this minibatch size (UAVHIP_TRUNK_SPLIT=0 turns it off: tests compare both ways).
 inline int split_blocks(int Bm) {
     const char* e = std::getenv("UAVHIP_TRUNK_SPLIT");
@@ -662,6 +671,7 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
     // ---------------------------------------------------------------- weight gradients
     SegBatch sb{};
     int seg_blocks = 0;
+    int sq_base = 0;  // direct-mode k_wgrad's g^2 partials come first in sq_part
     auto seg = [&](const float* src, int dst, int count, int parts, int part_stride, const float* src_rest = nullptr,
                    int dst_ld = 0) {
         if (sb.n >= kMaxSegs) { ++sb.n; return; }
@@ -698,6 +708,7 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         auto dw = [&](const float* dY, int ldy, const XSrc& X, int ldx, int M, int N, int K, int dst_w) {
             dst[wp.b.n] = dst_w;
             wp.add(dY, ldy, X.x, ldx, M, N, K, X.mode, X.g, X.b);
+            if (wp.ok) wp.b.p[wp.b.n - 1].dst = dst_w;
         };
         auto layer_dw = [&](const LayerBufs& B, int tr_, int ly, const XSrc& hin, int rows) {
             const int pw = kOffs.o[layer_param(tr_, ly, INW)];
@@ -717,17 +728,29 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         dw(p.dz_a, HID, ln_out(A.xhat2, ta, 0, N2W), D, HID, D, Bm, kOffs.o[kActorHead]);
         dw(p.dz_c, HID, ln_out(C1.xhat2, tc, 1, N2W), D, HID, D, Bm, kOffs.o[kCriticHead]);
         wp.b.part = p.wg_part;
-        const bool sched = wp.ok && wp.tiles([&](const WgTileRuns& t) {
-            const WgProb& P = wp.b.p[t.prob];
-            seg(p.wg_part + (size_t)t.first_slot * kWgSlot, dst[t.prob] + t.m0 * P.N + t.n0, t.rows * kWgT, t.runs,
-                kWgRuns * kWgSlot, p.wg_part + (size_t)t.rest_slot * kWgSlot, P.N);
-        });
-        if (!sched) {
-            set_error("uavhip_ppo_step: weight-gradient problems do not fit the stream-K schedule");
-            return UAVHIP_EINVAL;
+        if (wp.ok && wgrad_direct(wp.max_slabs())) {
+            // direct mode: one workgroup per output tile writes dW (unscaled) and its g^2 partial; the
+            // reduction below covers the other gradients, its g^2 partials after these
+            wp.b.direct = 1;
+            wp.b.grads = c->grads;
+            wp.b.sq = p.sq_part;
+            wp.b.unscale = 1.0f / grad_prescale(Bg);
+            sq_base = wp.b.tiles;
+            hipLaunchKernelGGL(k_wgrad, dim3(wp.b.tiles), dim3(kWgThreads), 0, st, wp.b);
+            TR_CHECK(check_launch("k_wgrad"));
+        } else {
+            const bool sched = wp.ok && wp.tiles([&](const WgTileRuns& t) {
+                const WgProb& P = wp.b.p[t.prob];
+                seg(p.wg_part + (size_t)t.first_slot * kWgSlot, dst[t.prob] + t.m0 * P.N + t.n0, t.rows * kWgT, t.runs,
+                    kWgRuns * kWgSlot, p.wg_part + (size_t)t.rest_slot * kWgSlot, P.N);
+            });
+            if (!sched) {
+                set_error("uavhip_ppo_step: weight-gradient problems do not fit the stream-K schedule");
+                return UAVHIP_EINVAL;
+            }
+            hipLaunchKernelGGL(k_wgrad, dim3(wp.grid), dim3(kWgThreads), 0, st, wp.b);
+            TR_CHECK(check_launch("k_wgrad"));
         }
-        hipLaunchKernelGGL(k_wgrad, dim3(wp.grid), dim3(kWgThreads), 0, st, wp.b);
-        TR_CHECK(check_launch("k_wgrad"));
     }
     // biases of the encoder layers (K6's per-workgroup sums of the dY rows)
     {
@@ -766,8 +789,8 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         return UAVHIP_EINVAL;
     }
     // padding floats between parameters stay zero
-    hipLaunchKernelGGL(k_reduce_grads, dim3(seg_blocks), dim3(256), 0, st, sb, c->grads, p.sq_part, step, adam_hyper(c),
-                       p.adam_sc, 1.0f / grad_prescale(Bg));
-    *n_sq = seg_blocks;
+    hipLaunchKernelGGL(k_reduce_grads, dim3(seg_blocks), dim3(256), 0, st, sb, c->grads, p.sq_part + sq_base, step,
+                       adam_hyper(c), p.adam_sc, 1.0f / grad_prescale(Bg));
+    *n_sq = sq_base + seg_blocks;
     return check_launch("k_reduce_grads");
 }

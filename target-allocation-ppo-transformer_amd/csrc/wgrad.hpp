@@ -40,13 +40,23 @@ struct WgProb {
     int M, N, K, lda, ldb;
     int tiles_n, tiles, slabs;  // per problem: column tiles, tiles, slabs per tile
     int unit_begin;             // first slab unit of this problem
+    int tile_begin;             // first output tile of this problem (direct mode: its workgroup)
+    int dst;                    // direct mode: float offset of dW [M][N] in `grads`
 };
+// Direct mode (small minibatches: every tile a few slabs): one workgroup per output tile runs all
+// of its slabs and writes dW itself -- times `unscale` (BwdIO::gscale undone, exact) -- into the
+// flat gradient, with the block's sum of squares in sq[blockIdx.x]; no partial tiles, no reduction.
 struct WgBatch {
     WgProb p[kWgMaxProbs];
     int n;
     int units;
     float* part;  // [grid * kWgRuns][kWgSlot]
+    int direct, tiles;
+    float* grads;
+    float* sq;
+    float unscale;
 };
+constexpr int kWgDirectMaxSlabs = 12;  // direct mode when no tile has more slabs (K <= 384 rows)
 
 
 // Stamps (make TRACE=1 only): per workgroup, s_memtime at kernel start and, per run, after the
@@ -61,6 +71,15 @@ __device__ unsigned long long g_wtrace[kWgGrid * 16];
 #define WTR(slot) do {} while (0)
 #endif
 
+__device__ __forceinline__ int wg_find_tile(const WgBatch& b, int t) {
+    int lo = 0, hi = b.n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (t >= b.p[mid].tile_begin) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
 __device__ __forceinline__ int wg_find(const WgBatch& b, int u) {
     int lo = 0, hi = b.n;
     while (hi - lo > 1) {
@@ -168,7 +187,12 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
     const int mt0 = 4 * (wv & 1), nt0 = 2 * (wv >> 1);  // this wave's first m-tile / n-tile
     const long long U = wb.units, G = gridDim.x;
     int u = (int)(blockIdx.x * U / G);
-    const int u_end = (int)((blockIdx.x + 1) * U / G);
+    int u_end = (int)((blockIdx.x + 1) * U / G);
+    if (wb.direct) {  // workgroup = output tile: all of its slabs
+        const WgProb& Q = wb.p[wg_find_tile(wb, blockIdx.x)];
+        u = Q.unit_begin + (blockIdx.x - Q.tile_begin) * Q.slabs;
+        u_end = u + Q.slabs;
+    }
     int run = 0;
     WTR(0);
     while (u < u_end) {
@@ -225,6 +249,35 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
         }
         WTR(2 + 4 * run);
         // lane (i16, g) of tile (a, b) holds dW[m0 + 16 (mt0 + a) + 4 g + r][n0 + 16 (nt0 + b) + i16]
+        if (wb.direct) {  // the whole tile: dW itself, unscaled, rows < M (a 64-row problem), and g^2
+            float sq = 0.f;
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const f32x4 v = (hi[a][b] + (mid[a][b] + lo[a][b] * (1.0f / 2048.0f)) * (1.0f / 2048.0f)) *
+                                    wb.unscale;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = m0 + 16 * (mt0 + a) + 4 * g + r;
+                        if (row < P.M) {
+                            wb.grads[P.dst + (size_t)row * P.N + n0 + 16 * (nt0 + b) + i16] = v[r];
+                            sq += v[r] * v[r];
+                        }
+                    }
+                }
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) sq += __shfl_xor(sq, o);
+            float* red = reinterpret_cast<float*>(wg_smem);  // the stages are dead after the last barrier
+            if (l == 0) red[wv] = sq;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                float t = 0.f;
+                for (int w = 0; w < kWgThreads / 64; ++w) t += red[w];
+                wb.sq[blockIdx.x] = t;
+            }
+            return;
+        }
         float* out = wb.part + (size_t)(blockIdx.x * kWgRuns + run) * kWgSlot;
 #pragma unroll
         for (int a = 0; a < 4; ++a)
@@ -266,7 +319,15 @@ struct WgPlan {
         P.tiles = ((M + kWgT - 1) / kWgT) * P.tiles_n;
         P.slabs = K / kWgBK;
         P.unit_begin = b.units;
+        P.tile_begin = b.tiles;
+        P.dst = 0;
         b.units += P.tiles * P.slabs;
+        b.tiles += P.tiles;
+    }
+    int max_slabs() const {
+        int m = 0;
+        for (int i = 0; i < b.n; ++i) m = std::max(m, b.p[i].slabs);
+        return m;
     }
     // Workgroup w's unit range, as the kernel computes it.
     int w_begin(int w) const { return (int)((long long)w * b.units / grid); }

@@ -402,6 +402,44 @@ def test_device_pack_matches_host_pack():
     assert torch.equal(packed, pack_weights(net.state_dict(), device="cuda"))
 
 
+def test_wgrad_direct_mode_matches_stream_k(monkeypatch):
+    """Minibatch 64: the weight-gradient GEMM in direct mode (one workgroup per output tile runs all
+    its slabs and writes dW and its g^2 partial itself; UAVHIP_WGRAD_DIRECT=1, the default when no
+    tile has more than 12 slabs) against the stream-K form with partial tiles summed by
+    k_reduce_grads (UAVHIP_WGRAD_DIRECT=0): the same products summed in another order, so every
+    gradient agrees to fp32 reordering (1e-6 of its tensor's max); and four whole optimizer steps
+    agree to the teacher-forced Adam bound's scale (parameters to 1e-6 lr-relative)."""
+    from uavhip import _lib
+    from uavhip.policy import TransformerActorCritic, layout
+    from uavhip.train import FusedPPOTrainer
+    torch.manual_seed(41)
+    base = TransformerActorCritic().cuda()
+    bufs = _buffers(256, seed=42)
+    idx = torch.randperm(256, generator=torch.Generator().manual_seed(43))[:64].to(torch.int32).cuda()
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("UAVHIP_WGRAD_DIRECT", mode)
+        tr = FusedPPOTrainer(copy.deepcopy(base), 64)
+        tr.set_buffers(*bufs)
+        g = tr.gradients(idx).clone()
+        for b in range(4):
+            tr.step(_lib.PPO_FULL | tr._packed(b), idx)
+        torch.cuda.synchronize()
+        out[mode] = (g, tr.params.clone(), tr.stats.clone())
+    offs, _ = layout()
+    for (k, p), o in zip(base.named_parameters(), offs):
+        a, b = out["0"][0][o:o + p.numel()], out["1"][0][o:o + p.numel()]
+        scale = float(a.abs().max())
+        err = float((a - b).abs().max())
+        assert err <= 1e-6 * scale + 1e-12, f"{k}: {err:.3e} vs max {scale:.3e}"
+    d = (out["0"][1] - out["1"][1]).abs()
+    print(f"4 steps, stream-K vs direct: max |d param| = {float(d.max()):.3e}, mean {float(d.mean()):.3e}")
+    # Adam normalises each element: an element with a near-zero gradient can turn fp32 reordering into
+    # a step difference of up to lr (tests/adam_bound.py); on average the runs agree closely
+    assert float(d.max()) <= 2 * 4 * 1e-3 and float(d.mean()) <= 1e-6
+    torch.testing.assert_close(out["0"][2], out["1"][2], rtol=1e-5, atol=1e-7)
+
+
 def test_packed_weights_repack_on_device():
     """TransformerActorCritic.packed_weights() repacks on the device (uavhip_policy_pack) from the
     flat parameter buffer -- zero-copy when the parameters are views of FusedPPOTrainer's buffer,
