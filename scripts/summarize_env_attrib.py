@@ -17,7 +17,8 @@ WHAT = {"noenv": "the whole env step", "exp21": "scene values (tgt_value / uav_c
         "exp22": "per-target / per-UAV state loads (nh_final, nh_pure, t_cost, n_lock, assigned)",
         "exp23": "istate / dstate row loads", "exp24": "the env's own window load",
         "exp25": "the env-state stores", "exp26": "the step outputs (obs, reward, done, info)",
-        "exp27": "the dependent p_dmg load of the new pointer pair"}
+        "exp27": "the dependent p_dmg load of the new pointer pair",
+        "exp32": "the ring rows' L2 misses (every ring load reads one hot row; policy.hip kExpHotRing)"}
 
 
 def counters(path):

@@ -31,6 +31,8 @@ constexpr int L = 32;  // lanes per env
 #define UAVHIP_EXP 0
 #endif
 constexpr int kAttr = UAVHIP_EXP;
+// (24: the window registers take 1.0 instead of memory, so no later window row is padding: a zero
+// window would turn the policy's ring loads of padded positions into reads of one hot row, policy.hip)
 constexpr int kWin = 96;  // LDS scratch per env: window at [2, 72), new row at [72, 86)
 
 struct GRegs {
@@ -256,7 +258,7 @@ __device__ __forceinline__ void gload_issue(GRegs& R, GPending& q, const uavhip_
     }
     const float* w = env.window + (long long)e * kObs;
     if (kAttr == 24) {
-        R.w0 = R.w1 = R.w2 = 0.0f;
+        R.w0 = R.w1 = R.w2 = 1.0f;
     } else {
         R.w0 = w[j];
         R.w1 = w[L + j];
@@ -379,8 +381,8 @@ template <bool TAB = true>
 __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int auto_reset, float* obs_o,
                       double* rew_o, uint8_t* done_o, double* info_o) {
     const int N = env.N, M = env.M;
-    if (kAttr == 26) {
-        obs_o = nullptr; rew_o = nullptr; done_o = nullptr; info_o = nullptr;
+    if (kAttr == 26) {  // the scalar outputs only: without the obs window the next inputs would be padding
+        rew_o = nullptr; done_o = nullptr; info_o = nullptr;
     }
     if (R.u >= N) {  // stepping a finished env: the reference raises IndexError (:296)
         R.err |= 1;

@@ -54,12 +54,24 @@ constexpr bool kExpNoStore = true;
 constexpr bool kExpNoStore = false;
 #endif
 // make NOENV=1 (profiling builds only, wrong results): the fused rollout kernels skip the env step
-// (scripts/profile_env_share.sh prices the env step as the time / PMC bytes it adds)
+// but still write the next windows -- the input windows shifted by one row, every row's constant
+// feature (index 13, 1.0 in every real observation row) set -- so no position of the next step's
+// windows is padding and the policy's data-dependent ring loads (a padded position reads one hot
+// dummy row, ring_load) stay those of a real rollout. bench.py prices the env step as the product
+// build's time minus this build's; scripts/profile_env_share.sh the same for PMC bytes. (Until round
+// 4 the NOENV build left the next windows all zero -- every position but the last padded -- which also
+// dropped ~41 MB per step of ring-row reads: that differential was not the env step's cost.)
 #ifdef UAVHIP_EXP_NOENV
 constexpr bool kExpNoEnv = true;
 #else
 constexpr bool kExpNoEnv = false;
 #endif
+// Timing build EXP=32 (profiling only, WRONG results): every ring-row load reads one hot row (the
+// load still issued, its value used): the cost of the ring rows' L2 misses, by difference.
+#ifndef UAVHIP_EXP
+#define UAVHIP_EXP 0
+#endif
+constexpr bool kExpHotRing = UAVHIP_EXP == 32;
 
 // Phase tracing (make TRACE=1 only): waves 0 and 4 of the first 256 workgroups stamp s_memtime at
 // the phase boundaries below; uavhip_policy_trace copies the stamps out. Off in the product build.
@@ -1277,7 +1289,7 @@ __device__ __forceinline__ void ring_load(TID_F RowPre<NP>& r, const Smem& sm, c
     // makes the compiler's vmcnt bookkeeping assume it may be missing and wait for everything
 #pragma unroll
     for (int u = 0; u < 2 * NP; ++u) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(slots + (off[u] >= 0 ? off[u] : 4 * q));
+        const f32x4 v = *reinterpret_cast<const f32x4*>(slots + (off[u] >= 0 && !kExpHotRing ? off[u] : 4 * q));
         r.v[c][u] = off[u] >= 0 ? v : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 }
@@ -1841,6 +1853,15 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
         }
     }
     PTR(7);
+    if constexpr (ENV && kExpNoEnv) {  // NOENV: the next windows without the env step (timing only)
+        __syncthreads();
+        for (int i = TIDX(); i < SPW * envdev::kObs; i += NTHR) {
+            const int p = i / envdev::kObs, r = i - p * envdev::kObs, s_ = r / IN, k = r - s_ * IN;
+            const int e = b0 + p;
+            const float v = sm.x[((s_ < S - 1 ? s_ + 1 : S - 1) * SPW + p) * LDX + k];
+            if (e < B) envdev::obs_at(eo.obs, e, false)[r] = k == IN - 1 ? 1.0f : v;
+        }
+    }
     if constexpr (ENV && !kExpNoEnv) {
         // UAVEnv.step of this workgroup's 16 envs, two per wave (one env per wave at a time,
         // envdev::step_once on register state; the wave's row scratch in the dead sm.x). Both envs'

@@ -502,13 +502,14 @@ inline bool pos_split(int Bm) {
     return pol::ps_capable(Bm) && !(e && e[0] == '0');
 }
 
-// Weight gradients in direct mode (WgBatch::direct) when no tile has more than kWgDirectMaxSlabs
-// slabs (UAVHIP_WGRAD_DIRECT=0 / 1 forces stream-K / direct: tests compare both ways).
+// Weight gradients in direct mode (WgBatch::direct) only on request (UAVHIP_WGRAD_DIRECT=1, and
+// only when no tile has more than kWgDirectMaxSlabs slabs): measured at minibatch 64 (r04b, same box,
+// scripts/train_probe.py) the stream-K form with k_reduce_grads is faster, 0.098 against 0.113 ms
+// per step -- one workgroup walking a tile's 10 slabs is a longer chain than spreading them over
+// 148 workgroups and summing the partials.
 inline bool wgrad_direct(int max_slabs) {
     const char* e = std::getenv("UAVHIP_WGRAD_DIRECT");
-    if (e && e[0] == '0') return false;
-    if (e && e[0] == '1') return true;
-    return max_slabs <= kWgDirectMaxSlabs;
+    return e && e[0] == '1' && max_slabs <= kWgDirectMaxSlabs;
 }
 
 // Trunk split for this minibatch size (UAVHIP_TRUNK_SPLIT=0 turns it off: tests compare both ways).

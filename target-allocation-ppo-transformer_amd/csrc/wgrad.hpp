@@ -56,7 +56,7 @@ struct WgBatch {
     float* sq;
     float unscale;
 };
-constexpr int kWgDirectMaxSlabs = 12;  // direct mode when no tile has more slabs (K <= 384 rows)
+constexpr int kWgDirectMaxSlabs = 12;  // direct mode only when no tile has more slabs (K <= 384 rows)
 
 
 // Stamps (make TRACE=1 only): per workgroup, s_memtime at kernel start and, per run, after the

@@ -72,10 +72,11 @@ def pack_compact(obs, actions, logp, values, returns, advantages, dones):
     return torch.cat([rows.float(), scal, obs[0].reshape(-1).float()]).contiguous()
 
 
-def unpack_compact(payloads, T, E):
+def unpack_compact(payloads, T, E, copy=False):
     """[world, compact_floats] gathered payloads -> dict of [world * T * E, ...] tensors in (rank,
     step, env) order; obs rebuilt on the GPU (uavhip_windows_from_rows; the HIP library is
-    required -- there is no host fallback)."""
+    required -- there is no host fallback). The scalar columns are views into `payloads` unless
+    copy=True (a receive buffer that is rewritten later: IpcAllGather's)."""
     from ._lib import LIB, check, ptr, stream_handle
     world = payloads.shape[0]
     F = compact_floats(T, E)
@@ -84,6 +85,8 @@ def unpack_compact(payloads, T, E):
     nr = T * E * ROW_FLOATS
     ns = T * E * len(SCALARS)
     scal = payloads[:, nr:nr + ns].reshape(world * T * E, len(SCALARS))
+    if copy:
+        scal = scal.clone()
     obs = torch.empty(world * T * E, 5, 14, dtype=torch.float32, device=payloads.device)
     base = payloads.data_ptr()
     check(LIB.uavhip_windows_from_rows(base + 4 * (nr + ns), base, base + 4 * (nr + len(SCALARS) - 1),

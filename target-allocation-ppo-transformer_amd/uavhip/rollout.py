@@ -280,7 +280,9 @@ class RolloutEngine:
         recv, ev = exchange.progress()
         side = exchange.side
         with torch.cuda.stream(side):
-            batch = unpack_compact(recv, self.T, self.env.E)
+            # scalars copied out of the receive buffer: progress() rewrites it two iterations later
+            # without waiting for this batch's consumers
+            batch = unpack_compact(recv, self.T, self.env.E, copy=True)
         done = torch.cuda.Event()
         done.record(side)
         if self._submitted == self.iteration:

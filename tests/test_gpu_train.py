@@ -404,9 +404,9 @@ def test_device_pack_matches_host_pack():
 
 def test_wgrad_direct_mode_matches_stream_k(monkeypatch):
     """Minibatch 64: the weight-gradient GEMM in direct mode (one workgroup per output tile runs all
-    its slabs and writes dW and its g^2 partial itself; UAVHIP_WGRAD_DIRECT=1, the default when no
-    tile has more than 12 slabs) against the stream-K form with partial tiles summed by
-    k_reduce_grads (UAVHIP_WGRAD_DIRECT=0): the same products summed in another order, so every
+    its slabs and writes dW and its g^2 partial itself; opt-in, UAVHIP_WGRAD_DIRECT=1: it measured
+    slower than stream-K at minibatch 64) against the default stream-K form with partial tiles summed
+    by k_reduce_grads (UAVHIP_WGRAD_DIRECT=0): the same products summed in another order, so every
     gradient agrees to fp32 reordering (1e-6 of its tensor's max); and four whole optimizer steps
     agree to the teacher-forced Adam bound's scale (parameters to 1e-6 lr-relative)."""
     from uavhip import _lib
