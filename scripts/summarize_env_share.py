@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""gpurun_out/envshare_<tag> (scripts/profile_env_share.sh) -> profiles/<round>_env_share.json: per
+"""gpurun_out/envshare_<tag> (scripts/profile_env_share.sh, or the product / noenv directories of
+scripts/profile_env_attrib.sh's gpurun_out/envattr_<tag>) -> profiles/<round>_env_share.json: per
 step of k_rollout_steps (launch / T) the average duration and the HBM bytes (FETCH_SIZE x 2 +
 WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md 'HBM') of the product build and of the build
 without the env step; their differences are the env step's time and traffic per step (all E envs)."""
@@ -20,10 +21,12 @@ for b in ("product", "noenv"):
             if KERNEL in r["Kernel_Name"]]
     d["launches"] = len(durs)
     d["avg_ns_per_step"] = sum(durs[1:]) / max(1, len(durs) - 1) / T  # the first launch warms up
-    for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(src, b, f"pmc_{c}",
-                                                                                 "run_counter_collection.csv")))
-             if KERNEL in r["Kernel_Name"]]
+    for i, c in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
+        d_ = os.path.join(src, b, f"pmc_{c}")
+        if not os.path.isdir(d_):  # scripts/profile_env_attrib.sh's layout: pmc_1 = FETCH, pmc_2 = WRITE
+            d_ = os.path.join(src, b, f"pmc_{i + 1}")
+        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d_, "run_counter_collection.csv")))
+             if KERNEL in r["Kernel_Name"] and r.get("Counter_Name", c) == c]
         d[c + "_KiB_per_step"] = sum(v) / len(v) / T
     d["hbm_bytes_per_step"] = (2 * d["FETCH_SIZE_KiB_per_step"] + d["WRITE_SIZE_KiB_per_step"]) * 1024
     out[b] = d
