@@ -46,6 +46,10 @@ struct GRegs {
     double r, J, asg_cost, cov_val, tot_cost, tot_val, sum_pd, sum_pf, pd_cur, pp_cur;
     double den_c, rcp_c, den_v, rcp_v, rcp_m;
     double rcp_n;  // lane j: RN(1 / (j + 1))
+    // single-step use (TAB = false, the fused rollout): which per-target / per-UAV entries the step
+    // changed, so gstore_delta writes only those -- bit 0: all (a reset), bit 1: target ct and UAV cu
+    // (an accepted assign); group-uniform
+    int dmask, ct, cu;
     // window element j in w0, 32 + j in w1, 64 + j (j < 6) in w2
     float w0, w1, w2;
     double* tab;   // LDS p_dmg table of this env [N][M]
@@ -287,6 +291,8 @@ __device__ __forceinline__ void gload_finish(GRegs& R, const GPending& q, const 
     R.pd_cur = grl_d(q.dsv, UAVHIP_DST_PD_CUR);
     R.sel = env.scene_buffers == 2 ? (sel_raw & 1) : 0;
     R.sb = (long long)R.sel * env.E + e;
+    R.dmask = 0;
+    R.ct = R.cu = -1;
     R.val = R.sel ? q.valb[1] : q.valb[0];
     R.ucost = R.sel ? q.ucb[1] : q.ucb[0];
     R.ppen = R.sel ? q.ppb[1] : q.ppb[0];
@@ -376,6 +382,52 @@ __device__ void gstore_regs(const GRegs& R, const uavhip_env& env, int e, int j)
     if (j < kObs - 2 * L) w[2 * L + j] = R.w2;
 }
 
+// gstore_regs for the single-step fused rollout: the per-target / per-UAV arrays only where the step
+// changed them (R.dmask: after an accepted assign the one target's nh_final / nh_pure / t_cost / n_lock
+// and the one UAV's assigned entry, after a reset all of them, else none) -- the same memory state as
+// gstore_regs, with 8-20 instead of 960 bytes per env-step of those arrays on most steps.
+__device__ void gstore_delta(const GRegs& R, const uavhip_env& env, int e, int j) {
+    const int N = env.N, M = env.M;
+    if (kAttr == 25) return;
+    const bool all = (R.dmask & 1) != 0;
+    const bool tgt = all ? j < M : ((R.dmask & 2) != 0 && j == R.ct);
+    const bool uav = all ? j < N : ((R.dmask & 2) != 0 && j == R.cu);
+    if (tgt) {
+        const long long o = (long long)e * M + j;
+        env.nh_final[o] = R.nhf;
+        env.nh_pure[o] = R.nhp;
+        env.t_cost[o] = R.tc;
+        env.n_lock[o] = R.nlk;
+    }
+    if (uav) env.assigned[(long long)e * N + j] = R.asg;
+    if (j == 0) {
+        int* is = env.istate + (long long)e * UAVHIP_IST_COUNT;
+        double* ds = env.dstate + (long long)e * UAVHIP_DST_COUNT;
+        is[UAVHIP_IST_UAV_IDX] = R.u;
+        is[UAVHIP_IST_TARGET_IDX] = R.t;
+        is[UAVHIP_IST_N_COVERED] = R.ncov;
+        is[UAVHIP_IST_N_ASSIGNED] = R.nasg;
+        is[UAVHIP_IST_EPISODE] = R.ep;
+        is[UAVHIP_IST_ERROR] = R.err;
+        is[UAVHIP_IST_SCENE_SEL] = R.sel;
+        is[UAVHIP_IST_SCENE_STALE] = R.stale;
+        is[UAVHIP_IST_SCENE_GEN] = R.gen;
+        ds[UAVHIP_DST_R] = R.r;
+        ds[UAVHIP_DST_J] = R.J;
+        ds[UAVHIP_DST_ASG_COST] = R.asg_cost;
+        ds[UAVHIP_DST_COV_VALUE] = R.cov_val;
+        ds[UAVHIP_DST_TOTAL_COST] = R.tot_cost;
+        ds[UAVHIP_DST_TOTAL_VALUE] = R.tot_val;
+        ds[UAVHIP_DST_PD_CUR] = R.pd_cur;
+        ds[UAVHIP_DST_SUM_PDMG] = R.sum_pd;
+        ds[UAVHIP_DST_SUM_PFIN] = R.sum_pf;
+    }
+    float* w = env.window + (long long)e * kObs;
+    w[j] = R.w0;
+    w[L + j] = R.w1;
+    if (j < kObs - 2 * L) w[2 * L + j] = R.w2;
+}
+
 // One UAVEnv.step (uav_env.py:295-435) of this group's env (envdev::step_once).
 template <bool TAB = true>
 __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int auto_reset, float* obs_o,
@@ -431,6 +483,11 @@ __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int 
                 R.nlk = R.nlk + 1;
             }
             if (j == u) R.asg = t;
+            if (!TAB) {
+                R.dmask |= 2;
+                R.ct = t;
+                R.cu = u;
+            }
             R.sum_pd = R.sum_pd + pd;
             R.sum_pf = R.sum_pf + pf;
             R.asg_cost = cost_all;
@@ -479,6 +536,7 @@ __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int 
             }
         }
         greset_regs<TAB>(R, env, j, flipped);
+        if (!TAB) R.dmask |= 1;
         if (obs_o) gwrite_obs(obs_o, R, j, false, obs_f16(env));
     } else {
         if (obs_o) gwrite_obs(obs_o, R, j, true, obs_f16(env));  // _get_obs returns zeros when done (:188-189)

@@ -352,7 +352,7 @@ __device__ __forceinline__ void hsplit_store(_Float16* Y, int o, const f32x4 v) 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         v1[j] = (_Float16)v[j];
-        v2[j] = (_Float16)((v[j] - (float)v1[j]) * 2048.f);
+        v2[j] = f16_lo(v[j], v1[j]);
     }
     *reinterpret_cast<f16x4*>(Y + o) = v1;
     *reinterpret_cast<f16x4*>(Y + o + kPlane) = v2;
@@ -1881,7 +1881,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             envgrp::gstep<false>(R, env, e, j, sm.mask[2 * wve + g], eo.auto_reset, obs_at(eo.obs, e, obs_f16(env)),
                           eo.rew + e, eo.done + e, eo.info ? eo.info + (size_t)e * UAVHIP_INFO_COUNT : nullptr);
             PTR(62);
-            envgrp::gstore_regs(R, env, e, j);
+            envgrp::gstore_delta(R, env, e, j);  // only the entries the step changed
             PTR(63);
         }
         if constexpr ((ENV & kEnvWave) != 0) if (!env_grp && e0 < B) {
@@ -2231,8 +2231,7 @@ __device__ __forceinline__ void attn_out2(Smem& sm, float* __restrict__ dqkv, in
         const _Float16 a0 = (_Float16)v.x, a1 = (_Float16)v.y;
         typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
         *reinterpret_cast<f16x2*>(bp) = f16x2{a0, a1};
-        *reinterpret_cast<f16x2*>(bp + kPlaneB) = f16x2{(_Float16)((v.x - (float)a0) * 2048.f),
-                                                          (_Float16)((v.y - (float)a1) * 2048.f)};
+        *reinterpret_cast<f16x2*>(bp + kPlaneB) = f16x2{f16_lo(v.x, a0), f16_lo(v.y, a1)};
         if (kvc && part > 0)  // position split: this query position's share of every position's dk / dv
             st2(kvc + ((size_t)kblk * TOK + tok) * 2 * D + (part - 1) * D + 64 * c + col, v);
         else
@@ -3212,7 +3211,7 @@ __device__ __forceinline__ void ps_big_store(Smem& sm, int p, int q, const f32x4
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             a[j] = (_Float16)v[j];
-            b[j] = (_Float16)((v[j] - (float)a[j]) * 2048.f);
+            b[j] = f16_lo(v[j], a[j]);
         }
         *reinterpret_cast<f16x4*>(bp + p * 2 * LDQ + 4 * q) = a;  // [p][plane 1 | plane 2 | pad]
         *reinterpret_cast<f16x4*>(bp + p * 2 * LDQ + 3 * D + 4 * q) = b;
@@ -3480,7 +3479,7 @@ __global__ __launch_bounds__(256) void k_policy_split(const float* __restrict__ 
     for (int j = 0; j < 8; ++j) {
         const float w = j < 4 ? a[j] : b[j - 4];
         w1[j] = (_Float16)w;
-        w2[j] = (_Float16)((w - (float)w1[j]) * 2048.f);
+        w2[j] = f16_lo(w, w1[j]);
     }
     f16x8* dst = reinterpret_cast<f16x8*>(packed + kSplitOffs.o[si]) + (size_t)blk * 128 + l;
     dst[0] = w1;
@@ -3513,7 +3512,7 @@ __global__ __launch_bounds__(256) void k_policyT_split(const float* __restrict__
     for (int j = 0; j < 8; ++j) {
         const float v = w[(size_t)(k0 + j) * Rt];
         w1[j] = (_Float16)v;
-        w2[j] = (_Float16)((v - (float)w1[j]) * 2048.f);
+        w2[j] = f16_lo(v, w1[j]);
     }
     f16x8* dst = reinterpret_cast<f16x8*>(packedT + kTSplit + li * kLayerT + base) + (size_t)blk * 128 + l;
     dst[0] = w1;

@@ -362,7 +362,7 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             w1[e] = (_Float16)p[e];
-            w2[e] = (_Float16)((p[e] - (float)w1[e]) * 2048.f);
+            w2[e] = f16_lo(p[e], w1[e]);
         }
         _Float16* sp = reinterpret_cast<_Float16*>(a.packed + sb) +
                        (((i >> 4) * (NC >> 5) + (j >> 5)) * 128 + (i & 15) + 16 * ((j & 31) >> 3)) * 8 + (j & 7);
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             w1[e] = (_Float16)col[e];
-            w2[e] = (_Float16)((col[e] - (float)w1[e]) * 2048.f);
+            w2[e] = f16_lo(col[e], w1[e]);
         }
         _Float16* sp = reinterpret_cast<_Float16*>(a.packedT + kTSplit + tb) +
                        (((jt >> 4) * (NR >> 5) + (it >> 5)) * 128 + (jt & 15) + 16 * ((it & 31) >> 3)) * 8 + (it & 7);
