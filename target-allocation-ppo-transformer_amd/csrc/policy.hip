@@ -3,9 +3,10 @@
 // MFMA (v_mfma_f32_16x16x32_f16, each operand as two fp16 planes x1 = f16(x), x2 = f16((x - x1) 2^11),
 // three MFMAs per block, fp32 accumulation), the embeddings (K = 14) and the heads on
 // the f32 MFMA (v_mfma_f32_16x16x4_f32, exact fp32 products). Range of the split operands: 2^-22
-// relative per product for |x| in [2^-14, 65504]; below 2^-14 an absolute floor of ~2^-36 (the
-// backward therefore carries its gradients pre-scaled, BwdIO::gscale); at or above 65520 x1 is inf
-// and every output that reads it is non-finite (never a finite wrong value).
+// relative per product for |x| in [2^-14, 65536); below 2^-14 an absolute floor of ~2^-36 (the
+// backward therefore carries its gradients pre-scaled, BwdIO::gscale); beyond, the second plane is
+// NaN (common.hpp f16_lo: gfx950's f16 conversion saturates, so without that guard an overflowing
+// operand would be a finite wrong value) and every output that reads it is NaN.
 // (The notes below on tiles and layout date from the all-f32 design and still describe the f32
 // building blocks.)
 //

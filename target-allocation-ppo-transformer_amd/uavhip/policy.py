@@ -6,8 +6,8 @@ reference's initial weights.
 Two execution paths:
   * `get_action` (rollout, no grad): the fused HIP forward of libuavhip.so (policy.hip) on packed
     weights -- every encoder GEMM as fp32-accurate split products on the f16 MFMA (two fp16 planes per
-    operand, DESIGN.md 4a: 2^-22 relative per product for |x| in [2^-14, 65504); a larger operand
-    overflows fp16 and makes the outputs non-finite), the embeddings and heads on the f32 MFMA; the action is drawn on device from Philox. GPU only: raises otherwise.
+    operand, DESIGN.md 4a: 2^-22 relative per product for |x| in [2^-14, 65536); a larger operand
+    makes its plane NaN and the outputs that read it non-finite), the embeddings and heads on the f32 MFMA; the action is drawn on device from Philox. GPU only: raises otherwise.
   * `evaluate` (PPO update, autograd): the module's own torch forward, used by the update (SURVEY 8f
     "next" row); also the torch fp32 reference the fused kernel is tested against.
 """

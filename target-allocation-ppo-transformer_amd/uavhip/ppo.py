@@ -148,7 +148,7 @@ class PPOAgent:
         a = int(action.item())  # the host sync the reference's loop already has
         if not bool(torch.isfinite(logp).all() & torch.isfinite(value).all()):
             # torch's Categorical rejects non-finite probabilities (transformer_net.py:118-120); here
-            # they mean a split-product operand left fp16's range (|x| >= 65520, policy.hip header)
+            # they mean a split-product operand left fp16's range (|x| >= 65536, common.hpp f16_lo)
             raise ValueError("the policy produced a non-finite log-probability / value (an activation beyond "
                              "the split products' fp16 range)")
         return a

@@ -173,7 +173,7 @@ class RolloutEngine:
     def check_finite(self):
         """Raise if the last iteration's log-probabilities or values are not finite (one reduction and
         a host sync; not called by collect()). Non-finite policy outputs are how the split-product
-        forward flags an activation beyond fp16's range (|x| >= 65520, policy.hip header): never a
+        forward flags an activation beyond fp16's range (|x| >= 65536, common.hpp f16_lo): never a
         finite wrong value."""
         tr = self.traj
         ok = torch.isfinite(tr.logp).all() & torch.isfinite(tr.values).all()
