@@ -191,6 +191,22 @@ def env_counters(kernel):
                 hbm_frac=k["hbm_bytes_per_launch"] / (k["avg_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS)
 
 
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2, 8 XCDs
+
+
+def weight_stream(step_ms, E):
+    """The rollout kernel's weight traffic from L2: every workgroup (16 samples, one per CU at E =
+    4096) reads each GEMM weight once per step (fp32 fragments or the split copies' two fp16 planes:
+    4 B per weight either way), so per step the chip reads (E / 16) x the parameter bytes from L2."""
+    from uavhip._lib import LIB
+    n = int(LIB.uavhip_policy_layout(None, 0))
+    wg = (E + 15) // 16
+    gbs = 4.0 * n * wg / (step_ms * 1e-3) / 1e9
+    return {"bytes_per_workgroup_step": 4 * n, "workgroups": wg, "achieved": gbs, "peak": L2_PEAK_GBS,
+            "unit": "GB/s (L2 -> CU, chip-wide)", "frac": gbs / L2_PEAK_GBS,
+            "per_cu_gbs": gbs / min(wg, 256)}
+
+
 def env_bytes_per_step(M):
     return 24 * M + 490
 
@@ -211,6 +227,8 @@ def parse():
                     help="PPO update implementation timed for ppo_samples_per_s")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end rollout + update iteration legs")
+    ap.add_argument("--no-env-diff", action="store_true",
+                    help="skip the env step's live differential and phase share (child processes; A/B runs)")
     ap.add_argument("--rccl-gather", action="store_true",
                     help="N > 1: the exchange as one RCCL all-gather after each rollout instead of the pipelined "
                          "peer-to-peer copies beside the next rollout (uavhip.dist.IpcAllGather)")
@@ -648,7 +666,7 @@ def main():
     if eng.fused_step:
         pol_ms = float(np.mean(pol_list[:T]))
         env_ms = None
-        if eng.persistent and rank == 0 and world == 1:
+        if eng.persistent and rank == 0 and world == 1 and not args.no_env_diff:
             # the env step's cost = the compiled-out differential (product minus NOENV build, HIP
             # events, child processes on this box); the TRACE build's phase share is a diagnostic
             env_diff, env_err = env_differential(args)
@@ -774,6 +792,9 @@ def main():
                          "executed_peak": peak_exec, "executed_frac": exec_tf / peak_exec,
                          # round 2's measure (every executed FLOP priced on the f32 MFMA, 157.3 TFLOP/s)
                          "f32_mfma_equivalent_frac": exec_tf / MFMA_F32_PEAK_TFLOPS,
+                         # the other resource every step of the kernel streams: its weights from L2,
+                         # once per step in every workgroup (one 16-sample workgroup per CU)
+                         "weight_stream": weight_stream(pol_ms, E),
                          "split_flop_per_launch": split * E,
                          "steps_per_launch": T if eng.persistent else 1,
                          "path": ("fused rollout steps (window-row forward + sample + env step), all T steps of the "

@@ -57,10 +57,14 @@ __device__ __forceinline__ int ffs64(unsigned long long m) { return __ffsll((lon
 // residual |(x - x1) 2^11| > 65504 -- x1 saturated, or x already inf / NaN -- makes the plane NaN, and
 // every product and output that reads it NaN: overflow is flagged, never silent. (|x| < 65536 is
 // exact to 2^-22 relative: between 65504 and 65536 the saturated x1 = 65504 plus x2 still carry x.)
+#if defined(UAVHIP_EXP) && UAVHIP_EXP == 41  // timing build: the unguarded plane (A/B of the guard's cost)
+__device__ __forceinline__ _Float16 f16_lo(float x, _Float16 x1) { return (_Float16)((x - (float)x1) * 2048.f); }
+#else
 __device__ __forceinline__ _Float16 f16_lo(float x, _Float16 x1) {
     const float r = (x - (float)x1) * 2048.f;
     return (_Float16)(fabsf(r) <= 65504.f ? r : __builtin_nanf(""));
 }
+#endif
 
 // ------------------------------------------------------------------ mechanics (fp64)
 __device__ __forceinline__ double clipd(double x, double lo, double hi) {

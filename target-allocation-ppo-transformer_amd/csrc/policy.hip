@@ -347,6 +347,9 @@ __device__ __forceinline__ void hgemm_tile(TID_F f32x4 (&hi)[CT], f32x4 (&lo)[CT
         __builtin_amdgcn_sched_barrier(0);
     }
 }
+// ReLU that keeps NaN: a NaN flagged by a split operand beyond fp16's range (common.hpp f16_lo) must
+// reach the outputs, and fmaxf(NaN, 0) = 0 (IEEE maxNum) would swallow it at the FFN and head ReLUs
+__device__ __forceinline__ float relu_nan(float v) { return v < 0.f ? 0.f : v; }
 // v -> its two planes at Y + psw(tok, c) (plane 2 at + kPlane): one 8-byte store per plane
 __device__ __forceinline__ void hsplit_store(_Float16* Y, int o, const f32x4 v) {
     f16x4 v1, v2;
@@ -367,7 +370,7 @@ __device__ __forceinline__ void hstore_tile(TID_F const f32x4 (&hi)[CT], const f
     for (int ct = 0; ct < CT; ++ct) {
         f32x4 v = hi[ct] + lo[ct] * kLoScale + bb;
         if (RELU) {
-            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+            v.x = relu_nan(v.x); v.y = relu_nan(v.y); v.z = relu_nan(v.z); v.w = relu_nan(v.w);
         }
         hsplit_store(Y, psw((ytok0 + 16 * ct + i16), ycol + 4 * g), v);
     }
@@ -382,7 +385,7 @@ __device__ __forceinline__ void store_tile(TID_F const f32x4 (&acc)[CT], const f
     for (int ct = 0; ct < CT; ++ct) {
         f32x4 v = acc[ct] + bb;
         if (RELU) {
-            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+            v.x = relu_nan(v.x); v.y = relu_nan(v.y); v.z = relu_nan(v.z); v.w = relu_nan(v.w);
         }
         *reinterpret_cast<f32x4*>(Y + (ytok0 + 16 * ct + i16) * ldy + ycol + 4 * g) = v;
     }
@@ -1882,7 +1885,8 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             envgrp::gstep<false>(R, env, e, j, sm.mask[2 * wve + g], eo.auto_reset, obs_at(eo.obs, e, obs_f16(env)),
                           eo.rew + e, eo.done + e, eo.info ? eo.info + (size_t)e * UAVHIP_INFO_COUNT : nullptr);
             PTR(62);
-            envgrp::gstore_delta(R, env, e, j);  // only the entries the step changed
+            if constexpr (UAVHIP_EXP == 42) envgrp::gstore_regs(R, env, e, j);  // timing build: every entry
+            else envgrp::gstore_delta(R, env, e, j);  // only the entries the step changed
             PTR(63);
         }
         if constexpr ((ENV & kEnvWave) != 0) if (!env_grp && e0 < B) {
