@@ -1,5 +1,6 @@
 # Round-4 call f: policy / rollout tests after the NaN-preserving ReLU, then a same-box A/B of the
-# rollout: current build, without the overflow guard (EXP=41), without the delta env stores (EXP=42),
+# rollout: current build, with a per-element overflow guard in the plane writers (EXP=41 at the time;
+# since dropped), without the delta env stores (EXP=42),
 # and round 3's final code (scripts/r03: bash scripts/build_variant.sh r03 407cce9).
 set -o pipefail
 cd $GRAFT_REPO_ROOT

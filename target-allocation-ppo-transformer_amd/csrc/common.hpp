@@ -51,20 +51,13 @@ __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p
 __device__ __forceinline__ int ffs64(unsigned long long m) { return __ffsll((long long)m) - 1; }
 
 // ------------------------------------------------------------------ split-product planes
-// The second fp16 plane of a split operand, x2 = f16((x - x1) 2^11) with x1 = f16(x),
-// guarded: gfx950's f16 conversions saturate at 65504 instead of overflowing to inf, so an operand
-// beyond the planes' range (|x| >= 65536) would otherwise be carried as a FINITE WRONG value. Any
-// residual |(x - x1) 2^11| > 65504 -- x1 saturated, or x already inf / NaN -- makes the plane NaN, and
-// every product and output that reads it NaN: overflow is flagged, never silent. (|x| < 65536 is
-// exact to 2^-22 relative: between 65504 and 65536 the saturated x1 = 65504 plus x2 still carry x.)
-#if defined(UAVHIP_EXP) && UAVHIP_EXP == 41  // timing build: the unguarded plane (A/B of the guard's cost)
+// The second fp16 plane of a split operand, x2 = f16((x - x1) 2^11) with x1 = f16(x).
+// Out of range: gfx950's f32 -> f16 conversions (v_cvt_pk_f16_f32 and v_cvt_f16_f32) round to inf at
+// |x| >= 65520 (scripts/micro/f16_ovfl.hip: MODE.FP16_OVFL is 0 at kernel start), so x1 = inf and
+// x2 = -inf, every product that reads them is +-inf or NaN, and the next LayerNorm turns the token
+// row into NaN. What could hide that is a ReLU written as fmaxf (IEEE maxNum returns 0 for NaN):
+// the GEMM epilogues use relu_nan (policy.hip) instead, so overflow reaches the outputs.
 __device__ __forceinline__ _Float16 f16_lo(float x, _Float16 x1) { return (_Float16)((x - (float)x1) * 2048.f); }
-#else
-__device__ __forceinline__ _Float16 f16_lo(float x, _Float16 x1) {
-    const float r = (x - (float)x1) * 2048.f;
-    return (_Float16)(fabsf(r) <= 65504.f ? r : __builtin_nanf(""));
-}
-#endif
 
 // ------------------------------------------------------------------ mechanics (fp64)
 __device__ __forceinline__ double clipd(double x, double lo, double hi) {

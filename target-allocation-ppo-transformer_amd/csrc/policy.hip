@@ -3,10 +3,10 @@
 // MFMA (v_mfma_f32_16x16x32_f16, each operand as two fp16 planes x1 = f16(x), x2 = f16((x - x1) 2^11),
 // three MFMAs per block, fp32 accumulation), the embeddings (K = 14) and the heads on
 // the f32 MFMA (v_mfma_f32_16x16x4_f32, exact fp32 products). Range of the split operands: 2^-22
-// relative per product for |x| in [2^-14, 65536); below 2^-14 an absolute floor of ~2^-36 (the
-// backward therefore carries its gradients pre-scaled, BwdIO::gscale); beyond, the second plane is
-// NaN (common.hpp f16_lo: gfx950's f16 conversion saturates, so without that guard an overflowing
-// operand would be a finite wrong value) and every output that reads it is NaN.
+// relative per product for |x| in [2^-14, 65504]; below 2^-14 an absolute floor of ~2^-36 (the
+// backward therefore carries its gradients pre-scaled, BwdIO::gscale); from 65520 up the planes are
+// inf / -inf and every output that reads them is non-finite (common.hpp f16_lo; the ReLUs keep NaN,
+// relu_nan), never a finite wrong value.
 // (The notes below on tiles and layout date from the all-f32 design and still describe the f32
 // building blocks.)
 //
@@ -347,8 +347,9 @@ __device__ __forceinline__ void hgemm_tile(TID_F f32x4 (&hi)[CT], f32x4 (&lo)[CT
         __builtin_amdgcn_sched_barrier(0);
     }
 }
-// ReLU that keeps NaN: a NaN flagged by a split operand beyond fp16's range (common.hpp f16_lo) must
-// reach the outputs, and fmaxf(NaN, 0) = 0 (IEEE maxNum) would swallow it at the FFN and head ReLUs
+// ReLU that keeps NaN: the NaN a split operand beyond fp16's range produces (common.hpp f16_lo) must
+// reach the outputs, and fmaxf(NaN, 0) = 0 (IEEE maxNum) swallowed it at the FFN and head ReLUs
+// (measured: a 1.4e5 FFN activation gave finite, wrong values); same cost on the same box (r04f A/B)
 __device__ __forceinline__ float relu_nan(float v) { return v < 0.f ? 0.f : v; }
 // v -> its two planes at Y + psw(tok, c) (plane 2 at + kPlane): one 8-byte store per plane
 __device__ __forceinline__ void hsplit_store(_Float16* Y, int o, const f32x4 v) {

@@ -152,7 +152,7 @@ __device__ __forceinline__ void wg_split_store(const f32x4 v, char* plane, int o
     for (int j = 0; j < 4; ++j) {
         x1[j] = (_Float16)v[j];
         const float r1 = v[j] - (float)x1[j];                 // exact
-        x2[j] = f16_lo(v[j], x1[j]);                          // = f16(r1 2^11), NaN beyond the range
+        x2[j] = f16_lo(v[j], x1[j]);                          // = f16(r1 2^11)
         x3[j] = (_Float16)((r1 - (float)x2[j] * (1.0f / 2048.0f)) * 4194304.f);  // r1 - x2 2^-11: exact
     }
     *reinterpret_cast<wg_f16x4*>(plane + off) = x1;

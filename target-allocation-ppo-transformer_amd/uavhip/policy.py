@@ -284,12 +284,8 @@ def to_split_fragment_order(w):
     l = r%16 + 16 ((k%32)//8) holding k%8 = 0..7 (the f16 MFMA operand layout, policy.hip hgemm_tile)."""
     R, K = w.shape
     w = w.to(torch.float32)
-    # the device conversions (common.hpp f16_lo): f16 saturates at +-65504 instead of overflowing, and
-    # a second plane beyond the range is NaN (overflow flagged, never a finite wrong weight)
-    w1 = w.to(torch.float16)
-    w1 = torch.where(torch.isinf(w1) & torch.isfinite(w), torch.copysign(torch.tensor(65504.0), w).to(torch.float16), w1)
-    r = (w - w1.to(torch.float32)) * 2048.0
-    w2 = torch.where(r.abs() <= 65504.0, r, torch.full_like(r, float("nan"))).to(torch.float16)
+    w1 = w.to(torch.float16)  # IEEE round-to-nearest, inf beyond 65504: what the device conversions do
+    w2 = ((w - w1.to(torch.float32)) * 2048.0).to(torch.float16)
 
     def frag(p):
         return p.reshape(R // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(R // 16, K // 32, 512)
