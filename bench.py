@@ -174,16 +174,24 @@ def env_share_traffic():
     return d.get("env_bytes_per_step"), os.path.basename(files[-1]), d.get("env_ns_per_step")
 
 
-def env_counters(kernel):
+def env_counters(kernel, grid=None):
     """The VALU side and the PMC traffic of an env kernel (K1 / K2 / K2g / K2r) from the newest
     profiles/rNN_env_counters.json (scripts/profile_env_counters.sh + summarize_env_counters.py, the
     same shapes as the bench's env legs): fp64 FLOP fraction of the 78.6 TFLOP/s fp64 vector peak,
-    VALU busy share of SIMD cycles, HBM bytes per launch (FETCH x 2 + WRITE)."""
+    VALU busy share of SIMD cycles, HBM bytes per launch (FETCH x 2 + WRITE). Matched by kernel name
+    without template arguments AND launch grid (threads) when the file keys its entries "name@grid"
+    (one template instance serves several shapes)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_env_counters.json")))
     if not files:
         return None
-    k = json.load(open(files[-1]))["kernels"].get(kernel)
+    ks = json.load(open(files[-1]))["kernels"]
+    k = None
+    for name, v in ks.items():
+        base, _, g = name.partition("@")
+        if _kernel_base(base) == _kernel_base(kernel) and (not g or grid is None or int(g) == int(grid)):
+            k, kernel = v, name
+            break
     if k is None:
         return None
     keep = ("avg_ns", "fp64_frac", "fp64_tflops", "valu_busy", "hbm_bytes_per_launch", "valu_insts", "salu_insts")
@@ -205,6 +213,19 @@ def weight_stream(step_ms, E):
     return {"bytes_per_workgroup_step": 4 * n, "workgroups": wg, "achieved": gbs, "peak": L2_PEAK_GBS,
             "unit": "GB/s (L2 -> CU, chip-wide)", "frac": gbs / L2_PEAK_GBS,
             "per_cu_gbs": gbs / min(wg, 256)}
+
+
+def check_traffic(traffic, ms):
+    """Consistency of a PMC byte count with a measured time: bytes / time must not exceed the HBM peak
+    (a traffic figure from another code state, or a time that is not the traffic's, would). Returns
+    (traffic or None if dropped, implied GB/s, within peak, reason)."""
+    if traffic is None or ms is None:
+        return traffic, None, None, None
+    gbs = traffic / (ms * 1e-3) / 1e9
+    if gbs <= HBM_PEAK_GBS:
+        return traffic, gbs, True, None
+    return None, gbs, False, (f"traffic {traffic / 1e6:.1f} MB per step over {ms * 1e3:.2f} us implies "
+                              f"{gbs:.0f} GB/s > HBM peak: traffic dropped")
 
 
 def env_bytes_per_step(M):
@@ -699,13 +720,14 @@ def main():
         env_fused = [env_fused_rate(1024, 8, 16, 256, dev), env_fused_rate(E, args.uavs, args.targets, 256, dev),
                      env_fused_rate(8192, 64, 128, 64, dev, obs_dtype=torch.float16)]
         # the kernel uavhip_env_step dispatches for each leg (env.hip): K2r wherever omega = 0 and
-        # M <= 32 (64-step chunks when the LDS tables fit, else 32), K2 one env per wave (M > 32)
-        for leg, kern in zip(env_fused, ("uavhip::envrep::k_env_replay<64>", "uavhip::envrep::k_env_replay<32>",
-                                         "uavhip::k_env_step<2, false>")):
-            leg["kernel"] = kern
-            leg["counters"] = env_counters(kern)
+        # M <= 32 (512-thread workgroups of 4 envs: 128 threads per env), K2 one env per wave (M > 32,
+        # 256-thread workgroups of 4 envs); matched to the profile by name and launch grid
+        for leg, (kern, grid) in zip(env_fused, (("k_env_replay", 128 * 1024), ("k_env_replay", 128 * E),
+                                                 ("k_env_step", 64 * 8192))):
+            leg["counters"] = env_counters(kern, grid)
+            leg["kernel"] = leg["counters"]["kernel"] if leg["counters"] else kern
         stress = score_pairs_rate(8192, 64, 128, dev)
-        stress["counters"] = env_counters("uavhip::k_score_pairs")
+        stress["counters"] = env_counters("k_score_pairs", 256 * 8192)
 
     ppo = ppo64 = None
     if not args.no_ppo and world == 1 and args.ppo_impl == "fused":
@@ -752,17 +774,9 @@ def main():
         env_traffic, env_traffic_src = None, None
     else:
         env_traffic, env_traffic_src = profiled_traffic("k_env_step<1, false>")
-    # consistency: PMC bytes over the env step's time must not exceed the HBM peak (a traffic figure
-    # from another code state, or a time that is not the env step's, would); such traffic is dropped
-    env_traffic_gbs = env_traffic_check = None
-    if env_traffic is not None and env_ms is not None:
-        env_traffic_gbs = env_traffic / (env_ms * 1e-3) / 1e9
-        env_traffic_check = env_traffic_gbs <= HBM_PEAK_GBS
-        if not env_traffic_check:
-            env_err = (env_err + "; " if env_err else "") + (
-                f"traffic {env_traffic / 1e6:.1f} MB per step over {env_ms * 1e3:.2f} us implies "
-                f"{env_traffic_gbs:.0f} GB/s > HBM peak: traffic dropped")
-            env_traffic = None
+    env_traffic, env_traffic_gbs, env_traffic_check, why = check_traffic(env_traffic, env_ms)
+    if why:
+        env_err = (env_err + "; " if env_err else "") + why
     if rank == 0:
         line = {
             "metric": "env-steps/sec (whole node), full PPO rollout, 4096 envs x 16 UAV x 32 tgt per GPU",

@@ -20,12 +20,19 @@ SIMDS, XCDS, FP64_PEAK = 1024, 8, 78.6e12
 
 
 def main(src, dst):
+    # keyed by kernel name AND grid size ("name@grid"): one template instance serves several of the
+    # probe's shapes (k_env_replay<64> runs both the 1024- and the 4096-env legs since round 4), and
+    # averaging them together would price neither
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            agg[r["Kernel_Name"].split("(")[0].replace("void ", "")][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    trace = {r["Name"].split("(")[0].replace("void ", ""): float(r["AverageNs"])
-             for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
+            key = r["Kernel_Name"].split("(")[0].replace("void ", "") + "@" + r["Grid_Size"]
+            agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    durs = collections.defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
+        key = r["Kernel_Name"].split("(")[0].replace("void ", "") + "@" + r["Grid_Size_X"]
+        durs[key].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    trace = {k: sum(v) / len(v) for k, v in durs.items()}
     out = {}
     for k, d in agg.items():
         if not any(x in k for x in ("score_pairs", "env_step", "env_replay")) or k not in trace:
