@@ -17,7 +17,8 @@ from uavhip.policy import TransformerActorCritic  # noqa: E402
 from uavhip.train import FusedPPOTrainer  # noqa: E402
 
 NAMES = {0: "start", 1: "heads bwd", 2: "c.head.0", 52: "c.embed", 53: "a.head.0", 54: "a.embed",
-         55: "c.emb loads", 56: "c.emb acc", 57: "a.emb loads", 58: "a.emb acc"}
+         55: "c.emb loads", 56: "c.emb acc", 57: "a.emb loads", 58: "a.emb acc",
+         59: "hb.loads+sums", 60: "hb.per-sample+sync", 61: "hb.dz+sync"}
 LAYER = ["start", "LN2", "sync", "du gemm", "sync", "W1 gemm", "sync", "LN1", "sync", "Wo gemm", "sync",
          "attn0+sync", "Win0+sync", "attn1+sync", "Win1", "res+sync"]
 for base, tag in ((4, "C1"), (20, "C0"), (36, "A")):

@@ -2801,6 +2801,7 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     } else {
         tot0 = io.tot[0]; tot1 = io.tot[1]; tot2 = io.tot[2]; tot3 = io.tot[3];
     }
+    BTR(59);
     st4(zs + (zt * SPW + zp) * HID + 4 * zq, zr);
     if (tid_x() < SPW) {
         const int p = tid_x();
@@ -2847,6 +2848,7 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         }
     }
     __syncthreads();
+    BTR(60);
     static_assert(NTHR % HID == 0, "dz loop: j = tid % 64 for every i");
     for (int i = tid_x(); i < 2 * SPW * HID; i += NTHR) {
         const int trunk = i / (SPW * HID), p = (i / HID) % SPW, j = i % HID;
@@ -2858,6 +2860,7 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         (trunk ? dzc : sm.z)[p * LDZ + j] = dz;
     }
     __syncthreads();
+    BTR(61);
     // head.0 bias partials (sum over the 16 samples of dz, from LDS)
     if (tid_x() < 2 * HID && role != 1 + (tid_x() / HID ^ 1)) {
         const int trunk = tid_x() / HID, j = tid_x() % HID;
