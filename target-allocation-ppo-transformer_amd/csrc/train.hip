@@ -512,6 +512,15 @@ inline bool wgrad_direct(int max_slabs) {
     return e && e[0] == '1' && max_slabs <= kWgDirectMaxSlabs;
 }
 
+// Weight gradients in chunked mode (WgBatch::chunk: one (chunk, tile) per workgroup, operand-sharing
+// tiles on one XCD) for long k ranges (>= 64 slabs: 2048 rows); UAVHIP_WGRAD_CHUNK=0 / 1 forces
+// stream-K / chunked.
+inline bool wgrad_chunked(int max_slabs) {
+    const char* e = std::getenv("UAVHIP_WGRAD_CHUNK");
+    if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+    return max_slabs >= 64;
+}
+
 // Trunk split for this minibatch size (UAVHIP_TRUNK_SPLIT=0 turns it off: tests compare both ways).
 inline int split_blocks(int Bm) {
     const char* e = std::getenv("UAVHIP_TRUNK_SPLIT");
@@ -740,10 +749,11 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
             hipLaunchKernelGGL(k_wgrad, dim3(wp.b.tiles), dim3(kWgThreads), 0, st, wp.b);
             TR_CHECK(check_launch("k_wgrad"));
         } else {
+            if (wp.ok && wgrad_chunked(wp.max_slabs()) && !wp.chunked()) wp.b.chunk = 0;
             const bool sched = wp.ok && wp.tiles([&](const WgTileRuns& t) {
                 const WgProb& P = wp.b.p[t.prob];
                 seg(p.wg_part + (size_t)t.first_slot * kWgSlot, dst[t.prob] + t.m0 * P.N + t.n0, t.rows * kWgT, t.runs,
-                    kWgRuns * kWgSlot, p.wg_part + (size_t)t.rest_slot * kWgSlot, P.N);
+                    t.run_stride * kWgSlot, p.wg_part + (size_t)t.rest_slot * kWgSlot, P.N);
             });
             if (!sched) {
                 set_error("uavhip_ppo_step: weight-gradient problems do not fit the stream-K schedule");

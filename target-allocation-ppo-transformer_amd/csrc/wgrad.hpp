@@ -9,10 +9,23 @@
 // tile per (workgroup, tile) run into slot kWgRuns w + j (j = the run's index within the
 // workgroup). The host enumerates the same runs (WgPlan) to build the reduction segments: a tile's
 // runs are slot kWgRuns w0 + j0, then kWgRuns w + 0 for w = w0 + 1 .. w1.
+//
+// Chunked mode (WgBatch::chunk > 0, large minibatches): every tile's k range is cut into chunks of
+// `chunk` slabs, and workgroup v takes exactly one (problem, chunk, tile) triple, numbered
+// problem-major, then chunk, then tile -- so the tiles that share an operand slab (the m-tiles of
+// in_proj / FFN1 share X, FFN2's two n-tiles share dY) are consecutive. v is the XCD-aware virtual
+// index of blockIdx.x (workgroups are dealt to the 8 XCDs round-robin: v = (b % 8) G / 8 + b / 8), so
+// consecutive v run at the same time on the same XCD and the second and third readers of a slab find
+// it in that XCD's L2 instead of HBM. One run per workgroup: slot kWgRuns v; a tile's runs are
+// slot kWgRuns (wg_begin + t), then every kWgRuns tiles slots.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+
+#ifndef UAVHIP_EXP
+#define UAVHIP_EXP 0  // timing experiments (A/B builds, results wrong): 51 no loads after the first two
+#endif                // slabs, 52 one MFMA of six, 53 no split arithmetic
 
 namespace uavhip {
 namespace tr {
@@ -41,6 +54,7 @@ struct WgProb {
     int tiles_n, tiles, slabs;  // per problem: column tiles, tiles, slabs per tile
     int unit_begin;             // first slab unit of this problem
     int tile_begin;             // first output tile of this problem (direct mode: its workgroup)
+    int wg_begin;               // chunked mode: first workgroup (virtual index) of this problem
     int dst;                    // direct mode: float offset of dW [M][N] in `grads`
 };
 // Direct mode (small minibatches: every tile a few slabs): one workgroup per output tile runs all
@@ -52,6 +66,7 @@ struct WgBatch {
     int units;
     float* part;  // [grid * kWgRuns][kWgSlot]
     int direct, tiles;
+    int chunk, wgs;  // chunked mode: slabs per chunk (0: stream-K), workgroups holding work
     float* grads;
     float* sq;
     float unscale;
@@ -76,6 +91,15 @@ __device__ __forceinline__ int wg_find_tile(const WgBatch& b, int t) {
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
         if (t >= b.p[mid].tile_begin) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int wg_find_wg(const WgBatch& b, int v) {
+    int lo = 0, hi = b.n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (v >= b.p[mid].wg_begin) lo = mid;
         else hi = mid;
     }
     return lo;
@@ -151,6 +175,10 @@ __device__ __forceinline__ void wg_split_store(const f32x4 v, char* plane, int o
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         x1[j] = (_Float16)v[j];
+        if constexpr (UAVHIP_EXP == 53) {
+            x2[j] = x3[j] = x1[j];
+            continue;
+        }
         const float r1 = v[j] - (float)x1[j];                 // exact
         x2[j] = f16_lo(v[j], x1[j]);                          // = f16(r1 2^11)
         x3[j] = (_Float16)((r1 - (float)x2[j] * (1.0f / 2048.0f)) * 4194304.f);  // r1 - x2 2^-11: exact
@@ -188,7 +216,16 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
     const long long U = wb.units, G = gridDim.x;
     int u = (int)(blockIdx.x * U / G);
     int u_end = (int)((blockIdx.x + 1) * U / G);
-    if (wb.direct) {  // workgroup = output tile: all of its slabs
+    int slot_wg = blockIdx.x;
+    if (wb.chunk) {  // one (chunk, tile) per workgroup, siblings on one XCD (G % 8 == 0: host)
+        slot_wg = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+        if (slot_wg >= wb.wgs) return;
+        const WgProb& Q = wb.p[wg_find_wg(wb, slot_wg)];
+        const int local = slot_wg - Q.wg_begin, c = local / Q.tiles, t = local - c * Q.tiles;
+        const int s0 = c * wb.chunk;
+        u = Q.unit_begin + t * Q.slabs + s0;
+        u_end = u + min(wb.chunk, Q.slabs - s0);
+    } else if (wb.direct) {  // workgroup = output tile: all of its slabs
         const WgProb& Q = wb.p[wg_find_tile(wb, blockIdx.x)];
         u = Q.unit_begin + (blockIdx.x - Q.tile_begin) * Q.slabs;
         u_end = u + Q.slabs;
@@ -235,6 +272,11 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
 #pragma unroll
                 for (int b = 0; b < 2; ++b) {
                     hi[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[a], b1[b], hi[a][b], 0, 0, 0);
+                    if constexpr (UAVHIP_EXP == 52) {  // keep the operands live
+                        mid[a][b] += __builtin_bit_cast(f32x4, a2[a]) + __builtin_bit_cast(f32x4, b2[b]);
+                        lo[a][b] += __builtin_bit_cast(f32x4, a3[a]) + __builtin_bit_cast(f32x4, b3[b]);
+                        continue;
+                    }
                     mid[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[a], b2[b], mid[a][b], 0, 0, 0);
                     mid[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[a], b1[b], mid[a][b], 0, 0, 0);
                     lo[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[a], b3[b], lo[a][b], 0, 0, 0);
@@ -243,7 +285,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
                 }
             if (s + 1 < n_slabs) {  // slab s + 1 (landed in registers meanwhile) -> the other stage
                 wg_stage_store(nx, wg_smem + ((s + 1) & 1) * kWgStageB, xmode, xg);
-                if (s + 2 < n_slabs) wg_gload(nx, P, (s0 + s + 2) * kWgBK, m0, n0);
+                if (s + 2 < n_slabs && UAVHIP_EXP != 51) wg_gload(nx, P, (s0 + s + 2) * kWgBK, m0, n0);
             }
             __syncthreads();  // the next stage is written; everyone is done reading this one
         }
@@ -278,7 +320,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
             }
             return;
         }
-        float* out = wb.part + (size_t)(blockIdx.x * kWgRuns + run) * kWgSlot;
+        float* out = wb.part + (size_t)(slot_wg * kWgRuns + run) * kWgSlot;
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -297,8 +339,8 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
 struct WgTileRuns {
     int prob, m0, n0, rows;  // output tile (rows = valid rows, <= 128)
     int first_slot;          // slot of the first run
-    int rest_slot;           // slot of the second run; later runs every kWgRuns slots
-    int runs;
+    int rest_slot;           // slot of the second run; later runs every run_stride slots
+    int runs, run_stride;
 };
 struct WgPlan {
     WgBatch b{};
@@ -320,6 +362,7 @@ struct WgPlan {
         P.slabs = K / kWgBK;
         P.unit_begin = b.units;
         P.tile_begin = b.tiles;
+        P.wg_begin = 0;
         P.dst = 0;
         b.units += P.tiles * P.slabs;
         b.tiles += P.tiles;
@@ -329,12 +372,49 @@ struct WgPlan {
         for (int i = 0; i < b.n; ++i) m = std::max(m, b.p[i].slabs);
         return m;
     }
+    // Chunked mode: the smallest chunk (slabs) whose (problem, chunk, tile) triples fit kWgGrid
+    // workgroups; grid = their count rounded up to the 8 XCDs. False if none fits.
+    bool chunked() {
+        const int ms = max_slabs();
+        for (int ch = 1; ch <= ms; ++ch) {
+            int wgs = 0;
+            for (int i = 0; i < b.n; ++i) {
+                b.p[i].wg_begin = wgs;
+                wgs += b.p[i].tiles * ((b.p[i].slabs + ch - 1) / ch);
+            }
+            if (wgs <= kWgGrid) {
+                b.chunk = ch;
+                b.wgs = wgs;
+                grid = (wgs + 7) / 8 * 8;
+                return true;
+            }
+        }
+        return false;
+    }
     // Workgroup w's unit range, as the kernel computes it.
     int w_begin(int w) const { return (int)((long long)w * b.units / grid); }
     // Enumerate every tile's runs (calls f(WgTileRuns)); false if a workgroup would need more than
     // kWgRuns slots.
     template <class F>
     bool tiles(F&& f) {
+        if (b.chunk) {
+            for (int pi = 0; pi < b.n; ++pi) {
+                const WgProb& P = b.p[pi];
+                for (int t = 0; t < P.tiles; ++t) {
+                    WgTileRuns tr;
+                    tr.prob = pi;
+                    tr.m0 = (t / P.tiles_n) * kWgT;
+                    tr.n0 = (t % P.tiles_n) * kWgT;
+                    tr.rows = std::min(kWgT, P.M - tr.m0);
+                    tr.first_slot = (P.wg_begin + t) * kWgRuns;
+                    tr.rest_slot = (P.wg_begin + t + P.tiles) * kWgRuns;
+                    tr.runs = (P.slabs + b.chunk - 1) / b.chunk;
+                    tr.run_stride = P.tiles * kWgRuns;
+                    f(tr);
+                }
+            }
+            return true;
+        }
         grid = std::min(kWgGrid, b.units);
         for (int w = 0; w < grid; ++w) {  // runs per workgroup = tiles its range meets
             int u = w_begin(w), e = w_begin(w + 1), runs = 0;
@@ -377,6 +457,7 @@ struct WgPlan {
                 tr.first_slot = w0 * kWgRuns + j0;
                 tr.rest_slot = (w0 + 1) * kWgRuns;
                 tr.runs = w1 - w0 + 1;
+                tr.run_stride = kWgRuns;
                 f(tr);
             }
         }

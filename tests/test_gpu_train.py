@@ -440,6 +440,39 @@ def test_wgrad_direct_mode_matches_stream_k(monkeypatch):
     torch.testing.assert_close(out["0"][2], out["1"][2], rtol=1e-5, atol=1e-7)
 
 
+def test_wgrad_chunked_mode_matches_stream_k(monkeypatch):
+    """Minibatch 4096: the weight-gradient GEMM in chunked mode (the default for k ranges of >= 64
+    slabs: one (chunk, tile) per workgroup, the tiles that share an operand slab consecutive on one
+    XCD, wgrad.hpp) against stream-K (UAVHIP_WGRAD_CHUNK=0): the same split products summed in
+    another grouping, so every gradient agrees to fp32 reordering (1e-5 of its tensor's max at 20480
+    rows), the statistics to 1e-5, and both runs are deterministic (a repeat is bitwise equal)."""
+    from uavhip.policy import TransformerActorCritic, layout
+    from uavhip.train import FusedPPOTrainer
+    torch.manual_seed(51)
+    base = TransformerActorCritic().cuda()
+    bufs = _buffers(4096, seed=52)
+    idx = torch.randperm(4096, generator=torch.Generator().manual_seed(53)).to(torch.int32).cuda()
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("UAVHIP_WGRAD_CHUNK", mode)
+        tr = FusedPPOTrainer(copy.deepcopy(base), 4096)
+        tr.set_buffers(*bufs)
+        g = tr.gradients(idx).clone()
+        g2 = tr.gradients(idx).clone()
+        torch.cuda.synchronize()
+        assert torch.equal(g, g2), f"mode {mode}: not deterministic"
+        out[mode] = g
+    offs, _ = layout()
+    worst = 0.0
+    for (k, p), o in zip(base.named_parameters(), offs):
+        a, b = out["0"][o:o + p.numel()], out["1"][o:o + p.numel()]
+        scale = float(a.abs().max())
+        err = float((a - b).abs().max())
+        worst = max(worst, err / (scale + 1e-30))
+        assert err <= 1e-5 * scale + 1e-12, f"{k}: {err:.3e} vs max {scale:.3e}"
+    print(f"chunked vs stream-K: worst |d| / tensor max = {worst:.3e}")
+
+
 def test_packed_weights_repack_on_device():
     """TransformerActorCritic.packed_weights() repacks on the device (uavhip_policy_pack) from the
     flat parameter buffer -- zero-copy when the parameters are views of FusedPPOTrainer's buffer,
