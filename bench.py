@@ -409,8 +409,8 @@ def ppo_update_rate(args, eng, policy, world, dist, dev, E, T):
         trainer.set_buffers(*bufs)
         if world == 1:
             trainer.capture()  # once per buffer set (not timed): replays cover every later update
-            impl = ("HIP training step (uavhip_ppo_step: fused forward / backward kernels, stream-K weight-gradient "
-                    "MFMA GEMM, fused clip + Adam), one hipGraph replay per epoch")
+            impl = ("HIP training step (uavhip_ppo_step: fused forward / backward kernels, weight-gradient "
+                    "MFMA GEMM (chunked, XCD-aware), fused clip + Adam), one hipGraph replay per epoch")
         else:
             impl = ("HIP training step, data parallel: forward / all-reduce loss sums / backward / "
                     "all-reduce grads / clip+Adam per global minibatch")
