@@ -9,6 +9,11 @@ import sys
 
 import numpy as np
 
+# one trunk order in every workgroup, so "cycles since block start" medians line up phase by phase
+# (TrainIO::mix / BwdIO::mix run half the workgroups in the other order)
+os.environ.setdefault("UAVHIP_FWD_MIX", "0")
+os.environ.setdefault("UAVHIP_BWD_MIX", "0")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "target-allocation-ppo-transformer_amd"))
 import torch  # noqa: E402

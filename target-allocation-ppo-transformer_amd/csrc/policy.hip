@@ -1700,6 +1700,11 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     }
     const bool do_actor = role != 2, do_critic = role != 1;
     const int b0 = blk * SPW;
+    // training forward without the trunk split (TrainIO::mix): every other group of 8 workgroups
+    // runs the critic trunk first, so the two trunks' HBM-heavy activation stores and compute phases
+    // overlap across the chip (as K6's BwdIO::mix)
+    [[maybe_unused]] bool critic_first = false;
+    if constexpr (TR) critic_first = role == 0 && io.mix && ((blk >> 3) & 1);
     PTR(0);
     // training mode: the first trunk's embedding operands and first K/V weight blocks are loaded
     // before the minibatch gather stores its rows (a load behind a store burst waits for the burst)
@@ -1707,7 +1712,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     [[maybe_unused]] KvPre<kActorTrunk, 0, TR, kTrainSplit> pkv_a;
     [[maybe_unused]] KvPre<kCriticTrunk, 0, TR, kTrainSplit> pkv_c;
     if constexpr (TR) {
-        if (do_actor) {
+        if (do_actor && !critic_first) {
             ep_a = embed_load<kActorTrunk>(TID_C P);
             pkv_a = kv_prefetch<kActorTrunk, 0, TR, kTrainSplit>(TID_C P);
         } else {
@@ -1733,7 +1738,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     // training mode: the actor head's and the critic embedding's / first GEMM's operands are loaded
     // ahead of the actor's LN2 activation stores (layer_tail hook)
     APre<4> ph;
-    if (do_actor) {
+    auto actor = [&] {
         if constexpr (!ROWS) {
             if constexpr (TR) {
                 // the split layer-0 in_proj reads the embedding's planes in sm.ctx
@@ -1743,7 +1748,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
                 __syncthreads();
                 auto hook = [&] {
                     if (wv < 4) ph = prefetch<4>(TID_C headw_a, D, 16 * wv, 0);
-                    if (do_critic) {
+                    if (do_critic && !critic_first) {
                         ep_c = embed_load<kCriticTrunk>(TID_C P);
                         pkv_c = kv_prefetch<kCriticTrunk, 0, TR, kTrainSplit>(TID_C P);
                     }
@@ -1762,7 +1767,8 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
         PTR(3);
         head_mlp<kActorHead, 2>(TID_C sm, P, ph, sm.logits);
         if (TR) store_hidden(TID_C sm, io.z[0], b0);  // before the critic's LayerNorm partials reuse sm.z
-    }  // do_actor
+    };
+    if (do_actor && !critic_first) actor();
     PTR(4);
     // fused env step (ENV): two envs per wave side by side, state loads issued before the critic head
     [[maybe_unused]] const bool env_grp =
@@ -1817,6 +1823,14 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
         PTR(6);
         if (TR) store_hidden(TID_C sm, io.z[1], b0);
     }  // do_critic
+    if constexpr (TR) {
+        if (critic_first) {  // the actor's operands now (not prefetched: the critic's hooks are full)
+            ep_a = embed_load<kActorTrunk>(TID_C P);
+            pkv_a = kv_prefetch<kActorTrunk, 0, TR, kTrainSplit>(TID_C P);
+            __syncthreads();  // the actor's trunk reuses the critic's buffers (sm.z after store_hidden)
+            actor();
+        }
+    }
     if (TR) {
         if (role == 0) {
             loss_partials(TID_C sm, io, b0);
@@ -2916,6 +2930,31 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
     heads_bwd(sm, P, io, b0, role);
     __syncthreads();
     BTR(1);
+    // Trunk order (BwdIO::mix): the actor and critic trunks are independent below the heads, so
+    // every other group of 8 workgroups (one per XCD) runs the actor first: at any time half the
+    // chip is in the other trunk's phases, and the HBM-heavy phases of one overlap the compute of
+    // the other instead of all 256 workgroups streaming at once. The critic's dz rows (sm.ctx + 64,
+    // clobbered by the actor's layer) come back from io.dz[1], which heads_bwd wrote with them.
+    const bool actor_first = role == 0 && io.mix && ((blk >> 3) & 1);
+    // actor: head.0, layer 0 (pruned), embedding (twice in the code, once per order: a loop over
+    // the two trunks let LICM keep weight prefetches live across both and spilled 578 VGPRs)
+    auto actor = [&] {
+        head_input_grad(sm, PT + kHeadT, sm.z);
+        __syncthreads();
+        BTR(53);
+        EmbBwdPre ep;
+        bwd_layer<kActorTrunk, 0, true, 36, NoHook, kBwdFull, kBwdSplit>(sm, P, PT, io.L[0], b0, &ep, io.e[0], io.xg);
+        embed_bwd(sm, ep, io.epart + (size_t)blk * 2 * kEmbPart, 57);
+        BTR(54);
+    };
+    if (actor_first) {
+        actor();
+        __syncthreads();  // the critic's trunk reuses every buffer
+        float* dzc = sm.ctx + 64;
+        for (int i = tid_x(); i < SPW * HID; i += NTHR)
+            dzc[(i / HID) * LDZ + i % HID] = io.dz[1][(size_t)(b0 + i / HID) * HID + i % HID];
+        __syncthreads();
+    }
     if (role != 1) {  // critic: head.0, layer 1 (pruned), layer 0, embedding
         head_input_grad(sm, PT + kHeadT + D * HID, sm.ctx + 64);
         __syncthreads();
@@ -2934,15 +2973,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_backward(const float* __restric
         __syncthreads();
         BTR(52);
     }
-    if (role != 2) {  // actor: head.0, layer 0 (pruned), embedding
-        head_input_grad(sm, PT + kHeadT, sm.z);
-        __syncthreads();
-        BTR(53);
-        EmbBwdPre ep;
-        bwd_layer<kActorTrunk, 0, true, 36, NoHook, kBwdFull, kBwdSplit>(sm, P, PT, io.L[0], b0, &ep, io.e[0], io.xg);
-        embed_bwd(sm, ep, io.epart + (size_t)blk * 2 * kEmbPart, 57);
-        BTR(54);
-    }
+    if (role != 2 && !actor_first) actor();
 }
 
 // ================================================================== K7: position-split training step

@@ -33,6 +33,7 @@ struct TrainIO {
     // (the two trunks are independent until the loss); the loss partials then come from
     // k_loss_partials. 0: both trunks in every workgroup.
     int split;
+    int mix;    // no trunk split: every other group of 8 workgroups runs the critic trunk first
 };
 
 // ---- K6: fused backward of the three encoder layers + embeddings (policy.hip), one workgroup per
@@ -80,6 +81,7 @@ struct BwdIO {
     float* epart;            // [Bm/16][2][kEmbPart] embedding gradient partials
     BwdLayerIO L[3];         // actor L0 (pruned), critic L0 (full), critic L1 (pruned)
     int split;               // trunk split as in TrainIO (actor workgroups first)
+    int mix;                 // K6 without the trunk split: every other group of 8 workgroups runs the actor first
 };
 // Transposed copies of each layer's GEMM weights in fragment order (the dX GEMMs' A operands):
 // in_proj^T [128][384] | out_proj^T [128][128] | linear1^T [128][256] | linear2^T [256][128].

@@ -521,6 +521,18 @@ inline bool wgrad_chunked(int max_slabs) {
     return max_slabs >= 64;
 }
 
+// K6's trunk order mixed across workgroups (BwdIO::mix; UAVHIP_BWD_MIX=0: every workgroup critic first)
+inline int bwd_mix() {
+    const char* e = std::getenv("UAVHIP_BWD_MIX");
+    return !(e && e[0] == '0');
+}
+
+// The training forward's trunk order mixed across workgroups (TrainIO::mix; UAVHIP_FWD_MIX=0: actor first)
+inline int fwd_mix() {
+    const char* e = std::getenv("UAVHIP_FWD_MIX");
+    return !(e && e[0] == '0');
+}
+
 // Trunk split for this minibatch size (UAVHIP_TRUNK_SPLIT=0 turns it off: tests compare both ways).
 inline int split_blocks(int Bm) {
     const char* e = std::getenv("UAVHIP_TRUNK_SPLIT");
@@ -606,6 +618,7 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
             TR_CHECK(pol::policy_forward_ps(p.packed, states, io, Bm, st));
         } else {
             io.split = split_blocks(Bm);
+            io.mix = fwd_mix();
             TR_CHECK(pol::policy_forward_train(p.packed, states, io, Bm, st));
             if (io.split) TR_CHECK(pol::policy_loss_partials(io, Bm, st));
         }
@@ -669,6 +682,7 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         io.e[1] = p.e_c;
         io.epart = p.epart;
         io.split = ps ? 0 : split_blocks(Bm);
+        io.mix = bwd_mix();
         const LayerBufs* lb[3] = {&A, &C0, &C1};
         for (int i = 0; i < 3; ++i)
             io.L[i] = pol::BwdLayerIO{lb[i]->qkv, lb[i]->xhat1, lb[i]->rstd1, lb[i]->u, lb[i]->xhat2, lb[i]->rstd2,

@@ -473,6 +473,32 @@ def test_wgrad_chunked_mode_matches_stream_k(monkeypatch):
     print(f"chunked vs stream-K: worst |d| / tensor max = {worst:.3e}")
 
 
+def test_trunk_order_mix_is_bitwise(monkeypatch):
+    """Minibatch 4096 (no trunk split): the training forward with every other group of 8 workgroups
+    running the critic trunk first (TrainIO::mix) and K6 with them running the actor first
+    (BwdIO::mix), both the default, against the fixed orders (UAVHIP_FWD_MIX=0, UAVHIP_BWD_MIX=0)
+    in all four combinations. Each workgroup computes the same values in another order of its two
+    independent trunks (K6's critic dz rows come back from the buffer heads_bwd wrote them to):
+    gradients and loss sums bitwise equal."""
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.train import FusedPPOTrainer
+    torch.manual_seed(61)
+    base = TransformerActorCritic().cuda()
+    bufs = _buffers(4096, seed=62)
+    idx = torch.randperm(4096, generator=torch.Generator().manual_seed(63)).to(torch.int32).cuda()
+    out = {}
+    for mode in ("00", "01", "10", "11"):
+        monkeypatch.setenv("UAVHIP_FWD_MIX", mode[0])
+        monkeypatch.setenv("UAVHIP_BWD_MIX", mode[1])
+        tr = FusedPPOTrainer(copy.deepcopy(base), 4096)
+        tr.set_buffers(*bufs)
+        out[mode] = (tr.gradients(idx).clone(), tr.loss_sums.clone())
+    torch.cuda.synchronize()
+    for mode in ("01", "10", "11"):
+        assert torch.equal(out["00"][0], out[mode][0]), mode
+        assert torch.equal(out["00"][1], out[mode][1]), mode
+
+
 def test_packed_weights_repack_on_device():
     """TransformerActorCritic.packed_weights() repacks on the device (uavhip_policy_pack) from the
     flat parameter buffer -- zero-copy when the parameters are views of FusedPPOTrainer's buffer,
