@@ -533,6 +533,12 @@ inline int fwd_mix() {
     return !(e && e[0] == '0');
 }
 
+// Every weight-gradient tile on three-plane products (UAVHIP_WGRAD_PLANES=3; default: the key rows only)
+inline bool wgrad_all_three_planes() {
+    const char* e = std::getenv("UAVHIP_WGRAD_PLANES");
+    return e && e[0] == '3';
+}
+
 // Trunk split for this minibatch size (UAVHIP_TRUNK_SPLIT=0 turns it off: tests compare both ways).
 inline int split_blocks(int Bm) {
     const char* e = std::getenv("UAVHIP_TRUNK_SPLIT");
@@ -729,17 +735,24 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
             return XSrc{xhat, kWgXAffine, prm(c, layer_param(tr_, ly, w)), prm(c, layer_param(tr_, ly, w + 1))};
         };
         auto emb_out = [&](const float* e, int tr_) { return XSrc{e, kWgXPosRow, nullptr, prm(c, tr_ + POS)}; };
-        auto dw = [&](const float* dY, int ldy, const XSrc& X, int ldx, int M, int N, int K, int dst_w) {
+        // p3: the tiles that keep three-plane products (WgProb::p3_tiles): the key rows of in_proj,
+        // whose sums cancel (softmax drops any per-query constant, so a sample's dk rows sum to
+        // zero); every other tile is two-plane. UAVHIP_WGRAD_PLANES=3: every tile three-plane.
+        const bool all3 = wgrad_all_three_planes();
+        auto dw = [&](const float* dY, int ldy, const XSrc& X, int ldx, int M, int N, int K, int dst_w, int p3 = 0) {
             dst[wp.b.n] = dst_w;
             wp.add(dY, ldy, X.x, ldx, M, N, K, X.mode, X.g, X.b);
-            if (wp.ok) wp.b.p[wp.b.n - 1].dst = dst_w;
+            if (wp.ok) {
+                wp.b.p[wp.b.n - 1].dst = dst_w;
+                wp.b.p[wp.b.n - 1].p3_tiles = all3 ? ~0 : p3;
+            }
         };
         auto layer_dw = [&](const LayerBufs& B, int tr_, int ly, const XSrc& hin, int rows) {
             const int pw = kOffs.o[layer_param(tr_, ly, INW)];
-            if (rows == R) {
-                dw(B.dqkv, 3 * D, hin, D, 3 * D, D, R, pw);
-            } else {  // pruned: K/V rows over all R rows, Q rows over the Bm token-4 rows
-                dw(B.dqkv + D, 3 * D, hin, D, 2 * D, D, R, pw + D * D);
+            if (rows == R) {  // Q | K | V rows: m-tile 1 = the key rows
+                dw(B.dqkv, 3 * D, hin, D, 3 * D, D, R, pw, 0b010);
+            } else {  // pruned: K/V rows over all R rows (m-tile 0 = keys), Q rows over the Bm token-4 rows
+                dw(B.dqkv + D, 3 * D, hin, D, 2 * D, D, R, pw + D * D, 0b01);
                 dw(B.dqkv + (S - 1) * 3 * D, S * 3 * D, hin.at_token4(), S * D, D, D, Bm, pw);
             }
             dw(B.dz1, D, XSrc{B.o, kWgX, nullptr, nullptr}, D, D, D, rows, kOffs.o[layer_param(tr_, ly, OUTW)]);

@@ -55,6 +55,7 @@ struct WgProb {
     int unit_begin;             // first slab unit of this problem
     int tile_begin;             // first output tile of this problem (direct mode: its workgroup)
     int wg_begin;               // chunked mode: first workgroup (virtual index) of this problem
+    int p3_tiles;               // bit t: tile t runs three-plane products (else two-plane)
     int dst;                    // direct mode: float offset of dW [M][N] in `grads`
 };
 // Direct mode (small minibatches: every tile a few slabs): one workgroup per output tile runs all
@@ -170,6 +171,7 @@ __device__ __forceinline__ f32x4 wg_xgamma(const WgProb& P, int n0) {
     const f32x4 g = *reinterpret_cast<const f32x4*>(P.xg + n0 + 4 * (threadIdx.x & 31));
     return P.xmode == kWgXAffine ? g : f32x4{1.f, 1.f, 1.f, 1.f};
 }
+template <bool P3>  // P3: the third plane (two-plane tiles neither write nor read it)
 __device__ __forceinline__ void wg_split_store(const f32x4 v, char* plane, int off) {
     wg_f16x4 x1, x2, x3;
 #pragma unroll
@@ -181,21 +183,22 @@ __device__ __forceinline__ void wg_split_store(const f32x4 v, char* plane, int o
         }
         const float r1 = v[j] - (float)x1[j];                 // exact
         x2[j] = f16_lo(v[j], x1[j]);                          // = f16(r1 2^11)
-        x3[j] = (_Float16)((r1 - (float)x2[j] * (1.0f / 2048.0f)) * 4194304.f);  // r1 - x2 2^-11: exact
+        if constexpr (P3) x3[j] = (_Float16)((r1 - (float)x2[j] * (1.0f / 2048.0f)) * 4194304.f);  // exact
     }
     *reinterpret_cast<wg_f16x4*>(plane + off) = x1;
     *reinterpret_cast<wg_f16x4*>(plane + kWgPlaneB + off) = x2;
-    *reinterpret_cast<wg_f16x4*>(plane + 2 * kWgPlaneB + off) = x3;
+    if constexpr (P3) *reinterpret_cast<wg_f16x4*>(plane + 2 * kWgPlaneB + off) = x3;
 }
 // the X operand as the forward formed it: x-hat * gamma + beta (its LayerNorm epilogue's expression),
 // e + pos[s] (gamma 1: exact), or x itself (applied at staging: the slab's loads have landed by then)
+template <bool P3>
 __device__ __forceinline__ void wg_stage_store(const WgSlab& r, char* stage, int xmode, const f32x4 xg) {
     const int t = threadIdx.x, c4 = t & 31;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int off = wg_swz((t >> 5) + 16 * i, c4 >> 1) + 8 * (c4 & 1);
-        wg_split_store(r.a[i], stage, off);
-        wg_split_store(xmode != kWgX ? r.b[i] * xg + r.x[i] : r.b[i], stage + 3 * kWgPlaneB, off);
+        wg_split_store<P3>(r.a[i], stage, off);
+        wg_split_store<P3>(xmode != kWgX ? r.b[i] * xg + r.x[i] : r.b[i], stage + 3 * kWgPlaneB, off);
     }
 }
 // 16 columns (c16 .. c16 + 15) x 8 consecutive k (8 g ..) of a plane: lane (i16, g) gets column
@@ -207,6 +210,63 @@ __device__ __forceinline__ wg_f16x8 wg_frag(const char* plane, int c16) {
     const wg_i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((wg_lds_i16x4*)(plane + wg_swz(r0 + 4, ch) + sub));
     const wg_f16x4 a = __builtin_bit_cast(wg_f16x4, lo), b = __builtin_bit_cast(wg_f16x4, hi);
     return wg_f16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+// One tile run's k-loop: slabs s0 .. s0 + n_slabs - 1 of problem P into hi / mid / lo. P3: the
+// three-plane products (6 MFMAs per block); otherwise two planes (x = x1 + 2^-11 x2, dropped terms
+// 2^-22 of a product: hi += a1b1, mid += a1b2 + a2b1, lo += a2b2, 4 MFMAs), for the tiles whose sums
+// do not cancel (WgProb::p3_tiles).
+template <bool P3>
+__device__ __forceinline__ void wg_kloop(char* wg_smem, const WgProb& P, int s0, int n_slabs, int m0, int n0, int mt0,
+                                         int nt0, f32x4 (&hi)[4][2], f32x4 (&mid)[4][2], f32x4 (&lo)[4][2],
+                                         [[maybe_unused]] int run) {
+        const int xmode = P.xmode;
+        const f32x4 xg = wg_xgamma(P, n0);
+        WgSlab nx;
+        wg_gload(nx, P, s0 * kWgBK, m0, n0);
+        wg_stage_store<P3>(nx, wg_smem, xmode, xg);
+        if (n_slabs > 1) wg_gload(nx, P, (s0 + 1) * kWgBK, m0, n0);
+        __syncthreads();
+        WTR(1 + 4 * run);
+        for (int s = 0; s < n_slabs; ++s) {
+            const char* st = wg_smem + (s & 1) * kWgStageB;
+            wg_f16x8 a1[4], a2[4], a3[4], b1[2], b2[2], b3[2];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                a1[a] = wg_frag(st, 16 * (mt0 + a));
+                a2[a] = wg_frag(st + kWgPlaneB, 16 * (mt0 + a));
+                if constexpr (P3) a3[a] = wg_frag(st + 2 * kWgPlaneB, 16 * (mt0 + a));
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                b1[b] = wg_frag(st + 3 * kWgPlaneB, 16 * (nt0 + b));
+                b2[b] = wg_frag(st + 4 * kWgPlaneB, 16 * (nt0 + b));
+                if constexpr (P3) b3[b] = wg_frag(st + 5 * kWgPlaneB, 16 * (nt0 + b));
+            }
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    hi[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[a], b1[b], hi[a][b], 0, 0, 0);
+                    if constexpr (UAVHIP_EXP == 52 && P3) {  // keep the operands live
+                        mid[a][b] += __builtin_bit_cast(f32x4, a2[a]) + __builtin_bit_cast(f32x4, b2[b]);
+                        lo[a][b] += __builtin_bit_cast(f32x4, a3[a]) + __builtin_bit_cast(f32x4, b3[b]);
+                        continue;
+                    }
+                    mid[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[a], b2[b], mid[a][b], 0, 0, 0);
+                    mid[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[a], b1[b], mid[a][b], 0, 0, 0);
+                    if constexpr (P3) {
+                        lo[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[a], b3[b], lo[a][b], 0, 0, 0);
+                        lo[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a3[a], b1[b], lo[a][b], 0, 0, 0);
+                    }
+                    lo[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[a], b2[b], lo[a][b], 0, 0, 0);
+                }
+            if (s + 1 < n_slabs) {  // slab s + 1 (landed in registers meanwhile) -> the other stage
+                wg_stage_store<P3>(nx, wg_smem + ((s + 1) & 1) * kWgStageB, xmode, xg);
+                if (s + 2 < n_slabs && UAVHIP_EXP != 51) wg_gload(nx, P, (s0 + s + 2) * kWgBK, m0, n0);
+            }
+            __syncthreads();  // the next stage is written; everyone is done reading this one
+        }
 }
 
 __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
@@ -244,51 +304,8 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
         for (int a = 0; a < 4; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) hi[a][b] = mid[a][b] = lo[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int xmode = P.xmode;
-        const f32x4 xg = wg_xgamma(P, n0);
-        WgSlab nx;
-        wg_gload(nx, P, s0 * kWgBK, m0, n0);
-        wg_stage_store(nx, wg_smem, xmode, xg);
-        if (n_slabs > 1) wg_gload(nx, P, (s0 + 1) * kWgBK, m0, n0);
-        __syncthreads();
-        WTR(1 + 4 * run);
-        for (int s = 0; s < n_slabs; ++s) {
-            const char* st = wg_smem + (s & 1) * kWgStageB;
-            wg_f16x8 a1[4], a2[4], a3[4], b1[2], b2[2], b3[2];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                a1[a] = wg_frag(st, 16 * (mt0 + a));
-                a2[a] = wg_frag(st + kWgPlaneB, 16 * (mt0 + a));
-                a3[a] = wg_frag(st + 2 * kWgPlaneB, 16 * (mt0 + a));
-            }
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                b1[b] = wg_frag(st + 3 * kWgPlaneB, 16 * (nt0 + b));
-                b2[b] = wg_frag(st + 4 * kWgPlaneB, 16 * (nt0 + b));
-                b3[b] = wg_frag(st + 5 * kWgPlaneB, 16 * (nt0 + b));
-            }
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int b = 0; b < 2; ++b) {
-                    hi[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[a], b1[b], hi[a][b], 0, 0, 0);
-                    if constexpr (UAVHIP_EXP == 52) {  // keep the operands live
-                        mid[a][b] += __builtin_bit_cast(f32x4, a2[a]) + __builtin_bit_cast(f32x4, b2[b]);
-                        lo[a][b] += __builtin_bit_cast(f32x4, a3[a]) + __builtin_bit_cast(f32x4, b3[b]);
-                        continue;
-                    }
-                    mid[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[a], b2[b], mid[a][b], 0, 0, 0);
-                    mid[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[a], b1[b], mid[a][b], 0, 0, 0);
-                    lo[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[a], b3[b], lo[a][b], 0, 0, 0);
-                    lo[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a3[a], b1[b], lo[a][b], 0, 0, 0);
-                    lo[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[a], b2[b], lo[a][b], 0, 0, 0);
-                }
-            if (s + 1 < n_slabs) {  // slab s + 1 (landed in registers meanwhile) -> the other stage
-                wg_stage_store(nx, wg_smem + ((s + 1) & 1) * kWgStageB, xmode, xg);
-                if (s + 2 < n_slabs && UAVHIP_EXP != 51) wg_gload(nx, P, (s0 + s + 2) * kWgBK, m0, n0);
-            }
-            __syncthreads();  // the next stage is written; everyone is done reading this one
-        }
+        if ((P.p3_tiles >> tile) & 1) wg_kloop<true>(wg_smem, P, s0, n_slabs, m0, n0, mt0, nt0, hi, mid, lo, run);
+        else wg_kloop<false>(wg_smem, P, s0, n_slabs, m0, n0, mt0, nt0, hi, mid, lo, run);
         WTR(2 + 4 * run);
         // lane (i16, g) of tile (a, b) holds dW[m0 + 16 (mt0 + a) + 4 g + r][n0 + 16 (nt0 + b) + i16]
         if (wb.direct) {  // the whole tile: dW itself, unscaled, rows < M (a 64-row problem), and g^2
@@ -363,6 +380,7 @@ struct WgPlan {
         P.unit_begin = b.units;
         P.tile_begin = b.tiles;
         P.wg_begin = 0;
+        P.p3_tiles = ~0;
         P.dst = 0;
         b.units += P.tiles * P.slabs;
         b.tiles += P.tiles;
