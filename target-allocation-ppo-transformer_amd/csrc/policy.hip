@@ -1738,37 +1738,46 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     // training mode: the actor head's and the critic embedding's / first GEMM's operands are loaded
     // ahead of the actor's LN2 activation stores (layer_tail hook)
     APre<4> ph;
-    auto actor = [&] {
-        if constexpr (!ROWS) {
-            if constexpr (TR) {
-                // the split layer-0 in_proj reads the embedding's planes in sm.ctx
-                embed_apply<kActorTrunk, TR, kEmbH, split_kv<kActorTrunk, 0, TR, kTrainSplit>()>(TID_C sm, ep_a, io.e[0],
-                                                                                               nullptr, b0);
-                PTR(2);
-                __syncthreads();
-                auto hook = [&] {
-                    if (wv < 4) ph = prefetch<4>(TID_C headw_a, D, 16 * wv, 0);
-                    if (do_critic && !critic_first) {
-                        ep_c = embed_load<kCriticTrunk>(TID_C P);
-                        pkv_c = kv_prefetch<kCriticTrunk, 0, TR, kTrainSplit>(TID_C P);
-                    }
-                };
-                encoder_layer<kActorTrunk, 0, true, TR, decltype(hook), kTrainSplit>(TID_C sm, P, pkv_a, io.L[0], b0, hook);
-            } else {
-                APre<2> pkv = prefetch<2>(TID_C P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
-                embed<kActorTrunk, TR>(TID_C sm, P, io.e[0], nullptr, b0);
-                PTR(2);
-                __syncthreads();
-                encoder_layer<kActorTrunk, 0, true, TR>(TID_C sm, P, pkv, io.L[0], b0);
-            }
+    // the training forward's actor (a lambda: TrainIO::mix calls it after the critic in half the
+    // workgroups); the inference forward keeps its inline block below (the same code as before the
+    // mix: as a lambda, its register allocation changed and the NOENV build of k_rollout_steps went
+    // from 3 to 11 VGPR spills, skewing the env-step differential)
+    [[maybe_unused]] auto actor = [&] {
+        if constexpr (TR && !ROWS) {
+            // the split layer-0 in_proj reads the embedding's planes in sm.ctx
+            embed_apply<kActorTrunk, TR, kEmbH, split_kv<kActorTrunk, 0, TR, kTrainSplit>()>(TID_C sm, ep_a, io.e[0],
+                                                                                           nullptr, b0);
+            PTR(2);
+            __syncthreads();
+            auto hook = [&] {
+                if (wv < 4) ph = prefetch<4>(TID_C headw_a, D, 16 * wv, 0);
+                if (do_critic && !critic_first) {
+                    ep_c = embed_load<kCriticTrunk>(TID_C P);
+                    pkv_c = kv_prefetch<kCriticTrunk, 0, TR, kTrainSplit>(TID_C P);
+                }
+            };
+            encoder_layer<kActorTrunk, 0, true, TR, decltype(hook), kTrainSplit>(TID_C sm, P, pkv_a, io.L[0], b0, hook);
+            __syncthreads();
+            PTR(3);
+            head_mlp<kActorHead, 2>(TID_C sm, P, ph, sm.logits);
+            store_hidden(TID_C sm, io.z[0], b0);  // before the critic's LayerNorm partials reuse sm.z
         }
-        if (!TR && wv < 4) ph = prefetch<4>(TID_C headw_a, D, 16 * wv, 0);
+    };
+    if constexpr (TR) {
+        if (do_actor && !critic_first) actor();
+    } else if (do_actor) {
+        if constexpr (!ROWS) {
+            APre<2> pkv = prefetch<2>(TID_C P + kOffs.o[layer_param(kActorTrunk, 0, INW)], D, kv_row(wv, 0), 0);
+            embed<kActorTrunk, TR>(TID_C sm, P, io.e[0], nullptr, b0);
+            PTR(2);
+            __syncthreads();
+            encoder_layer<kActorTrunk, 0, true, TR>(TID_C sm, P, pkv, io.L[0], b0);
+        }
+        if (wv < 4) ph = prefetch<4>(TID_C headw_a, D, 16 * wv, 0);
         __syncthreads();
         PTR(3);
         head_mlp<kActorHead, 2>(TID_C sm, P, ph, sm.logits);
-        if (TR) store_hidden(TID_C sm, io.z[0], b0);  // before the critic's LayerNorm partials reuse sm.z
-    };
-    if (do_actor && !critic_first) actor();
+    }  // do_actor
     PTR(4);
     // fused env step (ENV): two envs per wave side by side, state loads issued before the critic head
     [[maybe_unused]] const bool env_grp =
