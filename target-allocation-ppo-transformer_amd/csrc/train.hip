@@ -533,6 +533,14 @@ inline int fwd_mix() {
     return !(e && e[0] == '0');
 }
 
+// Chunk length of the three-plane problems relative to the two-plane ones in the chunked schedule
+// (UAVHIP_WGRAD_P3_RATIO, default 0.75: the per-slab cost ratio of the two forms)
+inline float wgrad_p3_ratio() {
+    const char* e = std::getenv("UAVHIP_WGRAD_P3_RATIO");
+    const float r = e ? (float)std::atof(e) : 0.75f;
+    return r > 0.f && r <= 1.f ? r : 0.75f;
+}
+
 // Every weight-gradient tile on three-plane products (UAVHIP_WGRAD_PLANES=3; default: the key rows only)
 inline bool wgrad_all_three_planes() {
     const char* e = std::getenv("UAVHIP_WGRAD_PLANES");
@@ -749,10 +757,15 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         };
         auto layer_dw = [&](const LayerBufs& B, int tr_, int ly, const XSrc& hin, int rows) {
             const int pw = kOffs.o[layer_param(tr_, ly, INW)];
-            if (rows == R) {  // Q | K | V rows: m-tile 1 = the key rows
-                dw(B.dqkv, 3 * D, hin, D, 3 * D, D, R, pw, 0b010);
-            } else {  // pruned: K/V rows over all R rows (m-tile 0 = keys), Q rows over the Bm token-4 rows
-                dw(B.dqkv + D, 3 * D, hin, D, 2 * D, D, R, pw + D * D, 0b01);
+            // Q, K and V rows as problems of their own, so that the chunked schedule can give the
+            // three-plane key rows shorter chunks (WgPlan::chunked)
+            if (rows == R) {
+                dw(B.dqkv, 3 * D, hin, D, D, D, R, pw);
+                dw(B.dqkv + D, 3 * D, hin, D, D, D, R, pw + D * D, 1);
+                dw(B.dqkv + 2 * D, 3 * D, hin, D, D, D, R, pw + 2 * D * D);
+            } else {  // pruned: K / V rows over all R rows, Q rows over the Bm token-4 rows
+                dw(B.dqkv + D, 3 * D, hin, D, D, D, R, pw + D * D, 1);
+                dw(B.dqkv + 2 * D, 3 * D, hin, D, D, D, R, pw + 2 * D * D);
                 dw(B.dqkv + (S - 1) * 3 * D, S * 3 * D, hin.at_token4(), S * D, D, D, Bm, pw);
             }
             dw(B.dz1, D, XSrc{B.o, kWgX, nullptr, nullptr}, D, D, D, rows, kOffs.o[layer_param(tr_, ly, OUTW)]);
@@ -776,7 +789,7 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
             hipLaunchKernelGGL(k_wgrad, dim3(wp.b.tiles), dim3(kWgThreads), 0, st, wp.b);
             TR_CHECK(check_launch("k_wgrad"));
         } else {
-            if (wp.ok && wgrad_chunked(wp.max_slabs()) && !wp.chunked()) wp.b.chunk = 0;
+            if (wp.ok && wgrad_chunked(wp.max_slabs()) && !wp.chunked(wgrad_p3_ratio())) wp.b.chunk = 0;
             const bool sched = wp.ok && wp.tiles([&](const WgTileRuns& t) {
                 const WgProb& P = wp.b.p[t.prob];
                 seg(p.wg_part + (size_t)t.first_slot * kWgSlot, dst[t.prob] + t.m0 * P.N + t.n0, t.rows * kWgT, t.runs,

@@ -11,7 +11,8 @@
 // runs are slot kWgRuns w0 + j0, then kWgRuns w + 0 for w = w0 + 1 .. w1.
 //
 // Chunked mode (WgBatch::chunk > 0, large minibatches): every tile's k range is cut into chunks of
-// `chunk` slabs, and workgroup v takes exactly one (problem, chunk, tile) triple, numbered
+// WgProb::chunk slabs (shorter for the three-plane problems: WgPlan::chunked), and workgroup v takes
+// exactly one (problem, chunk, tile) triple, numbered
 // problem-major, then chunk, then tile -- so the tiles that share an operand slab (the m-tiles of
 // in_proj / FFN1 share X, FFN2's two n-tiles share dY) are consecutive. v is the XCD-aware virtual
 // index of blockIdx.x (workgroups are dealt to the 8 XCDs round-robin: v = (b % 8) G / 8 + b / 8), so
@@ -37,7 +38,7 @@ constexpr int kWgBK = 32;                 // k rows per slab (one 32-k MFMA bloc
 constexpr int kWgThreads = 512;
 constexpr int kWgRuns = 3;                // partial slots per workgroup
 constexpr int kWgSlot = kWgT * kWgT;      // floats per partial slot
-constexpr int kWgMaxProbs = 16;
+constexpr int kWgMaxProbs = 24;
 constexpr int kWgGrid = 256;              // one workgroup per CU
 
 // X operands the training forward does not store: a LayerNorm output is formed from
@@ -56,6 +57,7 @@ struct WgProb {
     int tile_begin;             // first output tile of this problem (direct mode: its workgroup)
     int wg_begin;               // chunked mode: first workgroup (virtual index) of this problem
     int p3_tiles;               // bit t: tile t runs three-plane products (else two-plane)
+    int chunk;                  // chunked mode: slabs per chunk of this problem's tiles
     int dst;                    // direct mode: float offset of dW [M][N] in `grads`
 };
 // Direct mode (small minibatches: every tile a few slabs): one workgroup per output tile runs all
@@ -282,9 +284,9 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
         if (slot_wg >= wb.wgs) return;
         const WgProb& Q = wb.p[wg_find_wg(wb, slot_wg)];
         const int local = slot_wg - Q.wg_begin, c = local / Q.tiles, t = local - c * Q.tiles;
-        const int s0 = c * wb.chunk;
+        const int s0 = c * Q.chunk;
         u = Q.unit_begin + t * Q.slabs + s0;
-        u_end = u + min(wb.chunk, Q.slabs - s0);
+        u_end = u + min(Q.chunk, Q.slabs - s0);
     } else if (wb.direct) {  // workgroup = output tile: all of its slabs
         const WgProb& Q = wb.p[wg_find_tile(wb, blockIdx.x)];
         u = Q.unit_begin + (blockIdx.x - Q.tile_begin) * Q.slabs;
@@ -381,6 +383,7 @@ struct WgPlan {
         P.tile_begin = b.tiles;
         P.wg_begin = 0;
         P.p3_tiles = ~0;
+        P.chunk = 0;
         P.dst = 0;
         b.units += P.tiles * P.slabs;
         b.tiles += P.tiles;
@@ -390,15 +393,21 @@ struct WgPlan {
         for (int i = 0; i < b.n; ++i) m = std::max(m, b.p[i].slabs);
         return m;
     }
-    // Chunked mode: the smallest chunk (slabs) whose (problem, chunk, tile) triples fit kWgGrid
-    // workgroups; grid = their count rounded up to the 8 XCDs. False if none fits.
-    bool chunked() {
+    // Chunked mode: the smallest chunk ch (slabs) whose (problem, chunk, tile) triples fit kWgGrid
+    // workgroups, where a problem with three-plane tiles gets chunks of ch * p3_ratio slabs (a
+    // three-plane slab costs more: 6 MFMAs and three planes against 4 and two, so its workgroups
+    // would otherwise finish last and set the launch's time); grid = the count rounded up to the 8
+    // XCDs. False if none fits.
+    bool chunked(float p3_ratio = 0.75f) {
         const int ms = max_slabs();
         for (int ch = 1; ch <= ms; ++ch) {
+            const int ch3 = std::max(1, (int)(ch * p3_ratio + 0.5f));
             int wgs = 0;
             for (int i = 0; i < b.n; ++i) {
-                b.p[i].wg_begin = wgs;
-                wgs += b.p[i].tiles * ((b.p[i].slabs + ch - 1) / ch);
+                WgProb& P = b.p[i];
+                P.wg_begin = wgs;
+                P.chunk = P.p3_tiles & ((1 << P.tiles) - 1) ? ch3 : ch;
+                wgs += P.tiles * ((P.slabs + P.chunk - 1) / P.chunk);
             }
             if (wgs <= kWgGrid) {
                 b.chunk = ch;
@@ -426,7 +435,7 @@ struct WgPlan {
                     tr.rows = std::min(kWgT, P.M - tr.m0);
                     tr.first_slot = (P.wg_begin + t) * kWgRuns;
                     tr.rest_slot = (P.wg_begin + t + P.tiles) * kWgRuns;
-                    tr.runs = (P.slabs + b.chunk - 1) / b.chunk;
+                    tr.runs = (P.slabs + P.chunk - 1) / P.chunk;
                     tr.run_stride = P.tiles * kWgRuns;
                     f(tr);
                 }

@@ -21,16 +21,23 @@ namespace {
 constexpr int D = 128, FF = 256, HID = 64, S = 5;
 alignas(16) float g_dummy[64];
 
-// train.hip layer_dw: C0 (full, R rows), A and C1 (pruned: K|V over R rows, the rest over Bm), the heads
+// train.hip layer_dw: C0 (full, R rows: Q, K, V rows as three problems), A and C1 (pruned: K and V
+// over R rows, the rest over Bm), the heads; the key-row problems three-plane (p3_tiles)
 bool build(WgPlan& wp, int Bm) {
     const int R = S * Bm;
-    auto dw = [&](int M, int N, int K) { wp.add(g_dummy, M, g_dummy, N, M, N, K); };
-    dw(3 * D, D, R);
+    auto dw = [&](int M, int N, int K, int p3 = 0) {
+        wp.add(g_dummy, M, g_dummy, N, M, N, K);
+        if (wp.ok) wp.b.p[wp.b.n - 1].p3_tiles = p3;
+    };
+    dw(D, D, R);
+    dw(D, D, R, 1);
+    dw(D, D, R);
     dw(D, D, R);
     dw(FF, D, R);
     dw(D, FF, R);
     for (int l = 0; l < 2; ++l) {
-        dw(2 * D, D, R);
+        dw(D, D, R, 1);
+        dw(D, D, R);
         dw(D, D, Bm);
         dw(D, D, Bm);
         dw(FF, D, Bm);
@@ -61,9 +68,9 @@ std::vector<Run> decode(const WgBatch& wb, int G, int b) {
         while (qi + 1 < wb.n && slot_wg >= wb.p[qi + 1].wg_begin) ++qi;
         const WgProb& Q = wb.p[qi];
         const int local = slot_wg - Q.wg_begin, c = local / Q.tiles, t = local - c * Q.tiles;
-        const int s0 = c * wb.chunk;
+        const int s0 = c * Q.chunk;
         u = Q.unit_begin + t * Q.slabs + s0;
-        u_end = u + std::min(wb.chunk, Q.slabs - s0);
+        u_end = u + std::min(Q.chunk, Q.slabs - s0);
     }
     int run = 0;
     while (u < u_end) {
@@ -125,8 +132,11 @@ int check(int Bm, bool chunked) {
         if (named != slots_of[{t.prob, tile}]) return fail("reduction map != the tile's run slots", Bm, mode);
         if (t.rows != std::min(kWgT, P.M - t.m0)) return fail("tile rows", Bm, mode);
     }
-    std::printf("ok Bm=%d %s: %d problems, %d tiles, %lld units, grid %d, chunk %d\n", Bm, mode, wb.n, wb.tiles,
-                units, G, wb.chunk);
+    int ch3 = 0;
+    for (int pi = 0; pi < wb.n; ++pi)
+        if (wb.p[pi].p3_tiles) ch3 = wb.p[pi].chunk;
+    std::printf("ok Bm=%d %s: %d problems, %d tiles, %lld units, grid %d, chunk %d (three-plane %d)\n", Bm, mode,
+                wb.n, wb.tiles, units, G, wb.chunk, ch3);
     return 0;
 }
 }  // namespace
