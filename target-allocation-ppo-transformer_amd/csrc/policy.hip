@@ -2031,14 +2031,41 @@ int launch_rollout_steps(const float* P, float* obs, int B, uint64_t seed, uint6
 
 #ifndef UAVHIP_STEPS_TU
 // Ring fill of one trunk: u rows of positions 0-3 of the workgroup's 16 windows -> slots
-// (g + 1 + s) mod 5, the same GEMM (k order, bias add) as the forward's new-row u.
+// (g + 1 + s) mod 5, the same GEMM (k order, bias add) as the forward's new-row u. Every global
+// operand of a trunk's fill -- the embedding's, the wave's in_proj row tiles (all k blocks) and
+// their biases -- is one FillPre, loaded ahead (k_policy_rows_fill: the actor's before the window
+// rows, the critic's before the actor's GEMMs), so a trunk's fill waits for one L2 round trip
+// instead of one per row tile and k-block pair.
 template <int trunk>
-__device__ void rows_fill_trunk(Smem& sm, const float* __restrict__ P, const RowIO& rio, int b0) {
+struct FillPre {
+    static constexpr int NP = row_parts<trunk>();
+    using W = std::conditional_t<split_ring<trunk>(), HPre<4>, APre<KB>>;
+    EmbPre ep;
+    W w[NP];
+    f32x4 bb[NP];
+};
+template <int trunk>
+__device__ __forceinline__ void fill_load_w(FillPre<trunk>& r, const float* __restrict__ P) {
+    constexpr int NP = row_parts<trunk>(), P0 = 3 - NP;
+    const int g = lane_id() >> 4, wv = tid_x() >> 6;
+    const float* bin = P + kOffs.o[layer_param(trunk, 0, INB)];
+#pragma unroll
+    for (int j = P0; j < 3; ++j) {
+        const int row = j * D + 16 * wv;
+        if constexpr (split_ring<trunk>()) r.w[j - P0] = hprefetch<4>(P, split_slot(layer_param(trunk, 0, INW)), D, row, 0);
+        else r.w[j - P0] = prefetch<KB>(P + kOffs.o[layer_param(trunk, 0, INW)], D, row, 0);
+        r.bb[j - P0] = *reinterpret_cast<const f32x4*>(bin + row + 4 * g);
+    }
+}
+// `after_first` runs after the first row tile's GEMM (the next trunk's weights are issued there,
+// once this trunk's first tile has released its registers).
+template <int trunk, class F>
+__device__ void rows_fill_trunk(Smem& sm, const float* __restrict__ P, const FillPre<trunk>& pre, const RowIO& rio,
+                                int b0, F after_first) {
     constexpr int NP = row_parts<trunk>(), P0 = 3 - NP, ROFF = trunk == kActorTrunk ? 0 : 2 * D;
     const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
-    const float* bin = P + kOffs.o[layer_param(trunk, 0, INB)];
     const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
-    embed_apply<trunk, false, kEmbRows>(sm, embed_load<trunk>(P));
+    embed_apply<trunk, false, kEmbRows>(sm, pre.ep);
     __syncthreads();
     float* slots = rio.rp + kPposFloats;
 #pragma unroll
@@ -2050,14 +2077,14 @@ __device__ void rows_fill_trunk(Smem& sm, const float* __restrict__ P, const Row
             constexpr int si = split_slot(layer_param(trunk, 0, INW));
             f32x4 lo[S - 1];
             zero(lo);
-            hgemm_tile<S - 1, 2>(acc, lo, hprefetch<2>(P, si, D, row, 0), P, si, D, row, 0,
-                                 reinterpret_cast<const _Float16*>(sm.ctx), 0);
+            hgemm_tile<S - 1, 4>(acc, lo, pre.w[j - P0], P, si, D, row, 0, reinterpret_cast<const _Float16*>(sm.ctx), 0);
 #pragma unroll
             for (int s = 0; s < S - 1; ++s) acc[s] += lo[s] * kLoScale;
         } else {
-            gemm_tile<S - 1, 2>(acc, prefetch<2>(Win, D, row, 0), Win, D, row, 0, sm.ctx, LDH, 0);
+            gemm_tile<S - 1, KB>(acc, pre.w[j - P0], Win, D, row, 0, sm.ctx, LDH, 0);
         }
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(bin + row + 4 * g);
+        if (j == P0) after_first();
+        const f32x4 bb = pre.bb[j - P0];
         const int b = b0 + i16;
         if (b < rio.B) {
 #pragma unroll
@@ -2069,47 +2096,56 @@ __device__ void rows_fill_trunk(Smem& sm, const float* __restrict__ P, const Row
     __syncthreads();  // sm.ctx is the next trunk's embedding
 }
 
-// Win pos_s of one trunk -> rp[trunk][s][384] (no bias): pos rows as activation tile columns 0-4.
+// Win pos_s of one trunk -> rp[trunk][s][384] (no bias): pos rows as activation tile columns 0-4;
+// part j = rows [128 j, 128 j + 128) (Q, K or V), its weight blocks loaded before the pos rows.
+constexpr int kPposParts = 6;  // (trunk, j) pairs
 template <int trunk>
-__device__ void rows_ppos_trunk(Smem& sm, const float* __restrict__ P, float* out) {
+__device__ void rows_ppos_part(Smem& sm, const float* __restrict__ P, float* out, int j) {
     const float* Win = P + kOffs.o[layer_param(trunk, 0, INW)];
     const float* pos = P + kOffs.o[trunk + POS];
     const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
+    const int row = j * D + 16 * wv;
+    const APre<KB> pw = prefetch<KB>(Win, D, row, 0);
     for (int i = tid_x(); i < SPW * D; i += NTHR) {
         const int t = i / D, k = i - t * D;
         sm.h[t * LDH + k] = t < S ? pos[t * D + k] : 0.f;
     }
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const int row = j * D + 16 * wv;
-        f32x4 acc[1];
-        zero(acc);
-        gemm_tile<1, 2>(acc, prefetch<2>(Win, D, row, 0), Win, D, row, 0, sm.h, LDH, 0);
-        if (i16 < S) *reinterpret_cast<f32x4*>(out + i16 * 3 * D + row + 4 * g) = acc[0];
-    }
-    __syncthreads();
+    f32x4 acc[1];
+    zero(acc);
+    gemm_tile<1, KB>(acc, pw, Win, D, row, 0, sm.h, LDH, 0);
+    if (i16 < S) *reinterpret_cast<f32x4*>(out + i16 * 3 * D + row + 4 * g) = acc[0];
 }
 
 // uavhip_policy_forward_rows with fill: rebuilds the ring rows of positions 0-3 of every window
-// (blocks < nb) and the Win pos_s table (block nb) from the current weights.
+// (blocks < nb) and the Win pos_s table (blocks < kPposParts, one (trunk, part) each, after their
+// fill: the grid is max(nb, kPposParts) blocks). The table used to be one extra block of its own:
+// with one workgroup per CU it waited for a free CU and then ran six serial GEMMs, 28 us per
+// launch against ~10 us now (r04x / r04y).
 __global__ __launch_bounds__(NTHR) void k_policy_rows_fill(const float* __restrict__ P,
                                                            const float* __restrict__ states, const RowIO rio) {
     __shared__ __attribute__((aligned(16))) Smem sm;
     const int nb = (rio.B + SPW - 1) / SPW;
-    if ((int)blockIdx.x == nb) {
-        rows_ppos_trunk<kActorTrunk>(sm, P, rio.rp);
-        rows_ppos_trunk<kCriticTrunk>(sm, P, rio.rp + S * 3 * D);
-        return;
+    if ((int)blockIdx.x < nb) {
+        const int b0 = blockIdx.x * SPW;
+        FillPre<kActorTrunk> fa;
+        FillPre<kCriticTrunk> fc;
+        fa.ep = embed_load<kActorTrunk>(P);
+        fill_load_w(fa, P);
+        fc.ep = embed_load<kCriticTrunk>(P);
+        for (int i = tid_x(); i < (S - 1) * SPW * LDX; i += NTHR) {  // positions 0-3 only
+            const int t = i / LDX, k = i - t * LDX, s = t / SPW, p = t - s * SPW;
+            sm.x[i] = (k < IN && b0 + p < rio.B) ? states[((size_t)(b0 + p) * S + s) * IN + k] : 0.f;
+        }
+        __syncthreads();
+        rows_fill_trunk<kActorTrunk>(sm, P, fa, rio, b0, [&] { fill_load_w(fc, P); });
+        rows_fill_trunk<kCriticTrunk>(sm, P, fc, rio, b0, [] {});  // ends with a barrier
     }
-    const int b0 = blockIdx.x * SPW;
-    for (int i = tid_x(); i < (S - 1) * SPW * LDX; i += NTHR) {  // positions 0-3 only
-        const int t = i / LDX, k = i - t * LDX, s = t / SPW, p = t - s * SPW;
-        sm.x[i] = (k < IN && b0 + p < rio.B) ? states[((size_t)(b0 + p) * S + s) * IN + k] : 0.f;
+    if ((int)blockIdx.x < kPposParts) {  // block-uniform
+        const int t = blockIdx.x;
+        if (t < 3) rows_ppos_part<kActorTrunk>(sm, P, rio.rp, t);
+        else rows_ppos_part<kCriticTrunk>(sm, P, rio.rp + S * 3 * D, t - 3);
     }
-    __syncthreads();
-    rows_fill_trunk<kActorTrunk>(sm, P, rio, b0);
-    rows_fill_trunk<kCriticTrunk>(sm, P, rio, b0);
 }
 
 // ================================================================== K6: fused training backward
@@ -3023,19 +3059,28 @@ __device__ __forceinline__ void ps_rows_in(float* dst, int lds, const float* __r
 
 // Embedding of window position s (transformer_net.py:57-59): h = relu(W_e x + b_e) + pos[s] -> sm.h
 // rows 16 s + p and the e / h0 workspace rows; wave w computes features [16 w, 16 w + 16).
-template <int trunk, bool PL = false>  // PL: also the planes of h into sm.ctx (ps_inproj_split's operand)
-__device__ void ps_embed(Smem& sm, const float* __restrict__ P, float* __restrict__ e_out, float* __restrict__ h_out,
-                         int b0, int s) {
+// The embedding's global operands (ps_embed_load: issued by k_ps_f1 before the window gather).
+struct PsEmbPre {
+    f32x4 a, bb, pp;
+};
+__device__ __forceinline__ PsEmbPre ps_embed_load(const float* __restrict__ P, int trunk, int s) {
     const float* We = P + kOffs.o[trunk + EMB_W];
     const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
     const int f = 16 * wv + i16;
-    f32x4 a;
-    a.x = 4 * g + 0 < IN ? We[f * IN + 4 * g + 0] : 0.f;
-    a.y = 4 * g + 1 < IN ? We[f * IN + 4 * g + 1] : 0.f;
-    a.z = 4 * g + 2 < IN ? We[f * IN + 4 * g + 2] : 0.f;
-    a.w = 4 * g + 3 < IN ? We[f * IN + 4 * g + 3] : 0.f;
-    const f32x4 bb = ld4(P + kOffs.o[trunk + EMB_B] + 16 * wv + 4 * g);
-    const f32x4 pp = ld4(P + kOffs.o[trunk + POS] + s * D + 16 * wv + 4 * g);
+    PsEmbPre r;
+    r.a.x = 4 * g + 0 < IN ? We[f * IN + 4 * g + 0] : 0.f;
+    r.a.y = 4 * g + 1 < IN ? We[f * IN + 4 * g + 1] : 0.f;
+    r.a.z = 4 * g + 2 < IN ? We[f * IN + 4 * g + 2] : 0.f;
+    r.a.w = 4 * g + 3 < IN ? We[f * IN + 4 * g + 3] : 0.f;
+    r.bb = ld4(P + kOffs.o[trunk + EMB_B] + 16 * wv + 4 * g);
+    r.pp = ld4(P + kOffs.o[trunk + POS] + s * D + 16 * wv + 4 * g);
+    return r;
+}
+template <bool PL = false>  // PL: also the planes of h into sm.ctx (ps_inproj_split's operand)
+__device__ void ps_embed(Smem& sm, const PsEmbPre& ep, float* __restrict__ e_out, float* __restrict__ h_out, int b0,
+                         int s) {
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
+    const f32x4 a = ep.a, bb = ep.bb, pp = ep.pp;
     const f32x4 x = ld4(sm.x + (s * SPW + i16) * LDX + 4 * g);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -3066,21 +3111,43 @@ __device__ void ps_inproj(Smem& sm, const float* __restrict__ W, const float* __
     }
 }
 
-// ps_inproj as split products: the operand planes of the 16 tokens at X rows 16 s + p, W's split copy at soff
-__device__ void ps_inproj_split(const float* __restrict__ P, int soff, const float* __restrict__ bias,
-                                float* __restrict__ qkv, int tile0, int s, int b0, const _Float16* X) {
+// ps_inproj as split products: the operand planes of the 16 tokens at X rows 16 s + p, W's split copy at soff.
+// Every weight block and bias of the wave's (at most 3) row tiles is loaded in one round
+// (ps_inproj_load, which a caller issues ahead of the operand's producer): one exposed L2 round trip
+// instead of one per tile -- the same MFMA sequence per tile, so the same sums.
+constexpr int kPsInTiles = 3;  // row tiles per wave: 24 tiles of in_proj over 8 waves
+struct PsInPre {
+    HPre<4> w[kPsInTiles];
+    f32x4 bb[kPsInTiles];
+};
+__device__ __forceinline__ void ps_inproj_load(PsInPre& r, const float* __restrict__ P, int soff,
+                                               const float* __restrict__ bias, int tile0) {
+    const int g = lane_id() >> 4, wv = tid_x() >> 6;
+#pragma unroll
+    for (int k = 0; k < kPsInTiles; ++k) {
+        // unconditional loads (a tile below tile0 reloads tile wv: loaded, never used)
+        const int t = tile0 + wv + NW * k, row = 16 * (t < 3 * D / 16 ? t : wv);
+        r.w[k] = hprefetch<4>(P, soff, D, row, 0);
+        r.bb[k] = ld4(bias + row + 4 * g);
+    }
+}
+__device__ void ps_inproj_split(const PsInPre& pre, const float* __restrict__ P, int soff, float* __restrict__ qkv,
+                                int tile0, int s, int b0, const _Float16* X) {
     const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
     const size_t r = (size_t)trow(s * SPW + i16, b0);
-    for (int t = tile0 + wv; t < 3 * D / 16; t += NW) {  // wave-uniform
+#pragma unroll
+    for (int k = 0; k < kPsInTiles; ++k) {
+        const int t = tile0 + wv + NW * k;
+        if (t >= 3 * D / 16) break;  // wave-uniform
         const int row = 16 * t;
-        const f32x4 bb = ld4(bias + row + 4 * g);
         f32x4 hi[1], lo[1];
         zero(hi);
         zero(lo);
-        hgemm_tile<1, 2>(hi, lo, hprefetch<2>(P, soff, D, row, 0), P, soff, D, row, 0, X, s * SPW);
-        st4(qkv + r * 3 * D + row + 4 * g, hi[0] + lo[0] * kLoScale + bb);
+        hgemm_tile<1, 4>(hi, lo, pre.w[k], P, soff, D, row, 0, X, s * SPW);
+        st4(qkv + r * 3 * D + row + 4 * g, hi[0] + lo[0] * kLoScale + pre.bb[k]);
     }
 }
+static_assert(NW * kPsInTiles == 3 * D / 16, "ps_inproj_load covers every in_proj row tile");
 
 // Q of position s and K | V of all five positions for the heads of chunk c -> sm.big [tok][Q|K|V];
 // in two halves so that chunk 1's loads can be in flight during chunk 0's attention
@@ -3139,17 +3206,21 @@ __global__ __launch_bounds__(NTHR) void k_ps_f1(const float* __restrict__ P, con
     __shared__ __attribute__((aligned(16))) Smem sm;
     const int blk = blockIdx.x / 10, r = blockIdx.x % 10, s = r % S, b0 = blk * SPW;
     const bool critic = r >= S;
+    const int trunk = critic ? kCriticTrunk : kActorTrunk;
+    // the actor's only layer is pruned: Q at position 4 only
+    const int tile0 = critic || s == S - 1 ? 0 : D / 16;
+    const int soff = critic ? split_slot(layer_param(kCriticTrunk, 0, INW)) : split_slot(layer_param(kActorTrunk, 0, INW));
+    // every global operand of the embedding and of the in_proj GEMM first: their L2 round trip
+    // overlaps the window gather's
+    const PsEmbPre ep = ps_embed_load(P, trunk, s);
+    [[maybe_unused]] PsInPre wp;
+    if constexpr (kPsSplit) ps_inproj_load(wp, P, soff, P + kOffs.o[layer_param(trunk, 0, INB)], tile0);
     gather_windows<true>(sm, states, B, io, b0, r == 0);  // one workgroup per block writes the rows
     __syncthreads();
-    const int trunk = critic ? kCriticTrunk : kActorTrunk;
-    if (critic) ps_embed<kCriticTrunk, kPsSplit>(sm, P, io.e[1], io.h0[1], b0, s);
-    else ps_embed<kActorTrunk, kPsSplit>(sm, P, io.e[0], io.h0[0], b0, s);
+    ps_embed<kPsSplit>(sm, ep, io.e[critic ? 1 : 0], io.h0[critic ? 1 : 0], b0, s);
     __syncthreads();
-    // the actor's only layer is pruned: Q at position 4 only
     if constexpr (kPsSplit) {
-        ps_inproj_split(P, critic ? split_slot(layer_param(kCriticTrunk, 0, INW)) : split_slot(layer_param(kActorTrunk, 0, INW)),
-                        P + kOffs.o[layer_param(trunk, 0, INB)], io.L[critic ? 1 : 0].qkv, critic || s == S - 1 ? 0 : D / 16,
-                        s, b0, reinterpret_cast<const _Float16*>(sm.ctx));
+        ps_inproj_split(wp, P, soff, io.L[critic ? 1 : 0].qkv, tile0, s, b0, reinterpret_cast<const _Float16*>(sm.ctx));
     } else {
         ps_inproj(sm, P + kOffs.o[layer_param(trunk, 0, INW)], P + kOffs.o[layer_param(trunk, 0, INB)],
                   io.L[critic ? 1 : 0].qkv, critic || s == S - 1 ? 0 : D / 16, s, b0);
@@ -3161,21 +3232,34 @@ __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, con
     const int blk = blockIdx.x / 6, r = blockIdx.x % 6, b0 = blk * SPW, wv = tid_x() >> 6;
     const bool critic = r < S;
     const int s = critic ? r : S - 1, ti = critic ? 1 : 0;
+    // the out-projection's first weight blocks ahead of the attention (whose Q | K | V loads and
+    // barriers then cover their round trip)
+    [[maybe_unused]] HPre<2> po;
+    if constexpr (kPsSplit)
+        po = hprefetch<2>(P, critic ? split_slot(layer_param(kCriticTrunk, 0, OUTW)) : split_slot(layer_param(kActorTrunk, 0, OUTW)),
+                          D, 16 * wv, 0);
     ps_mask(sm, io.mask, b0);
     ps_rows_in(sm.h, LDH, io.h0[ti], D, 0, D, s, b0);  // the layer input (residual) of the position
     ps_attention<kPsSplit>(sm, io.L[ti].qkv, s, b0);
+    [[maybe_unused]] APre<4> ph;
     if constexpr (kPsSplit) {  // the layer tails and the next in_proj as split products
         if (critic) {
-            const HPre<2> po = hprefetch<2>(P, split_slot(layer_param(kCriticTrunk, 0, OUTW)), D, 16 * wv, 0);
-            layer_tail_split<kCriticTrunk, 0, false, true, NoHook, 1>(sm, P, po, io.L[1], b0, NoHook{}, s * SPW);
+            // layer 1's in_proj weights and biases are issued before LN2 (the tail's hook), behind
+            // every weight load of the tail
+            constexpr int s1 = split_slot(layer_param(kCriticTrunk, 1, INW));
+            const int tile0 = s == S - 1 ? 0 : D / 16;
+            PsInPre wp;
+            auto hook = [&] { ps_inproj_load(wp, P, s1, P + kOffs.o[layer_param(kCriticTrunk, 1, INB)], tile0); };
+            layer_tail_split<kCriticTrunk, 0, false, true, decltype(hook), 1>(sm, P, po, io.L[1], b0, hook, s * SPW);
             __syncthreads();
             // layer 1 (pruned) of this position: K | V, and Q at position 4, from LN2's planes in sm.h
-            ps_inproj_split(P, split_slot(layer_param(kCriticTrunk, 1, INW)), P + kOffs.o[layer_param(kCriticTrunk, 1, INB)],
-                            io.L[2].qkv, s == S - 1 ? 0 : D / 16, s, b0, reinterpret_cast<const _Float16*>(sm.h));
+            ps_inproj_split(wp, P, s1, io.L[2].qkv, tile0, s, b0, reinterpret_cast<const _Float16*>(sm.h));
             return;
         }
-        const HPre<2> po = hprefetch<2>(P, split_slot(layer_param(kActorTrunk, 0, OUTW)), D, 16 * wv, 0);
-        layer_tail_split<kActorTrunk, 0, true, true>(sm, P, po, io.L[0], b0);
+        auto hook = [&] {  // the head's weights before LN2
+            if (wv < 4) ph = prefetch<4>(P + kOffs.o[kActorHead], D, 16 * wv, 0);
+        };
+        layer_tail_split<kActorTrunk, 0, true, true, decltype(hook)>(sm, P, po, io.L[0], b0, hook);
     } else {
         if (critic) {
             const APre<4> po = prefetch<4>(P + kOffs.o[layer_param(kCriticTrunk, 0, OUTW)], D, 16 * wv, 0);
@@ -3188,9 +3272,8 @@ __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, con
         }
         const APre<4> po = prefetch<4>(P + kOffs.o[layer_param(kActorTrunk, 0, OUTW)], D, 16 * wv, 0);
         layer_tail<kActorTrunk, 0, true, true>(sm, P, po, io.L[0], b0);
+        if (wv < 4) ph = prefetch<4>(P + kOffs.o[kActorHead], D, 16 * wv, 0);
     }
-    APre<4> ph;
-    if (wv < 4) ph = prefetch<4>(P + kOffs.o[kActorHead], D, 16 * wv, 0);
     __syncthreads();
     head_mlp<kActorHead, 2>(sm, P, ph, sm.logits);
     store_hidden(sm, io.z[0], b0);
@@ -3204,18 +3287,23 @@ __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, con
 __global__ __launch_bounds__(NTHR) void k_ps_f3(const float* __restrict__ P, const TrainIO io) {
     __shared__ __attribute__((aligned(16))) Smem sm;
     const int b0 = blockIdx.x * SPW, wv = tid_x() >> 6;
+    // the out-projection's first weight blocks ahead of the attention (as k_ps_f2)
+    [[maybe_unused]] HPre<2> po;
+    if constexpr (kPsSplit) po = hprefetch<2>(P, split_slot(layer_param(kCriticTrunk, 1, OUTW)), D, 16 * wv, 0);
     ps_mask(sm, io.mask, b0);
     ps_rows_in(sm.h, LDH, io.L[1].h2, D, 0, D, S - 1, b0);  // layer 1's input (residual) at position 4
     ps_attention<kPsSplit>(sm, io.L[2].qkv, S - 1, b0);
+    APre<4> ph;
     if constexpr (kPsSplit) {  // the residual is in sm.h (ps_rows_in): PSX = 2
-        const HPre<2> po = hprefetch<2>(P, split_slot(layer_param(kCriticTrunk, 1, OUTW)), D, 16 * wv, 0);
-        layer_tail_split<kCriticTrunk, 1, true, true, NoHook, 2>(sm, P, po, io.L[2], b0);
+        auto hook = [&] {  // the head's weights before LN2
+            if (wv < 4) ph = prefetch<4>(P + kOffs.o[kCriticHead], D, 16 * wv, 0);
+        };
+        layer_tail_split<kCriticTrunk, 1, true, true, decltype(hook), 2>(sm, P, po, io.L[2], b0, hook);
     } else {
         const APre<4> po = prefetch<4>(P + kOffs.o[layer_param(kCriticTrunk, 1, OUTW)], D, 16 * wv, 0);
         layer_tail<kCriticTrunk, 1, true, true>(sm, P, po, io.L[2], b0);
+        if (wv < 4) ph = prefetch<4>(P + kOffs.o[kCriticHead], D, 16 * wv, 0);
     }
-    APre<4> ph;
-    if (wv < 4) ph = prefetch<4>(P + kOffs.o[kCriticHead], D, 16 * wv, 0);
     __syncthreads();
     head_mlp<kCriticHead, 1>(sm, P, ph, sm.value);
     store_hidden(sm, io.z[1], b0);
@@ -3277,8 +3365,22 @@ __device__ __forceinline__ void ps_dqkv_in(Smem& sm, const float* __restrict__ d
     }
 }
 // dL/d(layer input) of position s = W_in^T [dq | dk | dv] (sm.big, ps_dqkv_in) + the residual rows
-// res + p * res_ld (nullptr: none) -> sm.h rows 16 s + p
-__device__ void ps_dx(Smem& sm, const float* __restrict__ WinT, bool with_q, const float* __restrict__ res, int res_ld,
+// res + p * res_ld (nullptr: none) -> sm.h rows 16 s + p. The split GEMM's weights (all three parts,
+// every k block: ps_dx_load) are issued by the caller before the [dq | dk | dv] rows are read in, so
+// their L2 round trip overlaps that one (one exposed round trip instead of one per part).
+struct PsDxPre {
+    HPre<4> w[3];
+    f32x4 res;  // this lane's residual float4 (zero without a residual)
+};
+__device__ __forceinline__ void ps_dx_load(PsDxPre& r, const float* __restrict__ WinT, const float* __restrict__ res,
+                                           int res_ld) {
+    const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
+#pragma unroll
+    for (int part = 0; part < 3; ++part) r.w[part] = hprefetch<4>(WinT, kTSplit, 3 * D, 16 * wv, part * D);
+    // unconditional (WinT's first float4 stands in when there is no residual; ps_dx then ignores it)
+    r.res = ld4(res ? res + (size_t)i16 * res_ld + 16 * wv + 4 * g : WinT);
+}
+__device__ void ps_dx(Smem& sm, const PsDxPre& pw, const float* __restrict__ WinT, bool with_q, bool has_res,
                       int s) {
     const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
     const int fo = 16 * wv + 4 * g;
@@ -3291,8 +3393,8 @@ __device__ void ps_dx(Smem& sm, const float* __restrict__ WinT, bool with_q, con
 #pragma unroll
         for (int part = 0; part < 3; ++part) {
             if (part == 0 && !with_q) continue;
-            hgemm_tile<1, 2, 4, 2 * LDQ, 3 * D>(acc, lo, hprefetch<2>(WinT, kTSplit, 3 * D, 16 * wv, part * D), WinT,
-                                                kTSplit, 3 * D, 16 * wv, part * D, bp + part * D, 0);
+            hgemm_tile<1, 4, 4, 2 * LDQ, 3 * D>(acc, lo, pw.w[part], WinT, kTSplit, 3 * D, 16 * wv, part * D,
+                                                bp + part * D, 0);
         }
         acc[0] += lo[0] * kLoScale;
     } else {
@@ -3304,22 +3406,36 @@ __device__ void ps_dx(Smem& sm, const float* __restrict__ WinT, bool with_q, con
         }
     }
     f32x4 v = acc[0];
-    if (res) v += ld4(res + (size_t)i16 * res_ld + fo);
+    if (has_res) v += pw.res;  // (wave-uniform) the residual ps_dx_load read
     st4(sm.h + (s * SPW + i16) * LDH + fo, v);
 }
 
 // Embedding backward of position s from sm.h rows 16 s + p = dL/d(h0): thread = (feature, token
 // group of 4); the [pos | We | be] partial row of (block, position) -> part (only pos row s nonzero).
-__device__ void ps_embed_bwd(Smem& sm, const float* __restrict__ e, const float* __restrict__ xg,
-                             float* __restrict__ part, int s, int b0) {
+// Its global operands (ps_embed_bwd_load, issued by the caller ahead of the W_in^T GEMM): this
+// thread's embedding values (the ReLU mask) and one float4 of the position's input rows.
+struct PsEmbBwdPre {
+    float ev[SPW / 4];
+    f32x4 xv;
+};
+__device__ __forceinline__ void ps_embed_bwd_load(PsEmbBwdPre& r, const float* __restrict__ e,
+                                                  const float* __restrict__ xg, int s, int b0) {
+    const int f = tid_x() & (D - 1), grp = tid_x() >> 7;
+    const int i = tid_x() < SPW * LDX / 4 ? tid_x() : 0;  // unconditional load (threads >= 64: unused)
+    const int p = i / (LDX / 4), q = i % (LDX / 4);
+    r.xv = ld4(xg + (size_t)trow(s * SPW + p, b0) * 16 + 4 * q);
+#pragma unroll
+    for (int k = 0; k < SPW / 4; ++k) r.ev[k] = e[(size_t)trow(s * SPW + grp + 4 * k, b0) * D + f];
+}
+__device__ void ps_embed_bwd(Smem& sm, const PsEmbBwdPre& r, float* __restrict__ part, int s) {
     const int f = tid_x() & (D - 1), grp = tid_x() >> 7;
     if (tid_x() < SPW * LDX / 4) {
         const int p = tid_x() / (LDX / 4), q = tid_x() % (LDX / 4);
-        st4(sm.x + p * LDX + 4 * q, ld4(xg + (size_t)trow(s * SPW + p, b0) * 16 + 4 * q));
+        st4(sm.x + p * LDX + 4 * q, r.xv);
     }
     float ev[SPW / 4];
 #pragma unroll
-    for (int i = 0; i < SPW / 4; ++i) ev[i] = e[(size_t)trow(s * SPW + grp + 4 * i, b0) * D + f];
+    for (int i = 0; i < SPW / 4; ++i) ev[i] = r.ev[i];
     __syncthreads();
     float acc[IN + 1], accp = 0.f;
 #pragma unroll
@@ -3359,18 +3475,27 @@ __global__ __launch_bounds__(NTHR) void k_ps_b2(const float* __restrict__ P, con
     if (tid_x() >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
     const int blk = blockIdx.x / 10, r = blockIdx.x % 10, s = r % S, b0 = blk * SPW, prow = blk * S + s;
     const bool critic = r >= S, q4 = s == S - 1;
-    ps_mask(sm, io.mask, b0);
     // dL/d(input of the trunk's top, pruned layer) at position s; its residual path (LN1's input
     // gradient, compact [b] rows) exists at the query position 4 only
     const BwdLayerIO& top = io.L[critic ? 2 : 0];
+    const float* WinT = PT + (critic ? 2 : 0) * kLayerT + kTWin;
+    ps_mask(sm, io.mask, b0);
     ps_dqkv_in(sm, top.dqkv, q4, s, b0);
     __syncthreads();
-    ps_dx(sm, PT + (critic ? 2 : 0) * kLayerT + kTWin, q4, q4 ? top.dz1 + (size_t)b0 * D : nullptr, D, s);
-    __syncthreads();
-    if (!critic) {
-        ps_embed_bwd(sm, io.e[0], io.xg, io.epart + (size_t)prow * 2 * kEmbPart, s, b0);
+    // (the GEMM's operands loaded here, not ahead of the dq | dk | dv rows: ahead measured 0.2-0.3 us
+    // slower in this kernel, r04x)
+    PsDxPre pw;
+    ps_dx_load(pw, WinT, q4 ? top.dz1 + (size_t)b0 * D : nullptr, D);
+    if (!critic) {  // the actor: the embedding backward's operands ahead of the GEMM
+        PsEmbBwdPre eb;
+        ps_embed_bwd_load(eb, io.e[0], io.xg, s, b0);
+        ps_dx(sm, pw, WinT, q4, q4, s);
+        __syncthreads();
+        ps_embed_bwd(sm, eb, io.epart + (size_t)prow * 2 * kEmbPart, s);
         return;
     }
+    ps_dx(sm, pw, WinT, q4, q4, s);
+    __syncthreads();
     bwd_layer<kCriticTrunk, 0, false, 20, NoHook, kBwdPos, kPsSplit>(sm, P, PT + kLayerT, io.L[1], b0, nullptr, nullptr, nullptr,
                                                               nullptr, NoHook{}, s * SPW, prow, kvc);
 }
@@ -3382,6 +3507,13 @@ __global__ __launch_bounds__(NTHR) void k_ps_b3(const float* __restrict__ PT, co
     // [dq | dk | dv] rows of position j: dq from B2 (position j), dk / dv = the five query
     // positions' shares summed in position order (deterministic); dk / dv -> the dqkv rows
     float* dqkv = io.L[1].dqkv;
+    // + LN1's input gradient of layer 0 at position j (the residual path); the GEMM's weights, the
+    // residual rows and the embedding backward's operands are loaded ahead of the [dq | dk | dv] rows
+    const float* WinT = PT + kLayerT + kTWin;
+    PsDxPre pw;
+    ps_dx_load(pw, WinT, io.L[1].dz1 + (size_t)trow(j * SPW, b0) * D, S * D);
+    PsEmbBwdPre eb;
+    ps_embed_bwd_load(eb, io.e[1], io.xg, j, b0);
     for (int i = tid_x(); i < SPW * 96; i += NTHR) {
         const int p = i / 96, q = i - 96 * p, tok = j * SPW + p;
         const size_t row = (size_t)trow(tok, b0);
@@ -3397,10 +3529,9 @@ __global__ __launch_bounds__(NTHR) void k_ps_b3(const float* __restrict__ PT, co
         ps_big_store(sm, p, q, v);
     }
     __syncthreads();
-    // + LN1's input gradient of layer 0 at position j (the residual path)
-    ps_dx(sm, PT + kLayerT + kTWin, true, io.L[1].dz1 + (size_t)trow(j * SPW, b0) * D, S * D, j);
+    ps_dx(sm, pw, WinT, true, true, j);
     __syncthreads();
-    ps_embed_bwd(sm, io.e[1], io.xg, io.epart + ((size_t)prow * 2 + 1) * kEmbPart, j, b0);
+    ps_embed_bwd(sm, eb, io.epart + ((size_t)prow * 2 + 1) * kEmbPart, j);
 }
 
 
@@ -3669,7 +3800,8 @@ extern "C" int uavhip_policy_forward_rows(const uavhip_policy* policy, const flo
     const int grid = (B + pol::SPW - 1) / pol::SPW;
     const pol::RowIO rio{rowproj, (int)B, (int)step};
     if (fill) {
-        hipLaunchKernelGGL(pol::k_policy_rows_fill, dim3(grid + 1), dim3(pol::NTHR), 0, (hipStream_t)stream,
+        hipLaunchKernelGGL(pol::k_policy_rows_fill, dim3(grid > pol::kPposParts ? grid : pol::kPposParts), dim3(pol::NTHR), 0,
+                           (hipStream_t)stream,
                            policy->weights, states, rio);
         if (const int rc = check_launch("k_policy_rows_fill")) return rc;
     }
@@ -3700,7 +3832,8 @@ extern "C" int uavhip_rollout_step(const uavhip_policy* policy, const uavhip_env
     const int grid = (B + pol::SPW - 1) / pol::SPW;
     const pol::RowIO rio{rowproj, (int)B, (int)step};
     if (fill) {
-        hipLaunchKernelGGL(pol::k_policy_rows_fill, dim3(grid + 1), dim3(pol::NTHR), 0, (hipStream_t)stream,
+        hipLaunchKernelGGL(pol::k_policy_rows_fill, dim3(grid > pol::kPposParts ? grid : pol::kPposParts), dim3(pol::NTHR), 0,
+                           (hipStream_t)stream,
                            policy->weights, states, rio);
         if (const int rc = check_launch("k_policy_rows_fill")) return rc;
     }
@@ -3732,7 +3865,8 @@ extern "C" int uavhip_rollout_steps(const uavhip_policy* policy, const uavhip_en
     const int grid = (B + pol::SPW - 1) / pol::SPW;
     const pol::RowIO rio{rowproj, (int)B, (int)step};
     if (fill) {
-        hipLaunchKernelGGL(pol::k_policy_rows_fill, dim3(grid + 1), dim3(pol::NTHR), 0, (hipStream_t)stream,
+        hipLaunchKernelGGL(pol::k_policy_rows_fill, dim3(grid > pol::kPposParts ? grid : pol::kPposParts), dim3(pol::NTHR), 0,
+                           (hipStream_t)stream,
                            policy->weights, obs, rio);
         if (const int rc = check_launch("k_policy_rows_fill")) return rc;
     }
