@@ -306,6 +306,13 @@ int uavhip_policy_forward_rows(const uavhip_policy* policy, const float* states,
                                const uint64_t* offset_dev, int8_t* action_out, float* logp, float* value,
                                float* entropy, float* logits, uavhip_stream_t stream);
 
+/* The value head alone on the window-row ring (the rollout's bootstrap V(s_T) after the last step,
+ * ppo.py:70-94's next value): uavhip_policy_forward_rows' value output, bitwise, from the critic
+ * trunk and head only (no actor trunk, no sampling: about 2/3 of the forward). The actor's ring row
+ * of this step is not written, so the next call on the sequence must pass fill != 0. */
+int uavhip_policy_value_rows(const uavhip_policy* policy, const float* states, int32_t B, float* rowproj,
+                             int32_t step, int32_t fill, float* value, uavhip_stream_t stream);
+
 /* One rollout step in ONE launch (main_train.py:109-117: select_action, then env.step): the
  * window-row forward of uavhip_policy_forward_rows with sampling, followed in the same
  * workgroups by the env step (uavhip_env_step, T = 1) of env e with the action sampled for

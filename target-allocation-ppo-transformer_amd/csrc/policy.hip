@@ -1679,7 +1679,10 @@ struct EnvOut {
 // one-launch rollout instantiates one path per launch (71 -> 58.5 KB of code, 28 -> 9 VGPR spills).
 enum { kEnvGrp = 1, kEnvWave = 2, kEnvBoth = 3 };
 // One workgroup's whole forward (+ env step) of its 16 samples; the kernels below wrap it.
-template <bool TR, bool ROWS, int ENV>
+// VONLY (inference, ROWS): the critic trunk and head only -- the value of each window, nothing
+// else (the rollout's bootstrap V(s_T), uavhip_policy_value_rows); the actor's ring row of the step
+// is not written.
+template <bool TR, bool ROWS, int ENV, bool VONLY = false>
 __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __restrict__ P, const float* __restrict__ states,
                                              int B, const int8_t* __restrict__ actions_in, uint64_t seed,
                                              uint64_t offset, const uint64_t* __restrict__ offset_dev,
@@ -1689,9 +1692,10 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
                                              const uavhip_env& env, const EnvOut& eo, int bx) {
     static_assert(!(TR && ROWS), "the training forward recomputes every row");
     static_assert(!ENV || ROWS, "the fused env step follows the rollout forward");
+    static_assert(!VONLY || (ROWS && !ENV && !TR), "value only: the inference ring forward");
     // training trunk split (TrainIO::split): role 1 = actor trunk + head, 2 = critic trunk + head
     // of sample block blk; role 0 = both (the rollout always)
-    int blk = bx, role = 0;
+    int blk = bx, role = VONLY ? 2 : 0;
     if constexpr (TR) {
         if (io.split) {
             role = blk < io.split ? 1 : 2;
@@ -1728,12 +1732,14 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     const float* headw_c = P + kOffs.o[kCriticHead];
     // actor trunk (1 layer) + head
     if constexpr (ROWS) {
-        RingPre<kActorTrunk> pw[3];
-        RowPre<2> rp;
-        rows_prologue<kActorTrunk>(TID_C sm, P, pw, rp, rio, b0);
-        PTR(2);
-        __syncthreads();
-        encoder_layer_rows<kActorTrunk>(TID_C sm, P, pw, rp, rio, b0);
+        if (do_actor) {
+            RingPre<kActorTrunk> pw[3];
+            RowPre<2> rp;
+            rows_prologue<kActorTrunk>(TID_C sm, P, pw, rp, rio, b0);
+            PTR(2);
+            __syncthreads();
+            encoder_layer_rows<kActorTrunk>(TID_C sm, P, pw, rp, rio, b0);
+        }
     }
     // training mode: the actor head's and the critic embedding's / first GEMM's operands are loaded
     // ahead of the actor's LN2 activation stores (layer_tail hook)
@@ -1854,6 +1860,10 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
         }
         return;
     }
+    if constexpr (VONLY) {  // the value alone
+        if (TIDX() < SPW && b0 + (int)TIDX() < B) value_out[b0 + TIDX()] = sm.value[TIDX()];
+        return;
+    }
     // Categorical(softmax(logits)): sample / log_prob / entropy (transformer_net.py:118-122)
     if (TIDX() < SPW) {
         const int p = TIDX(), b = b0 + p;
@@ -1933,7 +1943,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     }
 }
 
-template <bool TR, bool ROWS = false, int ENV = 0>
+template <bool TR, bool ROWS = false, int ENV = 0, bool VONLY = false>
 __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict__ P, const float* __restrict__ states,
                                                          int B, const int8_t* __restrict__ actions_in, uint64_t seed,
                                                          uint64_t offset, const uint64_t* __restrict__ offset_dev,
@@ -1945,8 +1955,8 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     __shared__ __attribute__((aligned(16))) Smem sm;
     // the younger half (waves 4-7, the arbitration loser of every phase) at priority 1
     if (tid_x() >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
-    policy_block<TR, ROWS, ENV>(TID_K sm, P, states, B, actions_in, seed, offset, offset_dev, action_out, logp_out, value_out,
-                                ent_out, logits_out, io, rio, env, eo, blockIdx.x);
+    policy_block<TR, ROWS, ENV, VONLY>(TID_K sm, P, states, B, actions_in, seed, offset, offset_dev, action_out, logp_out,
+                                       value_out, ent_out, logits_out, io, rio, env, eo, blockIdx.x);
 }
 
 // Multi-step fused rollout (uavhip_rollout_steps). A workgroup's 16 envs and their windows, ring
@@ -2502,6 +2512,10 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
     ln_bwd_load(lnp, io.xhat1, io.rstd1, P + kOffs.o[layer_param(trunk, layer, N1W)], qtok0, b0, last, qtok1);
     AttnPre ap;
     attn_bwd_load<last>(ap, io.qkv, 0, b0, qsel);
+    // the position-split modes have no W_in^T GEMM to hide chunk 1's Q / K / V rows behind: both
+    // chunks' rows are loaded here (K6 loads chunk 1's behind chunk 0's weight loads, below)
+    [[maybe_unused]] AttnPre ap1;
+    if constexpr (MODE != kBwdFull) attn_bwd_load<last>(ap1, io.qkv, 1, b0, qsel);
     BTR(TB + 5);
     __syncthreads();
     BTR(TB + 6);
@@ -2531,7 +2545,8 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
     for (int c = 0; c < 2; ++c) {
         [[maybe_unused]] HPre<2> pw;
         if constexpr (MODE == kBwdFull) pw = hprefetch<2>(PT, sWin, 3 * D, 16 * wv, 64 * c);
-        attn_bwd_chunk<last, true>(sm, ap, c, sm.scr, qsel, io.dqkv, b0, MODE == kBwdPos ? kvc : nullptr, blk);
+        attn_bwd_chunk<last, true>(sm, MODE != kBwdFull && c == 1 ? ap1 : ap, c, sm.scr, qsel, io.dqkv, b0,
+                                   MODE == kBwdPos ? kvc : nullptr, blk);
         __syncthreads();
         BTR(TB + 11 + 2 * c);
         if (tid_x() < 3 * 64) {  // in_proj bias partial of the chunk: the 8 wave rows of sm.scr
@@ -2542,7 +2557,6 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
             bias[kBiasIn + (i >> 6) * D + 64 * c + (i & 63)] = v;
         }
         if constexpr (MODE != kBwdFull) {  // the per-position kernels form dL/d(layer input)
-            if (c == 0) attn_bwd_load<last>(ap, io.qkv, 1, b0, qsel);
             if (c == 0) __syncthreads();  // sm.scr is rewritten by chunk 1
             continue;
         }
@@ -3809,6 +3823,29 @@ extern "C" int uavhip_policy_forward_rows(const uavhip_policy* policy, const flo
                        policy->weights, states, (int)B, actions_in, seed, offset, offset_dev, action_out, logp, value,
                        entropy, logits, pol::TrainIO{}, rio, uavhip_env{}, pol::EnvOut{});
     return check_launch("k_policy_forward_rows");
+}
+
+// Value-only ring forward (the rollout's bootstrap V(s_T)): the critic trunk and head of
+// uavhip_policy_forward_rows, bitwise its value output; the actor's ring row is not written.
+extern "C" int uavhip_policy_value_rows(const uavhip_policy* policy, const float* states, int32_t B, float* rowproj,
+                                        int32_t step, int32_t fill, float* value, uavhip_stream_t stream) {
+    if (const int rc = check_policy("uavhip_policy_value_rows", policy, states, B)) return rc;
+    if (!rowproj || !value || step < 0 || (int64_t)B * pol::S * pol::kRowFloats >= (int64_t)1 << 31) {
+        set_error("uavhip_policy_value_rows: NULL rowproj / value, step=%d < 0 or B=%d above the ring's 32-bit offsets",
+                  step, B);
+        return UAVHIP_EINVAL;
+    }
+    const int grid = (B + pol::SPW - 1) / pol::SPW;
+    const pol::RowIO rio{rowproj, (int)B, (int)step};
+    if (fill) {
+        hipLaunchKernelGGL(pol::k_policy_rows_fill, dim3(grid > pol::kPposParts ? grid : pol::kPposParts), dim3(pol::NTHR), 0,
+                           (hipStream_t)stream, policy->weights, states, rio);
+        if (const int rc = check_launch("k_policy_rows_fill")) return rc;
+    }
+    hipLaunchKernelGGL((pol::k_policy_forward<false, true, 0, true>), dim3(grid), dim3(pol::NTHR), 0, (hipStream_t)stream,
+                       policy->weights, states, (int)B, nullptr, 0ull, 0ull, nullptr, nullptr, nullptr, value, nullptr,
+                       nullptr, pol::TrainIO{}, rio, uavhip_env{}, pol::EnvOut{});
+    return check_launch("k_policy_value_rows");
 }
 
 // Fused rollout step: uavhip_policy_forward_rows (sampling) + uavhip_env_step (T = 1) of env e

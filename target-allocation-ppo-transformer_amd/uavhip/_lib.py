@@ -95,6 +95,7 @@ _SIGS = {
     "uavhip_policy_forward_rows": (ctypes.c_int, [ctypes.POINTER(PolicyDesc), _vp, _i32, _vp, _i32, _i32, _vp,
                                                   ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp,
                                                   _vp]),
+    "uavhip_policy_value_rows": (ctypes.c_int, [ctypes.POINTER(PolicyDesc), _vp, _i32, _vp, _i32, _i32, _vp, _vp]),
     "uavhip_rollout_step": (ctypes.c_int, [ctypes.POINTER(PolicyDesc), ctypes.POINTER(EnvDesc), _vp, _vp, _i32,
                                            _i32, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp, _vp, _i32, _vp,
                                            _vp, _vp, _vp, _vp]),

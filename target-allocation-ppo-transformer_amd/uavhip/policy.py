@@ -187,6 +187,23 @@ class TransformerActorCritic(nn.Module):
                                         ptr(entropy), ptr(logits), stream_handle()), "uavhip_policy_forward")
         return action_out, logp, value, entropy, logits
 
+    def value_rows(self, states, rowproj, step, value, fill=False):
+        """uavhip_policy_value_rows: the critic's value of [B, 5, 14] fp32 device windows on the
+        window-sequence ring (the rollout's bootstrap V(s_T)) -- fused_forward(rowproj=...)'s value,
+        bitwise, without the actor trunk and sampling. The actor's ring row of this step is not
+        written, so the next call on the sequence must fill (RolloutEngine refills every iteration).
+        The weights must be packed (packed_weights())."""
+        if self._packed is None:
+            self.packed_weights()
+        B = states.shape[0]
+        check_out(states, "states", torch.float32, (B,), states.device, (cfg.SEQ_LEN, cfg.STATE_DIM))
+        check_out(value, "value", torch.float32, (B,), states.device)
+        if rowproj.numel() < LIB.uavhip_policy_rowproj_floats(B) or rowproj.dtype != torch.float32:
+            raise ValueError("rowproj: need a float32 buffer of rowproj_buffer(B) elements")
+        check(LIB.uavhip_policy_value_rows(self._desc, ptr(states), B, ptr(rowproj), int(step), int(bool(fill)),
+                                           ptr(value), stream_handle()), "uavhip_policy_value_rows")
+        return value
+
     def rollout_step(self, env, states, rowproj, step, fill, action_out, logp, value, obs_out, reward_out, done_out,
                      info_out=None, auto_reset=True, seed=None, offset=0, offset_dev=None):
         """uavhip_rollout_step: the window-row forward + sampling over env's E windows `states`

@@ -15,11 +15,17 @@ step after T-1 is bootstrapped with V(s_T) (the reference only ever updates on c
 main_train.py:140-146, and uses next_value 0 at the buffer end). Pass bootstrap=False for the
 reference's rule.
 """
+import os
+
 import torch
 
 from . import _lib
 from .policy import rowproj_buffer
 from .ppo import gae, gae_workspace
+
+# UAVHIP_BOOTSTRAP_FULL=1: the bootstrap V(s_T) through the full forward (actor + sampling + critic)
+# instead of the critic-only launch -- the same values, bitwise (A/B switch of scripts/gpu_r04z.sh)
+_BOOTSTRAP_FULL = os.environ.get("UAVHIP_BOOTSTRAP_FULL", "0") == "1"
 
 
 class Trajectory:
@@ -35,9 +41,7 @@ class Trajectory:
         self.rewards = torch.zeros(T, E, dtype=torch.float64, device=device)
         self.dones = torch.zeros(T, E, dtype=torch.uint8, device=device)
         self.info = torch.zeros(T, E, _lib.INFO_COUNT, dtype=torch.float64, device=device) if want_info else None
-        self.last_values = torch.zeros(E, **f32)
-        self.last_actions = torch.zeros(E, dtype=torch.int8, device=device)
-        self.last_logp = torch.zeros(E, **f32)
+        self.last_values = torch.zeros(E, **f32)  # V(s_T), the bootstrap
         self.ret, self.adv, self.partials, self.stats = gae_workspace(T, E, device)
 
 
@@ -151,7 +155,17 @@ class RolloutEngine:
                 eev[t][1].record()
         last = None
         if self.bootstrap:
-            self._forward(self.T, tr.obs[self.T], tr.last_actions, tr.last_logp, tr.last_values)
+            if self.rowproj is not None and not _BOOTSTRAP_FULL:
+                # the critic alone (uavhip_policy_value_rows): nothing reads an action at step T; the
+                # actor ring row it skips is rebuilt by the next iteration's fill (step 0, fill=True)
+                ev = self.policy_events
+                if ev is not None:
+                    ev[self.T][0].record()
+                self.policy.value_rows(tr.obs[self.T], self.rowproj, self.T, tr.last_values)
+                if ev is not None:
+                    ev[self.T][1].record()
+            else:
+                self._forward(self.T, tr.obs[self.T], None, None, tr.last_values)
             last = tr.last_values
         gae(tr.rewards, tr.dones, tr.values, last_values=last, normalize=self.normalize,
             out=(tr.ret, tr.adv, tr.partials, tr.stats))

@@ -81,7 +81,7 @@ def test_rollout_steps_code_object(tmp_path):
 def test_policy_kernels_code_objects(tmp_path):
     ks = kernels(compile_asm("policy.hip", tmp_path))
     wanted = {"k_policy_backward": 0, "k_policy_forwardILb1ELb0ELi0E": 0, "k_policy_forwardILb0ELb1ELi3E": 0,
-              "k_policy_forwardILb0ELb0ELi0E": 0}
+              "k_policy_forwardILb0ELb0ELi0E": 0, "k_policy_forwardILb0ELb1ELi0ELb1E": 0}
     for frag in wanted:
         names = [k for k in ks if frag in k]
         assert names, frag

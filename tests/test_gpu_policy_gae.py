@@ -82,6 +82,38 @@ def test_row_projection_sequence(B, step0):
             torch.testing.assert_close(x, y, rtol=1e-5, atol=2e-6)
 
 
+@pytest.mark.parametrize("B", [200, 4096])
+def test_value_rows_matches_forward_rows(B):
+    """uavhip_policy_value_rows (the rollout's bootstrap: critic trunk + head only) against the full
+    ring forward's value, bitwise, along a window sequence whose steps advance the ring through the
+    full forward -- with fill, and on the ring the previous steps left (fill = 0)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle.windows import windows_from_rows
+    from uavhip.policy import TransformerActorCritic, rowproj_buffer
+    torch.manual_seed(3)
+    net = TransformerActorCritic().cuda()
+    T = 6
+    g = np.random.default_rng(B + 1)
+    first = g.standard_normal((B, 5, 14)).astype(np.float32)
+    first[: B // 4, :2] = 0
+    rows = g.standard_normal((T, B, 14)).astype(np.float32)
+    dones = g.random((T, B)) < 0.2
+    wins = torch.from_numpy(windows_from_rows(first, rows, dones)).cuda()
+    ring, fresh = rowproj_buffer(B), rowproj_buffer(B)
+    for t in range(T):
+        before = ring.clone()  # the ring the full forward of steps 0 .. t-1 left
+        _, _, v, _, _ = net.fused_forward(wins[t], rowproj=ring, step=t, fill=t == 0)
+        v_fill = net.value_rows(wins[t], fresh, t, torch.empty(B, device="cuda"), fill=True)
+        torch.cuda.synchronize()
+        assert torch.equal(v, v_fill), f"step {t}: value_rows(fill) != forward_rows value"
+        if t > 0:
+            v_ring = net.value_rows(wins[t], before, t, torch.empty(B, device="cuda"))
+            torch.cuda.synchronize()
+            assert torch.equal(v, v_ring), f"step {t}: value_rows(ring) != forward_rows value"
+
+
 @pytest.mark.parametrize("tag", ["a", "b"])
 def test_fused_policy_vs_reference(policy_npz, tag):
     net = _load_policy(policy_npz, tag)
