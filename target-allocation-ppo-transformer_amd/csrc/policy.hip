@@ -2514,8 +2514,6 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
     attn_bwd_load<last>(ap, io.qkv, 0, b0, qsel);
     // the position-split modes have no W_in^T GEMM to hide chunk 1's Q / K / V rows behind: both
     // chunks' rows are loaded here (K6 loads chunk 1's behind chunk 0's weight loads, below)
-    [[maybe_unused]] AttnPre ap1;
-    if constexpr (MODE != kBwdFull) attn_bwd_load<last>(ap1, io.qkv, 1, b0, qsel);
     BTR(TB + 5);
     __syncthreads();
     BTR(TB + 6);
@@ -2545,8 +2543,7 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
     for (int c = 0; c < 2; ++c) {
         [[maybe_unused]] HPre<2> pw;
         if constexpr (MODE == kBwdFull) pw = hprefetch<2>(PT, sWin, 3 * D, 16 * wv, 64 * c);
-        attn_bwd_chunk<last, true>(sm, MODE != kBwdFull && c == 1 ? ap1 : ap, c, sm.scr, qsel, io.dqkv, b0,
-                                   MODE == kBwdPos ? kvc : nullptr, blk);
+        attn_bwd_chunk<last, true>(sm, ap, c, sm.scr, qsel, io.dqkv, b0, MODE == kBwdPos ? kvc : nullptr, blk);
         __syncthreads();
         BTR(TB + 11 + 2 * c);
         if (tid_x() < 3 * 64) {  // in_proj bias partial of the chunk: the 8 wave rows of sm.scr
@@ -2557,6 +2554,7 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
             bias[kBiasIn + (i >> 6) * D + 64 * c + (i & 63)] = v;
         }
         if constexpr (MODE != kBwdFull) {  // the per-position kernels form dL/d(layer input)
+            if (c == 0) attn_bwd_load<last>(ap, io.qkv, 1, b0, qsel);
             if (c == 0) __syncthreads();  // sm.scr is rewritten by chunk 1
             continue;
         }
