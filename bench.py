@@ -858,6 +858,10 @@ def main():
                                "same payloads: the multi-GPU throughput is not valid")
         print(json.dumps(line), flush=True)
     if dist is not None:
+        if xchg is not None:  # unmap the peers' send buffers before any rank (an exporter) exits
+            torch.cuda.synchronize()
+            dist.barrier()
+            xchg.close()
         dist.barrier()
         dist.destroy_process_group()
     if exchange is not None and exchange.get("check") is False:

@@ -432,8 +432,13 @@ int uavhip_episode_stats(const double* reward, const uint8_t* done, const int8_t
  * The all-gather of trajectories before the update (the reference has no multi-GPU
  * path, main_train.py:109-146 runs one process) as peer-to-peer copies beside the next rollout
  * (uavhip.dist.IpcAllGather). Host-side helpers over the HIP runtime:
- *   uavhip_peer_access  : can the current device read peer_device's memory? enables peer access
- *                         (an already enabled one is fine); *can_access = 1 for the same device
+ *   uavhip_device_pci_id: the PCI bus id of a device of this process (>= 13 bytes): the identity
+ *                         the ranks exchange, since ordinals are local to a process
+ *   uavhip_device_from_pci_id: this process's ordinal of the device with that bus id (-1: not
+ *                         visible here)
+ *   uavhip_peer_access  : can the current device read peer_device's memory (an ordinal of THIS
+ *                         process)? enables peer access (an already enabled one is fine);
+ *                         *can_access = 1 for the same device
  *   uavhip_ipc_export   : IPC handle (UAVHIP_IPC_HANDLE_BYTES) of the allocation holding ptr, and
  *                         ptr's offset inside it
  *   uavhip_ipc_open     : map a peer's exported allocation into the CURRENT device's address space
@@ -441,6 +446,8 @@ int uavhip_episode_stats(const double* reward, const uint8_t* done, const int8_t
  *   uavhip_ipc_close    : unmap (the base returned by open minus its offset)
  *   uavhip_copy_async   : device-to-device copy on `stream` (a mapped peer buffer as the source) */
 #define UAVHIP_IPC_HANDLE_BYTES 64
+int uavhip_device_pci_id(int32_t device, char* buf, int32_t len);
+int uavhip_device_from_pci_id(const char* pci_id, int32_t* device);
 int uavhip_peer_access(int32_t peer_device, int32_t* can_access);
 int uavhip_ipc_export(const void* ptr, void* handle, uint64_t* offset);
 int uavhip_ipc_open(const void* handle, uint64_t offset, void** ptr);

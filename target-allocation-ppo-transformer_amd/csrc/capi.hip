@@ -33,6 +33,37 @@ extern "C" int32_t uavhip_abi_version(void) { return 4; }
 // as IPC handles, every other rank opens them into ITS OWN device's address space (no context on the
 // exporter's device) after checking and enabling peer access, and copies out of them on a stream of
 // its own device.
+// A device's identity across processes: its PCI bus id. Device ordinals are local to a process (a
+// rank started with its own HIP_VISIBLE_DEVICES sees its GPU as device 0), so the ranks compare bus
+// ids to find a shared device and map a peer's bus id back to THIS process's ordinal before asking
+// for peer access (-1: the peer's device is not visible here, so no peer access can be checked).
+extern "C" int uavhip_device_pci_id(int32_t device, char* buf, int32_t len) {
+    if (!buf || len < 13) {
+        uavhip::set_error("uavhip_device_pci_id: buffer of at least 13 bytes required");
+        return UAVHIP_EINVAL;
+    }
+    const hipError_t e = hipDeviceGetPCIBusId(buf, len, device);
+    if (e != hipSuccess) {
+        uavhip::set_error("uavhip_device_pci_id(%d): %s", device, hipGetErrorString(e));
+        return UAVHIP_EHIP;
+    }
+    return UAVHIP_OK;
+}
+
+extern "C" int uavhip_device_from_pci_id(const char* pci_id, int32_t* device) {
+    if (!pci_id || !device) {
+        uavhip::set_error("uavhip_device_from_pci_id: NULL pointer");
+        return UAVHIP_EINVAL;
+    }
+    int d = -1;
+    if (hipDeviceGetByPCIBusId(&d, pci_id) != hipSuccess) {
+        (void)hipGetLastError();
+        d = -1;
+    }
+    *device = d;
+    return UAVHIP_OK;
+}
+
 extern "C" int uavhip_peer_access(int32_t peer_device, int32_t* can_access) {
     int cur = 0, can = 0;
     if (!can_access) {

@@ -1,7 +1,8 @@
 """uavhip -- MI355X-native (gfx950) PPO rollout hot path of the UAV->target allocation reference.
 
     VecUAVEnv          E envs resident in HBM, stepped by HIP kernels (env.hip)
-    TransformerActorCritic  reference-compatible policy; fused fp32-MFMA forward (policy.hip)
+    TransformerActorCritic  reference-compatible policy; fused forward (policy.hip): fp32-accurate split
+                       products on the f16 MFMA, embeddings and heads on the f32 MFMA
     gae                GAE + advantage normalisation on the GPU (gae.hip)
     RolloutEngine      T-step batched rollout (+ RCCL trajectory all-gather)
     PPOAgent           agents/ppo.py API

@@ -105,6 +105,8 @@ _SIGS = {
     "uavhip_ppo_workspace_floats": (ctypes.c_int64, [_i32]),
     "uavhip_ppo_step": (ctypes.c_int, [ctypes.POINTER(PPODesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
     "uavhip_episode_stats": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _i32, _vp, _vp]),
+    "uavhip_device_pci_id": (ctypes.c_int, [_i32, ctypes.c_char_p, _i32]),
+    "uavhip_device_from_pci_id": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_i32)]),
     "uavhip_peer_access": (ctypes.c_int, [_i32, ctypes.POINTER(_i32)]),
     "uavhip_ipc_export": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
     "uavhip_ipc_open": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_vp)]),

@@ -146,6 +146,15 @@ class HipPeerMapper:
     def device_index(self):
         return self.device.index if self.device.index is not None else torch.cuda.current_device()
 
+    def identity(self):
+        """This rank's device as the ranks can compare it: its PCI bus id (ordinals are local to a
+        process -- ranks started with their own HIP_VISIBLE_DEVICES all see device 0)."""
+        import ctypes
+        from ._lib import LIB, check
+        buf = ctypes.create_string_buffer(64)
+        check(LIB.uavhip_device_pci_id(int(self.device_index()), buf, 64), "uavhip_device_pci_id")
+        return buf.value.decode().lower()
+
     def alloc(self, shape):
         return torch.zeros(*shape, dtype=torch.float32, device=self.device)
 
@@ -160,12 +169,21 @@ class HipPeerMapper:
         check(LIB.uavhip_ipc_export(t.data_ptr(), h, ctypes.byref(off)), "uavhip_ipc_export")
         return bytes(h), int(off.value)
 
-    def can_access(self, peer_device):
+    def can_access(self, peer):
+        """Peer access from this rank's device to the device a peer published as identity(): the
+        same bus id is the same device; otherwise the bus id is mapped to this process's ordinal
+        (not visible here -> no access) and hipDeviceCanAccessPeer / hipDeviceEnablePeerAccess ask."""
         import ctypes
         from ._lib import LIB, check
+        if peer == self.identity():
+            return True
+        local = ctypes.c_int32(-1)
+        check(LIB.uavhip_device_from_pci_id(str(peer).encode(), ctypes.byref(local)), "uavhip_device_from_pci_id")
+        if local.value < 0:
+            return False
         ok = ctypes.c_int32(0)
         with torch.cuda.device(self.device):
-            check(LIB.uavhip_peer_access(int(peer_device), ctypes.byref(ok)), "uavhip_peer_access")
+            check(LIB.uavhip_peer_access(int(local.value), ctypes.byref(ok)), "uavhip_peer_access")
         return bool(ok.value)
 
     def open(self, handle):
@@ -232,7 +250,7 @@ class IpcAllGather:
             self.send = [self.mapper.alloc((self.floats,)) for _ in range(2)]
             self.recv = [self.mapper.alloc((self.world, self.floats)) for _ in range(2)]
             self.mapper.sync()
-            mine = (self.mapper.device_index(), [self.mapper.export(t) for t in self.send])
+            mine = (self.mapper.identity(), [self.mapper.export(t) for t in self.send])
         except Exception as exc:  # noqa: BLE001 -- reported collectively below
             err = exc
         objs = [None] * self.world

@@ -92,6 +92,7 @@ class FusedPPOTrainer:
         self.desc = d
         self.bufs = None
         self.graphs = {}    # steps per epoch -> captured epoch hipGraph over the current buffers
+        self.capture_failed = {}  # steps per epoch -> why a (voted) capture failed: run() steps eagerly
         self._store = None  # stage(): the trainer's own trajectory buffers
         self._cap = 0
         self.n_local = None  # set_shard(): rows of this rank's shard
@@ -117,6 +118,7 @@ class FusedPPOTrainer:
         self.n = n
         self.perm = torch.zeros(n, dtype=torch.int32, device=dev)  # the epoch's minibatch order
         self.graphs = {}
+        self.capture_failed = {}
         self._store = None
         self.n_local = None
 
@@ -230,31 +232,43 @@ class FusedPPOTrainer:
         steps = min(self.n // self.global_minibatch, self.max_graph_steps)
         if self.dp:  # the communicator is created at its first collective, which must not be in a capture
             self.allreduce(torch.zeros(1, dtype=torch.float32, device=self.device))
-            torch.cuda.synchronize()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
         g, err = None, None
         try:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            g = torch.cuda.CUDAGraph()
-            # thread_local: the process group's watchdog thread keeps polling its events during the capture
-            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local" if self.dp else "global"):
-                for b in range(steps):  # one epoch (or chunk): every minibatch step
-                    if self.dp:
-                        self.ddp_step(self._rows(self.perm, b), self._packed(b))
-                    else:
-                        self.step(_lib.PPO_FULL | self._packed(b), self._rows(self.perm, b))
-            torch.cuda.current_stream().wait_stream(s)
+            g = self._capture_graph(steps)
         except Exception as exc:  # noqa: BLE001 -- data parallel: voted on below, then re-raised / eager
             g, err = None, exc
         if self.dp:
             ok = torch.tensor([0.0 if g is None else 1.0], dtype=torch.float32, device=self.device)
             self.allreduce(ok)
             if int(ok.item()) != self.world:
+                # remembered per step count: later run()s step eagerly without voting again
+                why = repr(err) if err is not None else f"the capture failed on {self.world - int(ok.item())} other rank(s)"
+                self.capture_failed[steps] = why
                 self.graphs.pop(steps, None)
+                import sys
+                print(f"[FusedPPOTrainer rank {self.rank}] epoch graph capture ({steps} steps) failed, "
+                      f"eager steps: {why}", file=sys.stderr)
                 return None
         elif err is not None:
             raise err
         self.graphs[steps] = g
+        return g
+
+    def _capture_graph(self, steps):
+        """The capture itself: `steps` minibatch steps over perm into a new hipGraph."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        # thread_local: the process group's watchdog thread keeps polling its events during the capture
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local" if self.dp else "global"):
+            for b in range(steps):  # one epoch (or chunk): every minibatch step
+                if self.dp:
+                    self.ddp_step(self._rows(self.perm, b), self._packed(b))
+                else:
+                    self.step(_lib.PPO_FULL | self._packed(b), self._rows(self.perm, b))
+        torch.cuda.current_stream().wait_stream(s)
         return g
 
     @property
@@ -279,9 +293,9 @@ class FusedPPOTrainer:
         if self.n_local is not None and self.dp:
             return self._run_shard(epochs, generator, perms, steps)
         graph = self.graph if use_graph else None
-        if use_graph and graph is None and steps > 0:
-            graph = self.capture()
         chunk = min(steps, self.max_graph_steps)
+        if use_graph and graph is None and steps > 0 and chunk not in self.capture_failed:
+            graph = self.capture()
         Bg = self.global_minibatch
         order_dev = None
         if graph is not None and steps > chunk:

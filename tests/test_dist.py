@@ -193,7 +193,7 @@ class _FakeMapper:
         self.dev, self.fail_alloc, self.no_peer = dev, fail_alloc, set(no_peer)
         self.opened, self.closed = [], []
 
-    def device_index(self):
+    def identity(self):
         return self.dev
 
     def alloc(self, shape):
@@ -284,3 +284,71 @@ def test_ipc_exchange_peer_access_decision():
         status, peers, devs, opened = res[r]
         assert status == "ok" and peers == [j for j in range(world) if j != r], res
         assert devs == {j: j for j in range(world)} and opened == 2 * (world - 1)
+
+
+def _capture_vote_worker(rank, world, port, q):
+    import sys
+    import types
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "target-allocation-ppo-transformer_amd"))
+    import torch.distributed as dist
+    from uavhip.train import FusedPPOTrainer
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class _Trainer(FusedPPOTrainer):
+        """The data-parallel capture / run logic without a GPU: the capture fails on rank 1, an
+        eager step only counts."""
+        captures = 0
+        eager = 0
+
+        def _capture_graph(self, steps):
+            self.captures += 1
+            if self.rank == 1:
+                raise RuntimeError("simulated capture failure")
+            return object()
+
+        def _eager_step(self, perm, b):
+            self.eager += 1
+            self.stats[3] += 1
+
+    try:
+        tr = _Trainer.__new__(_Trainer)
+        tr.world, tr.rank, tr.dp, tr.graph_collectives = world, rank, True, True
+        tr.allreduce = lambda t: dist.all_reduce(t)
+        tr.device, tr.global_minibatch, tr.minibatch, tr.n, tr.n_local = torch.device("cpu"), 128, 64, 3 * 128, None
+        tr.graphs, tr.capture_failed = {}, {}
+        tr.perm, tr.stats = torch.zeros(3 * 128, dtype=torch.int32), torch.zeros(4, dtype=torch.float64)
+        tr.policy = types.SimpleNamespace()
+        res = []
+        for _ in range(2):  # the second run must not capture (nor vote) again
+            out = tr.run(epochs=2, generator=torch.Generator().manual_seed(1), use_graph=True)
+            res.append(out[3])
+        q.put((rank, (tr.captures, tr.eager, res, dict(tr.capture_failed), tr.graph is None)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_capture_failure_is_voted_and_remembered():
+    """FusedPPOTrainer.capture on a data-parallel group: a capture that fails on one rank makes every
+    rank drop its graph (the ranks vote with an all-reduce), each rank keeps why (the failing rank its
+    exception, the others the vote) per step count, and later run()s step eagerly without capturing
+    or voting again -- so no rank replays a graph whose collectives the others never join."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_capture_vote_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        captures, eager, counts, failed, no_graph = res[r]
+        assert captures == 1, res            # one capture attempt, then remembered
+        assert eager == 2 * 2 * 3 and counts == [6, 6], res  # 2 runs x 2 epochs x 3 steps, all eager
+        assert no_graph and list(failed) == [3], res
+        assert ("simulated capture failure" if r == 1 else "other rank") in failed[3], res

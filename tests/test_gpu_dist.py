@@ -310,3 +310,24 @@ def test_pipelined_ipc_exchange_matches_all_gather():
         assert set(ref) == set(got)
         for k in ref:
             assert np.array_equal(ref[k], got[k]), (r, k)
+
+
+def test_hip_peer_mapper_identity_is_the_pci_bus_id():
+    """The ranks of the pipelined exchange compare devices by PCI bus id (ordinals are local to a
+    process): HipPeerMapper.identity() is this device's bus id, which maps back to this process's
+    ordinal; its own identity counts as reachable without a peer mapping, and an id no device of
+    this process has is not reachable (no peer access can be checked for it)."""
+    import ctypes
+    from uavhip._lib import LIB, check
+    from uavhip.dist import HipPeerMapper
+    m = HipPeerMapper(torch.device("cuda", 0))
+    ident = m.identity()
+    print("device 0 PCI bus id:", ident)
+    assert ident.count(":") >= 2, ident
+    d = ctypes.c_int32(-5)
+    check(LIB.uavhip_device_from_pci_id(ident.encode(), ctypes.byref(d)), "uavhip_device_from_pci_id")
+    assert d.value == 0
+    assert m.can_access(ident)
+    check(LIB.uavhip_device_from_pci_id(b"0000:ff:1f.7", ctypes.byref(d)), "uavhip_device_from_pci_id")
+    assert d.value == -1
+    assert not m.can_access("0000:ff:1f.7")

@@ -215,6 +215,33 @@ def test_fused_graph_replay_matches_direct_steps():
     torch.testing.assert_close(lp_fused, lp_torch.detach(), rtol=1e-5, atol=2e-6)
 
 
+def test_chunked_epoch_replay_matches_eager_steps():
+    """An epoch longer than max_graph_steps replays one captured chunk graph per chunk (the chunk's
+    rows copied into the front of the permutation buffer first, its step 0 repacking the weights)
+    and steps the ragged rest eagerly (FusedPPOTrainer.run). With max_graph_steps = 4 and 10 steps
+    per epoch (two chunk replays + two eager steps, two epochs) against use_graph=False: bitwise the
+    same loss statistics, parameters and Adam moments."""
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.train import FusedPPOTrainer
+    torch.manual_seed(31)
+    n1 = TransformerActorCritic().cuda()
+    n2 = copy.deepcopy(n1)
+    Bm = 64
+    bufs = _buffers(10 * Bm, seed=32)
+    t1, t2 = FusedPPOTrainer(n1, Bm), FusedPPOTrainer(n2, Bm)
+    t2.max_graph_steps = 4
+    for t in (t1, t2):
+        t.set_buffers(*bufs)
+    s1 = t1.run(epochs=2, generator=torch.Generator().manual_seed(33), use_graph=False)
+    s2 = t2.run(epochs=2, generator=torch.Generator().manual_seed(33), use_graph=True)
+    assert 4 in t2.graphs and s2[3] == 20, (list(t2.graphs), s2)
+    assert s1 == s2, (s1, s2)
+    for name, a, b in (("params", t1.params, t2.params), ("adam_m", t1.adam_m, t2.adam_m),
+                       ("adam_v", t1.adam_v, t2.adam_v), ("adam_step", t1.adam_step, t2.adam_step)):
+        d = int((a != b).sum())
+        assert d == 0, f"{name}: {d} elements differ"
+
+
 @pytest.mark.parametrize("Bm", [64, 4096])
 def test_update_repack_skip_matches_repacking_every_step(Bm):
     """UPDATE refreshes the packed weight copies (k_adam's pack_scatter: the forward's fragment
