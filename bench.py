@@ -33,6 +33,9 @@ Also reported (same JSON line):
                 and gradients)
   ppo_samples_per_s_mb64  the same update at the reference's minibatch 64 (parity mode: the
                 reference's optimizer trajectory) over 16,384 of the iteration's transitions, N = 1
+  dropin_loop   the reference's own loop (main_train.py:79-146) at E = 1 through the drop-in UAVEnv /
+                PPOAgent (30 x 10 and the headline shape): env-steps/s, update() samples/s at minibatch
+                64, host syncs per step; the CPU port of the same loop beside it (oracle/cpu_loop_bench.py)
   cpu_baseline  the CPU port (C oracle env.step + torch-CPU fp32 policy + numpy GAE) on host cores,
                 rank 0 at N = 1 only, bounded sample
   cpu_env_baseline  UAVEnv.step alone (C oracle, reference algorithm) on all host cores (one process
@@ -111,6 +114,22 @@ def profiled_traffic(kernel):
     if len(hits) == 1:
         return hits[0]["hbm_bytes_per_launch"], os.path.basename(files[-1])
     return None, None
+
+
+def profiled_kernel_time(kernel):
+    """rocprofv3 --kernel-trace --stats durations of `kernel` from the newest committed profile summary
+    (profiles/rNN_pmc.json kernel_stats, scripts/profile.sh in the same gpurun lease as a bench run of
+    the same code): the average over every launch of the profiled bench run (warm-up and capture
+    launches included) and over its timed launches only (summarize_profile.py TIMED_LAUNCHES)."""
+    import glob
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")) if "train" not in f)
+    if not files:
+        return None
+    ks = json.load(open(files[-1])).get("kernel_stats", {})
+    for k, v in ks.items():
+        if _kernel_base(k) == _kernel_base(kernel):
+            return dict(v, kernel=k, source=os.path.basename(files[-1]))
+    return None
 
 
 def env_differential(args, pairs=2):
@@ -253,6 +272,8 @@ def parse():
     ap.add_argument("--rccl-gather", action="store_true",
                     help="N > 1: the exchange as one RCCL all-gather after each rollout instead of the pipelined "
                          "peer-to-peer copies beside the next rollout (uavhip.dist.IpcAllGather)")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the dropin_loop leg (main_train.py's loop at E = 1 through the drop-ins)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--eager", action="store_true", help="launch kernels eagerly instead of replaying a hipGraph")
     ap.add_argument("--unfused", action="store_true",
@@ -540,6 +561,87 @@ def e2e_iteration_rate(eng, policy, E, T, minibatch, iters=2):
             "timing": "host clock over the loop; phase split from HIP events around the rollout replay and the update"}
 
 
+def dropin_loop_rate(N, M, seconds, cpu_seconds=None):
+    """The reference's own training loop (main_train.py:79-146) at E = 1 through the drop-ins
+    (envs.uav_env.UAVEnv over the HIP env kernel, agents.ppo.PPOAgent over the fused forward and the
+    HIP training step at the reference's minibatch 64): per episode reset + the first state's value,
+    per step select_action -> step -> store_transition, update() when the buffer holds >= 4 x 64
+    transitions. Warm-up up to and including the third update (captures the epoch graphs of the
+    common buffer lengths), then timed for `seconds`. Host syncs per env step: select_action's one
+    device->host copy of (action, finite flag) and step's one 368-byte copy of the step's outputs.
+    Beside it, the CPU port of the same loop (oracle/cpu_loop_bench.py: C oracle env + torch-CPU
+    forward + torch-CPU autograd update, 1 thread) in a child process."""
+    import random
+    import subprocess
+    from agents.ppo import PPOAgent
+    from envs.uav_env import UAVEnv
+    from uavhip.config import cfg
+    saved = (cfg.NUM_UAVS, cfg.NUM_TARGETS)
+    cfg.NUM_UAVS, cfg.NUM_TARGETS = N, M
+    try:
+        np.random.seed(0)
+        random.seed(0)
+        torch.manual_seed(0)
+        env, agent = UAVEnv(), PPOAgent()
+        st = dict(steps=0, roll_s=0.0, upd_s=0.0, upd_samples=0, updates=0, episodes=0)
+
+        def episode(i):
+            state = env.reset(full_reset=(i == 1 or i % 200 == 0))
+            with torch.no_grad():  # main_train.py:87-93
+                agent.policy_old.get_action(torch.as_tensor(state).unsqueeze(0).to(agent.device))[2].item()
+            done, n = False, 0
+            while not done:
+                a = agent.select_action(state)
+                state, r, done, _ = env.step(a)
+                agent.store_transition(r, done)
+                n += 1
+            return n
+
+        i = warm_updates = 0
+        while warm_updates < 3:
+            i += 1
+            episode(i)
+            if len(agent.buffer["states"]) >= cfg.BATCH_SIZE * 4:
+                agent.update()
+                warm_updates += 1
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        while time.perf_counter() - t_start < seconds:
+            i += 1
+            t0 = time.perf_counter()
+            st["steps"] += episode(i)
+            st["roll_s"] += time.perf_counter() - t0
+            st["episodes"] += 1
+            if len(agent.buffer["states"]) >= cfg.BATCH_SIZE * 4:
+                nb = len(agent.buffer["states"])
+                t1 = time.perf_counter()
+                agent.update()
+                torch.cuda.synchronize()
+                st["upd_s"] += time.perf_counter() - t1
+                st["upd_samples"] += nb
+                st["updates"] += 1
+        total = time.perf_counter() - t_start
+    finally:
+        cfg.NUM_UAVS, cfg.NUM_TARGETS = saved
+    res = {"workload": f"E = 1, {N} UAV x {M} tgt: main_train.py:79-146 through envs.uav_env.UAVEnv / agents.ppo.PPOAgent",
+           "value": st["steps"] / total, "unit": "env-steps/s (loop wall time, updates included)",
+           "rollout_env_steps_per_s": st["steps"] / st["roll_s"],
+           "update_samples_per_s": st["upd_samples"] / st["upd_s"] if st["upd_s"] > 0 else None,
+           "update_unit": "transitions per update() wall time (5 epochs at minibatch 64, HIP training step)",
+           "host_syncs_per_env_step": 2,
+           "host_syncs": "select_action: one device->host copy of (action, finite flag); UAVEnv.step: one 368-byte "
+                         "copy of obs / reward / info / done; plus one per episode (the first state's value)",
+           "episodes": st["episodes"], "updates": st["updates"], "seconds": total}
+    try:
+        out = subprocess.run([sys.executable, "-m", "oracle.cpu_loop_bench", "--uavs", str(N), "--targets", str(M),
+                              "--seconds", str(cpu_seconds or seconds), "--threads", "1"],
+                             cwd=ROOT, capture_output=True, text=True, timeout=(cpu_seconds or seconds) + 180, check=True)
+        res["cpu_baseline"] = json.loads(out.stdout.strip().splitlines()[-1])
+    except Exception as exc:  # the headline line must still print
+        res["cpu_baseline"] = {"value": None, "error": repr(exc)}
+    return res
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -692,7 +794,12 @@ def main():
             # events, child processes on this box); the TRACE build's phase share is a diagnostic
             env_diff, env_err = env_differential(args)
             if env_diff is not None and env_diff["env_ms"] > 0:
-                env_ms = env_diff["env_ms"]
+                # the differential's share of its own product time, applied to the headline kernel's
+                # time (the child runs replay the iteration warm like the bench; the share carries the
+                # measurement to the headline's operating point either way)
+                env_diff["share"] = env_diff["env_ms"] / env_diff["product_ms"]
+                env_diff["product_vs_headline"] = env_diff["product_ms"] / pol_ms
+                env_ms = env_diff["share"] * pol_ms
             elif env_diff is not None:
                 env_err = f"non-positive differential {env_diff['env_ms']:.4f} ms"
             env_phase, phase_err = env_phase_share(args)
@@ -753,6 +860,16 @@ def main():
                 print(f"[bench] end-to-end iteration at minibatch {mb} failed: {exc!r}", file=sys.stderr)
                 e2e[f"minibatch_{mb}"] = {"value": None, "error": repr(exc)}
 
+    dropin = None
+    if rank == 0 and world == 1 and not args.no_dropin:
+        dropin = []
+        for N_, M_ in ((30, 10), (args.uavs, args.targets)):
+            try:
+                dropin.append(dropin_loop_rate(N_, M_, 6.0))
+            except Exception as exc:  # the headline line must still print
+                print(f"[bench] dropin loop {N_}x{M_} failed: {exc!r}", file=sys.stderr)
+                dropin.append({"workload": f"E = 1, {N_} UAV x {M_} tgt", "value": None, "error": repr(exc)})
+
     cpu = cpu_env = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, policy.state_dict(), args.cpu_seconds)
@@ -767,6 +884,17 @@ def main():
     pol_traffic, pol_src = profiled_traffic(pol_kernel)
     if pol_traffic is not None and eng.persistent:  # one launch = T steps: per-step bytes
         pol_traffic /= T
+    prof_kernel = None
+    pk = profiled_kernel_time(pol_kernel)
+    if pk is not None:  # rocprofv3 of the same code, same lease as a bench run (scripts/profile.sh)
+        per = T if eng.persistent else 1
+        prof_kernel = {"kernel": pk["kernel"], "source": pk["source"],
+                       "avg_ms_per_step": pk["avg_ns"] * 1e-6 / per,
+                       "timed_avg_ms_per_step": pk["timed_avg_ns"] * 1e-6 / per if "timed_avg_ns" in pk else None,
+                       "timed_min_ms_per_step": pk["timed_min_ns"] * 1e-6 / per if "timed_min_ns" in pk else None,
+                       "launches": pk.get("calls"),
+                       "what": "rocprofv3 --kernel-trace --stats of bench.py --steps 10 --warmup 2: average over all "
+                               "launches and over the 10 timed ones, per step"}
     env_prof_ns = None
     if eng.persistent:
         env_traffic, env_traffic_src, env_prof_ns = env_share_traffic()
@@ -800,7 +928,9 @@ def main():
                          "traffic": pol_traffic,
                          "traffic_unit": "bytes per step (PMC bytes per launch / T)" if eng.persistent else
                          "bytes/launch (PMC)", "traffic_source": pol_src,
-                         "avg_launch_ms": pol_ms, "flop_per_launch": POLICY_FLOP_PER_SAMPLE * E,
+                         "avg_launch_ms": pol_ms,
+                         "profiled": prof_kernel,
+                         "flop_per_launch": POLICY_FLOP_PER_SAMPLE * E,
                          "flop_per_launch_source": "SURVEY.md 8(d): 2,446,208 FLOP/sample x E",
                          "executed_flop_per_launch": flop_exec * E, "executed_achieved": exec_tf,
                          "executed_peak": peak_exec, "executed_frac": exec_tf / peak_exec,
@@ -825,8 +955,10 @@ def main():
                 "kernel": "env step inside k_rollout_steps" if eng.persistent else
                 "env step inside the fused rollout launch" if eng.fused_step else "k_env_step",
                 "timing": ("the compiled-out differential: k_rollout_steps per step on the product build minus "
-                           "on the NOENV build (env step compiled out), HIP events, median of alternating "
-                           "child-process runs on this box (scripts/rollout_run.py)" if eng.persistent else
+                           "on the NOENV build (env step compiled out), HIP events on an eager iteration after warm "
+                           "graph replays, median of alternating child-process runs on this box "
+                           "(scripts/rollout_run.py); its share of the product time x the headline kernel's time"
+                           if eng.persistent else
                            "per-step fused launch minus the bootstrap forward launch" if eng.fused_step else
                            "HIP events around each of the T env launches"),
                 "differential": env_diff,
@@ -850,6 +982,7 @@ def main():
             "exchange": exchange,
             "ppo_samples_per_s_mb64": ppo64,
             "e2e_iteration": e2e,
+            "dropin_loop": dropin,
             "cpu_baseline": cpu,
             "cpu_env_baseline": cpu_env,
         }

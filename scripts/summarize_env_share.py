@@ -20,7 +20,8 @@ for b in ("product", "noenv"):
             for r in csv.DictReader(open(os.path.join(src, b, "trace", "run_kernel_trace.csv")))
             if KERNEL in r["Kernel_Name"]]
     d["launches"] = len(durs)
-    d["avg_ns_per_step"] = sum(durs[1:]) / max(1, len(durs) - 1) / T  # the first launch warms up
+    warm = durs[len(durs) // 2:] if len(durs) > 2 else durs[1:]  # steady state: the later half of the launches
+    d["avg_ns_per_step"] = sum(warm) / max(1, len(warm)) / T
     for i, c in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
         d_ = os.path.join(src, b, f"pmc_{c}")
         if not os.path.isdir(d_):  # scripts/profile_env_attrib.sh's layout: pmc_1 = FETCH, pmc_2 = WRITE

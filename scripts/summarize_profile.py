@@ -39,9 +39,16 @@ if os.path.exists(trace_csv):
     for r in csv.DictReader(open(trace_csv)):
         durs[r["Kernel_Name"].split("(")[0].replace("void ", "")].append(
             int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    timed = int(os.environ.get("TIMED_LAUNCHES", "10"))  # profile.sh's --steps: the bench's timed iterations
     for k, v in durs.items():
         if k in stats and len(v) >= 128:
             stats[k]["last64_avg_ns"] = sum(v[-64:]) / 64
+        if k in stats and "k_rollout_steps" in k and len(v) > timed:
+            # the bench's timed region: the last `timed` launches (graph replays + the eager one),
+            # after the warm-up, capture and capture-warm-up launches
+            stats[k]["timed_avg_ns"] = sum(v[-timed:]) / timed
+            stats[k]["timed_min_ns"] = min(v[-timed:])
+            stats[k]["timed_launches"] = timed
 json.dump({"pmc": out, "kernel_stats": stats, "source": os.path.basename(src)},
           open(os.path.join(dst, f"{rnd}_pmc.json"), "w"), indent=1)
 print(json.dumps({k: v for k, v in out.items() if "uavhip" in k}, indent=1))

@@ -145,8 +145,11 @@ class PPOAgent:
         self.buffer["actions"].append(action)
         self.buffer["logprobs"].append(logp)
         self.buffer["values"].append(value)
-        a = int(action.item())  # the host sync the reference's loop already has
-        if not bool(torch.isfinite(logp).all() & torch.isfinite(value).all()):
+        # one device->host copy (the sync the reference's loop already has): the action and a finite flag
+        ok = torch.isfinite(logp).all() & torch.isfinite(value).all()
+        host = torch.stack([action.reshape(-1)[0].to(torch.float32), ok.to(torch.float32)]).cpu()
+        a = int(host[0])
+        if not bool(host[1]):
             # torch's Categorical rejects non-finite probabilities (transformer_net.py:118-120); here
             # they mean a split-product operand left fp16's range (|x| >= 65536, common.hpp f16_lo)
             raise ValueError("the policy produced a non-finite log-probability / value (an activation beyond "

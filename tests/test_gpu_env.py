@@ -650,3 +650,97 @@ def test_configs4_shard_at_size():
             if d_c:
                 ref.reset()
     print(f"configs[4] shard: {int(ends.sum())} episodes ended over {E} envs x {T} steps")
+
+
+def test_configs1_k2r_at_size_vs_oracle():
+    """BASELINE configs[1] at its own size: 1024 envs x 8 UAVs x 16 targets, one 256-step env-only
+    launch (K2r, the omega = 0 replay: auto-reset, full_reset_period 200 as main_train.py:79) on
+    device-generated scenes; 8 sampled envs replayed step by step through the CPU oracle
+    (uav_env.py:295-435) -- done / num_assigned / is_valid bit-exact, rewards and J to 1e-12,
+    windows to the fp32 bar (2e-6) -- and every env's outputs finite with no stepping error."""
+    import oracle
+    from uavhip import _lib
+    from uavhip.vec_env import VecUAVEnv
+    E, N, M, T = 1024, 8, 16, 256
+    v = VecUAVEnv(E, N, M, 1, 1, full_reset_period=200, seed=21)
+    v.istate[:, _lib.IST["EPISODE"]] = 1
+    v.generate_scenes()
+    scenes = {}
+    picks = [int(e) for e in np.random.default_rng(4).choice(E, 8, replace=False)]
+    for e in picks:
+        scenes[e] = _device_scene(v, e)
+    obs0 = v.reset(episode=1).cpu().numpy()
+    g = torch.Generator(device="cuda").manual_seed(22)
+    acts = (torch.rand(T, E, device="cuda", generator=g) < 0.5).to(torch.int8)
+    obs, rew, done, info = (x.cpu().numpy() for x in v.step(acts))
+    assert np.isfinite(rew).all() and np.isfinite(info).all() and int(v.errors().max()) == 0
+    prm = np.array([v.desc.prm[i] for i in range(_lib.PRM_COUNT)])
+    a_np = acts.cpu().numpy()
+    ends = 0
+    for e in picks:
+        ref = oracle.OracleEnv(scenes[e], prm)
+        np.testing.assert_allclose(obs0[e], ref.reset(), rtol=2e-6, atol=1e-6)
+        for t in range(T):
+            o_c, r_c, d_c, i_c = ref.step(int(a_np[t, e]))
+            assert bool(done[t, e]) == d_c, (e, t)
+            assert abs(rew[t, e] - r_c) <= 1e-12 * max(1.0, abs(r_c)), (e, t, rew[t, e], r_c)
+            np.testing.assert_array_equal(info[t, e, [1, 2, 5, 6]], i_c[[1, 2, 5, 6]])
+            assert abs(info[t, e, 0] - i_c[0]) <= 1e-12 * max(1.0, abs(i_c[0]))
+            if d_c:
+                ends += 1
+                o_c = ref.reset()
+            np.testing.assert_allclose(obs[t, e], o_c, rtol=2e-6, atol=1e-6)
+    print(f"configs[1]: {ends} episodes ended in the 8 replayed envs; {int(done.sum())} over all {E} envs")
+    assert ends > 8
+
+
+def test_configs2_rollout_iteration_at_size_vs_oracle():
+    """BASELINE configs[2] at its own size: one full k_rollout_steps iteration over 4096 envs x 16
+    UAVs x 32 targets, T = 64 (window-row forward + sampling + env step, auto-reset, full_reset_period
+    200) on device-generated scenes. 8 sampled envs replayed through the CPU oracle with the actions
+    the kernel sampled -- done bit-exact, rewards and J to 1e-12, windows to 2e-6 -- and their
+    log-probabilities / values against the torch fp32 `evaluate` of the same windows and actions
+    (transformer_net.py:124-144; 1e-5). Every env's outputs finite."""
+    import oracle
+    from uavhip import _lib
+    from uavhip.policy import TransformerActorCritic
+    from uavhip.rollout import RolloutEngine
+    from uavhip.vec_env import VecUAVEnv
+    E, N, M, T = 4096, 16, 32, 64
+    torch.manual_seed(23)
+    pol = TransformerActorCritic().cuda()
+    v = VecUAVEnv(E, N, M, 1, 1, full_reset_period=200, seed=24)
+    eng = RolloutEngine(v, pol, T, seed=25)
+    assert eng.persistent
+    eng.start()
+    picks = [int(e) for e in np.random.default_rng(6).choice(E, 8, replace=False)]
+    scenes = {e: _device_scene(v, e) for e in picks}
+    tr = eng.collect()
+    torch.cuda.synchronize()
+    assert torch.isfinite(tr.logp).all() and torch.isfinite(tr.values).all() and torch.isfinite(tr.rewards).all()
+    assert int((v.errors() & 1).max()) == 0
+    prm = np.array([v.desc.prm[i] for i in range(_lib.PRM_COUNT)])
+    obs, act = tr.obs.cpu().numpy(), tr.actions.cpu().numpy()
+    rew, done, info = tr.rewards.cpu().numpy(), tr.dones.cpu().numpy(), tr.info.cpu().numpy()
+    ends = 0
+    for e in picks:
+        ref = oracle.OracleEnv(scenes[e], prm)
+        np.testing.assert_allclose(obs[0, e], ref.reset(), rtol=2e-6, atol=1e-6)
+        for t in range(T):
+            o_c, r_c, d_c, i_c = ref.step(int(act[t, e]))
+            assert bool(done[t, e]) == d_c, (e, t)
+            assert abs(rew[t, e] - r_c) <= 1e-12 * max(1.0, abs(r_c)), (e, t, rew[t, e], r_c)
+            np.testing.assert_array_equal(info[t, e, [1, 2, 5, 6]], i_c[[1, 2, 5, 6]])
+            assert abs(info[t, e, 0] - i_c[0]) <= 1e-12 * max(1.0, abs(i_c[0]))
+            if d_c:
+                ends += 1
+                o_c = ref.reset()
+            np.testing.assert_allclose(obs[t + 1, e], o_c, rtol=2e-6, atol=1e-6)
+    idx = torch.tensor(picks, device="cuda")
+    x = tr.obs[:T, idx].reshape(T * len(picks), 5, 14)
+    a = tr.actions[:, idx].reshape(-1).long()
+    with torch.no_grad():
+        lp_t, v_t, _ = pol.evaluate(x, a)
+    torch.testing.assert_close(tr.logp[:, idx].reshape(-1), lp_t, rtol=1e-5, atol=2e-6)
+    torch.testing.assert_close(tr.values[:, idx].reshape(-1), v_t[:, 0], rtol=1e-5, atol=1e-5)
+    print(f"configs[2]: {ends} episodes ended in the 8 replayed envs over {T} steps")
