@@ -271,8 +271,18 @@ int32_t uavhip_policy_layout(int32_t* offsets, int32_t max_offsets);
 int32_t uavhip_policy_split_layout(int32_t* params, int32_t* offsets, int32_t max_entries);
 
 /* flat (state_dict order, uavhip_policy_layout offsets, every parameter row-major) -> packed
- * (the same with the uavhip_policy_tiling weights in MFMA fragment order), on the device. */
+ * (the same with the uavhip_policy_tiling weights in MFMA fragment order, the split copies and the
+ * range table), on the device. */
 int uavhip_policy_pack(const float* flat, float* packed, uavhip_stream_t stream);
+
+/* The range table that ends the packed buffer (its last n floats, n = the return value): the
+ * split products multiply every activation operand by a power of two 2^-s before splitting it into
+ * fp16 planes and the GEMM output by 2^s, with s from a rigorous bound on the operand's magnitude
+ * (0 on realistic weights), so no operand the reference's fp32 can hold leaves fp16's range.
+ * Host side: max_abs[50] = max |param| of each state_dict tensor (key order) -> table[n] (the
+ * maxima, the per-token constants of layer 0, the static operands' (2^-s, 2^s) pairs), the same
+ * floats uavhip_policy_pack writes on the device. Either pointer NULL: only returns n. */
+int32_t uavhip_policy_range_table(const float* max_abs, float* table);
 
 /* Per parameter (state_dict key order): the in-features K of the weight matrices stored in MFMA
  * fragment order, 0 for parameters stored flat. An [R][K] matrix W in fragment order puts
@@ -457,8 +467,9 @@ int uavhip_copy_async(void* dst, const void* src, uint64_t bytes, uavhip_stream_
 /* ---------------------------------------------------------------- misc */
 const char* uavhip_last_error(void);
 /* 4 since round 3 (struct uavhip_ppo: the Adam hyper-parameters are doubles; the inference packed
-   buffer carries split weight copies, uavhip_policy_split_layout); the ctypes binding refuses a
-   library of another version */
+   buffer carries split weight copies, uavhip_policy_split_layout); 5 since round 5 (the packed
+   buffer ends with the range table, uavhip_policy_range_table; N > 1 peers by PCI bus id); the
+   ctypes binding refuses a library of another version */
 int32_t uavhip_abi_version(void);
 
 #ifdef __cplusplus

@@ -26,7 +26,7 @@ int check_launch(const char* what) {
 }  // namespace uavhip
 
 extern "C" const char* uavhip_last_error(void) { return uavhip::g_err; }
-extern "C" int32_t uavhip_abi_version(void) { return 4; }
+extern "C" int32_t uavhip_abi_version(void) { return 5; }
 
 // ------------------------------------------------------------------ the N > 1 trajectory exchange
 // Peer-to-peer plumbing for uavhip.dist.IpcAllGather: a rank exports its send buffers

@@ -123,6 +123,8 @@ struct Smem {
     float logits[SPW * 2];
     float value[SPW];
     int mask[SPW * S];          // key padding mask (transformer_net.py:52-54)
+    float tmax[TOK];            // max_k |x_k| of each token's window row (layer 0's operand range)
+    float smax[SPW];            // max over a sample's five tokens (its layer-0 attention output's range)
 };
 
 // Lane index plumbing. In the multi-step rollout TU (rollout_steps.hip) every forward helper takes
@@ -362,18 +364,68 @@ __device__ __forceinline__ void hsplit_store(_Float16* Y, int o, const f32x4 v) 
     *reinterpret_cast<f16x4*>(Y + o) = v1;
     *reinterpret_cast<f16x4*>(Y + o + kPlane) = v2;
 }
+// ------------------------------------------------------------------ operand ranges of the split products
+// Every activation operand is split as x 2^-s and the consuming GEMM's output multiplied by 2^s
+// (policy_layout.hpp range table: s = 0 on realistic weights). Static operands (LayerNorm outputs,
+// FFN hidden units, the attention output of a layer >= 1) take (2^-s, 2^s) from the table; layer 0's
+// input takes s per token from the token's window-row max (Smem::tmax) and layer 0's attention
+// output per sample (Smem::smax). Producer and consumer evaluate the same uncontracted expression
+// (__fmul_rn / __fadd_rn), so both sides always agree on s.
+struct OpSc {
+    float sc, inv;  // 2^-s (the producer's factor), 2^s (the consumer's)
+};
+template <int trunk, int layer, int kind>
+__device__ __forceinline__ OpSc op_sc(const float* __restrict__ P) {
+    constexpr int op = range_op(trunk, layer, kind);
+    static_assert(op >= 0, "a static operand");
+    return OpSc{P[kRangeOff + kRgOp + 2 * op], P[kRangeOff + kRgOp + 2 * op + 1]};
+}
+// bound of layer 0's input (e or e + pos) at a token whose window row has max |x_k| = m, from the
+// trunk's constants ea = 14 max|W_e|, ec = max|b_e| + max|pos|
+__device__ __forceinline__ float e_bound_v(float ea, float ec, float m) { return __fadd_rn(__fmul_rn(ea, m), ec); }
+__device__ __forceinline__ OpSc e_sc_v(float ea, float ec, float m) {
+    const int s = range_exp(e_bound_v(ea, ec, m));
+    return OpSc{ldexpf(1.0f, -s), ldexpf(1.0f, s)};
+}
+template <int trunk>
+__device__ __forceinline__ float e_bound(const float* __restrict__ P, float m) {
+    constexpr int ti = trunk_index(trunk);
+    return e_bound_v(P[kRangeOff + kRgE + 2 * ti], P[kRangeOff + kRgE + 2 * ti + 1], m);
+}
+template <int trunk>
+__device__ __forceinline__ OpSc e_sc(const float* __restrict__ P, float m) {
+    constexpr int ti = trunk_index(trunk);
+    return e_sc_v(P[kRangeOff + kRgE + 2 * ti], P[kRangeOff + kRgE + 2 * ti + 1], m);
+}
+// layer 0's attention output of a sample whose window has max |x_k| = m (over its five rows)
+template <int trunk>
+__device__ __forceinline__ OpSc a0_sc(const float* __restrict__ P, float m) {
+    constexpr int ti = trunk_index(trunk);
+    const float b = __fadd_rn(__fmul_rn(P[kRangeOff + kRgA0 + 2 * ti], e_bound<trunk>(P, m)),
+                              P[kRangeOff + kRgA0 + 2 * ti + 1]);
+    const int s = range_exp(b);
+    return OpSc{ldexpf(1.0f, -s), ldexpf(1.0f, s)};
+}
+// The scale of an attention output (layer 0: the sample's, else the static one)
+template <int trunk, int layer>
+__device__ __forceinline__ OpSc att_sc(const float* __restrict__ P, const float* smax, int p) {
+    if constexpr (layer == 0) return a0_sc<trunk>(P, smax[p]);
+    else return op_sc<trunk, layer, kOpAtt>(P);
+}
+
 // Y planes [ytok0 + 16 ct + j][ycol + i] = epi(hi + 2^-11 lo + bias[row + i])
+// (the operand's scale undone: x inv; the output's planes scaled: x osc)
 template <int CT, bool RELU>
 __device__ __forceinline__ void hstore_tile(TID_F const f32x4 (&hi)[CT], const f32x4 (&lo)[CT], const f32x4 bb,
-                                            _Float16* Y, int ycol, int ytok0) {
+                                            _Float16* Y, int ycol, int ytok0, float inv, float osc) {
     const int l = LANE(), i16 = l & 15, g = l >> 4;
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-        f32x4 v = hi[ct] + lo[ct] * kLoScale + bb;
+        f32x4 v = (hi[ct] + lo[ct] * kLoScale) * inv + bb;
         if (RELU) {
             v.x = relu_nan(v.x); v.y = relu_nan(v.y); v.z = relu_nan(v.z); v.w = relu_nan(v.w);
         }
-        hsplit_store(Y, psw((ytok0 + 16 * ct + i16), ycol + 4 * g), v);
+        hsplit_store(Y, psw((ytok0 + 16 * ct + i16), ycol + 4 * g), v * osc);
     }
 }
 
@@ -422,6 +474,22 @@ __device__ __forceinline__ float add_xor32(float v) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// max over each row of 16 lanes (quad permutes, then row_ror 4 / 8), the same in every lane of the row
+template <int ctrl>
+__device__ __forceinline__ float max_dpp(float v) {
+    return fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xF, 0xF, true)));
+}
+__device__ __forceinline__ float row16_max(float v) {
+    return max_dpp<0x128>(max_dpp<0x124>(max_dpp<0x4E>(max_dpp<0xB1>(v))));
+}
+// max over the wave (the same value in every lane)
+__device__ __forceinline__ float wave_max(float v) {
+    v = row16_max(v);
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
 
 // Fused GEMM epilogue + post-LN (nn.TransformerEncoderLayer norm1 / norm2, eps 1e-5):
 //   h[tok][f] = LN(h[tok] + acc + bias)[f] * w[f] + b[f]
@@ -457,13 +525,13 @@ __device__ __forceinline__ LnPar ln_load(TID_F const f32x4 bb, const float* __re
 // operand; the caller keeps the fp32 output from `outv`); resid: the residual from registers (the
 // lane's own elements, as `outv` returned them) instead of sm.h.
 // ROW4 (with PLANES): the fp32 output of position 4 (tokens 64-79) also goes to sm.ctx rows 0-15 (the
-// next, pruned layer's residual and query rows).
+// next, pruned layer's residual and query rows). psc: the planes' scale (the operand's 2^-s).
 // T0 / T1 / T2 (trace builds, >= 0): phase stamps when the GEMM accumulators are consumed, when the
 // partial statistics are written, after the barrier
 template <int CT, bool TR = false, bool PLANES = false, bool ROW4 = false, int T0 = -1, int T1 = -1, int T2 = -1>
 __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (&acc)[CT], const LnPar& lp, int ytok0,
                                                    const LnOut& lo = LnOut{}, f32x4* outv = nullptr,
-                                                   const f32x4* resid = nullptr) {
+                                                   const f32x4* resid = nullptr, float psc = 1.f) {
     const int l = LANE(), i16 = l & 15, g = l >> 4, wv = TIDX() >> 6;
     const int f0 = 16 * wv + 4 * g;
     const f32x4 bb = lp.bb;
@@ -542,7 +610,7 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
         }
         const f32x4 xh = (v[ct] - mean) * rs;
         const f32x4 out = xh * ww + lb;
-        if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.h), psw(tok, f0), out);
+        if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.h), psw(tok, f0), out * psc);
         else *reinterpret_cast<f32x4*>(sm.h + tok * LDH + f0) = out;
         if constexpr (ROW4) {
             if (ct == CT - 1) *reinterpret_cast<f32x4*>(sm.ctx + (tok - (S - 1) * SPW) * LDH + f0) = out;
@@ -617,8 +685,9 @@ __device__ __forceinline__ void attention_full_core(TID_F Smem& sm, int c, f32x4
         }
     }
 }
+// sc: the planes' scale (PLANES), of this thread's sample p (attn_sc)
 template <bool PLANES>
-__device__ __forceinline__ void attention_full_store(TID_F Smem& sm, int c, const f32x4 (&o)[3]) {
+__device__ __forceinline__ void attention_full_store(TID_F Smem& sm, int c, const f32x4 (&o)[3], float sc = 1.f) {
     const int q4 = TIDX() & 3, task = TIDX() >> 2;
     const int hh = task & 3, p = (task >> 2) & 15, grp = task >> 6;
     const int d0 = hh * HD + 4 * q4, qs0 = grp ? 3 : 0, nq = grp ? 2 : 3;
@@ -626,17 +695,24 @@ __device__ __forceinline__ void attention_full_store(TID_F Smem& sm, int c, cons
     for (int qi = 0; qi < 3; ++qi) {
         if (qi < nq) {
             const int ti = (qs0 + qi) * SPW + p;
-            if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw(ti, 4 * c * HD + d0), o[qi]);
+            if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw(ti, 4 * c * HD + d0), o[qi] * sc);
             else *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o[qi];
         }
     }
 }
-// PLANES: the output goes to sm.ctx as the two fp16 planes of the split products (the out-projection's operand).
-template <bool PLANES = false>
-__device__ void attention_full(TID_F Smem& sm, int c) {
+// The planes' scale of an attention output of sample p (1 when it is stored in fp32)
+template <bool PLANES, int trunk, int layer>
+__device__ __forceinline__ float attn_sc(const float* __restrict__ P, const Smem& sm, int p) {
+    if constexpr (PLANES) return att_sc<trunk, layer>(P, sm.smax, p).sc;
+    else return 1.f;
+}
+// PLANES: the output goes to sm.ctx as the two fp16 planes of the split products (the out-projection's
+// operand), scaled for layer `layer` of trunk `trunk`.
+template <bool PLANES = false, int trunk = kCriticTrunk, int layer = 1>
+__device__ void attention_full(TID_F Smem& sm, int c, const float* __restrict__ P = nullptr) {
     f32x4 o[3];
     attention_full_core(TID_C sm, c, o);
-    attention_full_store<PLANES>(TID_C sm, c, o);
+    attention_full_store<PLANES>(TID_C sm, c, o, attn_sc<PLANES, trunk, layer>(P, sm, (int)((TIDX() >> 4) & 15)));
 }
 
 // Scaled-dot-product attention for heads [4c, 4c+4) of the query positions [qs0, qs0 + nqs) over
@@ -675,18 +751,18 @@ __device__ __forceinline__ void attention_task(TID_F Smem& sm, int task, int qs0
     }
 }
 template <bool PLANES>
-__device__ __forceinline__ void attention_out(TID_F Smem& sm, int c, int ti, int d0, const f32x4 o) {
-    if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw(ti, 4 * c * HD + d0), o);
+__device__ __forceinline__ void attention_out(TID_F Smem& sm, int c, int ti, int d0, const f32x4 o, float sc = 1.f) {
+    if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw(ti, 4 * c * HD + d0), o * sc);
     else *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o;
 }
-template <bool PLANES = false>
-__device__ void attention_chunk(TID_F Smem& sm, int c, int qs0, int nqs) {
+template <bool PLANES = false, int trunk = kCriticTrunk, int layer = 1>
+__device__ void attention_chunk(TID_F Smem& sm, int c, int qs0, int nqs, const float* __restrict__ P = nullptr) {
     const int ntask = nqs * SPW * 4;
     for (int task = TIDX() >> 2; task < ntask; task += NTHR / 4) {
         f32x4 o;
         int ti, d0;
         attention_task(TID_C sm, task, qs0, o, ti, d0);
-        attention_out<PLANES>(TID_C sm, c, ti, d0, o);
+        attention_out<PLANES>(TID_C sm, c, ti, d0, o, attn_sc<PLANES, trunk, layer>(P, sm, ti & 15));
     }
 }
 
@@ -696,6 +772,7 @@ __device__ void attention_chunk(TID_F Smem& sm, int c, int qs0, int nqs) {
 // can issue later loads behind them without the embedding waiting for those (in-order vmcnt).
 struct EmbPre {
     f32x4 a, bb, pp[S];
+    float ea, ec;  // the layer-0 input's range constants (e_sc_v)
 };
 template <int trunk>
 __device__ __forceinline__ EmbPre embed_load(TID_F const float* __restrict__ P) {
@@ -712,6 +789,8 @@ __device__ __forceinline__ EmbPre embed_load(TID_F const float* __restrict__ P) 
     r.bb = *reinterpret_cast<const f32x4*>(be + 16 * wv + 4 * g);
 #pragma unroll
     for (int ct = 0; ct < S; ++ct) r.pp[ct] = *reinterpret_cast<const f32x4*>(pos + ct * D + 16 * wv + 4 * g);
+    r.ea = P[kRangeOff + kRgE + 2 * trunk_index(trunk)];
+    r.ec = P[kRangeOff + kRgE + 2 * trunk_index(trunk) + 1];
     return r;
 }
 // MODE kEmbH: h = e + pos for all 5 positions (sm.h). kEmbSplit: also e of position 4 (no pos)
@@ -741,13 +820,15 @@ __device__ void embed_apply(TID_F Smem& sm, const EmbPre& ep, float* e_out = nul
         e.x = fmaxf(e.x, 0.f); e.y = fmaxf(e.y, 0.f); e.z = fmaxf(e.z, 0.f); e.w = fmaxf(e.w, 0.f);
         const int o = (ct * SPW + i16) * LDH + 16 * wv + 4 * g;
         constexpr bool ring_planes = split_slot(layer_param(trunk, 0, INW)) >= 0;  // the ring GEMM's operand
+        // the planes of layer 0's input scaled per token (its window row's range)
+        const float esc = (ring_planes || PL) ? e_sc_v(ep.ea, ep.ec, sm.tmax[ct * SPW + i16]).sc : 1.f;
         if ((MODE == kEmbRows || (MODE == kEmbSplit && ct == S - 1)) && ring_planes)
-            hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((ct * SPW + i16), 16 * wv + 4 * g), e);
+            hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((ct * SPW + i16), 16 * wv + 4 * g), e * esc);
         else if (MODE == kEmbRows || (MODE == kEmbSplit && ct == S - 1)) *reinterpret_cast<f32x4*>(sm.ctx + o) = e;
         if (MODE == kEmbRows) continue;
         const f32x4 v = e + ep.pp[ct];
         *reinterpret_cast<f32x4*>(sm.h + o) = v;
-        if constexpr (PL) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((ct * SPW + i16), 16 * wv + 4 * g), v);
+        if constexpr (PL) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((ct * SPW + i16), 16 * wv + 4 * g), v * esc);
         if (TR && !kExpNoStore) {
             const size_t r = (size_t)trow(ct * SPW + i16, b0);
             *reinterpret_cast<f32x4*>(e_out + r * D + 16 * wv + 4 * g) = e;
@@ -838,20 +919,31 @@ __device__ __forceinline__ void store_qkv_chunk(TID_F const Smem& sm, float* __r
     }
 }
 // Training mode: fp32 rows from the two planes of a split-product operand in LDS (the values the
-// GEMM consumed: x1 + 2^-11 x2) -> workspace rows (stride ldo, column offset c0), tokens [t0, t1).
+// GEMM consumed: (x1 + 2^-11 x2) 2^s, inv(tok) = 2^s of the token's operand scale) -> workspace rows
+// (stride ldo, column offset c0), tokens [t0, t1).
+template <class Inv>
 __device__ __forceinline__ void store_rows_planes(TID_F const _Float16* src, float* dst, int ldo, int c0, int ncols,
-                                                  int t0, int b0, bool compact, int t1) {
+                                                  int t0, int b0, bool compact, int t1, Inv inv) {
     if (kExpNoStore) return;
     const int n4 = ncols / 4, items = (t1 - t0) * n4;
     for (int i = TIDX(); i < items; i += NTHR) {
         const int tok = t0 + i / n4, q = i % n4;
         const f16x4 x1 = *reinterpret_cast<const f16x4*>(src + psw(tok, 4 * q));
         const f16x4 x2 = *reinterpret_cast<const f16x4*>(src + kPlane + psw(tok, 4 * q));
+        const float s = inv(tok);
         f32x4 v;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (float)x1[j] + (float)x2[j] * kLoScale;
+        for (int j = 0; j < 4; ++j) v[j] = ((float)x1[j] + (float)x2[j] * kLoScale) * s;
         *reinterpret_cast<f32x4*>(dst + (size_t)orow(tok, b0, compact) * ldo + c0 + 4 * q) = v;
     }
+}
+
+// 2^s of a layer's in_proj operand at token tok: layer 0's input per token (its window row's range),
+// a later layer's input = the previous layer's LN2 output (static)
+template <int trunk, int layer>
+__device__ __forceinline__ float in_inv(TID_F const float* __restrict__ P, const Smem& sm, int tok) {
+    if constexpr (layer == 0) return e_sc<trunk>(P, sm.tmax[tok]).inv;
+    else return op_sc<trunk, layer - 1, kOpLn2>(P).inv;
 }
 
 // An encoder layer whose in_proj runs as split products: K / V of all 80 tokens and Q of the query
@@ -891,7 +983,8 @@ __device__ __forceinline__ void encoder_layer_split(TID_F Smem& sm, const float*
             const int col = (1 + (wv >> 2)) * 64 + 16 * (wv & 3) + 4 * g;
 #pragma unroll
             for (int ct = 0; ct < S; ++ct)
-                *reinterpret_cast<f32x4*>(sm.big + (16 * ct + i16) * LDB + col) = hi[ct] + lo[ct] * kLoScale + bb;
+                *reinterpret_cast<f32x4*>(sm.big + (16 * ct + i16) * LDB + col) =
+                    (hi[ct] + lo[ct] * kLoScale) * in_inv<trunk, layer>(TID_C P, sm, 16 * ct + i16) + bb;
         }
         if (wv < 4) {  // Q of the chunk for the query tokens (their SIMD partners did V)
             const f32x4 bq = *reinterpret_cast<const f32x4*>(bin + 64 * c + 16 * wv + 4 * g);
@@ -902,7 +995,7 @@ __device__ __forceinline__ void encoder_layer_split(TID_F Smem& sm, const float*
 #pragma unroll
             for (int ct = 0; ct < CTQ; ++ct)
                 *reinterpret_cast<f32x4*>(sm.big + (qtok0 + 16 * ct + i16) * LDB + 16 * wv + 4 * g) =
-                    hi[ct] + lo[ct] * kLoScale + bq;
+                    (hi[ct] + lo[ct] * kLoScale) * in_inv<trunk, layer>(TID_C P, sm, qtok0 + 16 * ct + i16) + bq;
         }
         if (c == 0) pkv = hprefetch<2>(TID_C P, si, D, kv_row(wv, 1), 0);
         else po = tail_prefetch<trunk, layer, last, TR, true>(TID_C P);
@@ -911,7 +1004,7 @@ __device__ __forceinline__ void encoder_layer_split(TID_F Smem& sm, const float*
         PTR(tb + 2 + 3 * c);
         if constexpr (TR) store_qkv_chunk(TID_C sm, io.qkv, c, qtok0, b0);
         if constexpr (!in_ctx) {
-            attention_chunk<planes>(TID_C sm, c, S - 1, 1);
+            attention_chunk<planes, trunk, layer>(TID_C sm, c, S - 1, 1, P);
         } else if constexpr (last) {  // one query position: threads < 256 own one task each
             f32x4 o;
             int ti = 0, d0 = 0;
@@ -921,8 +1014,9 @@ __device__ __forceinline__ void encoder_layer_split(TID_F Smem& sm, const float*
                 ti0 = ti;
                 d00 = d0;
             } else if (TIDX() < 4 * SPW * 4) {
-                attention_out<planes>(TID_C sm, 0, ti0, d00, att0[0]);
-                attention_out<planes>(TID_C sm, 1, ti, d0, o);
+                const float asc = attn_sc<planes, trunk, layer>(P, sm, ti & 15);
+                attention_out<planes>(TID_C sm, 0, ti0, d00, att0[0], asc);
+                attention_out<planes>(TID_C sm, 1, ti, d0, o, asc);
             }
         } else {
             if (c == 0) {
@@ -930,8 +1024,9 @@ __device__ __forceinline__ void encoder_layer_split(TID_F Smem& sm, const float*
             } else {
                 f32x4 o[3];
                 attention_full_core(TID_C sm, 1, o);
-                attention_full_store<planes>(TID_C sm, 0, att0);
-                attention_full_store<planes>(TID_C sm, 1, o);
+                const float asc = attn_sc<planes, trunk, layer>(P, sm, (int)((TIDX() >> 4) & 15));
+                attention_full_store<planes>(TID_C sm, 0, att0, asc);
+                attention_full_store<planes>(TID_C sm, 1, o, asc);
             }
         }
         __syncthreads();
@@ -985,8 +1080,8 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
                     *reinterpret_cast<const f32x4*>(sm.big + tok * LDB + part * 64 + 4 * q);
             }
         }
-        if (last) attention_chunk<planes>(TID_C sm, c, S - 1, 1);
-        else attention_full<planes>(TID_C sm, c);
+        if (last) attention_chunk<planes, trunk, layer>(TID_C sm, c, S - 1, 1, P);
+        else attention_full<planes, trunk, layer>(TID_C sm, c, P);
         __syncthreads();
         PTR(tb + 3 + 3 * c);
     }
@@ -1032,7 +1127,14 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     _Float16* const cp = reinterpret_cast<_Float16*>(sm.ctx);
     f32x4 h1[CT];  // LN1's output: LN2's residual
     HPre<2> w1a;
-    if constexpr (TR) store_rows_planes(TID_C cp, io.o, D, 0, D, t0, b0, last, t1);  // attention output
+    // the operand scales (policy_layout.hpp range table): the attention output (layer 0: per sample,
+    // the lane's column i16), LN1's output, the FFN hidden units; LN2's output when it is the next
+    // layer's split operand
+    const OpSc s_ln1 = op_sc<trunk, layer, kOpLn1>(P), s_hid = op_sc<trunk, layer, kOpHid>(P);
+    const float att_inv = att_sc<trunk, layer>(P, sm.smax, LANE() & 15).inv;
+    if constexpr (TR)  // attention output
+        store_rows_planes(TID_C cp, io.o, D, 0, D, t0, b0, last, t1,
+                          [&](int tok) { return att_sc<trunk, layer>(P, sm.smax, tok & 15).inv; });
     {
         // the epilogue's bias and LN1's weight / bias ahead of the GEMM: issued after it, their L2
         // round trip (~2 k cycles with every CU reading the same lines) outlasted the partials +
@@ -1046,7 +1148,7 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
             zero(lo);
             hgemm_tile<CT, 2>(TID_C hi, lo, po, P, so, D, 16 * wv, 0, cp, t0);
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) acc[ct] = hi[ct] + lo[ct] * kLoScale;
+            for (int ct = 0; ct < CT; ++ct) acc[ct] = (hi[ct] + lo[ct] * kLoScale) * att_inv;
         }
         PTR(tb + 7);
         w1a = hprefetch<2>(TID_C P, s1, D, 16 * wv, 0);
@@ -1055,9 +1157,10 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
         const LnOut lo1{io.xhat1, PSX ? io.h1 : nullptr, io.rstd1, b0, last};
         if constexpr (res_ctx) {
             const f32x4 r4[1] = {*reinterpret_cast<const f32x4*>(sm.ctx + (LANE() & 15) * LDH + 16 * wv + 4 * (LANE() >> 4))};
-            residual_layernorm<CT, TR, true>(TID_C sm, acc, lp, t0, lo1, h1, r4);
+            residual_layernorm<CT, TR, true>(TID_C sm, acc, lp, t0, lo1, h1, r4, s_ln1.sc);
         } else {
-            residual_layernorm<CT, TR, true, false, kC0 ? 55 : -1, kC0 ? 56 : -1, kC0 ? 57 : -1>(TID_C sm, acc, lp, t0, lo1, h1);
+            residual_layernorm<CT, TR, true, false, kC0 ? 55 : -1, kC0 ? 56 : -1, kC0 ? 57 : -1>(TID_C sm, acc, lp, t0, lo1, h1,
+                                                                                            nullptr, s_ln1.sc);
         }
     }
     PTR(tb + 8);
@@ -1072,11 +1175,11 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
         zero(lo);
         hgemm_tile<CT, 2>(TID_C hi, lo, w1a, P, s1, D, 16 * wv, 0, hp, t0);
         const HPre<2> w1b = hprefetch<2>(TID_C P, s1, D, 128 + 16 * wv, 0);
-        hstore_tile<CT, true>(TID_C hi, lo, ba, bp, 16 * wv, t0);
+        hstore_tile<CT, true>(TID_C hi, lo, ba, bp, 16 * wv, t0, s_ln1.inv, s_hid.sc);
         zero(hi);
         zero(lo);
         hgemm_tile<CT, 2>(TID_C hi, lo, w1b, P, s1, D, 128 + 16 * wv, 0, hp, t0);
-        hstore_tile<CT, true>(TID_C hi, lo, bb, cp, 16 * wv, t0);
+        hstore_tile<CT, true>(TID_C hi, lo, bb, cp, 16 * wv, t0, s_ln1.inv, s_hid.sc);
     }
     const HPre<2> w2a = hprefetch<2>(TID_C P, s2, FF, 16 * wv, 0);
     PTR(tb + 10);
@@ -1084,8 +1187,8 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     PTR(tb + 11);
     const HPre<2> w2b = hprefetch<2>(TID_C P, s2, FF, 16 * wv, 128);
     if constexpr (TR) {  // FFN hidden (post-ReLU): features 0-127 from big, 128-255 from ctx
-        store_rows_planes(TID_C bp, io.u, FF, 0, D, t0, b0, last, t1);
-        store_rows_planes(TID_C cp, io.u, FF, D, D, t0, b0, last, t1);
+        store_rows_planes(TID_C bp, io.u, FF, 0, D, t0, b0, last, t1, [&](int) { return s_hid.inv; });
+        store_rows_planes(TID_C cp, io.u, FF, D, D, t0, b0, last, t1, [&](int) { return s_hid.inv; });
     }
     const LnPar lp2 = ln_load(TID_C ln_bias(TID_C b2), P + kOffs.o[layer_param(trunk, layer, N2W)],
                               P + kOffs.o[layer_param(trunk, layer, N2B)]);  // ahead of the GEMM, as LN1's
@@ -1097,10 +1200,12 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     PTR(tb + 12);
     f32x4 acc2[CT];
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) acc2[ct] = hi[ct] + lo[ct] * kLoScale;
+    for (int ct = 0; ct < CT; ++ct) acc2[ct] = (hi[ct] + lo[ct] * kLoScale) * s_hid.inv;
     pre_ln2();
+    float ln2_sc = 1.f;
+    if constexpr (next_planes) ln2_sc = op_sc<trunk, layer, kOpLn2>(P).sc;
     residual_layernorm<CT, TR, next_planes, row4, kC0 ? 23 : -1, kC0 ? 39 : -1, kC0 ? 58 : -1>(
-        TID_C sm, acc2, lp2, t0, LnOut{io.xhat2, PSX ? io.h2 : nullptr, io.rstd2, b0, last}, nullptr, h1);
+        TID_C sm, acc2, lp2, t0, LnOut{io.xhat2, PSX ? io.h2 : nullptr, io.rstd2, b0, last}, nullptr, h1, ln2_sc);
     PTR(tb + 14);
 }
 
@@ -1406,8 +1511,9 @@ __device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* 
         f32x4 lo[3] = {};
         hgemm_rows<3, 2>(TID_C acc, lo, pw, P, split_slot(layer_param(trunk, 0, INW)), D, rows,
                          reinterpret_cast<const _Float16*>(sm.ctx), (S - 1) * SPW, ring_issue);
+        const float inv = e_sc<trunk>(P, sm.tmax[(S - 1) * SPW + i16]).inv;  // the new row's scale
 #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[j] += lo[j] * kLoScale;
+        for (int j = 0; j < 3; ++j) acc[j] = (acc[j] + lo[j] * kLoScale) * inv;
     } else {
         gemm_rows<3, kPwD>(TID_C acc, pw, Win, D, rows, sm.ctx, LDH, (S - 1) * SPW, ring_issue);
     }
@@ -1447,8 +1553,8 @@ __device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* 
         __syncthreads();
         PTR(tb + 2 + 3 * c);
         if (c == 0) ppos_stage(TID_C sm, rp, 1);  // sm.red is read again only by the chunk-1 assembly
-        if (last) attention_chunk<planes>(TID_C sm, c, S - 1, 1);
-        else attention_full<planes>(TID_C sm, c);
+        if (last) attention_chunk<planes, trunk, 0>(TID_C sm, c, S - 1, 1, P);
+        else attention_full<planes, trunk, 0>(TID_C sm, c, P);
         __syncthreads();
         PTR(tb + 3 + 3 * c);
     }
@@ -1559,12 +1665,18 @@ __device__ __forceinline__ void loss_terms(const float (&o)[5], float l0, float 
     t[2] = pad ? 0.f : (vc - R) * (vc - R);
     t[3] = pad ? 0.f : -(c.lc0 * c.p0 + c.lc1 * c.p1);
 }
-// the block's sums in sample order (threads 0-3, one term each) -> fpart[blk][4]
-__device__ __forceinline__ void loss_block_sums(TID_F const float* red, float* fpart, int blk) {
+// the block's sums in sample order (threads 0-3, one term each) -> fpart[blk][4]; thread 4: the
+// block's largest value error max(|v - R|, |vc - R|) -> vpart[blk] (the critic backward's gradient
+// scale, heads_bwd)
+__device__ __forceinline__ void loss_block_sums(TID_F const float* red, float* fpart, float* vpart, int blk) {
     if (TIDX() < 4) {
         float acc = 0.f;
         for (int i = 0; i < SPW; ++i) acc += red[4 * i + TIDX()];
         fpart[blk * 4 + TIDX()] = acc;
+    } else if (TIDX() == 4 && vpart) {
+        float m = 0.f;
+        for (int i = 0; i < SPW; ++i) m = fmaxf(m, fmaxf(red[4 * i + 1], red[4 * i + 2]));
+        vpart[blk] = sqrtf(m);
     }
 }
 __device__ void loss_partials(TID_F Smem& sm, const TrainIO& io, int b0) {
@@ -1580,7 +1692,7 @@ __device__ void loss_partials(TID_F Smem& sm, const TrainIO& io, int b0) {
         loss_terms(oi, l0, l1, v, io.eps_clip, red + 4 * p);
     }
     __syncthreads();
-    loss_block_sums(TID_C red, io.fpart, b0 / SPW);
+    loss_block_sums(TID_C red, io.fpart, io.vpart, b0 / SPW);
 }
 #ifndef UAVHIP_STEPS_TU
 // Trunk split: the same partials once both trunks' workgroups have written smp[5..7].
@@ -1593,7 +1705,7 @@ __global__ __launch_bounds__(64) void k_loss_partials(const TrainIO io) {
         loss_terms(oi, o[5], o[6], o[7], io.eps_clip, red + 4 * TIDX());
     }
     __syncthreads();
-    loss_block_sums(TID_C red, io.fpart, blockIdx.x);
+    loss_block_sums(TID_C red, io.fpart, io.vpart, blockIdx.x);
 }
 #endif
 
@@ -1641,14 +1753,19 @@ __device__ __forceinline__ void gather_windows(TID_F Smem& sm, const float* __re
         for (int u = 0; u < kEl; ++u) {
             const int i = TIDX() + u * NTHR;
             {  // key padding mask (all-zero rows, the last never masked) from the registers: the 16
-               // lanes of a token row vote
+               // lanes of a token row vote; and the row's max |x_k| (layer 0's operand range)
                 static_assert(LDX == 16 && NTHR % LDX == 0, "one token row = 16 lanes");
                 const unsigned long long nz = __ballot(v[u] != 0.f);
+                const float rmax = row16_max(fabsf(v[u]));
                 if (i < TOK * LDX && (i % LDX) == 0) {
                     const int t = i / LDX, s = t / SPW, p = t - s * SPW;
                     const bool m = (s < S - 1) && ((nz >> (LANE() & 48)) & 0xFFFFull) == 0;
                     sm.mask[p * S + s] = m;
-                    if (TR && do_actor) io.mask[(size_t)(b0 + p) * S + s] = m ? 1.f : 0.f;
+                    sm.tmax[t] = rmax;
+                    if (TR && do_actor) {
+                        io.mask[(size_t)(b0 + p) * S + s] = m ? 1.f : 0.f;
+                        io.tmax[(size_t)(b0 + p) * S + s] = rmax;
+                    }
                 }
             }
             if (i >= TOK * LDX) continue;
@@ -1659,6 +1776,17 @@ __device__ __forceinline__ void gather_windows(TID_F Smem& sm, const float* __re
             float* o = io.smp + (size_t)(b0 + TIDX()) * 8;
             for (int c = 0; c < 5; ++c) o[c] = ld[c];
         }
+    }
+}
+
+// Each sample's max over its five window rows (Smem::smax, layer 0's attention-output range), from
+// Smem::tmax once the barrier after gather_windows has passed; read behind a later barrier.
+__device__ __forceinline__ void smax_from_tmax(TID_F Smem& sm) {
+    if (TIDX() < SPW) {
+        float m = sm.tmax[TIDX()];
+#pragma unroll
+        for (int s = 1; s < S; ++s) m = fmaxf(m, sm.tmax[s * SPW + TIDX()]);
+        sm.smax[TIDX()] = m;
     }
 }
 
@@ -1727,6 +1855,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     gather_windows<TR>(TID_C sm, states, B, io, b0, do_actor);
     __syncthreads();
     PTR(1);
+    smax_from_tmax(TID_C sm);  // read behind the next barrier (layer 0's attention)
     const int wv = TIDX() >> 6;
     const float* headw_a = P + kOffs.o[kActorHead];
     const float* headw_c = P + kOffs.o[kCriticHead];
@@ -2089,7 +2218,7 @@ __device__ void rows_fill_trunk(Smem& sm, const float* __restrict__ P, const Fil
             zero(lo);
             hgemm_tile<S - 1, 4>(acc, lo, pre.w[j - P0], P, si, D, row, 0, reinterpret_cast<const _Float16*>(sm.ctx), 0);
 #pragma unroll
-            for (int s = 0; s < S - 1; ++s) acc[s] += lo[s] * kLoScale;
+            for (int s = 0; s < S - 1; ++s) acc[s] = (acc[s] + lo[s] * kLoScale) * e_sc<trunk>(P, sm.tmax[s * SPW + i16]).inv;
         } else {
             gemm_tile<S - 1, KB>(acc, pre.w[j - P0], Win, D, row, 0, sm.ctx, LDH, 0);
         }
@@ -2145,7 +2274,10 @@ __global__ __launch_bounds__(NTHR) void k_policy_rows_fill(const float* __restri
         fc.ep = embed_load<kCriticTrunk>(P);
         for (int i = tid_x(); i < (S - 1) * SPW * LDX; i += NTHR) {  // positions 0-3 only
             const int t = i / LDX, k = i - t * LDX, s = t / SPW, p = t - s * SPW;
-            sm.x[i] = (k < IN && b0 + p < rio.B) ? states[((size_t)(b0 + p) * S + s) * IN + k] : 0.f;
+            const float x = (k < IN && b0 + p < rio.B) ? states[((size_t)(b0 + p) * S + s) * IN + k] : 0.f;
+            sm.x[i] = x;
+            const float rmax = row16_max(fabsf(x));  // the row's range (one 16-lane row per token)
+            if (k == 0) sm.tmax[t] = rmax;
         }
         __syncthreads();
         rows_fill_trunk<kActorTrunk>(sm, P, fa, rio, b0, [&] { fill_load_w(fc, P); });
@@ -2840,6 +2972,21 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     // leave this function gscale x the loss's, bit for bit (power-of-two scaling commutes with every
     // rounding), and stay that way through the linear backward until k_reduce_grads' 1/gscale
     const float ginv = inv * io.gscale;
+    // the critic's gradients additionally x 2^-k (k > 0 only when a value error of the minibatch
+    // reaches 16): its per-sample gradient is ~ |v - R|, which returns of configs[4]'s scale and
+    // beyond would carry past fp16's range in the split-product dX GEMMs. Every workgroup forms the
+    // same k from the forward's per-block maxima (vpart); the critic's reductions undo it
+    // (k_reduce_grads reads 2^k from gsc_out).
+    float vmx = 0.f;
+    if (tid_x() < 64) {
+        for (int i = tid_x(); i < io.nvpart; i += 64) vmx = fmaxf(vmx, io.vpart[i]);
+        vmx = wave_max(vmx);
+    }
+    int vexp = 0;
+    (void)frexpf(vmx, &vexp);
+    const int ck = vexp >= 5 && vmx < 3.0e38f ? vexp - 4 : 0;  // vmx 2^-ck in [8, 16)
+    const float ginv_c = ginv * ldexpf(1.0f, -ck);
+    if (tid_x() == 0 && blk == 0 && role != 1 && io.gsc_out) io.gsc_out[0] = ldexpf(1.0f, ck);
     // the four loss sums (used by wave 0 only): from the all-reduced buffer, or summed here from
     // the forward's workgroup partials with k_loss_sums' exact order (train.hip)
     // every global input issued before the first use: z rows (one float4 per thread), the head.2
@@ -2909,8 +3056,8 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
         const float w2 = L2 > L1 ? 1.f : (L1 == L2 ? 0.5f : 0.f);
         gs[4 * p + 0] = pad ? 0.f : c.y0 * (gy0 - dot);
         gs[4 * p + 1] = pad ? 0.f : c.y1 * (gy1 - dot);
-        gs[4 * p + 2] = pad ? 0.f : io.value_coef * (w1 * 2.f * (v - R) * ginv +
-                                         ((dv >= -io.eps_clip && dv <= io.eps_clip) ? w2 * 2.f * (vc - R) * ginv : 0.f));
+        gs[4 * p + 2] = pad ? 0.f : io.value_coef * (w1 * 2.f * (v - R) * ginv_c +
+                                         ((dv >= -io.eps_clip && dv <= io.eps_clip) ? w2 * 2.f * (vc - R) * ginv_c : 0.f));
         if (p == 0 && blk == 0 && role != 2 && io.stats) {
             io.stats[0] += (double)(-tot0 * inv);
             io.stats[1] += (double)fmaxf(L1, L2);
@@ -3074,6 +3221,7 @@ __device__ __forceinline__ void ps_rows_in(float* dst, int lds, const float* __r
 // The embedding's global operands (ps_embed_load: issued by k_ps_f1 before the window gather).
 struct PsEmbPre {
     f32x4 a, bb, pp;
+    float ea, ec;  // the layer-0 input's range constants (e_sc_v)
 };
 __device__ __forceinline__ PsEmbPre ps_embed_load(const float* __restrict__ P, int trunk, int s) {
     const float* We = P + kOffs.o[trunk + EMB_W];
@@ -3086,6 +3234,8 @@ __device__ __forceinline__ PsEmbPre ps_embed_load(const float* __restrict__ P, i
     r.a.w = 4 * g + 3 < IN ? We[f * IN + 4 * g + 3] : 0.f;
     r.bb = ld4(P + kOffs.o[trunk + EMB_B] + 16 * wv + 4 * g);
     r.pp = ld4(P + kOffs.o[trunk + POS] + s * D + 16 * wv + 4 * g);
+    r.ea = P[kRangeOff + kRgE + 2 * trunk_index(trunk)];
+    r.ec = P[kRangeOff + kRgE + 2 * trunk_index(trunk) + 1];
     return r;
 }
 template <bool PL = false>  // PL: also the planes of h into sm.ctx (ps_inproj_split's operand)
@@ -3101,7 +3251,9 @@ __device__ void ps_embed(Smem& sm, const PsEmbPre& ep, float* __restrict__ e_out
     e.x = fmaxf(e.x, 0.f); e.y = fmaxf(e.y, 0.f); e.z = fmaxf(e.z, 0.f); e.w = fmaxf(e.w, 0.f);
     const f32x4 v = e + pp;
     st4(sm.h + (s * SPW + i16) * LDH + 16 * wv + 4 * g, v);
-    if constexpr (PL) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((s * SPW + i16), 16 * wv + 4 * g), v);
+    if constexpr (PL)  // scaled per token (its window row's range)
+        hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((s * SPW + i16), 16 * wv + 4 * g),
+                     v * e_sc_v(ep.ea, ep.ec, sm.tmax[s * SPW + i16]).sc);
     const size_t r = (size_t)trow(s * SPW + i16, b0);
     st4(e_out + r * D + 16 * wv + 4 * g, e);
     st4(h_out + r * D + 16 * wv + 4 * g, v);
@@ -3143,8 +3295,9 @@ __device__ __forceinline__ void ps_inproj_load(PsInPre& r, const float* __restri
         r.bb[k] = ld4(bias + row + 4 * g);
     }
 }
+// inv: 2^s of the operand at this lane's token (the caller's: layer 0 per token, layer 1 static)
 __device__ void ps_inproj_split(const PsInPre& pre, const float* __restrict__ P, int soff, float* __restrict__ qkv,
-                                int tile0, int s, int b0, const _Float16* X) {
+                                int tile0, int s, int b0, const _Float16* X, float inv) {
     const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
     const size_t r = (size_t)trow(s * SPW + i16, b0);
 #pragma unroll
@@ -3156,7 +3309,7 @@ __device__ void ps_inproj_split(const PsInPre& pre, const float* __restrict__ P,
         zero(hi);
         zero(lo);
         hgemm_tile<1, 4>(hi, lo, pre.w[k], P, soff, D, row, 0, X, s * SPW);
-        st4(qkv + r * 3 * D + row + 4 * g, hi[0] + lo[0] * kLoScale + pre.bb[k]);
+        st4(qkv + r * 3 * D + row + 4 * g, (hi[0] + lo[0] * kLoScale) * inv + pre.bb[k]);
     }
 }
 static_assert(NW * kPsInTiles == 3 * D / 16, "ps_inproj_load covers every in_proj row tile");
@@ -3198,18 +3351,20 @@ __device__ __forceinline__ void ps_qkv_store(Smem& sm, const QkvPre& r, int s) {
     }
 }
 // the attention of both chunks (K7 F2 / F3): chunk 1's Q | K | V loads overlap chunk 0's attention
-template <bool PLANES>
-__device__ __forceinline__ void ps_attention(Smem& sm, const float* __restrict__ qkv, int s, int b0) {
+// (PLANES: the output's planes scaled for layer `layer` of trunk `trunk`, P's range table)
+template <bool PLANES, int trunk, int layer>
+__device__ __forceinline__ void ps_attention(Smem& sm, const float* __restrict__ qkv, int s, int b0,
+                                             const float* __restrict__ P) {
     QkvPre r;
     ps_qkv_load(r, qkv, 0, s, b0);
     ps_qkv_store(sm, r, s);
     __syncthreads();
     ps_qkv_load(r, qkv, 1, s, b0);
-    attention_chunk<PLANES>(sm, 0, s, 1);
+    attention_chunk<PLANES, trunk, layer>(sm, 0, s, 1, P);
     __syncthreads();
     ps_qkv_store(sm, r, s);
     __syncthreads();
-    attention_chunk<PLANES>(sm, 1, s, 1);
+    attention_chunk<PLANES, trunk, layer>(sm, 1, s, 1, P);
     __syncthreads();
 }
 
@@ -3232,7 +3387,9 @@ __global__ __launch_bounds__(NTHR) void k_ps_f1(const float* __restrict__ P, con
     ps_embed<kPsSplit>(sm, ep, io.e[critic ? 1 : 0], io.h0[critic ? 1 : 0], b0, s);
     __syncthreads();
     if constexpr (kPsSplit) {
-        ps_inproj_split(wp, P, soff, io.L[critic ? 1 : 0].qkv, tile0, s, b0, reinterpret_cast<const _Float16*>(sm.ctx));
+        const float m = sm.tmax[s * SPW + (lane_id() & 15)];
+        ps_inproj_split(wp, P, soff, io.L[critic ? 1 : 0].qkv, tile0, s, b0, reinterpret_cast<const _Float16*>(sm.ctx),
+                        critic ? e_sc<kCriticTrunk>(P, m).inv : e_sc<kActorTrunk>(P, m).inv);
     } else {
         ps_inproj(sm, P + kOffs.o[layer_param(trunk, 0, INW)], P + kOffs.o[layer_param(trunk, 0, INB)],
                   io.L[critic ? 1 : 0].qkv, critic || s == S - 1 ? 0 : D / 16, s, b0);
@@ -3251,8 +3408,14 @@ __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, con
         po = hprefetch<2>(P, critic ? split_slot(layer_param(kCriticTrunk, 0, OUTW)) : split_slot(layer_param(kActorTrunk, 0, OUTW)),
                           D, 16 * wv, 0);
     ps_mask(sm, io.mask, b0);
+    if (tid_x() < SPW) {  // each sample's window range (F1's rows), for the attention output's planes
+        float m = io.tmax[(size_t)(b0 + tid_x()) * S];
+        for (int k = 1; k < S; ++k) m = fmaxf(m, io.tmax[(size_t)(b0 + tid_x()) * S + k]);
+        sm.smax[tid_x()] = m;
+    }
     ps_rows_in(sm.h, LDH, io.h0[ti], D, 0, D, s, b0);  // the layer input (residual) of the position
-    ps_attention<kPsSplit>(sm, io.L[ti].qkv, s, b0);
+    if (critic) ps_attention<kPsSplit, kCriticTrunk, 0>(sm, io.L[ti].qkv, s, b0, P);
+    else ps_attention<kPsSplit, kActorTrunk, 0>(sm, io.L[ti].qkv, s, b0, P);
     [[maybe_unused]] APre<4> ph;
     if constexpr (kPsSplit) {  // the layer tails and the next in_proj as split products
         if (critic) {
@@ -3265,7 +3428,8 @@ __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, con
             layer_tail_split<kCriticTrunk, 0, false, true, decltype(hook), 1>(sm, P, po, io.L[1], b0, hook, s * SPW);
             __syncthreads();
             // layer 1 (pruned) of this position: K | V, and Q at position 4, from LN2's planes in sm.h
-            ps_inproj_split(wp, P, s1, io.L[2].qkv, tile0, s, b0, reinterpret_cast<const _Float16*>(sm.h));
+            ps_inproj_split(wp, P, s1, io.L[2].qkv, tile0, s, b0, reinterpret_cast<const _Float16*>(sm.h),
+                            op_sc<kCriticTrunk, 0, kOpLn2>(P).inv);
             return;
         }
         auto hook = [&] {  // the head's weights before LN2
@@ -3304,7 +3468,7 @@ __global__ __launch_bounds__(NTHR) void k_ps_f3(const float* __restrict__ P, con
     if constexpr (kPsSplit) po = hprefetch<2>(P, split_slot(layer_param(kCriticTrunk, 1, OUTW)), D, 16 * wv, 0);
     ps_mask(sm, io.mask, b0);
     ps_rows_in(sm.h, LDH, io.L[1].h2, D, 0, D, S - 1, b0);  // layer 1's input (residual) at position 4
-    ps_attention<kPsSplit>(sm, io.L[2].qkv, S - 1, b0);
+    ps_attention<kPsSplit, kCriticTrunk, 1>(sm, io.L[2].qkv, S - 1, b0, P);
     APre<4> ph;
     if constexpr (kPsSplit) {  // the residual is in sm.h (ps_rows_in): PSX = 2
         auto hook = [&] {  // the head's weights before LN2
@@ -3678,10 +3842,45 @@ __global__ __launch_bounds__(256) void k_policy_split(const float* __restrict__ 
     dst[64] = w2;
 }
 
+// The range table (policy_layout.hpp) of the flat parameters: block q writes max |param q|; the
+// last block to finish (a ticket counter in the table: policy_split zeroes it with a memset first,
+// and the last block -- here and in k_adam, which refreshes the table after every update -- resets
+// it) derives the operand scales from all of them.
+__global__ __launch_bounds__(256) void k_policy_range(const float* __restrict__ flat, float* __restrict__ packed) {
+    __shared__ float red[4];
+    __shared__ int last;
+    const int q = blockIdx.x;
+    float m = 0.f;
+    for (int i = tid_x(); i < kSizes[q]; i += 256) m = fmaxf(m, fabsf(flat[kOffs.o[q] + i]));
+    m = wave_max(m);
+    if (lane_id() == 0) red[tid_x() >> 6] = m;
+    __syncthreads();
+    float* tab = packed + kRangeOff;
+    if (tid_x() == 0) {
+        tab[kRgMax + q] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        __threadfence();
+        last = atomicAdd(reinterpret_cast<unsigned*>(tab + kRgTicket), 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last || tid_x() != 0) return;
+    __threadfence();
+    float t[kRangeFloats] = {};
+    for (int k = 0; k < kNumParams; ++k) t[kRgMax + k] = tab[kRgMax + k];
+    range_derive(t);
+    for (int k = kNumParams; k < kRgTicket; ++k) tab[k] = t[k];
+    *reinterpret_cast<unsigned*>(tab + kRgTicket) = 0u;  // ready for the next pack
+}
+
 int policy_split(const float* flat, float* packed, hipStream_t st) {
-    constexpr int n = (kPackedFloats - kOffs.o[kNumParams]) / 8;
+    constexpr int n = (kRangeOff - kOffs.o[kNumParams]) / 8;
     hipLaunchKernelGGL(k_policy_split, dim3((n + 255) / 256), dim3(256), 0, st, flat, packed);
-    return check_launch("k_policy_split");
+    if (const int rc = check_launch("k_policy_split")) return rc;
+    if (hipMemsetAsync(packed + kRangeOff + kRgTicket, 0, sizeof(unsigned), st) != hipSuccess) {
+        set_error("policy_split: hipMemsetAsync of the range ticket failed");
+        return UAVHIP_EHIP;
+    }
+    hipLaunchKernelGGL(k_policy_range, dim3(kNumParams), dim3(256), 0, st, flat, packed);
+    return check_launch("k_policy_range");
 }
 
 // flat -> the split copies of the three layers' transposed weights (packedT + kTSplit): one thread
@@ -3746,6 +3945,15 @@ extern "C" int32_t uavhip_policy_split_layout(int32_t* params, int32_t* offsets,
         if (offsets) offsets[i] = pol::kSplitOffs.o[i];
     }
     return pol::kPackedFloats;
+}
+
+extern "C" int32_t uavhip_policy_range_table(const float* max_abs, float* table) {
+    if (!max_abs || !table) return pol::kRangeFloats;
+    float t[pol::kRangeFloats] = {};
+    for (int q = 0; q < pol::kNumParams; ++q) t[pol::kRgMax + q] = max_abs[q];
+    pol::range_derive(t);
+    for (int k = 0; k < pol::kRangeFloats; ++k) table[k] = t[k];
+    return pol::kRangeFloats;
 }
 
 extern "C" int32_t uavhip_policy_tiling(int32_t* kcols, int32_t max_params) {

@@ -70,11 +70,94 @@ constexpr SplitOffs make_split_offs() {
     return r;
 }
 constexpr SplitOffs kSplitOffs = make_split_offs();
-constexpr int kPackedFloats = kSplitOffs.o[kNumSplit];  // the inference forward's packed buffer
 constexpr int split_slot(int q) {
     for (int i = 0; i < kNumSplit; ++i)
         if (kSplitParam[i] == q) return kSplitOffs.o[i];
     return -1;
+}
+
+// ---- range table (DESIGN.md 4a "range"): after the split copies. The split products carry each
+// activation operand as fp16 planes, exact to 2^-22 only for |x| in [2^-14, 65504], so every operand
+// is multiplied by a power of two 2^-s before it is split and the consuming GEMM's output by 2^s
+// (exact both ways: Y^T = W (2^-s X)^T 2^s). s comes from a rigorous bound B on the operand's
+// magnitude: s = 0 while B is in [2^-4, 2^15) (every realistic weight set: the results are bitwise
+// those without scaling), else B 2^-s lands in [2^14, 2^15), so no scaled value reaches fp16's
+// overflow and the largest ones keep all 22 bits. The bounds (transformer_net.py's post-LN layers):
+//   LayerNorm output  |x^ g + b| <= sqrt(D - 1) max|g| + max|b|            (|x^| <= sqrt(127))
+//   FFN hidden        relu(W1 h + b1) <= D max|W1| B(h) + max|b1|
+//   attention output  convex combination of V rows: <= D max|W_in| B(input) + max|b_in|
+//   layer-0 input     e (+ pos) <= 14 max|W_e| max_k|x_k| + max|b_e| + max|pos| -- per token, from
+//                     that token's window row (the kernels keep max_k|x_k| of every token in LDS)
+// so the table holds max|param| of every parameter (kept current by k_policy_range after a pack and
+// by k_adam after every update), the per-token constants of layer 0, and the (2^-s, 2^s) pairs of
+// the operands whose bound depends on the weights alone.
+constexpr int kRangeOff = kSplitOffs.o[kNumSplit];
+constexpr int kRangeFloats = 96;
+constexpr int kPackedFloats = kRangeOff + kRangeFloats;  // the inference forward's packed buffer
+enum : int {
+    kRgMax = 0,     // [q]: max |param q|, q < kNumParams
+    kRgE = 52,      // + 2 t: 14 max|W_e|, + 2 t + 1: max|b_e| + max|pos| (trunk index t: 0 actor, 1 critic)
+    kRgA0 = 56,     // + 2 t: D max|W_in(layer 0)|, + 2 t + 1: max|b_in(layer 0)|
+    kRgOp = 64,     // + 2 op: 2^-s, + 2 op + 1: 2^s of static operand op
+    kRgTicket = 92  // k_policy_range / k_adam: the last-arriving block's counter (uint32 bits)
+};
+enum : int { kOpLn1 = 0, kOpHid = 1, kOpLn2 = 2, kOpAtt = 3 };  // static operand kinds
+// static operand slot of (trunk, layer, kind): actor L0 {LN1, HID}; critic L0 {LN1, HID, LN2};
+// critic L1 {ATT, LN1, HID}; -1: not a static operand (layer 0's attention output, layer-0 input)
+__host__ __device__ constexpr int range_op(int trunk, int layer, int kind) {
+    return trunk == kActorTrunk ? (layer == 0 && kind <= kOpHid ? kind : -1)
+           : layer == 0         ? (kind <= kOpLn2 ? 2 + kind : -1)
+           : layer == 1         ? (kind == kOpAtt ? 5 : kind <= kOpHid ? 6 + kind : -1)
+                                : -1;
+}
+constexpr int kNumRangeOps = 8;
+static_assert(kRgOp + 2 * kNumRangeOps <= kRgTicket && kRgTicket < kRangeFloats && kNumParams <= kRgE, "range table");
+__host__ __device__ constexpr int trunk_index(int trunk) { return trunk == kActorTrunk ? 0 : 1; }
+
+// The scale exponent of an operand bounded by B: 0 for B in [2^-4, 2^15) (and for 0, inf, NaN: a
+// non-finite operand stays non-finite), else B 2^-s in [2^14, 2^15). frexp: B = f 2^e, f in [0.5, 1).
+__host__ __device__ inline int range_exp(float B) {
+    if (!(B > 0.f) || !(B < 3.0e38f)) return 0;
+    int e = 0;
+    (void)frexpf(B, &e);
+    if (e >= -3 && e <= 15) return 0;
+    const int s = e - 15;
+    return s < -100 ? -100 : (s > 100 ? 100 : s);
+}
+// table[kRgMax + q] (max|param q|) -> every derived entry. Host (uavhip_policy_range_table) and
+// device (k_policy_range, k_adam) evaluate the same fp32 operations without contraction: bitwise
+// the same table.
+__host__ __device__ inline void range_derive(float* t) {
+#pragma clang fp contract(off)
+    const float* M = t + kRgMax;
+    constexpr float kLnMax = 11.5f;  // >= sqrt(D - 1): the largest |x^| of a D-feature LayerNorm
+    const int trunks[2] = {kActorTrunk, kCriticTrunk};
+    for (int ti = 0; ti < 2; ++ti) {
+        const int tr = trunks[ti];
+        t[kRgE + 2 * ti] = (float)IN * M[tr + EMB_W];
+        t[kRgE + 2 * ti + 1] = M[tr + EMB_B] + M[tr + POS];
+        t[kRgA0 + 2 * ti] = (float)D * M[layer_param(tr, 0, INW)];
+        t[kRgA0 + 2 * ti + 1] = M[layer_param(tr, 0, INB)];
+    }
+    auto put = [&](int op, float B) {
+        const int s = range_exp(B);
+        t[kRgOp + 2 * op] = ldexpf(1.0f, -s);
+        t[kRgOp + 2 * op + 1] = ldexpf(1.0f, s);
+    };
+    for (int ti = 0; ti < 2; ++ti) {
+        const int tr = trunks[ti];
+        const int nl = tr == kActorTrunk ? 1 : 2;
+        float ln2_prev = 0.f;
+        for (int l = 0; l < nl; ++l) {
+            if (l > 0) put(range_op(tr, l, kOpAtt), (float)D * M[layer_param(tr, l, INW)] * ln2_prev +
+                                                         M[layer_param(tr, l, INB)]);
+            const float ln1 = kLnMax * M[layer_param(tr, l, N1W)] + M[layer_param(tr, l, N1B)];
+            put(range_op(tr, l, kOpLn1), ln1);
+            put(range_op(tr, l, kOpHid), (float)D * M[layer_param(tr, l, L1W)] * ln1 + M[layer_param(tr, l, L1B)]);
+            ln2_prev = kLnMax * M[layer_param(tr, l, N2W)] + M[layer_param(tr, l, N2B)];
+            if (range_op(tr, l, kOpLn2) >= 0) put(range_op(tr, l, kOpLn2), ln2_prev);
+        }
+    }
 }
 
 }  // namespace pol

@@ -22,11 +22,13 @@ struct TrainIO {
     float* smp;                  // [Bm][8]: action, old_logp, old_value, return, advantage
     float* xg;                   // [R][16]
     float* mask;                 // [R]
+    float* tmax;                 // [R] max |x_k| of each window row (layer 0's operand range; K7 F2 reads it)
     float *e[2], *h0[2];         // [R][128] actor, critic embeddings (post-ReLU) and layer inputs
     TrainLayerIO L[3];           // actor L0 (pruned), critic L0 (full), critic L1 (pruned)
     float* z[2];                 // [Bm][64] relu(head.0) of the actor / critic head
     float* fpart;                // [Bm/16][4] per-workgroup loss partials: sum min(s1, s2),
                                  // sum (v-R)^2, sum (vc-R)^2, sum entropy (smp[5..7] = logits, value)
+    float* vpart;                // [Bm/16] per-workgroup max(|v - R|, |vc - R|) (BwdIO::vpart)
     float eps_clip;
     // trunk split (small minibatches, 2 Bm/16 <= the CU count): workgroups [0, split) run the
     // actor trunk + head, [split, 2 split) the critic trunk + head of the same 16-sample blocks
@@ -75,6 +77,12 @@ struct BwdIO {
     // the dX GEMMs' fp16 operand planes stay above the fp16 subnormal range (x2 = f16((x - x1) 2^11)
     // loses relative accuracy below 2^-14); k_reduce_grads multiplies by 1/gscale (exact)
     float gscale;
+    // the critic's gradients carry gscale x 2^-k, k from the minibatch's largest value error (the
+    // forward's per-block maxima vpart[nvpart]; heads_bwd), and workgroup 0 writes 2^k to gsc_out
+    // for the reductions (k_reduce_grads: critic segments x 2^k / gscale). k = 0 below |v - R| = 16.
+    const float* vpart;
+    int nvpart;
+    float* gsc_out;
     const float* xg;         // [R][16] input windows (TrainIO::xg)
     const float* mask;       // [R] key padding mask
     const float* e[2];       // [R][128] embeddings after ReLU

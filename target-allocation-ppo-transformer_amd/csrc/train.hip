@@ -58,6 +58,17 @@ __device__ __forceinline__ float quad_sum(float v) { return add_xor2(add_xor1(v)
 __device__ __forceinline__ float wave_sum(float v) {
     return add_xor32(add_xor16(add_ror8(add_ror4(add_xor2(add_xor1(v))))));
 }
+template <int ctrl>
+__device__ __forceinline__ float dpp_max(float v) {
+    return fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xF, 0xF, true)));
+}
+__device__ __forceinline__ float wave_max(float v) {  // the same value in every lane
+    v = dpp_max<0x128>(dpp_max<0x124>(dpp_max<0x4E>(dpp_max<0xB1>(v))));
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
 
 // ================================================================== heads + loss
 // 16 samples per 1024-thread block (one wave per sample). Head weights staged in LDS with a
@@ -116,11 +127,12 @@ struct SegBatch {
     int n;
 };
 // unscale = 1 / BwdIO::gscale (a power of two: exact): the backward's partials carry the pre-scaled
-// gradient, the flat buffer the loss's.
+// gradient, the flat buffer the loss's. The critic's segments (destinations from crit_off on: the
+// critic trunk and head) carry gscale x 2^-k (heads_bwd): x gsc[0] = 2^k as well.
 __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* __restrict__ grads,
                                                       float* __restrict__ sq_part, double* __restrict__ step,
                                                       const AdamHyper h, AdamScalars* __restrict__ sc,
-                                                      const float unscale) {
+                                                      float unscale, const float* __restrict__ gsc, int crit_off) {
     __shared__ float red[4];
     __shared__ float wsum[4][64];
     // segment of this block: lane l tests segment l (one round of kernarg loads, not a dependent
@@ -130,6 +142,7 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
     const bool begun = sl < sb.n && (int)blockIdx.x >= sb.s[sl].block_begin;
     const int si = __popcll(__ballot(begun)) - 1;
     const Segment S_ = sb.s[si];  // by value: one batch of scalar loads, not one per field use
+    if (S_.dst >= crit_off) unscale *= gsc[0];
     const size_t ps = S_.part_stride;
     auto part = [&](int p) { return p == 0 ? S_.src : S_.src_rest + (size_t)(p - 1) * ps; };
     auto dsti = [&](int i) { return S_.dst + (S_.dst_ld ? (i >> 7) * S_.dst_ld + (i & 127) : i); };
@@ -295,6 +308,7 @@ struct AdamArgs {
     double beta1, beta2, eps;
     float max_norm;
     float *packed, *packedT;  // nullable: refreshed with the updated params
+    float* amax_part;         // [kAdamBlocks.n] per-block max |updated param| (the packed range table)
 };
 
 __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
@@ -344,6 +358,41 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
         *reinterpret_cast<f32x4*>(a.params + f) = p;
     }
     if (!a.packed) return;
+    {   // the packed range table (policy_layout.hpp) of the updated parameters: per block the max
+        // |param|, then the last block to finish (ticket in the table) takes every parameter's max
+        // over its blocks and derives the operand scales the next forward reads
+        float am = live ? fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fmaxf(fabsf(p[2]), fabsf(p[3]))) : 0.f;
+        am = wave_max(am);
+        __shared__ float amw[4];
+        __shared__ int last;
+        if (lane_id() == 0) amw[threadIdx.x >> 6] = am;
+        __syncthreads();
+        float* tab = a.packed + kRangeOff;
+        if (threadIdx.x == 0) {
+            a.amax_part[blockIdx.x] = fmaxf(fmaxf(amw[0], amw[1]), fmaxf(amw[2], amw[3]));
+            __threadfence();
+            last = atomicAdd(reinterpret_cast<unsigned*>(tab + kRgTicket), 1u) == gridDim.x - 1;
+        }
+        __syncthreads();
+        if (last) {
+            __threadfence();
+            __shared__ float mq[kNumParams];
+            if (threadIdx.x < kNumParams) {
+                float mx = 0.f;
+                for (int b = 0; b < kAdamBlocks.n; ++b)
+                    if (kAdamBlocks.param[b] == (int)threadIdx.x) mx = fmaxf(mx, a.amax_part[b]);
+                mq[threadIdx.x] = mx;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                float t[kRangeFloats] = {};
+                for (int k = 0; k < kNumParams; ++k) t[kRgMax + k] = mq[k];
+                range_derive(t);
+                for (int k = 0; k < kRgTicket; ++k) tab[k] = t[k];
+                *reinterpret_cast<unsigned*>(tab + kRgTicket) = 0u;
+            }
+        }
+    }
     if (!NC) {  // plain parameters are copied as they are
         if (live) *reinterpret_cast<f32x4*>(a.packed + f) = p;
         return;
@@ -413,10 +462,13 @@ struct LayerBufs {  // one encoder layer (pruned: tail tensors are [Bm] rows)
 
 struct Plan {
     int Bm, R;
-    float *xg, *mask, *smp, *e_a, *h0_a, *e_c, *h0_c;
+    float *xg, *mask, *tmax, *smp, *e_a, *h0_a, *e_c, *h0_c;
     LayerBufs la, lc0, lc1;
     float *z_a, *z_c, *dz_a, *dz_c, *fpart, *hpart, *epart, *sq_part;
     AdamScalars* adam_sc;  // Adam's step-dependent scalars (k_reduce_grads / k_grad_norm -> k_adam)
+    float* amax_part;      // k_adam's per-block max |param| (the packed range table)
+    float* vpart;          // [Bm/16] the forward's per-block value-error maxima (BwdIO::vpart)
+    float* gsc;            // 2^k of the critic's gradient scale (heads_bwd -> k_reduce_grads)
     float* wg_part;  // weight-gradient partial tiles [kWgGrid * kWgRuns][kWgSlot]
     float* bpart;    // [prows][kBiasPart] bias partials of K6 / K7
     float* kvc;      // K7: [prows][80][256] each query position's share of every position's dk | dv
@@ -456,6 +508,7 @@ inline Plan make_plan(int Bm, float* base) {
     p.prows = (pol::ps_capable(Bm) ? S : 1) * (Bm / kHeadSamples);
     p.xg = w.take((size_t)R * 16);
     p.mask = w.take(R);
+    p.tmax = w.take(R);
     p.smp = w.take((size_t)Bm * 8);
     p.e_a = w.take((size_t)R * D);
     p.h0_a = w.take((size_t)R * D);
@@ -473,6 +526,9 @@ inline Plan make_plan(int Bm, float* base) {
     p.epart = w.take((size_t)p.prows * 2 * kEmbPart);
     p.sq_part = w.take(1 << 16);
     p.adam_sc = reinterpret_cast<AdamScalars*>(w.take(4));
+    p.amax_part = w.take(kAdamMaxBlocks);
+    p.vpart = w.take((size_t)(Bm / kHeadSamples));
+    p.gsc = w.take(4);
     p.wg_part = w.take((size_t)kWgGrid * kWgRuns * kWgSlot);
     p.bpart = w.take((size_t)p.prows * pol::kBiasPart);
     p.kvc = pol::ps_capable(Bm) ? w.take((size_t)p.prows * S * kHeadSamples * 2 * D) : nullptr;  // [prows][80][256]
@@ -618,6 +674,7 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
         io.smp = p.smp;
         io.xg = p.xg;
         io.mask = p.mask;
+        io.tmax = p.tmax;
         io.e[0] = p.e_a; io.e[1] = p.e_c;
         io.h0[0] = p.h0_a; io.h0[1] = p.h0_c;
         const LayerBufs* lb[3] = {&A, &C0, &C1};
@@ -627,6 +684,7 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
         io.z[0] = p.z_a;
         io.z[1] = p.z_c;
         io.fpart = p.fpart;
+        io.vpart = p.vpart;
         io.eps_clip = c->eps_clip;
         if (pos_split(Bm)) {  // K7: F1 / F2 / F3 (F3 writes the loss partials)
             TR_CHECK(pol::policy_forward_ps(p.packed, states, io, Bm, st));
@@ -652,7 +710,7 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
             TR_CHECK(check_launch("k_grad_norm"));
         }
         AdamArgs aa{c->params, c->grads, c->adam_m, c->adam_v, p.adam_sc, p.sq_part, n_sq, c->beta1, c->beta2,
-                    c->adam_eps, c->max_grad_norm, p.packed, p.packedT};
+                    c->adam_eps, c->max_grad_norm, p.packed, p.packedT, p.amax_part};
         hipLaunchKernelGGL(k_adam, dim3(kAdamBlocks.n), dim3(256), 0, st, aa);
         TR_CHECK(check_launch("k_adam"));
     }
@@ -690,6 +748,9 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         io.entropy_coef = c->entropy_coef;
         io.Bg = Bg;
         io.gscale = grad_prescale(Bg);
+        io.vpart = p.vpart;
+        io.nvpart = nblk;
+        io.gsc_out = p.gsc;
         io.xg = p.xg;
         io.mask = p.mask;
         io.e[0] = p.e_a;
@@ -785,6 +846,8 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
             wp.b.grads = c->grads;
             wp.b.sq = p.sq_part;
             wp.b.unscale = 1.0f / grad_prescale(Bg);
+            wp.b.gsc = p.gsc;
+            wp.b.crit_off = kOffs.o[kCriticTrunk];
             sq_base = wp.b.tiles;
             hipLaunchKernelGGL(k_wgrad, dim3(wp.b.tiles), dim3(kWgThreads), 0, st, wp.b);
             TR_CHECK(check_launch("k_wgrad"));
@@ -841,7 +904,8 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
     }
     // padding floats between parameters stay zero
     hipLaunchKernelGGL(k_reduce_grads, dim3(seg_blocks), dim3(256), 0, st, sb, c->grads, p.sq_part + sq_base, step,
-                       adam_hyper(c), p.adam_sc, 1.0f / grad_prescale(Bg));
+                       adam_hyper(c), p.adam_sc, 1.0f / grad_prescale(Bg), static_cast<const float*>(p.gsc),
+                       kOffs.o[kCriticTrunk]);
     *n_sq = sq_base + seg_blocks;
     return check_launch("k_reduce_grads");
 }

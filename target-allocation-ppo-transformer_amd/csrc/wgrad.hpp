@@ -73,6 +73,8 @@ struct WgBatch {
     float* grads;
     float* sq;
     float unscale;
+    const float* gsc;  // the critic's extra 2^k (heads_bwd): problems with dst >= crit_off
+    int crit_off;
 };
 constexpr int kWgDirectMaxSlabs = 12;  // direct mode only when no tile has more slabs (K <= 384 rows)
 
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
 #pragma unroll
                 for (int b = 0; b < 2; ++b) {
                     const f32x4 v = (hi[a][b] + (mid[a][b] + lo[a][b] * (1.0f / 2048.0f)) * (1.0f / 2048.0f)) *
-                                    wb.unscale;
+                                    (P.dst >= wb.crit_off ? wb.unscale * wb.gsc[0] : wb.unscale);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int row = m0 + 16 * (mt0 + a) + 4 * g + r;

@@ -88,6 +88,7 @@ _SIGS = {
     "uavhip_policy_layout": (_i32, [ctypes.POINTER(_i32), _i32]),
     "uavhip_policy_split_layout": (_i32, [_vp, _vp, _i32]),
     "uavhip_policy_tiling": (_i32, [ctypes.POINTER(_i32), _i32]),
+    "uavhip_policy_range_table": (_i32, [_vp, _vp]),
     "uavhip_policy_pack": (ctypes.c_int, [_vp, _vp, _vp]),
     "uavhip_policy_forward": (ctypes.c_int, [ctypes.POINTER(PolicyDesc), _vp, _i32, _vp, ctypes.c_uint64,
                                              ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -122,7 +123,7 @@ class UavHipError(RuntimeError):
     pass
 
 
-ABI_VERSION = 4  # include/uavhip.h uavhip_abi_version
+ABI_VERSION = 5  # include/uavhip.h uavhip_abi_version
 
 
 def _load():

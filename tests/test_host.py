@@ -43,7 +43,7 @@ def test_library_exports_every_header_symbol():
     for f in fns:
         assert hasattr(_lib.LIB, f), f
     assert set(fns) == set(_lib.EXPORTS)
-    assert _lib.LIB.uavhip_abi_version() == _lib.ABI_VERSION == 4
+    assert _lib.LIB.uavhip_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_ctypes_mirrors_header_enums():
@@ -219,7 +219,9 @@ def test_split_copies_encode_the_weights():
     from uavhip.policy import TransformerActorCritic, layout, pack_weights, split_layout
     _, n = layout()
     splits, total = split_layout()
-    assert splits and total == n + sum(list(TransformerActorCritic().state_dict().values())[q].numel() for q, _ in splits)
+    from uavhip.policy import RANGE_FLOATS
+    assert splits and total == n + sum(list(TransformerActorCritic().state_dict().values())[q].numel()
+                                       for q, _ in splits) + RANGE_FLOATS
     torch.manual_seed(3)
     sd = TransformerActorCritic().state_dict()
     buf = pack_weights(sd)
@@ -299,3 +301,47 @@ def test_rollout_step_argument_checks_without_gpu():
         setattr(d, name, 16)  # non-NULL placeholders: validation never dereferences them
     assert _lib.LIB.uavhip_rollout_step(pol, d, *args) == -1
     assert b"uavhip_rollout_step" in _lib.LIB.uavhip_last_error()  # NULL weights / states
+
+
+def test_range_table_scales():
+    """The packed buffer's closing range table (include/uavhip.h uavhip_policy_range_table,
+    policy_layout.hpp): the max |param| of every tensor, the layer-0 constants, and for every static
+    split-product operand a pair (2^-s, 2^s) -- (1, 1) for the reference's initial weights (results
+    bitwise those without scaling), and a power of two putting the operand's bound in [2^14, 2^15)
+    when the weights drive it out of [2^-4, 2^15). Each bound holds: the LayerNorm and FFN-hidden
+    activations of a torch forward on random windows stay below the bound the table was made from."""
+    import numpy as np
+    from uavhip.policy import RANGE_FLOATS, TransformerActorCritic, range_table
+    torch.manual_seed(4)
+    net = TransformerActorCritic()
+    sd = list(net.state_dict().values())
+    t = range_table(sd).numpy()
+    assert t.shape == (RANGE_FLOATS,)
+    np.testing.assert_array_equal(t[:50], np.array([float(p.abs().max()) for p in sd], np.float32))
+    ops = t[64:80].reshape(8, 2)
+    np.testing.assert_array_equal(ops, np.ones((8, 2), np.float32))  # realistic weights: unscaled
+    # the critic's layer-0 FFN1 x 1e5: its hidden bound ~1e7 -> s = 9..10; LN1 x 1e-6 -> s < 0
+    c0 = net.critic_net.transformer.layers[0]
+    with torch.no_grad():
+        c0.linear1.weight.mul_(1e5)
+        c0.norm1.weight.mul_(1e-6)
+        c0.norm1.bias.mul_(1e-6)
+    sd = list(net.state_dict().values())
+    t = range_table(sd).numpy()
+    ln1 = 11.5 * float(c0.norm1.weight.abs().max()) + float(c0.norm1.bias.abs().max())
+    hid = 128 * float(c0.linear1.weight.abs().max()) * ln1 + float(c0.linear1.bias.abs().max())
+    assert not 2 ** -4 <= ln1 < 2 ** 15  # LN1's output is driven out of the unscaled band
+    for op, bound in ((2, ln1), (3, hid)):  # critic layer 0: LN1, HID (policy_layout.hpp range_op)
+        sc, inv = t[64 + 2 * op], t[65 + 2 * op]
+        assert sc * inv == 1.0 and np.log2(inv) == round(np.log2(inv))
+        if 2 ** -4 <= bound < 2 ** 15:
+            assert sc == 1.0, (op, bound, sc)
+        else:
+            assert 2 ** 14 <= bound * sc < 2 ** 15, (op, bound, sc)
+    # the bounds are bounds: a forward on random windows never exceeds them
+    acts = {}
+    c0.norm1.register_forward_hook(lambda m, i, o: acts.__setitem__("ln1", float(o.abs().max())))
+    c0.linear1.register_forward_hook(lambda m, i, o: acts.__setitem__("hid", float(o.relu().abs().max())))
+    with torch.no_grad():
+        net.evaluate(torch.randn(64, 5, 14) * 3, torch.zeros(64, dtype=torch.long))
+    assert acts["ln1"] <= ln1 and acts["hid"] <= hid, (acts, ln1, hid)
