@@ -22,6 +22,7 @@ for r in range(rounds):
         if b != "base":
             env["UAVHIP_LIB"] = os.path.join(ROOT, "scripts", b, "libuavhip.so")
         out = subprocess.run([sys.executable, "bench.py", "--no-ppo", "--no-env-fused", "--no-cpu-baseline", "--no-env-diff",
+                              "--no-dropin", "--no-e2e",
                               "--steps", "20", "--warmup", "3", *extra], cwd=ROOT, env=env, capture_output=True,
                              text=True, timeout=300)
         if out.returncode != 0:

@@ -125,6 +125,7 @@ struct Smem {
     int mask[SPW * S];          // key padding mask (transformer_net.py:52-54)
     float tmax[TOK];            // max_k |x_k| of each token's window row (layer 0's operand range)
     float smax[SPW];            // max over a sample's five tokens (its layer-0 attention output's range)
+    int selp[SPW];              // k_rollout_steps: each env's active scene buffer after its last step
 };
 
 // Lane index plumbing. In the multi-step rollout TU (rollout_steps.hip) every forward helper takes
@@ -1798,7 +1799,18 @@ struct EnvOut {
     double* rew;    // [E]
     uint8_t* done;  // [E]
     double* info;   // [E][UAVHIP_INFO_COUNT] (nullable)
+    // k_rollout_steps: not the launch's last step (env.window is not written: the next window is the
+    // trajectory's, the next step's policy input); 0 in single-step launches
+    int not_last;
 };
+// The multi-step launch (the steps TU) knows each env's scene buffer from its previous step
+// (Smem::selp, set at kernel start from istate) and takes the env's window from the policy's input
+// rows in sm.x, so its env step reads one scene buffer and no env.window (envgrp::gload_issue)
+#ifdef UAVHIP_STEPS_TU
+constexpr bool kStepsEnv = true;
+#else
+constexpr bool kStepsEnv = false;
+#endif
 
 // ROWS: layer 0 of both trunks on the window-row projection ring (inference only).
 // ENV: the env step of the sampled actions follows (needs ROWS; envs b0 .. b0 + 15): a bit mask of
@@ -1956,8 +1968,9 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
         // the env step's state loads land while the critic head runs
         if constexpr ((ENV & kEnvGrp) && !kExpNoEnv) {
             if (env_grp) {
-                const int le = tid_env() & 63;
-                envgrp::gload_issue(gR, gq, env, b0 + 2 * (int)(tid_env() >> 6) + (le >> 5), le & 31);
+                const int le = tid_env() & 63, pe = 2 * (int)(tid_env() >> 6) + (le >> 5);
+                envgrp::gload_issue(gR, gq, env, b0 + pe, le & 31, kStepsEnv ? sm.selp[pe] : -1,
+                                    kStepsEnv ? sm.x + pe * LDX : nullptr);
             }
         }
         if (!TR && wv < 4) ph = prefetch<4>(TID_C headw_c, D, 16 * wv, 0);
@@ -2049,7 +2062,8 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
                           eo.rew + e, eo.done + e, eo.info ? eo.info + (size_t)e * UAVHIP_INFO_COUNT : nullptr);
             PTR(62);
             if constexpr (UAVHIP_EXP == 42) envgrp::gstore_regs(R, env, e, j);  // timing build: every entry
-            else envgrp::gstore_delta(R, env, e, j);  // only the entries the step changed
+            else envgrp::gstore_delta(R, env, e, j, !eo.not_last);  // only the entries the step changed
+            if (j == 0) sm.selp[2 * wve + g] = R.sel;  // the next step of this launch reads one scene buffer
             PTR(63);
         }
         if constexpr ((ENV & kEnvWave) != 0) if (!env_grp && e0 < B) {
@@ -2126,6 +2140,11 @@ __global__ __launch_bounds__(NTHR) void k_rollout_steps(const StepsArgs args) {
     __shared__ __attribute__((aligned(16))) Smem sm;
     if (threadIdx.x >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
     if (threadIdx.x == 0) g_tid_zero = 0;
+    if (threadIdx.x < SPW) {  // each env's active scene buffer (envgrp::gload_issue's prediction)
+        const int e = blockIdx.x * SPW + threadIdx.x;
+        sm.selp[threadIdx.x] = e < args.B && args.env.scene_buffers == 2
+                                   ? args.env.istate[(size_t)e * UAVHIP_IST_COUNT + UAVHIP_IST_SCENE_SEL] & 1 : 0;
+    }
     for (int t = 0; t < args.seq.n; ++t) {
         __syncthreads();  // g_tid_zero; the previous step's LDS scratch and global stores
         // Every argument is read through a kernarg pointer laundered per step, so the loads sit where
@@ -2141,7 +2160,7 @@ __global__ __launch_bounds__(NTHR) void k_rollout_steps(const StepsArgs args) {
         const size_t o = (size_t)t * a.B;
         const RowIO r{a.rio.rp, a.rio.B, a.rio.g + t};
         const EnvOut e{a.eo.auto_reset, a.eo.obs + t * a.seq.obs_stride, a.eo.rew + o, a.eo.done + o,
-                       a.eo.info ? a.eo.info + o * UAVHIP_INFO_COUNT : nullptr};
+                       a.eo.info ? a.eo.info + o * UAVHIP_INFO_COUNT : nullptr, t < a.seq.n - 1};
         policy_block<false, true, ENVP>(tid, sm, a.P, a.states + t * a.seq.obs_stride, a.B, nullptr, a.seed,
                                         a.offset + t * a.seq.off_stride, a.offset_dev, a.action_out + o, a.logp_out + o,
                                         a.value_out + o, nullptr, nullptr, TrainIO{}, r, a.env, e, bx);

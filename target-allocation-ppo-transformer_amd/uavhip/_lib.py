@@ -137,7 +137,10 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.uavhip_abi_version() != ABI_VERSION:  # a stale build would misread the descriptors
+    # a stale build would misread the descriptors; an A/B timing build (UAVHIP_LIB) of the previous
+    # ABI (4: no range table, peers by ordinal) is accepted for scripts/ab_rollout.py's rollout legs
+    ok = (ABI_VERSION, ABI_VERSION - 1) if os.environ.get("UAVHIP_LIB") else (ABI_VERSION,)
+    if lib.uavhip_abi_version() not in ok:
         raise ImportError(f"{LIB_PATH}: ABI version {lib.uavhip_abi_version()}, this binding needs {ABI_VERSION}: "
                           f"rebuild (make -C target-allocation-ppo-transformer_amd/csrc)")
     return lib

@@ -366,11 +366,13 @@ def pack_weights(state_dict, device=None):
     for q, o in splits:  # the split copies of the f16-matrix-core GEMM weights
         flat = to_split_fragment_order(items[q][1].detach().to(device=dev, dtype=torch.float32))
         buf[o:o + flat.numel()] = flat
-    buf[total - RANGE_FLOATS:] = range_table([v for _, v in items]).to(dev)
+    if RANGE_FLOATS:
+        buf[total - RANGE_FLOATS:] = range_table([v for _, v in items]).to(dev)
     return buf
 
 
-RANGE_FLOATS = int(LIB.uavhip_policy_range_table(None, None))
+# (0 only for an A/B timing build of the previous ABI, which has no range table: _lib)
+RANGE_FLOATS = int(LIB.uavhip_policy_range_table(None, None)) if hasattr(LIB, "uavhip_policy_range_table") else 0
 
 
 def range_table(params):
