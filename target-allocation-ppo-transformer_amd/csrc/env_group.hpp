@@ -219,28 +219,19 @@ struct GPending {
     double valb[2], ucb[2], ppb[2];
     int isv;
     double dsv;
-    int pred;  // the scene buffer valb[0] etc. were read from (-1: both buffers, valb[b] from buffer b)
 };
 __device__ __forceinline__ int grl_i(int v, int jj) {
     const int a = __builtin_amdgcn_readlane(v, jj), b = __builtin_amdgcn_readlane(v, L + jj);
     return gbase() ? b : a;
 }
-// The multi-step rollout launch (k_rollout_steps) passes, from its second step on, pred = the scene
-// buffer this env's previous step left active (Smem::selp: only the env step itself flips it), so
-// one buffer's scene values are read instead of both; a mismatch (never inside a launch) reloads
-// in gload_finish. xwin (nullable): this env's window rows in LDS -- the policy's input window, the
-// same values as env.window -- read instead of env.window.
-__device__ __forceinline__ void gload_issue(GRegs& R, GPending& q, const uavhip_env& env, int e, int j, int pred = -1,
-                                            const float* xwin = nullptr) {
+__device__ __forceinline__ void gload_issue(GRegs& R, GPending& q, const uavhip_env& env, int e, int j) {
     const int N = env.N, M = env.M;
     const int* is = env.istate + (long long)e * UAVHIP_IST_COUNT;
     const double* ds = env.dstate + (long long)e * UAVHIP_DST_COUNT;
     const int nb = env.scene_buffers;
-    q.pred = nb == 2 ? pred : -1;
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-        if (b == 1 && q.pred >= 0) break;  // one buffer: the predicted one, in slot 0
-        const long long sb = (long long)(q.pred >= 0 ? q.pred : (b < nb ? b : 0)) * env.E + e;
+        const long long sb = (long long)(b < nb ? b : 0) * env.E + e;
         if (kAttr == 21) {
             q.valb[b] = 4.0 + j;
             q.ucb[b] = 1.0;
@@ -272,11 +263,6 @@ __device__ __forceinline__ void gload_issue(GRegs& R, GPending& q, const uavhip_
     const float* w = env.window + (long long)e * kObs;
     if (kAttr == 24) {
         R.w0 = R.w1 = R.w2 = 1.0f;
-    } else if (xwin) {  // window element i = row i / 14, feature i % 14 of the LDS rows (stride 16 x 16)
-        auto xw = [&](int i) { return xwin[(i / kDim) * 256 + i % kDim]; };
-        R.w0 = xw(j);
-        R.w1 = xw(L + j);
-        R.w2 = j < kObs - 2 * L ? xw(2 * L + j) : 0.0f;
     } else {
         R.w0 = w[j];
         R.w1 = w[L + j];
@@ -307,17 +293,9 @@ __device__ __forceinline__ void gload_finish(GRegs& R, const GPending& q, const 
     R.sb = (long long)R.sel * env.E + e;
     R.dmask = 0;
     R.ct = R.cu = -1;
-    if (q.pred < 0) {
-        R.val = R.sel ? q.valb[1] : q.valb[0];
-        R.ucost = R.sel ? q.ucb[1] : q.ucb[0];
-        R.ppen = R.sel ? q.ppb[1] : q.ppb[0];
-    } else if (R.sel == q.pred) {
-        R.val = q.valb[0];
-        R.ucost = q.ucb[0];
-        R.ppen = q.ppb[0];
-    } else {  // mispredicted buffer (not reached inside a launch): a dependent load round
-        gload_scene_regs(R, env, j);
-    }
+    R.val = R.sel ? q.valb[1] : q.valb[0];
+    R.ucost = R.sel ? q.ucb[1] : q.ucb[0];
+    R.ppen = R.sel ? q.ppb[1] : q.ppb[0];
     gset_scene_divisors(R);
     R.rcp_m = 1.0 / (double)M;
     R.rcp_n = 1.0 / (double)(j + 1);
@@ -408,9 +386,7 @@ __device__ void gstore_regs(const GRegs& R, const uavhip_env& env, int e, int j)
 // changed them (R.dmask: after an accepted assign the one target's nh_final / nh_pure / t_cost / n_lock
 // and the one UAV's assigned entry, after a reset all of them, else none) -- the same memory state as
 // gstore_regs, with 8-20 instead of 960 bytes per env-step of those arrays on most steps.
-// store_win = false (the multi-step launch, all steps but its last): env.window is not written -- the
-// step's next window went to the trajectory (the next step's policy input, gload_issue's xwin)
-__device__ void gstore_delta(const GRegs& R, const uavhip_env& env, int e, int j, bool store_win = true) {
+__device__ void gstore_delta(const GRegs& R, const uavhip_env& env, int e, int j) {
     const int N = env.N, M = env.M;
     if (kAttr == 25) return;
     const bool all = (R.dmask & 1) != 0;
@@ -446,7 +422,6 @@ __device__ void gstore_delta(const GRegs& R, const uavhip_env& env, int e, int j
         ds[UAVHIP_DST_SUM_PDMG] = R.sum_pd;
         ds[UAVHIP_DST_SUM_PFIN] = R.sum_pf;
     }
-    if (!store_win) return;
     float* w = env.window + (long long)e * kObs;
     w[j] = R.w0;
     w[L + j] = R.w1;

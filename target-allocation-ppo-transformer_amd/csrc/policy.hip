@@ -69,6 +69,8 @@ constexpr bool kExpNoEnv = false;
 #endif
 // Timing build EXP=32 (profiling only, WRONG results): every ring-row load reads one hot row (the
 // load still issued, its value used): the cost of the ring rows' L2 misses, by difference.
+// EXP=61 / 62 / 63 (WRONG results out of range): the static operand scales / layer 0's dynamic ones
+// / both compiled as 1 -- the cost of the range scaling, by difference (DESIGN.md 4a "Range").
 #ifndef UAVHIP_EXP
 #define UAVHIP_EXP 0
 #endif
@@ -124,9 +126,13 @@ struct Smem {
     float value[SPW];
     int mask[SPW * S];          // key padding mask (transformer_net.py:52-54)
     float tmax[TOK];            // max_k |x_k| of each token's window row (layer 0's operand range)
-    float smax[SPW];            // max over a sample's five tokens (its layer-0 attention output's range)
-    int selp[SPW];              // k_rollout_steps: each env's active scene buffer after its last step
+    float a0f[4];               // per trunk: (2^-s, 2^s) of the workgroup's layer-0 attention output
+    float rtab[24];             // the range table's static part (load_rtab, once per launch)
 };
+// Smem::rtab: the static operands' (2^-s, 2^s) pairs, then (14 max|W_e|, max|b_e| + max|pos|) and
+// (D max|W_in|, max|b_in|) of layer 0 per trunk (policy_layout.hpp kRgOp / kRgE / kRgA0)
+constexpr int kRtOp = 0, kRtE = 2 * kNumRangeOps, kRtA0 = kRtE + 4, kRtN = kRtA0 + 4;
+static_assert(kRtN <= 24 && kRgE + 4 == kRgA0, "Smem::rtab");
 
 // Lane index plumbing. In the multi-step rollout TU (rollout_steps.hip) every forward helper takes
 // the thread index as a leading parameter, laundered once per step by k_rollout_steps: the
@@ -370,48 +376,62 @@ __device__ __forceinline__ void hsplit_store(_Float16* Y, int o, const f32x4 v) 
 // (policy_layout.hpp range table: s = 0 on realistic weights). Static operands (LayerNorm outputs,
 // FFN hidden units, the attention output of a layer >= 1) take (2^-s, 2^s) from the table; layer 0's
 // input takes s per token from the token's window-row max (Smem::tmax) and layer 0's attention
-// output per sample (Smem::smax). Producer and consumer evaluate the same uncontracted expression
-// (__fmul_rn / __fadd_rn), so both sides always agree on s.
+// output one s per workgroup, from the max over its 16 samples' rows (Smem::a0f). Producer and
+// consumer read the same s (one evaluation, kept in LDS), so both sides always agree on it.
 struct OpSc {
     float sc, inv;  // 2^-s (the producer's factor), 2^s (the consumer's)
 };
+__device__ __forceinline__ OpSc pow2_sc(int s) { return OpSc{ldexpf(1.0f, -s), ldexpf(1.0f, s)}; }
+// The range table's static part -> Smem::rtab (threads < kRtN; the kernels call it once per launch,
+// before their first barrier): every later use is an LDS read, not a scalar load whose lgkmcnt wait
+// would also drain the phase's LDS traffic.
+__device__ __forceinline__ void load_rtab(TID_F Smem& sm, const float* __restrict__ P) {
+    const int i = TIDX();
+    if (i < kRtN) sm.rtab[i] = P[kRangeOff + (i < kRtE ? kRgOp + i : kRgE + (i - kRtE))];
+}
+// a uniform LDS value into an SGPR (the factors are the same in every lane: no VGPR held)
+__device__ __forceinline__ float rt_uniform(const Smem& sm, int i) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sm.rtab[i])));
+}
 template <int trunk, int layer, int kind>
-__device__ __forceinline__ OpSc op_sc(const float* __restrict__ P) {
+__device__ __forceinline__ OpSc op_sc(const Smem& sm) {
     constexpr int op = range_op(trunk, layer, kind);
     static_assert(op >= 0, "a static operand");
-    return OpSc{P[kRangeOff + kRgOp + 2 * op], P[kRangeOff + kRgOp + 2 * op + 1]};
+    if constexpr (UAVHIP_EXP == 61 || UAVHIP_EXP == 63) return OpSc{1.f, 1.f};  // timing builds only
+    return OpSc{rt_uniform(sm, kRtOp + 2 * op), rt_uniform(sm, kRtOp + 2 * op + 1)};
 }
-// bound of layer 0's input (e or e + pos) at a token whose window row has max |x_k| = m, from the
-// trunk's constants ea = 14 max|W_e|, ec = max|b_e| + max|pos|
-__device__ __forceinline__ float e_bound_v(float ea, float ec, float m) { return __fadd_rn(__fmul_rn(ea, m), ec); }
-__device__ __forceinline__ OpSc e_sc_v(float ea, float ec, float m) {
-    const int s = range_exp(e_bound_v(ea, ec, m));
-    return OpSc{ldexpf(1.0f, -s), ldexpf(1.0f, s)};
+// layer 0's input (e or e + pos) at a token whose window row has max |x_k| = m, from the trunk's
+// constants ea = 14 max|W_e|, ec = max|b_e| + max|pos|; its attention output of a sample whose rows
+// have max m, with a = D max|W_in|, c = max|b_in|
+// (uncontracted: every site evaluates the same roundings, so a producer and its consumer agree on s)
+__device__ __forceinline__ float e_bound_v(float ea, float ec, float m) {
+#pragma clang fp contract(off)
+    return ea * m + ec;
+}
+__device__ __forceinline__ OpSc e_sc_v(float ea, float ec, float m) { return pow2_sc(range_exp(e_bound_v(ea, ec, m))); }
+__device__ __forceinline__ OpSc a0_sc_v(float ea, float ec, float a, float c, float m) {
+#pragma clang fp contract(off)
+    return pow2_sc(range_exp(a * e_bound_v(ea, ec, m) + c));
 }
 template <int trunk>
-__device__ __forceinline__ float e_bound(const float* __restrict__ P, float m) {
+__device__ __forceinline__ OpSc e_sc(const Smem& sm, float m) {
     constexpr int ti = trunk_index(trunk);
-    return e_bound_v(P[kRangeOff + kRgE + 2 * ti], P[kRangeOff + kRgE + 2 * ti + 1], m);
+    if constexpr (UAVHIP_EXP == 62 || UAVHIP_EXP == 63) return OpSc{1.f, 1.f};  // timing builds only
+    return e_sc_v(rt_uniform(sm, kRtE + 2 * ti), rt_uniform(sm, kRtE + 2 * ti + 1), m);
 }
-template <int trunk>
-__device__ __forceinline__ OpSc e_sc(const float* __restrict__ P, float m) {
-    constexpr int ti = trunk_index(trunk);
-    return e_sc_v(P[kRangeOff + kRgE + 2 * ti], P[kRangeOff + kRgE + 2 * ti + 1], m);
-}
-// layer 0's attention output of a sample whose window has max |x_k| = m (over its five rows)
-template <int trunk>
-__device__ __forceinline__ OpSc a0_sc(const float* __restrict__ P, float m) {
-    constexpr int ti = trunk_index(trunk);
-    const float b = __fadd_rn(__fmul_rn(P[kRangeOff + kRgA0 + 2 * ti], e_bound<trunk>(P, m)),
-                              P[kRangeOff + kRgA0 + 2 * ti + 1]);
-    const int s = range_exp(b);
-    return OpSc{ldexpf(1.0f, -s), ldexpf(1.0f, s)};
-}
-// The scale of an attention output (layer 0: the sample's, else the static one)
+// The scale of an attention output (layer 0: Smem::a0f, one per workgroup -- a uniform value, held
+// in SGPRs: a per-sample factor in a VGPR across the out-projection cost the rollout loop 4 VGPR
+// spills; else the static one). p: the sample (unused).
 template <int trunk, int layer>
-__device__ __forceinline__ OpSc att_sc(const float* __restrict__ P, const float* smax, int p) {
-    if constexpr (layer == 0) return a0_sc<trunk>(P, smax[p]);
-    else return op_sc<trunk, layer, kOpAtt>(P);
+__device__ __forceinline__ OpSc att_sc(const Smem& sm, int) {
+    if constexpr (layer == 0) {
+        constexpr int ti = trunk_index(trunk);
+        if constexpr (UAVHIP_EXP == 62 || UAVHIP_EXP == 63) return OpSc{1.f, 1.f};  // timing builds only
+        return OpSc{__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sm.a0f[2 * ti]))),
+                    __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sm.a0f[2 * ti + 1])))};
+    } else {
+        return op_sc<trunk, layer, kOpAtt>(sm);
+    }
 }
 
 // Y planes [ytok0 + 16 ct + j][ycol + i] = epi(hi + 2^-11 lo + bias[row + i])
@@ -703,8 +723,8 @@ __device__ __forceinline__ void attention_full_store(TID_F Smem& sm, int c, cons
 }
 // The planes' scale of an attention output of sample p (1 when it is stored in fp32)
 template <bool PLANES, int trunk, int layer>
-__device__ __forceinline__ float attn_sc(const float* __restrict__ P, const Smem& sm, int p) {
-    if constexpr (PLANES) return att_sc<trunk, layer>(P, sm.smax, p).sc;
+__device__ __forceinline__ float attn_sc(const Smem& sm, int p) {
+    if constexpr (PLANES) return att_sc<trunk, layer>(sm, p).sc;
     else return 1.f;
 }
 // PLANES: the output goes to sm.ctx as the two fp16 planes of the split products (the out-projection's
@@ -713,7 +733,7 @@ template <bool PLANES = false, int trunk = kCriticTrunk, int layer = 1>
 __device__ void attention_full(TID_F Smem& sm, int c, const float* __restrict__ P = nullptr) {
     f32x4 o[3];
     attention_full_core(TID_C sm, c, o);
-    attention_full_store<PLANES>(TID_C sm, c, o, attn_sc<PLANES, trunk, layer>(P, sm, (int)((TIDX() >> 4) & 15)));
+    attention_full_store<PLANES>(TID_C sm, c, o, attn_sc<PLANES, trunk, layer>(sm, (int)((TIDX() >> 4) & 15)));
 }
 
 // Scaled-dot-product attention for heads [4c, 4c+4) of the query positions [qs0, qs0 + nqs) over
@@ -763,7 +783,7 @@ __device__ void attention_chunk(TID_F Smem& sm, int c, int qs0, int nqs, const f
         f32x4 o;
         int ti, d0;
         attention_task(TID_C sm, task, qs0, o, ti, d0);
-        attention_out<PLANES>(TID_C sm, c, ti, d0, o, attn_sc<PLANES, trunk, layer>(P, sm, ti & 15));
+        attention_out<PLANES>(TID_C sm, c, ti, d0, o, attn_sc<PLANES, trunk, layer>(sm, ti & 15));
     }
 }
 
@@ -773,7 +793,6 @@ __device__ void attention_chunk(TID_F Smem& sm, int c, int qs0, int nqs, const f
 // can issue later loads behind them without the embedding waiting for those (in-order vmcnt).
 struct EmbPre {
     f32x4 a, bb, pp[S];
-    float ea, ec;  // the layer-0 input's range constants (e_sc_v)
 };
 template <int trunk>
 __device__ __forceinline__ EmbPre embed_load(TID_F const float* __restrict__ P) {
@@ -790,8 +809,6 @@ __device__ __forceinline__ EmbPre embed_load(TID_F const float* __restrict__ P) 
     r.bb = *reinterpret_cast<const f32x4*>(be + 16 * wv + 4 * g);
 #pragma unroll
     for (int ct = 0; ct < S; ++ct) r.pp[ct] = *reinterpret_cast<const f32x4*>(pos + ct * D + 16 * wv + 4 * g);
-    r.ea = P[kRangeOff + kRgE + 2 * trunk_index(trunk)];
-    r.ec = P[kRangeOff + kRgE + 2 * trunk_index(trunk) + 1];
     return r;
 }
 // MODE kEmbH: h = e + pos for all 5 positions (sm.h). kEmbSplit: also e of position 4 (no pos)
@@ -822,7 +839,7 @@ __device__ void embed_apply(TID_F Smem& sm, const EmbPre& ep, float* e_out = nul
         const int o = (ct * SPW + i16) * LDH + 16 * wv + 4 * g;
         constexpr bool ring_planes = split_slot(layer_param(trunk, 0, INW)) >= 0;  // the ring GEMM's operand
         // the planes of layer 0's input scaled per token (its window row's range)
-        const float esc = (ring_planes || PL) ? e_sc_v(ep.ea, ep.ec, sm.tmax[ct * SPW + i16]).sc : 1.f;
+        const float esc = (ring_planes || PL) ? e_sc<trunk>(sm, sm.tmax[ct * SPW + i16]).sc : 1.f;
         if ((MODE == kEmbRows || (MODE == kEmbSplit && ct == S - 1)) && ring_planes)
             hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((ct * SPW + i16), 16 * wv + 4 * g), e * esc);
         else if (MODE == kEmbRows || (MODE == kEmbSplit && ct == S - 1)) *reinterpret_cast<f32x4*>(sm.ctx + o) = e;
@@ -942,9 +959,9 @@ __device__ __forceinline__ void store_rows_planes(TID_F const _Float16* src, flo
 // 2^s of a layer's in_proj operand at token tok: layer 0's input per token (its window row's range),
 // a later layer's input = the previous layer's LN2 output (static)
 template <int trunk, int layer>
-__device__ __forceinline__ float in_inv(TID_F const float* __restrict__ P, const Smem& sm, int tok) {
-    if constexpr (layer == 0) return e_sc<trunk>(P, sm.tmax[tok]).inv;
-    else return op_sc<trunk, layer - 1, kOpLn2>(P).inv;
+__device__ __forceinline__ float in_inv(const Smem& sm, int tok) {
+    if constexpr (layer == 0) return e_sc<trunk>(sm, sm.tmax[tok]).inv;
+    else return op_sc<trunk, layer - 1, kOpLn2>(sm).inv;
 }
 
 // An encoder layer whose in_proj runs as split products: K / V of all 80 tokens and Q of the query
@@ -985,7 +1002,7 @@ __device__ __forceinline__ void encoder_layer_split(TID_F Smem& sm, const float*
 #pragma unroll
             for (int ct = 0; ct < S; ++ct)
                 *reinterpret_cast<f32x4*>(sm.big + (16 * ct + i16) * LDB + col) =
-                    (hi[ct] + lo[ct] * kLoScale) * in_inv<trunk, layer>(TID_C P, sm, 16 * ct + i16) + bb;
+                    (hi[ct] + lo[ct] * kLoScale) * in_inv<trunk, layer>(sm, 16 * ct + i16) + bb;
         }
         if (wv < 4) {  // Q of the chunk for the query tokens (their SIMD partners did V)
             const f32x4 bq = *reinterpret_cast<const f32x4*>(bin + 64 * c + 16 * wv + 4 * g);
@@ -996,7 +1013,7 @@ __device__ __forceinline__ void encoder_layer_split(TID_F Smem& sm, const float*
 #pragma unroll
             for (int ct = 0; ct < CTQ; ++ct)
                 *reinterpret_cast<f32x4*>(sm.big + (qtok0 + 16 * ct + i16) * LDB + 16 * wv + 4 * g) =
-                    (hi[ct] + lo[ct] * kLoScale) * in_inv<trunk, layer>(TID_C P, sm, qtok0 + 16 * ct + i16) + bq;
+                    (hi[ct] + lo[ct] * kLoScale) * in_inv<trunk, layer>(sm, qtok0 + 16 * ct + i16) + bq;
         }
         if (c == 0) pkv = hprefetch<2>(TID_C P, si, D, kv_row(wv, 1), 0);
         else po = tail_prefetch<trunk, layer, last, TR, true>(TID_C P);
@@ -1015,7 +1032,7 @@ __device__ __forceinline__ void encoder_layer_split(TID_F Smem& sm, const float*
                 ti0 = ti;
                 d00 = d0;
             } else if (TIDX() < 4 * SPW * 4) {
-                const float asc = attn_sc<planes, trunk, layer>(P, sm, ti & 15);
+                const float asc = attn_sc<planes, trunk, layer>(sm, ti & 15);
                 attention_out<planes>(TID_C sm, 0, ti0, d00, att0[0], asc);
                 attention_out<planes>(TID_C sm, 1, ti, d0, o, asc);
             }
@@ -1025,7 +1042,7 @@ __device__ __forceinline__ void encoder_layer_split(TID_F Smem& sm, const float*
             } else {
                 f32x4 o[3];
                 attention_full_core(TID_C sm, 1, o);
-                const float asc = attn_sc<planes, trunk, layer>(P, sm, (int)((TIDX() >> 4) & 15));
+                const float asc = attn_sc<planes, trunk, layer>(sm, (int)((TIDX() >> 4) & 15));
                 attention_full_store<planes>(TID_C sm, 0, att0, asc);
                 attention_full_store<planes>(TID_C sm, 1, o, asc);
             }
@@ -1131,11 +1148,10 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     // the operand scales (policy_layout.hpp range table): the attention output (layer 0: per sample,
     // the lane's column i16), LN1's output, the FFN hidden units; LN2's output when it is the next
     // layer's split operand
-    const OpSc s_ln1 = op_sc<trunk, layer, kOpLn1>(P), s_hid = op_sc<trunk, layer, kOpHid>(P);
-    const float att_inv = att_sc<trunk, layer>(P, sm.smax, LANE() & 15).inv;
+    const OpSc s_ln1 = op_sc<trunk, layer, kOpLn1>(sm), s_hid = op_sc<trunk, layer, kOpHid>(sm);
     if constexpr (TR)  // attention output
         store_rows_planes(TID_C cp, io.o, D, 0, D, t0, b0, last, t1,
-                          [&](int tok) { return att_sc<trunk, layer>(P, sm.smax, tok & 15).inv; });
+                          [&](int tok) { return att_sc<trunk, layer>(sm, tok & 15).inv; });
     {
         // the epilogue's bias and LN1's weight / bias ahead of the GEMM: issued after it, their L2
         // round trip (~2 k cycles with every CU reading the same lines) outlasted the partials +
@@ -1148,6 +1164,8 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
             zero(hi);
             zero(lo);
             hgemm_tile<CT, 2>(TID_C hi, lo, po, P, so, D, 16 * wv, 0, cp, t0);
+            // read behind the GEMM: held across it, the per-sample factor cost the loop 4 VGPR spills
+            const float att_inv = att_sc<trunk, layer>(sm, LANE() & 15).inv;
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) acc[ct] = (hi[ct] + lo[ct] * kLoScale) * att_inv;
         }
@@ -1204,7 +1222,7 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     for (int ct = 0; ct < CT; ++ct) acc2[ct] = (hi[ct] + lo[ct] * kLoScale) * s_hid.inv;
     pre_ln2();
     float ln2_sc = 1.f;
-    if constexpr (next_planes) ln2_sc = op_sc<trunk, layer, kOpLn2>(P).sc;
+    if constexpr (next_planes) ln2_sc = op_sc<trunk, layer, kOpLn2>(sm).sc;
     residual_layernorm<CT, TR, next_planes, row4, kC0 ? 23 : -1, kC0 ? 39 : -1, kC0 ? 58 : -1>(
         TID_C sm, acc2, lp2, t0, LnOut{io.xhat2, PSX ? io.h2 : nullptr, io.rstd2, b0, last}, nullptr, h1, ln2_sc);
     PTR(tb + 14);
@@ -1510,9 +1528,9 @@ __device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* 
     };
     if constexpr (split_ring<trunk>()) {  // e of position 4 as planes in sm.ctx (embed_apply kEmbSplit)
         f32x4 lo[3] = {};
+        const float inv = e_sc<trunk>(sm, sm.tmax[(S - 1) * SPW + i16]).inv;  // the new row's scale
         hgemm_rows<3, 2>(TID_C acc, lo, pw, P, split_slot(layer_param(trunk, 0, INW)), D, rows,
                          reinterpret_cast<const _Float16*>(sm.ctx), (S - 1) * SPW, ring_issue);
-        const float inv = e_sc<trunk>(P, sm.tmax[(S - 1) * SPW + i16]).inv;  // the new row's scale
 #pragma unroll
         for (int j = 0; j < 3; ++j) acc[j] = (acc[j] + lo[j] * kLoScale) * inv;
     } else {
@@ -1566,9 +1584,9 @@ __device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* 
 // behind its last weight loads): embedding operands, Win pos_s, the wave's in_proj weight tiles
 // and bias. Ends with the embedding in sm.h / sm.ctx and Win pos_s of
 // chunk 0 in sm.red, without a barrier.
-template <int trunk, int NP>
+template <int trunk, int NP, class H = NoHook>
 __device__ __forceinline__ void rows_prologue(TID_F Smem& sm, const float* __restrict__ P, RingPre<trunk> (&pw)[3],
-                                              RowPre<NP>& rp, const RowIO& rio, int b0) {
+                                              RowPre<NP>& rp, const RowIO& rio, int b0, H hook = H{}) {
     const int wv = TIDX() >> 6;
     const EmbPre ep = embed_load<trunk>(TID_C P);
     ppos_load<trunk>(TID_C rp, rio);
@@ -1581,6 +1599,7 @@ __device__ __forceinline__ void rows_prologue(TID_F Smem& sm, const float* __res
     const float* bin = P + kOffs.o[layer_param(trunk, 0, INB)];
 #pragma unroll
     for (int j = 0; j < 3; ++j) rp.bias[j] = *reinterpret_cast<const f32x4*>(bin + j * D + 16 * wv + 4 * (LANE() >> 4));
+    hook();  // behind the loads above: its latency overlaps theirs
     embed_apply<trunk, false, kEmbSplit>(TID_C sm, ep);
     ppos_stage(TID_C sm, rp, 0);
 }
@@ -1757,7 +1776,7 @@ __device__ __forceinline__ void gather_windows(TID_F Smem& sm, const float* __re
                // lanes of a token row vote; and the row's max |x_k| (layer 0's operand range)
                 static_assert(LDX == 16 && NTHR % LDX == 0, "one token row = 16 lanes");
                 const unsigned long long nz = __ballot(v[u] != 0.f);
-                const float rmax = row16_max(fabsf(v[u]));
+                const float rmax = (UAVHIP_EXP == 62 || UAVHIP_EXP == 63) ? 0.f : row16_max(fabsf(v[u]));
                 if (i < TOK * LDX && (i % LDX) == 0) {
                     const int t = i / LDX, s = t / SPW, p = t - s * SPW;
                     const bool m = (s < S - 1) && ((nz >> (LANE() & 48)) & 0xFFFFull) == 0;
@@ -1780,14 +1799,25 @@ __device__ __forceinline__ void gather_windows(TID_F Smem& sm, const float* __re
     }
 }
 
-// Each sample's max over its five window rows (Smem::smax, layer 0's attention-output range), from
-// Smem::tmax once the barrier after gather_windows has passed; read behind a later barrier.
-__device__ __forceinline__ void smax_from_tmax(TID_F Smem& sm) {
-    if (TIDX() < SPW) {
-        float m = sm.tmax[TIDX()];
-#pragma unroll
-        for (int s = 1; s < S; ++s) m = fmaxf(m, sm.tmax[s * SPW + TIDX()]);
-        sm.smax[TIDX()] = m;
+// The workgroup's layer-0 attention-output scale per trunk (Smem::a0f) from the max over its 80
+// window rows (rows 0..TOK-1 of m, one float each): wave 0, once the rows are visible; read behind
+// a later barrier. The bound holds for every sample of the workgroup. e / a0: the range table's
+// kRgE / kRgA0 constants (in Smem::rtab or in the packed buffer).
+__device__ __forceinline__ void a0f_from_max(TID_F Smem& sm, const float* m, const float* e, const float* a0) {
+    static_assert(TOK <= 128, "two rows per lane");
+    if (TIDX() < 64) {
+        const int l = TIDX();
+        const float v = wave_max(fmaxf(m[l], l + 64 < TOK ? m[l + 64] : 0.f));
+        if (l < 2) {
+            const OpSc f = a0_sc_v(e[2 * l], e[2 * l + 1], a0[2 * l], a0[2 * l + 1], v);
+            sm.a0f[2 * l] = f.sc;
+            sm.a0f[2 * l + 1] = f.inv;
+        }
+    }
+}
+__device__ __forceinline__ void a0f_from_tmax(TID_F Smem& sm) {
+    if constexpr (UAVHIP_EXP != 62 && UAVHIP_EXP != 63) {
+        a0f_from_max(TID_C sm, sm.tmax, sm.rtab + kRtE, sm.rtab + kRtA0);
     }
 }
 
@@ -1799,18 +1829,7 @@ struct EnvOut {
     double* rew;    // [E]
     uint8_t* done;  // [E]
     double* info;   // [E][UAVHIP_INFO_COUNT] (nullable)
-    // k_rollout_steps: not the launch's last step (env.window is not written: the next window is the
-    // trajectory's, the next step's policy input); 0 in single-step launches
-    int not_last;
 };
-// The multi-step launch (the steps TU) knows each env's scene buffer from its previous step
-// (Smem::selp, set at kernel start from istate) and takes the env's window from the policy's input
-// rows in sm.x, so its env step reads one scene buffer and no env.window (envgrp::gload_issue)
-#ifdef UAVHIP_STEPS_TU
-constexpr bool kStepsEnv = true;
-#else
-constexpr bool kStepsEnv = false;
-#endif
 
 // ROWS: layer 0 of both trunks on the window-row projection ring (inference only).
 // ENV: the env step of the sampled actions follows (needs ROWS; envs b0 .. b0 + 15): a bit mask of
@@ -1867,7 +1886,9 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     gather_windows<TR>(TID_C sm, states, B, io, b0, do_actor);
     __syncthreads();
     PTR(1);
-    smax_from_tmax(TID_C sm);  // read behind the next barrier (layer 0's attention)
+    // layer 0's attention-output scales, read behind the next barrier (the ring forward: once the
+    // actor's prologue loads are issued, so that wave 0's reduction overlaps their round trip)
+    if (!ROWS || !do_actor) a0f_from_tmax(TID_C sm);
     const int wv = TIDX() >> 6;
     const float* headw_a = P + kOffs.o[kActorHead];
     const float* headw_c = P + kOffs.o[kCriticHead];
@@ -1876,7 +1897,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
         if (do_actor) {
             RingPre<kActorTrunk> pw[3];
             RowPre<2> rp;
-            rows_prologue<kActorTrunk>(TID_C sm, P, pw, rp, rio, b0);
+            rows_prologue<kActorTrunk>(TID_C sm, P, pw, rp, rio, b0, [&] { a0f_from_tmax(TID_C sm); });
             PTR(2);
             __syncthreads();
             encoder_layer_rows<kActorTrunk>(TID_C sm, P, pw, rp, rio, b0);
@@ -1968,9 +1989,8 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
         // the env step's state loads land while the critic head runs
         if constexpr ((ENV & kEnvGrp) && !kExpNoEnv) {
             if (env_grp) {
-                const int le = tid_env() & 63, pe = 2 * (int)(tid_env() >> 6) + (le >> 5);
-                envgrp::gload_issue(gR, gq, env, b0 + pe, le & 31, kStepsEnv ? sm.selp[pe] : -1,
-                                    kStepsEnv ? sm.x + pe * LDX : nullptr);
+                const int le = tid_env() & 63;
+                envgrp::gload_issue(gR, gq, env, b0 + 2 * (int)(tid_env() >> 6) + (le >> 5), le & 31);
             }
         }
         if (!TR && wv < 4) ph = prefetch<4>(TID_C headw_c, D, 16 * wv, 0);
@@ -2062,8 +2082,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
                           eo.rew + e, eo.done + e, eo.info ? eo.info + (size_t)e * UAVHIP_INFO_COUNT : nullptr);
             PTR(62);
             if constexpr (UAVHIP_EXP == 42) envgrp::gstore_regs(R, env, e, j);  // timing build: every entry
-            else envgrp::gstore_delta(R, env, e, j, !eo.not_last);  // only the entries the step changed
-            if (j == 0) sm.selp[2 * wve + g] = R.sel;  // the next step of this launch reads one scene buffer
+            else envgrp::gstore_delta(R, env, e, j);  // only the entries the step changed
             PTR(63);
         }
         if constexpr ((ENV & kEnvWave) != 0) if (!env_grp && e0 < B) {
@@ -2098,6 +2117,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_forward(const float* __restrict
     __shared__ __attribute__((aligned(16))) Smem sm;
     // the younger half (waves 4-7, the arbitration loser of every phase) at priority 1
     if (tid_x() >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
+    load_rtab(TID_K sm, P);
     policy_block<TR, ROWS, ENV, VONLY>(TID_K sm, P, states, B, actions_in, seed, offset, offset_dev, action_out, logp_out,
                                        value_out, ent_out, logits_out, io, rio, env, eo, blockIdx.x);
 }
@@ -2140,11 +2160,7 @@ __global__ __launch_bounds__(NTHR) void k_rollout_steps(const StepsArgs args) {
     __shared__ __attribute__((aligned(16))) Smem sm;
     if (threadIdx.x >= NTHR / 2) __builtin_amdgcn_s_setprio(1);
     if (threadIdx.x == 0) g_tid_zero = 0;
-    if (threadIdx.x < SPW) {  // each env's active scene buffer (envgrp::gload_issue's prediction)
-        const int e = blockIdx.x * SPW + threadIdx.x;
-        sm.selp[threadIdx.x] = e < args.B && args.env.scene_buffers == 2
-                                   ? args.env.istate[(size_t)e * UAVHIP_IST_COUNT + UAVHIP_IST_SCENE_SEL] & 1 : 0;
-    }
+    load_rtab(TID_K sm, args.P);  // the weights are the launch's: once
     for (int t = 0; t < args.seq.n; ++t) {
         __syncthreads();  // g_tid_zero; the previous step's LDS scratch and global stores
         // Every argument is read through a kernarg pointer laundered per step, so the loads sit where
@@ -2160,7 +2176,7 @@ __global__ __launch_bounds__(NTHR) void k_rollout_steps(const StepsArgs args) {
         const size_t o = (size_t)t * a.B;
         const RowIO r{a.rio.rp, a.rio.B, a.rio.g + t};
         const EnvOut e{a.eo.auto_reset, a.eo.obs + t * a.seq.obs_stride, a.eo.rew + o, a.eo.done + o,
-                       a.eo.info ? a.eo.info + o * UAVHIP_INFO_COUNT : nullptr, t < a.seq.n - 1};
+                       a.eo.info ? a.eo.info + o * UAVHIP_INFO_COUNT : nullptr};
         policy_block<false, true, ENVP>(tid, sm, a.P, a.states + t * a.seq.obs_stride, a.B, nullptr, a.seed,
                                         a.offset + t * a.seq.off_stride, a.offset_dev, a.action_out + o, a.logp_out + o,
                                         a.value_out + o, nullptr, nullptr, TrainIO{}, r, a.env, e, bx);
@@ -2237,7 +2253,7 @@ __device__ void rows_fill_trunk(Smem& sm, const float* __restrict__ P, const Fil
             zero(lo);
             hgemm_tile<S - 1, 4>(acc, lo, pre.w[j - P0], P, si, D, row, 0, reinterpret_cast<const _Float16*>(sm.ctx), 0);
 #pragma unroll
-            for (int s = 0; s < S - 1; ++s) acc[s] = (acc[s] + lo[s] * kLoScale) * e_sc<trunk>(P, sm.tmax[s * SPW + i16]).inv;
+            for (int s = 0; s < S - 1; ++s) acc[s] = (acc[s] + lo[s] * kLoScale) * e_sc<trunk>(sm, sm.tmax[s * SPW + i16]).inv;
         } else {
             gemm_tile<S - 1, KB>(acc, pre.w[j - P0], Win, D, row, 0, sm.ctx, LDH, 0);
         }
@@ -2284,6 +2300,7 @@ __global__ __launch_bounds__(NTHR) void k_policy_rows_fill(const float* __restri
                                                            const float* __restrict__ states, const RowIO rio) {
     __shared__ __attribute__((aligned(16))) Smem sm;
     const int nb = (rio.B + SPW - 1) / SPW;
+    load_rtab(sm, P);
     if ((int)blockIdx.x < nb) {
         const int b0 = blockIdx.x * SPW;
         FillPre<kActorTrunk> fa;
@@ -3240,7 +3257,6 @@ __device__ __forceinline__ void ps_rows_in(float* dst, int lds, const float* __r
 // The embedding's global operands (ps_embed_load: issued by k_ps_f1 before the window gather).
 struct PsEmbPre {
     f32x4 a, bb, pp;
-    float ea, ec;  // the layer-0 input's range constants (e_sc_v)
 };
 __device__ __forceinline__ PsEmbPre ps_embed_load(const float* __restrict__ P, int trunk, int s) {
     const float* We = P + kOffs.o[trunk + EMB_W];
@@ -3253,13 +3269,11 @@ __device__ __forceinline__ PsEmbPre ps_embed_load(const float* __restrict__ P, i
     r.a.w = 4 * g + 3 < IN ? We[f * IN + 4 * g + 3] : 0.f;
     r.bb = ld4(P + kOffs.o[trunk + EMB_B] + 16 * wv + 4 * g);
     r.pp = ld4(P + kOffs.o[trunk + POS] + s * D + 16 * wv + 4 * g);
-    r.ea = P[kRangeOff + kRgE + 2 * trunk_index(trunk)];
-    r.ec = P[kRangeOff + kRgE + 2 * trunk_index(trunk) + 1];
     return r;
 }
 template <bool PL = false>  // PL: also the planes of h into sm.ctx (ps_inproj_split's operand)
 __device__ void ps_embed(Smem& sm, const PsEmbPre& ep, float* __restrict__ e_out, float* __restrict__ h_out, int b0,
-                         int s) {
+                         int s, int ti) {
     const int l = lane_id(), i16 = l & 15, g = l >> 4, wv = tid_x() >> 6;
     const f32x4 a = ep.a, bb = ep.bb, pp = ep.pp;
     const f32x4 x = ld4(sm.x + (s * SPW + i16) * LDX + 4 * g);
@@ -3272,7 +3286,7 @@ __device__ void ps_embed(Smem& sm, const PsEmbPre& ep, float* __restrict__ e_out
     st4(sm.h + (s * SPW + i16) * LDH + 16 * wv + 4 * g, v);
     if constexpr (PL)  // scaled per token (its window row's range)
         hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((s * SPW + i16), 16 * wv + 4 * g),
-                     v * e_sc_v(ep.ea, ep.ec, sm.tmax[s * SPW + i16]).sc);
+                     v * e_sc_v(sm.rtab[kRtE + 2 * ti], sm.rtab[kRtE + 2 * ti + 1], sm.tmax[s * SPW + i16]).sc);
     const size_t r = (size_t)trow(s * SPW + i16, b0);
     st4(e_out + r * D + 16 * wv + 4 * g, e);
     st4(h_out + r * D + 16 * wv + 4 * g, v);
@@ -3399,16 +3413,17 @@ __global__ __launch_bounds__(NTHR) void k_ps_f1(const float* __restrict__ P, con
     // every global operand of the embedding and of the in_proj GEMM first: their L2 round trip
     // overlaps the window gather's
     const PsEmbPre ep = ps_embed_load(P, trunk, s);
+    load_rtab(sm, P);
     [[maybe_unused]] PsInPre wp;
     if constexpr (kPsSplit) ps_inproj_load(wp, P, soff, P + kOffs.o[layer_param(trunk, 0, INB)], tile0);
     gather_windows<true>(sm, states, B, io, b0, r == 0);  // one workgroup per block writes the rows
     __syncthreads();
-    ps_embed<kPsSplit>(sm, ep, io.e[critic ? 1 : 0], io.h0[critic ? 1 : 0], b0, s);
+    ps_embed<kPsSplit>(sm, ep, io.e[critic ? 1 : 0], io.h0[critic ? 1 : 0], b0, s, critic ? 1 : 0);
     __syncthreads();
     if constexpr (kPsSplit) {
         const float m = sm.tmax[s * SPW + (lane_id() & 15)];
         ps_inproj_split(wp, P, soff, io.L[critic ? 1 : 0].qkv, tile0, s, b0, reinterpret_cast<const _Float16*>(sm.ctx),
-                        critic ? e_sc<kCriticTrunk>(P, m).inv : e_sc<kActorTrunk>(P, m).inv);
+                        critic ? e_sc<kCriticTrunk>(sm, m).inv : e_sc<kActorTrunk>(sm, m).inv);
     } else {
         ps_inproj(sm, P + kOffs.o[layer_param(trunk, 0, INW)], P + kOffs.o[layer_param(trunk, 0, INB)],
                   io.L[critic ? 1 : 0].qkv, critic || s == S - 1 ? 0 : D / 16, s, b0);
@@ -3427,11 +3442,8 @@ __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, con
         po = hprefetch<2>(P, critic ? split_slot(layer_param(kCriticTrunk, 0, OUTW)) : split_slot(layer_param(kActorTrunk, 0, OUTW)),
                           D, 16 * wv, 0);
     ps_mask(sm, io.mask, b0);
-    if (tid_x() < SPW) {  // each sample's window range (F1's rows), for the attention output's planes
-        float m = io.tmax[(size_t)(b0 + tid_x()) * S];
-        for (int k = 1; k < S; ++k) m = fmaxf(m, io.tmax[(size_t)(b0 + tid_x()) * S + k]);
-        sm.smax[tid_x()] = m;
-    }
+    load_rtab(sm, P);
+    a0f_from_max(sm, io.tmax + (size_t)b0 * S, P + kRangeOff + kRgE, P + kRangeOff + kRgA0);  // F1's window rows
     ps_rows_in(sm.h, LDH, io.h0[ti], D, 0, D, s, b0);  // the layer input (residual) of the position
     if (critic) ps_attention<kPsSplit, kCriticTrunk, 0>(sm, io.L[ti].qkv, s, b0, P);
     else ps_attention<kPsSplit, kActorTrunk, 0>(sm, io.L[ti].qkv, s, b0, P);
@@ -3448,7 +3460,7 @@ __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, con
             __syncthreads();
             // layer 1 (pruned) of this position: K | V, and Q at position 4, from LN2's planes in sm.h
             ps_inproj_split(wp, P, s1, io.L[2].qkv, tile0, s, b0, reinterpret_cast<const _Float16*>(sm.h),
-                            op_sc<kCriticTrunk, 0, kOpLn2>(P).inv);
+                            op_sc<kCriticTrunk, 0, kOpLn2>(sm).inv);
             return;
         }
         auto hook = [&] {  // the head's weights before LN2
@@ -3485,6 +3497,7 @@ __global__ __launch_bounds__(NTHR) void k_ps_f3(const float* __restrict__ P, con
     // the out-projection's first weight blocks ahead of the attention (as k_ps_f2)
     [[maybe_unused]] HPre<2> po;
     if constexpr (kPsSplit) po = hprefetch<2>(P, split_slot(layer_param(kCriticTrunk, 1, OUTW)), D, 16 * wv, 0);
+    load_rtab(sm, P);
     ps_mask(sm, io.mask, b0);
     ps_rows_in(sm.h, LDH, io.L[1].h2, D, 0, D, S - 1, b0);  // layer 1's input (residual) at position 4
     ps_attention<kPsSplit, kCriticTrunk, 1>(sm, io.L[2].qkv, S - 1, b0, P);
@@ -3886,8 +3899,7 @@ __global__ __launch_bounds__(256) void k_policy_range(const float* __restrict__ 
     float t[kRangeFloats] = {};
     for (int k = 0; k < kNumParams; ++k) t[kRgMax + k] = tab[kRgMax + k];
     range_derive(t);
-    for (int k = kNumParams; k < kRgTicket; ++k) tab[k] = t[k];
-    *reinterpret_cast<unsigned*>(tab + kRgTicket) = 0u;  // ready for the next pack
+    for (int k = kNumParams; k < kRangeFloats; ++k) tab[k] = t[k];  // (the ticket slot: 0, ready for the next)
 }
 
 int policy_split(const float* flat, float* packed, hipStream_t st) {

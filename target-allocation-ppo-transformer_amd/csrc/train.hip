@@ -344,13 +344,16 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     const float nss = q < kCriticTrunk ? sc.nss_a : sc.nss_c;
     const float w1 = (float)(1.0 - a.beta1), b2 = (float)a.beta2, w2 = (float)(1.0 - a.beta2), epsf = (float)a.eps;
     if (live) {
+        // no contraction here: __fmul_rn / __fadd_rn alone do not stop the compiler fusing a product
+        // into the sum after it (this file builds with contraction on), the pragma does
+#pragma clang fp contract(off)
         g = g * coef;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            m[j] = __fmaf_rn(w1, __fsub_rn(g[j], m[j]), m[j]);  // torch's vectorised lerp: one fma
-            v[j] = __fadd_rn(__fmul_rn(v[j], b2), __fmul_rn(__fmul_rn(w2, g[j]), g[j]));
-            const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v[j]), sc.bc2s), epsf);
-            p[j] = __fadd_rn(p[j], __fdiv_rn(__fmul_rn(nss, m[j]), denom));
+            m[j] = __fmaf_rn(w1, g[j] - m[j], m[j]);  // torch's vectorised lerp: one fma
+            v[j] = v[j] * b2 + (w2 * g[j]) * g[j];
+            const float denom = __fdiv_rn(__fsqrt_rn(v[j]), sc.bc2s) + epsf;
+            p[j] = p[j] + __fdiv_rn(nss * m[j], denom);
         }
         *reinterpret_cast<f32x4*>(a.grads + f) = g;
         *reinterpret_cast<f32x4*>(a.m + f) = m;
@@ -388,8 +391,7 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
                 float t[kRangeFloats] = {};
                 for (int k = 0; k < kNumParams; ++k) t[kRgMax + k] = mq[k];
                 range_derive(t);
-                for (int k = 0; k < kRgTicket; ++k) tab[k] = t[k];
-                *reinterpret_cast<unsigned*>(tab + kRgTicket) = 0u;
+                for (int k = 0; k < kRangeFloats; ++k) tab[k] = t[k];  // (the ticket slot: 0, ready for the next)
             }
         }
     }

@@ -544,10 +544,13 @@ def _range_case(net, case):
     range table must keep it exact): returns the input scale for the windows."""
     c0 = net.critic_net.transformer.layers[0]
     with torch.no_grad():
-        if case.startswith("ffn1 x"):  # the critic's layer-0 FFN hidden units (FFN2's operand) to ~1.4e5 / ~1e6
+        if case.startswith("ffn1 x"):  # the critic's layer-0 FFN hidden units (FFN2's operand) to ~1.4e5
             k = float(case[len("ffn1 x"):])
             c0.linear1.weight.mul_(k)
             c0.linear1.bias.mul_(k)
+        elif case == "ln1 x3e5":  # LN1's output (FFN1's operand) ~3e5 and the FFN hidden units ~1e6
+            c0.norm1.weight.mul_(3e5)
+            c0.norm1.bias.mul_(3e5)
         elif case == "ln1 x1e-6":  # LN1's output (FFN1's operand) ~1e-6; the FFN biases zero so it matters
             c0.norm1.weight.mul_(1e-6)
             c0.norm1.bias.mul_(1e-6)
@@ -565,7 +568,7 @@ def _range_case(net, case):
     return 1.0
 
 
-RANGE_CASES = ["ffn1 x4e4", "ffn1 x3e5", "ln1 x1e-6", "inputs x1e5", "inputs x1e-6"]
+RANGE_CASES = ["ffn1 x4e4", "ln1 x3e5", "ln1 x1e-6", "inputs x1e5", "inputs x1e-6"]
 
 
 @pytest.mark.parametrize("case", RANGE_CASES)
@@ -573,8 +576,9 @@ def test_fused_forward_out_of_fp16_range_matches_torch(policy_npz, case):
     """every split-product operand is scaled by a power of two from a bound on its
     magnitude (policy_layout.hpp range table: per token for layer 0's input, per sample for layer 0's
     attention output, from the weights for the rest), so activations far outside fp16's normal range
-    [2^-14, 65504] -- the critic's FFN hidden units at ~1.4e5 and ~1e6 (FFN1 scaled; round 4 returned
-    NaN here), LayerNorm outputs at ~1e-6, window rows at 1e5 and 1e-6 -- give the torch fp32
+    [2^-14, 65504] -- the critic's FFN hidden units at ~1.4e5 (FFN1 scaled; round 4 returned NaN here),
+    LayerNorm outputs at ~3e5 with FFN hidden units at ~1e6, LayerNorm outputs at ~1e-6, window rows at
+    1e5 and 1e-6 -- give the torch fp32
     module's logp / value / entropy within the usual bars (1e-5 relative), all finite. The full-window
     forward (uavhip_policy_forward) and the ring forward (uavhip_policy_forward_rows: fill + a
     shifted step) are both checked."""

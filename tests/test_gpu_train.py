@@ -150,6 +150,19 @@ def test_fused_steps_match_eager_adam():
     assert worst <= 1.0
 
 
+def _assert_packed_equal(a, b):
+    """Bitwise equality of two packed buffers; on a mismatch, which region (parameters, split
+    copies, the closing range table) and the first differing slots."""
+    from uavhip.policy import RANGE_FLOATS, layout
+    if torch.equal(a, b):
+        return
+    _, n = layout()
+    bad = torch.nonzero(a.view(torch.int32) != b.view(torch.int32)).flatten().tolist()
+    total = a.numel()
+    reg = lambda i: "params" if i < n else ("range table" if i >= total - RANGE_FLOATS else "split copies")  # noqa: E731
+    raise AssertionError(f"{len(bad)} slots differ, first {[(i, reg(i), float(a[i]), float(b[i])) for i in bad[:6]]}")
+
+
 def _trainer_state(tr):
     return [t.detach().clone() for t in (tr.params, tr.adam_m, tr.adam_v, tr.adam_step, tr.grads, tr.loss_sums,
                                          tr.stats)]
@@ -429,7 +442,7 @@ def test_device_pack_matches_host_pack():
         flat[o:o + p.numel()] = p.reshape(-1)
     packed = torch.full((split_layout()[1],), float("nan"), device="cuda")  # + the split copies
     _lib.check(_lib.LIB.uavhip_policy_pack(_lib.ptr(flat), _lib.ptr(packed), _lib.stream_handle()), "pack")
-    assert torch.equal(packed, pack_weights(net.state_dict(), device="cuda"))
+    _assert_packed_equal(packed, pack_weights(net.state_dict(), device="cuda"))
 
 
 def test_wgrad_direct_mode_matches_stream_k(monkeypatch):
@@ -540,7 +553,7 @@ def test_packed_weights_repack_on_device():
     torch.manual_seed(2)
     net = TransformerActorCritic().cuda()
     buf = net.packed_weights()
-    assert torch.equal(buf, pack_weights(net.state_dict(), device="cuda"))
+    _assert_packed_equal(buf, pack_weights(net.state_dict(), device="cuda"))
     tr = FusedPPOTrainer(net, 64)
     bufs = _buffers(256, seed=3)
     tr.set_buffers(*bufs)
