@@ -279,9 +279,11 @@ int uavhip_policy_pack(const float* flat, float* packed, uavhip_stream_t stream)
  * split products multiply every activation operand by a power of two 2^-s before splitting it into
  * fp16 planes and the GEMM output by 2^s, with s from a rigorous bound on the operand's magnitude
  * (0 on realistic weights), so no operand the reference's fp32 can hold leaves fp16's range.
- * Host side: max_abs[50] = max |param| of each state_dict tensor (key order) -> table[n] (the
- * maxima, the per-token constants of layer 0, the static operands' (2^-s, 2^s) pairs), the same
- * floats uavhip_policy_pack writes on the device. Either pointer NULL: only returns n. */
+ * The packed buffer's table holds the maxima (max |param| of each state_dict tensor, floats 0..49;
+ * the rest zero; uavhip_policy_pack writes them, an UPDATE step refreshes them) and every kernel
+ * derives the scales from them. Host side: max_abs[50] (key order) -> table[n]: the maxima, the
+ * per-token constants of layer 0 and the static operands' (2^-s, 2^s) pairs -- bitwise what the
+ * kernels derive. Either pointer NULL: only returns n. */
 int32_t uavhip_policy_range_table(const float* max_abs, float* table);
 
 /* Per parameter (state_dict key order): the in-features K of the weight matrices stored in MFMA

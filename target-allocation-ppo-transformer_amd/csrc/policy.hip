@@ -126,6 +126,7 @@ struct Smem {
     float value[SPW];
     int mask[SPW * S];          // key padding mask (transformer_net.py:52-54)
     float tmax[TOK];            // max_k |x_k| of each token's window row (layer 0's operand range)
+    signed char es[2][TOK];     // per trunk and token: layer 0's input scale exponent s (from tmax)
     float a0f[4];               // per trunk: (2^-s, 2^s) of the workgroup's layer-0 attention output
     float rtab[24];             // the range table's static part (load_rtab, once per launch)
 };
@@ -169,13 +170,19 @@ struct APre {
 __device__ __forceinline__ const float* frag_ptr(TID_F const float* W, int ldw, int row, int kw0) {
     return W + ((size_t)(row >> 4) * (ldw >> 4) + (kw0 >> 4)) * 256 + 4 * LANE();
 }
-template <int D>
+template <int D, int N = D>  // N < D: only blocks 0 .. N-1 now (prefetch_rest loads the others)
 __device__ __forceinline__ APre<D> prefetch(TID_F const float* __restrict__ W, int ldw, int row, int kw0) {
     const float* wp = frag_ptr(TID_C W, ldw, row, kw0);
     APre<D> r;
 #pragma unroll
-    for (int p = 0; p < D; ++p) r.a[p] = *reinterpret_cast<const f32x4*>(wp + 256 * p);
+    for (int p = 0; p < N; ++p) r.a[p] = *reinterpret_cast<const f32x4*>(wp + 256 * p);
     return r;
+}
+template <int N, int D>
+__device__ __forceinline__ void prefetch_rest(TID_F APre<D>& r, const float* __restrict__ W, int ldw, int row, int kw0) {
+    const float* wp = frag_ptr(TID_C W, ldw, row, kw0);
+#pragma unroll
+    for (int p = N; p < D; ++p) r.a[p] = *reinterpret_cast<const f32x4*>(wp + 256 * p);
 }
 
 // acc[ct] += W[row + i][kw0 + k] * X[xtok0 + 16 ct + j][k]  over k in [0, 128), one 16-row tile.
@@ -382,12 +389,29 @@ struct OpSc {
     float sc, inv;  // 2^-s (the producer's factor), 2^s (the consumer's)
 };
 __device__ __forceinline__ OpSc pow2_sc(int s) { return OpSc{ldexpf(1.0f, -s), ldexpf(1.0f, s)}; }
-// The range table's static part -> Smem::rtab (threads < kRtN; the kernels call it once per launch,
-// before their first barrier): every later use is an LDS read, not a scalar load whose lgkmcnt wait
-// would also drain the phase's LDS traffic.
+// The scales the kernels derive from the packed table's maxima (policy_layout.hpp range_entry) ->
+// Smem::rtab, once per launch before the first barrier: every later use is an LDS read, not a scalar
+// load whose lgkmcnt wait would also drain the phase's LDS traffic. Waves 0-3 take 6 entries each,
+// every index a compile-time constant (the maxima they need are uniform scalar loads, one round; a
+// thread per entry ran every entry's branch one after another, +1 us per kernel).
+template <int W>
+__device__ __forceinline__ void rtab_part(TID_F Smem& sm, const float* __restrict__ M) {
+#pragma unroll
+    for (int j = 0; j < kRtN / 4; ++j) {
+        const int i = (kRtN / 4) * W + j;
+        const float v = range_entry(M, i < kRtE ? kRgOp + i : kRgE + (i - kRtE));
+        if ((TIDX() & 63) == 0) sm.rtab[i] = v;
+    }
+}
 __device__ __forceinline__ void load_rtab(TID_F Smem& sm, const float* __restrict__ P) {
-    const int i = TIDX();
-    if (i < kRtN) sm.rtab[i] = P[kRangeOff + (i < kRtE ? kRgOp + i : kRgE + (i - kRtE))];
+    static_assert(kRtN % 4 == 0, "4 waves");
+    switch (TIDX() >> 6) {  // wave-uniform
+        case 0: rtab_part<0>(TID_C sm, P + kRangeOff); break;
+        case 1: rtab_part<1>(TID_C sm, P + kRangeOff); break;
+        case 2: rtab_part<2>(TID_C sm, P + kRangeOff); break;
+        case 3: rtab_part<3>(TID_C sm, P + kRangeOff); break;
+        default: break;
+    }
 }
 // a uniform LDS value into an SGPR (the factors are the same in every lane: no VGPR held)
 __device__ __forceinline__ float rt_uniform(const Smem& sm, int i) {
@@ -418,6 +442,13 @@ __device__ __forceinline__ OpSc e_sc(const Smem& sm, float m) {
     constexpr int ti = trunk_index(trunk);
     if constexpr (UAVHIP_EXP == 62 || UAVHIP_EXP == 63) return OpSc{1.f, 1.f};  // timing builds only
     return e_sc_v(rt_uniform(sm, kRtE + 2 * ti), rt_uniform(sm, kRtE + 2 * ti + 1), m);
+}
+// layer 0's input scale at token tok from Smem::es (gather_windows: e_sc's exponent, evaluated once
+// per token): dir -1 the producer's 2^-s, +1 the consumer's 2^s
+template <int trunk, int dir>
+__device__ __forceinline__ float es_factor(const Smem& sm, int tok) {
+    if constexpr (UAVHIP_EXP == 62 || UAVHIP_EXP == 63) return 1.f;  // timing builds only
+    return ldexpf(1.0f, dir * (int)sm.es[trunk_index(trunk)][tok]);
 }
 // The scale of an attention output (layer 0: Smem::a0f, one per workgroup -- a uniform value, held
 // in SGPRs: a per-sample factor in a VGPR across the out-projection cost the rollout loop 4 VGPR
@@ -839,7 +870,7 @@ __device__ void embed_apply(TID_F Smem& sm, const EmbPre& ep, float* e_out = nul
         const int o = (ct * SPW + i16) * LDH + 16 * wv + 4 * g;
         constexpr bool ring_planes = split_slot(layer_param(trunk, 0, INW)) >= 0;  // the ring GEMM's operand
         // the planes of layer 0's input scaled per token (its window row's range)
-        const float esc = (ring_planes || PL) ? e_sc<trunk>(sm, sm.tmax[ct * SPW + i16]).sc : 1.f;
+        const float esc = (ring_planes || PL) ? es_factor<trunk, -1>(sm, ct * SPW + i16) : 1.f;
         if ((MODE == kEmbRows || (MODE == kEmbSplit && ct == S - 1)) && ring_planes)
             hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((ct * SPW + i16), 16 * wv + 4 * g), e * esc);
         else if (MODE == kEmbRows || (MODE == kEmbSplit && ct == S - 1)) *reinterpret_cast<f32x4*>(sm.ctx + o) = e;
@@ -960,7 +991,7 @@ __device__ __forceinline__ void store_rows_planes(TID_F const _Float16* src, flo
 // a later layer's input = the previous layer's LN2 output (static)
 template <int trunk, int layer>
 __device__ __forceinline__ float in_inv(const Smem& sm, int tok) {
-    if constexpr (layer == 0) return e_sc<trunk>(sm, sm.tmax[tok]).inv;
+    if constexpr (layer == 0) return es_factor<trunk, 1>(sm, tok);
     else return op_sc<trunk, layer - 1, kOpLn2>(sm).inv;
 }
 
@@ -998,6 +1029,7 @@ __device__ __forceinline__ void encoder_layer_split(TID_F Smem& sm, const float*
             zero(hi);
             zero(lo);
             hgemm_tile<S, 2>(TID_C hi, lo, pkv, P, si, D, kv_row(wv, c), 0, hp, 0);
+            if constexpr (layer == 0) __asm__ volatile("" ::: "memory");  // the scales' LDS reads after the GEMM
             const int col = (1 + (wv >> 2)) * 64 + 16 * (wv & 3) + 4 * g;
 #pragma unroll
             for (int ct = 0; ct < S; ++ct)
@@ -1010,6 +1042,7 @@ __device__ __forceinline__ void encoder_layer_split(TID_F Smem& sm, const float*
             zero(hi);
             zero(lo);
             hgemm_tile<CTQ, 2>(TID_C hi, lo, pq, P, si, D, 64 * c + 16 * wv, 0, hp, qtok0);
+            if constexpr (layer == 0) __asm__ volatile("" ::: "memory");
 #pragma unroll
             for (int ct = 0; ct < CTQ; ++ct)
                 *reinterpret_cast<f32x4*>(sm.big + (qtok0 + 16 * ct + i16) * LDB + 16 * wv + 4 * g) =
@@ -1528,7 +1561,7 @@ __device__ __forceinline__ void encoder_layer_rows(TID_F Smem& sm, const float* 
     };
     if constexpr (split_ring<trunk>()) {  // e of position 4 as planes in sm.ctx (embed_apply kEmbSplit)
         f32x4 lo[3] = {};
-        const float inv = e_sc<trunk>(sm, sm.tmax[(S - 1) * SPW + i16]).inv;  // the new row's scale
+        const float inv = es_factor<trunk, 1>(sm, (S - 1) * SPW + i16);  // the new row's scale
         hgemm_rows<3, 2>(TID_C acc, lo, pw, P, split_slot(layer_param(trunk, 0, INW)), D, rows,
                          reinterpret_cast<const _Float16*>(sm.ctx), (S - 1) * SPW, ring_issue);
 #pragma unroll
@@ -1605,8 +1638,8 @@ __device__ __forceinline__ void rows_prologue(TID_F Smem& sm, const float* __res
 }
 
 // 128 -> 64 (MFMA, waves 0-3) -> relu -> nout (VALU) on the last-position rows (transformer_net.py:77-91)
-template <int head, int nout>
-__device__ void head_mlp(TID_F Smem& sm, const float* __restrict__ P, const APre<4>& pw, float* out) {
+template <int head, int nout, int DQ = 4>
+__device__ void head_mlp(TID_F Smem& sm, const float* __restrict__ P, const APre<DQ>& pw, float* out) {
     const float* W0 = P + kOffs.o[head + 0];
     const float* b0 = P + kOffs.o[head + 1];
     const float* W2 = P + kOffs.o[head + 2];
@@ -1619,7 +1652,7 @@ __device__ void head_mlp(TID_F Smem& sm, const float* __restrict__ P, const APre
     const int p = item / nout, a = (item - p * nout) % nout;  // in range for every thread
     const f32x4 w2 = *reinterpret_cast<const f32x4*>(W2 + a * HID + 4 * k4);
     const float bb2 = b2[a];
-    if (wv < HID / 16) linear1<1, true, 4>(TID_C pw, W0, D, b0, 16 * wv, sm.h, LDH, (S - 1) * SPW, sm.z, LDZ, 16 * wv, 0);
+    if (wv < HID / 16) linear1<1, true, DQ>(TID_C pw, W0, D, b0, 16 * wv, sm.h, LDH, (S - 1) * SPW, sm.z, LDZ, 16 * wv, 0);
     __syncthreads();
     if (item < kItems) {  // wave-uniform: kItems * 16 is a multiple of 64
         const f32x4 z = *reinterpret_cast<const f32x4*>(sm.z + p * LDZ + 4 * k4);
@@ -1736,7 +1769,7 @@ __global__ __launch_bounds__(64) void k_loss_partials(const TrainIO io) {
 // and the per-sample loss inputs into the workspace. Ends without a barrier.
 template <bool TR>
 __device__ __forceinline__ void gather_windows(TID_F Smem& sm, const float* __restrict__ states, int B, const TrainIO& io,
-                                               int b0, bool do_actor) {
+                                               int b0, bool do_actor, const float* __restrict__ rg) {
     {   // <= 3 elements per thread, every load of a round issued before any is used: the
         // training gather is two dependent rounds (row index, then window / loss inputs)
         constexpr int kEl = (TOK * LDX + NTHR - 1) / NTHR;
@@ -1782,6 +1815,10 @@ __device__ __forceinline__ void gather_windows(TID_F Smem& sm, const float* __re
                     const bool m = (s < S - 1) && ((nz >> (LANE() & 48)) & 0xFFFFull) == 0;
                     sm.mask[p * S + s] = m;
                     sm.tmax[t] = rmax;
+#pragma unroll
+                    for (int ti = 0; ti < 2; ++ti)  // layer 0's constants from the table's maxima (rg)
+                        sm.es[ti][t] = (signed char)range_exp(
+                            e_bound_v(range_entry(rg, kRgE + 2 * ti), range_entry(rg, kRgE + 2 * ti + 1), rmax));
                     if (TR && do_actor) {
                         io.mask[(size_t)(b0 + p) * S + s] = m ? 1.f : 0.f;
                         io.tmax[(size_t)(b0 + p) * S + s] = rmax;
@@ -1801,19 +1838,27 @@ __device__ __forceinline__ void gather_windows(TID_F Smem& sm, const float* __re
 
 // The workgroup's layer-0 attention-output scale per trunk (Smem::a0f) from the max over its 80
 // window rows (rows 0..TOK-1 of m, one float each): wave 0, once the rows are visible; read behind
-// a later barrier. The bound holds for every sample of the workgroup. e / a0: the range table's
-// kRgE / kRgA0 constants (in Smem::rtab or in the packed buffer).
-__device__ __forceinline__ void a0f_from_max(TID_F Smem& sm, const float* m, const float* e, const float* a0) {
+// a later barrier. The bound holds for every sample of the workgroup. e / a0: layer 0's constants
+// (policy_layout.hpp kRgE / kRgA0: Smem::rtab, or a0f_consts of the table's maxima).
+// (a0f_load: wave 0's two rows per lane, issued early; a0f_finish: the reduction and the factors)
+__device__ __forceinline__ float a0f_load(TID_F const float* m) {
     static_assert(TOK <= 128, "two rows per lane");
+    const int l = TIDX();
+    return l < 64 ? fmaxf(m[l], l + 64 < TOK ? m[l + 64] : 0.f) : 0.f;
+}
+__device__ __forceinline__ void a0f_finish(TID_F Smem& sm, float v, const float* e, const float* a0) {
     if (TIDX() < 64) {
         const int l = TIDX();
-        const float v = wave_max(fmaxf(m[l], l + 64 < TOK ? m[l + 64] : 0.f));
+        v = wave_max(v);
         if (l < 2) {
             const OpSc f = a0_sc_v(e[2 * l], e[2 * l + 1], a0[2 * l], a0[2 * l + 1], v);
             sm.a0f[2 * l] = f.sc;
             sm.a0f[2 * l + 1] = f.inv;
         }
     }
+}
+__device__ __forceinline__ void a0f_from_max(TID_F Smem& sm, const float* m, const float* e, const float* a0) {
+    a0f_finish(TID_C sm, a0f_load(TID_C m), e, a0);
 }
 __device__ __forceinline__ void a0f_from_tmax(TID_F Smem& sm) {
     if constexpr (UAVHIP_EXP != 62 && UAVHIP_EXP != 63) {
@@ -1883,7 +1928,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             pkv_c = kv_prefetch<kCriticTrunk, 0, TR, kTrainSplit>(TID_C P);
         }
     }
-    gather_windows<TR>(TID_C sm, states, B, io, b0, do_actor);
+    gather_windows<TR>(TID_C sm, states, B, io, b0, do_actor, P + kRangeOff);
     __syncthreads();
     PTR(1);
     // layer 0's attention-output scales, read behind the next barrier (the ring forward: once the
@@ -1905,7 +1950,10 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     }
     // training mode: the actor head's and the critic embedding's / first GEMM's operands are loaded
     // ahead of the actor's LN2 activation stores (layer_tail hook)
-    APre<4> ph;
+    // the head's weight prefetch depth: the training forward holds two blocks (four spilled one,
+    // reloaded behind the activation store burst)
+    constexpr int kHd = TR ? 2 : 4;
+    APre<kHd> ph;
     // the training forward's actor (a lambda: TrainIO::mix calls it after the critic in half the
     // workgroups); the inference forward keeps its inline block below (the same code as before the
     // mix: as a lambda, its register allocation changed and the NOENV build of k_rollout_steps went
@@ -1918,7 +1966,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             PTR(2);
             __syncthreads();
             auto hook = [&] {
-                if (wv < 4) ph = prefetch<4>(TID_C headw_a, D, 16 * wv, 0);
+                if (wv < 4) ph = prefetch<kHd>(TID_C headw_a, D, 16 * wv, 0);
                 if (do_critic && !critic_first) {
                     ep_c = embed_load<kCriticTrunk>(TID_C P);
                     pkv_c = kv_prefetch<kCriticTrunk, 0, TR, kTrainSplit>(TID_C P);
@@ -1927,7 +1975,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             encoder_layer<kActorTrunk, 0, true, TR, decltype(hook), kTrainSplit>(TID_C sm, P, pkv_a, io.L[0], b0, hook);
             __syncthreads();
             PTR(3);
-            head_mlp<kActorHead, 2>(TID_C sm, P, ph, sm.logits);
+            head_mlp<kActorHead, 2, kHd>(TID_C sm, P, ph, sm.logits);
             store_hidden(TID_C sm, io.z[0], b0);  // before the critic's LayerNorm partials reuse sm.z
         }
     };
@@ -1941,10 +1989,10 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             __syncthreads();
             encoder_layer<kActorTrunk, 0, true, TR>(TID_C sm, P, pkv, io.L[0], b0);
         }
-        if (wv < 4) ph = prefetch<4>(TID_C headw_a, D, 16 * wv, 0);
+        if (wv < 4) ph = prefetch<kHd>(TID_C headw_a, D, 16 * wv, 0);
         __syncthreads();
         PTR(3);
-        head_mlp<kActorHead, 2>(TID_C sm, P, ph, sm.logits);
+        head_mlp<kActorHead, 2, kHd>(TID_C sm, P, ph, sm.logits);
     }  // do_actor
     PTR(4);
     // fused env step (ENV): two envs per wave side by side, state loads issued before the critic head
@@ -1980,7 +2028,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
         __syncthreads();
         if constexpr (TR) {
             auto hook = [&] {
-                if (wv < 4) ph = prefetch<4>(TID_C headw_c, D, 16 * wv, 0);
+                if (wv < 4) ph = prefetch<kHd>(TID_C headw_c, D, 16 * wv, 0);
             };
             encoder_layer<kCriticTrunk, 1, true, TR, decltype(hook), kTrainSplit>(TID_C sm, P, pkv, io.L[2], b0, hook);
         } else {
@@ -1993,10 +2041,10 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
                 envgrp::gload_issue(gR, gq, env, b0 + 2 * (int)(tid_env() >> 6) + (le >> 5), le & 31);
             }
         }
-        if (!TR && wv < 4) ph = prefetch<4>(TID_C headw_c, D, 16 * wv, 0);
+        if (!TR && wv < 4) ph = prefetch<kHd>(TID_C headw_c, D, 16 * wv, 0);
         __syncthreads();
         PTR(5);
-        head_mlp<kCriticHead, 1>(TID_C sm, P, ph, sm.value);
+        head_mlp<kCriticHead, 1, kHd>(TID_C sm, P, ph, sm.value);
         PTR(6);
         if (TR) store_hidden(TID_C sm, io.z[1], b0);
     }  // do_critic
@@ -2253,7 +2301,7 @@ __device__ void rows_fill_trunk(Smem& sm, const float* __restrict__ P, const Fil
             zero(lo);
             hgemm_tile<S - 1, 4>(acc, lo, pre.w[j - P0], P, si, D, row, 0, reinterpret_cast<const _Float16*>(sm.ctx), 0);
 #pragma unroll
-            for (int s = 0; s < S - 1; ++s) acc[s] = (acc[s] + lo[s] * kLoScale) * e_sc<trunk>(sm, sm.tmax[s * SPW + i16]).inv;
+            for (int s = 0; s < S - 1; ++s) acc[s] = (acc[s] + lo[s] * kLoScale) * es_factor<trunk, 1>(sm, s * SPW + i16);
         } else {
             gemm_tile<S - 1, KB>(acc, pre.w[j - P0], Win, D, row, 0, sm.ctx, LDH, 0);
         }
@@ -2313,7 +2361,14 @@ __global__ __launch_bounds__(NTHR) void k_policy_rows_fill(const float* __restri
             const float x = (k < IN && b0 + p < rio.B) ? states[((size_t)(b0 + p) * S + s) * IN + k] : 0.f;
             sm.x[i] = x;
             const float rmax = row16_max(fabsf(x));  // the row's range (one 16-lane row per token)
-            if (k == 0) sm.tmax[t] = rmax;
+            if (k == 0) {
+                sm.tmax[t] = rmax;
+#pragma unroll
+                for (int ti = 0; ti < 2; ++ti)  // as gather_windows
+                    sm.es[ti][t] = (signed char)range_exp(
+                        e_bound_v(range_entry(P + kRangeOff, kRgE + 2 * ti), range_entry(P + kRangeOff, kRgE + 2 * ti + 1),
+                                  rmax));
+            }
         }
         __syncthreads();
         rows_fill_trunk<kActorTrunk>(sm, P, fa, rio, b0, [&] { fill_load_w(fc, P); });
@@ -3416,7 +3471,7 @@ __global__ __launch_bounds__(NTHR) void k_ps_f1(const float* __restrict__ P, con
     load_rtab(sm, P);
     [[maybe_unused]] PsInPre wp;
     if constexpr (kPsSplit) ps_inproj_load(wp, P, soff, P + kOffs.o[layer_param(trunk, 0, INB)], tile0);
-    gather_windows<true>(sm, states, B, io, b0, r == 0);  // one workgroup per block writes the rows
+    gather_windows<true>(sm, states, B, io, b0, r == 0, P + kRangeOff);  // one workgroup per block writes the rows
     __syncthreads();
     ps_embed<kPsSplit>(sm, ep, io.e[critic ? 1 : 0], io.h0[critic ? 1 : 0], b0, s, critic ? 1 : 0);
     __syncthreads();
@@ -3441,10 +3496,16 @@ __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, con
     if constexpr (kPsSplit)
         po = hprefetch<2>(P, critic ? split_slot(layer_param(kCriticTrunk, 0, OUTW)) : split_slot(layer_param(kActorTrunk, 0, OUTW)),
                           D, 16 * wv, 0);
+    // the block's window-row maxima (F1's) first: reduced once the rows below have landed (the
+    // vector memory counter retires in order), not waited for ahead of their loads
+    const float a0v = a0f_load(io.tmax + (size_t)b0 * S);
     ps_mask(sm, io.mask, b0);
     load_rtab(sm, P);
-    a0f_from_max(sm, io.tmax + (size_t)b0 * S, P + kRangeOff + kRgE, P + kRangeOff + kRgA0);  // F1's window rows
     ps_rows_in(sm.h, LDH, io.h0[ti], D, 0, D, s, b0);  // the layer input (residual) of the position
+    float ec[8];  // layer 0's constants (kRgE .. kRgA0 + 3) from the table's maxima
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ec[k] = range_entry(P + kRangeOff, kRgE + k);
+    a0f_finish(sm, a0v, ec, ec + 4);
     if (critic) ps_attention<kPsSplit, kCriticTrunk, 0>(sm, io.L[ti].qkv, s, b0, P);
     else ps_attention<kPsSplit, kActorTrunk, 0>(sm, io.L[ti].qkv, s, b0, P);
     [[maybe_unused]] APre<4> ph;
@@ -3874,42 +3935,24 @@ __global__ __launch_bounds__(256) void k_policy_split(const float* __restrict__ 
     dst[64] = w2;
 }
 
-// The range table (policy_layout.hpp) of the flat parameters: block q writes max |param q|; the
-// last block to finish (a ticket counter in the table: policy_split zeroes it with a memset first,
-// and the last block -- here and in k_adam, which refreshes the table after every update -- resets
-// it) derives the operand scales from all of them.
+// The range table (policy_layout.hpp) of the flat parameters: block q writes max |param q|, block 0
+// also the zero slots after the maxima (the kernels derive every scale from the maxima themselves).
 __global__ __launch_bounds__(256) void k_policy_range(const float* __restrict__ flat, float* __restrict__ packed) {
     __shared__ float red[4];
-    __shared__ int last;
     const int q = blockIdx.x;
     float m = 0.f;
     for (int i = tid_x(); i < kSizes[q]; i += 256) m = fmaxf(m, fabsf(flat[kOffs.o[q] + i]));
     m = wave_max(m);
     if (lane_id() == 0) red[tid_x() >> 6] = m;
+    if (q == 0 && tid_x() >= kNumParams && tid_x() < kRangeFloats) packed[kRangeOff + tid_x()] = 0.f;
     __syncthreads();
-    float* tab = packed + kRangeOff;
-    if (tid_x() == 0) {
-        tab[kRgMax + q] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-        __threadfence();
-        last = atomicAdd(reinterpret_cast<unsigned*>(tab + kRgTicket), 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last || tid_x() != 0) return;
-    __threadfence();
-    float t[kRangeFloats] = {};
-    for (int k = 0; k < kNumParams; ++k) t[kRgMax + k] = tab[kRgMax + k];
-    range_derive(t);
-    for (int k = kNumParams; k < kRangeFloats; ++k) tab[k] = t[k];  // (the ticket slot: 0, ready for the next)
+    if (tid_x() == 0) packed[kRangeOff + kRgMax + q] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
 int policy_split(const float* flat, float* packed, hipStream_t st) {
     constexpr int n = (kRangeOff - kOffs.o[kNumParams]) / 8;
     hipLaunchKernelGGL(k_policy_split, dim3((n + 255) / 256), dim3(256), 0, st, flat, packed);
     if (const int rc = check_launch("k_policy_split")) return rc;
-    if (hipMemsetAsync(packed + kRangeOff + kRgTicket, 0, sizeof(unsigned), st) != hipSuccess) {
-        set_error("policy_split: hipMemsetAsync of the range ticket failed");
-        return UAVHIP_EHIP;
-    }
     hipLaunchKernelGGL(k_policy_range, dim3(kNumParams), dim3(256), 0, st, flat, packed);
     return check_launch("k_policy_range");
 }

@@ -88,9 +88,12 @@ constexpr int split_slot(int q) {
 //   attention output  convex combination of V rows: <= D max|W_in| B(input) + max|b_in|
 //   layer-0 input     e (+ pos) <= 14 max|W_e| max_k|x_k| + max|b_e| + max|pos| -- per token, from
 //                     that token's window row (the kernels keep max_k|x_k| of every token in LDS)
-// so the table holds max|param| of every parameter (kept current by k_policy_range after a pack and
-// by k_adam after every update), the per-token constants of layer 0, and the (2^-s, 2^s) pairs of
-// the operands whose bound depends on the weights alone.
+// The packed buffer's table holds max|param| of every parameter (written by k_policy_range after a
+// pack; after every update by k_adam, as atomic maxima) and zeros; each kernel derives the per-token
+// constants of layer 0 and the (2^-s, 2^s) pairs of the operands whose bound depends on the weights
+// alone from those maxima (range_entry: a few flops per entry, at kernel start), so a refresh is
+// order-free and needs no second pass over the blocks' maxima. The host's range_derive fills the
+// same entries into a full table (uavhip_policy_range_table).
 constexpr int kRangeOff = kSplitOffs.o[kNumSplit];
 constexpr int kRangeFloats = 96;
 constexpr int kPackedFloats = kRangeOff + kRangeFloats;  // the inference forward's packed buffer
@@ -99,8 +102,10 @@ enum : int {
     kRgE = 52,      // + 2 t: 14 max|W_e|, + 2 t + 1: max|b_e| + max|pos| (trunk index t: 0 actor, 1 critic)
     kRgA0 = 56,     // + 2 t: D max|W_in(layer 0)|, + 2 t + 1: max|b_in(layer 0)|
     kRgOp = 64,     // + 2 op: 2^-s, + 2 op + 1: 2^s of static operand op
-    kRgTicket = 92  // k_policy_range / k_adam: the last-arriving block's counter (uint32 bits)
+    kRgSpare = 80   // [kRgSpare, kRangeFloats): zero
 };
+// (in the packed buffer only the maxima [kRgMax, kRgMax + kNumParams) are stored; every other entry
+// is what range_entry derives from them)
 enum : int { kOpLn1 = 0, kOpHid = 1, kOpLn2 = 2, kOpAtt = 3 };  // static operand kinds
 // static operand slot of (trunk, layer, kind): actor L0 {LN1, HID}; critic L0 {LN1, HID, LN2};
 // critic L1 {ATT, LN1, HID}; -1: not a static operand (layer 0's attention output, layer-0 input)
@@ -111,7 +116,7 @@ __host__ __device__ constexpr int range_op(int trunk, int layer, int kind) {
                                 : -1;
 }
 constexpr int kNumRangeOps = 8;
-static_assert(kRgOp + 2 * kNumRangeOps <= kRgTicket && kRgTicket < kRangeFloats && kNumParams <= kRgE, "range table");
+static_assert(kRgOp + 2 * kNumRangeOps <= kRgSpare && kRgSpare <= kRangeFloats && kNumParams <= kRgE, "range table");
 __host__ __device__ constexpr int trunk_index(int trunk) { return trunk == kActorTrunk ? 0 : 1; }
 
 // The scale exponent of an operand bounded by B: 0 for B in [2^-4, 2^15) (and for 0, inf, NaN: a
@@ -124,40 +129,46 @@ __host__ __device__ inline int range_exp(float B) {
     const int s = e - 15;
     return s < -100 ? -100 : (s > 100 ? 100 : s);
 }
-// table[kRgMax + q] (max|param q|) -> every derived entry. Host (uavhip_policy_range_table) and
-// device (k_policy_range, k_adam) evaluate the same fp32 operations without contraction: bitwise
-// the same table.
-__host__ __device__ inline void range_derive(float* t) {
+// The bound of static operand op (range_op's numbering) from M = max|param q| (table[kRgMax ..]).
+__host__ __device__ inline float range_bound(const float* M, int op) {
 #pragma clang fp contract(off)
-    const float* M = t + kRgMax;
     constexpr float kLnMax = 11.5f;  // >= sqrt(D - 1): the largest |x^| of a D-feature LayerNorm
-    const int trunks[2] = {kActorTrunk, kCriticTrunk};
-    for (int ti = 0; ti < 2; ++ti) {
-        const int tr = trunks[ti];
-        t[kRgE + 2 * ti] = (float)IN * M[tr + EMB_W];
-        t[kRgE + 2 * ti + 1] = M[tr + EMB_B] + M[tr + POS];
-        t[kRgA0 + 2 * ti] = (float)D * M[layer_param(tr, 0, INW)];
-        t[kRgA0 + 2 * ti + 1] = M[layer_param(tr, 0, INB)];
-    }
-    auto put = [&](int op, float B) {
-        const int s = range_exp(B);
-        t[kRgOp + 2 * op] = ldexpf(1.0f, -s);
-        t[kRgOp + 2 * op + 1] = ldexpf(1.0f, s);
+    const int tr = op < 2 ? kActorTrunk : kCriticTrunk, l = op < 5 ? 0 : 1;
+    auto ln = [&](int layer, int w) { return kLnMax * M[layer_param(tr, layer, w)] + M[layer_param(tr, layer, w + 1)]; };
+    auto hid = [&](int layer) {
+        return (float)D * M[layer_param(tr, layer, L1W)] * ln(layer, N1W) + M[layer_param(tr, layer, L1B)];
     };
-    for (int ti = 0; ti < 2; ++ti) {
-        const int tr = trunks[ti];
-        const int nl = tr == kActorTrunk ? 1 : 2;
-        float ln2_prev = 0.f;
-        for (int l = 0; l < nl; ++l) {
-            if (l > 0) put(range_op(tr, l, kOpAtt), (float)D * M[layer_param(tr, l, INW)] * ln2_prev +
-                                                         M[layer_param(tr, l, INB)]);
-            const float ln1 = kLnMax * M[layer_param(tr, l, N1W)] + M[layer_param(tr, l, N1B)];
-            put(range_op(tr, l, kOpLn1), ln1);
-            put(range_op(tr, l, kOpHid), (float)D * M[layer_param(tr, l, L1W)] * ln1 + M[layer_param(tr, l, L1B)]);
-            ln2_prev = kLnMax * M[layer_param(tr, l, N2W)] + M[layer_param(tr, l, N2B)];
-            if (range_op(tr, l, kOpLn2) >= 0) put(range_op(tr, l, kOpLn2), ln2_prev);
-        }
+    switch (op) {
+        case 0: case 2: case 6: return ln(l, N1W);     // LN1 outputs
+        case 1: case 3: case 7: return hid(l);         // FFN hidden units
+        case 4: return ln(0, N2W);                     // the critic's layer-0 LN2 output (layer 1's input)
+        default:                                       // 5: the critic's layer-1 attention output
+            return (float)D * M[layer_param(tr, 1, INW)] * ln(0, N2W) + M[layer_param(tr, 1, INB)];
     }
+}
+// Derived entry k (kRgE <= k < kRangeFloats; 0 for the spare slots) from M. Host (range_derive:
+// uavhip_policy_range_table) and device (load_rtab and the layer-0 constants of the forward
+// kernels) evaluate the same fp32 operations without contraction: bitwise the same entries.
+__host__ __device__ inline float range_entry(const float* M, int k) {
+#pragma clang fp contract(off)
+    if (k >= kRgE && k < kRgE + 4) {
+        const int tr = k < kRgE + 2 ? kActorTrunk : kCriticTrunk;
+        return (k & 1) ? M[tr + EMB_B] + M[tr + POS] : (float)IN * M[tr + EMB_W];
+    }
+    if (k >= kRgA0 && k < kRgA0 + 4) {
+        const int tr = k < kRgA0 + 2 ? kActorTrunk : kCriticTrunk;
+        return (k & 1) ? M[layer_param(tr, 0, INB)] : (float)D * M[layer_param(tr, 0, INW)];
+    }
+    if (k >= kRgOp && k < kRgOp + 2 * kNumRangeOps) {
+        const int s = range_exp(range_bound(M, (k - kRgOp) >> 1));
+        return ldexpf(1.0f, (k & 1) ? s : -s);
+    }
+    return 0.f;
+}
+static_assert(kRgE % 2 == 0 && kRgA0 % 2 == 0 && kRgOp % 2 == 0, "entry pairs start at even slots");
+// table[kRgMax + q] (max|param q|) -> every derived entry (the host's table)
+__host__ __device__ inline void range_derive(float* t) {
+    for (int k = kRgE; k < kRangeFloats; ++k) t[k] = range_entry(t + kRgMax, k);
 }
 
 }  // namespace pol

@@ -132,7 +132,8 @@ struct SegBatch {
 __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* __restrict__ grads,
                                                       float* __restrict__ sq_part, double* __restrict__ step,
                                                       const AdamHyper h, AdamScalars* __restrict__ sc,
-                                                      float unscale, const float* __restrict__ gsc, int crit_off) {
+                                                      float unscale, const float* __restrict__ gsc, int crit_off,
+                                                      float* __restrict__ range_m) {
     __shared__ float red[4];
     __shared__ float wsum[4][64];
     // segment of this block: lane l tests segment l (one round of kernarg loads, not a dependent
@@ -215,13 +216,16 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const SegBatch sb, float* 
         sq_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
         if (step && blockIdx.x == 0) adam_advance(step, h, sc);  // single-GPU step: these are the final grads
     }
+    // the range table's maxima, ahead of k_adam's atomic maxima (nullable: no update in this call)
+    if (range_m && blockIdx.x == 0 && threadIdx.x < kNumParams) range_m[threadIdx.x] = 0.f;
 }
 
 // Block partial sums of g^2 over the flat gradient after a cross-rank all-reduce (data-parallel
 // UPDATE phase; a single-GPU step takes them from k_reduce_grads); advances Adam's step counter.
 __global__ __launch_bounds__(256) void k_grad_norm(const float* __restrict__ grads, int n, float* __restrict__ sq_part,
                                                    double* __restrict__ step, const AdamHyper h,
-                                                   AdamScalars* __restrict__ sc) {
+                                                   AdamScalars* __restrict__ sc, float* __restrict__ range_m) {
+    if (blockIdx.x == 0 && threadIdx.x < kNumParams) range_m[threadIdx.x] = 0.f;  // as k_reduce_grads'
     __shared__ float red[4];
     float s = 0.f;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) s += grads[i] * grads[i];
@@ -262,6 +266,7 @@ struct AdamBlocks {
     int first[kAdamMaxBlocks];  // its first float4 within the parameter
     int tbase[kAdamMaxBlocks];  // packedT offset of the parameter's transposed copy, -1: none
     int sbase[kAdamMaxBlocks];  // packed offset of the parameter's split copy, -1: none
+    int pbeg[kNumParams + 1];   // parameter q's blocks: [pbeg[q], pbeg[q + 1])
 };
 constexpr int adam_items(int q) { return pad4(kSizes[q]) / 4; }
 constexpr int packedT_base(int q) {
@@ -278,7 +283,8 @@ constexpr int packedT_base(int q) {
 }
 constexpr AdamBlocks make_adam_blocks() {
     AdamBlocks b{};
-    for (int q = 0; q < kNumParams; ++q)
+    for (int q = 0; q < kNumParams; ++q) {
+        b.pbeg[q] = b.n;
         for (int f = 0; f < adam_items(q); f += 256) {
             b.param[b.n] = q;
             b.first[b.n] = f;
@@ -286,6 +292,8 @@ constexpr AdamBlocks make_adam_blocks() {
             b.sbase[b.n] = split_slot(q);
             ++b.n;
         }
+    }
+    b.pbeg[kNumParams] = b.n;
     return b;
 }
 constexpr AdamBlocks kAdamBlocks = make_adam_blocks();
@@ -308,7 +316,6 @@ struct AdamArgs {
     double beta1, beta2, eps;
     float max_norm;
     float *packed, *packedT;  // nullable: refreshed with the updated params
-    float* amax_part;         // [kAdamBlocks.n] per-block max |updated param| (the packed range table)
 };
 
 __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
@@ -361,39 +368,18 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
         *reinterpret_cast<f32x4*>(a.params + f) = p;
     }
     if (!a.packed) return;
-    {   // the packed range table (policy_layout.hpp) of the updated parameters: per block the max
-        // |param|, then the last block to finish (ticket in the table) takes every parameter's max
-        // over its blocks and derives the operand scales the next forward reads
+    {   // the packed range table (policy_layout.hpp) of the updated parameters: each block's max
+        // |param| into its parameter's slot by an atomic max on the float bits (non-negative floats
+        // order like their bits; the slots were zeroed by k_reduce_grads / k_grad_norm, earlier in
+        // this step; order-free, so deterministic). The kernels derive every scale from these maxima.
         float am = live ? fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fmaxf(fabsf(p[2]), fabsf(p[3]))) : 0.f;
         am = wave_max(am);
         __shared__ float amw[4];
-        __shared__ int last;
         if (lane_id() == 0) amw[threadIdx.x >> 6] = am;
         __syncthreads();
-        float* tab = a.packed + kRangeOff;
-        if (threadIdx.x == 0) {
-            a.amax_part[blockIdx.x] = fmaxf(fmaxf(amw[0], amw[1]), fmaxf(amw[2], amw[3]));
-            __threadfence();
-            last = atomicAdd(reinterpret_cast<unsigned*>(tab + kRgTicket), 1u) == gridDim.x - 1;
-        }
-        __syncthreads();
-        if (last) {
-            __threadfence();
-            __shared__ float mq[kNumParams];
-            if (threadIdx.x < kNumParams) {
-                float mx = 0.f;
-                for (int b = 0; b < kAdamBlocks.n; ++b)
-                    if (kAdamBlocks.param[b] == (int)threadIdx.x) mx = fmaxf(mx, a.amax_part[b]);
-                mq[threadIdx.x] = mx;
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                float t[kRangeFloats] = {};
-                for (int k = 0; k < kNumParams; ++k) t[kRgMax + k] = mq[k];
-                range_derive(t);
-                for (int k = 0; k < kRangeFloats; ++k) tab[k] = t[k];  // (the ticket slot: 0, ready for the next)
-            }
-        }
+        if (threadIdx.x == 0)
+            atomicMax(reinterpret_cast<unsigned*>(a.packed + kRangeOff + kRgMax + q),
+                      __float_as_uint(fmaxf(fmaxf(amw[0], amw[1]), fmaxf(amw[2], amw[3]))));
     }
     if (!NC) {  // plain parameters are copied as they are
         if (live) *reinterpret_cast<f32x4*>(a.packed + f) = p;
@@ -468,7 +454,6 @@ struct Plan {
     LayerBufs la, lc0, lc1;
     float *z_a, *z_c, *dz_a, *dz_c, *fpart, *hpart, *epart, *sq_part;
     AdamScalars* adam_sc;  // Adam's step-dependent scalars (k_reduce_grads / k_grad_norm -> k_adam)
-    float* amax_part;      // k_adam's per-block max |param| (the packed range table)
     float* vpart;          // [Bm/16] the forward's per-block value-error maxima (BwdIO::vpart)
     float* gsc;            // 2^k of the critic's gradient scale (heads_bwd -> k_reduce_grads)
     float* wg_part;  // weight-gradient partial tiles [kWgGrid * kWgRuns][kWgSlot]
@@ -528,7 +513,6 @@ inline Plan make_plan(int Bm, float* base) {
     p.epart = w.take((size_t)p.prows * 2 * kEmbPart);
     p.sq_part = w.take(1 << 16);
     p.adam_sc = reinterpret_cast<AdamScalars*>(w.take(4));
-    p.amax_part = w.take(kAdamMaxBlocks);
     p.vpart = w.take((size_t)(Bm / kHeadSamples));
     p.gsc = w.take(4);
     p.wg_part = w.take((size_t)kWgGrid * kWgRuns * kWgSlot);
@@ -708,11 +692,11 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
     if (upd) {
         if (!bwd) {
             hipLaunchKernelGGL(k_grad_norm, dim3(kSqBlocks), dim3(256), 0, st, c->grads, c->n_floats, p.sq_part,
-                               c->adam_step, adam_hyper(c), p.adam_sc);
+                               c->adam_step, adam_hyper(c), p.adam_sc, p.packed + kRangeOff + kRgMax);
             TR_CHECK(check_launch("k_grad_norm"));
         }
         AdamArgs aa{c->params, c->grads, c->adam_m, c->adam_v, p.adam_sc, p.sq_part, n_sq, c->beta1, c->beta2,
-                    c->adam_eps, c->max_grad_norm, p.packed, p.packedT, p.amax_part};
+                    c->adam_eps, c->max_grad_norm, p.packed, p.packedT};
         hipLaunchKernelGGL(k_adam, dim3(kAdamBlocks.n), dim3(256), 0, st, aa);
         TR_CHECK(check_launch("k_adam"));
     }
@@ -907,7 +891,7 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
     // padding floats between parameters stay zero
     hipLaunchKernelGGL(k_reduce_grads, dim3(seg_blocks), dim3(256), 0, st, sb, c->grads, p.sq_part + sq_base, step,
                        adam_hyper(c), p.adam_sc, 1.0f / grad_prescale(Bg), static_cast<const float*>(p.gsc),
-                       kOffs.o[kCriticTrunk]);
+                       kOffs.o[kCriticTrunk], step ? p.packed + kRangeOff + kRgMax : nullptr);
     *n_sq = sq_base + seg_blocks;
     return check_launch("k_reduce_grads");
 }

@@ -366,8 +366,10 @@ def pack_weights(state_dict, device=None):
     for q, o in splits:  # the split copies of the f16-matrix-core GEMM weights
         flat = to_split_fragment_order(items[q][1].detach().to(device=dev, dtype=torch.float32))
         buf[o:o + flat.numel()] = flat
-    if RANGE_FLOATS:
-        buf[total - RANGE_FLOATS:] = range_table([v for _, v in items]).to(dev)
+    if RANGE_FLOATS:  # the packed table holds the maxima only (the kernels derive the scales)
+        t = range_table([v for _, v in items])
+        t[len(items):] = 0.0
+        buf[total - RANGE_FLOATS:] = t.to(dev)
     return buf
 
 
@@ -376,9 +378,10 @@ RANGE_FLOATS = int(LIB.uavhip_policy_range_table(None, None)) if hasattr(LIB, "u
 
 
 def range_table(params):
-    """The packed buffer's closing range table (include/uavhip.h uavhip_policy_range_table) of the
-    50 parameters: their max |value|, then the scales of the split products' operands derived from
-    them by the library's own host code (the floats uavhip_policy_pack writes on the device)."""
+    """The range table (include/uavhip.h uavhip_policy_range_table) of the 50 parameters: their max
+    |value|, then the scales of the split products' operands derived from them by the library's own
+    host code -- bitwise what every kernel derives from the maxima, the part of the table the packed
+    buffer carries (pack_weights)."""
     m = torch.tensor([float(p.detach().abs().max()) for p in params], dtype=torch.float32)
     out = torch.zeros(RANGE_FLOATS, dtype=torch.float32)
     LIB.uavhip_policy_range_table(ctypes.c_void_p(m.data_ptr()), ctypes.c_void_p(out.data_ptr()))

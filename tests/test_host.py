@@ -304,8 +304,9 @@ def test_rollout_step_argument_checks_without_gpu():
 
 
 def test_range_table_scales():
-    """The packed buffer's closing range table (include/uavhip.h uavhip_policy_range_table,
-    policy_layout.hpp): the max |param| of every tensor, the layer-0 constants, and for every static
+    """The range table (include/uavhip.h uavhip_policy_range_table, policy_layout.hpp; the packed
+    buffer carries its maxima, the kernels derive the rest bitwise the same way): the max |param| of
+    every tensor, the layer-0 constants, and for every static
     split-product operand a pair (2^-s, 2^s) -- (1, 1) for the reference's initial weights (results
     bitwise those without scaling), and a power of two putting the operand's bound in [2^14, 2^15)
     when the weights drive it out of [2^-4, 2^15). Each bound holds: the LayerNorm and FFN-hidden
