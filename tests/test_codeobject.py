@@ -96,7 +96,8 @@ READELF = os.environ.get("READELF", "/opt/rocm/lib/llvm/bin/llvm-readelf")
 def test_rollout_steps_carries_one_env_path(tmp_path):
     """k_rollout_steps is instantiated per env-step path (policy.hip kEnvGrp / kEnvWave): with both
     paths compiled in it was 71 KB of code and spilled 28 VGPRs; the grouped instantiation the bench
-    runs is 58.5 KB. Guard on its code size, so both paths do not creep back into one kernel."""
+    runs is 58.5 KB (62 KB since round 5's range scaling). Guard on its code size, so both paths do not
+    creep back into one kernel."""
     out = tmp_path / "rs.o"
     subprocess.run([HIPCC] + [f for f in FLAGS if f != "-S"] + ["--no-gpu-bundle-output", "-c",
                    os.path.join(CSRC, "rollout_steps.hip"), "-o", str(out)], check=True, cwd=CSRC,
@@ -105,4 +106,4 @@ def test_rollout_steps_carries_one_env_path(tmp_path):
     sizes = {l.split()[7]: int(l.split()[2]) for l in syms.splitlines() if " FUNC " in l and "k_rollout_steps" in l}
     print(sizes)
     grp = next(v for k, v in sizes.items() if "k_rollout_stepsILi1E" in k)
-    assert grp <= 62 * 1024, sizes
+    assert grp <= 65 * 1024, sizes
