@@ -3916,6 +3916,7 @@ __global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ f
 // (16-row tile, 32-k block), two f16x8 stores (w1 = f16(w), w2 = f16((w - w1) 2^11), round to nearest).
 __global__ __launch_bounds__(256) void k_policy_split(const float* __restrict__ flat, float* __restrict__ packed) {
     const int i = blockIdx.x * 256 + tid_x();
+    if (i < kRangeFloats) packed[kRangeOff + i] = 0.f;  // the range table, ahead of k_policy_range's maxima
     int si = 0, base = 0;
     while (si < kNumSplit && i >= base + kSizes[kSplitParam[si]] / 8) base += kSizes[kSplitParam[si++]] / 8;
     if (si >= kNumSplit) return;
@@ -3935,25 +3936,30 @@ __global__ __launch_bounds__(256) void k_policy_split(const float* __restrict__ 
     dst[64] = w2;
 }
 
-// The range table (policy_layout.hpp) of the flat parameters: block q writes max |param q|, block 0
-// also the zero slots after the maxima (the kernels derive every scale from the maxima themselves).
+// The range table (policy_layout.hpp) of the flat parameters: kRangeSlices blocks per parameter,
+// each an atomic max of its slice's max |param| on the float bits into the parameter's slot (zeroed
+// by k_policy_split; non-negative floats order like their bits). One block per parameter looped
+// over up to 49 k floats: 28 us per pack.
+constexpr int kRangeSlices = 8;
 __global__ __launch_bounds__(256) void k_policy_range(const float* __restrict__ flat, float* __restrict__ packed) {
     __shared__ float red[4];
-    const int q = blockIdx.x;
+    const int q = blockIdx.x / kRangeSlices, sl = blockIdx.x % kRangeSlices;
+    const int n = kSizes[q], per = (n + kRangeSlices - 1) / kRangeSlices, i0 = sl * per, i1 = min(n, i0 + per);
     float m = 0.f;
-    for (int i = tid_x(); i < kSizes[q]; i += 256) m = fmaxf(m, fabsf(flat[kOffs.o[q] + i]));
+    for (int i = i0 + tid_x(); i < i1; i += 256) m = fmaxf(m, fabsf(flat[kOffs.o[q] + i]));
     m = wave_max(m);
     if (lane_id() == 0) red[tid_x() >> 6] = m;
-    if (q == 0 && tid_x() >= kNumParams && tid_x() < kRangeFloats) packed[kRangeOff + tid_x()] = 0.f;
     __syncthreads();
-    if (tid_x() == 0) packed[kRangeOff + kRgMax + q] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (tid_x() == 0)
+        atomicMax(reinterpret_cast<unsigned*>(packed + kRangeOff + kRgMax + q),
+                  __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 int policy_split(const float* flat, float* packed, hipStream_t st) {
     constexpr int n = (kRangeOff - kOffs.o[kNumParams]) / 8;
     hipLaunchKernelGGL(k_policy_split, dim3((n + 255) / 256), dim3(256), 0, st, flat, packed);
     if (const int rc = check_launch("k_policy_split")) return rc;
-    hipLaunchKernelGGL(k_policy_range, dim3(kNumParams), dim3(256), 0, st, flat, packed);
+    hipLaunchKernelGGL(k_policy_range, dim3(kNumParams * kRangeSlices), dim3(256), 0, st, flat, packed);
     return check_launch("k_policy_range");
 }
 
