@@ -128,12 +128,11 @@ struct Smem {
     float tmax[TOK];            // max_k |x_k| of each token's window row (layer 0's operand range)
     signed char es[2][TOK];     // per trunk and token: layer 0's input scale exponent s (from tmax)
     float a0f[4];               // per trunk: (2^-s, 2^s) of the workgroup's layer-0 attention output
-    float rtab[24];             // the range table's static part (load_rtab, once per launch)
+    float rtab[28];             // the range table's static part (load_rtab, once per launch)
 };
 // Smem::rtab: the static operands' (2^-s, 2^s) pairs, then (14 max|W_e|, max|b_e| + max|pos|) and
 // (D max|W_in|, max|b_in|) of layer 0 per trunk (policy_layout.hpp kRgOp / kRgE / kRgA0)
-constexpr int kRtOp = 0, kRtE = 2 * kNumRangeOps, kRtA0 = kRtE + 4, kRtN = kRtA0 + 4;
-static_assert(kRtN <= 24 && kRgE + 4 == kRgA0, "Smem::rtab");
+static_assert(kRtN <= 28 && kRgE + 4 == kRgA0, "Smem::rtab");
 
 // Lane index plumbing. In the multi-step rollout TU (rollout_steps.hip) every forward helper takes
 // the thread index as a leading parameter, laundered once per step by k_rollout_steps: the
@@ -170,19 +169,13 @@ struct APre {
 __device__ __forceinline__ const float* frag_ptr(TID_F const float* W, int ldw, int row, int kw0) {
     return W + ((size_t)(row >> 4) * (ldw >> 4) + (kw0 >> 4)) * 256 + 4 * LANE();
 }
-template <int D, int N = D>  // N < D: only blocks 0 .. N-1 now (prefetch_rest loads the others)
+template <int D>
 __device__ __forceinline__ APre<D> prefetch(TID_F const float* __restrict__ W, int ldw, int row, int kw0) {
     const float* wp = frag_ptr(TID_C W, ldw, row, kw0);
     APre<D> r;
 #pragma unroll
-    for (int p = 0; p < N; ++p) r.a[p] = *reinterpret_cast<const f32x4*>(wp + 256 * p);
+    for (int p = 0; p < D; ++p) r.a[p] = *reinterpret_cast<const f32x4*>(wp + 256 * p);
     return r;
-}
-template <int N, int D>
-__device__ __forceinline__ void prefetch_rest(TID_F APre<D>& r, const float* __restrict__ W, int ldw, int row, int kw0) {
-    const float* wp = frag_ptr(TID_C W, ldw, row, kw0);
-#pragma unroll
-    for (int p = N; p < D; ++p) r.a[p] = *reinterpret_cast<const f32x4*>(wp + 256 * p);
 }
 
 // acc[ct] += W[row + i][kw0 + k] * X[xtok0 + 16 ct + j][k]  over k in [0, 128), one 16-row tile.
@@ -1846,7 +1839,8 @@ __device__ __forceinline__ float a0f_load(TID_F const float* m) {
     const int l = TIDX();
     return l < 64 ? fmaxf(m[l], l + 64 < TOK ? m[l + 64] : 0.f) : 0.f;
 }
-__device__ __forceinline__ void a0f_finish(TID_F Smem& sm, float v, const float* e, const float* a0) {
+// returns the workgroup's max (wave 0 only; 0 elsewhere)
+__device__ __forceinline__ float a0f_finish(TID_F Smem& sm, float v, const float* e, const float* a0) {
     if (TIDX() < 64) {
         const int l = TIDX();
         v = wave_max(v);
@@ -1855,15 +1849,16 @@ __device__ __forceinline__ void a0f_finish(TID_F Smem& sm, float v, const float*
             sm.a0f[2 * l] = f.sc;
             sm.a0f[2 * l + 1] = f.inv;
         }
+        return v;
     }
+    return 0.f;
 }
-__device__ __forceinline__ void a0f_from_max(TID_F Smem& sm, const float* m, const float* e, const float* a0) {
-    a0f_finish(TID_C sm, a0f_load(TID_C m), e, a0);
+__device__ __forceinline__ float a0f_from_max(TID_F Smem& sm, const float* m, const float* e, const float* a0) {
+    return a0f_finish(TID_C sm, a0f_load(TID_C m), e, a0);
 }
-__device__ __forceinline__ void a0f_from_tmax(TID_F Smem& sm) {
-    if constexpr (UAVHIP_EXP != 62 && UAVHIP_EXP != 63) {
-        a0f_from_max(TID_C sm, sm.tmax, sm.rtab + kRtE, sm.rtab + kRtA0);
-    }
+__device__ __forceinline__ float a0f_from_tmax(TID_F Smem& sm) {
+    if constexpr (UAVHIP_EXP != 62 && UAVHIP_EXP != 63) return a0f_from_max(TID_C sm, sm.tmax, sm.rtab + kRtE, sm.rtab + kRtA0);
+    return 0.f;
 }
 
 // Fused rollout step (uavhip_rollout_step): the env step of the sampled actions (uav_env.py:295-435)
@@ -1933,7 +1928,12 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
     PTR(1);
     // layer 0's attention-output scales, read behind the next barrier (the ring forward: once the
     // actor's prologue loads are issued, so that wave 0's reduction overlaps their round trip)
-    if (!ROWS || !do_actor) a0f_from_tmax(TID_C sm);
+    if (!ROWS || !do_actor) {
+        const float xm = a0f_from_tmax(TID_C sm);
+        if (TR && TIDX() == 0 && io.xmax) io.xmax[blk] = xm;  // the block's range for the weight gradients
+    }
+    // the training forward exports its derived scales for the weight-gradient GEMM (TrainIO::rtab_out)
+    if (TR && blk == 0 && TIDX() < kRtN && io.rtab_out) io.rtab_out[TIDX()] = sm.rtab[TIDX()];
     const int wv = TIDX() >> 6;
     const float* headw_a = P + kOffs.o[kActorHead];
     const float* headw_c = P + kOffs.o[kCriticHead];
@@ -3505,9 +3505,11 @@ __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, con
     float ec[8];  // layer 0's constants (kRgE .. kRgA0 + 3) from the table's maxima
 #pragma unroll
     for (int k = 0; k < 8; ++k) ec[k] = range_entry(P + kRangeOff, kRgE + k);
-    a0f_finish(sm, a0v, ec, ec + 4);
+    const float xm = a0f_finish(sm, a0v, ec, ec + 4);
+    if (r == 0 && tid_x() == 0 && io.xmax) io.xmax[blk] = xm;  // the block's range for the weight gradients
     if (critic) ps_attention<kPsSplit, kCriticTrunk, 0>(sm, io.L[ti].qkv, s, b0, P);
     else ps_attention<kPsSplit, kActorTrunk, 0>(sm, io.L[ti].qkv, s, b0, P);
+    if (blk == 0 && r == 0 && tid_x() < kRtN && io.rtab_out) io.rtab_out[tid_x()] = sm.rtab[tid_x()];  // (as the fused forward)
     [[maybe_unused]] APre<4> ph;
     if constexpr (kPsSplit) {  // the layer tails and the next in_proj as split products
         if (critic) {

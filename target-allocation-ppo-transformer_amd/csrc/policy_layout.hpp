@@ -102,22 +102,28 @@ enum : int {
     kRgE = 52,      // + 2 t: 14 max|W_e|, + 2 t + 1: max|b_e| + max|pos| (trunk index t: 0 actor, 1 critic)
     kRgA0 = 56,     // + 2 t: D max|W_in(layer 0)|, + 2 t + 1: max|b_in(layer 0)|
     kRgOp = 64,     // + 2 op: 2^-s, + 2 op + 1: 2^s of static operand op
-    kRgSpare = 80   // [kRgSpare, kRangeFloats): zero
+    kRgSpare = 84   // [kRgSpare, kRangeFloats): zero
 };
 // (in the packed buffer only the maxima [kRgMax, kRgMax + kNumParams) are stored; every other entry
 // is what range_entry derives from them)
 enum : int { kOpLn1 = 0, kOpHid = 1, kOpLn2 = 2, kOpAtt = 3 };  // static operand kinds
-// static operand slot of (trunk, layer, kind): actor L0 {LN1, HID}; critic L0 {LN1, HID, LN2};
-// critic L1 {ATT, LN1, HID}; -1: not a static operand (layer 0's attention output, layer-0 input)
+// static operand slot of (trunk, layer, kind): actor L0 {LN1 0, HID 1, LN2 8}; critic L0 {LN1 2,
+// HID 3, LN2 4}; critic L1 {ATT 5, LN1 6, HID 7, LN2 9}; -1: not a static operand (layer 0's attention
+// output, layer-0 input). The last layers' LN2 outputs (8, 9) are the heads' inputs: only the
+// weight-gradient GEMM splits them (the heads run on the f32 MFMA).
 __host__ __device__ constexpr int range_op(int trunk, int layer, int kind) {
-    return trunk == kActorTrunk ? (layer == 0 && kind <= kOpHid ? kind : -1)
+    return trunk == kActorTrunk ? (layer == 0 && kind <= kOpHid ? kind : layer == 0 && kind == kOpLn2 ? 8 : -1)
            : layer == 0         ? (kind <= kOpLn2 ? 2 + kind : -1)
-           : layer == 1         ? (kind == kOpAtt ? 5 : kind <= kOpHid ? 6 + kind : -1)
+           : layer == 1         ? (kind == kOpAtt ? 5 : kind <= kOpHid ? 6 + kind : kind == kOpLn2 ? 9 : -1)
                                 : -1;
 }
-constexpr int kNumRangeOps = 8;
+constexpr int kNumRangeOps = 10;
 static_assert(kRgOp + 2 * kNumRangeOps <= kRgSpare && kRgSpare <= kRangeFloats && kNumParams <= kRgE, "range table");
 __host__ __device__ constexpr int trunk_index(int trunk) { return trunk == kActorTrunk ? 0 : 1; }
+// The scales a kernel derives at start (policy.hip load_rtab -> Smem::rtab; the training forward
+// exports them, TrainIO::rtab_out, for the weight-gradient GEMM): the static operands' (2^-s, 2^s)
+// pairs, then layer 0's (14 max|W_e|, max|b_e| + max|pos|) and (D max|W_in|, max|b_in|) per trunk
+constexpr int kRtOp = 0, kRtE = 2 * kNumRangeOps, kRtA0 = kRtE + 4, kRtN = kRtA0 + 4;
 
 // The scale exponent of an operand bounded by B: 0 for B in [2^-4, 2^15) (and for 0, inf, NaN: a
 // non-finite operand stays non-finite), else B 2^-s in [2^14, 2^15). frexp: B = f 2^e, f in [0.5, 1).
@@ -133,7 +139,7 @@ __host__ __device__ inline int range_exp(float B) {
 __host__ __device__ inline float range_bound(const float* M, int op) {
 #pragma clang fp contract(off)
     constexpr float kLnMax = 11.5f;  // >= sqrt(D - 1): the largest |x^| of a D-feature LayerNorm
-    const int tr = op < 2 ? kActorTrunk : kCriticTrunk, l = op < 5 ? 0 : 1;
+    const int tr = op < 2 || op == 8 ? kActorTrunk : kCriticTrunk, l = op < 5 || op == 8 ? 0 : 1;
     auto ln = [&](int layer, int w) { return kLnMax * M[layer_param(tr, layer, w)] + M[layer_param(tr, layer, w + 1)]; };
     auto hid = [&](int layer) {
         return (float)D * M[layer_param(tr, layer, L1W)] * ln(layer, N1W) + M[layer_param(tr, layer, L1B)];
@@ -141,7 +147,8 @@ __host__ __device__ inline float range_bound(const float* M, int op) {
     switch (op) {
         case 0: case 2: case 6: return ln(l, N1W);     // LN1 outputs
         case 1: case 3: case 7: return hid(l);         // FFN hidden units
-        case 4: return ln(0, N2W);                     // the critic's layer-0 LN2 output (layer 1's input)
+        case 4: case 8: return ln(0, N2W);             // layer-0 LN2 outputs (critic: layer 1's input)
+        case 9: return ln(1, N2W);                     // the critic's layer-1 LN2 output
         default:                                       // 5: the critic's layer-1 attention output
             return (float)D * M[layer_param(tr, 1, INW)] * ln(0, N2W) + M[layer_param(tr, 1, INB)];
     }

@@ -23,6 +23,9 @@ struct TrainIO {
     float* xg;                   // [R][16]
     float* mask;                 // [R]
     float* tmax;                 // [R] max |x_k| of each window row (layer 0's operand range; K7 F2 reads it)
+    float* xmax;                 // [Bm/16] max over each 16-sample block's window rows (the weight-gradient
+                                 // GEMM's range of the layer-0 operands; nullable)
+    float* rtab_out;             // [kRtN] the forward's derived scales (policy_layout.hpp kRtOp ..; nullable)
     float *e[2], *h0[2];         // [R][128] actor, critic embeddings (post-ReLU) and layer inputs
     TrainLayerIO L[3];           // actor L0 (pruned), critic L0 (full), critic L1 (pruned)
     float* z[2];                 // [Bm][64] relu(head.0) of the actor / critic head

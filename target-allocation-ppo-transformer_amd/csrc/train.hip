@@ -456,6 +456,8 @@ struct Plan {
     AdamScalars* adam_sc;  // Adam's step-dependent scalars (k_reduce_grads / k_grad_norm -> k_adam)
     float* vpart;          // [Bm/16] the forward's per-block value-error maxima (BwdIO::vpart)
     float* gsc;            // 2^k of the critic's gradient scale (heads_bwd -> k_reduce_grads)
+    float* xmax;           // [Bm/16] the forward's per-block window-row maxima (k_wgrad's layer-0 X range)
+    float* rt;             // [kRtN] the forward's derived scales (TrainIO::rtab_out -> k_wgrad)
     float* wg_part;  // weight-gradient partial tiles [kWgGrid * kWgRuns][kWgSlot]
     float* bpart;    // [prows][kBiasPart] bias partials of K6 / K7
     float* kvc;      // K7: [prows][80][256] each query position's share of every position's dk | dv
@@ -496,6 +498,9 @@ inline Plan make_plan(int Bm, float* base) {
     p.xg = w.take((size_t)R * 16);
     p.mask = w.take(R);
     p.tmax = w.take(R);
+    p.xmax = w.take(Bm / kHeadSamples);
+    static_assert(kRtN <= 32, "Plan::rt");
+    p.rt = w.take(32);
     p.smp = w.take((size_t)Bm * 8);
     p.e_a = w.take((size_t)R * D);
     p.h0_a = w.take((size_t)R * D);
@@ -661,6 +666,8 @@ extern "C" int uavhip_ppo_step(const uavhip_ppo* c, const float* states, const i
         io.xg = p.xg;
         io.mask = p.mask;
         io.tmax = p.tmax;
+        io.xmax = p.xmax;
+        io.rtab_out = p.rt;
         io.e[0] = p.e_a; io.e[1] = p.e_c;
         io.h0[0] = p.h0_a; io.h0[1] = p.h0_c;
         const LayerBufs* lb[3] = {&A, &C0, &C1};
@@ -777,19 +784,24 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         int dst[kWgMaxProbs];
         // X operands the fused forward does not store (wgrad.hpp kWgX*): a LayerNorm output from its
         // x-hat (x-hat * gamma + beta), a layer-0 input from the embedding (e + pos[s])
+        // rk / rarg: the X operand's range for k_wgrad (WgProb::rk), as the forward bounds it
         struct XSrc {
             const float* x;
             int mode;
             const float *g, *b;
+            int rk, rarg;
             XSrc at_token4() const {  // the token-4 rows (stride S D): one position of the pos table
                 return XSrc{x + (S - 1) * D, mode == kWgXPosRow ? (int)kWgXPosFixed : mode, g,
-                            mode == kWgXPosRow ? b + (S - 1) * D : b};
+                            mode == kWgXPosRow ? b + (S - 1) * D : b, rk, rarg};
             }
         };
         auto ln_out = [&](const float* xhat, int tr_, int ly, int w) {  // w = N1W or N2W (+1: bias)
-            return XSrc{xhat, kWgXAffine, prm(c, layer_param(tr_, ly, w)), prm(c, layer_param(tr_, ly, w + 1))};
+            return XSrc{xhat, kWgXAffine, prm(c, layer_param(tr_, ly, w)), prm(c, layer_param(tr_, ly, w + 1)),
+                        kWgRStatic, range_op(tr_, ly, w == N1W ? kOpLn1 : kOpLn2)};
         };
-        auto emb_out = [&](const float* e, int tr_) { return XSrc{e, kWgXPosRow, nullptr, prm(c, tr_ + POS)}; };
+        auto emb_out = [&](const float* e, int tr_) {
+            return XSrc{e, kWgXPosRow, nullptr, prm(c, tr_ + POS), kWgRE, trunk_index(tr_)};
+        };
         // p3: the tiles that keep three-plane products (WgProb::p3_tiles): the key rows of in_proj,
         // whose sums cancel (softmax drops any per-query constant, so a sample's dk rows sum to
         // zero); every other tile is two-plane. UAVHIP_WGRAD_PLANES=3: every tile three-plane.
@@ -798,8 +810,13 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
             dst[wp.b.n] = dst_w;
             wp.add(dY, ldy, X.x, ldx, M, N, K, X.mode, X.g, X.b);
             if (wp.ok) {
-                wp.b.p[wp.b.n - 1].dst = dst_w;
-                wp.b.p[wp.b.n - 1].p3_tiles = all3 ? ~0 : p3;
+                WgProb& Q = wp.b.p[wp.b.n - 1];
+                Q.dst = dst_w;
+                Q.p3_tiles = all3 ? ~0 : p3;
+                Q.rk = X.rk;
+                Q.rarg = X.rarg;
+                Q.rpb = K == R ? S * kHeadSamples : kHeadSamples;  // rows per 16-sample block
+                Q.xmax = p.xmax;
             }
         };
         auto layer_dw = [&](const LayerBufs& B, int tr_, int ly, const XSrc& hin, int rows) {
@@ -815,9 +832,12 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
                 dw(B.dqkv + 2 * D, 3 * D, hin, D, D, D, R, pw + 2 * D * D);
                 dw(B.dqkv + (S - 1) * 3 * D, S * 3 * D, hin.at_token4(), S * D, D, D, Bm, pw);
             }
-            dw(B.dz1, D, XSrc{B.o, kWgX, nullptr, nullptr}, D, D, D, rows, kOffs.o[layer_param(tr_, ly, OUTW)]);
+            const XSrc o = ly == 0 ? XSrc{B.o, kWgX, nullptr, nullptr, kWgRA0, trunk_index(tr_)}
+                                   : XSrc{B.o, kWgX, nullptr, nullptr, kWgRStatic, range_op(tr_, ly, kOpAtt)};
+            dw(B.dz1, D, o, D, D, D, rows, kOffs.o[layer_param(tr_, ly, OUTW)]);
             dw(B.du, FF, ln_out(B.xhat1, tr_, ly, N1W), D, FF, D, rows, kOffs.o[layer_param(tr_, ly, L1W)]);
-            dw(B.df, D, XSrc{B.u, kWgX, nullptr, nullptr}, FF, D, FF, rows, kOffs.o[layer_param(tr_, ly, L2W)]);
+            dw(B.df, D, XSrc{B.u, kWgX, nullptr, nullptr, kWgRStatic, range_op(tr_, ly, kOpHid)}, FF, D, FF, rows,
+               kOffs.o[layer_param(tr_, ly, L2W)]);
         };
         layer_dw(C0, tc, 0, emb_out(p.e_c, tc), R);  // the long problems first
         layer_dw(A, ta, 0, emb_out(p.e_a, ta), Bm);
@@ -825,6 +845,7 @@ static int ppo_backward(const uavhip_ppo* c, const Plan& p, hipStream_t st, int 
         dw(p.dz_a, HID, ln_out(A.xhat2, ta, 0, N2W), D, HID, D, Bm, kOffs.o[kActorHead]);
         dw(p.dz_c, HID, ln_out(C1.xhat2, tc, 1, N2W), D, HID, D, Bm, kOffs.o[kCriticHead]);
         wp.b.part = p.wg_part;
+        wp.b.rt = p.rt;  // the forward's derived scales
         if (wp.ok && wgrad_direct(wp.max_slabs())) {
             // direct mode: one workgroup per output tile writes dW (unscaled) and its g^2 partial; the
             // reduction below covers the other gradients, its g^2 partials after these

@@ -24,6 +24,8 @@
 
 #include <algorithm>
 
+#include "policy_layout.hpp"  // the operand range bounds (range_exp / range_bound / range_entry)
+
 #ifndef UAVHIP_EXP
 #define UAVHIP_EXP 0  // timing experiments (A/B builds, results wrong): 51 no loads after the first two
 #endif                // slabs, 52 one MFMA of six, 53 no split arithmetic
@@ -59,7 +61,14 @@ struct WgProb {
     int p3_tiles;               // bit t: tile t runs three-plane products (else two-plane)
     int chunk;                  // chunked mode: slabs per chunk of this problem's tiles
     int dst;                    // direct mode: float offset of dW [M][N] in `grads`
+    // the X operand's range (policy_layout.hpp): X is staged as X 2^-s and the run's dW multiplied by
+    // 2^s (exact), s from a bound on |X| -- rk: kWgRStatic (rarg = the forward's static operand: its
+    // (2^-s, 2^s) pair), kWgRE / kWgRA0 (layer 0's input / attention output of trunk rarg: from the
+    // run's rows' block maxima xmax, rpb rows each, and the forward's layer-0 constants)
+    int rk, rarg, rpb;
+    const float* xmax;
 };
+enum { kWgRNone = 0, kWgRStatic = 1, kWgRE = 3, kWgRA0 = 4 };
 // Direct mode (small minibatches: every tile a few slabs): one workgroup per output tile runs all
 // of its slabs and writes dW itself -- times `unscale` (BwdIO::gscale undone, exact) -- into the
 // flat gradient, with the block's sum of squares in sq[blockIdx.x]; no partial tiles, no reduction.
@@ -75,6 +84,7 @@ struct WgBatch {
     float unscale;
     const float* gsc;  // the critic's extra 2^k (heads_bwd): problems with dst >= crit_off
     int crit_off;
+    const float* rt;   // the training forward's derived scales (TrainIO::rtab_out, policy_layout.hpp kRtOp ..)
 };
 constexpr int kWgDirectMaxSlabs = 12;  // direct mode only when no tile has more slabs (K <= 384 rows)
 
@@ -196,13 +206,14 @@ __device__ __forceinline__ void wg_split_store(const f32x4 v, char* plane, int o
 // the X operand as the forward formed it: x-hat * gamma + beta (its LayerNorm epilogue's expression),
 // e + pos[s] (gamma 1: exact), or x itself (applied at staging: the slab's loads have landed by then)
 template <bool P3>
-__device__ __forceinline__ void wg_stage_store(const WgSlab& r, char* stage, int xmode, const f32x4 xg) {
+__device__ __forceinline__ void wg_stage_store(const WgSlab& r, char* stage, int xmode, const f32x4 xg, float xsc) {
     const int t = threadIdx.x, c4 = t & 31;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int off = wg_swz((t >> 5) + 16 * i, c4 >> 1) + 8 * (c4 & 1);
         wg_split_store<P3>(r.a[i], stage, off);
-        wg_split_store<P3>(xmode != kWgX ? r.b[i] * xg + r.x[i] : r.b[i], stage + 3 * kWgPlaneB, off);
+        // X 2^-s (xsc, exact): every element inside fp16's range (wg_xrange)
+        wg_split_store<P3>((xmode != kWgX ? r.b[i] * xg + r.x[i] : r.b[i]) * xsc, stage + 3 * kWgPlaneB, off);
     }
 }
 // 16 columns (c16 .. c16 + 15) x 8 consecutive k (8 g ..) of a plane: lane (i16, g) gets column
@@ -216,6 +227,52 @@ __device__ __forceinline__ wg_f16x8 wg_frag(const char* plane, int c16) {
     return wg_f16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
+// The exponent s of the X operand of rows [k0, k1) of problem P (WgProb::rk). Block-uniform; the
+// dynamic kinds reduce the rows' block maxima over the workgroup (one barrier).
+__device__ __forceinline__ float wg_dpp_max(float v) {
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xF, 0xF, true)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, true)));
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+// (xsc, xinv) = (2^-s, 2^s) of the X operand of rows [k0, k1) of problem P (WgProb::rk), every
+// operand a plain (vector) load issued behind the run's first slab loads: their in-order wait adds no
+// round trip. Uniform over the workgroup; the dynamic kinds reduce many blocks with one barrier.
+__device__ __forceinline__ void wg_xrange(const WgBatch& wb, const WgProb& P, int k0, int k1, float* wred, float& xsc,
+                                          float& xinv) {
+#pragma clang fp contract(off)
+    xsc = xinv = 1.f;
+    const float* rt = wb.rt;
+    if (P.rk == kWgRNone || !rt) return;
+    if (P.rk == kWgRStatic) {
+        xsc = rt[pol::kRtOp + 2 * P.rarg];
+        xinv = rt[pol::kRtOp + 2 * P.rarg + 1];
+        return;
+    }
+    float m = 0.f;
+    const int b0 = k0 / P.rpb, b1 = (k1 - 1) / P.rpb;  // the run's 16-sample blocks
+    if (b1 - b0 < 32) {  // few: every thread takes them all (no barrier)
+        for (int b = b0; b <= b1; ++b) m = fmaxf(m, P.xmax[b]);
+    } else {
+        for (int b = b0 + (int)threadIdx.x; b <= b1; b += kWgThreads) m = fmaxf(m, P.xmax[b]);
+        m = wg_dpp_max(m);
+        if ((threadIdx.x & 63) == 0) wred[threadIdx.x >> 6] = m;
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < kWgThreads / 64; ++w) m = fmaxf(m, wred[w]);
+    }
+    const int t = P.rarg;
+    float B = rt[pol::kRtE + 2 * t] * m + rt[pol::kRtE + 2 * t + 1];
+    if (P.rk == kWgRA0) B = rt[pol::kRtA0 + 2 * t] * B + rt[pol::kRtA0 + 2 * t + 1];
+    const int xs = pol::range_exp(B);
+    xsc = ldexpf(1.0f, -xs);
+    xinv = ldexpf(1.0f, xs);
+}
+
 // One tile run's k-loop: slabs s0 .. s0 + n_slabs - 1 of problem P into hi / mid / lo. P3: the
 // three-plane products (6 MFMAs per block); otherwise two planes (x = x1 + 2^-11 x2, dropped terms
 // 2^-22 of a product: hi += a1b1, mid += a1b2 + a2b1, lo += a2b2, 4 MFMAs), for the tiles whose sums
@@ -223,12 +280,15 @@ __device__ __forceinline__ wg_f16x8 wg_frag(const char* plane, int c16) {
 template <bool P3>
 __device__ __forceinline__ void wg_kloop(char* wg_smem, const WgProb& P, int s0, int n_slabs, int m0, int n0, int mt0,
                                          int nt0, f32x4 (&hi)[4][2], f32x4 (&mid)[4][2], f32x4 (&lo)[4][2],
-                                         [[maybe_unused]] int run) {
+                                         [[maybe_unused]] int run, const WgBatch& wb, float* wred, float& xinv) {
         const int xmode = P.xmode;
         const f32x4 xg = wg_xgamma(P, n0);
         WgSlab nx;
         wg_gload(nx, P, s0 * kWgBK, m0, n0);
-        wg_stage_store<P3>(nx, wg_smem, xmode, xg);
+        // the X range behind the first slab's loads (its own loads then cost no extra round trip)
+        float xsc;
+        wg_xrange(wb, P, s0 * kWgBK, (s0 + n_slabs) * kWgBK, wred, xsc, xinv);
+        wg_stage_store<P3>(nx, wg_smem, xmode, xg, xsc);
         if (n_slabs > 1) wg_gload(nx, P, (s0 + 1) * kWgBK, m0, n0);
         __syncthreads();
         WTR(1 + 4 * run);
@@ -266,7 +326,7 @@ __device__ __forceinline__ void wg_kloop(char* wg_smem, const WgProb& P, int s0,
                     lo[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[a], b2[b], lo[a][b], 0, 0, 0);
                 }
             if (s + 1 < n_slabs) {  // slab s + 1 (landed in registers meanwhile) -> the other stage
-                wg_stage_store<P3>(nx, wg_smem + ((s + 1) & 1) * kWgStageB, xmode, xg);
+                wg_stage_store<P3>(nx, wg_smem + ((s + 1) & 1) * kWgStageB, xmode, xg, xsc);
                 if (s + 2 < n_slabs && UAVHIP_EXP != 51) wg_gload(nx, P, (s0 + s + 2) * kWgBK, m0, n0);
             }
             __syncthreads();  // the next stage is written; everyone is done reading this one
@@ -275,6 +335,7 @@ __device__ __forceinline__ void wg_kloop(char* wg_smem, const WgProb& P, int s0,
 
 __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
     __shared__ __attribute__((aligned(16))) char wg_smem[2 * kWgStageB];
+    __shared__ float wred[kWgThreads / 64];
     const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, i16 = l & 15, g = l >> 4;
     const int mt0 = 4 * (wv & 1), nt0 = 2 * (wv >> 1);  // this wave's first m-tile / n-tile
     const long long U = wb.units, G = gridDim.x;
@@ -308,8 +369,9 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
         for (int a = 0; a < 4; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) hi[a][b] = mid[a][b] = lo[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if ((P.p3_tiles >> tile) & 1) wg_kloop<true>(wg_smem, P, s0, n_slabs, m0, n0, mt0, nt0, hi, mid, lo, run);
-        else wg_kloop<false>(wg_smem, P, s0, n_slabs, m0, n0, mt0, nt0, hi, mid, lo, run);
+        float xinv;  // 2^s of the run's X operand (wg_xrange)
+        if ((P.p3_tiles >> tile) & 1) wg_kloop<true>(wg_smem, P, s0, n_slabs, m0, n0, mt0, nt0, hi, mid, lo, run, wb, wred, xinv);
+        else wg_kloop<false>(wg_smem, P, s0, n_slabs, m0, n0, mt0, nt0, hi, mid, lo, run, wb, wred, xinv);
         WTR(2 + 4 * run);
         // lane (i16, g) of tile (a, b) holds dW[m0 + 16 (mt0 + a) + 4 g + r][n0 + 16 (nt0 + b) + i16]
         if (wb.direct) {  // the whole tile: dW itself, unscaled, rows < M (a 64-row problem), and g^2
@@ -319,7 +381,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
 #pragma unroll
                 for (int b = 0; b < 2; ++b) {
                     const f32x4 v = (hi[a][b] + (mid[a][b] + lo[a][b] * (1.0f / 2048.0f)) * (1.0f / 2048.0f)) *
-                                    (P.dst >= wb.crit_off ? wb.unscale * wb.gsc[0] : wb.unscale);
+                                    (P.dst >= wb.crit_off ? wb.unscale * wb.gsc[0] : wb.unscale) * xinv;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int row = m0 + 16 * (mt0 + a) + 4 * g + r;
@@ -346,7 +408,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const WgBatch wb) {
         for (int a = 0; a < 4; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
-                const f32x4 v = hi[a][b] + (mid[a][b] + lo[a][b] * (1.0f / 2048.0f)) * (1.0f / 2048.0f);
+                const f32x4 v = (hi[a][b] + (mid[a][b] + lo[a][b] * (1.0f / 2048.0f)) * (1.0f / 2048.0f)) * xinv;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) out[(16 * (mt0 + a) + 4 * g + r) * kWgT + 16 * (nt0 + b) + i16] = v[r];
             }
@@ -387,6 +449,10 @@ struct WgPlan {
         P.p3_tiles = ~0;
         P.chunk = 0;
         P.dst = 0;
+        P.rk = kWgRNone;
+        P.rarg = 0;
+        P.rpb = 1;
+        P.xmax = nullptr;
         b.units += P.tiles * P.slabs;
         b.tiles += P.tiles;
     }

@@ -21,11 +21,11 @@ from conftest import has_gpu
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_gpu(), reason="needs an MI355X")]
 
 
-def _buffers(n, seed=11, rscale=1.0):
+def _buffers(n, seed=11, rscale=1.0, sscale=1.0):
     """rscale: the scale of the old values and returns (configs[4]'s 64 x 128 scenes give returns of
-    ~1e3: target values {4..16} x 128 targets, discounted over ~160 steps)."""
+    ~1e3: target values {4..16} x 128 targets, discounted over ~160 steps); sscale: of the windows."""
     g = torch.Generator(device="cpu").manual_seed(seed)
-    states = torch.randn(n, 5, 14, generator=g) * 0.5
+    states = torch.randn(n, 5, 14, generator=g) * 0.5 * sscale
     states[: n // 3, :2] = 0          # padded windows (masked keys)
     states[n // 3: n // 2, :4] = 0    # only the current step
     acts = torch.randint(0, 2, (n,), generator=g)
@@ -684,8 +684,9 @@ def _fp64_reference_grads(net, bufs, idx):
     return {k: p.grad for k, p in ref.named_parameters()}, dys
 
 
-@pytest.mark.parametrize("Bm,rscale", [(64, 1.0), (4096, 1.0), (64, 1e3), (4096, 1e3), (64, 1e5), (4096, 1e5)])
-def test_gradients_per_element_vs_fp64(Bm, rscale):
+@pytest.mark.parametrize("Bm,rscale,sscale", [(64, 1.0, 1.0), (4096, 1.0, 1.0), (64, 1e3, 1.0), (4096, 1e3, 1.0),
+                                               (64, 1e5, 1.0), (4096, 1e5, 1.0), (64, 1.0, 3e4), (4096, 1.0, 3e4)])
+def test_gradients_per_element_vs_fp64(Bm, rscale, sscale):
     """Every gradient ELEMENT of the HIP step against fp64 autograd on the CPU.
     The backward carries its gradients pre-scaled by the power of two >= Bm (BwdIO::gscale), so the
     dY operands of the split-product dX GEMMs are O(1) instead of O(1/Bm) (at Bm = 4096 the actor
@@ -701,13 +702,16 @@ def test_gradients_per_element_vs_fp64(Bm, rscale):
     many elements needed the second clause; and the |dY| quantiles of the trunk outputs and embeddings
     (unscaled, as the loss defines them). rscale = 1e3: old values and returns of configs[4]'s scale
     (VERDICT r04 item 1), where the critic's gradients are ~1e3 x larger; 1e5: past fp16's range
-    unless the critic's gradients are scaled by the minibatch's largest value error (heads_bwd)."""
+    unless the critic's gradients are scaled by the minibatch's largest value error (heads_bwd).
+    sscale = 3e4: windows whose layer-0 embeddings (~1e5) and attention outputs leave fp16's range,
+    so the training forward and the weight-gradient GEMM scale those operands (k_wgrad's per-run
+    exponent from the forward's block maxima, WgProb::rk)."""
     from uavhip.policy import TransformerActorCritic, layout
     from uavhip.train import FusedPPOTrainer
     torch.manual_seed(31)
     net = TransformerActorCritic().cuda()
     n = 2 * Bm
-    bufs = _buffers(n, seed=32, rscale=rscale)
+    bufs = _buffers(n, seed=32, rscale=rscale, sscale=sscale)
     idx = torch.randperm(n, generator=torch.Generator().manual_seed(33))[:Bm]
     ref64, dys = _fp64_reference_grads(net, bufs, idx)
     ref32 = copy.deepcopy(net).cpu()
@@ -751,7 +755,18 @@ def test_gradients_per_element_vs_fp64(Bm, rscale):
     pt = float(torch.cat(rels_t).quantile(0.99))
     print(f"Bm {Bm}: worst bar use HIP {worst_hip:.3f}, torch fp32 CPU {worst_t32:.3f}; p99 rel HIP {ph:.2e}, "
           f"torch fp32 {pt:.2e}; {n_second} element(s) passed by the fp32-reference clause")
-    assert not bad, f"elements outside both per-element bars: {bad}"
+    assert bool(torch.isfinite(grads).all()), "non-finite gradient"
+    if sscale == 1.0:
+        assert not bad, f"elements outside both per-element bars: {bad}"
+    else:
+        # windows of ~1e4: fp32 itself is ill-conditioned there (the LayerNorms of ~1e5-scale rows:
+        # torch fp32 misses fp64 by ~1e-1 relative at p99), so per element neither fp32
+        # implementation tracks fp64 and the bar is the distribution: the HIP step's median and p99
+        # relative error no worse than torch fp32's
+        mh = float(torch.cat(rels_h).median())
+        mt = float(torch.cat(rels_t).median())
+        print(f"Bm {Bm} windows x{sscale:g}: median rel HIP {mh:.2e}, torch fp32 {mt:.2e}")
+        assert mh <= mt + 1e-6, (mh, mt)
     assert ph <= 2 * pt + 1e-6, (ph, pt)
 
 

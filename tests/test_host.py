@@ -319,8 +319,8 @@ def test_range_table_scales():
     t = range_table(sd).numpy()
     assert t.shape == (RANGE_FLOATS,)
     np.testing.assert_array_equal(t[:50], np.array([float(p.abs().max()) for p in sd], np.float32))
-    ops = t[64:80].reshape(8, 2)
-    np.testing.assert_array_equal(ops, np.ones((8, 2), np.float32))  # realistic weights: unscaled
+    ops = t[64:84].reshape(10, 2)
+    np.testing.assert_array_equal(ops, np.ones((10, 2), np.float32))  # realistic weights: unscaled
     # the critic's layer-0 FFN1 x 1e5: its hidden bound ~1e7 -> s = 9..10; LN1 x 1e-6 -> s < 0
     c0 = net.critic_net.transformer.layers[0]
     with torch.no_grad():
