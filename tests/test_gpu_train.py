@@ -171,8 +171,8 @@ def _trainer_state(tr):
 @pytest.mark.parametrize("Bm", [64, 4096])
 def test_ppo_step_is_deterministic(Bm):
     """The HIP step reduces every partial in a fixed order (k_wgrad's stream-K partial tiles,
-    k_reduce_grads, the backward's per-workgroup partials, k_adam's norm; k_adam's one atomic is the
-    ticket that picks the block deriving the range table, from maxima -- order-free): the same 4
+    k_reduce_grads, the backward's per-workgroup partials, k_adam's norm; k_adam's one atomic per block
+    is a max into the range table -- order-free): the same 4
     FULL steps run twice from the same state give bitwise the same parameters, Adam moments and
     step counter, gradients, loss sums and statistics. The torch-on-GPU reference of the Adam tests
     is checked the same way and the result printed (its run-to-run behaviour is torch's / the BLAS
