@@ -321,18 +321,26 @@ def test_range_table_scales():
     np.testing.assert_array_equal(t[:50], np.array([float(p.abs().max()) for p in sd], np.float32))
     ops = t[64:84].reshape(10, 2)
     np.testing.assert_array_equal(ops, np.ones((10, 2), np.float32))  # realistic weights: unscaled
-    # the critic's layer-0 FFN1 x 1e5: its hidden bound ~1e7 -> s = 9..10; LN1 x 1e-6 -> s < 0
+    # the critic's layer-0 FFN1 x 1e5: its hidden bound ~1e7 -> s = 9..10; LN1 x 1e-6 -> s < 0; the
+    # last LayerNorms (the heads' inputs, static operands 8 / 9 of the weight-gradient GEMM) x 1e5
     c0 = net.critic_net.transformer.layers[0]
+    a0 = net.actor_net.transformer.layers[0]
+    c1 = net.critic_net.transformer.layers[1]
     with torch.no_grad():
         c0.linear1.weight.mul_(1e5)
         c0.norm1.weight.mul_(1e-6)
         c0.norm1.bias.mul_(1e-6)
+        a0.norm2.weight.mul_(1e5)
+        c1.norm2.weight.mul_(1e5)
     sd = list(net.state_dict().values())
     t = range_table(sd).numpy()
     ln1 = 11.5 * float(c0.norm1.weight.abs().max()) + float(c0.norm1.bias.abs().max())
     hid = 128 * float(c0.linear1.weight.abs().max()) * ln1 + float(c0.linear1.bias.abs().max())
+    ln2a = 11.5 * float(a0.norm2.weight.abs().max()) + float(a0.norm2.bias.abs().max())
+    ln2c = 11.5 * float(c1.norm2.weight.abs().max()) + float(c1.norm2.bias.abs().max())
     assert not 2 ** -4 <= ln1 < 2 ** 15  # LN1's output is driven out of the unscaled band
-    for op, bound in ((2, ln1), (3, hid)):  # critic layer 0: LN1, HID (policy_layout.hpp range_op)
+    assert not ln2a < 2 ** 15 and not ln2c < 2 ** 15
+    for op, bound in ((2, ln1), (3, hid), (8, ln2a), (9, ln2c)):  # policy_layout.hpp range_op
         sc, inv = t[64 + 2 * op], t[65 + 2 * op]
         assert sc * inv == 1.0 and np.log2(inv) == round(np.log2(inv))
         if 2 ** -4 <= bound < 2 ** 15:
