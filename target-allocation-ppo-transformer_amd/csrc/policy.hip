@@ -1760,7 +1760,7 @@ __global__ __launch_bounds__(64) void k_loss_partials(const TrainIO io) {
 // of the trajectory buffer (idx < 0: a padding row, computed on row 0 and flagged by action -1 in
 // smp, so it adds nothing to the loss or gradients) and, if `writer`, stores the windows, the mask
 // and the per-sample loss inputs into the workspace. Ends without a barrier.
-template <bool TR>
+template <bool TR, bool RING = false>  // RING: only position 4's exponents are read (the new row's)
 __device__ __forceinline__ void gather_windows(TID_F Smem& sm, const float* __restrict__ states, int B, const TrainIO& io,
                                                int b0, bool do_actor, const float* __restrict__ rg) {
     {   // <= 3 elements per thread, every load of a round issued before any is used: the
@@ -1808,6 +1808,8 @@ __device__ __forceinline__ void gather_windows(TID_F Smem& sm, const float* __re
                     const bool m = (s < S - 1) && ((nz >> (LANE() & 48)) & 0xFFFFull) == 0;
                     sm.mask[p * S + s] = m;
                     sm.tmax[t] = rmax;
+                    // element u's rows start at token u NTHR / LDX: the ring forward needs position 4 only
+                    if (!RING || (u * NTHR) / LDX >= (S - 1) * SPW)
 #pragma unroll
                     for (int ti = 0; ti < 2; ++ti)  // layer 0's constants from the table's maxima (rg)
                         sm.es[ti][t] = (signed char)range_exp(
@@ -1923,7 +1925,7 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             pkv_c = kv_prefetch<kCriticTrunk, 0, TR, kTrainSplit>(TID_C P);
         }
     }
-    gather_windows<TR>(TID_C sm, states, B, io, b0, do_actor, P + kRangeOff);
+    gather_windows<TR, ROWS>(TID_C sm, states, B, io, b0, do_actor, P + kRangeOff);
     __syncthreads();
     PTR(1);
     // layer 0's attention-output scales, read behind the next barrier (the ring forward: once the
@@ -3468,10 +3470,10 @@ __global__ __launch_bounds__(NTHR) void k_ps_f1(const float* __restrict__ P, con
     // every global operand of the embedding and of the in_proj GEMM first: their L2 round trip
     // overlaps the window gather's
     const PsEmbPre ep = ps_embed_load(P, trunk, s);
-    load_rtab(sm, P);
     [[maybe_unused]] PsInPre wp;
     if constexpr (kPsSplit) ps_inproj_load(wp, P, soff, P + kOffs.o[layer_param(trunk, 0, INB)], tile0);
     gather_windows<true>(sm, states, B, io, b0, r == 0, P + kRangeOff);  // one workgroup per block writes the rows
+    load_rtab(sm, P);  // behind the gather's loads (its arithmetic waits on nothing they need)
     __syncthreads();
     ps_embed<kPsSplit>(sm, ep, io.e[critic ? 1 : 0], io.h0[critic ? 1 : 0], b0, s, critic ? 1 : 0);
     __syncthreads();
@@ -3500,8 +3502,8 @@ __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, con
     // vector memory counter retires in order), not waited for ahead of their loads
     const float a0v = a0f_load(io.tmax + (size_t)b0 * S);
     ps_mask(sm, io.mask, b0);
-    load_rtab(sm, P);
     ps_rows_in(sm.h, LDH, io.h0[ti], D, 0, D, s, b0);  // the layer input (residual) of the position
+    load_rtab(sm, P);  // behind the loads above
     float ec[8];  // layer 0's constants (kRgE .. kRgA0 + 3) from the table's maxima
 #pragma unroll
     for (int k = 0; k < 8; ++k) ec[k] = range_entry(P + kRangeOff, kRgE + k);
@@ -3560,9 +3562,9 @@ __global__ __launch_bounds__(NTHR) void k_ps_f3(const float* __restrict__ P, con
     // the out-projection's first weight blocks ahead of the attention (as k_ps_f2)
     [[maybe_unused]] HPre<2> po;
     if constexpr (kPsSplit) po = hprefetch<2>(P, split_slot(layer_param(kCriticTrunk, 1, OUTW)), D, 16 * wv, 0);
-    load_rtab(sm, P);
     ps_mask(sm, io.mask, b0);
     ps_rows_in(sm.h, LDH, io.L[1].h2, D, 0, D, S - 1, b0);  // layer 1's input (residual) at position 4
+    load_rtab(sm, P);  // behind the loads above
     ps_attention<kPsSplit, kCriticTrunk, 1>(sm, io.L[2].qkv, S - 1, b0, P);
     APre<4> ph;
     if constexpr (kPsSplit) {  // the residual is in sm.h (ps_rows_in): PSX = 2
