@@ -45,6 +45,7 @@ Launch for N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.p
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -95,14 +96,25 @@ def _kernel_base(name):
     return re.sub(r"<.*>$", "", name).split("::")[-1].strip()
 
 
+def _round_files(pattern, exclude=None):
+    """profiles/<tag>_... files in round order: tags rNN<suffix> sort by round, then suffix length, then
+    suffix (r05t < r05aa: a measurement set tagged after r05z), so files[-1] is the newest set."""
+    import glob
+    files = [f for f in glob.glob(os.path.join(ROOT, "profiles", pattern)) if not (exclude and exclude in f)]
+
+    def key(f):
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, os.path.basename(f))
+    return sorted(files, key=key)
+
+
 def profiled_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/rNN_pmc.json, written by scripts/summarize_profile.py from separate rocprofv3
     --pmc FETCH_SIZE / WRITE_SIZE passes of this benchmark; FETCH doubled per the gfx950 note).
     Matched on the exact name first, then on the name without namespaces / template arguments
     (a template kernel such as k_rollout_steps<1> is reported with its arguments)."""
-    import glob
-    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")) if "train" not in f)
+    files = _round_files("r*_pmc.json", exclude="train")
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -121,8 +133,7 @@ def profiled_kernel_time(kernel):
     (profiles/rNN_pmc.json kernel_stats, scripts/profile.sh in the same gpurun lease as a bench run of
     the same code): the average over every launch of the profiled bench run (warm-up and capture
     launches included) and over its timed launches only (summarize_profile.py TIMED_LAUNCHES)."""
-    import glob
-    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")) if "train" not in f)
+    files = _round_files("r*_pmc.json", exclude="train")
     if not files:
         return None
     ks = json.load(open(files[-1])).get("kernel_stats", {})
@@ -185,8 +196,7 @@ def env_share_traffic():
     newest profiles/rNN_env_share.json (scripts/profile_env_share.sh: PMC FETCH/WRITE passes of the
     product build and of a build with the env step compiled out; the difference), with the
     profiled time differential of the same runs."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_env_share.json")))
+    files = _round_files("r*_env_share.json")
     if not files:
         return None, None, None
     d = json.load(open(files[-1]))
@@ -200,8 +210,7 @@ def env_counters(kernel, grid=None):
     VALU busy share of SIMD cycles, HBM bytes per launch (FETCH x 2 + WRITE). Matched by kernel name
     without template arguments AND launch grid (threads) when the file keys its entries "name@grid"
     (one template instance serves several shapes)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_env_counters.json")))
+    files = _round_files("r*_env_counters.json")
     if not files:
         return None
     ks = json.load(open(files[-1]))["kernels"]
