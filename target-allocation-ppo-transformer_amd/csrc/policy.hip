@@ -1171,9 +1171,9 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     _Float16* const cp = reinterpret_cast<_Float16*>(sm.ctx);
     f32x4 h1[CT];  // LN1's output: LN2's residual
     HPre<2> w1a;
-    // the operand scales (policy_layout.hpp range table): the attention output (layer 0: per sample,
-    // the lane's column i16), LN1's output, the FFN hidden units; LN2's output when it is the next
-    // layer's split operand
+    // the operand scales (policy_layout.hpp range table): the attention output (layer 0: one per
+    // workgroup, att_sc), LN1's output, the FFN hidden units; LN2's output when it is the next layer's
+    // split operand
     const OpSc s_ln1 = op_sc<trunk, layer, kOpLn1>(sm), s_hid = op_sc<trunk, layer, kOpHid>(sm);
     if constexpr (TR)  // attention output
         store_rows_planes(TID_C cp, io.o, D, 0, D, t0, b0, last, t1,
@@ -1190,8 +1190,7 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
             zero(hi);
             zero(lo);
             hgemm_tile<CT, 2>(TID_C hi, lo, po, P, so, D, 16 * wv, 0, cp, t0);
-            // read behind the GEMM: held across it, the per-sample factor cost the loop 4 VGPR spills
-            const float att_inv = att_sc<trunk, layer>(sm, LANE() & 15).inv;
+            const float att_inv = att_sc<trunk, layer>(sm, LANE() & 15).inv;  // uniform (SGPRs)
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) acc[ct] = (hi[ct] + lo[ct] * kLoScale) * att_inv;
         }
