@@ -19,12 +19,16 @@ NAMES = {0: "start", 1: "x+mask", 2: "a.embed", 3: "a.layer+sync", 4: "a.head", 
          7: "sample", 60: "env.sync", 61: "env.loads", 62: "env.step", 63: "env.store",
          55: "C0.LN1 acc ready", 56: "C0.LN1 partials", 57: "C0.LN1 barrier", 23: "C0.LN2 acc ready",
          39: "C0.LN2 partials", 58: "C0.LN2 barrier"}
+ENVFINE = {40: "g.pair reads", 41: "g.rev loop", 42: "g.accept", 43: "g.rew/done", 44: "g.pair+push_obs",
+           45: "g.write_obs"}
 LAYER = ["start", "c0 gemm", "c0 sync", "c0 attn+sync", "c1 gemm", "c1 sync", "c1 attn+sync", "outproj", "sync",
          "LN1+sync", "FFN1", "sync", "FFN2+sync", "store+sync", "LN2"]
 for li, tag in enumerate(["A", "C0", "C1"]):
     for j, n in enumerate(LAYER):
         NAMES[8 + 16 * li + j] = f"{tag}.{n}"
     NAMES[8 + 16 * li + 13] = f"{tag}.ring gemm"
+if os.environ.get("ENVFINE") == "1":  # a make TRACE=1 ENVFINE=1 build: stamps inside the env step
+    NAMES.update(ENVFINE)
 
 B = int(os.environ.get("B", "4096"))
 torch.manual_seed(0)
@@ -76,7 +80,7 @@ if os.environ.get("WAVES") == "8":  # a TRACE_WAVES=8 build: [64 workgroups][8 w
         print(f"{k:3d} {NAMES[k]:18s} " + " ".join(f"{int(np.median(rel[:, w, k])):7d}" for w in range(8)))
     sys.exit(0)
 t = buf.reshape(256, 2, 64).astype(np.int64)
-slots = sorted((k for k in NAMES if (t[:, 0, k] != 0).all()), key=lambda k: np.median(t[:, 0, k] - t[:, 0, 0]))
+slots = sorted((k for k in NAMES if (t[:, 0, k] != 0).all() and k not in ENVFINE), key=lambda k: np.median(t[:, 0, k] - t[:, 0, 0]))
 base = t[:, :, 0:1]
 rel = t - base
 print(f"B={B}; median cycles since block start (wave0 / wave4) and per-phase delta (wave0)")
@@ -86,6 +90,12 @@ for k in slots:
     m4 = int(np.median(rel[:, 1, k])) if (t[:, 1, k] != 0).all() else -1
     print(f"{k:3d} {NAMES[k]:18s} {m0:8d} {m4:8d}  +{m0 - prev:6d}")
     prev = m0
+if os.environ.get("ENVFINE") == "1":  # conditional stamps: only blocks whose stamp lies in this step's env step
+    print("env step detail (wave 0; median cycles since env.loads over the blocks that stamped the slot)")
+    for k in sorted(ENVFINE):
+        ok = (t[:, 0, k] >= t[:, 0, 61]) & (t[:, 0, k] <= t[:, 0, 62])
+        if ok.any():
+            print(f"{k:3d} {ENVFINE[k]:18s} {int(np.median(t[ok, 0, k] - t[ok, 0, 61])):8d}  ({int(ok.sum())} blocks)")
 start = t[:, 0, 0]
 end = t[:, 0, 63 if ENV else 7]
 dur = (t[:, 0, 63 if ENV else 7] - t[:, 0, 0]).astype(np.float64)

@@ -31,6 +31,9 @@ constexpr int L = 32;  // lanes per env
 #define UAVHIP_EXP 0
 #endif
 constexpr int kAttr = UAVHIP_EXP;
+#ifndef GTR  // phase stamps inside gstep (policy.hip, make TRACE=1 ENVFINE=1 only)
+#define GTR(id) do {} while (0)
+#endif
 // (24: the window registers take 1.0 instead of memory, so no later window row is padding: a zero
 // window would turn the policy's ring loads of padded positions into reads of one hot row, policy.hip)
 constexpr int kWin = 96;  // LDS scratch per env: window at [2, 72), new row at [72, 86)
@@ -45,7 +48,6 @@ struct GRegs {
     long long sb;
     double r, J, asg_cost, cov_val, tot_cost, tot_val, sum_pd, sum_pf, pd_cur, pp_cur;
     double den_c, rcp_c, den_v, rcp_v, rcp_m;
-    double rcp_n;  // lane j: RN(1 / (j + 1))
     // single-step use (TAB = false, the fused rollout): which per-target / per-UAV entries the step
     // changed, so gstore_delta writes only those -- bit 0: all (a reset), bit 1: target ct and UAV cu
     // (an accepted assign); group-uniform
@@ -146,7 +148,12 @@ __device__ void gpush_obs(GRegs& R, int j) {
         *reinterpret_cast<f32x4*>(w + 76) = f32x4{(float)chi_mc, (float)p_km, (float)pjp, (float)hat_p};
         *reinterpret_cast<f32x4*>(w + 80) =
             f32x4{(float)prev_rev / 16.0f, (float)hat_G / 16.0f, (float)d_pkm, (float)d_pm};
-        *reinterpret_cast<f32x2*>(w + 84) = f32x2{(float)d_G / 16.0f, 1.0f};
+        // the constant feature materialised here: left to itself the compiler takes 1.0f from the high
+        // half of a spilled register pair, a scratch round trip on the step's dependency chain (measured
+        // -0.5 us per rollout step, same box)
+        float one;
+        asm volatile("v_mov_b32 %0, 1.0" : "=v"(one));
+        *reinterpret_cast<f32x2*>(w + 84) = f32x2{(float)d_G / 16.0f, one};
     }
     R.w0 = w[16 + j];
     R.w1 = w[16 + L + j];
@@ -169,7 +176,7 @@ __device__ __forceinline__ void gwrite_obs(float* o, const GRegs& R, int j, bool
 
 __device__ void gwrite_info(const GRegs& R, double is_valid, double* o, int j) {
     const int cnt = R.nasg;
-    const double y = cnt > 0 ? gsh_d(R.rcp_n, cnt - 1) : 0.0;
+    const double y = cnt > 0 ? 1.0 / (double)cnt : 0.0;  // RN(1 / cnt): envdev's rcp_n[cnt - 1]
     const double avg_d = cnt > 0 ? div_by(R.sum_pd, (double)cnt, y) : 0.0;
     const double avg_f = cnt > 0 ? div_by(R.sum_pf, (double)cnt, y) : 0.0;
     if (j == 0) {
@@ -298,7 +305,6 @@ __device__ __forceinline__ void gload_finish(GRegs& R, const GPending& q, const 
     R.ppen = R.sel ? q.ppb[1] : q.ppb[0];
     gset_scene_divisors(R);
     R.rcp_m = 1.0 / (double)M;
-    R.rcp_n = 1.0 / (double)(j + 1);
     R.pp_cur = R.u < N ? gsh_d(R.ppen, R.u) : 0.0;
 }
 // Multi-step launches (once per launch): the plain order, scene index first (fewer live registers).
@@ -339,7 +345,6 @@ __device__ void gload_regs(GRegs& R, const uavhip_env& env, int e, int j) {
     drain_loads();
     gset_scene_divisors(R);
     R.rcp_m = 1.0 / (double)M;
-    R.rcp_n = 1.0 / (double)(j + 1);
     R.pp_cur = R.u < N ? gsh_d(R.ppen, R.u) : 0.0;
 }
 
@@ -456,6 +461,7 @@ __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int 
         const int nlk_t = gsh_i(R.nlk, t);
         const double nhf_new = nhf_t * (1.0 - pf);
         const int ncov_new = R.ncov + (nlk_t == 0 ? 1 : 0);
+        GTR(40);
         // J(X') revenue: sum over locked targets in list order (:252-265)
         const bool mine = j == t;
         const double nh = mine ? nhf_new : R.nhf;
@@ -470,6 +476,7 @@ __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int 
             const double tj = grl_d(term, jj);
             if ((mine_bits >> jj) & 1u) rev = rev + tj;
         }
+        GTR(41);
         const double ucost_u = gsh_d(R.ucost, u);
         const double cost_all = R.asg_cost + ucost_u;  // exact for costs in {1, 1.25}
         const double J = rev - (env.prm[UAVHIP_PRM_OMEGA] * cost_all);
@@ -508,18 +515,26 @@ __device__ void gstep(GRegs& R, const uavhip_env& env, int e, int j, int a, int 
         R.t = t + 1;
         if (R.t >= M) { R.u += 1; R.t = 0; }
     }
+    GTR(42);
     const bool done = R.u >= N;       // :355-356
     if (done) reward = reward + R.r;  // :361-363 goal reward r(X_final)
     const double is_valid = a == 1 ? (reward != 0.0 ? 1.0 : 0.0) : -1.0;
-    if (info_o) gwrite_info(R, is_valid, info_o, j);
+    // the next observation row before the step's stores: with the stores ahead of the pair's load the
+    // wait for the load is a wait for them too (one in-order vector memory counter)
+    if (!done) {
+        GTR(43);
+        gload_cur_pair<TAB>(R, env);
+        gpush_obs(R, j);
+        GTR(44);
+    }
+    if (info_o) gwrite_info(R, is_valid, info_o, j);  // before a reset clears the registers
     if (j == 0) {
         if (rew_o) *rew_o = reward;
         if (done_o) *done_o = done ? 1 : 0;
     }
     if (!done) {
-        gload_cur_pair<TAB>(R, env);
-        gpush_obs(R, j);
         if (obs_o) gwrite_obs(obs_o, R, j, false, obs_f16(env));
+        GTR(45);
     } else if (auto_reset) {
         R.ep += 1;
         const int P = env.full_reset_period;

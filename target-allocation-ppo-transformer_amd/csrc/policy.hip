@@ -30,6 +30,17 @@
 //    parity is defined on logits / logp / value / entropy for given actions).
 #include "common.hpp"
 #include "env_device.hpp"
+#if defined(UAVHIP_POLICY_TRACE) && defined(UAVHIP_STEPS_TU) && defined(UAVHIP_ENV_FINE)
+// make TRACE=1 ENVFINE=1 (k_rollout_steps only): stamps inside the grouped env step (env_group.hpp
+// GTR, slots 40-47) in the same buffer as PTR, waves 0 and 4 of the first 256 workgroups
+namespace uavhip { namespace pol { __device__ unsigned long long g_strace[256 * 2 * 64]; } }
+#define UAVHIP_STRACE_DEFINED 1
+#define GTR(id)                                                                                  \
+    do {                                                                                         \
+        if ((tid_x() & 255) == 0 && blockIdx.x < 256)                                        \
+            ::uavhip::pol::g_strace[(blockIdx.x * 2 + (tid_x() >> 8)) * 64 + (id)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#endif
 #include "env_group.hpp"
 #include "policy_layout.hpp"
 #include "policy_train.hpp"
@@ -84,7 +95,9 @@ constexpr bool kExpHotRing = UAVHIP_EXP == 32;
 #define g_btrace g_sbtrace
 #endif
 constexpr int kTraceSlots = 64;
+#ifndef UAVHIP_STRACE_DEFINED
 __device__ unsigned long long g_ptrace[256 * 2 * kTraceSlots];
+#endif
 #ifdef UAVHIP_TRACE_ALLWAVES  // make TRACE=1 TRACE_WAVES=8: all 8 waves of the first 64 workgroups
 #define PTR(id)                                                                                  \
     do {                                                                                         \
