@@ -40,7 +40,11 @@ Also reported (same JSON line):
                 rank 0 at N = 1 only, bounded sample
   cpu_env_baseline  UAVEnv.step alone (C oracle, reference algorithm) on all host cores (one process
                 per core, <= 16), 10 s
-Launch for N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Launch for N > 1: `python bench.py --gpus N` starts the N rank processes itself (launch_plan /
+spawn_ranks: RANK / LOCAL_RANK / WORLD_SIZE, MASTER_ADDR 127.0.0.1), or under a launcher
+(python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N), whose WORLD_SIZE must equal N.
+The N > 1 exchange (collective all-gather after each rollout, or pipelined peer copies beside the next
+rollout) is chosen by a short untimed measurement of both; the line reports both (exchange.calibration).
 """
 import argparse
 import json
@@ -279,8 +283,8 @@ def parse():
     ap.add_argument("--no-env-diff", action="store_true",
                     help="skip the env step's live differential and phase share (child processes; A/B runs)")
     ap.add_argument("--rccl-gather", action="store_true",
-                    help="N > 1: the exchange as one RCCL all-gather after each rollout instead of the pipelined "
-                         "peer-to-peer copies beside the next rollout (uavhip.dist.IpcAllGather)")
+                    help="N > 1: only the collective all-gather after each rollout (no pipelined peer-to-peer "
+                         "copies, uavhip.dist.IpcAllGather); by default the faster of the two, measured, is timed")
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the dropin_loop leg (main_train.py's loop at E = 1 through the drop-ins)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -651,9 +655,96 @@ def dropin_loop_rate(N, M, seconds, cpu_seconds=None):
     return res
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(gpus, environ, device_count=None):
+    """How `bench.py --gpus N` runs. Returns one of
+      ("run", world)       -- this process is a rank (WORLD_SIZE set by a launcher, or N = 1);
+      ("spawn", [env, ...]) -- N > 1 and no launcher: start N rank processes with these environments
+                              (RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+                              MASTER_PORT), relay rank 0's line, exit with the worst rank's code;
+      ("error", message)   -- WORLD_SIZE disagrees with --gpus, N < 1, or more RCCL ranks than devices
+                              (RCCL runs one rank per device; BENCH_DIST_BACKEND=gloo rehearses N ranks
+                              on fewer GPUs).
+    Decided before anything touches the GPU (device_count: torch.cuda.device_count(), which does not
+    initialise the device on this image)."""
+    if gpus < 1:
+        return ("error", f"--gpus {gpus}: need at least one GPU")
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            return ("error", f"WORLD_SIZE={ws} from the launcher but --gpus {gpus}: they must agree")
+        return ("run", int(ws))
+    if gpus == 1:
+        return ("run", 1)
+    backend = environ.get("BENCH_DIST_BACKEND", "nccl")
+    if backend == "nccl" and device_count is not None and device_count < gpus:
+        return ("error", f"--gpus {gpus} over RCCL needs {gpus} devices, {device_count} visible "
+                         f"(BENCH_DIST_BACKEND=gloo rehearses the ranks on fewer GPUs)")
+    port = str(_free_port())
+    envs = []
+    for r in range(gpus):
+        e = dict(environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC: the only mode the host driver supports
+        envs.append(e)
+    return ("spawn", envs)
+
+
+def spawn_ranks(envs, argv, grace_s=120.0, script=None):
+    """Run one bench.py process per rank (child processes; this parent never touches the GPU).
+    The children share this process's stdout / stderr, so rank 0's JSON line is the parent's output.
+    If a rank fails, the others get `grace_s` to finish (they may wait in a collective for it), then
+    are terminated. Returns the worst exit code (0 only if every rank exited 0)."""
+    import signal
+    import subprocess
+    script = script or os.path.abspath(__file__)
+    procs = [subprocess.Popen([sys.executable, script] + list(argv), env=e) for e in envs]
+
+    def forward(sig, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        failed_at = None
+        while any(p.poll() is None for p in procs):
+            if failed_at is None and any(p.returncode not in (None, 0) for p in procs):
+                failed_at = time.monotonic()
+            if failed_at is not None and time.monotonic() - failed_at > grace_s:
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+                time.sleep(10)
+                for p in procs:
+                    if p.poll() is None:
+                        p.kill()
+            time.sleep(0.2)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    if bad:
+        print(f"[bench] rank exit codes {codes}", file=sys.stderr)
+        return bad[0] if bad[0] > 0 else 1
+    return 0
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    plan = launch_plan(args.gpus, os.environ, device_count=torch.cuda.device_count())
+    if plan[0] == "error":
+        print(f"[bench] {plan[1]}", file=sys.stderr)
+        sys.exit(2)
+    if plan[0] == "spawn":
+        sys.exit(spawn_ranks(plan[1], sys.argv[1:]))
+    world = plan[1]
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -719,29 +810,68 @@ def main():
             xchg = None
             xchg_err = xchg_err or "the IPC mapping failed on another rank"
 
-    def iteration(eager=False):
+    def it_gather(eager=False):  # the exchange as one collective all-gather after the rollout
         eng.collect(eager=eager)
         if dist is not None:
-            if xchg is None:
-                eng.gather()
-                return
-            if xchg.pending is not None:
-                eng.gather_finish(xchg)  # the previous iteration's exchange, beside this rollout
-            eng.gather_submit(xchg)
+            eng.gather()
+
+    def it_pipelined(eager=False):  # the exchange as peer copies beside the next rollout
+        eng.collect(eager=eager)
+        if xchg.pending is not None:
+            eng.gather_finish(xchg)  # the previous iteration's exchange, beside this rollout
+        eng.gather_submit(xchg)
+
+    def drain():
+        if xchg is not None and xchg.pending is not None:
+            eng.gather_finish(xchg)
+            eng.gather()
+
+    def pipelined_check():
+        """The last drained pipelined exchange (the engine's current iteration) against the collective
+        all_gather of the same payloads, bitwise, on every rank."""
+        from uavhip.dist import all_gather_rows, pack_compact
+        tr_ = eng.traj
+        ref = all_gather_rows(pack_compact(tr_.obs, tr_.actions, tr_.logp, tr_.values, tr_.ret, tr_.adv,
+                                           tr_.dones).view(1, -1))
+        same = torch.tensor([int(torch.equal(ref, xchg.recv[(xchg.k - 1) & 1]))], device=dev, dtype=torch.int32)
+        dist.all_reduce(same, op=dist.ReduceOp.MIN)
+        return bool(same.item())
+
+    def per_iteration_ms(body, n):  # steady state, untimed region: max over ranks
+        torch.cuda.synchronize()
+        dist.barrier()
+        a = time.perf_counter()
+        for _ in range(n):
+            body()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([(time.perf_counter() - a) / n * 1e3], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item()
 
     for _ in range(args.warmup):
-        iteration()
-    if xchg is not None and xchg.pending is not None:
-        eng.gather_finish(xchg)
+        it_gather()
+    iteration, calibration = it_gather, None
+    if dist is not None:
+        # N > 1: the exchange the timed loop uses is chosen by measurement (VERDICT r05 item 1): a few
+        # untimed steady-state iterations of each, max over ranks; the faster one runs the timed loop
+        calibration = {"iterations_each": 3, "collective_ms_per_iteration": per_iteration_ms(it_gather, 3),
+                       "collective": f"{dist.get_backend()} all-gather after each rollout"}
+        if xchg is not None:
+            it_pipelined()  # fills the pipeline: every timed call below finishes one exchange and submits one
+            calibration["pipelined_ms_per_iteration"] = per_iteration_ms(it_pipelined, 3)
+            drain()
+            calibration["pipelined_check"] = pipelined_check()
+            if calibration["pipelined_ms_per_iteration"] < calibration["collective_ms_per_iteration"]:
+                iteration = it_pipelined
+        calibration["chosen"] = "pipelined" if iteration is it_pipelined else "collective"
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         iteration(eager=(i == args.steps - 1))
-    if xchg is not None:  # the last iteration's exchange (exposed: inside the timed region)
-        eng.gather_finish(xchg)
-        eng.gather()
+    drain()  # the last iteration's pipelined exchange (exposed: inside the timed region)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -755,19 +885,15 @@ def main():
     value = env_steps / elapsed
 
     exchange = None
-    if dist is not None:  # the exchange kind, and the pipelined copies checked against RCCL's all-gather
-        exchange = {"kind": "rccl all-gather after each rollout" if xchg is None else
-                    "peer-to-peer copies out of IPC-mapped buffers, pipelined beside the next rollout",
-                    "fallback_reason": xchg_err, "check": None}
-        if xchg is not None:
-            from uavhip.dist import all_gather_rows, pack_compact
-            tr_ = eng.traj
-            ref = all_gather_rows(pack_compact(tr_.obs, tr_.actions, tr_.logp, tr_.values, tr_.ret, tr_.adv,
-                                               tr_.dones).view(1, -1))
-            same = torch.tensor([int(torch.equal(ref, xchg.recv[(xchg.k - 1) & 1]))], device=dev, dtype=torch.int32)
-            dist.all_reduce(same, op=dist.ReduceOp.MIN)
-            exchange["check"] = bool(same.item())
-            exchange["check_what"] = "the last timed iteration's gathered payloads == RCCL all_gather of the same payloads, bitwise, every rank"
+    if dist is not None:  # the exchange used, how it was chosen, and the pipelined copies checked
+        pipelined = iteration is it_pipelined
+        exchange = {"kind": "peer-to-peer copies out of IPC-mapped buffers, pipelined beside the next rollout"
+                    if pipelined else f"{dist.get_backend()} all-gather after each rollout",
+                    "fallback_reason": xchg_err, "calibration": calibration,
+                    "check": pipelined_check() if pipelined else calibration.get("pipelined_check"),
+                    "check_what": ("the gathered payloads of the last " + ("timed" if pipelined else "calibration")
+                                   + " iteration's pipelined exchange == the collective all_gather of the same "
+                                   "payloads, bitwise, every rank") if xchg is not None else None}
 
     timeline = None
     if dist is not None:  # one more iteration, untimed, with the phases separated: rollout | exchange
@@ -923,7 +1049,8 @@ def main():
             "data": "synthetic (on-device Philox scenes, "
             "random-init policy, actions sampled from the policy)",
             "config": {"workload": "BASELINE configs[2]: full rollout (policy fwd -> sample -> env.step) + GAE"
-                       + (" + trajectory all-gather (" + ("RCCL" if xchg is None else "pipelined peer copies")
+                       + (" + trajectory all-gather (" + ("pipelined peer copies" if iteration is it_pipelined
+                                                                     else dist.get_backend() + " all-gather")
                           + ")" if world > 1 else ""),
                        "envs_per_gpu": E, "uavs": args.uavs, "targets": args.targets, "horizon": T,
                        "env_steps_per_step": E * T * world, "parallelism": f"env-sharded x{world}",
