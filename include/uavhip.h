@@ -278,10 +278,15 @@ int uavhip_policy_pack(const float* flat, float* packed, uavhip_stream_t stream)
 /* The range table that ends the packed buffer (its last n floats, n = the return value): the
  * split products multiply every activation operand by a power of two 2^-s before splitting it into
  * fp16 planes and the GEMM output by 2^s, with s from a rigorous bound on the operand's magnitude
- * (0 on realistic weights), so no operand the reference's fp32 can hold leaves fp16's range.
+ * (0 on realistic weights), so no ACTIVATION operand the reference's fp32 can hold leaves fp16's
+ * range (a bound that overflows fp32 takes the largest exponent, s = 113). The weights themselves
+ * are not scaled: their split copies hold f16(w), so a parameter of magnitude >= 65520 makes the
+ * outputs non-finite (never silently wrong); max_abs is the caller's check for that.
  * The packed buffer's table holds the maxima (max |param| of each state_dict tensor, floats 0..49;
  * the rest zero; uavhip_policy_pack writes them, an UPDATE step refreshes them) and every kernel
- * derives the scales from them. Host side: max_abs[50] (key order) -> table[n]: the maxima, the
+ * derives the scales from them. NaN elements do not count in a maximum (the device reduces with
+ * fmaxf; the ctypes mirror drops them the same way), so host and device tables agree for any
+ * parameters. Host side: max_abs[50] (key order) -> table[n]: the maxima, the
  * per-token constants of layer 0 and the static operands' (2^-s, 2^s) pairs -- bitwise what the
  * kernels derive. Either pointer NULL: only returns n. */
 int32_t uavhip_policy_range_table(const float* max_abs, float* table);

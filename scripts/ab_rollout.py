@@ -21,6 +21,7 @@ for r in range(rounds):
         env.pop("UAVHIP_LIB", None)
         if b != "base":
             env["UAVHIP_LIB"] = os.path.join(ROOT, "scripts", b, "libuavhip.so")
+            env["UAVHIP_ACCEPT_PREV_ABI"] = "1"
         out = subprocess.run([sys.executable, "bench.py", "--no-ppo", "--no-env-fused", "--no-cpu-baseline", "--no-env-diff",
                               "--no-dropin", "--no-e2e",
                               "--steps", "20", "--warmup", "3", *extra], cwd=ROOT, env=env, capture_output=True,

@@ -15,6 +15,6 @@ if [ -n "$AB" ]; then
   tail -4 gpurun_out/ab_$TAG.txt
 fi
 for b in $TRACES; do
-  UAVHIP_LIB=$PWD/scripts/$b/libuavhip.so STEPS=1 timeout -k 10 180 python scripts/policy_trace.py > gpurun_out/trace_${TAG}_$b.log 2>&1 || { tail -20 gpurun_out/trace_${TAG}_$b.log; exit 1; }
+  UAVHIP_ACCEPT_PREV_ABI=1 UAVHIP_LIB=$PWD/scripts/$b/libuavhip.so STEPS=1 timeout -k 10 180 python scripts/policy_trace.py > gpurun_out/trace_${TAG}_$b.log 2>&1 || { tail -20 gpurun_out/trace_${TAG}_$b.log; exit 1; }
   echo "== $b"; tail -3 gpurun_out/trace_${TAG}_$b.log | head -1
 done

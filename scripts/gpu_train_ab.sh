@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 for b in base $AB; do
   OUT=$GRAFT_REPO_ROOT/gpurun_out/trab_${TAG}_$b
   mkdir -p $OUT
-  if [ $b = base ]; then unset UAVHIP_LIB; else export UAVHIP_LIB=$GRAFT_REPO_ROOT/scripts/$b/libuavhip.so; fi
+  if [ $b = base ]; then unset UAVHIP_LIB; else export UAVHIP_LIB=$GRAFT_REPO_ROOT/scripts/$b/libuavhip.so UAVHIP_ACCEPT_PREV_ABI=1; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o run -- python3 $GRAFT_REPO_ROOT/scripts/train_probe.py > $OUT/probe.log 2>&1 || { tail -20 $OUT/probe.log; exit 1; }
   echo "== $b"; grep "bs=" $OUT/probe.log
   python3 - $OUT <<'EOF'

@@ -766,7 +766,8 @@ __device__ __forceinline__ float attn_sc(const Smem& sm, int p) {
 }
 // PLANES: the output goes to sm.ctx as the two fp16 planes of the split products (the out-projection's
 // operand), scaled for layer `layer` of trunk `trunk`.
-template <bool PLANES = false, int trunk = kCriticTrunk, int layer = 1>
+// (no defaults: every call site names the operand whose scale the planes carry -- ADVICE r05)
+template <bool PLANES, int trunk, int layer>
 __device__ void attention_full(TID_F Smem& sm, int c, const float* __restrict__ P = nullptr) {
     f32x4 o[3];
     attention_full_core(TID_C sm, c, o);
@@ -813,7 +814,7 @@ __device__ __forceinline__ void attention_out(TID_F Smem& sm, int c, int ti, int
     if constexpr (PLANES) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw(ti, 4 * c * HD + d0), o * sc);
     else *reinterpret_cast<f32x4*>(sm.ctx + ti * LDH + 4 * c * HD + d0) = o;
 }
-template <bool PLANES = false, int trunk = kCriticTrunk, int layer = 1>
+template <bool PLANES, int trunk, int layer>
 __device__ void attention_chunk(TID_F Smem& sm, int c, int qs0, int nqs, const float* __restrict__ P = nullptr) {
     const int ntask = nqs * SPW * 4;
     for (int task = TIDX() >> 2; task < ntask; task += NTHR / 4) {
@@ -1708,7 +1709,7 @@ __device__ __forceinline__ void store_hidden(TID_F const Smem& sm, float* __rest
 // One sample's four terms from its smp row o[0..4] (action, old logp, old value, return, advantage)
 // and its logits / value -> t[4].
 __device__ __forceinline__ void loss_terms(const float (&o)[5], float l0, float l1, float v, float eps_clip,
-                                           float* t) {
+                                           float* t, float* verr = nullptr) {
     const CatVals c = categorical(l0, l1);
     const float logp = o[0] > 0.f ? c.lc1 : c.lc0;
     const float ratio = expf(logp - o[1]);
@@ -1722,10 +1723,12 @@ __device__ __forceinline__ void loss_terms(const float (&o)[5], float l0, float 
     t[1] = pad ? 0.f : (v - R) * (v - R);
     t[2] = pad ? 0.f : (vc - R) * (vc - R);
     t[3] = pad ? 0.f : -(c.lc0 * c.p0 + c.lc1 * c.p1);
+    // the largest value error itself (its square overflows fp32 from |v - R| ~ 1.8e19 on: ADVICE r05)
+    if (verr) *verr = pad ? 0.f : fmaxf(fabsf(v - R), fabsf(vc - R));
 }
 // the block's sums in sample order (threads 0-3, one term each) -> fpart[blk][4]; thread 4: the
-// block's largest value error max(|v - R|, |vc - R|) -> vpart[blk] (the critic backward's gradient
-// scale, heads_bwd)
+// block's largest value error max(|v - R|, |vc - R|) (red[4 SPW + i], loss_terms' verr) -> vpart[blk]
+// (the critic backward's gradient scale, heads_bwd)
 __device__ __forceinline__ void loss_block_sums(TID_F const float* red, float* fpart, float* vpart, int blk) {
     if (TIDX() < 4) {
         float acc = 0.f;
@@ -1733,8 +1736,8 @@ __device__ __forceinline__ void loss_block_sums(TID_F const float* red, float* f
         fpart[blk * 4 + TIDX()] = acc;
     } else if (TIDX() == 4 && vpart) {
         float m = 0.f;
-        for (int i = 0; i < SPW; ++i) m = fmaxf(m, fmaxf(red[4 * i + 1], red[4 * i + 2]));
-        vpart[blk] = sqrtf(m);
+        for (int i = 0; i < SPW; ++i) m = fmaxf(m, red[4 * SPW + i]);
+        vpart[blk] = m;
     }
 }
 __device__ void loss_partials(TID_F Smem& sm, const TrainIO& io, int b0) {
@@ -1747,7 +1750,7 @@ __device__ void loss_partials(TID_F Smem& sm, const TrainIO& io, int b0) {
         o[6] = l1;
         o[7] = v;
         const float oi[5] = {o[0], o[1], o[2], o[3], o[4]};
-        loss_terms(oi, l0, l1, v, io.eps_clip, red + 4 * p);
+        loss_terms(oi, l0, l1, v, io.eps_clip, red + 4 * p, red + 4 * SPW + p);
     }
     __syncthreads();
     loss_block_sums(TID_C red, io.fpart, io.vpart, b0 / SPW);
@@ -1755,12 +1758,12 @@ __device__ void loss_partials(TID_F Smem& sm, const TrainIO& io, int b0) {
 #ifndef UAVHIP_STEPS_TU
 // Trunk split: the same partials once both trunks' workgroups have written smp[5..7].
 __global__ __launch_bounds__(64) void k_loss_partials(const TrainIO io) {
-    __shared__ float red[4 * SPW];
+    __shared__ float red[5 * SPW];
     const int b0 = blockIdx.x * SPW;
     if (TIDX() < SPW) {
         const float* o = io.smp + (size_t)(b0 + TIDX()) * 8;
         const float oi[5] = {o[0], o[1], o[2], o[3], o[4]};
-        loss_terms(oi, o[5], o[6], o[7], io.eps_clip, red + 4 * TIDX());
+        loss_terms(oi, o[5], o[6], o[7], io.eps_clip, red + 4 * TIDX(), red + 4 * SPW + TIDX());
     }
     __syncthreads();
     loss_block_sums(TID_C red, io.fpart, io.vpart, blockIdx.x);
@@ -3082,14 +3085,16 @@ __device__ void heads_bwd(Smem& sm, const float* __restrict__ P, const BwdIO& io
     // beyond would carry past fp16's range in the split-product dX GEMMs. Every workgroup forms the
     // same k from the forward's per-block maxima (vpart); the critic's reductions undo it
     // (k_reduce_grads reads 2^k from gsc_out).
+    // Every wave reduces the maxima itself (a few L2-resident loads per lane), so ck / ginv_c are the
+    // same in every lane of the workgroup (wave 0 alone had them). ck saturates at 124
+    // for an infinite maximum (2^-124 is still a normal float; a NaN maximum keeps ck = 0: the loss is
+    // NaN then anyway).
     float vmx = 0.f;
-    if (tid_x() < 64) {
-        for (int i = tid_x(); i < io.nvpart; i += 64) vmx = fmaxf(vmx, io.vpart[i]);
-        vmx = wave_max(vmx);
-    }
+    for (int i = tid_x() & 63; i < io.nvpart; i += 64) vmx = fmaxf(vmx, io.vpart[i]);
+    vmx = wave_max(vmx);
     int vexp = 0;
     (void)frexpf(vmx, &vexp);
-    const int ck = vexp >= 5 && vmx < 3.0e38f ? vexp - 4 : 0;  // vmx 2^-ck in [8, 16)
+    const int ck = !(vmx >= 16.f) ? 0 : vmx < 3.0e38f ? vexp - 4 : 124;  // vmx 2^-ck in [8, 16)
     const float ginv_c = ginv * ldexpf(1.0f, -ck);
     if (tid_x() == 0 && blk == 0 && role != 1 && io.gsc_out) io.gsc_out[0] = ldexpf(1.0f, ck);
     // the four loss sums (used by wave 0 only): from the all-reduced buffer, or summed here from

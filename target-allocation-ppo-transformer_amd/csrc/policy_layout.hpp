@@ -125,15 +125,22 @@ __host__ __device__ constexpr int trunk_index(int trunk) { return trunk == kActo
 // pairs, then layer 0's (14 max|W_e|, max|b_e| + max|pos|) and (D max|W_in|, max|b_in|) per trunk
 constexpr int kRtOp = 0, kRtE = 2 * kNumRangeOps, kRtA0 = kRtE + 4, kRtN = kRtA0 + 4;
 
-// The scale exponent of an operand bounded by B: 0 for B in [2^-4, 2^15) (and for 0, inf, NaN: a
+// The scale exponent of an operand bounded by B: 0 for B in [2^-4, 2^15) (and for 0 and NaN: a
 // non-finite operand stays non-finite), else B 2^-s in [2^14, 2^15). frexp: B = f 2^e, f in [0.5, 1).
+// A bound that overflowed fp32 (inf, or >= 2^115: the bounds are products of maxima and can overflow
+// while the activations they bound stay finite) takes the largest exponent any finite fp32 operand
+// needs, s = 113 (2^128 2^-113 = 2^15), instead of turning the scaling off; tiny bounds
+// stop at s = -100. Weights are not range-scaled: their split copies hold f16(w), so a weight of
+// 65520 or more is inf in the split products (non-finite outputs, never silently wrong;
+// uavhip_policy_range_table reports max |param| for a caller that wants to check).
 __host__ __device__ inline int range_exp(float B) {
-    if (!(B > 0.f) || !(B < 3.0e38f)) return 0;
+    if (!(B > 0.f)) return 0;
+    if (!(B < 0x1p115f)) return 113;
     int e = 0;
     (void)frexpf(B, &e);
     if (e >= -3 && e <= 15) return 0;
     const int s = e - 15;
-    return s < -100 ? -100 : (s > 100 ? 100 : s);
+    return s < -100 ? -100 : s;
 }
 // The bound of static operand op (range_op's numbering) from M = max|param q| (table[kRgMax ..]).
 __host__ __device__ inline float range_bound(const float* M, int op) {

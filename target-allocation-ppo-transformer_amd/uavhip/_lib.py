@@ -131,18 +131,29 @@ def _load():
         raise ImportError(f"libuavhip.so not built at {LIB_PATH}: run `make -C "
                           f"target-allocation-ppo-transformer_amd/csrc` (or __graft_entry__.build())")
     lib = ctypes.CDLL(LIB_PATH)
+    # UAVHIP_ACCEPT_PREV_ABI=1 (set by the A/B timing scripts only, scripts/ab_rollout.py): an older
+    # experimental build may predate an entry point and be of the previous ABI (4: no range table,
+    # peers by ordinal). Anything else -- a custom UAVHIP_LIB included -- must be the current ABI with
+    # every entry point, so a stale build fails here, not later and far from the cause.
+    lenient = os.environ.get("UAVHIP_ACCEPT_PREV_ABI") == "1"
+    missing = [name for name in _SIGS if not hasattr(lib, name)]
+    if missing and not lenient:
+        raise ImportError(f"{LIB_PATH}: missing entry points {missing[:4]}{'...' if len(missing) > 4 else ''}: "
+                          f"rebuild (make -C target-allocation-ppo-transformer_amd/csrc)")
     for name, (res, args) in _SIGS.items():
-        if os.environ.get("UAVHIP_LIB") and not hasattr(lib, name):
-            continue  # an older experimental build (A/B timing) may predate an entry point
+        if name in missing:
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    # a stale build would misread the descriptors; an A/B timing build (UAVHIP_LIB) of the previous
-    # ABI (4: no range table, peers by ordinal) is accepted for scripts/ab_rollout.py's rollout legs
-    ok = (ABI_VERSION, ABI_VERSION - 1) if os.environ.get("UAVHIP_LIB") else (ABI_VERSION,)
+    ok = (ABI_VERSION, ABI_VERSION - 1) if lenient else (ABI_VERSION,)
     if lib.uavhip_abi_version() not in ok:
         raise ImportError(f"{LIB_PATH}: ABI version {lib.uavhip_abi_version()}, this binding needs {ABI_VERSION}: "
                           f"rebuild (make -C target-allocation-ppo-transformer_amd/csrc)")
+    if lenient and (missing or lib.uavhip_abi_version() != ABI_VERSION):
+        import warnings
+        warnings.warn(f"UAVHIP_ACCEPT_PREV_ABI=1: {LIB_PATH} is ABI {lib.uavhip_abi_version()} with "
+                      f"{len(missing)} entry points missing (A/B timing builds only)")
     return lib
 
 

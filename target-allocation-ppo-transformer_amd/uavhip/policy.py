@@ -382,7 +382,10 @@ def range_table(params):
     |value|, then the scales of the split products' operands derived from them by the library's own
     host code -- bitwise what every kernel derives from the maxima, the part of the table the packed
     buffer carries (pack_weights)."""
-    m = torch.tensor([float(p.detach().abs().max()) for p in params], dtype=torch.float32)
+    # NaN elements are ignored, as the device's reductions do (k_policy_range / k_adam reduce with
+    # fmaxf, which drops NaN): the host and device tables agree bitwise for any parameter (ADVICE r05)
+    m = torch.tensor([float(torch.nan_to_num(p.detach().abs().float(), nan=0.0, posinf=float("inf")).max())
+                      for p in params], dtype=torch.float32)
     out = torch.zeros(RANGE_FLOATS, dtype=torch.float32)
     LIB.uavhip_policy_range_table(ctypes.c_void_p(m.data_ptr()), ctypes.c_void_p(out.data_ptr()))
     return out

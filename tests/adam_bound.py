@@ -60,12 +60,17 @@ class AdamStepBound:
         self.segs, self.lr = list(segments), lr.double()
         self.b1, self.b2, self.eps, self.rel, self.abs = betas[0], betas[1], eps, rel, abs_
         self.worst, self.worst_grad, self.worst_kb = {}, {}, {}
-        n = sum(n for _, _, n in self.segs)
-        self.key_bias = torch.zeros(n, dtype=torch.bool)  # in_proj_bias[D:2D]: softmax-invariant
+        self.d_model = d_model
+
+    def key_bias(self, n):
+        """Mask of the in_proj key-bias elements (in_proj_bias[D:2D], softmax-invariant) over a flat
+        vector of n elements (flat buffers may pad between and after the tensors)."""
+        kb = torch.zeros(n, dtype=torch.bool)
         for name, o, k in self.segs:
             if name.endswith("in_proj_bias"):
-                assert k == 3 * d_model, (name, k)
-                self.key_bias[o + d_model:o + 2 * d_model] = True
+                assert k == 3 * self.d_model, (name, k)
+                kb[o + self.d_model:o + 2 * self.d_model] = True
+        return kb
 
     def grad_error(self, g):
         g = g.double().cpu()
@@ -115,12 +120,13 @@ class AdamStepBound:
         # key bias: the cap for ANY gradient (its value is rounding noise on both sides)
         s_ = (v.double().cpu() / (1 - self.b2 ** t)).sqrt()
         u = (m.double().cpu() / (1 - self.b1 ** t)) / (s_ + self.eps)
-        b = torch.where(self.key_bias, self.lr.cpu() * (u.abs() + umax(t, self.b1, self.b2)), b)
+        key_bias = self.key_bias(b.numel())
+        b = torch.where(key_bias, self.lr.cpu() * (u.abs() + umax(t, self.b1, self.b2)), b)
         tol = b + 2.0 ** -22 * (want.abs() + p0.abs()) + 1e-6 * self.lr.cpu()
         d = (got - want).abs()
         ratio = d / tol
         for name, o, n in self.segs:
-            kb = self.key_bias[o:o + n]
+            kb = key_bias[o:o + n]
             r = ratio[o:o + n]
             self.worst[name] = max(self.worst.get(name, 0.0), float(r[~kb].max()))
             if bool(kb.any()):

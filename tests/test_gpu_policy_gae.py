@@ -615,3 +615,85 @@ def test_fused_forward_out_of_fp16_range_matches_torch(policy_npz, case):
                             atol=2e-6)
         assert_close_report(f"{case} ring step {step} value", vv.cpu().numpy(), vv_t[:, 0].cpu().numpy(), rtol=1e-5,
                             atol=1e-5 * max(1.0, float(vv_t.abs().max())))
+
+
+ROLLOUT_RANGE_CASES = ["ffn1 x4e4", "rows x1e5", "rows x1e-6", "embed x1e5"]
+
+
+@pytest.mark.parametrize("case", ROLLOUT_RANGE_CASES)
+def test_rollout_steps_out_of_fp16_range_matches_torch(policy_npz, case):
+    """the range scaling inside the headline kernel, k_rollout_steps (the
+    RolloutEngine's one-launch-per-iteration path: ring fill, window-row forward with the range table
+    and layer-0 constants staged in LDS once per launch, sampling, env step), T = 8 over 256 envs.
+    Cases: the critic's layer-0 FFN1 x 4e4 (FFN hidden units ~1e5, FFN2's operand); window rows x 1e5
+    and x 1e-6 (the env's window deque and the carried window scaled before the checked iteration, so
+    steps 0-3 mix scaled rows -- read from the ring the fill projected -- with the env's new rows:
+    per-token input exponents and the per-workgroup attention factor; for 1e-6 the embedding / position /
+    in_proj / out_proj biases are zero so the small rows matter); the embeddings x 1e5 (every step's
+    layer-0 input ~1e5 x). logp and value of every step against torch `evaluate` of the windows the
+    kernel consumed (tr.obs[t]) with the actions it sampled: 1e-5 relative (transformer_net.py:124-144),
+    or where torch fp32 is itself off the fp64 forward (mixed 1e5 / O(1) windows: attention logits
+    ~1e10), within twice torch fp32's worst error of fp64 on the same case; all finite."""
+    from uavhip.rollout import RolloutEngine
+    from uavhip.vec_env import VecUAVEnv
+    net = _load_policy(policy_npz, "b")
+    c0 = net.critic_net.transformer.layers[0]
+    rows = 1.0
+    with torch.no_grad():
+        if case == "ffn1 x4e4":
+            c0.linear1.weight.mul_(4e4)
+            c0.linear1.bias.mul_(4e4)
+        elif case == "embed x1e5":
+            for tb in (net.actor_net, net.critic_net):
+                tb.embedding[0].weight.mul_(1e5)
+                tb.embedding[0].bias.mul_(1e5)
+                tb.pos_embedding.mul_(1e5)
+        elif case == "rows x1e5":
+            rows = 1e5
+        elif case == "rows x1e-6":
+            rows = 1e-6
+            for tb in (net.actor_net, net.critic_net):
+                tb.embedding[0].bias.zero_()
+                tb.pos_embedding.zero_()
+                tb.transformer.layers[0].self_attn.in_proj_bias.zero_()
+                tb.transformer.layers[0].self_attn.out_proj.bias.zero_()
+    E, T = 256, 8
+    env = VecUAVEnv(E, 16, 32, 1, 1, full_reset_period=200, seed=31)
+    eng = RolloutEngine(env, net, T, seed=32)
+    assert eng.persistent, "the test is of k_rollout_steps"
+    eng.start()
+    eng.collect()  # one iteration first: the windows are full (no padding) when they are scaled
+    if rows != 1.0:
+        with torch.no_grad():
+            env.window.mul_(rows)
+            eng.traj.obs[T].mul_(rows)
+    tr = eng.collect()
+    torch.cuda.synchronize()
+    assert torch.isfinite(tr.logp).all() and torch.isfinite(tr.values).all(), "non-finite output"
+    x = tr.obs[:T].reshape(T * E, 5, 14)
+    a = tr.actions.reshape(-1).long()
+    if rows != 1.0:  # the scaled rows really were consumed: step 0's window holds them
+        big = float(tr.obs[0].abs().amax())
+        print(f"{case}: step-0 window max |x| {big:.3e}, step-{T - 1} window max |x| {float(tr.obs[T - 1].abs().amax()):.3e}")
+        assert (big > 1e3) if rows > 1 else (big < 1e-3)
+    import copy
+    with torch.no_grad():
+        lp_t, v_t, _ = net.evaluate(x, a)
+        lp_64, v_64, _ = copy.deepcopy(net).double().cpu().evaluate(x.double().cpu(), a.cpu())
+    assert torch.isfinite(lp_t).all() and torch.isfinite(v_t).all()
+    got = {"logp": tr.logp.reshape(-1).double().cpu(), "value": tr.values.reshape(-1).double().cpu()}
+    f32 = {"logp": lp_t.double().cpu(), "value": v_t[:, 0].double().cpu()}
+    f64 = {"logp": lp_64, "value": v_64[:, 0]}
+    for k, atol in (("logp", 2e-6), ("value", 1e-5 * max(1.0, float(v_t.abs().max())))):
+        # 1e-5 relative against torch fp32 -- or, where that fails, no further from the fp64 forward than
+        # twice torch fp32's worst error on the same case: windows mixing 1e5-scale rows with O(1) rows
+        # give attention logits ~1e10, where fp32 rounding moves the softmax itself (torch fp32 included)
+        bar = 1e-5 * f32[k].abs() + atol
+        e_hip, e_t32 = (got[k] - f64[k]).abs(), (f32[k] - f64[k]).abs()
+        near = (got[k] - f32[k]).abs() <= bar
+        ok = near | (e_hip <= 2 * float(e_t32.max()) + atol)
+        print(f"{case} rollout {k}: max |HIP - torch fp32| / bar {float(((got[k] - f32[k]).abs() / bar).max()):.3e} "
+              f"({int((~near).sum())} of {near.numel()} beyond); vs fp64: HIP max {float(e_hip.max()):.3e} "
+              f"p99 {float(e_hip.quantile(0.99)):.3e}, torch fp32 max {float(e_t32.max()):.3e} "
+              f"p99 {float(e_t32.quantile(0.99)):.3e}")
+        assert bool(ok.all()), f"{case} {k}: {int((~ok).sum())} elements beyond both bars"
