@@ -419,6 +419,12 @@ __device__ __forceinline__ void load_rtab(TID_F Smem& sm, const float* __restric
         default: break;
     }
 }
+// The derived table as an earlier kernel of the same step exported it (TrainIO::rtab_out: the K7
+// chain's F1 derives it once per optimizer step): one plain load per entry
+// instead of the maxima's scalar loads and every entry's derivation.
+__device__ __forceinline__ void load_rtab_ready(TID_F Smem& sm, const float* __restrict__ rt) {
+    if (TIDX() < kRtN) sm.rtab[TIDX()] = rt[TIDX()];
+}
 // a uniform LDS value into an SGPR (the factors are the same in every lane: no VGPR held)
 __device__ __forceinline__ float rt_uniform(const Smem& sm, int i) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sm.rtab[i])));
@@ -3492,6 +3498,8 @@ __global__ __launch_bounds__(NTHR) void k_ps_f1(const float* __restrict__ P, con
     gather_windows<true>(sm, states, B, io, b0, r == 0, P + kRangeOff);  // one workgroup per block writes the rows
     load_rtab(sm, P);  // behind the gather's loads (its arithmetic waits on nothing they need)
     __syncthreads();
+    // the step's derived scales, once: F2 / F3 and the weight-gradient GEMM read them (TrainIO::rtab_out)
+    if (blockIdx.x == 0 && tid_x() < kRtN && io.rtab_out) io.rtab_out[tid_x()] = sm.rtab[tid_x()];
     ps_embed<kPsSplit>(sm, ep, io.e[critic ? 1 : 0], io.h0[critic ? 1 : 0], b0, s, critic ? 1 : 0);
     __syncthreads();
     if constexpr (kPsSplit) {
@@ -3520,15 +3528,14 @@ __global__ __launch_bounds__(NTHR) void k_ps_f2(const float* __restrict__ P, con
     const float a0v = a0f_load(io.tmax + (size_t)b0 * S);
     ps_mask(sm, io.mask, b0);
     ps_rows_in(sm.h, LDH, io.h0[ti], D, 0, D, s, b0);  // the layer input (residual) of the position
-    load_rtab(sm, P);  // behind the loads above
-    float ec[8];  // layer 0's constants (kRgE .. kRgA0 + 3) from the table's maxima
+    load_rtab_ready(sm, io.rtab_out);  // F1's derived table, behind the loads above
+    float ec[8];  // layer 0's constants (kRgE .. kRgA0 + 3 = the table's kRtE ..): uniform loads
 #pragma unroll
-    for (int k = 0; k < 8; ++k) ec[k] = range_entry(P + kRangeOff, kRgE + k);
+    for (int k = 0; k < 8; ++k) ec[k] = io.rtab_out[kRtE + k];
     const float xm = a0f_finish(sm, a0v, ec, ec + 4);
     if (r == 0 && tid_x() == 0 && io.xmax) io.xmax[blk] = xm;  // the block's range for the weight gradients
     if (critic) ps_attention<kPsSplit, kCriticTrunk, 0>(sm, io.L[ti].qkv, s, b0, P);
     else ps_attention<kPsSplit, kActorTrunk, 0>(sm, io.L[ti].qkv, s, b0, P);
-    if (blk == 0 && r == 0 && tid_x() < kRtN && io.rtab_out) io.rtab_out[tid_x()] = sm.rtab[tid_x()];  // (as the fused forward)
     [[maybe_unused]] APre<4> ph;
     if constexpr (kPsSplit) {  // the layer tails and the next in_proj as split products
         if (critic) {
@@ -3581,7 +3588,7 @@ __global__ __launch_bounds__(NTHR) void k_ps_f3(const float* __restrict__ P, con
     if constexpr (kPsSplit) po = hprefetch<2>(P, split_slot(layer_param(kCriticTrunk, 1, OUTW)), D, 16 * wv, 0);
     ps_mask(sm, io.mask, b0);
     ps_rows_in(sm.h, LDH, io.L[1].h2, D, 0, D, S - 1, b0);  // layer 1's input (residual) at position 4
-    load_rtab(sm, P);  // behind the loads above
+    load_rtab_ready(sm, io.rtab_out);  // F1's derived table, behind the loads above
     ps_attention<kPsSplit, kCriticTrunk, 1>(sm, io.L[2].qkv, S - 1, b0, P);
     APre<4> ph;
     if constexpr (kPsSplit) {  // the residual is in sm.h (ps_rows_in): PSX = 2
