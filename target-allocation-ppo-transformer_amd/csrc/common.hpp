@@ -104,41 +104,72 @@ __device__ __forceinline__ void uav_heading(double uvx, double uvy, double& us, 
     if (!(us < 1e-6)) { hx = uvx / us; hy = uvy / us; }
 }
 
-// calc_damage_prob from the per-UAV (us, hx, hy, load) and per-target (ts) terms: the same fp64
-// operations as damage_prob below (|p_u - p_t| and |p_t - p_u| round identically), so bitwise.
-__device__ __forceinline__ double damage_prob_pre(double upx, double upy, double us, double hx, double hy,
-                                                  double load, double tpx, double tpy, double ts, const double* prm) {
-    const double vx = tpx - upx, vy = tpy - upy;
+// calc_damage_prob (mechanics.py:93-114) split into per-UAV, per-target and per-pair work, so the
+// pair loop of K1 (and the scene scorer, which evaluates the same functions per pair: bitwise the same
+// tables) does as little fp64 work per pair as the formula allows:
+//  * per UAV: speed us, unit heading (hx, hy) ([1, 0] when still, mechanics.py:37-41), 1/us, load;
+//  * per target: position and K * ts (speed_score's K ts / us evaluates (K ts) / us left to right);
+//  * per pair: dist, ONE reciprocal 1/dist (v_rcp_f64 + two Newton steps) for the unit direction and
+//    the angle's 1 / (b pi) = (1/dist) / (0.002 pi), acos, exp(-q^2), exp(-(dist / zeta)^2) with
+//    1/zeta per kernel, the speed score as (K ts) (1/us).
+// The products by reciprocals replace the reference's divisions: each differs from the quotient by
+// at most an ulp or two (relative 2^-52 class), far inside the pair bars (5e-12 against the reference,
+// tests/test_gpu_env.py); acos and exp are the same ocml functions as before.
+struct UavTerms {
+    double px, py, hx, hy, us, rus, load, pad;  // 64 B: four ds_read_b128 per UAV in K1's LDS table
+};
+__device__ __forceinline__ UavTerms uav_terms(double upx, double upy, double uvx, double uvy, double load) {
+    UavTerms r;
+    r.px = upx;
+    r.py = upy;
+    uav_heading(uvx, uvy, r.us, r.hx, r.hy);
+    r.rus = r.us < 1e-6 ? 0.0 : 1.0 / r.us;
+    r.load = load;
+    r.pad = 0.0;
+    return r;
+}
+struct PairConst {
+    double rzeta, rb, rb0, c1, c2;  // 1/zeta_d, 1/(0.002 pi), 1/(1e-6 pi), C1, C2
+};
+__device__ __forceinline__ PairConst pair_const(const double* prm) {
+    return PairConst{1.0 / prm[UAVHIP_PRM_ZETA_D], 1.0 / (0.002 * M_PI), 1.0 / (1e-6 * M_PI), prm[UAVHIP_PRM_C1],
+                     prm[UAVHIP_PRM_C2]};
+}
+// 1/d for d in [1e-6, 1e30]: the hardware estimate plus two Newton steps (correct to about an ulp;
+// no scaling needed in that range)
+__device__ __forceinline__ double recip_d(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+__device__ __forceinline__ double damage_pair(const UavTerms& u, double tpx, double tpy, double kts, const PairConst& pc) {
+    const double vx = tpx - u.px, vy = tpy - u.py;
     const double dist = norm2(vx, vy);
     double ea = 1.0;
     if (!(dist < 1e-6)) {
-        const double nx = vx / dist, ny = vy / dist;
-        const double c = nx * hx + ny * hy;
+        const double rd = recip_d(dist);
+        const double c = (vx * rd) * u.hx + (vy * rd) * u.hy;
         const double sigma = acos(clipd(c, -1.0, 1.0));
-        double b = 0.002 * dist;
-        if (b < 1e-6) b = 1e-6;
-        const double q = sigma / (b * M_PI);
+        // b = max(0.002 dist, 1e-6) (mechanics.py:52-54): sigma / (b pi)
+        const double q = sigma * (0.002 * dist < 1e-6 ? pc.rb0 : rd * pc.rb);
         ea = exp(-(q * q));
     }
-    const double ed = dist_score(dist, prm[UAVHIP_PRM_ZETA_D]);
-    const double es = speed_score(us, ts, prm[UAVHIP_PRM_K]);
-    const double term = prm[UAVHIP_PRM_C1] * ed + prm[UAVHIP_PRM_C2] * es;
-    const double p = ea * term * load;
+    const double qd = dist * pc.rzeta;  // dist_score, D_mid = 0
+    const double ed = exp(-(qd * qd));
+    const double es = u.us < 1e-6 ? 0.0 : clipd(1.0 - kts * u.rus, 0.0, 1.0);
+    const double term = pc.c1 * ed + pc.c2 * es;
+    const double p = ea * term * u.load;
     return clipd(p, 0.0, 1.0);
 }
 
-// mechanics.py:93-114 calc_damage_prob
+// mechanics.py:93-114 calc_damage_prob of one pair from the records (the per-wave scene scorer):
+// the same per-UAV / per-target / per-pair functions as K1, so bitwise K1's tables
 __device__ __forceinline__ double damage_prob(double upx, double upy, double uvx, double uvy, double load,
                                               double tpx, double tpy, double tvx, double tvy, const double* prm) {
-    const double dist = norm2(upx - tpx, upy - tpy);
-    const double us = norm2(uvx, uvy);
-    const double ts = norm2(tvx, tvy);
-    const double ea = angle_score(upx, upy, uvx, uvy, tpx, tpy);
-    const double ed = dist_score(dist, prm[UAVHIP_PRM_ZETA_D]);
-    const double es = speed_score(us, ts, prm[UAVHIP_PRM_K]);
-    const double term = prm[UAVHIP_PRM_C1] * ed + prm[UAVHIP_PRM_C2] * es;
-    const double p = ea * term * load;
-    return clipd(p, 0.0, 1.0);
+    const UavTerms u = uav_terms(upx, upy, uvx, uvy, load);
+    return damage_pair(u, tpx, tpy, prm[UAVHIP_PRM_K] * norm2(tvx, tvy), pair_const(prm));
 }
 
 // mechanics.py:118-163 calc_penetration_prob (independent of the target)

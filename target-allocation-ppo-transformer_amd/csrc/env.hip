@@ -23,54 +23,50 @@ constexpr int kBlock = kWavesPerBlock * kWave;
 }  // namespace
 
 // ================================================================== K1: pair tables (active buffer)
-// One workgroup per env (LDS-tiled pairwise scoring, BASELINE config 4): the env's UAV and target
-// records are staged in LDS once together with the per-entity terms every pair reuses (UAV speed +
-// unit heading, target speed: uav_heading), then the N x M pairs are scored from LDS broadcasts
-// with coalesced p_dmg stores (p_dmg[e] is one contiguous N*M run); p_pen (target-independent,
-// mechanics.py:118) by one thread per UAV. damage_prob_pre performs damage_prob's fp64 operations,
-// so the tables are bitwise those of the per-wave scene scorer (score_scene_wave).
+// One workgroup per env (LDS-tiled pairwise scoring, BASELINE config 4). The per-UAV terms every
+// pair reuses (common.hpp UavTerms: position, unit heading, speed and its reciprocal, load; 64 B)
+// are staged in LDS once; each thread then owns ONE target t (its position and K * speed in
+// registers) and walks the UAVs u = r, r + R, ... (R = 256 / M rows of M threads), reading the
+// UAV's terms as LDS broadcasts (the lanes of a row read the same 64 B) -- no per-pair index
+// division -- and storing p_dmg[u][t] coalesced (consecutive threads = consecutive targets).
+// p_pen (target-independent, mechanics.py:118) by one thread per UAV. The pair math is damage_pair,
+// which the per-wave scene scorer (score_scene_wave) runs too: bitwise the same tables.
 constexpr int kScoreThreads = 256;
-static_assert(UAVHIP_MAX_N + UAVHIP_MAX_M <= kScoreThreads, "one staging thread per entity");
+static_assert(UAVHIP_MAX_N + UAVHIP_MAX_M <= kScoreThreads && UAVHIP_MAX_M <= kScoreThreads,
+              "one staging thread per entity; at least one row of targets");
 __global__ __launch_bounds__(kScoreThreads) void k_score_pairs(uavhip_env env, const uint8_t* __restrict__ mask) {
-    __shared__ double s_u[6][UAVHIP_MAX_N];  // pos x, pos y, heading x, heading y, speed, load
-    __shared__ double s_t[3][UAVHIP_MAX_M];  // pos x, pos y, speed
+    __shared__ __attribute__((aligned(16))) UavTerms s_u[UAVHIP_MAX_N];
     const int e = blockIdx.x;
     if (mask && !mask[e]) return;
     const int N = env.N, M = env.M, tid = threadIdx.x;
     const int sel = env.scene_buffers == 2 ? (env.istate[(long long)e * UAVHIP_IST_COUNT + UAVHIP_IST_SCENE_SEL] & 1) : 0;
     const long long sb = (long long)sel * env.E + e;
+    // this thread's target: (row r, target t) of R = 256 / M rows; its loads issued before the barrier
+    const int R = kScoreThreads / M, r = tid / M, t = tid - r * M;
+    const bool tact = r < R;
+    double tpx = 0.0, tpy = 0.0, tvx = 0.0, tvy = 0.0;
+    if (tact) {
+        const double* tp = env.tgt_pos + 2 * (sb * M + t);
+        const double* tv = env.tgt_vel + 2 * (sb * M + t);
+        tpx = tp[0];
+        tpy = tp[1];
+        tvx = tv[0];
+        tvy = tv[1];
+    }
     if (tid < N) {
         const double* up = env.uav_pos + 2 * (sb * N + tid);
         const double* uv = env.uav_vel + 2 * (sb * N + tid);
-        double us, hx, hy;
-        uav_heading(uv[0], uv[1], us, hx, hy);
-        s_u[0][tid] = up[0];
-        s_u[1][tid] = up[1];
-        s_u[2][tid] = hx;
-        s_u[3][tid] = hy;
-        s_u[4][tid] = us;
-        s_u[5][tid] = env.uav_load[sb * N + tid];
+        s_u[tid] = uav_terms(up[0], up[1], uv[0], uv[1], env.uav_load[sb * N + tid]);
         env.p_pen[sb * N + tid] = penetration_prob(up[0], up[1], uv[0], uv[1], env.nfz_pos + 2 * sb * env.Kn, env.Kn,
                                                    env.icp_pos + 2 * sb * env.Ki, env.icp_vel + 2 * sb * env.Ki,
                                                    env.Ki, env.prm);
-    } else if (tid - UAVHIP_MAX_N < M && tid >= UAVHIP_MAX_N) {
-        const int t = tid - UAVHIP_MAX_N;
-        const double* tp = env.tgt_pos + 2 * (sb * M + t);
-        const double* tv = env.tgt_vel + 2 * (sb * M + t);
-        s_t[0][t] = tp[0];
-        s_t[1][t] = tp[1];
-        s_t[2][t] = norm2(tv[0], tv[1]);
     }
+    const PairConst pc = pair_const(env.prm);
+    const double kts = env.prm[UAVHIP_PRM_K] * norm2(tvx, tvy);
     __syncthreads();
-    double prm[UAVHIP_PRM_COUNT];
-#pragma unroll
-    for (int k = 0; k < UAVHIP_PRM_COUNT; ++k) prm[k] = env.prm[k];
-    double* out = env.p_dmg + sb * N * M;
-    for (int i = tid; i < N * M; i += kScoreThreads) {
-        const int u = i / M, t = i - u * M;
-        out[i] = damage_prob_pre(s_u[0][u], s_u[1][u], s_u[4][u], s_u[2][u], s_u[3][u], s_u[5][u], s_t[0][t],
-                                 s_t[1][t], s_t[2][t], prm);
-    }
+    if (!tact) return;
+    double* out = env.p_dmg + sb * N * M + t;
+    for (int u = r; u < N; u += R) out[(long long)u * M] = damage_pair(s_u[u], tpx, tpy, kts, pc);
 }
 
 // ================================================================== wave-per-env kernels
