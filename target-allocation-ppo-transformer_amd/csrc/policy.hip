@@ -86,6 +86,11 @@ constexpr bool kExpNoEnv = false;
 #define UAVHIP_EXP 0
 #endif
 constexpr bool kExpHotRing = UAVHIP_EXP == 32;
+// EXP=71 (timing only, WRONG results): the split-product GEMMs load only the blocks their callers
+// prefetched (blocks >= D_ of a tile repeat them): the cost of the in-loop weight loads' latency --
+// the ceiling of a deeper weight prefetch (an LDS-DMA ring). EXP=73: also every prefetch reads one
+// hot 1 KiB block (the weight stream from L2 compiled out of the split GEMMs).
+constexpr bool kExpNoWeightLoads = UAVHIP_EXP == 71 || UAVHIP_EXP == 73;
 
 // Phase tracing (make TRACE=1 only): waves 0 and 4 of the first 256 workgroups stamp s_memtime at
 // the phase boundaries below; uavhip_policy_trace copies the stamps out. Off in the product build.
@@ -308,6 +313,7 @@ struct HPre {
     f16x8 a1[D_], a2[D_];
 };
 __device__ __forceinline__ const f16x8* hfrag_ptr(TID_F const float* P, int soff, int K, int row, int kw0) {
+    if constexpr (UAVHIP_EXP == 73) return reinterpret_cast<const f16x8*>(P + soff) + LANE();  // timing only
     return reinterpret_cast<const f16x8*>(P + soff) + ((size_t)(row >> 4) * (K >> 5) + (kw0 >> 5)) * 128 + LANE();
 }
 template <int D_>
@@ -350,8 +356,14 @@ __device__ __forceinline__ void hgemm_tile(TID_F f32x4 (&hi)[CT], f32x4 (&lo)[CT
     for (int i = 0; i < NKB; ++i) {
         const int cur = i & 1;
         if (i + D_ < NKB) {
-            a1[i + D_] = wp[128 * (i + D_)];
-            a2[i + D_] = wp[128 * (i + D_) + 64];
+            if constexpr (kExpNoWeightLoads || (UAVHIP_EXP == 712 && CT == S) || (UAVHIP_EXP == 713 && CT == 1)) {
+                // timing builds only: blocks >= D_ repeat the prefetched ones
+                a1[i + D_] = a1[(i + D_) % D_];
+                a2[i + D_] = a2[(i + D_) % D_];
+            } else {
+                a1[i + D_] = wp[128 * (i + D_)];
+                a2[i + D_] = wp[128 * (i + D_) + 64];
+            }
         }
         if (i + 1 < NKB) {
 #pragma unroll
@@ -934,14 +946,21 @@ template <int trunk, int layer>
 constexpr bool split_l0() {  // layer 0's in_proj from the embedding's planes (the training forward)
     return layer == 0 && split_slot(layer_param(trunk, 0, INW)) >= 0;
 }
+// Weight blocks (of 32 k) a split tail GEMM has in registers before its k-loop starts: the pruned
+// (one 16-token tile) tails of the inference forward take their whole tile (4 blocks) -- their MFMA
+// work per block is a fifth of a full layer's, far too little to cover an in-loop L2 round trip --
+// the rest 2 (EXP=74: the A/B build of the full-tile prefetch)
+constexpr bool kExpTailDepth4 = UAVHIP_EXP == 74;
+template <bool last, bool TR, int PSX>
+constexpr int tail_depth() { return kExpTailDepth4 && last && !TR && !PSX ? 4 : 2; }
 template <int trunk, int layer, bool last, bool TR, int PSX = 0, bool SP = !TR>
-using TailPre = std::conditional_t<SP && !PSX && split_tail<trunk, layer>(), HPre<2>,
+using TailPre = std::conditional_t<SP && !PSX && split_tail<trunk, layer>(), HPre<tail_depth<last, TR, PSX>()>,
                                    APre<depth<(last || PSX) ? 1 : S>()>>;
 template <int trunk, int layer, bool last, bool TR, bool SP = !TR>
 __device__ __forceinline__ TailPre<trunk, layer, last, TR, 0, SP> tail_prefetch(TID_F const float* __restrict__ P) {
     const int wv = TIDX() >> 6;
     if constexpr (SP && split_tail<trunk, layer>())
-        return hprefetch<2>(TID_C P, split_slot(layer_param(trunk, layer, OUTW)), D, 16 * wv, 0);
+        return hprefetch<tail_depth<last, TR, 0>()>(TID_C P, split_slot(layer_param(trunk, layer, OUTW)), D, 16 * wv, 0);
     else
         return prefetch<depth<last ? 1 : S>()>(TID_C P + kOffs.o[layer_param(trunk, layer, OUTW)], D, 16 * wv, 0);
 }
@@ -1167,9 +1186,11 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
 // its residual in sm.h, LN2's output as planes for the kernel's next in_proj (ps_inproj_split); and
 // K7's pruned layers take their residual from sm.h (PSX = 2).
 template <int trunk, int layer, bool last, bool TR = false, class F = NoHook, int PSX = 0>
-__device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __restrict__ P, const HPre<2>& po,
+__device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __restrict__ P,
+                                                 const HPre<tail_depth<last, TR, PSX>()>& po,
                                                  const TrainLayerIO& io = TrainLayerIO{}, int b0 = 0, F pre_ln2 = F{},
                                                  int qt = 0) {
+    constexpr int DP = tail_depth<last, TR, PSX>();
     [[maybe_unused]] constexpr int tb = 8 + 16 * (trunk == 0 ? 0 : 1 + layer);  // trace slot base
     constexpr int CT = (last || PSX) ? 1 : S;
     const int t0 = last ? (S - 1) * SPW : (PSX ? qt : 0), t1 = t0 + SPW * CT;
@@ -1190,7 +1211,7 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     _Float16* const bp = reinterpret_cast<_Float16*>(sm.big);
     _Float16* const cp = reinterpret_cast<_Float16*>(sm.ctx);
     f32x4 h1[CT];  // LN1's output: LN2's residual
-    HPre<2> w1a;
+    HPre<DP> w1a;
     // the operand scales (policy_layout.hpp range table): the attention output (layer 0: one per
     // workgroup, att_sc), LN1's output, the FFN hidden units; LN2's output when it is the next layer's
     // split operand
@@ -1209,13 +1230,13 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
             f32x4 hi[CT], lo[CT];
             zero(hi);
             zero(lo);
-            hgemm_tile<CT, 2>(TID_C hi, lo, po, P, so, D, 16 * wv, 0, cp, t0);
+            hgemm_tile<CT, DP>(TID_C hi, lo, po, P, so, D, 16 * wv, 0, cp, t0);
             const float att_inv = att_sc<trunk, layer>(sm, LANE() & 15).inv;  // uniform (SGPRs)
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) acc[ct] = (hi[ct] + lo[ct] * kLoScale) * att_inv;
         }
         PTR(tb + 7);
-        w1a = hprefetch<2>(TID_C P, s1, D, 16 * wv, 0);
+        w1a = hprefetch<DP>(TID_C P, s1, D, 16 * wv, 0);
         // the LayerNorm outputs go to the workspace only for the position-split kernels (K7 reads
         // them across launches); the fused training step's weight gradients form them from x-hat
         const LnOut lo1{io.xhat1, PSX ? io.h1 : nullptr, io.rstd1, b0, last};
@@ -1237,19 +1258,19 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
         f32x4 hi[CT], lo[CT];
         zero(hi);
         zero(lo);
-        hgemm_tile<CT, 2>(TID_C hi, lo, w1a, P, s1, D, 16 * wv, 0, hp, t0);
-        const HPre<2> w1b = hprefetch<2>(TID_C P, s1, D, 128 + 16 * wv, 0);
+        hgemm_tile<CT, DP>(TID_C hi, lo, w1a, P, s1, D, 16 * wv, 0, hp, t0);
+        const HPre<DP> w1b = hprefetch<DP>(TID_C P, s1, D, 128 + 16 * wv, 0);
         hstore_tile<CT, true>(TID_C hi, lo, ba, bp, 16 * wv, t0, s_ln1.inv, s_hid.sc);
         zero(hi);
         zero(lo);
-        hgemm_tile<CT, 2>(TID_C hi, lo, w1b, P, s1, D, 128 + 16 * wv, 0, hp, t0);
+        hgemm_tile<CT, DP>(TID_C hi, lo, w1b, P, s1, D, 128 + 16 * wv, 0, hp, t0);
         hstore_tile<CT, true>(TID_C hi, lo, bb, cp, 16 * wv, t0, s_ln1.inv, s_hid.sc);
     }
-    const HPre<2> w2a = hprefetch<2>(TID_C P, s2, FF, 16 * wv, 0);
+    const HPre<DP> w2a = hprefetch<DP>(TID_C P, s2, FF, 16 * wv, 0);
     PTR(tb + 10);
     __syncthreads();
     PTR(tb + 11);
-    const HPre<2> w2b = hprefetch<2>(TID_C P, s2, FF, 16 * wv, 128);
+    const HPre<DP> w2b = hprefetch<DP>(TID_C P, s2, FF, 16 * wv, 128);
     if constexpr (TR) {  // FFN hidden (post-ReLU): features 0-127 from big, 128-255 from ctx
         store_rows_planes(TID_C bp, io.u, FF, 0, D, t0, b0, last, t1, [&](int) { return s_hid.inv; });
         store_rows_planes(TID_C cp, io.u, FF, D, D, t0, b0, last, t1, [&](int) { return s_hid.inv; });
@@ -1259,8 +1280,8 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     f32x4 hi[CT], lo[CT];
     zero(hi);
     zero(lo);
-    hgemm_tile<CT, 2>(TID_C hi, lo, w2a, P, s2, FF, 16 * wv, 0, bp, t0);
-    hgemm_tile<CT, 2>(TID_C hi, lo, w2b, P, s2, FF, 16 * wv, 128, cp, t0);
+    hgemm_tile<CT, DP>(TID_C hi, lo, w2a, P, s2, FF, 16 * wv, 0, bp, t0);
+    hgemm_tile<CT, DP>(TID_C hi, lo, w2b, P, s2, FF, 16 * wv, 128, cp, t0);
     PTR(tb + 12);
     f32x4 acc2[CT];
 #pragma unroll
@@ -1529,9 +1550,14 @@ __device__ __forceinline__ void hgemm_rows(TID_F f32x4 (&hi)[R], f32x4 (&lo)[R],
         if (i + D_ < NKB) {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const f16x8* wp = hfrag_ptr(TID_C P, soff, K, row[r], 0) + 128 * (i + D_);
-                a1[i + D_][r] = wp[0];
-                a2[i + D_][r] = wp[64];
+                if constexpr (kExpNoWeightLoads || UAVHIP_EXP == 711) {  // timing builds only
+                    a1[i + D_][r] = a1[(i + D_) % D_][r];
+                    a2[i + D_][r] = a2[(i + D_) % D_][r];
+                } else {
+                    const f16x8* wp = hfrag_ptr(TID_C P, soff, K, row[r], 0) + 128 * (i + D_);
+                    a1[i + D_][r] = wp[0];
+                    a2[i + D_][r] = wp[64];
+                }
             }
         }
         if (i == (D_ < NKB ? NKB - D_ - 1 : 0)) issued();
