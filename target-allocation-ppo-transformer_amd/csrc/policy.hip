@@ -989,8 +989,12 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
 
 // Training mode: the Q|K|V of chunk c of the tokens [qtok0, 80) (Q) / all (K, V) from sm.big to qkv
 // rows, by waves 4-7 (less MFMA work than the K + Q waves sharing their SIMDs).
+// EXP=81 (timing only, WRONG results): the Q | K | V stream between the training forward and K6
+// compiled out -- the forward does not store it, K6 reads one hot row for every sample (the ceiling
+// of recomputing it in K6, DESIGN.md 10 lever 3)
+constexpr bool kExpNoQkvStream = UAVHIP_EXP == 81;
 __device__ __forceinline__ void store_qkv_chunk(TID_F const Smem& sm, float* __restrict__ qkv, int c, int qtok0, int b0) {
-    if (kExpNoStore) return;
+    if (kExpNoStore || kExpNoQkvStream) return;
     for (int i = (int)TIDX() - NTHR / 2; i < TOK * 48; i += NTHR / 2) {
         if (i < 0) break;
         const int tok = i / 48, r = i - tok * 48, part = r >> 4, q = r & 15;
@@ -1153,7 +1157,7 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
         PTR(tb + 1 + 3 * c);
         __syncthreads();
         PTR(tb + 2 + 3 * c);
-        if (TR && !kExpNoStore) {  // this chunk's Q (query tokens) / K / V -> qkv[row][part * 128 + 64 c + d]
+        if (TR && !kExpNoStore && !kExpNoQkvStream) {  // this chunk's Q (query tokens) / K / V -> qkv[row][part * 128 + 64 c + d]
             // by waves 4-7 (V tiles: less MFMA work than the K + Q waves sharing their SIMDs)
             for (int i = (int)TIDX() - NTHR / 2; i < TOK * 48; i += NTHR / 2) {
                 if (i < 0) break;
@@ -2555,7 +2559,7 @@ template <bool last>
 __device__ __forceinline__ void attn_bwd_load(AttnPre& a, const float* __restrict__ qkv, int c, int b0, int qsel = -1) {
     const int o8 = tid_x() & 7, hh = (tid_x() >> 3) & 3, p = tid_x() >> 5;
     const int col = 64 * c + hh * HD + 2 * o8;
-    const size_t rb = (size_t)(b0 + p) * S;
+    const size_t rb = kExpNoQkvStream ? (size_t)p * S : (size_t)(b0 + p) * S;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
         a.k[j] = ld2(qkv + (rb + j) * 3 * D + D + col);
