@@ -91,6 +91,30 @@ constexpr bool kExpHotRing = UAVHIP_EXP == 32;
 // the ceiling of a deeper weight prefetch (an LDS-DMA ring). EXP=73: also every prefetch reads one
 // hot 1 KiB block (the weight stream from L2 compiled out of the split GEMMs).
 constexpr bool kExpNoWeightLoads = UAVHIP_EXP == 71 || UAVHIP_EXP == 73;
+// The training forward's activation stores (the rows K6 and the weight-gradient GEMM read back after
+// the whole forward: Q | K | V, x-hat, the embeddings, FFN hidden units, attention outputs) are
+// non-temporal: they stream past the L2 instead of evicting the weights and re-read rows there.
+// Same-box A/B (profiles/r06m_train_ab_nt_stores.txt): K6 104.4-108.5 -> 101.1-101.3 us at minibatch
+// 4096, the forward unchanged. Not in the position-split kernels (K7, minibatch <= 256), whose next
+// launch reads the rows back from the L2 (nt there: B1 / B2 +1 us each): nt = false. EXP=85 (A/B
+// build): plain stores everywhere.
+constexpr bool kNtAct = UAVHIP_EXP != 85;
+__device__ __forceinline__ void act_st(float* p, f32x4 v, bool nt = true) {
+    if (kNtAct && nt) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+    else *reinterpret_cast<f32x4*>(p) = v;
+}
+// EXP=84 (A/B build): K6's gradient rows for the weight-gradient GEMM (df, dz1, du, dq | dk | dv)
+// as non-temporal stores too
+constexpr bool kNtDy = UAVHIP_EXP == 84;
+__device__ __forceinline__ void dy_st4(float* p, f32x4 v) {
+    if constexpr (kNtDy) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+    else *reinterpret_cast<f32x4*>(p) = v;
+}
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void dy_st2(float* p, f32x2_t v) {
+    if constexpr (kNtDy) __builtin_nontemporal_store(v, reinterpret_cast<f32x2_t*>(p));
+    else *reinterpret_cast<f32x2_t*>(p) = v;
+}
 
 // Phase tracing (make TRACE=1 only): waves 0 and 4 of the first 256 workgroups stamp s_memtime at
 // the phase boundaries below; uavhip_policy_trace copies the stamps out. Off in the product build.
@@ -577,6 +601,7 @@ __device__ __forceinline__ float wave_max(float v) {
 struct LnOut {
     float *x, *h, *rs;
     int b0, compact;
+    bool nt = true;  // non-temporal stores (act_st): not in the position-split kernels
 };
 __device__ __forceinline__ int trow(int tok, int b0) { return (b0 + (tok & (SPW - 1))) * S + tok / SPW; }
 __device__ __forceinline__ int orow(int tok, int b0, bool compact) {
@@ -694,8 +719,8 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
         if (outv) outv[ct] = out;
         if (TR && !kExpNoStore) {
             const size_t r = (size_t)orow(tok, lo.b0, lo.compact);
-            *reinterpret_cast<f32x4*>(lo.x + r * D + f0) = xh;
-            if (lo.h) *reinterpret_cast<f32x4*>(lo.h + r * D + f0) = out;  // nullptr: formed by k_wgrad
+            act_st(lo.x + r * D + f0, xh, lo.nt);
+            if (lo.h) act_st(lo.h + r * D + f0, out, lo.nt);  // nullptr: formed by k_wgrad
             if (wv == 0 && g == 0) lo.rs[r] = rs;
         }
     }
@@ -704,15 +729,14 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
 // Training mode: copy [tok][cols] rows from LDS (stride lds) to workspace rows (stride ldo, column
 // offset c0) for tokens [t0, t1), all 512 threads, float4 granules.
 __device__ __forceinline__ void store_rows(TID_F const float* src, int lds, float* dst, int ldo, int c0, int ncols, int t0,
-                                           int b0, bool compact, int t1 = TOK) {
+                                           int b0, bool compact, int t1 = TOK, bool nt = true) {
 #ifdef UAVHIP_EXP_NOSTORE  // timing experiment only (make NOSTORE=1): activations not written
     return;
 #endif
     const int n4 = ncols / 4, items = (t1 - t0) * n4;
     for (int i = TIDX(); i < items; i += NTHR) {
         const int tok = t0 + i / n4, q = i % n4;
-        *reinterpret_cast<f32x4*>(dst + (size_t)orow(tok, b0, compact) * ldo + c0 + 4 * q) =
-            *reinterpret_cast<const f32x4*>(src + tok * lds + 4 * q);
+        act_st(dst + (size_t)orow(tok, b0, compact) * ldo + c0 + 4 * q, *reinterpret_cast<const f32x4*>(src + tok * lds + 4 * q), nt);
     }
 }
 
@@ -905,8 +929,8 @@ __device__ void embed_apply(TID_F Smem& sm, const EmbPre& ep, float* e_out = nul
         if constexpr (PL) hsplit_store(reinterpret_cast<_Float16*>(sm.ctx), psw((ct * SPW + i16), 16 * wv + 4 * g), v * esc);
         if (TR && !kExpNoStore) {
             const size_t r = (size_t)trow(ct * SPW + i16, b0);
-            *reinterpret_cast<f32x4*>(e_out + r * D + 16 * wv + 4 * g) = e;
-            if (h_out) *reinterpret_cast<f32x4*>(h_out + r * D + 16 * wv + 4 * g) = v;
+            act_st(e_out + r * D + 16 * wv + 4 * g, e);
+            if (h_out) act_st(h_out + r * D + 16 * wv + 4 * g, v);
         }
     }
 }
@@ -999,8 +1023,8 @@ __device__ __forceinline__ void store_qkv_chunk(TID_F const Smem& sm, float* __r
         if (i < 0) break;
         const int tok = i / 48, r = i - tok * 48, part = r >> 4, q = r & 15;
         if (part == 0 && tok < qtok0) continue;
-        *reinterpret_cast<f32x4*>(qkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q) =
-            *reinterpret_cast<const f32x4*>(sm.big + tok * LDB + part * 64 + 4 * q);
+        act_st(qkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q,
+               *reinterpret_cast<const f32x4*>(sm.big + tok * LDB + part * 64 + 4 * q));
     }
 }
 // Training mode: fp32 rows from the two planes of a split-product operand in LDS (the values the
@@ -1008,7 +1032,7 @@ __device__ __forceinline__ void store_qkv_chunk(TID_F const Smem& sm, float* __r
 // (stride ldo, column offset c0), tokens [t0, t1).
 template <class Inv>
 __device__ __forceinline__ void store_rows_planes(TID_F const _Float16* src, float* dst, int ldo, int c0, int ncols,
-                                                  int t0, int b0, bool compact, int t1, Inv inv) {
+                                                  int t0, int b0, bool compact, int t1, Inv inv, bool nt = true) {
     if (kExpNoStore) return;
     const int n4 = ncols / 4, items = (t1 - t0) * n4;
     for (int i = TIDX(); i < items; i += NTHR) {
@@ -1019,7 +1043,7 @@ __device__ __forceinline__ void store_rows_planes(TID_F const _Float16* src, flo
         f32x4 v;
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = ((float)x1[j] + (float)x2[j] * kLoScale) * s;
-        *reinterpret_cast<f32x4*>(dst + (size_t)orow(tok, b0, compact) * ldo + c0 + 4 * q) = v;
+        act_st(dst + (size_t)orow(tok, b0, compact) * ldo + c0 + 4 * q, v, nt);
     }
 }
 
@@ -1163,8 +1187,8 @@ __device__ __forceinline__ void encoder_layer(TID_F Smem& sm, const float* __res
                 if (i < 0) break;
                 const int tok = i / 48, r = i - tok * 48, part = r >> 4, q = r & 15;
                 if (part == 0 && tok < qtok0) continue;
-                *reinterpret_cast<f32x4*>(io.qkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q) =
-                    *reinterpret_cast<const f32x4*>(sm.big + tok * LDB + part * 64 + 4 * q);
+                act_st(io.qkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q,
+                       *reinterpret_cast<const f32x4*>(sm.big + tok * LDB + part * 64 + 4 * q));
             }
         }
         if (last) attention_chunk<planes, trunk, layer>(TID_C sm, c, S - 1, 1, P);
@@ -1222,7 +1246,7 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     const OpSc s_ln1 = op_sc<trunk, layer, kOpLn1>(sm), s_hid = op_sc<trunk, layer, kOpHid>(sm);
     if constexpr (TR)  // attention output
         store_rows_planes(TID_C cp, io.o, D, 0, D, t0, b0, last, t1,
-                          [&](int tok) { return att_sc<trunk, layer>(sm, tok & 15).inv; });
+                          [&](int tok) { return att_sc<trunk, layer>(sm, tok & 15).inv; }, !PSX);
     {
         // the epilogue's bias and LN1's weight / bias ahead of the GEMM: issued after it, their L2
         // round trip (~2 k cycles with every CU reading the same lines) outlasted the partials +
@@ -1243,7 +1267,7 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
         w1a = hprefetch<DP>(TID_C P, s1, D, 16 * wv, 0);
         // the LayerNorm outputs go to the workspace only for the position-split kernels (K7 reads
         // them across launches); the fused training step's weight gradients form them from x-hat
-        const LnOut lo1{io.xhat1, PSX ? io.h1 : nullptr, io.rstd1, b0, last};
+        const LnOut lo1{io.xhat1, PSX ? io.h1 : nullptr, io.rstd1, b0, last, !PSX};
         if constexpr (res_ctx) {
             const f32x4 r4[1] = {*reinterpret_cast<const f32x4*>(sm.ctx + (LANE() & 15) * LDH + 16 * wv + 4 * (LANE() >> 4))};
             residual_layernorm<CT, TR, true>(TID_C sm, acc, lp, t0, lo1, h1, r4, s_ln1.sc);
@@ -1276,8 +1300,8 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     PTR(tb + 11);
     const HPre<DP> w2b = hprefetch<DP>(TID_C P, s2, FF, 16 * wv, 128);
     if constexpr (TR) {  // FFN hidden (post-ReLU): features 0-127 from big, 128-255 from ctx
-        store_rows_planes(TID_C bp, io.u, FF, 0, D, t0, b0, last, t1, [&](int) { return s_hid.inv; });
-        store_rows_planes(TID_C cp, io.u, FF, D, D, t0, b0, last, t1, [&](int) { return s_hid.inv; });
+        store_rows_planes(TID_C bp, io.u, FF, 0, D, t0, b0, last, t1, [&](int) { return s_hid.inv; }, !PSX);
+        store_rows_planes(TID_C cp, io.u, FF, D, D, t0, b0, last, t1, [&](int) { return s_hid.inv; }, !PSX);
     }
     const LnPar lp2 = ln_load(TID_C ln_bias(TID_C b2), P + kOffs.o[layer_param(trunk, layer, N2W)],
                               P + kOffs.o[layer_param(trunk, layer, N2B)]);  // ahead of the GEMM, as LN1's
@@ -1294,7 +1318,7 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
     float ln2_sc = 1.f;
     if constexpr (next_planes) ln2_sc = op_sc<trunk, layer, kOpLn2>(sm).sc;
     residual_layernorm<CT, TR, next_planes, row4, kC0 ? 23 : -1, kC0 ? 39 : -1, kC0 ? 58 : -1>(
-        TID_C sm, acc2, lp2, t0, LnOut{io.xhat2, PSX ? io.h2 : nullptr, io.rstd2, b0, last}, nullptr, h1, ln2_sc);
+        TID_C sm, acc2, lp2, t0, LnOut{io.xhat2, PSX ? io.h2 : nullptr, io.rstd2, b0, last, !PSX}, nullptr, h1, ln2_sc);
     PTR(tb + 14);
 }
 
@@ -1315,7 +1339,7 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
     constexpr int DQ = depth<CTQ>();
     const int qtok0 = last ? (S - 1) * SPW : (PSX ? qt : 0);
     const int qtok1 = qtok0 + SPW * CTQ;
-    if (TR) store_rows(TID_C sm.ctx, LDH, io.o, D, 0, D, qtok0, b0, last, qtok1);  // attention output
+    if (TR) store_rows(TID_C sm.ctx, LDH, io.o, D, 0, D, qtok0, b0, last, qtok1, !PSX);  // attention output
     // out projection, h = LN1(h + attn) in its epilogue
     APre<DQ> pf1a, pf1b;
     // inference, full layer (the critic's layer 0): the FFN runs as split products on the f16
@@ -1348,7 +1372,7 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
             pf1a = prefetch_rot<DQ>(TID_C W1, D, 16 * wv, wv + 1);
             pf1b = prefetch_rot<DQ>(TID_C W1, D, 128 + 16 * wv, wv + 1);
             f32x4 outv[CTQ];
-            residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, PSX ? io.h1 : nullptr, io.rstd1, b0, last}, outv);
+            residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, PSX ? io.h1 : nullptr, io.rstd1, b0, last, !PSX}, outv);
             zero(fa);
             zero(fb);
 #pragma unroll
@@ -1365,7 +1389,7 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
                 const f32x4 r4[1] = {*reinterpret_cast<const f32x4*>(sm.ctx + (LANE() & 15) * LDH + 16 * wv + 4 * (LANE() >> 4))};
                 residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{}, nullptr, r4);
             } else {
-                residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, PSX ? io.h1 : nullptr, io.rstd1, b0, last});
+                residual_layernorm<CTQ, TR>(TID_C sm, acc, lp, qtok0, LnOut{io.xhat1, PSX ? io.h1 : nullptr, io.rstd1, b0, last, !PSX});
             }
         }
     }
@@ -1391,8 +1415,8 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
     PTR(tb + 11);
     const APre<DQ> pf2b = prefetch<DQ>(TID_C W2, FF, 16 * wv, 128);
     if (TR) {  // FFN hidden (post-ReLU): features 0-127 in big, 128-255 in ctx
-        store_rows(TID_C sm.big, LDF, io.u, FF, 0, D, qtok0, b0, last, qtok1);
-        store_rows(TID_C sm.ctx, LDF, io.u, FF, D, D, qtok0, b0, last, qtok1);
+        store_rows(TID_C sm.big, LDF, io.u, FF, 0, D, qtok0, b0, last, qtok1, !PSX);
+        store_rows(TID_C sm.ctx, LDF, io.u, FF, D, D, qtok0, b0, last, qtok1, !PSX);
     }
     const f32x4 b24 = ln_bias(TID_C b2);
     f32x4 acc2[CTQ];
@@ -1402,7 +1426,7 @@ __device__ __forceinline__ void layer_tail(TID_F Smem& sm, const float* __restri
     PTR(tb + 12);
     const LnPar lp2 = ln_load(TID_C b24, P + kOffs.o[layer_param(trunk, layer, N2W)], P + kOffs.o[layer_param(trunk, layer, N2B)]);
     pre_ln2();
-    residual_layernorm<CTQ, TR>(TID_C sm, acc2, lp2, qtok0, LnOut{io.xhat2, PSX ? io.h2 : nullptr, io.rstd2, b0, last});
+    residual_layernorm<CTQ, TR>(TID_C sm, acc2, lp2, qtok0, LnOut{io.xhat2, PSX ? io.h2 : nullptr, io.rstd2, b0, last, !PSX});
     PTR(tb + 14);
     }
 }
@@ -2510,8 +2534,8 @@ __device__ void ln_bwd_lds(const float* src, float* dst, const LnBwdPre& a, floa
             st4(dst + tok * LDH + f0, d0);
             st4(dst + tok * LDH + f0 + 4, d1);
         }
-        st4(gout + r * D + f0, d0);
-        st4(gout + r * D + f0 + 4, d1);
+        dy_st4(gout + r * D + f0, d0);
+        dy_st4(gout + r * D + f0 + 4, d1);
         pw0 += g0 * x0; pw1 += g1 * x1;
         pb0 += g0; pb1 += g1;
         pd0 += d0; pd1 += d1;
@@ -2586,7 +2610,7 @@ __device__ __forceinline__ void attn_out2(Smem& sm, float* __restrict__ dqkv, in
         if (kvc && part > 0)  // position split: this query position's share of every position's dk / dv
             st2(kvc + ((size_t)kblk * TOK + tok) * 2 * D + (part - 1) * D + 64 * c + col, v);
         else
-            st2(dqkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + col, v);
+            dy_st2(dqkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + col, v);
     } else {
         st2(sm.big + tok * LDB + part * 64 + col, v);
     }
@@ -2759,7 +2783,7 @@ __device__ void bwd_layer_split(Smem& sm, const float* __restrict__ P, const flo
             f32x4 d = hi[ct] + lo[ct] * kLoScale;
             d.x = u.x > 0.f ? d.x : 0.f; d.y = u.y > 0.f ? d.y : 0.f;
             d.z = u.z > 0.f ? d.z : 0.f; d.w = u.w > 0.f ? d.w : 0.f;
-            st4(io.du + r * FF + row + 4 * g, d);
+            dy_st4(io.du + r * FF + row + 4 * g, d);
             hsplit_store(dstp, psw(tok, fo), d);
             sd += d;
         }
@@ -2944,7 +2968,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
             f32x4 d = acc[ct];
             d.x = u.x > 0.f ? d.x : 0.f; d.y = u.y > 0.f ? d.y : 0.f;
             d.z = u.z > 0.f ? d.z : 0.f; d.w = u.w > 0.f ? d.w : 0.f;
-            st4(io.du + r * FF + row + 4 * g, d);
+            dy_st4(io.du + r * FF + row + 4 * g, d);
             st4(lds + tok * LDH + fo, d);
             sd += d;
         }
@@ -3027,7 +3051,7 @@ __device__ void bwd_layer(Smem& sm, const float* __restrict__ P, const float* __
             if (MODE == kBwdPos && part > 0)  // this query position's share of every position's dk / dv
                 st4(kvc + ((size_t)blk * TOK + tok) * 2 * D + (part - 1) * D + 64 * c + 4 * q, v);
             else
-                st4(io.dqkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q, v);
+                dy_st4(io.dqkv + (size_t)trow(tok, b0) * 3 * D + part * D + 64 * c + 4 * q, v);
         }
         if constexpr (kDx) {
             if (last) {  // dq is zero outside the query tile: Win_q^T dq only for column tile 4
