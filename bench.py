@@ -288,6 +288,8 @@ def parse():
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the dropin_loop leg (main_train.py's loop at E = 1 through the drop-ins)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--ppo-timeout", type=float, default=300.0,
+                    help="N > 1: the data-parallel update leg's watchdog (s); on expiry the line prints without it")
     ap.add_argument("--eager", action="store_true", help="launch kernels eagerly instead of replaying a hipGraph")
     ap.add_argument("--unfused", action="store_true",
                     help="separate policy and env launches per step instead of uavhip_rollout_step")
@@ -978,12 +980,14 @@ def main():
         except Exception as exc:  # the headline rollout line must still print
             print(f"[bench] minibatch-64 PPO measurement failed: {exc!r}", file=sys.stderr)
             ppo64 = {"value": None, "error": repr(exc)}
-    if not args.no_ppo:
+    def ppo_leg():
         try:
-            ppo = ppo_update_rate(args, eng, policy, world, dist, dev, E, T)
+            return ppo_update_rate(args, eng, policy, world, dist, dev, E, T)
         except Exception as exc:  # the headline rollout line must still print
             print(f"[bench] PPO update measurement failed: {exc!r}", file=sys.stderr)
-            ppo = {"value": None, "error": repr(exc)}
+            return {"value": None, "error": repr(exc)}
+    if not args.no_ppo and world == 1:
+        ppo = ppo_leg()
 
     e2e = None
     if not args.no_ppo and not args.no_e2e and world == 1 and args.ppo_impl == "fused":
@@ -1040,6 +1044,7 @@ def main():
     env_traffic, env_traffic_gbs, env_traffic_check, why = check_traffic(env_traffic, env_ms)
     if why:
         env_err = (env_err + "; " if env_err else "") + why
+    line = None
     if rank == 0:
         line = {
             "metric": "env-steps/sec (whole node), full PPO rollout, 4096 envs x 16 UAV x 32 tgt per GPU",
@@ -1125,6 +1130,28 @@ def main():
         if exchange is not None and exchange.get("check") is False:
             line["invalid"] = ("the pipelined exchange's gathered payloads differ from RCCL's all_gather of the "
                                "same payloads: the multi-GPU throughput is not valid")
+    if not args.no_ppo and world > 1:
+        # the data-parallel update leg runs last, under a watchdog on every rank: its collectives (an
+        # epoch graph with captured RCCL all-reduces) must not be able to hold back the line of the
+        # rollout measured above -- if it has not finished in --ppo-timeout s, rank 0 prints the line
+        # with the leg marked timed out and every rank exits 0
+        import threading
+
+        def timed_out():
+            if line is not None:
+                line["ppo_samples_per_s"] = {"value": None, "error": f"data-parallel update leg timed out after "
+                                                                     f"{args.ppo_timeout:.0f} s (watchdog)"}
+                print(json.dumps(line), flush=True)
+            sys.stderr.flush()
+            os._exit(0)
+        watchdog = threading.Timer(args.ppo_timeout, timed_out)
+        watchdog.daemon = True
+        watchdog.start()
+        ppo = ppo_leg()
+        watchdog.cancel()
+        if line is not None:
+            line["ppo_samples_per_s"] = ppo
+    if line is not None:
         print(json.dumps(line), flush=True)
     if dist is not None:
         if xchg is not None:  # unmap the peers' send buffers before any rank (an exporter) exits
