@@ -2570,6 +2570,13 @@ __device__ __forceinline__ float add_hmirror8(float v) {  // + lane 7 - i within
 __device__ __forceinline__ float sum8(float v) { return add_hmirror8(add_xor2(add_xor1(v))); }
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 ld2(const float* p) { return *reinterpret_cast<const f32x2*>(p); }
+// K6 reads the forward's Q | K | V rows (read once, by K6 alone) with non-temporal loads: they do not
+// displace the L2 lines the rest of the backward re-reads (same-box, three pairs at minibatch 4096:
+// K6 106.7 -> 102.1 us on average, profiles/r06s_train_ab_nt_qkv_loads.txt). EXP=87 (A/B build): plain.
+__device__ __forceinline__ f32x2 ld2_once(const float* p) {
+    if constexpr (UAVHIP_EXP != 87) return __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(p));
+    else return ld2(p);
+}
 __device__ __forceinline__ void st2(float* p, f32x2 v) { *reinterpret_cast<f32x2*>(p) = v; }
 
 // The chunk's saved Q / K / V values of this thread (2 head dims of one (sample, head)), loaded by
@@ -2586,12 +2593,12 @@ __device__ __forceinline__ void attn_bwd_load(AttnPre& a, const float* __restric
     const size_t rb = kExpNoQkvStream ? (size_t)p * S : (size_t)(b0 + p) * S;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-        a.k[j] = ld2(qkv + (rb + j) * 3 * D + D + col);
-        a.v[j] = ld2(qkv + (rb + j) * 3 * D + 2 * D + col);
+        a.k[j] = ld2_once(qkv + (rb + j) * 3 * D + D + col);
+        a.v[j] = ld2_once(qkv + (rb + j) * 3 * D + 2 * D + col);
     }
 #pragma unroll
     for (int i = 0; i < S; ++i)
-        if (qsel >= 0 ? i == qsel : (!last || i == S - 1)) a.q[i] = ld2(qkv + (rb + i) * 3 * D + col);
+        if (qsel >= 0 ? i == qsel : (!last || i == S - 1)) a.q[i] = ld2_once(qkv + (rb + i) * 3 * D + col);
 }
 // SP (split-product backward): dq | dk | dv go to sm.big as the two fp16 planes of the W_in^T GEMM's
 // operand -- both planes of a token in one row, [tok][plane 1: 192 halves | plane 2: 192 | pad 16]
