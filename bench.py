@@ -738,6 +738,29 @@ def spawn_ranks(envs, argv, grace_s=120.0, script=None):
     return 0
 
 
+def run_with_watchdog(fn, timeout_s, on_timeout):
+    """fn() with a watchdog thread: if it has not returned after timeout_s, on_timeout() runs (rank 0
+    prints the line) and the process exits 0 at once (os._exit: a rank blocked in a collective never
+    returns to let a normal exit run). Used for the N > 1 data-parallel update leg, whose collectives
+    could otherwise hold back every rank's exit and the rollout line with them."""
+    import threading
+
+    def fire():
+        try:
+            on_timeout()
+        finally:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
+    t = threading.Timer(timeout_s, fire)
+    t.daemon = True
+    t.start()
+    try:
+        return fn()
+    finally:
+        t.cancel()
+
+
 def main():
     args = parse()
     plan = launch_plan(args.gpus, os.environ, device_count=torch.cuda.device_count())
@@ -1135,20 +1158,12 @@ def main():
         # epoch graph with captured RCCL all-reduces) must not be able to hold back the line of the
         # rollout measured above -- if it has not finished in --ppo-timeout s, rank 0 prints the line
         # with the leg marked timed out and every rank exits 0
-        import threading
-
         def timed_out():
             if line is not None:
                 line["ppo_samples_per_s"] = {"value": None, "error": f"data-parallel update leg timed out after "
                                                                      f"{args.ppo_timeout:.0f} s (watchdog)"}
                 print(json.dumps(line), flush=True)
-            sys.stderr.flush()
-            os._exit(0)
-        watchdog = threading.Timer(args.ppo_timeout, timed_out)
-        watchdog.daemon = True
-        watchdog.start()
-        ppo = ppo_leg()
-        watchdog.cancel()
+        ppo = run_with_watchdog(ppo_leg, args.ppo_timeout, timed_out)
         if line is not None:
             line["ppo_samples_per_s"] = ppo
     if line is not None:

@@ -79,3 +79,16 @@ def test_spawn_relays_rank0_line_and_worst_exit_code(bench, tmp_path):
     bad = subprocess.run([sys.executable, "-c", child], input=json.dumps(bad_envs), capture_output=True, text=True,
                          timeout=300)
     assert bad.returncode == 3, bad.stderr[-500:]
+
+
+def test_watchdog_returns_the_leg_or_prints_and_exits(tmp_path):
+    """bench.run_with_watchdog (the N > 1 update leg): a leg that finishes returns its value; one that
+    hangs past the timeout runs on_timeout (rank 0's line) and ends the process with code 0."""
+    code = (f"import sys, time, json; sys.path.insert(0, {ROOT!r}); sys.argv = ['bench.py']; import bench\n"
+            "print(json.dumps({'fast': bench.run_with_watchdog(lambda: 7, 5.0, lambda: print('no'))}), flush=True)\n"
+            "bench.run_with_watchdog(lambda: time.sleep(60), 0.5, lambda: print(json.dumps({'timed_out': True})))\n"
+            "print('unreachable')\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-500:]
+    lines = out.stdout.strip().splitlines()
+    assert lines == ['{"fast": 7}', '{"timed_out": true}'], lines
