@@ -44,6 +44,16 @@ namespace uavhip { namespace pol { __device__ unsigned long long g_strace[256 * 
 #include "env_group.hpp"
 #include "policy_layout.hpp"
 #include "policy_train.hpp"
+// The policy code is contracted (a * b + c as one fma, v_pk_fma_f32 on float pairs): the env headers
+// above switch contraction off for the rest of the translation unit at file scope (their fp64 code must
+// follow the reference's operation order), which until round 6 silently applied to every function
+// below too. Their templates keep the state they were parsed with; the operand-range functions that
+// producer and consumer must evaluate identically keep their own contract(off). Same-box A/B
+// (profiles/r06u_ab_contract.txt): k_rollout_steps 49.4 -> 48.2 us per step, the training forward
+// 87.6 -> 84.5 us; every -m gpu test unchanged in outcome. EXP=91 (A/B build): uncontracted as before.
+#if UAVHIP_EXP != 91
+#pragma clang fp contract(fast)
+#endif
 
 namespace uavhip {
 namespace pol {
