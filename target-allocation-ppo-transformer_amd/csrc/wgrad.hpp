@@ -212,8 +212,16 @@ __device__ __forceinline__ void wg_stage_store(const WgSlab& r, char* stage, int
     for (int i = 0; i < 2; ++i) {
         const int off = wg_swz((t >> 5) + 16 * i, c4 >> 1) + 8 * (c4 & 1);
         wg_split_store<P3>(r.a[i], stage, off);
-        // X 2^-s (xsc, exact): every element inside fp16's range (wg_xrange)
-        wg_split_store<P3>((xmode != kWgX ? r.b[i] * xg + r.x[i] : r.b[i]) * xsc, stage + 3 * kWgPlaneB, off);
+        // X 2^-s (xsc, exact): every element inside fp16's range (wg_xrange). x-hat * gamma + beta as
+        // one fma per element: the forward's (contracted) LayerNorm epilogue rounds it once too, so the
+        // re-formed operand is its stored output bit for bit (this file itself stays uncontracted:
+        // contracting all of it measured 2.5 us slower in k_wgrad, profiles/r06v_train_ab_contract.txt)
+        f32x4 xv = r.b[i];
+        if (xmode != kWgX) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) xv[e] = __builtin_fmaf(r.b[i][e], xg[e], r.x[i][e]);
+        }
+        wg_split_store<P3>(xv * xsc, stage + 3 * kWgPlaneB, off);
     }
 }
 // 16 columns (c16 .. c16 + 15) x 8 consecutive k (8 g ..) of a plane: lane (i16, g) gets column
