@@ -341,6 +341,20 @@ static_assert(TOK * LDP * 2 == TOK * LDH * 4 && kPlane + D <= LDP, "the two plan
 // (4-way without it) while the GEMMs' ds_read_b128 stay conflict-free
 __device__ __forceinline__ int psw(int tok, int col) { return tok * LDP + (col ^ (((tok >> 2) & 1) << 3)); }
 constexpr float kLoScale = 1.0f / 2048.0f;
+// The LayerNorm's 1/sqrt(var + eps) and the attention's 1/sum(exp) on the hardware estimates
+// (v_rsq_f32 / v_rcp_f32, about 1 ulp) instead of the correctly rounded sqrt + division sequences
+// (~10 VALU each, on the LayerNorm and attention phases' dependency chains): same-box A/B
+// (profiles/r06x_ab_rsq_rcp.txt) k_rollout_steps 48.6 -> 47.8 us per step, K6 101.8 -> 98.8 us, the
+// training forward 85.8 -> 82.5 us; every -m gpu parity bar unchanged and green. EXP=94: the correctly
+// rounded forms (A/B build).
+__device__ __forceinline__ float ln_rstd(float v) {
+    if constexpr (UAVHIP_EXP != 94) return __builtin_amdgcn_rsqf(v);
+    else return 1.0f / sqrtf(v);
+}
+__device__ __forceinline__ float att_recip(float v) {
+    if constexpr (UAVHIP_EXP != 94) return __builtin_amdgcn_rcpf(v);
+    else return 1.0f / v;
+}
 
 template <int D_>
 struct HPre {
@@ -696,7 +710,7 @@ __device__ __forceinline__ void residual_layernorm(TID_F Smem& sm, const f32x4 (
             const float dm = pr[k].x - mean;
             m2 += pr[k].y + 16.0f * dm * dm;
         }
-        rs = 1.0f / sqrtf(m2 * (1.0f / D) + 1e-5f);
+        rs = ln_rstd(m2 * (1.0f / D) + 1e-5f);
     };
     static_assert(CT == 1 || CT == S, "pruned tile or all five");
     // all five tiles: lane (i16, g) combines the partials of tile g's token, the last tile's in a
@@ -789,7 +803,7 @@ __device__ __forceinline__ void attention_full_core(TID_F Smem& sm, int c, f32x4
                 sc[j] = __expf(sc[j] - mx);
                 den += sc[j];
             }
-            const float inv = 1.0f / den;
+            const float inv = att_recip(den);
 #pragma unroll
             for (int j = 0; j < S; ++j) o[qi] += (sc[j] * inv) * v[j];
         }
@@ -853,7 +867,7 @@ __device__ __forceinline__ void attention_task(TID_F Smem& sm, int task, int qs0
         sc[j] = __expf(sc[j] - mx);
         den += sc[j];
     }
-    const float inv = 1.0f / den;
+    const float inv = att_recip(den);
     o = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < S; ++j) {
@@ -2670,7 +2684,7 @@ __device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch
                 pr[j] = __expf(pr[j] - mx);
                 den += pr[j];
             }
-            const float inv = 1.0f / den;
+            const float inv = att_recip(den);
             float sdp = 0.f;
 #pragma unroll
             for (int j = 0; j < S; ++j) {
