@@ -378,10 +378,14 @@ __device__ __forceinline__ HPre<D_> hprefetch(TID_F const float* __restrict__ P,
 // hi / lo[ct] += W[row + i][kw0 + k] * X[xtok0 + 16 ct + j][k] over k in [0, 128) (4 blocks of 32):
 // A blocks >= D_ loaded one block ahead of their use, B (LDS) one block ahead.
 // NKB blocks of 32 k; the activation planes have rows of LDX_ halves, plane 2 at + PLX halves.
-template <int CT, int D_, int NKB = D / 32, int LDX_ = LDP, int PLX = kPlane>
+// NEXT: the blocks of the NEXT tile's prefetch (nxt, from nwp) are loaded in the last D_ iterations,
+// into the registers the current tile's first blocks free there -- the next GEMM's first weight
+// blocks then land under this GEMM's last MFMAs instead of after them (same register peak).
+template <int CT, int D_, int NKB = D / 32, int LDX_ = LDP, int PLX = kPlane, bool NEXT = false>
 __device__ __forceinline__ void hgemm_tile(TID_F f32x4 (&hi)[CT], f32x4 (&lo)[CT], const HPre<D_>& pre,
                                            const float* __restrict__ P, int soff, int K, int row, int kw0,
-                                           const _Float16* X, int xtok0) {
+                                           const _Float16* X, int xtok0, HPre<D_>* nxt = nullptr,
+                                           const f16x8* nwp = nullptr) {
     constexpr int kPlane = PLX;
     const int l = LANE(), i16 = l & 15, g = l >> 4;
     const f16x8* wp = hfrag_ptr(TID_C P, soff, K, row, kw0);
@@ -411,6 +415,13 @@ __device__ __forceinline__ void hgemm_tile(TID_F f32x4 (&hi)[CT], f32x4 (&lo)[CT
             } else {
                 a1[i + D_] = wp[128 * (i + D_)];
                 a2[i + D_] = wp[128 * (i + D_) + 64];
+            }
+        }
+        if constexpr (NEXT) {
+            if (i + D_ >= NKB) {
+                const int p = i - (NKB - D_);
+                nxt->a1[p] = nwp[128 * p];
+                nxt->a2[p] = nwp[128 * p + 64];
             }
         }
         if (i + 1 < NKB) {
@@ -1310,8 +1321,15 @@ __device__ __forceinline__ void layer_tail_split(TID_F Smem& sm, const float* __
         f32x4 hi[CT], lo[CT];
         zero(hi);
         zero(lo);
-        hgemm_tile<CT, DP>(TID_C hi, lo, w1a, P, s1, D, 16 * wv, 0, hp, t0);
-        const HPre<DP> w1b = hprefetch<DP>(TID_C P, s1, D, 128 + 16 * wv, 0);
+        // FFN1's second tile's first blocks load under the first tile's last MFMAs (EXP=96: after it)
+        HPre<DP> w1b;
+        if constexpr (UAVHIP_EXP != 96) {
+            hgemm_tile<CT, DP, D / 32, LDP, kPlane, true>(TID_C hi, lo, w1a, P, s1, D, 16 * wv, 0, hp, t0, &w1b,
+                                                          hfrag_ptr(TID_C P, s1, D, 128 + 16 * wv, 0));
+        } else {
+            hgemm_tile<CT, DP>(TID_C hi, lo, w1a, P, s1, D, 16 * wv, 0, hp, t0);
+            w1b = hprefetch<DP>(TID_C P, s1, D, 128 + 16 * wv, 0);
+        }
         hstore_tile<CT, true>(TID_C hi, lo, ba, bp, 16 * wv, t0, s_ln1.inv, s_hid.sc);
         zero(hi);
         zero(lo);
