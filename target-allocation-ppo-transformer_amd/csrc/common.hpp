@@ -58,6 +58,15 @@ __device__ __forceinline__ int ffs64(unsigned long long m) { return __ffsll((lon
 // row into NaN. What could hide that is a ReLU written as fmaxf (IEEE maxNum returns 0 for NaN):
 // the GEMM epilogues use relu_nan (policy.hip) instead, so overflow reaches the outputs.
 __device__ __forceinline__ _Float16 f16_lo(float x, _Float16 x1) { return (_Float16)((x - (float)x1) * 2048.f); }
+// f16_lo's split four at a time as packed conversions: x1 = f16(x) once (v_cvt_pk_f16_f32), its fp32
+// value from the packed halves -- element by element, the compiler converted every x twice (once for
+// the store, once for the residual); the same RNE roundings, so bitwise the same planes
+typedef float cm_f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 cm_f16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void f16_split4(const cm_f32x4 x, cm_f16x4& x1, cm_f16x4& x2) {
+    x1 = __builtin_convertvector(x, cm_f16x4);
+    x2 = __builtin_convertvector((x - __builtin_convertvector(x1, cm_f32x4)) * 2048.f, cm_f16x4);
+}
 
 // ------------------------------------------------------------------ mechanics (fp64)
 __device__ __forceinline__ double clipd(double x, double lo, double hi) {

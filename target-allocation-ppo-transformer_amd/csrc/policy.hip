@@ -445,12 +445,17 @@ __device__ __forceinline__ void hgemm_tile(TID_F f32x4 (&hi)[CT], f32x4 (&lo)[CT
 // (measured: a 1.4e5 FFN activation gave finite, wrong values); same cost on the same box (r04f A/B)
 __device__ __forceinline__ float relu_nan(float v) { return v < 0.f ? 0.f : v; }
 // v -> its two planes at Y + psw(tok, c) (plane 2 at + kPlane): one 8-byte store per plane
+// (common.hpp f16_split4: packed conversions. EXP=97: the per-element form, A/B build)
 __device__ __forceinline__ void hsplit_store(_Float16* Y, int o, const f32x4 v) {
     f16x4 v1, v2;
+    if constexpr (UAVHIP_EXP == 97) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        v1[j] = (_Float16)v[j];
-        v2[j] = f16_lo(v[j], v1[j]);
+        for (int j = 0; j < 4; ++j) {
+            v1[j] = (_Float16)v[j];
+            v2[j] = f16_lo(v[j], v1[j]);
+        }
+    } else {
+        f16_split4(v, v1, v2);
     }
     *reinterpret_cast<f16x4*>(Y + o) = v1;
     *reinterpret_cast<f16x4*>(Y + o + kPlane) = v2;
@@ -3745,11 +3750,7 @@ __device__ __forceinline__ void ps_big_store(Smem& sm, int p, int q, const f32x4
     if constexpr (kPsSplit) {
         _Float16* bp = reinterpret_cast<_Float16*>(sm.big);
         f16x4 a, b;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            a[j] = (_Float16)v[j];
-            b[j] = f16_lo(v[j], a[j]);
-        }
+        f16_split4(v, a, b);
         *reinterpret_cast<f16x4*>(bp + p * 2 * LDQ + 4 * q) = a;  // [p][plane 1 | plane 2 | pad]
         *reinterpret_cast<f16x4*>(bp + p * 2 * LDQ + 3 * D + 4 * q) = b;
     } else {

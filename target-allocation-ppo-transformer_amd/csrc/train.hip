@@ -396,11 +396,7 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
     // (i % 16) + 16 ((j % 32) / 8) of block (i / 16, j / 32), halves j % 8 .. + 3
     if (sb >= 0) {
         wg_f16x4 w1, w2;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            w1[e] = (_Float16)p[e];
-            w2[e] = f16_lo(p[e], w1[e]);
-        }
+        f16_split4(p, w1, w2);
         _Float16* sp = reinterpret_cast<_Float16*>(a.packed + sb) +
                        (((i >> 4) * (NC >> 5) + (j >> 5)) * 128 + (i & 15) + 16 * ((j & 31) >> 3)) * 8 + (j & 7);
         *reinterpret_cast<wg_f16x4*>(sp) = w1;
@@ -419,11 +415,7 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a) {
                                                     16 * ((it & 15) >> 2)) * 4) = col;
     if (tb < kHeadT) {  // a layer weight: its transposed split copy (W^T[jt][it .. it + 3], halves it % 8 ..)
         wg_f16x4 w1, w2;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            w1[e] = (_Float16)col[e];
-            w2[e] = f16_lo(col[e], w1[e]);
-        }
+        f16_split4(col, w1, w2);
         _Float16* sp = reinterpret_cast<_Float16*>(a.packedT + kTSplit + tb) +
                        (((jt >> 4) * (NR >> 5) + (it >> 5)) * 128 + (jt & 15) + 16 * ((it & 31) >> 3)) * 8 + (it & 7);
         *reinterpret_cast<wg_f16x4*>(sp) = w1;
