@@ -355,6 +355,21 @@ __device__ __forceinline__ float att_recip(float v) {
     if constexpr (UAVHIP_EXP != 94) return __builtin_amdgcn_rcpf(v);
     else return 1.0f / v;
 }
+// The forward attention's score of a query against a key over a lane's 4 head dims: one packed
+// multiply and one packed FMA (3 issue slots; left to itself the compiler formed 2 packed multiplies
+// and 3 adds). The 1/sqrt(16) of the scores is folded into the query (a power of two: exact).
+// EXP=99 (A/B build): the previous form, the scale applied to each score.
+constexpr bool kAttPk = UAVHIP_EXP != 99;
+__device__ __forceinline__ float att_dot(const f32x4 q, const f32x4 k) {
+    if constexpr (kAttPk) {
+        f32x2_t t = f32x2_t{q.x, q.y} * f32x2_t{k.x, k.y};
+        t = __builtin_elementwise_fma(f32x2_t{q.z, q.w}, f32x2_t{k.z, k.w}, t);
+        return t.x + t.y;
+    } else {
+        return q.x * k.x + q.y * k.y + q.z * k.z + q.w * k.w;
+    }
+}
+constexpr float kAttQ = kAttPk ? 0.25f : 1.f, kAttS = kAttPk ? 1.f : 0.25f;  // 1/sqrt(16) on q / on the score
 
 template <int D_>
 struct HPre {
@@ -803,21 +818,21 @@ __device__ __forceinline__ void attention_full_core(TID_F Smem& sm, int c, f32x4
         o[qi] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (qi < nq) {
             const int ti = (qs0 + qi) * SPW + p;
-            const f32x4 q = *reinterpret_cast<const f32x4*>(sm.big + ti * LDB + d0);
+            const f32x4 q = *reinterpret_cast<const f32x4*>(sm.big + ti * LDB + d0) * kAttQ;
             float sc[S];
             float mx = -INFINITY;
 #pragma unroll
             for (int j = 0; j < S; ++j) {
-                float part = q.x * k[j].x + q.y * k[j].y + q.z * k[j].z + q.w * k[j].w;
+                float part = att_dot(q, k[j]);
                 part = add_xor2(add_xor1(part));
-                sc[j] = msk[j] ? -INFINITY : part * 0.25f;  // 1/sqrt(16)
+                sc[j] = msk[j] ? -INFINITY : part * kAttS;  // 1/sqrt(16)
                 mx = fmaxf(mx, sc[j]);
             }
             float den = 0.f;
 #pragma unroll
             for (int j = 0; j < S; ++j) {
                 sc[j] = __expf(sc[j] - mx);
-                den += sc[j];
+                den = j ? den + sc[j] : sc[j];
             }
             const float inv = att_recip(den);
 #pragma unroll
@@ -866,22 +881,22 @@ __device__ __forceinline__ void attention_task(TID_F Smem& sm, int task, int qs0
     const int hh = task & 3, rest = task >> 2, p = rest & 15, si = qs0 + (rest >> 4);
     ti = si * SPW + p;
     d0 = hh * HD + 4 * q4;
-    const f32x4 q = *reinterpret_cast<const f32x4*>(sm.big + ti * LDB + d0);
+    const f32x4 q = *reinterpret_cast<const f32x4*>(sm.big + ti * LDB + d0) * kAttQ;
     float sc[S];
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
         const f32x4 k = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 64 + d0);
-        float part = q.x * k.x + q.y * k.y + q.z * k.z + q.w * k.w;
+        float part = att_dot(q, k);
         part = add_xor2(add_xor1(part));
-        sc[j] = sm.mask[p * S + j] ? -INFINITY : part * 0.25f;  // 1/sqrt(16)
+        sc[j] = sm.mask[p * S + j] ? -INFINITY : part * kAttS;  // 1/sqrt(16)
         mx = fmaxf(mx, sc[j]);
     }
     float den = 0.f;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
         sc[j] = __expf(sc[j] - mx);
-        den += sc[j];
+        den = j ? den + sc[j] : sc[j];
     }
     const float inv = att_recip(den);
     o = f32x4{0.f, 0.f, 0.f, 0.f};
