@@ -370,6 +370,23 @@ __device__ __forceinline__ float att_dot(const f32x4 q, const f32x4 k) {
     }
 }
 constexpr float kAttQ = kAttPk ? 0.25f : 1.f, kAttS = kAttPk ? 1.f : 0.25f;  // 1/sqrt(16) on q / on the score
+// o += sum_j (e_j / den) v_j as (sum_j e_j v_j) / den: one scale of the sum instead of one per key
+// (EXP=101 or 99: the per-key form). Not exp2(s log2e - mx log2e) as one FMA per score: for logits
+// of 1e10 (windows at 1e5) the FMA's residual at the maximum itself is hundreds, exp2 of it inf or 0
+// (NaN outputs in test_fused_forward_out_of_fp16_range_matches_torch); s - mx is exact there.
+constexpr bool kAttMix = kAttPk && UAVHIP_EXP != 101;
+template <int N>
+__device__ __forceinline__ void att_mix(f32x4& o, const float (&e)[N], float inv, const f32x4 (&v)[N]) {
+    if constexpr (kAttMix) {
+        f32x4 a = e[0] * v[0];
+#pragma unroll
+        for (int j = 1; j < N; ++j) a += e[j] * v[j];
+        o += a * inv;
+    } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) o += (e[j] * inv) * v[j];
+    }
+}
 
 template <int D_>
 struct HPre {
@@ -826,7 +843,7 @@ __device__ __forceinline__ void attention_full_core(TID_F Smem& sm, int c, f32x4
                 float part = att_dot(q, k[j]);
                 part = add_xor2(add_xor1(part));
                 sc[j] = msk[j] ? -INFINITY : part * kAttS;  // 1/sqrt(16)
-                mx = fmaxf(mx, sc[j]);
+                mx = j ? fmaxf(mx, sc[j]) : sc[j];
             }
             float den = 0.f;
 #pragma unroll
@@ -835,8 +852,7 @@ __device__ __forceinline__ void attention_full_core(TID_F Smem& sm, int c, f32x4
                 den = j ? den + sc[j] : sc[j];
             }
             const float inv = att_recip(den);
-#pragma unroll
-            for (int j = 0; j < S; ++j) o[qi] += (sc[j] * inv) * v[j];
+            att_mix(o[qi], sc, inv, v);
         }
     }
 }
@@ -890,7 +906,7 @@ __device__ __forceinline__ void attention_task(TID_F Smem& sm, int task, int qs0
         float part = att_dot(q, k);
         part = add_xor2(add_xor1(part));
         sc[j] = sm.mask[p * S + j] ? -INFINITY : part * kAttS;  // 1/sqrt(16)
-        mx = fmaxf(mx, sc[j]);
+        mx = j ? fmaxf(mx, sc[j]) : sc[j];
     }
     float den = 0.f;
 #pragma unroll
@@ -899,12 +915,11 @@ __device__ __forceinline__ void attention_task(TID_F Smem& sm, int task, int qs0
         den = j ? den + sc[j] : sc[j];
     }
     const float inv = att_recip(den);
-    o = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 v[S];
 #pragma unroll
-    for (int j = 0; j < S; ++j) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 128 + d0);
-        o += (sc[j] * inv) * v;
-    }
+    for (int j = 0; j < S; ++j) v[j] = *reinterpret_cast<const f32x4*>(sm.big + (j * SPW + p) * LDB + 128 + d0);
+    o = f32x4{0.f, 0.f, 0.f, 0.f};
+    att_mix(o, sc, inv, v);
 }
 template <bool PLANES>
 __device__ __forceinline__ void attention_out(TID_F Smem& sm, int c, int ti, int d0, const f32x4 o, float sc = 1.f) {
