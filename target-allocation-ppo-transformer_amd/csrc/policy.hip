@@ -2721,21 +2721,25 @@ __device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch
     for (int i = 0; i < S; ++i) {
         f32x2 dq = {0.f, 0.f};
         if (qsel >= 0 ? i == qsel : (!last || i == S - 1)) {
-            const f32x2 q = a.q[i];
+            // the scores' 1/sqrt(16) on the query (q4 = q / 4: exact), so dk[j] += ds q = (ds 4) q4 and
+            // dq = (sum_j (ds 4) k_j) / 4 -- the same values as scaling each score and each ds, without
+            // the 2 S multiplies (EXP=104, A/B build: that form)
+            constexpr bool kQ4 = UAVHIP_EXP != 104;
+            const f32x2 q = a.q[i], q4 = kQ4 ? q * 0.25f : q;
             const f32x2 g = ld2(sm.ctx + (i * SPW + p) * LDH + col);
             float pr[S], dp[S];
             float mx = -INFINITY;
 #pragma unroll
             for (int j = 0; j < S; ++j) {
-                const float part = sum8(q.x * k[j].x + q.y * k[j].y);
-                pr[j] = msk[j] ? -INFINITY : part * 0.25f;
-                mx = fmaxf(mx, pr[j]);
+                const float part = sum8(q4.x * k[j].x + q4.y * k[j].y);
+                pr[j] = msk[j] ? -INFINITY : (kQ4 ? part : part * 0.25f);
+                mx = (kQ4 && j == 0) ? pr[j] : fmaxf(mx, pr[j]);
             }
             float den = 0.f;
 #pragma unroll
             for (int j = 0; j < S; ++j) {
                 pr[j] = __expf(pr[j] - mx);
-                den += pr[j];
+                den = (kQ4 && j == 0) ? pr[j] : den + pr[j];
             }
             const float inv = att_recip(den);
             float sdp = 0.f;
@@ -2747,11 +2751,12 @@ __device__ void attn_bwd_chunk(Smem& sm, const AttnPre& a, int c, float* scratch
             }
 #pragma unroll
             for (int j = 0; j < S; ++j) {
-                const float ds = pr[j] * (dp[j] - sdp) * 0.25f;
+                const float ds = kQ4 ? pr[j] * (dp[j] - sdp) : pr[j] * (dp[j] - sdp) * 0.25f;
                 dq += ds * k[j];
-                dk[j] += ds * q;
+                dk[j] += ds * q4;
                 dv[j] += pr[j] * g;
             }
+            if (kQ4) dq *= 0.25f;
             sdq += dq;
         }
         if (!SP || (qsel >= 0 ? i == qsel : (!last || i == S - 1))) attn_out2(sm, dqkv, b0, i * SPW + p, d0, 0, c, dq, SP);
