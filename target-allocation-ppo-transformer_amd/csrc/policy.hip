@@ -96,6 +96,7 @@ constexpr bool kExpNoEnv = false;
 #define UAVHIP_EXP 0
 #endif
 constexpr bool kExpHotRing = UAVHIP_EXP == 32;
+constexpr bool kEarlyDraw = UAVHIP_EXP != 105;  // policy_block: the sampling draws at the step's start
 // EXP=71 (timing only, WRONG results): the split-product GEMMs load only the blocks their callers
 // prefetched (blocks >= D_ of a tile repeat them): the cost of the in-loop weight loads' latency --
 // the ceiling of a deeper weight prefetch (an LDS-DMA ring). EXP=73: also every prefetch reads one
@@ -181,6 +182,7 @@ struct Smem {
     signed char es[2][TOK];     // per trunk and token: layer 0's input scale exponent s (from tmax)
     float a0f[4];               // per trunk: (2^-s, 2^s) of the workgroup's layer-0 attention output
     float rtab[28];             // the range table's static part (load_rtab, once per launch)
+    float u01[SPW];             // the sampling draws, formed at the step's start (policy_block)
 };
 // Smem::rtab: the static operands' (2^-s, 2^s) pairs, then (14 max|W_e|, max|b_e| + max|pos|) and
 // (D max|W_in|, max|b_in|) of layer 0 per trunk (policy_layout.hpp kRgOp / kRgE / kRgA0)
@@ -2078,6 +2080,18 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
         }
     }
     gather_windows<TR, ROWS>(TID_C sm, states, B, io, b0, do_actor, P + kRangeOff);
+    // the sampling's Philox draws (a counter function of the sample's index alone) by the last wave's
+    // first lanes while the windows load, so that the serial tail after the heads (one wave's
+    // sampling) no longer runs the 10 Philox rounds (EXP=105, A/B build: drawn there)
+    if constexpr (!TR && kEarlyDraw) {
+        const int pd = (int)TIDX() - (NTHR - kWave);
+        if (!actions_in && pd >= 0 && pd < SPW) {
+            const unsigned long long c = offset + (offset_dev ? *offset_dev : 0ull) + (unsigned long long)(b0 + pd);
+            const u32x4 r = philox(u32x4{(uint32_t)c, (uint32_t)(c >> 32), 0x5eedu, 0x9e37u}, (uint32_t)seed,
+                                   (uint32_t)(seed >> 32));
+            sm.u01[pd] = u01f(r.x);
+        }
+    }
     __syncthreads();
     PTR(1);
     // layer 0's attention-output scales, read behind the next barrier (the ring forward: once the
@@ -2241,10 +2255,16 @@ __device__ __forceinline__ void policy_block(TID_F Smem& sm, const float* __rest
             if (actions_in) {
                 a = actions_in[b] != 0;
             } else {
-                const unsigned long long c = offset + (offset_dev ? *offset_dev : 0ull) + (unsigned long long)b;
-                const u32x4 r = philox(u32x4{(uint32_t)c, (uint32_t)(c >> 32), 0x5eedu, 0x9e37u}, (uint32_t)seed,
-                                       (uint32_t)(seed >> 32));
-                a = u01f(r.x) < p0 ? 0 : 1;
+                float u;
+                if constexpr (kEarlyDraw) {
+                    u = sm.u01[p];
+                } else {
+                    const unsigned long long c = offset + (offset_dev ? *offset_dev : 0ull) + (unsigned long long)b;
+                    const u32x4 r = philox(u32x4{(uint32_t)c, (uint32_t)(c >> 32), 0x5eedu, 0x9e37u}, (uint32_t)seed,
+                                           (uint32_t)(seed >> 32));
+                    u = u01f(r.x);
+                }
+                a = u < p0 ? 0 : 1;
             }
             if (action_out) action_out[b] = (int8_t)a;
             if (logp_out) logp_out[b] = a ? lp1 : lp0;
